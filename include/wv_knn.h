@@ -1,0 +1,170 @@
+/*
+ * wv_knn.h -- C ABI of the MI355X (gfx950) flat-index engine.
+ *
+ * Drop-in boundary for Weaviate's flat vector index and distancer hot path
+ * (SURVEY.md §8b).  Every entry point names the reference interface it
+ * replaces (paths relative to the reference repo root).  A Go shim would bind
+ * these through cgo; the Python mirror in weaviate_amd/ binds
+ * them through ctypes.
+ *
+ * Conventions:
+ *  - plain pointers + sizes only; host pointers are borrowed for the call and
+ *    copied (cgo forbids retaining Go pointers);  *_device entry points take
+ *    device pointers on the index's GPU;
+ *  - returns WV_OK (0) or a negative WV_ERR_*; wv_last_error() gives the
+ *    reference's error text for the calling thread;
+ *  - every entry point is thread-safe (calls on one index are serialised).
+ */
+#ifndef WV_KNN_H
+#define WV_KNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define WV_OK 0
+#define WV_ERR_INVALID (-1)        /* bad argument                                  */
+#define WV_ERR_VECTOR_LENGTH (-2)  /* distancer.ErrVectorLength (distancer/errors.go:16) */
+#define WV_ERR_INSERT (-3)         /* flat ValidateBeforeInsert / AddBatch errors   */
+#define WV_ERR_HIP (-4)            /* HIP runtime failure                           */
+#define WV_ERR_UNSUPPORTED (-5)    /* configuration not supported                   */
+#define WV_ERR_QUANTIZER (-6)      /* "quantizer not initialized" (flat/index.go:463) */
+
+/* distance providers: Shard.initVectorIndex (shard_init_vector.go:56-73) */
+#define WV_METRIC_L2_SQUARED 0     /* "l2-squared" distancer/l2.go                  */
+#define WV_METRIC_DOT 1            /* "dot"        distancer/dot_product.go         */
+#define WV_METRIC_COSINE_DOT 2     /* "cosine-dot" distancer/cosine_dist.go         */
+#define WV_METRIC_HAMMING 3        /* "hamming"    distancer/hamming.go             */
+
+/* compression: flatent.UserConfig (entities/vectorindex/flat/config.go:43-82) */
+#define WV_COMPRESSION_NONE 0
+#define WV_COMPRESSION_BQ 1
+
+/* which reference SIMD kernel's fp32 accumulation order to reproduce
+ * (distancer/l2_amd64.go:19-26: AVX-512 only if AMX-BF16 && AVX512) */
+#define WV_VARIANT_AUTO 0          /* same rule as the reference, on this host's CPU */
+#define WV_VARIANT_AVX256 1
+#define WV_VARIANT_AVX512 2
+
+typedef struct wv_index wv_index;
+
+/* flat.Config + flatent.UserConfig subset (flat/config.go:22-48) */
+typedef struct wv_config {
+    int32_t metric;          /* WV_METRIC_*                                           */
+    int32_t dims;            /* 0 = fixed by the first Add (flat/index.go:338-360)    */
+    int32_t compression;     /* WV_COMPRESSION_*                                      */
+    int32_t rescore_limit;   /* BQ.RescoreLimit (default -1 => k, flat/index.go:413)  */
+    int32_t device;          /* HIP device ordinal                                    */
+    int32_t variant;         /* WV_VARIANT_*                                          */
+    uint64_t id_base;        /* first doc id of this shard: slot = id - id_base       */
+    const char *root_path;   /* only used in error texts (flat/index.go:837)          */
+} wv_config;
+
+const char *wv_last_error(void);
+int wv_resolve_variant(int32_t requested); /* -> WV_VARIANT_AVX256 / _AVX512 */
+
+/* flat.New (flat/index.go:76-125) / Drop+Shutdown */
+int wv_index_create(const wv_config *cfg, wv_index **out);
+void wv_index_destroy(wv_index *idx);
+/* pre-size the id-indexed store (cache.Grow analogue, cache/sharded_lock_cache.go) */
+int wv_index_reserve(wv_index *idx, uint64_t nslots);
+
+/* flat.ValidateBeforeInsert (flat/index.go:823-842) */
+int wv_index_validate_before_insert(wv_index *idx, int64_t d);
+/* flat.Add (flat/index.go:362-390): validate, normalise (cosine), upsert */
+int wv_index_add(wv_index *idx, uint64_t id, const float *vec, int64_t d);
+/* flat.AddBatch (flat/index.go:289-308): n rows of d floats */
+int wv_index_add_batch(wv_index *idx, const uint64_t *ids, const float *vecs, int64_t n, int64_t d);
+/* bulk load of ids [first_id, first_id+n) from a device buffer (PostStartup /
+ * restore path, flat/index.go:867-1033) */
+int wv_index_add_range_device(wv_index *idx, uint64_t first_id, const float *d_vecs, int64_t n, int64_t d);
+/* flat.Delete (flat/index.go:392-411) */
+int wv_index_delete(wv_index *idx, const uint64_t *ids, int64_t n);
+/* flat.ContainsDoc (flat/index.go:1035-1055) */
+int wv_index_contains_doc(wv_index *idx, uint64_t id);
+/* flat.AlreadyIndexed (flat/index.go:1156-1158) */
+uint64_t wv_index_already_indexed(wv_index *idx);
+int32_t wv_index_dims(wv_index *idx);
+
+/* flat.SearchByVector (flat/index.go:423-448 + :578-688) for nq queries.
+ * allow_mode 0: allow list nil; 1: allow list = allow_ids[0..n_allow) (may be
+ * empty -> empty results, flat/index.go:590-594).
+ * out_ids/out_dists: nq x k, ascending, reference heap tie order; out_counts[nq]. */
+int wv_index_search_by_vector_batch(wv_index *idx, const float *queries, int64_t nq, int64_t d, int32_t k,
+                                    const uint64_t *allow_ids, int64_t n_allow, int32_t allow_mode,
+                                    uint64_t *out_ids, float *out_dists, int32_t *out_counts);
+
+/* flat.SearchByVectorDistance (flat/index.go:699-761); out_* capacity >= 100 */
+int wv_index_search_by_vector_distance(wv_index *idx, const float *query, int64_t d, float target_distance,
+                                       int64_t max_limit, const uint64_t *allow_ids, int64_t n_allow,
+                                       int32_t allow_mode, uint64_t *out_ids, float *out_dists,
+                                       int32_t *out_count);
+
+/* Device-resident batch search for sharded / benchmark callers.
+ * mode 0: like SearchByVector (kout = k, tie cases resolved by heap replay).
+ * mode 1: shard-local candidates: kout = k+1 verified results per query and
+ *         d_flags[q] = 1 where the query needs the cross-shard replay.
+ * stream: hipStream_t to order against (NULL = the index's own stream). */
+int wv_index_search_device(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k, int32_t mode,
+                           uint64_t *d_ids, float *d_dists, int32_t *d_counts, int32_t *d_flags, void *stream);
+
+/* Cross-shard exact replay (distributed tie path): continue the
+ * reference heap (priorityqueue NewMax + insertToHeap, flat/index.go:578-674)
+ * over this shard's id range for the query rows listed in h_qlist, starting
+ * from heap states in layout order h_in_ids/h_in_dists/h_in_len [nlist x k]
+ * (NULL = empty heaps).  extract=0 writes the updated heap states to h_out_*;
+ * extract=1 applies extractHeap (flat/index.go:676-688) and writes ascending
+ * results.  d_queries are the raw query rows on the index's device. */
+int wv_index_replay(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k,
+                    const int32_t *h_qlist, int32_t nlist, const uint64_t *h_in_ids, const float *h_in_dists,
+                    const int32_t *h_in_len, int32_t extract, uint64_t *h_out_ids, float *h_out_dists,
+                    int32_t *h_out_len);
+
+/* Merge shard-local candidate lists (mode-1 search outputs of G shards, each
+ * [nq x (k+1)], gathered shard-major on this device) into the final top-k by
+ * (distance, id); d_out_flags[q]=1 when a shard flagged q or the merged top
+ * k+1 distances tie, i.e. the cross-shard replay must decide. */
+int wv_merge_shards(int32_t device, int32_t nshards, int64_t nq, int32_t k, const uint64_t *d_ids,
+                    const float *d_dists, const int32_t *d_counts, const int32_t *d_flags, uint64_t *d_out_ids,
+                    float *d_out_dists, int32_t *d_out_counts, int32_t *d_out_flags, void *stream);
+
+/* Provider.SingleDist batched over n pairs of d floats, exact reference order
+ * (distancer/provider.go:14-24). Runs on device `device`. */
+int wv_distance_batch(int32_t device, int32_t metric, int32_t variant, const float *a, const float *b, int64_t n,
+                      int64_t d, float *out);
+/* distancer.HammingBitwise batched (distancer/hamming.go:63-68) */
+int wv_hamming_bitwise_batch(int32_t device, const uint64_t *a, const uint64_t *b, int64_t n, int64_t words,
+                             float *out);
+/* BinaryQuantizer.Encode batched (compressionhelpers/binary_quantization.go:28-47) */
+int wv_bq_encode_batch(int32_t device, const float *vecs, int64_t n, int64_t d, uint64_t *out_codes);
+/* distancer.Normalize batched (distancer/normalize.go:16-32) */
+int wv_normalize_batch(int32_t device, const float *vecs, int64_t n, int64_t d, float *out);
+
+/* synthetic data (bench/tests): kind 0 U[-1,1), 1 integer U{0..127}, 2 U[0,1) */
+int wv_gen_device(int32_t device, int32_t kind, uint64_t seed, uint64_t row0, int64_t rows, int64_t d, float *d_out,
+                  void *stream);
+
+/* counters (docs/metrics.md analogue) */
+typedef struct wv_stats {
+    uint64_t queries;
+    uint64_t batches;
+    uint64_t replayed_queries;
+    uint64_t mfma_launches;
+    double last_select_ms;   /* k_mfma_select time of the last batch (HIP events) */
+    double last_total_ms;
+} wv_stats;
+int wv_index_stats(wv_index *idx, wv_stats *out);
+
+/* tuning / testing knobs: "margin" (extra candidates, default 8),
+ * "force_replay" (1 = resolve every query by heap replay), "spans" (0 = auto),
+ * "timing" (1 = record kernel times with HIP events) */
+int wv_index_set_option(wv_index *idx, const char *key, int64_t value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WV_KNN_H */

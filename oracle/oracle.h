@@ -1,0 +1,59 @@
+/* oracle.h -- TEST INFRASTRUCTURE ONLY: CPU restatement of the reference's
+ * flat-index hot path (see oracle.c).  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this. */
+#ifndef WV_ORACLE_H
+#define WV_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { OR_L2 = 0, OR_DOT = 1, OR_COSINE = 2, OR_HAMMING = 3 };
+enum { OR_AVX256 = 1, OR_AVX512 = 2 };
+enum { OR_ERR_VECTOR_LENGTH = -1, OR_ERR_HAMMING_LENGTH = -2 };
+
+typedef struct {
+    uint64_t *id;
+    float *dist;
+    int len;
+} or_heap;
+
+float or_l2_256(const float *a, const float *b, long n);
+float or_l2_512(const float *a, const float *b, long n);
+float or_dot_256(const float *a, const float *b, long n);
+float or_dot_512(const float *a, const float *b, long n);
+float or_hamming_f32(const float *a, const float *b, long n);
+float or_hamming_bitwise(const uint64_t *a, const uint64_t *b, long n);
+void or_normalize(const float *v, float *out, long n);
+float or_single_dist(int metric, int variant, const float *a, const float *b, long n);
+
+void or_heap_insert(or_heap *h, uint64_t id, float dist);
+void or_heap_pop(or_heap *h, uint64_t *id, float *dist);
+void or_insert_to_heap(or_heap *h, int limit, uint64_t id, float dist);
+int or_extract_heap(or_heap *h, uint64_t *ids, float *dists);
+
+int or_find_top_vectors(or_heap *heap, int limit, int metric, int variant, const float *store,
+                        const uint8_t *present, long nslots, long d, const float *query, long qd,
+                        const uint8_t *allow, long slot_begin, long slot_end);
+int or_flat_search(int metric, int variant, const float *store, const uint8_t *present, long nslots,
+                   long d, const float *query, long qd, int k, const uint8_t *allow, int allow_empty,
+                   uint64_t *out_ids, float *out_dists, int *out_n);
+
+void or_bq_encode(const float *vec, long d, uint64_t *code);
+int or_flat_search_bq(int metric, int variant, const float *store, const uint8_t *present,
+                      const uint8_t *fp32_present, const uint64_t *codes, long nslots, long d,
+                      const float *query, long qd, int k, int rescore_limit, const uint8_t *allow,
+                      int allow_empty, uint64_t *out_ids, float *out_dists, int *out_n);
+
+int or_filter_by_distance(const uint64_t *ids, const float *dists, int n, float target,
+                          uint64_t *out_ids, float *out_dists);
+
+uint64_t or_gen_bits(uint64_t seed, uint64_t row, uint64_t col);
+float or_gen_value(int kind, uint64_t seed, uint64_t row, uint64_t col);
+void or_gen_matrix(int kind, uint64_t seed, uint64_t row0, long rows, long d, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

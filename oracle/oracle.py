@@ -1,0 +1,190 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes wrapper of oracle/liboracle.so (the CPU
+restatement of the reference's flat-index hot path, oracle/oracle.c) and of
+oracle/_ref/libref.so (the reference's own distance kernels compiled from
+/root/reference).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref.so")
+
+L2, DOT, COSINE, HAMMING = 0, 1, 2, 3
+AVX256, AVX512 = 1, 2
+METRIC = {"l2-squared": L2, "dot": DOT, "cosine": COSINE, "cosine-dot": COSINE, "hamming": HAMMING}
+
+pf = C.POINTER(C.c_float)
+pu = C.POINTER(C.c_uint64)
+pi = C.POINTER(C.c_int)
+pb = C.POINTER(C.c_uint8)
+
+_o = None
+_r = None
+
+
+def lib() -> C.CDLL:
+    global _o
+    if _o is None:
+        if not os.path.exists(ORACLE_SO):
+            import subprocess
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        o = C.CDLL(ORACLE_SO)
+        for n in ["or_l2_256", "or_l2_512", "or_dot_256", "or_dot_512", "or_hamming_f32"]:
+            getattr(o, n).restype = C.c_float
+            getattr(o, n).argtypes = [pf, pf, C.c_long]
+        o.or_hamming_bitwise.restype = C.c_float
+        o.or_hamming_bitwise.argtypes = [pu, pu, C.c_long]
+        o.or_normalize.argtypes = [pf, pf, C.c_long]
+        o.or_single_dist.restype = C.c_float
+        o.or_single_dist.argtypes = [C.c_int, C.c_int, pf, pf, C.c_long]
+        o.or_flat_search.restype = C.c_int
+        o.or_flat_search.argtypes = [C.c_int, C.c_int, pf, pb, C.c_long, C.c_long, pf, C.c_long, C.c_int, pb,
+                                     C.c_int, pu, pf, pi]
+        o.or_bq_encode.argtypes = [pf, C.c_long, pu]
+        o.or_flat_search_bq.restype = C.c_int
+        o.or_flat_search_bq.argtypes = [C.c_int, C.c_int, pf, pb, pb, pu, C.c_long, C.c_long, pf, C.c_long, C.c_int,
+                                        C.c_int, pb, C.c_int, pu, pf, pi]
+        o.or_filter_by_distance.restype = C.c_int
+        o.or_filter_by_distance.argtypes = [pu, pf, C.c_int, C.c_float, pu, pf]
+        o.or_gen_matrix.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_long, C.c_long, pf]
+        o.or_gen_value.restype = C.c_float
+        o.or_gen_value.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64]
+        o.bl_set_ref_kernels.argtypes = [C.c_void_p] * 4
+        o.bl_flat_search_batch.restype = C.c_int
+        o.bl_flat_search_batch.argtypes = [C.c_int, C.c_int, C.c_int, pf, C.c_long, C.c_long, pf, C.c_long, C.c_int,
+                                           C.c_int, pu, pf, pi]
+        _o = o
+    return _o
+
+
+def ref_lib() -> Optional[C.CDLL]:
+    """The reference's compiled kernels, if built (None otherwise)."""
+    global _r
+    if _r is None and os.path.exists(REF_SO):
+        _r = C.CDLL(REF_SO)
+    return _r
+
+
+def host_has_avx512() -> bool:
+    try:
+        flags = open("/proc/cpuinfo").read()
+    except OSError:
+        return False
+    return " avx512f" in flags and " avx512dq" in flags and " avx512vl" in flags
+
+
+def f(a):
+    return a.ctypes.data_as(pf)
+
+
+def single_dist(metric: int, variant: int, a: np.ndarray, b: np.ndarray) -> float:
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    return lib().or_single_dist(metric, variant, f(a), f(b), a.size)
+
+
+def ref_kernel(name: str, a: np.ndarray, b: np.ndarray) -> float:
+    """Call one of the reference's compiled kernels (l2_256, dot_512, ...)."""
+    r = ref_lib()
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    res = C.c_float()
+    n = C.c_long(a.size)
+    getattr(r, name)(f(a), f(b), C.byref(res), C.byref(n))
+    return res.value
+
+
+def normalize(v: np.ndarray) -> np.ndarray:
+    v = np.ascontiguousarray(v, dtype=np.float32)
+    out = np.zeros_like(v)
+    lib().or_normalize(f(v), f(out), v.size)
+    return out
+
+
+def bq_encode(v: np.ndarray) -> np.ndarray:
+    v = np.ascontiguousarray(v, dtype=np.float32)
+    out = np.zeros((v.size + 63) // 64, dtype=np.uint64)
+    lib().or_bq_encode(f(v), v.size, out.ctypes.data_as(pu))
+    return out
+
+
+def hamming_bitwise(a: np.ndarray, b: np.ndarray) -> float:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    return lib().or_hamming_bitwise(a.ctypes.data_as(pu), b.ctypes.data_as(pu), a.size)
+
+
+class OracleFlat:
+    """Oracle flat index: id-indexed store, vectors normalised at Add for cosine
+    (flat/index.go:371), scanned in ascending id order."""
+
+    def __init__(self, metric: int, variant: int, d: int, nslots: int):
+        self.metric, self.variant, self.d = metric, variant, d
+        self.store = np.zeros((nslots, d), dtype=np.float32)
+        self.present = np.zeros(nslots, dtype=np.uint8)
+
+    def add_batch(self, ids, vecs):
+        vecs = np.asarray(vecs, dtype=np.float32)
+        for i, v in zip(ids, vecs):
+            self.store[int(i)] = normalize(v) if self.metric == COSINE else v
+            self.present[int(i)] = 1
+
+    def delete(self, ids):
+        for i in ids:
+            self.present[int(i)] = 0
+
+    def search(self, query, k, allow=None):
+        """-> (rc, ids, dists); allow: iterable of ids or None."""
+        q = np.ascontiguousarray(query, dtype=np.float32)
+        ids = np.zeros(max(k, 1), dtype=np.uint64)
+        dd = np.zeros(max(k, 1), dtype=np.float32)
+        n = C.c_int(0)
+        allow_bm = None
+        allow_empty = 0
+        if allow is not None:
+            allow_bm = np.zeros(len(self.present), dtype=np.uint8)
+            a = [int(x) for x in allow if int(x) < len(self.present)]
+            allow_bm[a] = 1
+            allow_empty = 1 if len(list(allow)) == 0 else 0
+        rc = lib().or_flat_search(self.metric, self.variant, f(self.store), self.present.ctypes.data_as(pb),
+                                  len(self.present), self.d, f(q), q.size, k,
+                                  allow_bm.ctypes.data_as(pb) if allow_bm is not None else None, allow_empty,
+                                  ids.ctypes.data_as(pu), f(dd), C.byref(n))
+        return rc, ids[: n.value].copy(), dd[: n.value].copy()
+
+
+def gen_matrix(kind: int, seed: int, row0: int, rows: int, d: int) -> np.ndarray:
+    out = np.zeros((rows, d), dtype=np.float32)
+    lib().or_gen_matrix(kind, seed, row0, rows, d, f(out))
+    return out
+
+
+def cpu_baseline(metric: int, variant: int, store: np.ndarray, queries: np.ndarray, k: int, nthreads: int,
+                 use_ref: bool):
+    """Multi-threaded CPU scan (oracle/baseline.c).  queries must be
+    normalised already for cosine.  Returns (ids, dists, counts)."""
+    o = lib()
+    if use_ref:
+        r = ref_lib()
+        if r is None:
+            raise RuntimeError("oracle/_ref/libref.so not built")
+        o.bl_set_ref_kernels(C.cast(r.l2_256, C.c_void_p), C.cast(r.l2_512, C.c_void_p),
+                             C.cast(r.dot_256, C.c_void_p), C.cast(r.dot_512, C.c_void_p))
+    store = np.ascontiguousarray(store, dtype=np.float32)
+    queries = np.ascontiguousarray(queries, dtype=np.float32)
+    nq = queries.shape[0]
+    ids = np.zeros((nq, k), dtype=np.uint64)
+    dd = np.zeros((nq, k), dtype=np.float32)
+    cnt = np.zeros(nq, dtype=np.int32)
+    rc = o.bl_flat_search_batch(metric, variant, 1 if use_ref else 0, f(store), store.shape[0], store.shape[1],
+                                f(queries), nq, k, nthreads, ids.ctypes.data_as(pu), f(dd), cnt.ctypes.data_as(pi))
+    if rc != 0:
+        raise RuntimeError("baseline failed")
+    return ids, dd, cnt

@@ -1,0 +1,198 @@
+"""GPU parity: the HIP flat index vs the oracle (CPU restatement of
+flat/index.go + priorityqueue + distancer), bit-exact ids and distances.
+
+Runs on an MI355X only (marker gpu).  Sizes keep the oracle to seconds.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = {"avx256": 1, "avx512": 2}
+
+
+def gen(oracle, kind, seed, rows, d, row0=0):
+    return oracle.gen_matrix(kind, seed, row0, rows, d)
+
+
+def assert_same(oracle_res, ids, dists, ctx=""):
+    rc, oids, od = oracle_res
+    assert rc == 0
+    assert len(ids) == len(oids), f"{ctx}: count {len(ids)} vs {len(oids)}"
+    np.testing.assert_array_equal(ids, oids, err_msg=f"{ctx}: ids")
+    # bit-exact distances
+    np.testing.assert_array_equal(np.asarray(dists, np.float32).view(np.uint32),
+                                  np.asarray(od, np.float32).view(np.uint32), err_msg=f"{ctx}: dists")
+
+
+def build_pair(wv, oracle, metric_name, variant, data, ids=None, dims=0):
+    n, d = data.shape
+    ids = np.arange(n, dtype=np.uint64) if ids is None else ids
+    idx = wv.FlatIndex(distance=metric_name, variant=variant, dims=dims)
+    idx.add_batch(ids, data)
+    orc = oracle.OracleFlat(oracle.METRIC[metric_name], VARIANTS[variant], d, int(ids.max()) + 1)
+    orc.add_batch(ids, data)
+    return idx, orc
+
+
+@pytest.mark.parametrize("variant", ["avx256", "avx512"])
+@pytest.mark.parametrize("metric", ["l2-squared", "dot", "cosine"])
+def test_distance_batch_bit_exact(wv, oracle, metric, variant):
+    rng = np.random.default_rng(1)
+    for d in [1, 3, 7, 8, 9, 31, 32, 33, 100, 127, 128, 129, 200, 255, 256, 300, 768, 960, 1536]:
+        a = rng.standard_normal((64, d)).astype(np.float32)
+        b = rng.standard_normal((64, d)).astype(np.float32) * np.float32(3.0)
+        got = wv.single_dist_batch(metric, a, b, variant=variant)
+        exp = np.array([oracle.single_dist(oracle.METRIC[metric], VARIANTS[variant], a[i], b[i])
+                        for i in range(64)], dtype=np.float32)
+        np.testing.assert_array_equal(got.view(np.uint32), exp.view(np.uint32), err_msg=f"d={d}")
+
+
+def test_normalize_bit_exact(wv, oracle):
+    rng = np.random.default_rng(2)
+    for d in [1, 5, 128, 768, 1536]:
+        v = (rng.standard_normal((50, d)) * 10).astype(np.float32)
+        v[0] = 0
+        got = wv.normalize_batch(v)
+        exp = np.stack([oracle.normalize(x) for x in v])
+        np.testing.assert_array_equal(got.view(np.uint32), exp.view(np.uint32))
+
+
+def test_hamming_and_bq_exact(wv, oracle):
+    rng = np.random.default_rng(3)
+    for d in [1, 63, 64, 65, 128, 1536]:
+        v = rng.standard_normal((40, d)).astype(np.float32)
+        codes = wv.bq_encode_batch(v)
+        exp = np.stack([oracle.bq_encode(x) for x in v])
+        np.testing.assert_array_equal(codes, exp)
+        h = wv.hamming_bitwise_batch(codes[:20], codes[20:])
+        eh = np.array([oracle.hamming_bitwise(codes[i], codes[20 + i]) for i in range(20)], np.float32)
+        np.testing.assert_array_equal(h, eh)
+
+
+@pytest.mark.parametrize("variant", ["avx256", "avx512"])
+@pytest.mark.parametrize("metric,kind,n,d,k", [
+    ("l2-squared", 0, 20000, 128, 10),   # C1-shaped (scaled): U(-1,1)
+    ("cosine", 0, 6000, 768, 10),        # C3-shaped (scaled)
+    ("dot", 0, 8000, 96, 7),
+    ("l2-squared", 1, 6000, 128, 10),    # SIFT-shaped integer data: ties -> replay
+    ("cosine", 0, 3000, 33, 24),         # ragged dims, max fast-path k
+])
+def test_search_matches_oracle(wv, oracle, metric, kind, n, d, k, variant):
+    data = gen(oracle, kind, 11, n, d)
+    queries = gen(oracle, kind, 12, 48, d)
+    idx, orc = build_pair(wv, oracle, metric, variant, data)
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    for qi in range(len(queries)):
+        res = orc.search(queries[qi], k)
+        assert_same(res, ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"q{qi}")
+    idx.close()
+
+
+def test_forced_replay_equals_fast_path(wv, oracle):
+    data = gen(oracle, 0, 21, 5000, 64)
+    queries = gen(oracle, 0, 22, 32, 64)
+    idx, orc = build_pair(wv, oracle, "l2-squared", "avx256", data)
+    ids1, d1, c1 = idx.search_by_vector_batch(queries, 10)
+    idx.set_option("force_replay", 1)
+    ids2, d2, c2 = idx.search_by_vector_batch(queries, 10)
+    np.testing.assert_array_equal(ids1, ids2)
+    np.testing.assert_array_equal(d1.view(np.uint32), d2.view(np.uint32))
+    assert idx.stats()["replayed_queries"] >= 32
+
+
+def test_ties_duplicates_heap_order(wv, oracle):
+    """Many exactly duplicated vectors: result order must follow the reference
+    heap layout, not (dist, id)."""
+    base = gen(oracle, 1, 31, 50, 8)
+    data = np.concatenate([base] * 40)  # 2000 rows, each vector 40 times
+    queries = gen(oracle, 1, 32, 16, 8)
+    for k in [1, 5, 10, 17]:
+        idx, orc = build_pair(wv, oracle, "l2-squared", "avx256", data)
+        ids, dists, counts = idx.search_by_vector_batch(queries, k)
+        for qi in range(len(queries)):
+            assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"k{k} q{qi}")
+        idx.close()
+
+
+def test_large_k_replay_path(wv, oracle):
+    data = gen(oracle, 0, 41, 4000, 48)
+    queries = gen(oracle, 0, 42, 8, 48)
+    idx, orc = build_pair(wv, oracle, "cosine", "avx256", data)
+    ids, dists, counts = idx.search_by_vector_batch(queries, 100)
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], 100), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
+
+
+def test_allow_list_delete_upsert(wv, oracle):
+    data = gen(oracle, 0, 51, 3000, 40)
+    queries = gen(oracle, 0, 52, 8, 40)
+    idx, orc = build_pair(wv, oracle, "dot", "avx256", data)
+    # upsert some ids, delete others
+    new = gen(oracle, 0, 53, 100, 40)
+    up_ids = np.arange(500, 600, dtype=np.uint64)
+    idx.add_batch(up_ids, new)
+    orc.add_batch(up_ids, new)
+    dels = list(range(0, 3000, 7))
+    idx.delete(*dels)
+    orc.delete(dels)
+    allow = list(range(100, 2500, 3))
+    al = wv.AllowList(allow)
+    ids, dists, counts = idx.search_by_vector_batch(queries, 10, allow=al)
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], 10, allow=allow), ids[qi, :counts[qi]], dists[qi, :counts[qi]],
+                    f"q{qi}")
+    # empty allow list -> empty result, no error (flat/index.go:590-594)
+    ids, d_ = idx.search_by_vector(queries[0], 10, allow=wv.AllowList([]))
+    assert len(ids) == 0
+    assert idx.already_indexed() == 3100
+    assert not idx.contains_doc(7) and idx.contains_doc(8)
+
+
+def test_sparse_ids_and_small_corpus(wv, oracle):
+    data = gen(oracle, 0, 61, 5, 16)
+    ids = np.array([3, 1000, 17, 4096, 9], dtype=np.uint64)
+    idx, orc = build_pair(wv, oracle, "l2-squared", "avx256", data, ids=ids)
+    q = gen(oracle, 0, 62, 4, 16)
+    for k in [1, 3, 5, 10]:
+        got_ids, got_d, cnt = idx.search_by_vector_batch(q, k)
+        for qi in range(4):
+            assert_same(orc.search(q[qi], k), got_ids[qi, :cnt[qi]], got_d[qi, :cnt[qi]], f"k{k}")
+
+
+def test_errors_and_edge_cases(wv):
+    idx = wv.FlatIndex(distance="l2-squared", root_path="/tmp/x")
+    with pytest.raises(wv.WeaviateError, match="cannot insert vector of dimension 0"):
+        idx.add(1, np.zeros(0, np.float32))
+    # empty index: no error, empty result
+    ids, d = idx.search_by_vector(np.ones(3, np.float32), 5)
+    assert len(ids) == 0
+    idx.add(1, np.array([3, 4, 5], np.float32))
+    with pytest.raises(wv.WeaviateError, match=r"insert called with a vector of the wrong size: 2\. Saved length: 3, path: /tmp/x"):
+        idx.add(2, np.array([1, 2], np.float32))
+    with pytest.raises(wv.WeaviateError, match="vector lengths don't match"):
+        idx.search_by_vector(np.ones(4, np.float32), 5)
+    with pytest.raises(wv.WeaviateError, match="insertBatch called with empty lists"):
+        idx.add_batch([], [])
+    with pytest.raises(wv.WeaviateError, match="ids and vectors sizes does not match"):
+        idx.add_batch([1, 2], [np.ones(3, np.float32)])
+    ids, d = idx.search_by_vector(np.array([1.5, 2, 2.5], np.float32), 5)
+    assert list(ids) == [1] and d[0] == np.float32(12.5)  # distancer/l2_test.go known answer
+    # 1-d vectors (flat/index_test.go TestEdgeCases)
+    one = wv.FlatIndex(distance="cosine")
+    one.add(0, np.array([1.0], np.float32))
+    one.add(1, np.array([-2.0], np.float32))
+    ids, d = one.search_by_vector(np.array([5.0], np.float32), 2)
+    assert list(ids) == [0, 1] and d[0] == 0 and d[1] == 2
+
+
+def test_search_by_vector_distance(wv, oracle):
+    data = gen(oracle, 0, 71, 2000, 24)
+    idx, orc = build_pair(wv, oracle, "cosine", "avx256", data)
+    q = gen(oracle, 0, 72, 1, 24)[0]
+    rc, oids, od = orc.search(q, 100)
+    target = float(od[30])
+    ids, d = idx.search_by_vector_distance(q, target, 10000)
+    exp = [(i, x) for i, x in zip(oids, od) if x <= target or abs(float(x) - target) <= 1e-6]
+    assert list(ids) == [e[0] for e in exp][: len(ids)]
+    assert len(ids) == 31

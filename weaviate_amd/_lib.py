@@ -1,0 +1,126 @@
+"""ctypes binding of the C ABI in include/wv_knn.h.
+
+The library is the product: if libwvknn.so is missing or fails to load, every
+entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libwvknn.so")
+
+WV_OK = 0
+WV_ERR_INVALID = -1
+WV_ERR_VECTOR_LENGTH = -2
+WV_ERR_INSERT = -3
+WV_ERR_HIP = -4
+WV_ERR_UNSUPPORTED = -5
+WV_ERR_QUANTIZER = -6
+
+METRIC_L2 = 0
+METRIC_DOT = 1
+METRIC_COSINE = 2
+METRIC_HAMMING = 3
+
+VARIANT_AUTO = 0
+VARIANT_AVX256 = 1
+VARIANT_AVX512 = 2
+
+COMPRESSION_NONE = 0
+COMPRESSION_BQ = 1
+
+
+class WvConfig(C.Structure):
+    _fields_ = [
+        ("metric", C.c_int32),
+        ("dims", C.c_int32),
+        ("compression", C.c_int32),
+        ("rescore_limit", C.c_int32),
+        ("device", C.c_int32),
+        ("variant", C.c_int32),
+        ("id_base", C.c_uint64),
+        ("root_path", C.c_char_p),
+    ]
+
+
+class WvStats(C.Structure):
+    _fields_ = [
+        ("queries", C.c_uint64),
+        ("batches", C.c_uint64),
+        ("replayed_queries", C.c_uint64),
+        ("mfma_launches", C.c_uint64),
+        ("last_select_ms", C.c_double),
+        ("last_total_ms", C.c_double),
+    ]
+
+
+P = C.c_void_p
+i32, i64, u64, f32 = C.c_int32, C.c_int64, C.c_uint64, C.c_float
+pf32 = C.POINTER(C.c_float)
+pu64 = C.POINTER(C.c_uint64)
+pi32 = C.POINTER(C.c_int32)
+
+# name -> (restype, argtypes); every symbol declared in include/wv_knn.h
+SIGNATURES = {
+    "wv_last_error": (C.c_char_p, []),
+    "wv_resolve_variant": (C.c_int, [i32]),
+    "wv_index_create": (C.c_int, [C.POINTER(WvConfig), C.POINTER(P)]),
+    "wv_index_destroy": (None, [P]),
+    "wv_index_reserve": (C.c_int, [P, u64]),
+    "wv_index_validate_before_insert": (C.c_int, [P, i64]),
+    "wv_index_add": (C.c_int, [P, u64, pf32, i64]),
+    "wv_index_add_batch": (C.c_int, [P, pu64, pf32, i64, i64]),
+    "wv_index_add_range_device": (C.c_int, [P, u64, P, i64, i64]),
+    "wv_index_delete": (C.c_int, [P, pu64, i64]),
+    "wv_index_contains_doc": (C.c_int, [P, u64]),
+    "wv_index_already_indexed": (u64, [P]),
+    "wv_index_dims": (i32, [P]),
+    "wv_index_search_by_vector_batch": (C.c_int, [P, pf32, i64, i64, i32, pu64, i64, i32, pu64, pf32, pi32]),
+    "wv_index_search_by_vector_distance": (C.c_int, [P, pf32, i64, f32, i64, pu64, i64, i32, pu64, pf32, pi32]),
+    "wv_index_search_device": (C.c_int, [P, P, i64, i64, i32, i32, P, P, P, P, P]),
+    "wv_index_replay": (C.c_int, [P, P, i64, i64, i32, pi32, i32, pu64, pf32, pi32, i32, pu64, pf32, pi32]),
+    "wv_merge_shards": (C.c_int, [i32, i32, i64, i32, P, P, P, P, P, P, P, P, P]),
+    "wv_distance_batch": (C.c_int, [i32, i32, i32, pf32, pf32, i64, i64, pf32]),
+    "wv_hamming_bitwise_batch": (C.c_int, [i32, pu64, pu64, i64, i64, pf32]),
+    "wv_bq_encode_batch": (C.c_int, [i32, pf32, i64, i64, pu64]),
+    "wv_normalize_batch": (C.c_int, [i32, pf32, i64, i64, pf32]),
+    "wv_gen_device": (C.c_int, [i32, i32, u64, u64, i64, i64, P, P]),
+    "wv_index_stats": (C.c_int, [P, C.POINTER(WvStats)]),
+    "wv_index_set_option": (C.c_int, [P, C.c_char_p, i64]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libwvknn.so (raises if missing -- no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"weaviate_amd: {LIB_PATH} not built; run `python -m weaviate_amd.build` "
+            "(the HIP library is required, there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class WeaviateError(RuntimeError):
+    """Carries the reference's error text (wv_last_error)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+
+
+def check(rc: int) -> None:
+    if rc != WV_OK:
+        msg = load().wv_last_error()
+        raise WeaviateError(rc, msg.decode() if msg else f"error {rc}")

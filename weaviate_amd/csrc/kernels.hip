@@ -1,0 +1,709 @@
+// kernels.hip -- gfx950 kernels of the flat-index hot path.
+//
+// Pipeline for SearchByVector over a batch of queries (flat/index.go:423-448,
+// :578-688), per GPU:
+//   k_prepare_rows      normalise (cosine, distancer/normalize.go:16-32) and
+//                       store rows + squared norms          [Add, :362-390]
+//   k_mfma_select       f32 MFMA (v_mfma_f32_32x32x2_f32) query x corpus tiles
+//                       fused with per-(query, corpus span) top-KP selection
+//                       on an approximate distance; the B x N distance matrix
+//                       is never written.
+//   k_merge_spans       merge the span lists of a query       (wave per query)
+//   k_rescore           exact-order distance of the KP candidates (lane per pair)
+//   k_finalize          sort by exact distance, prove the result equals the
+//                       reference heap's (margin + no ties), else flag
+//   k_replay            flagged queries: exact replay of the reference heap
+//                       (priorityqueue NewMax + insertToHeap) over the id-ordered
+//                       scan, with exact-order distances.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "wv_device.h"
+
+namespace wv {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// row preparation
+// ---------------------------------------------------------------------------
+
+// One lane per row: out row = normalize(in row) for cosine, else a copy; pad
+// columns [d, dpad) are zeroed.  norm2[row] = sum of squares of the stored row
+// (any order: only feeds the approximate L2 and the error bound).
+// maxnorm2_bits: atomicMax over the float bits of norm2 (non-negative floats
+// order like their bit patterns).
+template <int METRIC>
+__global__ void k_prepare_rows(const float* __restrict__ in, int64_t n, int d, const uint32_t* __restrict__ slots,
+                               float* __restrict__ out, int dpad, float* __restrict__ norm2,
+                               uint32_t* __restrict__ present_bits, uint32_t* __restrict__ maxnorm2_bits) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* src = in + i * (int64_t)d;
+    int64_t slot = slots ? (int64_t)slots[i] : i;
+    float* dst = out + slot * (int64_t)dpad;
+    float divisor = 1.f;
+    bool zero = false;
+    if (METRIC == COSINE) {
+        float nrm = 0.f;
+        for (int c = 0; c < d; c++) { float v = src[c]; float sq = v * v; nrm = nrm + sq; }
+        if (nrm == 0.f) zero = true;
+        else divisor = (float)sqrt((double)nrm);
+    }
+    float s2 = 0.f;
+    for (int c = 0; c < d; c++) {
+        float v = src[c];
+        if (METRIC == COSINE) v = zero ? 0.f : v / divisor;
+        dst[c] = v;
+        s2 = fmaf(v, v, s2);
+    }
+    for (int c = d; c < dpad; c++) dst[c] = 0.f;
+    if (norm2) norm2[slot] = s2;
+    if (present_bits) atomicOr(&present_bits[slot >> 5], 1u << (slot & 31));
+    if (maxnorm2_bits) atomicMax(maxnorm2_bits, __float_as_uint(s2));
+}
+
+// ---------------------------------------------------------------------------
+// main MFMA + selection kernel
+// ---------------------------------------------------------------------------
+// Block: 256 threads = 4 waves in a 2 (queries) x 2 (corpus rows) layout over a
+// 128-query x 128-row tile; each wave owns 64x64 = 2x2 MFMA 32x32 blocks.  The
+// MFMA computes C^T: A = corpus rows (i = row), B = queries (j = query), so the
+// accumulator layout puts the query on the lane (col = lane&31) and 16 corpus
+// rows in registers (row = (r&3) + 8(r>>2) + 4(lane>>5)).
+//
+// LDS staging (per BK=32 slice): rows stored de-interleaved [even k | odd k]
+// with a 36-float stride, so a lane's 16 k-values for the 16 MFMA k-steps are
+// one contiguous 64 B run (4 x ds_read_b128) and the 16-lane ds_read_b128
+// groups hit 16 distinct 4-bank slots (conflict-free).
+constexpr int QB = 128;   // queries per workgroup tile
+constexpr int BN = 128;   // corpus rows per tile
+constexpr int BK = 32;    // k per staging step
+constexpr int LDSROW = 36;
+
+struct SelectArgs {
+    const float* X;           // [cap][dpad]
+    const float* xnorm2;      // [cap]
+    const uint32_t* valid;    // bitmap over slots: present & allowed
+    int64_t ntiles;           // tiles of BN rows to scan
+    const float* Q;           // [nq_pad][dpad]
+    const float* qnorm2;      // [nq_pad]
+    int nq;
+    int dpad;
+    int tiles_per_span;
+    int nspans;
+    int nqb;
+    int KP;
+    float* outA;              // [nq_pad][nspans][KP]
+    uint32_t* outI;
+};
+
+template <int R>
+__device__ __forceinline__ void merge_query_list(float* listA, uint32_t* listI, const float* cbA,
+                                                 const uint32_t* cbI, int KP, int C, int nc, int lane,
+                                                 float* thr_slot) {
+    float key[R];
+    uint32_t id[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        int e = r * 64 + lane;
+        if (e < KP) { key[r] = listA[e]; id[r] = listI[e]; }
+        else if (e - KP < nc) { key[r] = cbA[e - KP]; id[r] = cbI[e - KP]; }
+        else { key[r] = __builtin_inff(); id[r] = NO_ID; }
+    }
+    bitonic_sort<R>(key, id, lane);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        int e = r * 64 + lane;
+        if (e < KP) { listA[e] = key[r]; listI[e] = id[r]; }
+        if (e == KP - 1) *thr_slot = key[r];
+    }
+}
+
+template <int METRIC, int R>
+__global__ __launch_bounds__(256, 1) void k_mfma_select(SelectArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int KP = a.KP;
+    const int C = 64 * R - KP;
+    float* Xs = smem;                                   // QB*LDSROW
+    float* Qs = Xs + BN * LDSROW;                       // QB*LDSROW
+    float* listA = Qs + QB * LDSROW;                    // QB*KP
+    uint32_t* listI = reinterpret_cast<uint32_t*>(listA + QB * KP);
+    float* cbA = reinterpret_cast<float*>(listI + QB * KP);  // QB*C
+    uint32_t* cbI = reinterpret_cast<uint32_t*>(cbA + QB * C);
+    float* thr = reinterpret_cast<float*>(cbI + QB * C);     // QB
+    int* cnt = reinterpret_cast<int*>(thr + QB);             // QB
+    int* flags = cnt + QB;                                   // [0]=any, [1]=ovf
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wq = wave & 1, wx = wave >> 1;
+    const int li = lane & 31, lh = lane >> 5;
+
+    // block -> (query block, span) with an XCD-aware swizzle: blocks of one span
+    // land on one XCD so its corpus tiles are shared through that XCD's L2.
+    const int total = a.nqb * a.nspans;
+    int b = blockIdx.x;
+    int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int qb = logical % a.nqb;
+    const int span = logical / a.nqb;
+    const int q0 = qb * QB;
+
+    for (int i = tid; i < QB * KP; i += 256) { listA[i] = __builtin_inff(); listI[i] = NO_ID; }
+    if (tid < QB) { thr[tid] = __builtin_inff(); cnt[tid] = 0; }
+    if (tid == 0) { flags[0] = 0; flags[1] = 0; }
+
+    const int64_t t0 = (int64_t)span * a.tiles_per_span;
+    int64_t t1 = t0 + a.tiles_per_span;
+    if (t1 > a.ntiles) t1 = a.ntiles;
+    const int nk = a.dpad / BK;
+    const int64_t total_steps = t1 > t0 ? (t1 - t0) * nk : 0;
+
+    // staging: thread -> row tid>>1, 16 contiguous floats at 16*(tid&1)
+    const int srow = tid >> 1, shalf = tid & 1;
+    float4 px[4], pq[4];
+    auto prefetch = [&](int64_t step) {
+        int64_t tile = t0 + step / nk;
+        int kb = (int)(step % nk);
+        const float* xp = a.X + (tile * BN + srow) * (int64_t)a.dpad + kb * BK + 16 * shalf;
+        const float* qp = a.Q + (int64_t)(q0 + srow) * a.dpad + kb * BK + 16 * shalf;
+#pragma unroll
+        for (int c = 0; c < 4; c++) { px[c] = ld4(xp + 4 * c); pq[c] = ld4(qp + 4 * c); }
+    };
+    auto stage = [&](float* dst, const float4 (&p)[4]) {
+        // even elements -> [8*half, 8*half+8), odd -> 16 + [8*half, 8*half+8)
+        float4 e0 = make_float4(p[0].x, p[0].z, p[1].x, p[1].z);
+        float4 e1 = make_float4(p[2].x, p[2].z, p[3].x, p[3].z);
+        float4 o0 = make_float4(p[0].y, p[0].w, p[1].y, p[1].w);
+        float4 o1 = make_float4(p[2].y, p[2].w, p[3].y, p[3].w);
+        float* base = dst + srow * LDSROW + 8 * shalf;
+        *reinterpret_cast<float4*>(base) = e0;
+        *reinterpret_cast<float4*>(base + 4) = e1;
+        *reinterpret_cast<float4*>(base + 16) = o0;
+        *reinterpret_cast<float4*>(base + 20) = o1;
+    };
+
+    f32x16 acc[2][2];
+    int epoch = 0;
+    if (total_steps > 0) prefetch(0);
+    __syncthreads();
+
+    for (int64_t step = 0; step < total_steps; step++) {
+        const int64_t tile = t0 + step / nk;
+        const int kb = (int)(step % nk);
+        if (kb == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+        }
+        __syncthreads();
+        stage(Xs, px);
+        stage(Qs, pq);
+        __syncthreads();
+        if (step + 1 < total_steps) prefetch(step + 1);
+
+        // 16 MFMA k-steps over this BK slice
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            float fa[2][8], fb[2][8];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const float* xr = Xs + (64 * wx + 32 * i + li) * LDSROW + 16 * lh + 8 * half;
+                const float* qr = Qs + (64 * wq + 32 * i + li) * LDSROW + 16 * lh + 8 * half;
+                float4 x0 = *reinterpret_cast<const float4*>(xr), x1 = *reinterpret_cast<const float4*>(xr + 4);
+                float4 y0 = *reinterpret_cast<const float4*>(qr), y1 = *reinterpret_cast<const float4*>(qr + 4);
+                fa[i][0] = x0.x; fa[i][1] = x0.y; fa[i][2] = x0.z; fa[i][3] = x0.w;
+                fa[i][4] = x1.x; fa[i][5] = x1.y; fa[i][6] = x1.z; fa[i][7] = x1.w;
+                fb[i][0] = y0.x; fb[i][1] = y0.y; fb[i][2] = y0.z; fb[i][3] = y0.w;
+                fb[i][4] = y1.x; fb[i][5] = y1.y; fb[i][6] = y1.z; fb[i][7] = y1.w;
+            }
+#pragma unroll
+            for (int s = 0; s < 8; s++)
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+        }
+
+        if (kb != nk - 1) continue;
+
+        // ---------------- epilogue: selection over this tile ----------------
+        const int64_t row0 = tile * BN;
+        // values -> distances (in place); invalid rows / padded queries -> +inf
+        float qn[2];
+        int qidx[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            qidx[j] = 64 * wq + 32 * j + li;
+            qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
+        }
+        const uint32_t* vb = a.valid + (row0 >> 5);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                bool ok = (vb[rt >> 5] >> (rt & 31)) & 1u;
+                float xn = (METRIC == L2) ? a.xnorm2[row0 + rt] : 0.f;
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    float dot = acc[i][j][r];
+                    float v;
+                    if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
+                    else if (METRIC == DOT) v = -dot;
+                    else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
+                    bool qok = (q0 + qidx[j]) < a.nq;
+                    acc[i][j][r] = (ok && qok) ? v : __builtin_inff();
+                }
+            }
+        }
+        uint64_t pending = ~0ull;
+        for (;;) {
+            ++epoch;
+            float th[2] = {thr[qidx[0]], thr[qidx[1]]};
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int vi = (i * 16 + r) * 2 + j;
+                        if (!((pending >> vi) & 1ull)) continue;
+                        float v = acc[i][j][r];
+                        if (v < th[j]) {
+                            int slot = atomicAdd(&cnt[qidx[j]], 1);
+                            if (slot < C) {
+                                int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                                cbA[qidx[j] * C + slot] = v;
+                                cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
+                                pending &= ~(1ull << vi);
+                            }
+                            flags[0] = epoch;
+                        } else {
+                            pending &= ~(1ull << vi);
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            if (flags[0] != epoch) break;
+            // merge pass: wave w merges queries w, w+4, ...
+            for (int jq = 0; jq < QB / 4; jq++) {
+                const int q = wave + 4 * jq;
+                const int c = cnt[q];
+                if (c == 0) continue;
+                const int nc = c < C ? c : C;
+                merge_query_list<R>(listA + q * KP, listI + q * KP, cbA + q * C, cbI + q * C, KP, C, nc, lane,
+                                    &thr[q]);
+                if (lane == 0) {
+                    if (c > C) flags[1] = epoch;
+                    cnt[q] = 0;
+                }
+            }
+            __syncthreads();
+            if (flags[1] != epoch) break;
+        }
+    }
+
+    __syncthreads();
+    // write this span's lists
+    for (int jq = 0; jq < QB / 4; jq++) {
+        const int q = wave + 4 * jq;
+        if (q0 + q >= a.nq) continue;
+        int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
+        for (int e = lane; e < KP; e += 64) {
+            a.outA[base + e] = listA[q * KP + e];
+            a.outI[base + e] = listI[q * KP + e];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// merge the per-span lists of each query (wave per query), keep KP best (A,id)
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ void k_merge_spans(const float* __restrict__ inA, const uint32_t* __restrict__ inI, int nq, int nspans,
+                              int KP, float* __restrict__ outA, uint32_t* __restrict__ outI) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    float key[R];
+    uint32_t id[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) { key[r] = __builtin_inff(); id[r] = NO_ID; }
+    // running best in e < KP; each round loads up to (64R-KP)/KP spans behind it
+    const int per = (64 * R - KP) / KP;
+    for (int s0 = 0; s0 < nspans; s0 += per) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            int e = r * 64 + lane;
+            if (e >= KP) {
+                int k = e - KP;
+                int s = s0 + k / KP, w = k % KP;
+                if (k / KP < per && s < nspans) {
+                    int64_t off = ((int64_t)q * nspans + s) * KP + w;
+                    key[r] = inA[off];
+                    id[r] = inI[off];
+                } else {
+                    key[r] = __builtin_inff();
+                    id[r] = NO_ID;
+                }
+            }
+        }
+        bitonic_sort<R>(key, id, lane);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        int e = r * 64 + lane;
+        if (e < KP) { outA[(int64_t)q * KP + e] = key[r]; outI[(int64_t)q * KP + e] = id[r]; }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// exact-order rescoring of the candidates (lane per (query, candidate))
+// ---------------------------------------------------------------------------
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(64) void k_rescore(const float* __restrict__ X, int dpad, const float* __restrict__ Q, int d,
+                          const uint32_t* __restrict__ candI, int nq, int KP, float* __restrict__ outE) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (int64_t)nq * KP) return;
+    int q = (int)(p / KP);
+    uint32_t id = candI[p];
+    if (id == NO_ID) { outE[p] = __builtin_inff(); return; }
+    outE[p] = exact_dist<METRIC, VARIANT>(Q + (int64_t)q * dpad, X + (int64_t)id * dpad, d);
+}
+
+// ---------------------------------------------------------------------------
+// finalize: sort candidates by exact distance and prove equality with the
+// reference heap result.  Proof obligations (DESIGN.md "exactness"):
+//  * margin: every non-candidate j has A_j >= A_max and |A - E| <= eps, so if
+//    E_(m) < A_max - eps the m smallest exact distances are all candidates;
+//  * no ties among E_(1..m), m = min(k+1, n): then the heap (which keeps the
+//    k smallest, flat/index.go:665-674) holds exactly these and extractHeap
+//    returns them ascending.  Otherwise flag the query for k_replay.
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ void k_finalize(const float* __restrict__ candA, const uint32_t* __restrict__ candI,
+                           const float* __restrict__ candE, const float* __restrict__ qnorm2, int nq, int KP,
+                           int k, int kout, float eps_scale, float eps_base, int metric,
+                           uint64_t id_base, uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
+                           int32_t* __restrict__ out_n, int32_t* __restrict__ flagged) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    float key[R];
+    uint32_t id[R];
+    float amax = -__builtin_inff();
+    int nvalid = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        int e = r * 64 + lane;
+        if (e < KP) {
+            key[r] = candE[(int64_t)q * KP + e];
+            id[r] = candI[(int64_t)q * KP + e];
+            if (id[r] != NO_ID) { amax = fmaxf(amax, candA[(int64_t)q * KP + e]); nvalid++; }
+            else key[r] = __builtin_inff();
+        } else { key[r] = __builtin_inff(); id[r] = NO_ID; }
+    }
+    // wave max / sum
+    for (int o = 32; o > 0; o >>= 1) {
+        amax = fmaxf(amax, __shfl_xor(amax, o));
+        nvalid += __shfl_xor(nvalid, o);
+    }
+    bitonic_sort<R>(key, id, lane);
+    const int m = (k + 1) < nvalid ? (k + 1) : nvalid;
+    // eps: 2*gamma*(|q|*M + 1) for dot/cosine, 2*gamma*(|q| + M)^2 for l2
+    float qn = sqrtf(qnorm2[q]);
+    float eps;
+    if (metric == L2) { float t = qn + eps_base; eps = eps_scale * t * t; }
+    else eps = eps_scale * (qn * eps_base + 1.f);
+    bool ok = true;
+    if (nvalid >= KP) {
+        // E_(m) is element m-1
+        float em = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float v = __shfl(key[r], (m - 1) & 63);
+            if (((m - 1) >> 6) == r) em = v;
+        }
+        ok = em < amax - eps;
+    }
+    // strict increase over elements 0..m-1
+    bool inc = true;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const float up = __shfl_up(key[r], 1);
+        const float wrap = (r > 0) ? __shfl(key[r > 0 ? r - 1 : 0], 63) : 0.f;
+        const float pv = lane == 0 ? wrap : up;
+        const int e = r * 64 + lane;
+        if (e >= 1 && e < m && !(key[r] > pv)) inc = false;
+    }
+    inc = __all(inc);
+    ok = ok && inc;
+    if (!ok) {
+        if (lane == 0) flagged[q] = 1;
+        return;
+    }
+    if (lane == 0) flagged[q] = 0;
+    const int nout = kout < nvalid ? kout : nvalid;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        int e = r * 64 + lane;
+        if (e < nout) {
+            out_ids[(int64_t)q * kout + e] = id_base + id[r];
+            out_d[(int64_t)q * kout + e] = key[r];
+        }
+    }
+    if (lane == 0) out_n[q] = nout;
+}
+
+// ---------------------------------------------------------------------------
+// exact replay of the reference heap for flagged queries (one wave each)
+// priorityqueue/queue.go:58-198 (NewMax), flat/index.go:578-619,665-688.
+// ---------------------------------------------------------------------------
+struct ReplayHeap {
+    uint64_t* id;
+    float* dist;
+    int len;
+};
+__device__ __forceinline__ void rh_swap(ReplayHeap& h, int i, int j) {
+    uint64_t ti = h.id[i]; h.id[i] = h.id[j]; h.id[j] = ti;
+    float td = h.dist[i]; h.dist[i] = h.dist[j]; h.dist[j] = td;
+}
+__device__ void rh_insert(ReplayHeap& h, uint64_t id, float dist) {
+    h.id[h.len] = id; h.dist[h.len] = dist; h.len++;
+    int i = h.len - 1;
+    while (i != 0 && h.dist[i] > h.dist[(i - 1) / 2]) { rh_swap(h, i, (i - 1) / 2); i = (i - 1) / 2; }
+}
+__device__ void rh_pop(ReplayHeap& h, uint64_t* id, float* dist) {
+    *id = h.id[0]; *dist = h.dist[0];
+    h.id[0] = h.id[h.len - 1]; h.dist[0] = h.dist[h.len - 1];
+    h.len--;
+    int i = 0;
+    for (;;) {
+        int l = 2 * i + 1, r = 2 * i + 2, s = i;
+        if (l < h.len && h.dist[l] > h.dist[i]) s = l;
+        if (r < h.len && h.dist[r] > h.dist[s]) s = r;
+        if (s == i) break;
+        rh_swap(h, i, s);
+        i = s;
+    }
+}
+
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(64) void k_replay(const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
+                                               int64_t nslots, const float* __restrict__ Q, int d,
+                                               const int32_t* __restrict__ qlist, int nlist, int k, uint64_t id_base,
+                                               // optional starting heap state (layout order), per listed query
+                                               const uint64_t* __restrict__ in_hid, const float* __restrict__ in_hd,
+                                               const int32_t* __restrict__ in_hlen,
+                                               // extract=1: results [row][kout] (extractHeap), row = q if
+                                               // out_by_query else li; 0: raw heap state [li][k]
+                                               int extract, int out_by_query, int kout, uint64_t* __restrict__ out_ids,
+                                               float* __restrict__ out_d, int32_t* __restrict__ out_n) {
+    // all LDS in the dynamic region (Guideline 17): [k] ids, [64] tile dists, [k] heap dists, len
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+    uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
+    float* s_d = reinterpret_cast<float*>(hid + k);
+    float* hd = s_d + 64;
+    int* s_len = reinterpret_cast<int*>(hd + k);
+    const int lane = threadIdx.x;
+    const int li = blockIdx.x;
+    if (li >= nlist) return;
+    const int q = qlist[li];
+    const float* qv = Q + (int64_t)q * dpad;
+    if (lane == 0) {
+        int len = 0;
+        if (in_hlen) {
+            len = in_hlen[li];
+            for (int i = 0; i < len; i++) { hid[i] = in_hid[(int64_t)li * k + i]; hd[i] = in_hd[(int64_t)li * k + i]; }
+        }
+        *s_len = len;
+    }
+    __syncthreads();
+    for (int64_t base = 0; base < nslots; base += 64) {
+        const int64_t s = base + lane;
+        const bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
+        float dist = 0.f;
+        if (ok) dist = exact_dist<METRIC, VARIANT>(qv, X + s * dpad, d);
+        const int len = *s_len;
+        const float top = len > 0 ? hd[0] : 0.f;
+        // prefilter with the heap top at tile start; the top only decreases,
+        // so a row failing here fails insertToHeap's test later too.
+        const bool pass = ok && (len < k || top > dist);
+        uint64_t mask = __ballot(pass);
+        if (mask == 0) continue;
+        s_d[lane] = dist;
+        __syncthreads();
+        if (lane == 0) {
+            ReplayHeap h{hid, hd, *s_len};
+            while (mask) {
+                const int j = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const float dj = s_d[j];
+                const uint64_t idj = id_base + (uint64_t)(base + j);
+                // insertToHeap (flat/index.go:665-674)
+                if (h.len < k) rh_insert(h, idj, dj);
+                else if (h.dist[0] > dj) { uint64_t a; float b; rh_pop(h, &a, &b); rh_insert(h, idj, dj); }
+            }
+            *s_len = h.len;
+        }
+        __syncthreads();
+    }
+    if (lane == 0) {
+        ReplayHeap h{hid, hd, *s_len};
+        if (extract) {
+            // extractHeap (flat/index.go:676-688): pop max-first, fill from the back
+            const int n = h.len;
+            const int64_t row = out_by_query ? q : li;
+            for (int i = n - 1; i >= 0; i--) {
+                uint64_t a; float b;
+                rh_pop(h, &a, &b);
+                if (i < kout) { out_ids[row * kout + i] = a; out_d[row * kout + i] = b; }
+            }
+            out_n[row] = n < kout ? n : kout;
+        } else {
+            for (int i = 0; i < h.len; i++) { out_ids[(int64_t)li * k + i] = h.id[i]; out_d[(int64_t)li * k + i] = h.dist[i]; }
+            out_n[li] = h.len;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Provider.SingleDist over pairs, exact reference order (lane per pair)
+// ---------------------------------------------------------------------------
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(64) void k_distance_pairs(const float* __restrict__ A, const float* __restrict__ B, int64_t n, int d, int ld,
+                                 float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = exact_dist<METRIC, VARIANT>(A + i * ld, B + i * ld, d);
+}
+
+// exact normalisation of arbitrary rows into a padded buffer (queries)
+__global__ void k_normalize_rows(const float* __restrict__ in, int64_t n, int d, float* __restrict__ out, int ld) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* src = in + i * d;
+    float* dst = out + i * ld;
+    float nrm = 0.f;
+    for (int c = 0; c < d; c++) { float v = src[c]; float sq = v * v; nrm = nrm + sq; }
+    if (nrm == 0.f) { for (int c = 0; c < ld; c++) dst[c] = 0.f; return; }
+    float dv = (float)sqrt((double)nrm);
+    for (int c = 0; c < d; c++) dst[c] = src[c] / dv;
+    for (int c = d; c < ld; c++) dst[c] = 0.f;
+}
+
+// hamming over uint64 words: popcount(a^b) summed, as float (distancer/hamming.go:63-68)
+__global__ void k_hamming_pairs(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B, int64_t n, int words,
+                                float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t s = 0;
+    for (int w = 0; w < words; w++) s += (uint64_t)__popcll(A[i * words + w] ^ B[i * words + w]);
+    out[i] = (float)s;
+}
+
+// BinaryQuantizer.Encode (compressionhelpers/binary_quantization.go:28-47)
+__global__ void k_bq_encode(const float* __restrict__ in, int64_t n, int d, int ld, uint64_t* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int words = (d + 63) >> 6;
+    if (i >= n * words) return;
+    int64_t row = i / words;
+    int w = (int)(i % words);
+    const float* src = in + row * ld + 64 * w;
+    int lim = d - 64 * w < 64 ? d - 64 * w : 64;
+    uint64_t bits = 0;
+    for (int b = 0; b < lim; b++)
+        if (src[b] < 0.f) bits |= 1ull << b;
+    out[i] = bits;
+}
+
+// copy rows into a zero-padded [n][ld] buffer (queries for l2 / dot)
+__global__ void k_copy_pad_rows(const float* __restrict__ in, int64_t n, int d, float* __restrict__ out, int ld) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * ld) return;
+    int64_t r = i / ld;
+    int c = (int)(i % ld);
+    out[i] = c < d ? in[r * d + c] : 0.f;
+}
+
+// squared norm of each padded row (approximate path + error bound only)
+__global__ void k_row_norm2(const float* __restrict__ rows, int64_t n, int ld, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= n) return;
+    float s = 0.f;
+    for (int c = lane; c < ld; c += 64) { float v = rows[r * ld + c]; s = fmaf(v, v, s); }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) out[r] = s;
+}
+
+// merge G shard lists [g][q][kin] (kin = k+1, ascending exact distances) into
+// the final top-k; flag when a shard flagged q or the merged top k+1 tie.
+template <int R>
+__global__ void k_merge_shards(int G, int64_t nq, int k, const uint64_t* __restrict__ ids, const float* __restrict__ dd,
+                               const int32_t* __restrict__ cnt, const int32_t* __restrict__ flg,
+                               uint64_t* __restrict__ out_ids, float* __restrict__ out_d, int32_t* __restrict__ out_n,
+                               int32_t* __restrict__ out_flags) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int kin = k + 1;
+    float key[R];
+    uint32_t pos[R];  // position g*kin + j
+    int any_flag = 0;
+    for (int g = lane; g < G; g += 64) any_flag |= flg[(int64_t)g * nq + q];
+    any_flag = __any(any_flag);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        int e = r * 64 + lane;
+        int g = e / kin, j = e % kin;
+        if (g < G && j < cnt[(int64_t)g * nq + q]) { key[r] = dd[((int64_t)g * nq + q) * kin + j]; pos[r] = e; }
+        else { key[r] = __builtin_inff(); pos[r] = NO_ID; }
+    }
+    // (dist, id) order; pos order == id order because shards hold ascending id ranges
+    bitonic_sort<R>(key, pos, lane);
+    int nvalid = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) nvalid += pos[r] != NO_ID;
+    for (int o = 32; o > 0; o >>= 1) nvalid += __shfl_xor(nvalid, o);
+    const int m = kin < nvalid ? kin : nvalid;
+    bool inc = true;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const float up = __shfl_up(key[r], 1);
+        const float wrap = (r > 0) ? __shfl(key[r > 0 ? r - 1 : 0], 63) : 0.f;
+        const float pv = lane == 0 ? wrap : up;
+        const int e = r * 64 + lane;
+        if (e >= 1 && e < m && !(key[r] > pv)) inc = false;
+    }
+    inc = __all(inc);
+    const int nout = k < nvalid ? k : nvalid;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int e = r * 64 + lane;
+        if (e < nout) {
+            const int g = pos[r] / kin, j = pos[r] % kin;
+            out_ids[q * k + e] = ids[((int64_t)g * nq + q) * kin + j];
+            out_d[q * k + e] = key[r];
+        }
+    }
+    if (lane == 0) { out_n[q] = nout; out_flags[q] = (any_flag || !inc) ? 1 : 0; }
+}
+
+// synthetic data (same values as oracle or_gen_value)
+__global__ void k_gen(int kind, uint64_t seed, uint64_t row0, int64_t rows, int d, float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * d) return;
+    int64_t r = i / d;
+    int c = (int)(i % d);
+    out[i] = gen_value(kind, seed, row0 + r, c);
+}
+
+}  // namespace wv

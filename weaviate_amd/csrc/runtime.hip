@@ -1,0 +1,860 @@
+// runtime.hip -- host runtime and C ABI (include/wv_knn.h) of the gfx950
+// flat-index engine.  One translation unit: the kernels are included so the
+// template instantiations live next to their launches.
+//
+// Memory layout in HBM (DESIGN.md "data layout"):
+//   X       [cap][dpad] fp32   slot-major store, slot = doc id - id_base, rows
+//                               normalised for cosine (flat/index.go:371),
+//                               dpad = dims rounded up to 32 (zero padded)
+//   xnorm2  [cap]              sum of squares per stored row (approx. L2 path)
+//   present [cap/32] u32       bitmap of slots holding a vector (LSM key exists)
+// cap is a multiple of 128 (the MFMA tile) so tiles never read out of bounds.
+#include <cpuid.h>
+#include <stdarg.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/wv_knn.h"
+#include "kernels.hip"
+
+using namespace wv;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int set_err(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) return set_err(WV_ERR_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" const char* wv_last_error(void) { return g_err.c_str(); }
+
+// ---------------------------------------------------------------------------
+// reference kernel-variant dispatch rule: distancer/l2_amd64.go:19-26
+// (AVX-512 kernels only if cpu.X86.HasAMXBF16 && cpu.X86.HasAVX512)
+// ---------------------------------------------------------------------------
+static bool host_has_amxbf16_avx512() {
+    unsigned a, b, c, d;
+    if (!__get_cpuid_count(7, 0, &a, &b, &c, &d)) return false;
+    bool avx512f = (b >> 16) & 1u;
+    bool amxbf16 = (d >> 22) & 1u;
+    if (!__get_cpuid(1, &a, &b, &c, &d)) return false;
+    bool osxsave = (c >> 27) & 1u;
+    if (!osxsave) return false;
+    unsigned lo, hi;
+    __asm__ volatile("xgetbv" : "=a"(lo), "=d"(hi) : "c"(0));
+    bool os_avx512 = (lo & 0xE6) == 0xE6;
+    return avx512f && os_avx512 && amxbf16;
+}
+
+extern "C" int wv_resolve_variant(int32_t requested) {
+    if (requested == WV_VARIANT_AVX256 || requested == WV_VARIANT_AVX512) return requested;
+    return host_has_amxbf16_avx512() ? WV_VARIANT_AVX512 : WV_VARIANT_AVX256;
+}
+
+// ---------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t b) {
+        if (b <= bytes) return hipSuccess;
+        if (p) { hipFree(p); p = nullptr; bytes = 0; }
+        size_t nb = std::max(b, (size_t)256);
+        hipError_t e = hipMalloc(&p, nb);
+        if (e == hipSuccess) bytes = nb;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+static inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct wv_index {
+    std::mutex mu;
+    int metric = WV_METRIC_COSINE_DOT;
+    int variant = WV_VARIANT_AVX256;
+    int compression = WV_COMPRESSION_NONE;
+    int rescore_limit = -1;
+    int device = 0;
+    uint64_t id_base = 0;
+    std::string root_path;
+
+    int dims = 0, dpad = 0;
+    hipStream_t stream = nullptr;
+
+    int64_t cap = 0;       // slots allocated (multiple of BN)
+    int64_t hiwater = 0;   // 1 + highest slot ever written
+    float* X = nullptr;
+    float* xnorm2 = nullptr;
+    uint32_t* present = nullptr;
+    uint32_t* d_maxn2 = nullptr;
+    std::vector<uint8_t> h_present;
+    uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
+    int64_t npresent = 0;
+
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN;
+
+    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    wv_stats stats{};
+};
+
+// ---------------------------------------------------------------------------
+// create / destroy / capacity
+// ---------------------------------------------------------------------------
+extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
+    if (!cfg || !out) return set_err(WV_ERR_INVALID, "invalid config: nil");
+    if (cfg->metric < 0 || cfg->metric > WV_METRIC_HAMMING)
+        return set_err(WV_ERR_INVALID, "invalid config: unknown distance metric %d", cfg->metric);
+    if (cfg->compression != WV_COMPRESSION_NONE && cfg->compression != WV_COMPRESSION_BQ)
+        return set_err(WV_ERR_UNSUPPORTED, "invalid config: unsupported compression %d", cfg->compression);
+    if (cfg->compression == WV_COMPRESSION_BQ)
+        return set_err(WV_ERR_UNSUPPORTED, "bq compression: not available in this build");
+    HIPCHK(hipSetDevice(cfg->device));
+    wv_index* idx = new wv_index();
+    idx->metric = cfg->metric;
+    idx->variant = wv_resolve_variant(cfg->variant);
+    idx->compression = cfg->compression;
+    idx->rescore_limit = cfg->rescore_limit;
+    idx->device = cfg->device;
+    idx->id_base = cfg->id_base;
+    idx->root_path = cfg->root_path ? cfg->root_path : "";
+    if (cfg->dims > 0) { idx->dims = cfg->dims; idx->dpad = (int)round_up(cfg->dims, BK); }
+    hipError_t e = hipStreamCreateWithFlags(&idx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&idx->d_maxn2, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(idx->d_maxn2, 0, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipEventCreate(&idx->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&idx->ev1);
+    if (e != hipSuccess) {
+        delete idx;
+        return set_err(WV_ERR_HIP, "create: %s", hipGetErrorString(e));
+    }
+    *out = idx;
+    return WV_OK;
+}
+
+extern "C" void wv_index_destroy(wv_index* idx) {
+    if (!idx) return;
+    hipSetDevice(idx->device);
+    if (idx->stream) hipStreamSynchronize(idx->stream);
+    for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
+                    &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
+                    &idx->hI, &idx->hD, &idx->hN})
+        b->release();
+    if (idx->X) hipFree(idx->X);
+    if (idx->xnorm2) hipFree(idx->xnorm2);
+    if (idx->present) hipFree(idx->present);
+    if (idx->d_maxn2) hipFree(idx->d_maxn2);
+    if (idx->ev0) hipEventDestroy(idx->ev0);
+    if (idx->ev1) hipEventDestroy(idx->ev1);
+    if (idx->stream) hipStreamDestroy(idx->stream);
+    delete idx;
+}
+
+// grow the id-indexed store to hold `need` slots (requires dims set)
+static int ensure_capacity(wv_index* idx, int64_t need) {
+    if (need <= idx->cap) return WV_OK;
+    int64_t nc = std::max<int64_t>(need, idx->cap * 2);
+    nc = round_up(std::max<int64_t>(nc, 1024), BN);
+    float* X = nullptr;
+    float* xn = nullptr;
+    uint32_t* pr = nullptr;
+    HIPCHK(hipMalloc(&X, (size_t)nc * idx->dpad * sizeof(float)));
+    HIPCHK(hipMalloc(&xn, (size_t)nc * sizeof(float)));
+    HIPCHK(hipMalloc(&pr, (size_t)(nc / 32) * sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(pr, 0, (size_t)(nc / 32) * sizeof(uint32_t), idx->stream));
+    HIPCHK(hipMemsetAsync(xn, 0, (size_t)nc * sizeof(float), idx->stream));
+    HIPCHK(hipMemsetAsync(X + (size_t)idx->cap * idx->dpad, 0, (size_t)(nc - idx->cap) * idx->dpad * sizeof(float),
+                          idx->stream));
+    if (idx->cap > 0) {
+        HIPCHK(hipMemcpyAsync(X, idx->X, (size_t)idx->cap * idx->dpad * sizeof(float), hipMemcpyDeviceToDevice,
+                              idx->stream));
+        HIPCHK(hipMemcpyAsync(xn, idx->xnorm2, (size_t)idx->cap * sizeof(float), hipMemcpyDeviceToDevice, idx->stream));
+        HIPCHK(hipMemcpyAsync(pr, idx->present, (size_t)(idx->cap / 32) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                              idx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    if (idx->X) hipFree(idx->X);
+    if (idx->xnorm2) hipFree(idx->xnorm2);
+    if (idx->present) hipFree(idx->present);
+    idx->X = X;
+    idx->xnorm2 = xn;
+    idx->present = pr;
+    idx->cap = nc;
+    idx->h_present.resize((size_t)nc, 0);
+    return WV_OK;
+}
+
+extern "C" int wv_index_reserve(wv_index* idx, uint64_t nslots) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->dims == 0) return set_err(WV_ERR_INVALID, "reserve: dimensions not set yet");
+    return ensure_capacity(idx, (int64_t)nslots);
+}
+
+// ---------------------------------------------------------------------------
+// insert path
+// ---------------------------------------------------------------------------
+
+// flat.ValidateBeforeInsert (flat/index.go:823-842)
+static int validate_insert(wv_index* idx, int64_t d) {
+    if (d == 0) return set_err(WV_ERR_INSERT, "cannot insert vector of dimension 0");
+    if (idx->dims == 0) return WV_OK;
+    if (idx->dims != d)
+        return set_err(WV_ERR_INSERT, "insert called with a vector of the wrong size: %lld. Saved length: %d, path: %s",
+                       (long long)d, idx->dims, idx->root_path.c_str());
+    return WV_OK;
+}
+
+extern "C" int wv_index_validate_before_insert(wv_index* idx, int64_t d) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    return validate_insert(idx, d);
+}
+
+static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const uint32_t* d_slots) {
+    dim3 grid((unsigned)((n + 255) / 256));
+    switch (idx->metric) {
+    case WV_METRIC_COSINE_DOT:
+        k_prepare_rows<COSINE><<<grid, 256, 0, idx->stream>>>(d_in, n, idx->dims, d_slots, idx->X, idx->dpad,
+                                                              idx->xnorm2, idx->present, idx->d_maxn2);
+        break;
+    default:
+        k_prepare_rows<L2><<<grid, 256, 0, idx->stream>>>(d_in, n, idx->dims, d_slots, idx->X, idx->dpad, idx->xnorm2,
+                                                          idx->present, idx->d_maxn2);
+        break;
+    }
+}
+
+// rows: host pointer to n x d floats; ids: host doc ids
+static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs, int64_t n, int64_t d) {
+    int rc = validate_insert(idx, d);
+    if (rc) return rc;
+    if (idx->dims == 0) {  // initOnce: initializeDimensionsAndRQ (flat/index.go:338-360)
+        if (d > (1 << 20)) return set_err(WV_ERR_INVALID, "dimensions too large: %lld", (long long)d);
+        idx->dims = (int)d;
+        idx->dpad = (int)round_up(d, BK);
+    }
+    // upsert semantics of the replace bucket: the last write of an id wins.
+    std::unordered_map<uint64_t, int64_t> last;
+    last.reserve((size_t)n * 2);
+    int64_t maxslot = -1;
+    for (int64_t i = 0; i < n; i++) {
+        if (ids[i] < idx->id_base) return set_err(WV_ERR_INVALID, "id %llu below shard id_base %llu",
+                                                  (unsigned long long)ids[i], (unsigned long long)idx->id_base);
+        uint64_t s = ids[i] - idx->id_base;
+        if (s >= (1ull << 32) - BN) return set_err(WV_ERR_INVALID, "id %llu out of range", (unsigned long long)ids[i]);
+        last[ids[i]] = i;
+        maxslot = std::max<int64_t>(maxslot, (int64_t)s);
+    }
+    rc = ensure_capacity(idx, maxslot + 1);
+    if (rc) return rc;
+    std::vector<int64_t> rows;
+    rows.reserve(last.size());
+    for (int64_t i = 0; i < n; i++)
+        if (last[ids[i]] == i) rows.push_back(i);
+    const int64_t chunk = std::max<int64_t>(1, (256ll << 20) / (d * 4));
+    std::vector<float> hbuf;
+    std::vector<uint32_t> hslots;
+    for (size_t c0 = 0; c0 < rows.size(); c0 += (size_t)chunk) {
+        size_t c1 = std::min(rows.size(), c0 + (size_t)chunk);
+        size_t m = c1 - c0;
+        hbuf.resize(m * d);
+        hslots.resize(m);
+        for (size_t j = 0; j < m; j++) {
+            int64_t r = rows[c0 + j];
+            memcpy(&hbuf[j * d], vecs + r * d, d * sizeof(float));
+            hslots[j] = (uint32_t)(ids[r] - idx->id_base);
+        }
+        HIPCHK(idx->stage.ensure(m * d * sizeof(float)));
+        HIPCHK(idx->slots.ensure(m * sizeof(uint32_t)));
+        HIPCHK(hipMemcpyAsync(idx->stage.p, hbuf.data(), m * d * sizeof(float), hipMemcpyHostToDevice, idx->stream));
+        HIPCHK(hipMemcpyAsync(idx->slots.p, hslots.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, idx->stream));
+        launch_prepare(idx, idx->stage.as<float>(), (int64_t)m, idx->slots.as<uint32_t>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(idx->stream));
+        for (size_t j = 0; j < m; j++) {
+            uint32_t s = hslots[j];
+            if (!idx->h_present[s]) { idx->h_present[s] = 1; idx->npresent++; }
+            idx->hiwater = std::max<int64_t>(idx->hiwater, (int64_t)s + 1);
+        }
+    }
+    idx->count += (uint64_t)n;
+    return WV_OK;
+}
+
+extern "C" int wv_index_add(wv_index* idx, uint64_t id, const float* vec, int64_t d) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    return add_rows_locked(idx, &id, vec, 1, d);
+}
+
+extern "C" int wv_index_add_batch(wv_index* idx, const uint64_t* ids, const float* vecs, int64_t n, int64_t d) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (n == 0) return set_err(WV_ERR_INSERT, "insertBatch called with empty lists");  // flat/index.go:297
+    if (n < 0 || !ids || !vecs) return set_err(WV_ERR_INSERT, "ids and vectors sizes does not match");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    return add_rows_locked(idx, ids, vecs, n, d);
+}
+
+extern "C" int wv_index_add_range_device(wv_index* idx, uint64_t first_id, const float* d_vecs, int64_t n,
+                                         int64_t d) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (n == 0) return set_err(WV_ERR_INSERT, "insertBatch called with empty lists");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    int rc = validate_insert(idx, d);
+    if (rc) return rc;
+    if (idx->dims == 0) { idx->dims = (int)d; idx->dpad = (int)round_up(d, BK); }
+    if (first_id < idx->id_base) return set_err(WV_ERR_INVALID, "id below shard id_base");
+    int64_t s0 = (int64_t)(first_id - idx->id_base);
+    rc = ensure_capacity(idx, s0 + n);
+    if (rc) return rc;
+    std::vector<uint32_t> hs((size_t)n);
+    for (int64_t i = 0; i < n; i++) hs[i] = (uint32_t)(s0 + i);
+    HIPCHK(idx->slots.ensure((size_t)n * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(idx->slots.p, hs.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, idx->stream));
+    launch_prepare(idx, d_vecs, n, idx->slots.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    for (int64_t i = 0; i < n; i++) {
+        if (!idx->h_present[s0 + i]) { idx->h_present[s0 + i] = 1; idx->npresent++; }
+    }
+    idx->hiwater = std::max<int64_t>(idx->hiwater, s0 + n);
+    idx->count += (uint64_t)n;
+    return WV_OK;
+}
+
+// flat.Delete (flat/index.go:392-411): drop the key; count is not decremented
+extern "C" int wv_index_delete(wv_index* idx, const uint64_t* ids, int64_t n) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    bool dirty = false;
+    for (int64_t i = 0; i < n; i++) {
+        if (ids[i] < idx->id_base) continue;
+        uint64_t s = ids[i] - idx->id_base;
+        if ((int64_t)s >= idx->cap || !idx->h_present[s]) continue;
+        idx->h_present[s] = 0;
+        idx->npresent--;
+        dirty = true;
+    }
+    if (dirty) {
+        // rebuild the device bitmap from the host mirror
+        std::vector<uint32_t> bits((size_t)(idx->cap / 32), 0);
+        for (int64_t s = 0; s < idx->hiwater; s++)
+            if (idx->h_present[s]) bits[s >> 5] |= 1u << (s & 31);
+        HIPCHK(hipMemcpyAsync(idx->present, bits.data(), bits.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                              idx->stream));
+        HIPCHK(hipStreamSynchronize(idx->stream));
+    }
+    return WV_OK;
+}
+
+extern "C" int wv_index_contains_doc(wv_index* idx, uint64_t id) {
+    if (!idx) return 0;
+    std::lock_guard<std::mutex> g(idx->mu);
+    if (id < idx->id_base) return 0;
+    uint64_t s = id - idx->id_base;
+    return (int64_t)s < idx->cap && idx->h_present[s] ? 1 : 0;
+}
+
+extern "C" uint64_t wv_index_already_indexed(wv_index* idx) {
+    if (!idx) return 0;
+    std::lock_guard<std::mutex> g(idx->mu);
+    return idx->count;
+}
+
+extern "C" int32_t wv_index_dims(wv_index* idx) {
+    if (!idx) return 0;
+    std::lock_guard<std::mutex> g(idx->mu);
+    return idx->dims;
+}
+
+extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value) {
+    if (!idx || !key) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    std::string k(key);
+    if (k == "margin") { if (value < 2 || value > 30) return set_err(WV_ERR_INVALID, "margin out of range"); idx->margin = (int)value; }
+    else if (k == "force_replay") idx->force_replay = (int)value;
+    else if (k == "spans") idx->spans_opt = (int)value;
+    else if (k == "timing") idx->timing = (int)value;
+    else return set_err(WV_ERR_INVALID, "unknown option %s", key);
+    return WV_OK;
+}
+
+extern "C" int wv_index_stats(wv_index* idx, wv_stats* out) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    *out = idx->stats;
+    return WV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// search path
+// ---------------------------------------------------------------------------
+
+// gamma_n = n u / (1 - n u), u = 2^-24 (Higham): |fl(sum) - sum| <= gamma_n sum|terms|
+static double gamma_n(int n) {
+    const double u = 5.9604644775390625e-08;
+    return n * u / (1.0 - n * u);
+}
+
+template <int METRIC, int VARIANT>
+static void launch_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float* Qn, const int32_t* qlist,
+                          int nlist, int k, const uint64_t* in_i, const float* in_d, const int32_t* in_n, int extract,
+                          int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on) {
+    size_t lds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16;
+    k_replay<METRIC, VARIANT><<<nlist, 64, lds, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, qlist,
+                                                     nlist, k, idx->id_base, in_i, in_d, in_n, extract, out_by_query,
+                                                     kout, oi, od, on);
+}
+
+static void replay_dispatch(wv_index* idx, hipStream_t s, const uint32_t* valid, const float* Qn, const int32_t* qlist,
+                            int nlist, int k, const uint64_t* in_i, const float* in_d, const int32_t* in_n,
+                            int extract, int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on) {
+#define WV_RP(M, V) launch_replay<M, V>(idx, s, valid, Qn, qlist, nlist, k, in_i, in_d, in_n, extract, out_by_query, kout, oi, od, on)
+    const bool v5 = idx->variant == WV_VARIANT_AVX512;
+    switch (idx->metric) {
+    case WV_METRIC_L2_SQUARED: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;
+    case WV_METRIC_DOT: if (v5) WV_RP(DOT, AVX512); else WV_RP(DOT, AVX256); break;
+    case WV_METRIC_COSINE_DOT: if (v5) WV_RP(COSINE, AVX512); else WV_RP(COSINE, AVX256); break;
+    default: WV_RP(HAMMING, AVX256); break;
+    }
+#undef WV_RP
+}
+
+// prepare padded (and for cosine exactly normalised) query rows + norms
+static int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t nq_pad) {
+    HIPCHK(idx->qn.ensure((size_t)nq_pad * idx->dpad * sizeof(float)));
+    HIPCHK(idx->qn2.ensure((size_t)nq_pad * sizeof(float)));
+    float* Qn = idx->qn.as<float>();
+    if (nq_pad > nq)
+        HIPCHK(hipMemsetAsync(Qn + nq * idx->dpad, 0, (size_t)(nq_pad - nq) * idx->dpad * sizeof(float), s));
+    if (idx->metric == WV_METRIC_COSINE_DOT)
+        k_normalize_rows<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
+    else
+        k_copy_pad_rows<<<(unsigned)((nq * idx->dpad + 255) / 256), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
+    k_row_norm2<<<(unsigned)((nq_pad + 3) / 4), 256, 0, s>>>(Qn, nq_pad, idx->dpad, idx->qn2.as<float>());
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
+// Core batch search on device queries.  Outputs [nq][kout] device arrays.
+// mode 0: kout = k, flagged queries resolved by replay; mode 1: kout = k+1,
+// flags left for the caller.  n_valid = number of scan candidates.
+static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, int mode,
+                       const uint32_t* valid, int64_t n_valid, uint64_t* o_ids, float* o_d, int32_t* o_n,
+                       int32_t* o_flags) {
+    const int kout = mode == 1 ? k + 1 : k;
+    if (nq <= 0) return WV_OK;
+    if (n_valid == 0 || idx->dims == 0) {
+        HIPCHK(hipMemsetAsync(o_n, 0, (size_t)nq * sizeof(int32_t), s));
+        if (o_flags) HIPCHK(hipMemsetAsync(o_flags, 0, (size_t)nq * sizeof(int32_t), s));
+        return WV_OK;
+    }
+    // SingleDist length check on the first candidate: distancer/l2.go:47-50 etc.
+    if (qd != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)qd, idx->dims);
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    const int64_t nq_pad = round_up(nq, QB);
+    int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
+    if (rc) return rc;
+    const float* Qn = idx->qn.as<float>();
+    const int KP = k + idx->margin;
+    const bool mfma_ok = KP <= 32 && idx->metric != WV_METRIC_HAMMING && !idx->force_replay;
+    idx->stats.queries += (uint64_t)nq;
+    idx->stats.batches++;
+
+    HIPCHK(idx->oF.ensure((size_t)nq * sizeof(int32_t)));
+    int32_t* flags = o_flags ? o_flags : idx->oF.as<int32_t>();
+
+    if (mfma_ok) {
+        const int64_t ntiles = (idx->hiwater + BN - 1) / BN;
+        const int nqb = (int)(nq_pad / QB);
+        int64_t nspans = idx->spans_opt > 0 ? idx->spans_opt : std::max<int64_t>(1, (1024 + nqb - 1) / nqb);
+        nspans = std::min<int64_t>(nspans, ntiles);
+        int64_t tps = (ntiles + nspans - 1) / nspans;
+        nspans = (ntiles + tps - 1) / tps;
+        HIPCHK(idx->spanA.ensure((size_t)nq * nspans * KP * sizeof(float)));
+        HIPCHK(idx->spanI.ensure((size_t)nq * nspans * KP * sizeof(uint32_t)));
+        HIPCHK(idx->candA.ensure((size_t)nq * KP * sizeof(float)));
+        HIPCHK(idx->candI.ensure((size_t)nq * KP * sizeof(uint32_t)));
+        HIPCHK(idx->candE.ensure((size_t)nq * KP * sizeof(float)));
+        SelectArgs a;
+        a.X = idx->X; a.xnorm2 = idx->xnorm2; a.valid = valid; a.ntiles = ntiles;
+        a.Q = Qn; a.qnorm2 = idx->qn2.as<float>(); a.nq = (int)nq; a.dpad = idx->dpad;
+        a.tiles_per_span = (int)tps; a.nspans = (int)nspans; a.nqb = nqb; a.KP = KP;
+        a.outA = idx->spanA.as<float>(); a.outI = idx->spanI.as<uint32_t>();
+        const int C = 64 - KP;
+        size_t lds = (size_t)(2 * QB * LDSROW + QB * KP * 2 + QB * C * 2 + QB * 2 + 4) * sizeof(float);
+        dim3 grid((unsigned)(nqb * nspans));
+        if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
+        switch (idx->metric) {
+        case WV_METRIC_L2_SQUARED:
+            HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select<L2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            k_mfma_select<L2, 1><<<grid, 256, lds, s>>>(a);
+            break;
+        case WV_METRIC_DOT:
+            HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select<DOT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            k_mfma_select<DOT, 1><<<grid, 256, lds, s>>>(a);
+            break;
+        default:
+            HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select<COSINE, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            k_mfma_select<COSINE, 1><<<grid, 256, lds, s>>>(a);
+            break;
+        }
+        HIPCHK(hipGetLastError());
+        if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
+        idx->stats.mfma_launches++;
+        k_merge_spans<1><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(a.outA, a.outI, (int)nq, (int)nspans, KP,
+                                                                   idx->candA.as<float>(), idx->candI.as<uint32_t>());
+        const int64_t npairs = nq * KP;
+        const bool v5 = idx->variant == WV_VARIANT_AVX512;
+#define WV_RS(M, V) k_rescore<M, V><<<(unsigned)((npairs + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, Qn, idx->dims, idx->candI.as<uint32_t>(), (int)nq, KP, idx->candE.as<float>())
+        switch (idx->metric) {
+        case WV_METRIC_L2_SQUARED: if (v5) WV_RS(L2, AVX512); else WV_RS(L2, AVX256); break;
+        case WV_METRIC_DOT: if (v5) WV_RS(DOT, AVX512); else WV_RS(DOT, AVX256); break;
+        default: if (v5) WV_RS(COSINE, AVX512); else WV_RS(COSINE, AVX256); break;
+        }
+#undef WV_RS
+        // error bound of |A - E|: 2 gamma_{d+4} * bound, +5% slack
+        uint32_t mx = 0;
+        HIPCHK(hipMemcpyAsync(&mx, idx->d_maxn2, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        float maxn2;
+        memcpy(&maxn2, &mx, sizeof(float));
+        const float eps_scale = (float)(2.0 * gamma_n(idx->dpad + 4) * 1.05 + 1e-12);
+        const float eps_base = (float)(std::sqrt((double)maxn2) * (1.0 + 1e-6));
+        k_finalize<1><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(
+            idx->candA.as<float>(), idx->candI.as<uint32_t>(), idx->candE.as<float>(), idx->qn2.as<float>(), (int)nq,
+            KP, k, kout, eps_scale, eps_base, idx->metric == WV_METRIC_L2_SQUARED ? L2 : DOT, idx->id_base, o_ids,
+            o_d, o_n, flags);
+        HIPCHK(hipGetLastError());
+    } else {
+        std::vector<int32_t> ones((size_t)nq, 1);
+        HIPCHK(hipMemcpyAsync(flags, ones.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    if (mode == 1) {
+        if (idx->timing) {
+            HIPCHK(hipStreamSynchronize(s));
+            float ms = 0.f;
+            if (mfma_ok) hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
+            idx->stats.last_select_ms = ms;
+        }
+        return WV_OK;
+    }
+    // mode 0: replay the flagged queries
+    std::vector<int32_t> hf((size_t)nq);
+    HIPCHK(hipMemcpyAsync(hf.data(), flags, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (idx->timing && mfma_ok) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
+        idx->stats.last_select_ms = ms;
+    }
+    std::vector<int32_t> ql;
+    for (int64_t q = 0; q < nq; q++)
+        if (hf[q]) ql.push_back((int32_t)q);
+    if (!ql.empty()) {
+        idx->stats.replayed_queries += ql.size();
+        HIPCHK(idx->qlist.ensure(ql.size() * sizeof(int32_t)));
+        HIPCHK(hipMemcpyAsync(idx->qlist.p, ql.data(), ql.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        replay_dispatch(idx, s, valid, Qn, idx->qlist.as<int32_t>(), (int)ql.size(), k, nullptr, nullptr, nullptr, 1, 1,
+                        kout, o_ids, o_d, o_n);
+        HIPCHK(hipGetLastError());
+    }
+    return WV_OK;
+}
+
+// valid-slot bitmap for an allow list (present & allow); returns candidate count
+static int build_valid(wv_index* idx, hipStream_t s, const uint64_t* allow, int64_t n_allow, int32_t allow_mode,
+                       const uint32_t** valid_out, int64_t* n_valid) {
+    if (allow_mode == 0) {
+        *valid_out = idx->present;
+        *n_valid = idx->npresent;
+        return WV_OK;
+    }
+    std::vector<uint32_t> bits((size_t)std::max<int64_t>(idx->cap / 32, 1), 0);
+    int64_t nv = 0;
+    for (int64_t i = 0; i < n_allow; i++) {
+        if (allow[i] < idx->id_base) continue;
+        uint64_t sl = allow[i] - idx->id_base;
+        if ((int64_t)sl >= idx->cap || !idx->h_present[sl]) continue;
+        if (!(bits[sl >> 5] & (1u << (sl & 31)))) { bits[sl >> 5] |= 1u << (sl & 31); nv++; }
+    }
+    HIPCHK(idx->valid.ensure(bits.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(idx->valid.p, bits.data(), bits.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    *valid_out = idx->valid.as<uint32_t>();
+    *n_valid = nv;
+    return WV_OK;
+}
+
+extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
+                                               const uint64_t* allow_ids, int64_t n_allow, int32_t allow_mode,
+                                               uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = idx->stream;
+    if (allow_mode == 1 && n_allow == 0) {  // flat/index.go:590-594
+        for (int64_t q = 0; q < nq; q++) out_counts[q] = 0;
+        return WV_OK;
+    }
+    const uint32_t* valid = nullptr;
+    int64_t n_valid = 0;
+    int rc = build_valid(idx, s, allow_ids, n_allow, allow_mode, &valid, &n_valid);
+    if (rc) return rc;
+    if (n_valid == 0 || idx->dims == 0) {
+        for (int64_t q = 0; q < nq; q++) out_counts[q] = 0;
+        return WV_OK;
+    }
+    const int kk = std::max(k, 1);
+    HIPCHK(idx->qraw.ensure((size_t)nq * d * sizeof(float)));
+    HIPCHK(idx->oIds.ensure((size_t)nq * kk * sizeof(uint64_t)));
+    HIPCHK(idx->oD.ensure((size_t)nq * kk * sizeof(float)));
+    HIPCHK(idx->oN.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
+    rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, valid, n_valid, idx->oIds.as<uint64_t>(),
+                     idx->oD.as<float>(), idx->oN.as<int32_t>(), nullptr);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_counts, idx->oN.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// flat.SearchByVectorDistance (flat/index.go:699-761): recursiveSearch runs once
+// with totalLimit = 100 (common/search_by_dist_params.go DefaultSearchByDist-
+// InitialLimit); the for loop has no post statement, so later iterations only
+// advance the params until MaxLimitReached.
+extern "C" int wv_index_search_by_vector_distance(wv_index* idx, const float* query, int64_t d, float target,
+                                                  int64_t max_limit, const uint64_t* allow_ids, int64_t n_allow,
+                                                  int32_t allow_mode, uint64_t* out_ids, float* out_dists,
+                                                  int32_t* out_count) {
+    (void)max_limit;
+    const int total_limit = 100;
+    std::vector<uint64_t> ids(total_limit);
+    std::vector<float> dd(total_limit);
+    int32_t n = 0;
+    int rc = wv_index_search_by_vector_batch(idx, query, 1, d, total_limit, allow_ids, n_allow, allow_mode, ids.data(),
+                                             dd.data(), &n);
+    if (rc) return rc;
+    int m = 0;
+    for (int i = 0; i < n && i < total_limit; i++) {
+        double diff = std::fabs((double)dd[i] - (double)target);
+        if (dd[i] <= target || diff <= 1e-6) { out_ids[m] = ids[i]; out_dists[m] = dd[i]; m++; }
+        else break;
+    }
+    *out_count = m;
+    return WV_OK;
+}
+
+extern "C" int wv_index_search_device(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                      int32_t mode, uint64_t* d_ids, float* d_dists, int32_t* d_counts,
+                                      int32_t* d_flags, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (mode == 1 && !d_flags) return set_err(WV_ERR_INVALID, "mode 1 needs d_flags");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : idx->stream;
+    int rc = search_core(idx, s, d_queries, nq, d, k, mode, idx->present, idx->npresent, d_ids, d_dists, d_counts,
+                         mode == 1 ? d_flags : nullptr);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_index_replay(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                               const int32_t* h_qlist, int32_t nlist, const uint64_t* h_in_ids,
+                               const float* h_in_dists, const int32_t* h_in_len, int32_t extract,
+                               uint64_t* h_out_ids, float* h_out_dists, int32_t* h_out_len) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0 || nlist < 0) return set_err(WV_ERR_INVALID, "invalid k / list");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = idx->stream;
+    if (nlist == 0) return WV_OK;
+    const bool have_data = idx->dims != 0 && idx->npresent > 0;
+    if (have_data && d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    HIPCHK(idx->hI.ensure((size_t)nlist * k * sizeof(uint64_t) * 2));
+    HIPCHK(idx->hD.ensure((size_t)nlist * k * sizeof(float) * 2));
+    HIPCHK(idx->hN.ensure((size_t)nlist * sizeof(int32_t) * 2));
+    HIPCHK(idx->qlist.ensure((size_t)nlist * sizeof(int32_t)));
+    uint64_t* inI = idx->hI.as<uint64_t>();
+    uint64_t* outI = inI + (size_t)nlist * k;
+    float* inD = idx->hD.as<float>();
+    float* outD = inD + (size_t)nlist * k;
+    int32_t* inN = idx->hN.as<int32_t>();
+    int32_t* outN = inN + nlist;
+    if (h_in_len) {
+        HIPCHK(hipMemcpyAsync(inI, h_in_ids, (size_t)nlist * k * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(inD, h_in_dists, (size_t)nlist * k * sizeof(float), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(inN, h_in_len, (size_t)nlist * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    } else {
+        HIPCHK(hipMemsetAsync(inN, 0, (size_t)nlist * sizeof(int32_t), s));
+    }
+    HIPCHK(hipMemcpyAsync(idx->qlist.p, h_qlist, (size_t)nlist * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const float* Qn = nullptr;
+    if (have_data) {
+        const int64_t nq_pad = round_up(nq, QB);
+        int rc = prepare_queries(idx, s, d_queries, nq, nq_pad);
+        if (rc) return rc;
+        Qn = idx->qn.as<float>();
+    }
+    // list-ordered output rows (out_by_query = 0); an empty shard passes the
+    // heaps through unchanged (zero tiles scanned)
+    replay_dispatch(idx, s, idx->present, Qn, idx->qlist.as<int32_t>(), nlist, k, inI, inD, inN, extract, 0, k, outI,
+                    outD, outN);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h_out_ids, outI, (size_t)nlist * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h_out_dists, outD, (size_t)nlist * k * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h_out_len, outN, (size_t)nlist * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_merge_shards(int32_t device, int32_t nshards, int64_t nq, int32_t k, const uint64_t* d_ids,
+                               const float* d_dists, const int32_t* d_counts, const int32_t* d_flags,
+                               uint64_t* d_out_ids, float* d_out_dists, int32_t* d_out_counts, int32_t* d_out_flags,
+                               void* stream) {
+    HIPCHK(hipSetDevice(device));
+    const int64_t n = (int64_t)nshards * (k + 1);
+    hipStream_t s = (hipStream_t)stream;
+    unsigned grid = (unsigned)((nq + 3) / 4);
+    if (n <= 64) k_merge_shards<1><<<grid, 256, 0, s>>>(nshards, nq, k, d_ids, d_dists, d_counts, d_flags, d_out_ids, d_out_dists, d_out_counts, d_out_flags);
+    else if (n <= 128) k_merge_shards<2><<<grid, 256, 0, s>>>(nshards, nq, k, d_ids, d_dists, d_counts, d_flags, d_out_ids, d_out_dists, d_out_counts, d_out_flags);
+    else if (n <= 256) k_merge_shards<4><<<grid, 256, 0, s>>>(nshards, nq, k, d_ids, d_dists, d_counts, d_flags, d_out_ids, d_out_dists, d_out_counts, d_out_flags);
+    else if (n <= 512) k_merge_shards<8><<<grid, 256, 0, s>>>(nshards, nq, k, d_ids, d_dists, d_counts, d_flags, d_out_ids, d_out_dists, d_out_counts, d_out_flags);
+    else return set_err(WV_ERR_UNSUPPORTED, "merge: nshards*(k+1) > 512");
+    HIPCHK(hipGetLastError());
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// stateless distancer entry points
+// ---------------------------------------------------------------------------
+extern "C" int wv_distance_batch(int32_t device, int32_t metric, int32_t variant, const float* a, const float* b,
+                                 int64_t n, int64_t d, float* out) {
+    HIPCHK(hipSetDevice(device));
+    if (n <= 0) return WV_OK;
+    const int v = wv_resolve_variant(variant);
+    const int ld = (int)round_up(d, 4);  // 16-byte aligned rows for the float4 loads
+    DBuf A, B, O;
+    HIPCHK(A.ensure((size_t)n * ld * sizeof(float)));
+    HIPCHK(B.ensure((size_t)n * ld * sizeof(float)));
+    HIPCHK(O.ensure((size_t)n * sizeof(float)));
+    HIPCHK(hipMemcpy2D(A.p, ld * sizeof(float), a, d * sizeof(float), d * sizeof(float), n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy2D(B.p, ld * sizeof(float), b, d * sizeof(float), d * sizeof(float), n, hipMemcpyHostToDevice));
+    unsigned grid = (unsigned)((n + 255) / 256);
+#define WV_DP(M, V) k_distance_pairs<M, V><<<(unsigned)((n + 63) / 64), 64>>>(A.as<float>(), B.as<float>(), n, (int)d, ld, O.as<float>())
+    const bool v5 = v == WV_VARIANT_AVX512;
+    switch (metric) {
+    case WV_METRIC_L2_SQUARED: if (v5) WV_DP(L2, AVX512); else WV_DP(L2, AVX256); break;
+    case WV_METRIC_DOT: if (v5) WV_DP(DOT, AVX512); else WV_DP(DOT, AVX256); break;
+    case WV_METRIC_COSINE_DOT: if (v5) WV_DP(COSINE, AVX512); else WV_DP(COSINE, AVX256); break;
+    case WV_METRIC_HAMMING: WV_DP(HAMMING, AVX256); break;
+    default: A.release(); B.release(); O.release(); return set_err(WV_ERR_INVALID, "unknown metric %d", metric);
+    }
+#undef WV_DP
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, O.p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost);
+    A.release(); B.release(); O.release();
+    if (e != hipSuccess) return set_err(WV_ERR_HIP, "distance_batch: %s", hipGetErrorString(e));
+    return WV_OK;
+}
+
+extern "C" int wv_hamming_bitwise_batch(int32_t device, const uint64_t* a, const uint64_t* b, int64_t n,
+                                        int64_t words, float* out) {
+    HIPCHK(hipSetDevice(device));
+    if (n <= 0) return WV_OK;
+    DBuf A, B, O;
+    HIPCHK(A.ensure((size_t)n * words * 8));
+    HIPCHK(B.ensure((size_t)n * words * 8));
+    HIPCHK(O.ensure((size_t)n * 4));
+    HIPCHK(hipMemcpy(A.p, a, (size_t)n * words * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(B.p, b, (size_t)n * words * 8, hipMemcpyHostToDevice));
+    k_hamming_pairs<<<(unsigned)((n + 255) / 256), 256>>>(A.as<uint64_t>(), B.as<uint64_t>(), n, (int)words,
+                                                          O.as<float>());
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, O.p, (size_t)n * 4, hipMemcpyDeviceToHost);
+    A.release(); B.release(); O.release();
+    if (e != hipSuccess) return set_err(WV_ERR_HIP, "hamming: %s", hipGetErrorString(e));
+    return WV_OK;
+}
+
+extern "C" int wv_bq_encode_batch(int32_t device, const float* vecs, int64_t n, int64_t d, uint64_t* out_codes) {
+    HIPCHK(hipSetDevice(device));
+    if (n <= 0) return WV_OK;
+    const int64_t words = (d + 63) / 64;
+    DBuf A, O;
+    HIPCHK(A.ensure((size_t)n * d * 4));
+    HIPCHK(O.ensure((size_t)n * words * 8));
+    HIPCHK(hipMemcpy(A.p, vecs, (size_t)n * d * 4, hipMemcpyHostToDevice));
+    k_bq_encode<<<(unsigned)((n * words + 255) / 256), 256>>>(A.as<float>(), n, (int)d, (int)d, O.as<uint64_t>());
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out_codes, O.p, (size_t)n * words * 8, hipMemcpyDeviceToHost);
+    A.release(); O.release();
+    if (e != hipSuccess) return set_err(WV_ERR_HIP, "bq_encode: %s", hipGetErrorString(e));
+    return WV_OK;
+}
+
+extern "C" int wv_normalize_batch(int32_t device, const float* vecs, int64_t n, int64_t d, float* out) {
+    HIPCHK(hipSetDevice(device));
+    if (n <= 0) return WV_OK;
+    DBuf A, O;
+    HIPCHK(A.ensure((size_t)n * d * 4));
+    HIPCHK(O.ensure((size_t)n * d * 4));
+    HIPCHK(hipMemcpy(A.p, vecs, (size_t)n * d * 4, hipMemcpyHostToDevice));
+    k_normalize_rows<<<(unsigned)((n + 255) / 256), 256>>>(A.as<float>(), n, (int)d, O.as<float>(), (int)d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, O.p, (size_t)n * d * 4, hipMemcpyDeviceToHost);
+    A.release(); O.release();
+    if (e != hipSuccess) return set_err(WV_ERR_HIP, "normalize: %s", hipGetErrorString(e));
+    return WV_OK;
+}
+
+extern "C" int wv_gen_device(int32_t device, int32_t kind, uint64_t seed, uint64_t row0, int64_t rows, int64_t d,
+                             float* d_out, void* stream) {
+    HIPCHK(hipSetDevice(device));
+    int64_t n = rows * d;
+    if (n <= 0) return WV_OK;
+    k_gen<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(kind, seed, row0, rows, (int)d, d_out);
+    HIPCHK(hipGetLastError());
+    if (!stream) HIPCHK(hipStreamSynchronize(nullptr));
+    return WV_OK;
+}

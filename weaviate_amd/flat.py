@@ -1,0 +1,246 @@
+"""Host-side mirror of Weaviate's flat vector index (adapters/repos/db/vector/flat).
+
+Same method names, argument meaning and error behaviour as the reference's
+`db.VectorIndex` implementation for the flat index (vector_index.go:25-54,
+flat/index.go), backed by the gfx950 engine through the C ABI.  Vectors and
+queries are numpy float32 arrays; doc ids are uint64.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import WeaviateError, check
+
+# Shard.initVectorIndex distance names (shard_init_vector.go:56-73)
+DISTANCES = {
+    "": _lib.METRIC_COSINE,
+    "cosine": _lib.METRIC_COSINE,
+    "cosine-dot": _lib.METRIC_COSINE,
+    "dot": _lib.METRIC_DOT,
+    "l2-squared": _lib.METRIC_L2,
+    "hamming": _lib.METRIC_HAMMING,
+}
+VARIANTS = {"auto": _lib.VARIANT_AUTO, "avx256": _lib.VARIANT_AVX256, "avx512": _lib.VARIANT_AVX512}
+PROVIDER_TYPE = {_lib.METRIC_L2: "l2-squared", _lib.METRIC_DOT: "dot", _lib.METRIC_COSINE: "cosine-dot",
+                 _lib.METRIC_HAMMING: "hamming"}
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _uptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint64))
+
+
+def _iptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+class AllowList:
+    """helpers.AllowList (helpers/allow_list.go:19-37): a set of doc ids."""
+
+    def __init__(self, ids: Iterable[int] = ()):
+        self.ids = np.unique(np.asarray(list(ids), dtype=np.uint64))
+
+    def is_empty(self) -> bool:
+        return self.ids.size == 0
+
+
+def _allow_args(allow: Optional[AllowList]):
+    if allow is None:
+        return None, 0, 0, None
+    ids = np.ascontiguousarray(allow.ids, dtype=np.uint64)
+    return _uptr(ids), ids.size, 1, ids
+
+
+class FlatIndex:
+    """flat.New (flat/index.go:76-125) with the VectorIndex surface used on the
+    hot path: Add, AddBatch, Delete, SearchByVector, SearchByVectorDistance,
+    ValidateBeforeInsert, ContainsDoc, AlreadyIndexed."""
+
+    def __init__(self, distance: str = "cosine", dims: int = 0, device: int = 0, variant: str = "auto",
+                 root_path: str = "", id_base: int = 0, bq: bool = False, rescore_limit: int = -1):
+        if distance not in DISTANCES:
+            raise WeaviateError(_lib.WV_ERR_INVALID, f"unrecognized or unsupported distance metric {distance!r}")
+        self._l = _lib.load()
+        self._root = root_path.encode()
+        cfg = _lib.WvConfig(DISTANCES[distance], int(dims),
+                            _lib.COMPRESSION_BQ if bq else _lib.COMPRESSION_NONE, int(rescore_limit), int(device),
+                            VARIANTS[variant], int(id_base), self._root)
+        h = C.c_void_p()
+        check(self._l.wv_index_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.metric = DISTANCES[distance]
+        self.device = device
+        self.id_base = id_base
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._l.wv_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def type(self) -> str:  # flat.Type (flat/index.go:1242)
+        return "flat"
+
+    def distancer_type(self) -> str:  # Provider.Type()
+        return PROVIDER_TYPE[self.metric]
+
+    def compressed(self) -> bool:
+        return False
+
+    def reserve(self, nslots: int) -> None:
+        check(self._l.wv_index_reserve(self._h, int(nslots)))
+
+    def set_option(self, key: str, value: int) -> None:
+        check(self._l.wv_index_set_option(self._h, key.encode(), int(value)))
+
+    def stats(self) -> dict:
+        s = _lib.WvStats()
+        check(self._l.wv_index_stats(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
+    # -- insert path ------------------------------------------------------
+    def validate_before_insert(self, vector) -> None:  # flat/index.go:823-842
+        check(self._l.wv_index_validate_before_insert(self._h, len(vector)))
+
+    def add(self, id: int, vector) -> None:  # flat/index.go:362-390
+        v = np.ascontiguousarray(vector, dtype=np.float32)
+        check(self._l.wv_index_add(self._h, int(id), _fptr(v), v.size))
+
+    def add_batch(self, ids: Sequence[int], vectors) -> None:  # flat/index.go:289-308
+        if len(ids) != len(vectors):
+            raise WeaviateError(_lib.WV_ERR_INSERT, "ids and vectors sizes does not match")
+        if len(ids) == 0:
+            raise WeaviateError(_lib.WV_ERR_INSERT, "insertBatch called with empty lists")
+        if isinstance(vectors, np.ndarray) and vectors.ndim == 2:
+            v = np.ascontiguousarray(vectors, dtype=np.float32)
+            i = np.ascontiguousarray(ids, dtype=np.uint64)
+            check(self._l.wv_index_add_batch(self._h, _uptr(i), _fptr(v), v.shape[0], v.shape[1]))
+            return
+        # ragged input: the reference loops Add and stops at the first error
+        for id_, vec in zip(ids, vectors):
+            self.add(id_, vec)
+
+    def delete(self, *ids: int) -> None:  # flat/index.go:392-411
+        a = np.ascontiguousarray(ids, dtype=np.uint64)
+        check(self._l.wv_index_delete(self._h, _uptr(a), a.size))
+
+    def contains_doc(self, id: int) -> bool:  # flat/index.go:1035-1055
+        return bool(self._l.wv_index_contains_doc(self._h, int(id)))
+
+    def already_indexed(self) -> int:  # flat/index.go:1156-1158
+        return int(self._l.wv_index_already_indexed(self._h))
+
+    @property
+    def dims(self) -> int:
+        return int(self._l.wv_index_dims(self._h))
+
+    # -- search path ------------------------------------------------------
+    def search_by_vector_batch(self, queries, k: int, allow: Optional[AllowList] = None):
+        """SearchByVector for each row of `queries` (flat/index.go:423-448).
+        Returns (ids[nq,k] uint64, dists[nq,k] float32, counts[nq] int32)."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq, d = q.shape
+        kk = max(int(k), 1)
+        ids = np.zeros((nq, kk), dtype=np.uint64)
+        dists = np.zeros((nq, kk), dtype=np.float32)
+        counts = np.zeros(nq, dtype=np.int32)
+        ap, na, mode, _keep = _allow_args(allow)
+        check(self._l.wv_index_search_by_vector_batch(self._h, _fptr(q), nq, d, int(k), ap, na, mode, _uptr(ids),
+                                                      _fptr(dists), _iptr(counts)))
+        return ids, dists, counts
+
+    def search_by_vector(self, vector, k: int, allow: Optional[AllowList] = None):
+        """flat.SearchByVector: (ids, dists) ascending, len <= k."""
+        ids, dists, counts = self.search_by_vector_batch(np.asarray(vector, dtype=np.float32)[None, :], k, allow)
+        n = int(counts[0])
+        return ids[0, :n].copy(), dists[0, :n].copy()
+
+    def search_by_vector_distance(self, vector, target_distance: float, max_limit: int,
+                                  allow: Optional[AllowList] = None):
+        """flat.SearchByVectorDistance (flat/index.go:699-761)."""
+        v = np.ascontiguousarray(vector, dtype=np.float32)
+        ids = np.zeros(100, dtype=np.uint64)
+        dists = np.zeros(100, dtype=np.float32)
+        n = np.zeros(1, dtype=np.int32)
+        ap, na, mode, _keep = _allow_args(allow)
+        check(self._l.wv_index_search_by_vector_distance(self._h, _fptr(v), v.size, float(target_distance),
+                                                         int(max_limit), ap, na, mode, _uptr(ids), _fptr(dists),
+                                                         _iptr(n)))
+        return ids[: n[0]].copy(), dists[: n[0]].copy()
+
+
+# ---------------------------------------------------------------------------
+# distancer.Provider mirror (distancer/provider.go:14-24), batched on the GPU
+# ---------------------------------------------------------------------------
+def single_dist_batch(distance: str, a, b, variant: str = "auto", device: int = 0) -> np.ndarray:
+    """Provider.SingleDist(a[i], b[i]) for every row pair, exact reference order."""
+    lib = _lib.load()
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    if a.ndim == 1:
+        a, b = a[None, :], b[None, :]
+    if a.shape != b.shape:
+        raise WeaviateError(_lib.WV_ERR_VECTOR_LENGTH,
+                            f"{a.shape[-1]} vs {b.shape[-1]}: vector lengths don't match")
+    out = np.zeros(a.shape[0], dtype=np.float32)
+    check(lib.wv_distance_batch(device, DISTANCES[distance], VARIANTS[variant], _fptr(a), _fptr(b), a.shape[0],
+                                a.shape[1], _fptr(out)))
+    return out
+
+
+def hamming_bitwise_batch(a, b, device: int = 0) -> np.ndarray:
+    """distancer.HammingBitwise over rows of uint64 words."""
+    lib = _lib.load()
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    if a.ndim == 1:
+        a, b = a[None, :], b[None, :]
+    if a.shape != b.shape:
+        raise WeaviateError(_lib.WV_ERR_VECTOR_LENGTH, "both vectors should have the same len")
+    out = np.zeros(a.shape[0], dtype=np.float32)
+    check(lib.wv_hamming_bitwise_batch(device, _uptr(a), _uptr(b), a.shape[0], a.shape[1], _fptr(out)))
+    return out
+
+
+def bq_encode_batch(vecs, device: int = 0) -> np.ndarray:
+    """BinaryQuantizer.Encode over rows."""
+    lib = _lib.load()
+    v = np.ascontiguousarray(vecs, dtype=np.float32)
+    if v.ndim == 1:
+        v = v[None, :]
+    words = (v.shape[1] + 63) // 64
+    out = np.zeros((v.shape[0], words), dtype=np.uint64)
+    check(lib.wv_bq_encode_batch(device, _fptr(v), v.shape[0], v.shape[1], _uptr(out)))
+    return out
+
+
+def normalize_batch(vecs, device: int = 0) -> np.ndarray:
+    """distancer.Normalize over rows."""
+    lib = _lib.load()
+    v = np.ascontiguousarray(vecs, dtype=np.float32)
+    if v.ndim == 1:
+        v = v[None, :]
+    out = np.zeros_like(v)
+    check(lib.wv_normalize_batch(device, _fptr(v), v.shape[0], v.shape[1], _fptr(out)))
+    return out
