@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""bench.py -- exact k=10 flat-index search throughput on MI355X.
+
+Workload (BASELINE.json configs[2], the config north_star's target is quoted
+on): 10M x 768 fp32 vectors, cosine ("cosine-dot"), k = 10, corpus sharded
+over the N GPUs of one node by contiguous doc-id ranges (N=1: the whole 10M
+corpus on one GPU).  One step = one batch of B queries through the full
+SearchByVector pipeline (query normalisation, fused MFMA distance + top-k
+selection, exact-order rescoring, exactness proof, heap replay of any flagged
+query, and for N>1 the RCCL all-gather + merge).  Inputs are synthetic
+(counter-based generator, identical on CPU and GPU) and resident in HBM before
+timing starts.
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "exact kNN QPS (k=10) at 1/2/4/8 GPUs; % of HBM-BW or MFMA roofline"
+N_TOTAL = 10_000_000
+DIMS = 768
+K = 10
+SEED_CORPUS = 1
+SEED_QUERY = 2
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n_sample: int, nq: int, threads: int):
+    """Reference CPU flat scan on the host cores: the reference's own AVX2 dot
+    kernel (oracle/_ref, compiled from /root/reference) when the host can run
+    it, else the oracle's scalar restatement; one query per thread."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc  # test infrastructure, used only for this baseline leg
+    use_ref = orc.ref_lib() is not None and orc.host_has_avx512()
+    corpus = orc.gen_matrix(0, SEED_CORPUS, 0, n_sample, DIMS)
+    orc.lib().or_normalize_rows(orc.f(corpus), n_sample, DIMS)
+    queries = orc.gen_matrix(0, SEED_QUERY, 0, nq, DIMS)
+    orc.lib().or_normalize_rows(orc.f(queries), nq, DIMS)
+    t0 = time.perf_counter()
+    orc.cpu_baseline(orc.COSINE, orc.AVX256, corpus, queries, K, threads, use_ref)
+    dt = time.perf_counter() - t0
+    qps_sample = nq / dt
+    # the scan is linear in N: extrapolate to the full corpus
+    qps_full = qps_sample * n_sample / N_TOTAL
+    return {
+        "value": qps_full,
+        "unit": "queries/s",
+        "cores": threads,
+        "kind": "reference" if use_ref else "port",
+        "sample": (f"{nq} queries x {n_sample} rows (first rows of the same corpus), cosine k=10, "
+                   f"{'reference dot_256 AVX2 kernel (oracle/_ref)' if use_ref else 'oracle scalar restatement'} "
+                   f"+ NewMax heap scan, {dt:.1f} s, QPS scaled by {n_sample}/{N_TOTAL}"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--n", type=int, default=N_TOTAL)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=1_000_000)
+    ap.add_argument("--cpu-queries", type=int, default=128)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="HBM bytes per k_mfma_select launch from the rocprofv3 PMC pass")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import weaviate_amd as wv
+    from weaviate_amd import _lib
+    lib = _lib.load()
+
+    n_total = args.n
+    n_local = (n_total + world - 1) // world
+    id0 = rank * n_local
+    n_local = max(0, min(n_local, n_total - id0))
+    B = args.batch
+
+    # ---- build the shard: generate + add in 1M-row chunks (device resident) ----
+    t_build = time.perf_counter()
+    index = wv.FlatIndex(distance="cosine", dims=DIMS, device=local_rank, variant="avx256", id_base=id0)
+    index.reserve(n_local)
+    chunk = 1_000_000
+    stage = torch.empty((min(chunk, max(n_local, 1)), DIMS), dtype=torch.float32, device=dev)
+    for r0 in range(0, n_local, chunk):
+        m = min(chunk, n_local - r0)
+        _lib.check(lib.wv_gen_device(local_rank, 0, SEED_CORPUS, id0 + r0, m, DIMS, stage.data_ptr(), None))
+        _lib.check(lib.wv_index_add_range_device(index._h, id0 + r0, stage.data_ptr(), m, DIMS))
+    del stage
+    queries = torch.empty((B, DIMS), dtype=torch.float32, device=dev)
+    _lib.check(lib.wv_gen_device(local_rank, 0, SEED_QUERY, 0, B, DIMS, queries.data_ptr(), None))
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] shard ids [{id0}, {id0 + n_local}) built in {time.perf_counter() - t_build:.1f} s")
+    index.set_option("timing", 1)
+
+    out_ids = torch.empty((B, K), dtype=torch.int64, device=dev)
+    out_d = torch.empty((B, K), dtype=torch.float32, device=dev)
+    out_n = torch.empty(B, dtype=torch.int32, device=dev)
+
+    if world > 1:
+        from weaviate_amd.sharded import GpuShardBackend, ShardedFlatSearch
+        searcher = ShardedFlatSearch(GpuShardBackend(index, local_rank), dev)
+
+        def step():
+            return searcher.search(queries, K)
+    else:
+        def step():
+            s = torch.cuda.current_stream(dev).cuda_stream
+            _lib.check(lib.wv_index_search_device(index._h, queries.data_ptr(), B, DIMS, K, 0, out_ids.data_ptr(),
+                                                  out_d.data_ptr(), out_n.data_ptr(), None, s))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    sel_ms = []
+    replays0 = index.stats()["replayed_queries"]
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        sel_ms.append(index.stats()["last_select_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    replays = index.stats()["replayed_queries"] - replays0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        sm = torch.tensor([float(np.mean(sel_ms))], dtype=torch.float64, device=dev)
+        dist.all_reduce(sm, op=dist.ReduceOp.MAX)
+        sel_avg = float(sm.item())
+    else:
+        sel_avg = float(np.mean(sel_ms))
+
+    total_q = B * args.steps
+    value = total_q / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    # roofline of the dominant kernel (k_mfma_select): algorithmic flops per
+    # launch = 2 * B * n_local * d (one FMA per element pair), over its measured
+    # average duration (HIP events on the stream it runs on).
+    flops = 2.0 * B * n_local * DIMS
+    achieved = flops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(min(args.cpu_rows, n_total), args.cpu_queries, args.cpu_threads)
+            except Exception as e:  # baseline failure must not hide the GPU number
+                log(f"cpu baseline failed: {e}")
+        result = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (counter-based U[-1,1) generator, seed 1 corpus / 2 queries)",
+            "config": {
+                "workload": "10M x 768 fp32 cosine, k=10, exact flat search (BASELINE configs[2])",
+                "corpus_rows": n_total,
+                "dims": DIMS,
+                "k": K,
+                "query_batch": B,
+                "parallelism": f"corpus sharded over {world} GPU(s), contiguous id ranges"
+                               + (", RCCL all-gather merge" if world > 1 else ""),
+                "replayed_queries": int(replays),
+            },
+            "roofline": {
+                "bound": "mfma",
+                "kernel": "k_mfma_select",
+                "achieved": achieved,
+                "peak": MFMA_F32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / MFMA_F32_PEAK_TFLOPS,
+                "launch_ms": sel_avg,
+                "traffic": args.traffic_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    index.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

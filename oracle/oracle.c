@@ -432,3 +432,13 @@ void or_gen_matrix(int kind, uint64_t seed, uint64_t row0, long rows, long d, fl
     for (long r = 0; r < rows; r++)
         for (long c = 0; c < d; c++) out[(size_t)r * d + c] = or_gen_value(kind, seed, row0 + r, c);
 }
+
+/* in-place distancer.Normalize over n rows (test / baseline data prep) */
+void or_normalize_rows(float *v, long n, long d) {
+    float *tmp = (float *)malloc(sizeof(float) * (d > 0 ? d : 1));
+    for (long r = 0; r < n; r++) {
+        or_normalize(v + (size_t)r * d, tmp, d);
+        memcpy(v + (size_t)r * d, tmp, sizeof(float) * d);
+    }
+    free(tmp);
+}

@@ -52,6 +52,7 @@ int or_filter_by_distance(const uint64_t *ids, const float *dists, int n, float 
 uint64_t or_gen_bits(uint64_t seed, uint64_t row, uint64_t col);
 float or_gen_value(int kind, uint64_t seed, uint64_t row, uint64_t col);
 void or_gen_matrix(int kind, uint64_t seed, uint64_t row0, long rows, long d, float *out);
+void or_normalize_rows(float *v, long n, long d);
 
 #ifdef __cplusplus
 }

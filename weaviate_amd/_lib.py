@@ -99,6 +99,13 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # torch (if present) must load its HIP runtime first: our DT_NEEDED
+    # libamdhip64.so.7 then binds to the same copy, so device pointers and
+    # streams are shared with torch (one HIP runtime per process).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(
             f"weaviate_amd: {LIB_PATH} not built; run `python -m weaviate_amd.build` "

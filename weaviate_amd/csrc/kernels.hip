@@ -12,9 +12,10 @@
 //   k_rescore           exact-order distance of the KP candidates (lane per pair)
 //   k_finalize          sort by exact distance, prove the result equals the
 //                       reference heap's (margin + no ties), else flag
-//   k_replay            flagged queries: exact replay of the reference heap
+//   k_exact_rows +      flagged queries: exact-order distances of every row,
+//   k_replay_scan       then an exact replay of the reference heap
 //                       (priorityqueue NewMax + insertToHeap) over the id-ordered
-//                       scan, with exact-order distances.
+//                       scan, skipping 256-row blocks that cannot insert.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -495,18 +496,51 @@ __device__ void rh_pop(ReplayHeap& h, uint64_t* id, float* dist) {
     }
 }
 
+// (1) exact-order distances of every stored row to each listed query, plus
+//     per-256-row block minima (valid rows only).  Block b handles query
+//     f = b % F and rows [256*(b/F), +256): the F blocks of one row range are
+//     dispatched back to back so the rows are re-read from cache.
+constexpr int EBLK = 256;
 template <int METRIC, int VARIANT>
-__global__ __launch_bounds__(64) void k_replay(const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
-                                               int64_t nslots, const float* __restrict__ Q, int d,
-                                               const int32_t* __restrict__ qlist, int nlist, int k, uint64_t id_base,
-                                               // optional starting heap state (layout order), per listed query
-                                               const uint64_t* __restrict__ in_hid, const float* __restrict__ in_hd,
-                                               const int32_t* __restrict__ in_hlen,
-                                               // extract=1: results [row][kout] (extractHeap), row = q if
-                                               // out_by_query else li; 0: raw heap state [li][k]
-                                               int extract, int out_by_query, int kout, uint64_t* __restrict__ out_ids,
-                                               float* __restrict__ out_d, int32_t* __restrict__ out_n) {
-    // all LDS in the dynamic region (Guideline 17): [k] ids, [64] tile dists, [k] heap dists, len
+__global__ __launch_bounds__(256) void k_exact_rows(const float* __restrict__ X, int dpad,
+                                                    const uint32_t* __restrict__ valid, int64_t nslots,
+                                                    const float* __restrict__ Q, int d,
+                                                    const int32_t* __restrict__ qlist, int F, int64_t ld,
+                                                    float* __restrict__ E, float* __restrict__ bmin) {
+    __shared__ float red[4];
+    const int f = blockIdx.x % F;
+    const int64_t blk = blockIdx.x / F;
+    const int64_t s = blk * EBLK + threadIdx.x;
+    const float* qv = Q + (int64_t)qlist[f] * dpad;
+    float e = __builtin_inff();
+    bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
+    if (ok) e = exact_dist<METRIC, VARIANT>(qv, X + s * dpad, d);
+    if (s < ld) E[(int64_t)f * ld + s] = e;
+    float m = ok ? e : __builtin_inff();
+    for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float mm = fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
+        bmin[(int64_t)f * (ld / EBLK) + blk] = mm;
+    }
+}
+
+// (2) exact replay of the reference heap (priorityqueue NewMax +
+//     insertToHeap, flat/index.go:578-688) over the precomputed distances, in
+//     id order, one wave per listed query.  A 256-row block is skipped when the
+//     heap is full and !(top > block_min): no row in it can pass insertToHeap's
+//     `top.Dist > distance` test, and the top never increases.
+__global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E, const float* __restrict__ bmin,
+                                                    const uint32_t* __restrict__ valid, int64_t nslots, int64_t ld,
+                                                    const int32_t* __restrict__ qlist, int nlist, int k,
+                                                    uint64_t id_base,
+                                                    const uint64_t* __restrict__ in_hid,
+                                                    const float* __restrict__ in_hd,
+                                                    const int32_t* __restrict__ in_hlen, int extract,
+                                                    int out_by_query, int kout, uint64_t* __restrict__ out_ids,
+                                                    float* __restrict__ out_d, int32_t* __restrict__ out_n) {
+    // all LDS in the dynamic region (Guideline 17): [k] ids | [64] dists | [k] heap dists | len
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
     float* s_d = reinterpret_cast<float*>(hid + k);
@@ -516,7 +550,8 @@ __global__ __launch_bounds__(64) void k_replay(const float* __restrict__ X, int 
     const int li = blockIdx.x;
     if (li >= nlist) return;
     const int q = qlist[li];
-    const float* qv = Q + (int64_t)q * dpad;
+    const float* Eq = E + (int64_t)li * ld;
+    const float* Bq = bmin + (int64_t)li * (ld / EBLK);
     if (lane == 0) {
         int len = 0;
         if (in_hlen) {
@@ -526,34 +561,45 @@ __global__ __launch_bounds__(64) void k_replay(const float* __restrict__ X, int 
         *s_len = len;
     }
     __syncthreads();
-    for (int64_t base = 0; base < nslots; base += 64) {
-        const int64_t s = base + lane;
-        const bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
-        float dist = 0.f;
-        if (ok) dist = exact_dist<METRIC, VARIANT>(qv, X + s * dpad, d);
-        const int len = *s_len;
-        const float top = len > 0 ? hd[0] : 0.f;
-        // prefilter with the heap top at tile start; the top only decreases,
-        // so a row failing here fails insertToHeap's test later too.
-        const bool pass = ok && (len < k || top > dist);
-        uint64_t mask = __ballot(pass);
-        if (mask == 0) continue;
-        s_d[lane] = dist;
-        __syncthreads();
-        if (lane == 0) {
-            ReplayHeap h{hid, hd, *s_len};
-            while (mask) {
-                const int j = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                const float dj = s_d[j];
-                const uint64_t idj = id_base + (uint64_t)(base + j);
-                // insertToHeap (flat/index.go:665-674)
-                if (h.len < k) rh_insert(h, idj, dj);
-                else if (h.dist[0] > dj) { uint64_t a; float b; rh_pop(h, &a, &b); rh_insert(h, idj, dj); }
+    const int64_t nblk = (nslots + EBLK - 1) / EBLK;
+    for (int64_t b0 = 0; b0 < nblk; b0 += 64) {
+        const float bm = (b0 + lane < nblk) ? Bq[b0 + lane] : __builtin_inff();
+        int len = *s_len;
+        float top = len > 0 ? hd[0] : 0.f;
+        uint64_t bmask = __ballot((b0 + lane < nblk) && (len < k || top > bm));
+        while (bmask) {
+            const int j = __builtin_ctzll(bmask);
+            bmask &= bmask - 1;
+            const float bmj = __shfl(bm, j);
+            len = *s_len;
+            top = len > 0 ? hd[0] : 0.f;
+            if (!(len < k || top > bmj)) continue;
+            const int64_t r0 = (b0 + j) * EBLK;
+            for (int sub = 0; sub < EBLK; sub += 64) {
+                const int64_t s = r0 + sub + lane;
+                const bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
+                const float dist = ok ? Eq[s] : 0.f;
+                len = *s_len;
+                top = len > 0 ? hd[0] : 0.f;
+                uint64_t mask = __ballot(ok && (len < k || top > dist));
+                if (mask == 0) continue;
+                s_d[lane] = dist;
+                __syncthreads();
+                if (lane == 0) {
+                    ReplayHeap h{hid, hd, *s_len};
+                    while (mask) {
+                        const int jj = __builtin_ctzll(mask);
+                        mask &= mask - 1;
+                        const float dj = s_d[jj];
+                        const uint64_t idj = id_base + (uint64_t)(s - lane + jj);
+                        if (h.len < k) rh_insert(h, idj, dj);
+                        else if (h.dist[0] > dj) { uint64_t a; float b; rh_pop(h, &a, &b); rh_insert(h, idj, dj); }
+                    }
+                    *s_len = h.len;
+                }
+                __syncthreads();
             }
-            *s_len = h.len;
         }
-        __syncthreads();
     }
     if (lane == 0) {
         ReplayHeap h{hid, hd, *s_len};

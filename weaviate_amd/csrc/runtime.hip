@@ -120,7 +120,7 @@ struct wv_index {
     uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
     int64_t npresent = 0;
 
-    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN;
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB;
 
     int margin = 8, force_replay = 0, spans_opt = 0, timing = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -167,7 +167,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->stream) hipStreamSynchronize(idx->stream);
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
-                    &idx->hI, &idx->hD, &idx->hN})
+                    &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB})
         b->release();
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
@@ -431,28 +431,45 @@ static double gamma_n(int n) {
     return n * u / (1.0 - n * u);
 }
 
-template <int METRIC, int VARIANT>
-static void launch_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float* Qn, const int32_t* qlist,
-                          int nlist, int k, const uint64_t* in_i, const float* in_d, const int32_t* in_n, int extract,
-                          int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on) {
-    size_t lds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16;
-    k_replay<METRIC, VARIANT><<<nlist, 64, lds, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, qlist,
-                                                     nlist, k, idx->id_base, in_i, in_d, in_n, extract, out_by_query,
-                                                     kout, oi, od, on);
-}
-
-static void replay_dispatch(wv_index* idx, hipStream_t s, const uint32_t* valid, const float* Qn, const int32_t* qlist,
-                            int nlist, int k, const uint64_t* in_i, const float* in_d, const int32_t* in_n,
-                            int extract, int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on) {
-#define WV_RP(M, V) launch_replay<M, V>(idx, s, valid, Qn, qlist, nlist, k, in_i, in_d, in_n, extract, out_by_query, kout, oi, od, on)
+// Exact heap replay for the listed query rows (device qlist): exact-order
+// distances of every row (k_exact_rows) then the id-ordered heap replay
+// (k_replay_scan), in groups bounded by a 2 GiB distance buffer.
+// in_* / raw outputs are [nlist][k] device arrays indexed by list position;
+// extract + out_by_query writes results to row qlist[i] of [nq][kout] arrays.
+static int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float* Qn, const int32_t* d_qlist,
+                      int nlist, int k, const uint64_t* in_i, const float* in_d, const int32_t* in_n, int extract,
+                      int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on) {
+    const int64_t nslots = idx->hiwater;
+    const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
+    int64_t G = std::max<int64_t>(1, std::min<int64_t>(nlist, (2ll << 30) / (ld * 4)));
+    HIPCHK(idx->rE.ensure((size_t)G * ld * sizeof(float)));
+    HIPCHK(idx->rB.ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+    const size_t lds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16;
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
-    switch (idx->metric) {
-    case WV_METRIC_L2_SQUARED: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;
-    case WV_METRIC_DOT: if (v5) WV_RP(DOT, AVX512); else WV_RP(DOT, AVX256); break;
-    case WV_METRIC_COSINE_DOT: if (v5) WV_RP(COSINE, AVX512); else WV_RP(COSINE, AVX256); break;
-    default: WV_RP(HAMMING, AVX256); break;
+    for (int64_t g0 = 0; g0 < nlist; g0 += G) {
+        const int F = (int)std::min<int64_t>(G, nlist - g0);
+        if (nslots > 0 && Qn) {
+            const unsigned grid = (unsigned)(F * (ld / EBLK));
+#define WV_EX(M, V) k_exact_rows<M, V><<<grid, EBLK, 0, s>>>(idx->X, idx->dpad, valid, nslots, Qn, idx->dims, d_qlist + g0, F, ld, idx->rE.as<float>(), idx->rB.as<float>())
+            switch (idx->metric) {
+            case WV_METRIC_L2_SQUARED: if (v5) WV_EX(L2, AVX512); else WV_EX(L2, AVX256); break;
+            case WV_METRIC_DOT: if (v5) WV_EX(DOT, AVX512); else WV_EX(DOT, AVX256); break;
+            case WV_METRIC_COSINE_DOT: if (v5) WV_EX(COSINE, AVX512); else WV_EX(COSINE, AVX256); break;
+            default: WV_EX(HAMMING, AVX256); break;
+            }
+#undef WV_EX
+            HIPCHK(hipGetLastError());
+        }
+        const bool raw = !extract;
+        const int64_t ooff = (raw || !out_by_query) ? g0 : 0;
+        k_replay_scan<<<F, 64, lds, s>>>(idx->rE.as<float>(), idx->rB.as<float>(), valid, Qn ? nslots : 0, ld,
+                                         d_qlist + g0, F, k, idx->id_base, in_n ? in_i + g0 * k : nullptr,
+                                         in_n ? in_d + g0 * k : nullptr, in_n ? in_n + g0 : nullptr, extract,
+                                         out_by_query, kout, oi + ooff * (raw ? k : kout),
+                                         od + ooff * (raw ? k : kout), on + ooff);
+        HIPCHK(hipGetLastError());
     }
-#undef WV_RP
+    return WV_OK;
 }
 
 // prepare padded (and for cosine exactly normalised) query rows + norms
@@ -591,9 +608,9 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         idx->stats.replayed_queries += ql.size();
         HIPCHK(idx->qlist.ensure(ql.size() * sizeof(int32_t)));
         HIPCHK(hipMemcpyAsync(idx->qlist.p, ql.data(), ql.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
-        replay_dispatch(idx, s, valid, Qn, idx->qlist.as<int32_t>(), (int)ql.size(), k, nullptr, nullptr, nullptr, 1, 1,
-                        kout, o_ids, o_d, o_n);
-        HIPCHK(hipGetLastError());
+        int rc2 = run_replay(idx, s, valid, Qn, idx->qlist.as<int32_t>(), (int)ql.size(), k, nullptr, nullptr, nullptr,
+                             1, 1, kout, o_ids, o_d, o_n);
+        if (rc2) return rc2;
     }
     return WV_OK;
 }
@@ -737,9 +754,9 @@ extern "C" int wv_index_replay(wv_index* idx, const float* d_queries, int64_t nq
     }
     // list-ordered output rows (out_by_query = 0); an empty shard passes the
     // heaps through unchanged (zero tiles scanned)
-    replay_dispatch(idx, s, idx->present, Qn, idx->qlist.as<int32_t>(), nlist, k, inI, inD, inN, extract, 0, k, outI,
-                    outD, outN);
-    HIPCHK(hipGetLastError());
+    int rc2 = run_replay(idx, s, idx->present, Qn, idx->qlist.as<int32_t>(), nlist, k, inI, inD, h_in_len ? inN : nullptr,
+                         extract, 0, k, outI, outD, outN);
+    if (rc2) return rc2;
     HIPCHK(hipMemcpyAsync(h_out_ids, outI, (size_t)nlist * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h_out_dists, outD, (size_t)nlist * k * sizeof(float), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h_out_len, outN, (size_t)nlist * sizeof(int32_t), hipMemcpyDeviceToHost, s));

@@ -1,0 +1,135 @@
+"""Corpus sharded across the GPUs of one node (one process per GPU).
+
+Mirrors Weaviate's shard-local top-k + coordinator merge
+(adapters/repos/db/index.go:1928-2071) with contiguous doc-id ranges per rank,
+so the id-ordered scan of the single reference index is the concatenation of
+the rank scans in rank order.  Exactness (DESIGN.md "multi-GPU"):
+
+1. every rank runs the fused kernel pipeline on its range (mode 1) and emits
+   its verified top-(k+1) by exact distance, or a flag;
+2. all ranks all-gather those lists over RCCL (tiny: B*(k+1)*16 bytes/rank)
+   and merge them on-device (wv_merge_shards);
+3. if no rank flagged a query and the merged k+1 smallest distances are
+   distinct, the merged top-k IS the reference heap's result;
+4. otherwise the reference heap is replayed exactly across the ranks in id
+   order: rank r continues the heap state handed over by rank r-1
+   (wv_index_replay), the last rank applies extractHeap.
+
+The collective layer is torch.distributed (backend "nccl" = RCCL on ROCm,
+"gloo" on CPU for tests); the per-rank kernels sit behind a small backend
+interface so the protocol can be exercised on CPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+class GpuShardBackend:
+    """Rank-local engine: a FlatIndex holding ids [id_base, id_base + n)."""
+
+    def __init__(self, index, device: int):
+        self.index = index
+        self.device = device
+        self.dev = torch.device("cuda", device)
+        from . import _lib
+        self._l = _lib.load()
+        self._check = _lib.check
+
+    def local_search(self, q: torch.Tensor, k: int):
+        nq, d = q.shape
+        ids = torch.empty((nq, k + 1), dtype=torch.int64, device=self.dev)
+        dd = torch.empty((nq, k + 1), dtype=torch.float32, device=self.dev)
+        cnt = torch.empty(nq, dtype=torch.int32, device=self.dev)
+        flg = torch.empty(nq, dtype=torch.int32, device=self.dev)
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        self._check(self._l.wv_index_search_device(self.index._h, q.data_ptr(), nq, d, k, 1, ids.data_ptr(),
+                                                   dd.data_ptr(), cnt.data_ptr(), flg.data_ptr(), s))
+        return ids, dd, cnt, flg
+
+    def merge(self, G: int, k: int, ids, dd, cnt, flg):
+        nq = cnt.shape[-1]
+        oi = torch.empty((nq, k), dtype=torch.int64, device=self.dev)
+        od = torch.empty((nq, k), dtype=torch.float32, device=self.dev)
+        on = torch.empty(nq, dtype=torch.int32, device=self.dev)
+        of = torch.empty(nq, dtype=torch.int32, device=self.dev)
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        self._check(self._l.wv_merge_shards(self.device, G, nq, k, ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(),
+                                            flg.data_ptr(), oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+                                            of.data_ptr(), s))
+        return oi, od, on, of
+
+    def replay(self, q: torch.Tensor, qlist: np.ndarray, state, k: int, extract: bool):
+        import ctypes as C
+        nl = len(qlist)
+        ql = np.ascontiguousarray(qlist, dtype=np.int32)
+        oi = np.zeros((nl, k), dtype=np.uint64)
+        od = np.zeros((nl, k), dtype=np.float32)
+        on = np.zeros(nl, dtype=np.int32)
+        pu, pf, pi = C.POINTER(C.c_uint64), C.POINTER(C.c_float), C.POINTER(C.c_int32)
+        if state is None:
+            ii, idd, il = None, None, None
+        else:
+            si = np.ascontiguousarray(state[0], dtype=np.uint64)
+            sd = np.ascontiguousarray(state[1], dtype=np.float32)
+            sn = np.ascontiguousarray(state[2], dtype=np.int32)
+            ii, idd, il = si.ctypes.data_as(pu), sd.ctypes.data_as(pf), sn.ctypes.data_as(pi)
+        torch.cuda.current_stream(self.dev).synchronize()
+        self._check(self._l.wv_index_replay(self.index._h, q.data_ptr(), q.shape[0], q.shape[1], k,
+                                            ql.ctypes.data_as(pi), nl, ii, idd, il, 1 if extract else 0,
+                                            oi.ctypes.data_as(pu), od.ctypes.data_as(pf), on.ctypes.data_as(pi)))
+        return oi, od, on
+
+
+class ShardedFlatSearch:
+    """search(queries) over all ranks of the default process group."""
+
+    def __init__(self, backend, device: torch.device):
+        self.b = backend
+        self.dev = device
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+
+    def search(self, q: torch.Tensor, k: int):
+        ids, dd, cnt, flg = self.b.local_search(q, k)
+        gi = self._all_gather(ids)
+        gd = self._all_gather(dd)
+        gc = self._all_gather(cnt)
+        gf = self._all_gather(flg)
+        oi, od, on, of = self.b.merge(self.world, k, gi, gd, gc, gf)
+        flagged = torch.nonzero(of).flatten().cpu().numpy()
+        if flagged.size:
+            oi, od, on = self._replay_chain(q, k, flagged, oi, od, on)
+        return oi, od, on
+
+    def _replay_chain(self, q, k, qlist, oi, od, on):
+        """Exact heap replay across ranks in id order (rank 0 first)."""
+        nl = len(qlist)
+        state = None
+        for r in range(self.world):
+            extract = r == self.world - 1
+            if self.rank == r:
+                si, sd, sn = self.b.replay(q, qlist, state, k, extract)
+                ti = torch.from_numpy(si.view(np.int64)).to(self.dev)
+                td = torch.from_numpy(sd).to(self.dev)
+                tn = torch.from_numpy(sn).to(self.dev)
+            else:
+                ti = torch.empty((nl, k), dtype=torch.int64, device=self.dev)
+                td = torch.empty((nl, k), dtype=torch.float32, device=self.dev)
+                tn = torch.empty(nl, dtype=torch.int32, device=self.dev)
+            dist.broadcast(ti, src=r)
+            dist.broadcast(td, src=r)
+            dist.broadcast(tn, src=r)
+            state = (ti.cpu().numpy().view(np.uint64), td.cpu().numpy(), tn.cpu().numpy())
+        fi, fd, fn = state
+        idx = torch.from_numpy(qlist.astype(np.int64)).to(oi.device)
+        oi[idx] = torch.from_numpy(fi.view(np.int64)).to(oi.device)
+        od[idx] = torch.from_numpy(fd).to(od.device)
+        on[idx] = torch.from_numpy(fn).to(on.device)
+        return oi, od, on
