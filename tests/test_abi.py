@@ -1,0 +1,49 @@
+"""CPU: the C-ABI library loads and exports every symbol include/wv_knn.h
+declares (no compute calls -- there is no GPU here)."""
+import os
+import re
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "wv_knn.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(wv_[a-z0-9_]+)\s*\(", src)
+    return sorted(set(names))
+
+
+def test_header_declares_entry_points():
+    names = header_functions()
+    for must in ["wv_index_create", "wv_index_add_batch", "wv_index_search_by_vector_batch",
+                 "wv_index_search_by_vector_distance", "wv_distance_batch", "wv_last_error"]:
+        assert must in names
+
+
+def test_library_exports_every_header_symbol(wv):
+    lib = wv.load()
+    missing = [n for n in header_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_ctypes_signatures_cover_header(wv):
+    from weaviate_amd import _lib
+    assert set(header_functions()) == set(_lib.SIGNATURES)
+
+
+def test_no_fallback_when_library_missing(monkeypatch, tmp_path):
+    from weaviate_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    import pytest
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.load()
+
+
+def test_variant_rule_matches_reference_dispatch(wv):
+    """distancer/l2_amd64.go:19-26: AVX-512 kernels only with AMX-BF16 && AVX512."""
+    lib = wv.load()
+    flags = open("/proc/cpuinfo").read().split()
+    expect = 2 if ("amx_bf16" in flags and "avx512f" in flags) else 1
+    assert lib.wv_resolve_variant(0) == expect
+    assert lib.wv_resolve_variant(1) == 1 and lib.wv_resolve_variant(2) == 2

@@ -95,6 +95,7 @@ struct SelectArgs {
     int nspans;
     int nqb;
     int KP;
+    int C;                    // candidate buffer per query (KP + C <= 64*R)
     float* outA;              // [nq_pad][nspans][KP]
     uint32_t* outI;
 };
@@ -122,10 +123,10 @@ __device__ __forceinline__ void merge_query_list(float* listA, uint32_t* listI, 
 }
 
 template <int METRIC, int R>
-__global__ __launch_bounds__(256, 1) void k_mfma_select(SelectArgs a) {
+__global__ __launch_bounds__(256, 2) void k_mfma_select(SelectArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int KP = a.KP;
-    const int C = 64 * R - KP;
+    const int C = a.C;
     float* Xs = smem;                                   // QB*LDSROW
     float* Qs = Xs + BN * LDSROW;                       // QB*LDSROW
     float* listA = Qs + QB * LDSROW;                    // QB*KP

@@ -122,7 +122,7 @@ struct wv_index {
 
     DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB;
 
-    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0;
+    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     wv_stats stats{};
 };
@@ -410,6 +410,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "force_replay") idx->force_replay = (int)value;
     else if (k == "spans") idx->spans_opt = (int)value;
     else if (k == "timing") idx->timing = (int)value;
+    else if (k == "cbuf") idx->cbuf_opt = (int)value;
     else return set_err(WV_ERR_INVALID, "unknown option %s", key);
     return WV_OK;
 }
@@ -534,8 +535,12 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         a.Q = Qn; a.qnorm2 = idx->qn2.as<float>(); a.nq = (int)nq; a.dpad = idx->dpad;
         a.tiles_per_span = (int)tps; a.nspans = (int)nspans; a.nqb = nqb; a.KP = KP;
         a.outA = idx->spanA.as<float>(); a.outI = idx->spanI.as<uint32_t>();
-        const int C = 64 - KP;
-        size_t lds = (size_t)(2 * QB * LDSROW + QB * KP * 2 + QB * C * 2 + QB * 2 + 4) * sizeof(float);
+        // candidate buffer: as large as fits two workgroups per CU (<= 80 KiB each)
+        const int64_t fixed = (int64_t)(2 * QB * LDSROW + QB * KP * 2 + QB * 2 + 4) * (int64_t)sizeof(float);
+        int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(8, (80 * 1024 - fixed) / (QB * 8)));
+        if (idx->cbuf_opt > 0) C = std::min(64 - KP, idx->cbuf_opt);
+        size_t lds = (size_t)(fixed + (int64_t)QB * C * 8);
+        a.C = C;
         dim3 grid((unsigned)(nqb * nspans));
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
         switch (idx->metric) {

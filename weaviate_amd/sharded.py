@@ -92,9 +92,14 @@ class ShardedFlatSearch:
         self.world = dist.get_world_size()
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
-        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous())
-        return out
+        t = t.contiguous()
+        if dist.get_backend() == "nccl":  # RCCL: one fused gather into a [world, ...] tensor
+            out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t)
+            return out
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t)
+        return torch.stack(parts)
 
     def search(self, q: torch.Tensor, k: int):
         ids, dd, cnt, flg = self.b.local_search(q, k)
