@@ -196,3 +196,16 @@ def test_search_by_vector_distance(wv, oracle):
     exp = [(i, x) for i, x in zip(oids, od) if x <= target or abs(float(x) - target) <= 1e-6]
     assert list(ids) == [e[0] for e in exp][: len(ids)]
     assert len(ids) == 31
+
+
+@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("metric,kind,n,d,k", [("cosine", 0, 9000, 768, 10), ("l2-squared", 0, 7000, 96, 24),
+                                               ("dot", 1, 5000, 64, 5)])
+def test_select_kernel_variants(wv, oracle, kernel, metric, kind, n, d, k):
+    data = gen(oracle, kind, 81, n, d)
+    queries = gen(oracle, kind, 82, 300, d)   # > 2 query blocks, ragged last block
+    idx, orc = build_pair(wv, oracle, metric, "avx256", data)
+    idx.set_option("kernel", kernel)
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    for qi in range(0, len(queries), 7):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")

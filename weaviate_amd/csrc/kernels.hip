@@ -73,10 +73,9 @@ __global__ void k_prepare_rows(const float* __restrict__ in, int64_t n, int d, c
 // accumulator layout puts the query on the lane (col = lane&31) and 16 corpus
 // rows in registers (row = (r&3) + 8(r>>2) + 4(lane>>5)).
 //
-// LDS staging (per BK=32 slice): rows stored de-interleaved [even k | odd k]
-// with a 36-float stride, so a lane's 16 k-values for the 16 MFMA k-steps are
-// one contiguous 64 B run (4 x ds_read_b128) and the 16-lane ds_read_b128
-// groups hit 16 distinct 4-bank slots (conflict-free).
+// LDS staging (per BK=32 slice): rows at a 36-float stride; a lane's 16
+// k-values for the 16 MFMA k-steps are one contiguous 64 B run
+// (4 x ds_read_b128), bank-conflict-free for reads and writes (see stage()).
 constexpr int QB = 128;   // queries per workgroup tile
 constexpr int BN = 128;   // corpus rows per tile
 constexpr int BK = 32;    // k per staging step
@@ -96,6 +95,7 @@ struct SelectArgs {
     int nqb;
     int KP;
     int C;                    // candidate buffer per query (KP + C <= 64*R)
+    int qgroup;               // query blocks per XCD cell (divides nqb)
     float* outA;              // [nq_pad][nspans][KP]
     uint32_t* outI;
 };
@@ -143,13 +143,19 @@ __global__ __launch_bounds__(256, 2) void k_mfma_select(SelectArgs a) {
     const int wq = wave & 1, wx = wave >> 1;
     const int li = lane & 31, lh = lane >> 5;
 
-    // block -> (query block, span) with an XCD-aware swizzle: blocks of one span
-    // land on one XCD so its corpus tiles are shared through that XCD's L2.
+    // block -> (query block, span), XCD-aware (T1): blocks b and b+8 share an
+    // XCD, so logical = (b%8)*(total/8) + b/8 gives each XCD a contiguous run
+    // of "cells"; a cell is QG query blocks x one span.  Concurrent workgroups
+    // of an XCD then share QG query blocks (L2-resident, 4 x 393 KB at d=768)
+    // and each corpus tile is read by QG workgroups through one L2.
     const int total = a.nqb * a.nspans;
-    int b = blockIdx.x;
-    int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
-    const int qb = logical % a.nqb;
-    const int span = logical / a.nqb;
+    const int b = blockIdx.x;
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int QG = a.qgroup;
+    const int cell = logical / QG, qi = logical % QG;
+    const int group = cell / a.nspans;
+    const int span = cell % a.nspans;
+    const int qb = group * QG + qi;
     const int q0 = qb * QB;
 
     for (int i = tid; i < QB * KP; i += 256) { listA[i] = __builtin_inff(); listI[i] = NO_ID; }
@@ -173,17 +179,15 @@ __global__ __launch_bounds__(256, 2) void k_mfma_select(SelectArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; c++) { px[c] = ld4(xp + 4 * c); pq[c] = ld4(qp + 4 * c); }
     };
+    // a row's 32 k-values stay in order at a 36-float stride; MFMA step s
+    // takes k = s on lane half 0 and k = 16+s on lane half 1 (the k order of a
+    // sum is free), so each lane reads 16 contiguous floats.  Bank check: the
+    // 8-lane ds_write_b128 groups hit quads (r + 4h + j) mod 8, the 16-lane
+    // ds_read_b128 groups quads (9i + 4h + j) mod 16: both conflict-free.
     auto stage = [&](float* dst, const float4 (&p)[4]) {
-        // even elements -> [8*half, 8*half+8), odd -> 16 + [8*half, 8*half+8)
-        float4 e0 = make_float4(p[0].x, p[0].z, p[1].x, p[1].z);
-        float4 e1 = make_float4(p[2].x, p[2].z, p[3].x, p[3].z);
-        float4 o0 = make_float4(p[0].y, p[0].w, p[1].y, p[1].w);
-        float4 o1 = make_float4(p[2].y, p[2].w, p[3].y, p[3].w);
-        float* base = dst + srow * LDSROW + 8 * shalf;
-        *reinterpret_cast<float4*>(base) = e0;
-        *reinterpret_cast<float4*>(base + 4) = e1;
-        *reinterpret_cast<float4*>(base + 16) = o0;
-        *reinterpret_cast<float4*>(base + 20) = o1;
+        float* base = dst + srow * LDSROW + 16 * shalf;
+#pragma unroll
+        for (int c = 0; c < 4; c++) *reinterpret_cast<float4*>(base + 4 * c) = p[c];
     };
 
     f32x16 acc[2][2];
@@ -321,6 +325,452 @@ __global__ __launch_bounds__(256, 2) void k_mfma_select(SelectArgs a) {
         for (int e = lane; e < KP; e += 64) {
             a.outA[base + e] = listA[q * KP + e];
             a.outI[base + e] = listI[q * KP + e];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_mfma_select2: same math as k_mfma_select, pipelined:
+//  * LDS staging double-buffered -> one barrier per BK slice; the next slice's
+//    global loads are in flight during the MFMAs and written to the other
+//    buffer afterwards;
+//  * 32-float rows with an XOR chunk swizzle f(r) = (r&3) ^ ((r>>2)&7): the
+//    8-lane ds_write_b128 groups and 16-lane ds_read_b128 groups are
+//    conflict-free (offline check in DESIGN.md);
+//  * the per-(query, span) candidate lists live in the output buffer in global
+//    memory (each entry always touched by the same thread), leaving LDS for the
+//    staging buffers, thresholds and a small candidate buffer: <= 80 KiB, two
+//    workgroups per CU.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int swz(int r) { return ((r & 3) ^ ((r >> 2) & 7)); }
+
+template <int METRIC, int R>
+__global__ __launch_bounds__(256, 2) void k_mfma_select2(SelectArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int STG = (BN + QB) * BK;                      // floats per staging buffer
+    const int KP = a.KP;
+    const int C = a.C;
+    float* stg = smem;                                       // [2][STG]
+    float* thr = stg + 2 * STG;                              // QB
+    int* cnt = reinterpret_cast<int*>(thr + QB);             // QB
+    int* flags = cnt + QB;                                   // 4
+    float* cbA = reinterpret_cast<float*>(flags + 4);        // QB*C
+    uint32_t* cbI = reinterpret_cast<uint32_t*>(cbA + QB * C);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wq = wave & 1, wx = wave >> 1;
+    const int li = lane & 31, lh = lane >> 5;
+
+    const int total = a.nqb * a.nspans;
+    const int b = blockIdx.x;
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int QG = a.qgroup;
+    const int cell = logical / QG, qi = logical % QG;
+    const int group = cell / a.nspans;
+    const int span = cell % a.nspans;
+    const int qb = group * QG + qi;
+    const int q0 = qb * QB;
+
+    // lists: wave w owns queries w + 4j, lane e owns entry e (same thread for
+    // init, merges and the final state)
+    for (int jq = 0; jq < QB / 4; jq++) {
+        const int q = wave + 4 * jq;
+        if (q0 + q >= a.nq) continue;
+        const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
+        for (int e = lane; e < KP; e += 64) { a.outA[base + e] = __builtin_inff(); a.outI[base + e] = NO_ID; }
+    }
+    if (tid < QB) { thr[tid] = __builtin_inff(); cnt[tid] = 0; }
+    if (tid == 0) { flags[0] = 0; flags[1] = 0; }
+
+    const int64_t t0 = (int64_t)span * a.tiles_per_span;
+    int64_t t1 = t0 + a.tiles_per_span;
+    if (t1 > a.ntiles) t1 = a.ntiles;
+    const int nk = a.dpad / BK;
+    const int64_t total_steps = t1 > t0 ? (t1 - t0) * nk : 0;
+
+    const int srow = tid >> 1, shalf = tid & 1;
+    const int wsw = swz(srow & 31);
+    const int rsw = swz(li);
+    float4 px[4], pq[4];
+    auto prefetch = [&](int64_t step) {
+        int64_t tile = t0 + step / nk;
+        int kb = (int)(step % nk);
+        const float* xp = a.X + (tile * BN + srow) * (int64_t)a.dpad + kb * BK + 16 * shalf;
+        const float* qp = a.Q + (int64_t)(q0 + srow) * a.dpad + kb * BK + 16 * shalf;
+#pragma unroll
+        for (int c = 0; c < 4; c++) { px[c] = ld4(xp + 4 * c); pq[c] = ld4(qp + 4 * c); }
+    };
+    auto stage = [&](float* buf) {
+        float* xr = buf + srow * BK;
+        float* qr = buf + BN * BK + srow * BK;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const int pc = (4 * shalf + c) ^ wsw;
+            *reinterpret_cast<float4*>(xr + 4 * pc) = px[c];
+            *reinterpret_cast<float4*>(qr + 4 * pc) = pq[c];
+        }
+    };
+
+    f32x16 acc[2][2];
+    int epoch = 0;
+    if (total_steps > 0) { prefetch(0); stage(stg); }
+    __syncthreads();
+
+    for (int64_t step = 0; step < total_steps; step++) {
+        const int64_t tile = t0 + step / nk;
+        const int kb = (int)(step % nk);
+        const float* cur = stg + (step & 1) * STG;
+        if (kb == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+        }
+        const bool more = step + 1 < total_steps;
+        if (more) prefetch(step + 1);
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            float fa[2][8], fb[2][8];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const float* xr = cur + (64 * wx + 32 * i + li) * BK;
+                const float* qr = cur + BN * BK + (64 * wq + 32 * i + li) * BK;
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    const int pc = (4 * lh + 2 * half + c) ^ rsw;
+                    float4 x = *reinterpret_cast<const float4*>(xr + 4 * pc);
+                    float4 y = *reinterpret_cast<const float4*>(qr + 4 * pc);
+                    fa[i][4 * c + 0] = x.x; fa[i][4 * c + 1] = x.y; fa[i][4 * c + 2] = x.z; fa[i][4 * c + 3] = x.w;
+                    fb[i][4 * c + 0] = y.x; fb[i][4 * c + 1] = y.y; fb[i][4 * c + 2] = y.z; fb[i][4 * c + 3] = y.w;
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < 8; s++)
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+        }
+        if (more) stage(stg + ((step + 1) & 1) * STG);
+
+        if (kb == nk - 1) {
+            // ---------------- epilogue: selection over this tile ----------------
+            const int64_t row0 = tile * BN;
+            float qn[2];
+            int qidx[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                qidx[j] = 64 * wq + 32 * j + li;
+                qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
+            }
+            const uint32_t* vb = a.valid + (row0 >> 5);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    bool ok = (vb[rt >> 5] >> (rt & 31)) & 1u;
+                    float xn = (METRIC == L2) ? a.xnorm2[row0 + rt] : 0.f;
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        float dot = acc[i][j][r];
+                        float v;
+                        if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
+                        else if (METRIC == DOT) v = -dot;
+                        else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
+                        bool qok = (q0 + qidx[j]) < a.nq;
+                        acc[i][j][r] = (ok && qok) ? v : __builtin_inff();
+                    }
+                }
+            }
+            uint64_t pending = ~0ull;
+            for (;;) {
+                ++epoch;
+                float th[2] = {thr[qidx[0]], thr[qidx[1]]};
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+#pragma unroll
+                        for (int j = 0; j < 2; j++) {
+                            const int vi = (i * 16 + r) * 2 + j;
+                            if (!((pending >> vi) & 1ull)) continue;
+                            float v = acc[i][j][r];
+                            if (v < th[j]) {
+                                int slot = atomicAdd(&cnt[qidx[j]], 1);
+                                if (slot < C) {
+                                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                                    cbA[qidx[j] * C + slot] = v;
+                                    cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
+                                    pending &= ~(1ull << vi);
+                                }
+                                flags[0] = epoch;
+                            } else {
+                                pending &= ~(1ull << vi);
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                if (flags[0] != epoch) break;
+                for (int jq = 0; jq < QB / 4; jq++) {
+                    const int q = wave + 4 * jq;
+                    const int c = cnt[q];
+                    if (c == 0) continue;
+                    const int nc = c < C ? c : C;
+                    const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
+                    merge_query_list<R>(a.outA + base, a.outI + base, cbA + q * C, cbI + q * C, KP, C, nc, lane,
+                                        &thr[q]);
+                    if (lane == 0) {
+                        if (c > C) flags[1] = epoch;
+                        cnt[q] = 0;
+                    }
+                }
+                __syncthreads();
+                if (flags[1] != epoch) break;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_mfma_select3: 8 waves, 128-query x 256-row tiles, direct global->LDS DMA
+// (global_load_lds_dwordx4) into a 3-deep LDS ring: slice s+2 is in flight
+// while slice s is multiplied; one raw s_barrier per BK slice behind a counted
+// vmcnt (Guide §5 "Pipelining across barriers").  The DMA writes LDS
+// lane-linearly, so the XOR chunk swizzle f(r) is applied to the per-lane
+// SOURCE address and again on the read (rule 21).  Lists live in the output
+// buffer (global), thresholds / counters / candidate buffer in LDS;
+// ~156 KiB LDS, one workgroup (2 waves per SIMD) per CU.
+// ---------------------------------------------------------------------------
+constexpr int BN3 = 256;
+constexpr int NBUF3 = 3;
+constexpr int STG3 = (BN3 + QB) * BK;  // floats per ring slot
+constexpr int GLDS_PER_WAVE = (BN3 + QB) * BK * 4 / 1024 / 8;  // 1 KiB pieces per wave per slice (= 6)
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) const float lds_cfloat;
+
+// ds_read_b128 from an LDS pointer, invisible to hipcc's waitcnt insertion:
+// the caller waits with an explicit lgkmcnt + sched_barrier (rule 18).
+__device__ __forceinline__ float4 lds_ld4(const float* p) {
+    float4 v;
+    const unsigned off = (unsigned)(size_t)((lds_cfloat*)p);
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(off));
+    return v;
+}
+__device__ __forceinline__ float f4get(const float4& v, int t) { return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w; }
+
+template <int METRIC, int R>
+__global__ __launch_bounds__(512, 2) void k_mfma_select3(SelectArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int KP = a.KP;
+    const int C = a.C;
+    float* ring = smem;                                      // [NBUF3][STG3]
+    float* thr = ring + NBUF3 * STG3;                        // QB
+    int* cnt = reinterpret_cast<int*>(thr + QB);             // QB
+    int* flags = cnt + QB;                                   // 4
+    float* cbA = reinterpret_cast<float*>(flags + 4);        // QB*C
+    uint32_t* cbI = reinterpret_cast<uint32_t*>(cbA + QB * C);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;          // 0..7
+    const int wq = wave & 1, wx = wave >> 1;   // 2 query halves x 4 row quarters
+    const int li = lane & 31, lh = lane >> 5;
+
+    const int total = a.nqb * a.nspans;
+    const int b = blockIdx.x;
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int QG = a.qgroup;
+    const int cell = logical / QG, qi = logical % QG;
+    const int group = cell / a.nspans;
+    const int span = cell % a.nspans;
+    const int qb = group * QG + qi;
+    const int q0 = qb * QB;
+
+    for (int jq = 0; jq < QB / 8; jq++) {
+        const int q = wave + 8 * jq;
+        if (q0 + q >= a.nq) continue;
+        const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
+        for (int e = lane; e < KP; e += 64) { a.outA[base + e] = __builtin_inff(); a.outI[base + e] = NO_ID; }
+    }
+    if (tid < QB) { thr[tid] = __builtin_inff(); cnt[tid] = 0; }
+    if (tid == 0) { flags[0] = 0; flags[1] = 0; }
+
+    const int64_t t0 = (int64_t)span * a.tiles_per_span;
+    int64_t t1 = t0 + a.tiles_per_span;
+    if (t1 > a.ntiles) t1 = a.ntiles;
+    const int nk = a.dpad / BK;
+    const int64_t total_steps = t1 > t0 ? (t1 - t0) * nk : 0;
+
+    // DMA piece p (0..5) of this wave covers 8 rows: pieces 0-3 -> X rows
+    // 32*wave + 8p, pieces 4-5 -> Q rows 16*wave + 8(p-4).  Lane L writes LDS
+    // row (L>>3), physical chunk (L&7), i.e. logical chunk (L&7) ^ f(row).
+    const int prow = lane >> 3, pchunk = lane & 7;
+    auto issue = [&](int64_t step) {
+        const int64_t tile = t0 + step / nk;
+        const int kb = (int)(step % nk);
+        float* slot = ring + (int)(step % NBUF3) * STG3;
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int row = 32 * wave + 8 * p + prow;
+            const int c = pchunk ^ swz(row & 31);
+            const float* src = a.X + (tile * BN3 + row) * (int64_t)a.dpad + kb * BK + 4 * c;
+            __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(slot + (32 * wave + 8 * p) * BK), 16, 0, 0);
+        }
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+            const int row = 16 * wave + 8 * p + prow;
+            const int c = pchunk ^ swz(row & 31);
+            const float* src = a.Q + (int64_t)(q0 + row) * a.dpad + kb * BK + 4 * c;
+            __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(slot + BN3 * BK + (16 * wave + 8 * p) * BK), 16, 0, 0);
+        }
+    };
+
+    const int rsw = swz(li);
+    f32x16 acc[2][2];
+    int epoch = 0;
+    if (total_steps > 0) issue(0);
+    if (total_steps > 1) issue(1);
+
+    for (int64_t step = 0; step < total_steps; step++) {
+        const int64_t tile = t0 + step / nk;
+        const int kb = (int)(step % nk);
+        // this wave's pieces of `step` have landed (those of step+1 may fly)
+        if (step + 1 < total_steps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // everyone's pieces landed; slot (step+2)%3 is free
+        __builtin_amdgcn_sched_barrier(0);
+        if (step + 2 < total_steps) issue(step + 2);
+        const float* cur = ring + (int)(step % NBUF3) * STG3;
+        if (kb == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+        }
+        // fragment reads in inline asm: hipcc would otherwise put vmcnt(0) in
+        // front of them (the DMA writes LDS) and drain the ring.  All 16
+        // reads issue up front; half 0's MFMAs wait for the first 8.
+        float4 X4[2][4], Y4[2][4];
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++)
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const float* xr = cur + (64 * wx + 32 * i + li) * BK;
+                const float* qr = cur + BN3 * BK + (64 * wq + 32 * i + li) * BK;
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    const int cc = 2 * hh + c;
+                    const int pc = (4 * lh + cc) ^ rsw;
+                    X4[i][cc] = lds_ld4(xr + 4 * pc);
+                    Y4[i][cc] = lds_ld4(qr + 4 * pc);
+                }
+            }
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+            if (hh == 0) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const int cc = 2 * hh + c;
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+#pragma unroll
+                    for (int i = 0; i < 2; i++)
+#pragma unroll
+                        for (int j = 0; j < 2; j++)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(X4[i][cc], t), f4get(Y4[j][cc], t),
+                                                                             acc[i][j], 0, 0, 0);
+            }
+        }
+
+        if (kb == nk - 1) {
+            // ---------------- epilogue: selection over this 128 x 256 tile ----------------
+            const int64_t row0 = tile * BN3;
+            float qn[2];
+            int qidx[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                qidx[j] = 64 * wq + 32 * j + li;
+                qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
+            }
+            const uint32_t* vb = a.valid + (row0 >> 5);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    bool ok = (vb[rt >> 5] >> (rt & 31)) & 1u;
+                    float xn = (METRIC == L2) ? a.xnorm2[row0 + rt] : 0.f;
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        float dot = acc[i][j][r];
+                        float v;
+                        if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
+                        else if (METRIC == DOT) v = -dot;
+                        else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
+                        bool qok = (q0 + qidx[j]) < a.nq;
+                        acc[i][j][r] = (ok && qok) ? v : __builtin_inff();
+                    }
+                }
+            }
+            uint64_t pending = ~0ull;
+            for (;;) {
+                ++epoch;
+                float th[2] = {thr[qidx[0]], thr[qidx[1]]};
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+#pragma unroll
+                        for (int j = 0; j < 2; j++) {
+                            const int vi = (i * 16 + r) * 2 + j;
+                            if (!((pending >> vi) & 1ull)) continue;
+                            float v = acc[i][j][r];
+                            if (v < th[j]) {
+                                int slot = atomicAdd(&cnt[qidx[j]], 1);
+                                if (slot < C) {
+                                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                                    cbA[qidx[j] * C + slot] = v;
+                                    cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
+                                    pending &= ~(1ull << vi);
+                                }
+                                flags[0] = epoch;
+                            } else {
+                                pending &= ~(1ull << vi);
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                if (flags[0] != epoch) break;
+                for (int jq = 0; jq < QB / 8; jq++) {
+                    const int q = wave + 8 * jq;
+                    const int c = cnt[q];
+                    if (c == 0) continue;
+                    const int nc = c < C ? c : C;
+                    const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
+                    merge_query_list<R>(a.outA + base, a.outI + base, cbA + q * C, cbI + q * C, KP, C, nc, lane,
+                                        &thr[q]);
+                    if (lane == 0) {
+                        if (c > C) flags[1] = epoch;
+                        cnt[q] = 0;
+                    }
+                }
+                __syncthreads();
+                if (flags[1] != epoch) break;
+            }
         }
     }
 }

@@ -122,7 +122,7 @@ struct wv_index {
 
     DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB;
 
-    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0;
+    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     wv_stats stats{};
 };
@@ -183,7 +183,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
 static int ensure_capacity(wv_index* idx, int64_t need) {
     if (need <= idx->cap) return WV_OK;
     int64_t nc = std::max<int64_t>(need, idx->cap * 2);
-    nc = round_up(std::max<int64_t>(nc, 1024), BN);
+    nc = round_up(std::max<int64_t>(nc, 1024), BN3);
     float* X = nullptr;
     float* xn = nullptr;
     uint32_t* pr = nullptr;
@@ -411,6 +411,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "spans") idx->spans_opt = (int)value;
     else if (k == "timing") idx->timing = (int)value;
     else if (k == "cbuf") idx->cbuf_opt = (int)value;
+    else if (k == "kernel") idx->kernel_opt = (int)value;
     else return set_err(WV_ERR_INVALID, "unknown option %s", key);
     return WV_OK;
 }
@@ -519,9 +520,17 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     int32_t* flags = o_flags ? o_flags : idx->oF.as<int32_t>();
 
     if (mfma_ok) {
-        const int64_t ntiles = (idx->hiwater + BN - 1) / BN;
+        const int kver = idx->kernel_opt;
+        const int64_t bn = kver == 3 ? BN3 : BN;
+        const int64_t ntiles = (idx->hiwater + bn - 1) / bn;
         const int nqb = (int)(nq_pad / QB);
-        int64_t nspans = idx->spans_opt > 0 ? idx->spans_opt : std::max<int64_t>(1, (1024 + nqb - 1) / nqb);
+        int qgroup = 1;
+        for (int g : {4, 2, 1})
+            if (nqb % g == 0) { qgroup = g; break; }
+        // ~1024 workgroups (2 per CU resident, 2 waves of them); keep the
+        // workgroup count a multiple of 8 for the XCD mapping when possible
+        const int64_t target_wg = kver == 3 ? 768 : 1024;
+        int64_t nspans = idx->spans_opt > 0 ? idx->spans_opt : std::max<int64_t>(8, (target_wg + nqb - 1) / nqb);
         nspans = std::min<int64_t>(nspans, ntiles);
         int64_t tps = (ntiles + nspans - 1) / nspans;
         nspans = (ntiles + tps - 1) / tps;
@@ -533,30 +542,45 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         SelectArgs a;
         a.X = idx->X; a.xnorm2 = idx->xnorm2; a.valid = valid; a.ntiles = ntiles;
         a.Q = Qn; a.qnorm2 = idx->qn2.as<float>(); a.nq = (int)nq; a.dpad = idx->dpad;
-        a.tiles_per_span = (int)tps; a.nspans = (int)nspans; a.nqb = nqb; a.KP = KP;
+        a.tiles_per_span = (int)tps; a.nspans = (int)nspans; a.nqb = nqb; a.KP = KP; a.qgroup = qgroup;
         a.outA = idx->spanA.as<float>(); a.outI = idx->spanI.as<uint32_t>();
         // candidate buffer: as large as fits two workgroups per CU (<= 80 KiB each)
-        const int64_t fixed = (int64_t)(2 * QB * LDSROW + QB * KP * 2 + QB * 2 + 4) * (int64_t)sizeof(float);
-        int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(8, (80 * 1024 - fixed) / (QB * 8)));
+        const bool v2 = kver == 2;
+        const int64_t fixed = kver == 3 ? (int64_t)(NBUF3 * STG3 + QB * 2 + 4) * (int64_t)sizeof(float)
+                              : v2 ? (int64_t)(2 * (BN + QB) * BK + QB * 2 + 4) * (int64_t)sizeof(float)
+                                   : (int64_t)(2 * QB * LDSROW + QB * KP * 2 + QB * 2 + 4) * (int64_t)sizeof(float);
+        const int64_t budget = kver == 3 ? 160 * 1024 : 80 * 1024;
+        int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(4, (budget - fixed) / (QB * 8)));
         if (idx->cbuf_opt > 0) C = std::min(64 - KP, idx->cbuf_opt);
         size_t lds = (size_t)(fixed + (int64_t)QB * C * 8);
         a.C = C;
         dim3 grid((unsigned)(nqb * nspans));
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
-        switch (idx->metric) {
-        case WV_METRIC_L2_SQUARED:
-            HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select<L2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            k_mfma_select<L2, 1><<<grid, 256, lds, s>>>(a);
-            break;
-        case WV_METRIC_DOT:
-            HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select<DOT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            k_mfma_select<DOT, 1><<<grid, 256, lds, s>>>(a);
-            break;
-        default:
-            HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select<COSINE, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            k_mfma_select<COSINE, 1><<<grid, 256, lds, s>>>(a);
-            break;
+#define WV_SEL(KER, M)                                                                                       \
+    do {                                                                                                     \
+        HIPCHK(hipFuncSetAttribute((const void*)KER<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        KER<M, 1><<<grid, 256, lds, s>>>(a);                                                                 \
+    } while (0)
+#define WV_SEL3(M)                                                                                        \
+    do {                                                                                                  \
+        HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select3<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_mfma_select3<M, 1><<<grid, 512, lds, s>>>(a);                                                   \
+    } while (0)
+        if (kver == 3) {
+            switch (idx->metric) {
+            case WV_METRIC_L2_SQUARED: WV_SEL3(L2); break;
+            case WV_METRIC_DOT: WV_SEL3(DOT); break;
+            default: WV_SEL3(COSINE); break;
+            }
+        } else {
+            switch (idx->metric) {
+            case WV_METRIC_L2_SQUARED: if (v2) WV_SEL(k_mfma_select2, L2); else WV_SEL(k_mfma_select, L2); break;
+            case WV_METRIC_DOT: if (v2) WV_SEL(k_mfma_select2, DOT); else WV_SEL(k_mfma_select, DOT); break;
+            default: if (v2) WV_SEL(k_mfma_select2, COSINE); else WV_SEL(k_mfma_select, COSINE); break;
+            }
         }
+#undef WV_SEL3
+#undef WV_SEL
         HIPCHK(hipGetLastError());
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
         idx->stats.mfma_launches++;
