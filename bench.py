@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--n", type=int, default=N_TOTAL)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
-    ap.add_argument("--cpu-queries", type=int, default=128)
+    ap.add_argument("--cpu-queries", type=int, default=1024)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per k_mfma_select launch from the rocprofv3 PMC pass")
