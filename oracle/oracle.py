@@ -160,6 +160,40 @@ class OracleFlat:
         return rc, ids[: n.value].copy(), dd[: n.value].copy()
 
 
+class OracleFlatBQ(OracleFlat):
+    """Oracle flat index with BQ compression (flat/index.go:460-532): codes of the
+    stored (normalised) rows, R-heap by hamming, rescoring in pop order."""
+
+    def __init__(self, metric: int, variant: int, d: int, nslots: int, rescore_limit: int = -1):
+        super().__init__(metric, variant, d, nslots)
+        self.rescore_limit = rescore_limit
+        self.codes = np.zeros((nslots, (d + 63) // 64), dtype=np.uint64)
+
+    def add_batch(self, ids, vecs):
+        super().add_batch(ids, vecs)
+        for i in ids:
+            self.codes[int(i)] = bq_encode(self.store[int(i)])
+
+    def search(self, query, k, allow=None):
+        q = np.ascontiguousarray(query, dtype=np.float32)
+        ids = np.zeros(max(k, 1), dtype=np.uint64)
+        dd = np.zeros(max(k, 1), dtype=np.float32)
+        n = C.c_int(0)
+        allow_bm = None
+        allow_empty = 0
+        if allow is not None:
+            allow_bm = np.zeros(len(self.present), dtype=np.uint8)
+            a = [int(x) for x in allow if int(x) < len(self.present)]
+            allow_bm[a] = 1
+            allow_empty = 1 if len(list(allow)) == 0 else 0
+        rc = lib().or_flat_search_bq(self.metric, self.variant, f(self.store), self.present.ctypes.data_as(pb),
+                                     self.present.ctypes.data_as(pb), self.codes.ctypes.data_as(pu),
+                                     len(self.present), self.d, f(q), q.size, k, self.rescore_limit,
+                                     allow_bm.ctypes.data_as(pb) if allow_bm is not None else None, allow_empty,
+                                     ids.ctypes.data_as(pu), f(dd), C.byref(n))
+        return rc, ids[: n.value].copy(), dd[: n.value].copy()
+
+
 def gen_matrix(kind: int, seed: int, row0: int, rows: int, d: int) -> np.ndarray:
     out = np.zeros((rows, d), dtype=np.float32)
     lib().or_gen_matrix(kind, seed, row0, rows, d, f(out))

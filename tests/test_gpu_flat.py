@@ -209,3 +209,69 @@ def test_select_kernel_variants(wv, oracle, kernel, metric, kind, n, d, k):
     ids, dists, counts = idx.search_by_vector_batch(queries, k)
     for qi in range(0, len(queries), 7):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
+
+
+# ---------------------------------------------------------------------------
+# BQ-compressed flat search (flat/index.go:460-532)
+# ---------------------------------------------------------------------------
+def build_bq_pair(wv, oracle, metric_name, variant, data, rescore_limit, ids=None):
+    n, d = data.shape
+    ids = np.arange(n, dtype=np.uint64) if ids is None else ids
+    idx = wv.FlatIndex(distance=metric_name, variant=variant, bq=True, rescore_limit=rescore_limit)
+    idx.add_batch(ids, data)
+    orc = oracle.OracleFlatBQ(oracle.METRIC[metric_name], VARIANTS[variant], d, int(ids.max()) + 1, rescore_limit)
+    orc.add_batch(ids, data)
+    return idx, orc
+
+
+@pytest.mark.parametrize("metric,kind,n,d,k,rescore", [
+    ("cosine", 0, 20000, 1536, 10, 200),   # C4-shaped (scaled)
+    ("cosine", 0, 5000, 768, 10, -1),      # default rescore limit -> k
+    ("l2-squared", 0, 7000, 128, 10, 100),
+    ("dot", 0, 3000, 100, 5, 37),          # ragged words
+    ("cosine", 1, 3000, 64, 10, 50),       # all-positive data: every code is 0, hamming ties everywhere
+    ("l2-squared", 2, 2500, 200, 20, 20),  # rescore == k
+    ("cosine", 0, 600, 65, 10, 1000),      # rescore limit > corpus
+])
+def test_bq_search_matches_oracle(wv, oracle, metric, kind, n, d, k, rescore):
+    data = gen(oracle, kind, 11, n, d)
+    queries = gen(oracle, kind, 12, 24, d)
+    idx, orc = build_bq_pair(wv, oracle, metric, "avx256", data, rescore)
+    assert idx.compressed()
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    for q in range(len(queries)):
+        assert_same(orc.search(queries[q], k), ids[q, :counts[q]], dists[q, :counts[q]], f"bq {metric} q{q}")
+    idx.close()
+
+
+def test_bq_allow_delete_upsert_variant(wv, oracle):
+    n, d, k = 4000, 96, 10
+    data = gen(oracle, 0, 21, n, d)
+    idx, orc = build_bq_pair(wv, oracle, "cosine", "avx512", data, 64)
+    dele = np.arange(0, n, 7, dtype=np.uint64)
+    idx.delete(*dele)
+    orc.delete(dele)
+    up = gen(oracle, 0, 22, 50, d)
+    upids = np.arange(100, 150, dtype=np.uint64)
+    idx.add_batch(upids, up)
+    orc.add_batch(upids, up)
+    queries = gen(oracle, 0, 23, 8, d)
+    allow = np.arange(50, 3000, 3, dtype=np.uint64)
+    for q in range(len(queries)):
+        gi, gd = idx.search_by_vector(queries[q], k)
+        assert_same(orc.search(queries[q], k), gi, gd, f"q{q}")
+        gi, gd = idx.search_by_vector(queries[q], k, allow=wv.AllowList(allow))
+        assert_same(orc.search(queries[q], k, allow=allow), gi, gd, f"allow q{q}")
+        gi, gd = idx.search_by_vector(queries[q], k, allow=wv.AllowList([]))
+        assert len(gi) == 0
+    idx.close()
+
+
+def test_bq_errors(wv, oracle):
+    data = gen(oracle, 0, 31, 300, 128)
+    idx, _ = build_bq_pair(wv, oracle, "l2-squared", "avx256", data, -1)
+    with pytest.raises(wv.WeaviateError, match="both vectors should have the same len"):
+        idx.search_by_vector(np.zeros(200, np.float32), 5)
+    with pytest.raises(wv.WeaviateError, match="vector lengths don't match"):
+        idx.search_by_vector(np.zeros(100, np.float32), 5)  # same word count, rescoring length check
+    idx.close()

@@ -15,6 +15,7 @@ LIB = os.path.join(HERE, "libwvknn.so")
 SOURCES = [
     os.path.join(HERE, "csrc", "runtime.hip"),
     os.path.join(HERE, "csrc", "kernels.hip"),
+    os.path.join(HERE, "csrc", "bq_kernels.hip"),
     os.path.join(HERE, "csrc", "wv_device.h"),
     os.path.join(REPO, "include", "wv_knn.h"),
 ]

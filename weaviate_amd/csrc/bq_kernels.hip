@@ -1,0 +1,207 @@
+// bq_kernels.hip -- gfx950 kernels of the BQ-compressed flat search
+// (flat.searchByVectorQuantized, flat/index.go:460-532).
+//
+// Codes live word-major in HBM: codes[w * ccap + slot] = word w of the
+// BinaryQuantizer code of the stored (normalised) row `slot`
+// (compressionhelpers/binary_quantization.go:28-47), so a wave reading word w
+// of 64 consecutive slots issues one coalesced 512 B load.
+//
+// Search, per batch of queries (all integer work until the rescoring):
+//   k_bq_encode_rows   queries -> codes (same encoder as Add)
+//   k_bq_blockmin      hamming distance of every (query, row) pair, reduced
+//                      to the minimum per 256-row block; nothing else is
+//                      written (VALU-bound: 2 x v_xor + 2 x v_bcnt per word)
+//   k_bq_replay        one wave per query replays the reference's R-heap
+//                      (priorityqueue.NewMax + insertToHeap over id order,
+//                      flat/index.go:578-674) exactly: a block is visited only
+//                      while the heap is short or its minimum is < top (the
+//                      top never increases, so a skipped block cannot insert);
+//                      visited blocks recompute their distances in-register.
+//                      Then it pops the heap max-first (:485-487) and writes
+//                      the R candidates in that pop order.
+//   k_rescore          exact-order fp32 SingleDist of every candidate (shared
+//                      with the uncompressed path)
+//   k_bq_final         insertToHeap(heap, k, ...) in pop order + extractHeap
+//                      (:525-531)
+// Hamming ties are the rule, not the exception, so the replay is the path for
+// every query: the selected set and its tie order are the reference's.
+#pragma once
+
+namespace wv {
+
+constexpr int BQBLK = 256;  // rows per block minimum (== EBLK)
+
+// BinaryQuantizer.Encode of padded rows: bit (i mod 64) of word i/64 is set iff
+// v[i] < 0 (NaN / +-0 -> 0).  Thread per (row, word); row r reads and writes
+// slot = slots[r] (or r): rows[slot * ld ...] -> out[w * ldo + slot].
+__global__ void k_bq_encode_rows(const float* __restrict__ rows, int64_t ld, int64_t n, int d,
+                                 const uint32_t* __restrict__ slots, uint64_t* __restrict__ out, int64_t ldo) {
+    const int words = (d + 63) >> 6;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * words) return;
+    const int64_t r = i % n;  // consecutive threads -> consecutive rows: coalesced stores
+    const int w = (int)(i / n);
+    const int64_t slot = slots ? (int64_t)slots[r] : r;
+    const float* src = rows + slot * ld + 64 * w;
+    const int lim = d - 64 * w < 64 ? d - 64 * w : 64;
+    uint64_t bits = 0;
+    for (int b = 0; b < lim; b++)
+        if (src[b] < 0.f) bits |= 1ull << b;
+    out[(int64_t)w * ldo + slot] = bits;
+}
+
+// Block minima of the hamming distances.  Block (x, y): rows [256x, +256),
+// listed queries [QPB*y, +QPB).  Thread = row; the row's words are read once
+// (coalesced) and xor/popcounted against QPB query codes held in SGPRs.
+// Query codes are word-major too: word w of query q at qcodes[w * ldq + q].
+// bmin[f * nblk + x] = min over valid rows (+inf if none).
+template <int QPB>
+__global__ __launch_bounds__(256) void k_bq_blockmin(const uint64_t* __restrict__ codes, int64_t ccap, int words,
+                                                     const uint32_t* __restrict__ valid, int64_t nslots,
+                                                     const uint64_t* __restrict__ qcodes, int64_t ldq,
+                                                     const int32_t* __restrict__ qlist, int nlist, int64_t nblk,
+                                                     float* __restrict__ bmin) {
+    __shared__ uint32_t red[4][QPB];
+    const int64_t blk = blockIdx.x;
+    const int f0 = blockIdx.y * QPB;
+    const int64_t s = blk * BQBLK + threadIdx.x;
+    const bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
+    int qrow[QPB];
+#pragma unroll
+    for (int f = 0; f < QPB; f++) qrow[f] = qlist[(f0 + f) < nlist ? f0 + f : nlist - 1];
+    uint32_t acc[QPB];
+#pragma unroll
+    for (int f = 0; f < QPB; f++) acc[f] = 0;
+    const uint64_t* cp = codes + (s < nslots ? s : 0);
+    for (int w = 0; w < words; w++) {
+        const uint64_t x = cp[(int64_t)w * ccap];
+#pragma unroll
+        for (int f = 0; f < QPB; f++) acc[f] += (uint32_t)__popcll(x ^ qcodes[(int64_t)w * ldq + qrow[f]]);
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int f = 0; f < QPB; f++) {
+        uint32_t m = ok ? acc[f] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+        if (lane == 0) red[wv][f] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x < QPB && f0 + (int)threadIdx.x < nlist) {
+        const int f = threadIdx.x;
+        const uint32_t m = min(min(red[0][f], red[1][f]), min(red[2][f], red[3][f]));
+        bmin[(int64_t)(f0 + f) * nblk + blk] = m == 0xFFFFFFFFu ? __builtin_inff() : (float)m;
+    }
+}
+
+// Exact replay of the R-heap of searchByVectorQuantized (one wave per listed
+// query), then the max-first pop of the whole heap (flat/index.go:485-487).
+// out_slot[li * R + i] = slot of the i-th popped item, out_n[li] = heap length.
+// Dynamic LDS: [R] u64 ids | [64] f32 | [R] f32 dists | len.
+__global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ codes, int64_t ccap, int words,
+                                                  const uint32_t* __restrict__ valid, int64_t nslots,
+                                                  const uint64_t* __restrict__ qcodes, int64_t ldq,
+                                                  const int32_t* __restrict__ qlist, int nlist,
+                                                  const float* __restrict__ bmin, int64_t nblk, int R,
+                                                  uint32_t* __restrict__ out_slot, int32_t* __restrict__ out_n) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+    uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
+    float* s_d = reinterpret_cast<float*>(hid + R);
+    float* hd = s_d + 64;
+    int* s_len = reinterpret_cast<int*>(hd + R);
+    const int lane = threadIdx.x;
+    const int li = blockIdx.x;
+    if (li >= nlist) return;
+    const uint64_t* qc = qcodes + qlist[li];  // word w at qc[w * ldq]
+    const float* Bq = bmin + (int64_t)li * nblk;
+    if (lane == 0) *s_len = 0;
+    __syncthreads();
+    for (int64_t b0 = 0; b0 < nblk; b0 += 64) {
+        const float bm = (b0 + lane < nblk) ? Bq[b0 + lane] : __builtin_inff();
+        int len = *s_len;
+        float top = len > 0 ? hd[0] : 0.f;
+        uint64_t bmask = __ballot((b0 + lane < nblk) && bm != __builtin_inff() && (len < R || top > bm));
+        while (bmask) {
+            const int j = __builtin_ctzll(bmask);
+            bmask &= bmask - 1;
+            const float bmj = __shfl(bm, j);
+            len = *s_len;
+            top = len > 0 ? hd[0] : 0.f;
+            if (!(len < R || top > bmj)) continue;
+            const int64_t r0 = (b0 + j) * BQBLK;
+            for (int sub = 0; sub < BQBLK; sub += 64) {
+                const int64_t s = r0 + sub + lane;
+                const bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
+                uint32_t h = 0;
+                if (ok)
+                    for (int w = 0; w < words; w++) h += (uint32_t)__popcll(codes[(int64_t)w * ccap + s] ^ qc[(int64_t)w * ldq]);
+                const float dist = (float)h;
+                len = *s_len;
+                top = len > 0 ? hd[0] : 0.f;
+                uint64_t mask = __ballot(ok && (len < R || top > dist));
+                if (mask == 0) continue;
+                s_d[lane] = dist;
+                __syncthreads();
+                if (lane == 0) {
+                    ReplayHeap hp{hid, hd, *s_len};
+                    while (mask) {
+                        const int jj = __builtin_ctzll(mask);
+                        mask &= mask - 1;
+                        const float dj = s_d[jj];
+                        const uint64_t sj = (uint64_t)(s - lane + jj);
+                        if (hp.len < R) rh_insert(hp, sj, dj);
+                        else if (hp.dist[0] > dj) { uint64_t a; float b; rh_pop(hp, &a, &b); rh_insert(hp, sj, dj); }
+                    }
+                    *s_len = hp.len;
+                }
+                __syncthreads();
+            }
+        }
+    }
+    if (lane == 0) {
+        ReplayHeap hp{hid, hd, *s_len};
+        const int n = hp.len;
+        for (int i = 0; i < n; i++) {
+            uint64_t a; float b;
+            rh_pop(hp, &a, &b);
+            out_slot[(int64_t)li * R + i] = (uint32_t)a;
+        }
+        for (int i = n; i < R; i++) out_slot[(int64_t)li * R + i] = NO_ID;
+        out_n[li] = n;
+    }
+}
+
+// Rescoring heap (flat/index.go:525-531): the candidates, in pop order, go
+// through insertToHeap(heap, k, id, dist); extractHeap gives the result.
+// One wave per listed query; lane 0 runs the heap in LDS ([k] u64 | [k] f32).
+__global__ __launch_bounds__(64) void k_bq_final(const uint32_t* __restrict__ cand_slot,
+                                                 const float* __restrict__ candE,
+                                                 const int32_t* __restrict__ cand_n, const int32_t* __restrict__ qlist,
+                                                 int nlist, int R, int k, uint64_t id_base,
+                                                 uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
+                                                 int32_t* __restrict__ out_n) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+    uint64_t* hid = reinterpret_cast<uint64_t*>(fsm);
+    float* hd = reinterpret_cast<float*>(hid + k);
+    const int li = blockIdx.x;
+    if (li >= nlist || threadIdx.x != 0) return;
+    const int q = qlist[li];
+    ReplayHeap hp{hid, hd, 0};
+    const int n = cand_n[li];
+    for (int i = 0; i < n; i++) {
+        const uint64_t id = id_base + cand_slot[(int64_t)li * R + i];
+        const float dist = candE[(int64_t)li * R + i];
+        if (hp.len < k) rh_insert(hp, id, dist);
+        else if (hp.dist[0] > dist) { uint64_t a; float b; rh_pop(hp, &a, &b); rh_insert(hp, id, dist); }
+    }
+    const int m = hp.len;
+    for (int i = m - 1; i >= 0; i--) {
+        uint64_t a; float b;
+        rh_pop(hp, &a, &b);
+        out_ids[(int64_t)q * k + i] = a;
+        out_d[(int64_t)q * k + i] = b;
+    }
+    out_n[q] = m;
+}
+
+}  // namespace wv

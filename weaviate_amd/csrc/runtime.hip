@@ -23,6 +23,7 @@
 
 #include "../../include/wv_knn.h"
 #include "kernels.hip"
+#include "bq_kernels.hip"
 
 using namespace wv;
 
@@ -116,11 +117,13 @@ struct wv_index {
     float* xnorm2 = nullptr;
     uint32_t* present = nullptr;
     uint32_t* d_maxn2 = nullptr;
+    uint64_t* codes = nullptr;   // BQ: [words][cap] word-major codes of the stored rows
+    int words = 0;
     std::vector<uint8_t> h_present;
     uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
     int64_t npresent = 0;
 
-    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB;
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident;
 
     int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -136,8 +139,6 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
         return set_err(WV_ERR_INVALID, "invalid config: unknown distance metric %d", cfg->metric);
     if (cfg->compression != WV_COMPRESSION_NONE && cfg->compression != WV_COMPRESSION_BQ)
         return set_err(WV_ERR_UNSUPPORTED, "invalid config: unsupported compression %d", cfg->compression);
-    if (cfg->compression == WV_COMPRESSION_BQ)
-        return set_err(WV_ERR_UNSUPPORTED, "bq compression: not available in this build");
     HIPCHK(hipSetDevice(cfg->device));
     wv_index* idx = new wv_index();
     idx->metric = cfg->metric;
@@ -167,12 +168,14 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->stream) hipStreamSynchronize(idx->stream);
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
-                    &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB})
+                    &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
+                    &idx->cn, &idx->ident})
         b->release();
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
     if (idx->present) hipFree(idx->present);
     if (idx->d_maxn2) hipFree(idx->d_maxn2);
+    if (idx->codes) hipFree(idx->codes);
     if (idx->ev0) hipEventDestroy(idx->ev0);
     if (idx->ev1) hipEventDestroy(idx->ev1);
     if (idx->stream) hipStreamDestroy(idx->stream);
@@ -205,6 +208,19 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
     if (idx->present) hipFree(idx->present);
+    if (idx->compression == WV_COMPRESSION_BQ) {
+        const int words = (idx->dims + 63) / 64;
+        uint64_t* cd = nullptr;
+        HIPCHK(hipMalloc(&cd, (size_t)words * nc * sizeof(uint64_t)));
+        HIPCHK(hipMemsetAsync(cd, 0, (size_t)words * nc * sizeof(uint64_t), idx->stream));
+        if (idx->cap > 0)  // word-major: copy each word plane
+            HIPCHK(hipMemcpy2DAsync(cd, (size_t)nc * sizeof(uint64_t), idx->codes, (size_t)idx->cap * sizeof(uint64_t),
+                                    (size_t)idx->cap * sizeof(uint64_t), words, hipMemcpyDeviceToDevice, idx->stream));
+        HIPCHK(hipStreamSynchronize(idx->stream));
+        if (idx->codes) hipFree(idx->codes);
+        idx->codes = cd;
+        idx->words = words;
+    }
     idx->X = X;
     idx->xnorm2 = xn;
     idx->present = pr;
@@ -252,6 +268,11 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
         k_prepare_rows<L2><<<grid, 256, 0, idx->stream>>>(d_in, n, idx->dims, d_slots, idx->X, idx->dpad, idx->xnorm2,
                                                           idx->present, idx->d_maxn2);
         break;
+    }
+    if (idx->compression == WV_COMPRESSION_BQ) {  // Preload: quantizer.Encode of the stored row (flat/index.go:376)
+        const int64_t nt = n * idx->words;
+        k_bq_encode_rows<<<(unsigned)((nt + 255) / 256), 256, 0, idx->stream>>>(idx->X, idx->dpad, n, idx->dims, d_slots,
+                                                                                 idx->codes, idx->cap);
     }
 }
 
@@ -490,6 +511,93 @@ static int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, in
     return WV_OK;
 }
 
+// searchByVectorQuantized (flat/index.go:460-532) for BQ indexes, every query
+// through the exact R-heap replay (bq_kernels.hip).  Outputs [nq][k].
+static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
+                     const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+    // query code length vs stored code length: HammingBitwise (distancer/hamming.go:63-66)
+    if ((qd + 63) / 64 != idx->words) return set_err(WV_ERR_VECTOR_LENGTH, "both vectors should have the same len");
+    // the rescoring SingleDist then checks the float lengths (distancer/errors.go:16)
+    if (qd != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)qd, idx->dims);
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    const int R = idx->rescore_limit > k ? idx->rescore_limit : k;  // searchTimeRescore (:413-421)
+    if (R > 8192) return set_err(WV_ERR_UNSUPPORTED, "rescore limit %d > 8192", R);
+    const int64_t nq_pad = round_up(nq, QB);
+    int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
+    if (rc) return rc;
+    const float* Qn = idx->qn.as<float>();
+    const int words = idx->words;
+    HIPCHK(idx->qcodes.ensure((size_t)nq * words * sizeof(uint64_t)));
+    {
+        const int64_t nt = nq * words;
+        // word-major query codes: word w of query q at qcodes[w * nq + q]
+        k_bq_encode_rows<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(Qn, idx->dpad, nq, idx->dims, nullptr,
+                                                                       idx->qcodes.as<uint64_t>(), nq);
+        HIPCHK(hipGetLastError());
+    }
+    idx->stats.queries += (uint64_t)nq;
+    idx->stats.batches++;
+    idx->stats.replayed_queries += (uint64_t)nq;
+    const int64_t nslots = idx->hiwater;
+    const int64_t nblk = std::max<int64_t>((nslots + BQBLK - 1) / BQBLK, 1);
+    // identity query list
+    HIPCHK(idx->ident.ensure((size_t)nq * sizeof(int32_t)));
+    {
+        std::vector<int32_t> id((size_t)nq);
+        for (int64_t i = 0; i < nq; i++) id[i] = (int32_t)i;
+        HIPCHK(hipMemcpyAsync(idx->ident.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    const int32_t* qlist = idx->ident.as<int32_t>();
+    constexpr int QPB = 16;
+    const int64_t G = std::max<int64_t>(QPB, std::min<int64_t>(round_up(nq, QPB), ((1ll << 30) / (nblk * 4)) / QPB * QPB));
+    HIPCHK(idx->bqmin.ensure((size_t)G * nblk * sizeof(float)));
+    HIPCHK(idx->cslot.ensure((size_t)nq * R * sizeof(uint32_t)));
+    HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
+    if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
+    const size_t lds_r = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
+    if (lds_r > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_bq_replay, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_r));
+    for (int64_t g0 = 0; g0 < nq; g0 += G) {
+        const int F = (int)std::min<int64_t>(G, nq - g0);
+        dim3 grid((unsigned)nblk, (unsigned)((F + QPB - 1) / QPB));
+        k_bq_blockmin<QPB><<<grid, 256, 0, s>>>(idx->codes, idx->cap, words, valid, nslots, idx->qcodes.as<uint64_t>(),
+                                                nq, qlist + g0, F, nblk, idx->bqmin.as<float>());
+        HIPCHK(hipGetLastError());
+        k_bq_replay<<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots,
+                                                  idx->qcodes.as<uint64_t>(), nq, qlist + g0, F,
+                                                  idx->bqmin.as<float>(), nblk, R,
+                                                  idx->cslot.as<uint32_t>() + g0 * R, idx->cn.as<int32_t>() + g0);
+        HIPCHK(hipGetLastError());
+    }
+    if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
+    const int64_t npairs = nq * R;
+    const bool v5 = idx->variant == WV_VARIANT_AVX512;
+#define WV_RS(M, V) k_rescore<M, V><<<(unsigned)((npairs + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, Qn, idx->dims, idx->cslot.as<uint32_t>(), (int)nq, R, idx->candE.as<float>())
+    switch (idx->metric) {
+    case WV_METRIC_L2_SQUARED: if (v5) WV_RS(L2, AVX512); else WV_RS(L2, AVX256); break;
+    case WV_METRIC_DOT: if (v5) WV_RS(DOT, AVX512); else WV_RS(DOT, AVX256); break;
+    case WV_METRIC_COSINE_DOT: if (v5) WV_RS(COSINE, AVX512); else WV_RS(COSINE, AVX256); break;
+    default: WV_RS(HAMMING, AVX256); break;
+    }
+#undef WV_RS
+    HIPCHK(hipGetLastError());
+    const size_t lds_f = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
+    if (lds_f > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_bq_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
+    k_bq_final<<<(unsigned)nq, 64, lds_f, s>>>(idx->cslot.as<uint32_t>(), idx->candE.as<float>(), idx->cn.as<int32_t>(),
+                                               qlist, (int)nq, R, k, idx->id_base, o_ids, o_d, o_n);
+    HIPCHK(hipGetLastError());
+    if (idx->timing) {
+        HIPCHK(hipStreamSynchronize(s));
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
+        idx->stats.last_select_ms = ms;
+    }
+    return WV_OK;
+}
+
 // Core batch search on device queries.  Outputs [nq][kout] device arrays.
 // mode 0: kout = k, flagged queries resolved by replay; mode 1: kout = k+1,
 // flags left for the caller.  n_valid = number of scan candidates.
@@ -502,6 +610,10 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         HIPCHK(hipMemsetAsync(o_n, 0, (size_t)nq * sizeof(int32_t), s));
         if (o_flags) HIPCHK(hipMemsetAsync(o_flags, 0, (size_t)nq * sizeof(int32_t), s));
         return WV_OK;
+    }
+    if (idx->compression == WV_COMPRESSION_BQ) {
+        if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "bq: shard-candidate mode not available");
+        return search_bq(idx, s, d_qraw, nq, qd, k, valid, o_ids, o_d, o_n);
     }
     // SingleDist length check on the first candidate: distancer/l2.go:47-50 etc.
     if (qd != idx->dims)

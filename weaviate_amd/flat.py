@@ -76,6 +76,8 @@ class FlatIndex:
         check(self._l.wv_index_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self.metric = DISTANCES[distance]
+        self.bq = bool(bq)
+        self.rescore_limit = int(rescore_limit)
         self.device = device
         self.id_base = id_base
 
@@ -103,8 +105,8 @@ class FlatIndex:
     def distancer_type(self) -> str:  # Provider.Type()
         return PROVIDER_TYPE[self.metric]
 
-    def compressed(self) -> bool:
-        return False
+    def compressed(self) -> bool:  # flat.Compressed (flat/index.go): BQ quantizer built at New
+        return self.bq
 
     def reserve(self, nslots: int) -> None:
         check(self._l.wv_index_reserve(self._h, int(nslots)))
