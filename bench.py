@@ -34,6 +34,15 @@ K = 10
 SEED_CORPUS = 1
 SEED_QUERY = 2
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+# 32-bit integer VALU lane-ops/s: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  The
+# 32-lane/clk rate (78.6 T) is the f32 FMA rate; v_xor_b32 / v_bcnt_u32_b32 issue
+# at 4 cycles per wave64 (measured: k_bq_blockmin_lds sustains 33.6 T instr-lane-ops/s).
+VALU_PEAK_TOPS = 39.3
+
+# BASELINE configs[3]: BQ 50M x 1536 over 8 GPUs -> one GPU holds a 6.25M-row shard
+BQ_ROWS_PER_GPU = 6_250_000
+BQ_DIMS = 1536
+BQ_RESCORE = 200
 
 
 def log(*a):
@@ -68,16 +77,47 @@ def cpu_baseline(n_sample: int, nq: int, threads: int):
     }
 
 
+def cpu_baseline_bq(n_sample: int, nq: int, threads: int, n_full: int):
+    """Reference CPU BQ flat search (searchByVectorQuantized restated in
+    oracle/baseline.c) with the reference's own hamming_bitwise_256 and dot_256
+    kernels (oracle/_ref) when the host can run them; one query per thread."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc  # test infrastructure, used only for this baseline leg
+    use_ref = orc.ref_lib() is not None and orc.host_has_avx512()
+    corpus = orc.gen_matrix(0, SEED_CORPUS, 0, n_sample, BQ_DIMS)
+    orc.lib().or_normalize_rows(orc.f(corpus), n_sample, BQ_DIMS)
+    words = (BQ_DIMS + 63) // 64
+    bits = np.zeros((n_sample, words * 64), dtype=bool)
+    bits[:, :BQ_DIMS] = corpus < 0
+    codes = np.packbits(bits, axis=1, bitorder="little").view("<u8").reshape(n_sample, words)
+    queries = orc.gen_matrix(0, SEED_QUERY, 0, nq, BQ_DIMS)
+    orc.lib().or_normalize_rows(orc.f(queries), nq, BQ_DIMS)
+    t0 = time.perf_counter()
+    orc.cpu_baseline_bq(orc.COSINE, orc.AVX256, corpus, codes, queries, K, BQ_RESCORE, threads, use_ref)
+    dt = time.perf_counter() - t0
+    return {
+        "value": nq / dt * n_sample / n_full,
+        "unit": "queries/s",
+        "cores": threads,
+        "kind": "reference" if use_ref else "port",
+        "sample": (f"{nq} queries x {n_sample} rows, BQ hamming R={BQ_RESCORE} heap + fp32 rescoring, "
+                   f"{'reference hamming_bitwise_256 + dot_256 kernels (oracle/_ref)' if use_ref else 'oracle scalar restatement'}, "
+                   f"{dt:.1f} s, QPS scaled by {n_sample}/{n_full}"),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["c3", "bq"], default="c3",
+                    help="c3: 10M x 768 cosine exact (default, the headline); bq: BQ 1536-d shard of configs[3]")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=2048)
-    ap.add_argument("--n", type=int, default=N_TOTAL)
+    ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
-    ap.add_argument("--cpu-queries", type=int, default=1024)
+    ap.add_argument("--cpu-queries", type=int, default=None)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per k_mfma_select launch from the rocprofv3 PMC pass")
@@ -100,7 +140,11 @@ def main():
     from weaviate_amd import _lib
     lib = _lib.load()
 
-    n_total = args.n
+    bq = args.workload == "bq"
+    if bq and world > 1:
+        raise SystemExit("--workload bq: sharded BQ search is not available yet (1 GPU = one configs[3] shard)")
+    dims = BQ_DIMS if bq else DIMS
+    n_total = args.n if args.n is not None else (BQ_ROWS_PER_GPU if bq else N_TOTAL)
     n_local = (n_total + world - 1) // world
     id0 = rank * n_local
     n_local = max(0, min(n_local, n_total - id0))
@@ -108,17 +152,18 @@ def main():
 
     # ---- build the shard: generate + add in 1M-row chunks (device resident) ----
     t_build = time.perf_counter()
-    index = wv.FlatIndex(distance="cosine", dims=DIMS, device=local_rank, variant="avx256", id_base=id0)
+    index = wv.FlatIndex(distance="cosine", dims=dims, device=local_rank, variant="avx256", id_base=id0,
+                         bq=bq, rescore_limit=BQ_RESCORE if bq else -1)
     index.reserve(n_local)
     chunk = 1_000_000
-    stage = torch.empty((min(chunk, max(n_local, 1)), DIMS), dtype=torch.float32, device=dev)
+    stage = torch.empty((min(chunk, max(n_local, 1)), dims), dtype=torch.float32, device=dev)
     for r0 in range(0, n_local, chunk):
         m = min(chunk, n_local - r0)
-        _lib.check(lib.wv_gen_device(local_rank, 0, SEED_CORPUS, id0 + r0, m, DIMS, stage.data_ptr(), None))
-        _lib.check(lib.wv_index_add_range_device(index._h, id0 + r0, stage.data_ptr(), m, DIMS))
+        _lib.check(lib.wv_gen_device(local_rank, 0, SEED_CORPUS, id0 + r0, m, dims, stage.data_ptr(), None))
+        _lib.check(lib.wv_index_add_range_device(index._h, id0 + r0, stage.data_ptr(), m, dims))
     del stage
-    queries = torch.empty((B, DIMS), dtype=torch.float32, device=dev)
-    _lib.check(lib.wv_gen_device(local_rank, 0, SEED_QUERY, 0, B, DIMS, queries.data_ptr(), None))
+    queries = torch.empty((B, dims), dtype=torch.float32, device=dev)
+    _lib.check(lib.wv_gen_device(local_rank, 0, SEED_QUERY, 0, B, dims, queries.data_ptr(), None))
     torch.cuda.synchronize()
     log(f"[rank {rank}] shard ids [{id0}, {id0 + n_local}) built in {time.perf_counter() - t_build:.1f} s")
     index.set_option("timing", 1)
@@ -136,7 +181,7 @@ def main():
     else:
         def step():
             s = torch.cuda.current_stream(dev).cuda_stream
-            _lib.check(lib.wv_index_search_device(index._h, queries.data_ptr(), B, DIMS, K, 0, out_ids.data_ptr(),
+            _lib.check(lib.wv_index_search_device(index._h, queries.data_ptr(), B, dims, K, 0, out_ids.data_ptr(),
                                                   out_d.data_ptr(), out_n.data_ptr(), None, s))
 
     for _ in range(args.warmup):
@@ -170,20 +215,43 @@ def main():
     total_q = B * args.steps
     value = total_q / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    # roofline of the dominant kernel (k_mfma_select): algorithmic flops per
-    # launch = 2 * B * n_local * d (one FMA per element pair), over its measured
-    # average duration (HIP events on the stream it runs on).
-    flops = 2.0 * B * n_local * DIMS
-    achieved = flops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
+    if bq:
+        # dominant kernel k_bq_blockmin: VALU-bound integer work, per (query,
+        # row) pair and 64-bit code word 2 v_xor_b32 + 2 v_bcnt_u32_b32
+        words = (dims + 63) // 64
+        ops = 4.0 * B * n_local * words
+        achieved = ops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
+        roof = {"bound": "valu", "kernel": "k_bq_blockmin", "achieved": achieved, "peak": VALU_PEAK_TOPS,
+                "unit": "Tops/s (int32 lane-ops)", "frac": achieved / VALU_PEAK_TOPS, "launch_ms": sel_avg,
+                "hbm_GBps": n_local * words * 8 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
+                "traffic": args.traffic_bytes}
+    else:
+        # roofline of the dominant kernel (k_mfma_select): algorithmic flops per
+        # launch = 2 * B * n_local * d (one FMA per element pair), over its measured
+        # average duration (HIP events on the stream it runs on).
+        flops = 2.0 * B * n_local * dims
+        achieved = flops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
+        roof = {"bound": "mfma", "kernel": "k_mfma_select", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS, "launch_ms": sel_avg,
+                "traffic": args.traffic_bytes}
 
     result = None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(min(args.cpu_rows, n_total), args.cpu_queries, args.cpu_threads)
+                if bq:
+                    cpu = cpu_baseline_bq(min(args.cpu_rows, n_total), args.cpu_queries or 4096, args.cpu_threads,
+                                          n_total)
+                else:
+                    cpu = cpu_baseline(min(args.cpu_rows, n_total), args.cpu_queries or 1024, args.cpu_threads)
             except Exception as e:  # baseline failure must not hide the GPU number
                 log(f"cpu baseline failed: {e}")
+        if bq:
+            workload = (f"BQ {dims}-d cosine, k={K}, rescore R={BQ_RESCORE}: one {n_total}-row shard of "
+                        "BASELINE configs[3] (50M x 1536 over 8 GPUs)")
+        else:
+            workload = "10M x 768 fp32 cosine, k=10, exact flat search (BASELINE configs[2])"
         result = {
             "metric": METRIC,
             "value": value,
@@ -195,28 +263,19 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "u64 hamming + f32 rescoring" if bq else "f32",
             "data": "synthetic (counter-based U[-1,1) generator, seed 1 corpus / 2 queries)",
             "config": {
-                "workload": "10M x 768 fp32 cosine, k=10, exact flat search (BASELINE configs[2])",
+                "workload": workload,
                 "corpus_rows": n_total,
-                "dims": DIMS,
+                "dims": dims,
                 "k": K,
                 "query_batch": B,
                 "parallelism": f"corpus sharded over {world} GPU(s), contiguous id ranges"
                                + (", RCCL all-gather merge" if world > 1 else ""),
                 "replayed_queries": int(replays),
             },
-            "roofline": {
-                "bound": "mfma",
-                "kernel": "k_mfma_select",
-                "achieved": achieved,
-                "peak": MFMA_F32_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved / MFMA_F32_PEAK_TFLOPS,
-                "launch_ms": sel_avg,
-                "traffic": args.traffic_bytes,
-            },
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

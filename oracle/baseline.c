@@ -80,3 +80,78 @@ int bl_flat_search_batch(int metric, int variant, int use_ref, const float *stor
     free(th); free(jobs);
     return 0;
 }
+
+/* ---- BQ: searchByVectorQuantized (flat/index.go:460-532), one query per thread ---- */
+typedef void (*ref_hbw)(uint64_t *a, uint64_t *b, uint64_t *res, long *len, uint8_t *lookup, uint64_t *consts);
+static ref_hbw g_ref_hbw;
+static uint8_t g_lookup[32] = {0, 1, 1, 2, 1, 2, 2, 3, 1, 2, 2, 3, 2, 3, 3, 4, 0, 1, 1, 2, 1, 2, 2, 3, 1, 2, 2, 3, 2, 3, 3, 4};
+static uint64_t g_consts[5] = {0x5555555555555555ull, 0x3333333333333333ull, 0x0F0F0F0F0F0F0F0Full,
+                               0x0101010101010101ull, 0x0F0F0F0F0F0F0F0Full};
+
+/* hamming_bitwise_256 from oracle/_ref (asm/hamming_amd64.go:69-80 passes the
+ * lookup table and popcount constants) */
+void bl_set_ref_hamming(void *hamming_bitwise_256) { g_ref_hbw = (ref_hbw)hamming_bitwise_256; }
+
+typedef struct {
+    job_t base;
+    const uint64_t *codes; long words; int rescore;
+} bq_job_t;
+
+static void *bq_worker(void *arg) {
+    bq_job_t *bj = (bq_job_t *)arg;
+    job_t *j = &bj->base;
+    int R = bj->rescore;
+    or_heap h;
+    h.id = (uint64_t *)malloc(sizeof(uint64_t) * (R + 1));
+    h.dist = (float *)malloc(sizeof(float) * (R + 1));
+    uint64_t *cand = (uint64_t *)malloc(sizeof(uint64_t) * (R + 1));
+    float *cd = (float *)malloc(sizeof(float) * (R + 1));
+    uint64_t *qc = (uint64_t *)malloc(sizeof(uint64_t) * (bj->words + 1));
+    for (long qi = j->tid; qi < j->nq; qi += j->nthreads) {
+        const float *q = j->queries + (size_t)qi * j->d;
+        or_bq_encode(q, j->d, qc);
+        h.len = 0;
+        for (long s = 0; s < j->n; s++) {
+            float dist;
+            const uint64_t *x = bj->codes + (size_t)s * bj->words;
+            if (j->use_ref && g_ref_hbw) {
+                uint64_t res = 0; long len = bj->words;
+                g_ref_hbw((uint64_t *)x, qc, &res, &len, g_lookup, g_consts);
+                dist = (float)res;
+            } else {
+                dist = or_hamming_bitwise(x, qc, bj->words);
+            }
+            or_insert_to_heap(&h, R, (uint64_t)s, dist);
+        }
+        int n = h.len;
+        for (int i = 0; i < n; i++) { float t; or_heap_pop(&h, &cand[i], &t); }
+        for (int i = 0; i < n; i++) cd[i] = pair_dist(j, q, j->store + (size_t)cand[i] * j->d);
+        for (int i = 0; i < n; i++) or_insert_to_heap(&h, j->k, cand[i], cd[i]);
+        j->out_n[qi] = or_extract_heap(&h, j->out_ids + (size_t)qi * j->k, j->out_dists + (size_t)qi * j->k);
+    }
+    free(h.id); free(h.dist); free(cand); free(cd); free(qc);
+    return NULL;
+}
+
+/* store: normalised fp32 rows [n][d]; codes: [n][words] of the stored rows;
+ * queries normalised already for cosine. */
+int bl_flat_search_bq_batch(int metric, int variant, int use_ref, const float *store, const uint64_t *codes,
+                            long n, long d, const float *queries, long nq, int k, int rescore_limit, int nthreads,
+                            uint64_t *out_ids, float *out_dists, int *out_n) {
+    if (use_ref && !g_ref[0]) return -1;
+    if (nthreads < 1) nthreads = 1;
+    int R = rescore_limit > k ? rescore_limit : k;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+    bq_job_t *jobs = (bq_job_t *)malloc(sizeof(bq_job_t) * nthreads);
+    for (int t = 0; t < nthreads; t++) {
+        job_t j = {metric, variant, use_ref, k, store, n, d, queries, nq, out_ids, out_dists, out_n, t, nthreads};
+        jobs[t].base = j;
+        jobs[t].codes = codes;
+        jobs[t].words = (d + 63) / 64;
+        jobs[t].rescore = R;
+        pthread_create(&th[t], NULL, bq_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th); free(jobs);
+    return 0;
+}

@@ -57,9 +57,13 @@ def lib() -> C.CDLL:
         o.or_gen_value.restype = C.c_float
         o.or_gen_value.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64]
         o.bl_set_ref_kernels.argtypes = [C.c_void_p] * 4
+        o.bl_set_ref_hamming.argtypes = [C.c_void_p]
         o.bl_flat_search_batch.restype = C.c_int
         o.bl_flat_search_batch.argtypes = [C.c_int, C.c_int, C.c_int, pf, C.c_long, C.c_long, pf, C.c_long, C.c_int,
                                            C.c_int, pu, pf, pi]
+        o.bl_flat_search_bq_batch.restype = C.c_int
+        o.bl_flat_search_bq_batch.argtypes = [C.c_int, C.c_int, C.c_int, pf, pu, C.c_long, C.c_long, pf, C.c_long,
+                                              C.c_int, C.c_int, C.c_int, pu, pf, pi]
         _o = o
     return _o
 
@@ -192,6 +196,33 @@ class OracleFlatBQ(OracleFlat):
                                      allow_bm.ctypes.data_as(pb) if allow_bm is not None else None, allow_empty,
                                      ids.ctypes.data_as(pu), f(dd), C.byref(n))
         return rc, ids[: n.value].copy(), dd[: n.value].copy()
+
+
+def cpu_baseline_bq(metric: int, variant: int, store: np.ndarray, codes: np.ndarray, queries: np.ndarray, k: int,
+                    rescore_limit: int, nthreads: int, use_ref: bool):
+    """Multi-threaded CPU BQ flat search (oracle/baseline.c): hamming R-heap over
+    the codes, pop, fp32 rescoring, k-heap.  store/queries normalised for cosine."""
+    o = lib()
+    if use_ref:
+        r = ref_lib()
+        if r is None:
+            raise RuntimeError("oracle/_ref/libref.so not built")
+        o.bl_set_ref_kernels(C.cast(r.l2_256, C.c_void_p), C.cast(r.l2_512, C.c_void_p),
+                             C.cast(r.dot_256, C.c_void_p), C.cast(r.dot_512, C.c_void_p))
+        o.bl_set_ref_hamming(C.cast(r.hamming_bitwise_256, C.c_void_p))
+    store = np.ascontiguousarray(store, dtype=np.float32)
+    codes = np.ascontiguousarray(codes, dtype=np.uint64)
+    queries = np.ascontiguousarray(queries, dtype=np.float32)
+    nq = queries.shape[0]
+    ids = np.zeros((nq, k), dtype=np.uint64)
+    dd = np.zeros((nq, k), dtype=np.float32)
+    cnt = np.zeros(nq, dtype=np.int32)
+    rc = o.bl_flat_search_bq_batch(metric, variant, 1 if use_ref else 0, f(store), codes.ctypes.data_as(pu),
+                                   store.shape[0], store.shape[1], f(queries), nq, k, rescore_limit, nthreads,
+                                   ids.ctypes.data_as(pu), f(dd), cnt.ctypes.data_as(pi))
+    if rc != 0:
+        raise RuntimeError("baseline failed")
+    return ids, dd, cnt
 
 
 def gen_matrix(kind: int, seed: int, row0: int, rows: int, d: int) -> np.ndarray:

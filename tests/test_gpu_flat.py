@@ -232,6 +232,8 @@ def build_bq_pair(wv, oracle, metric_name, variant, data, rescore_limit, ids=Non
     ("cosine", 1, 3000, 64, 10, 50),       # all-positive data: every code is 0, hamming ties everywhere
     ("l2-squared", 2, 2500, 200, 20, 20),  # rescore == k
     ("cosine", 0, 600, 65, 10, 1000),      # rescore limit > corpus
+    ("l2-squared", 0, 1500, 2500, 10, 30),  # 40 words: generic (non-LDS) kernels
+    ("cosine", 0, 9000, 1000, 10, 64),     # 16 words
 ])
 def test_bq_search_matches_oracle(wv, oracle, metric, kind, n, d, k, rescore):
     data = gen(oracle, kind, 11, n, d)
@@ -274,4 +276,17 @@ def test_bq_errors(wv, oracle):
         idx.search_by_vector(np.zeros(200, np.float32), 5)
     with pytest.raises(wv.WeaviateError, match="vector lengths don't match"):
         idx.search_by_vector(np.zeros(100, np.float32), 5)  # same word count, rescoring length check
+    idx.close()
+
+
+def test_bq_generic_kernels_equal_lds_kernels(wv, oracle):
+    data = gen(oracle, 0, 51, 6000, 512)
+    queries = gen(oracle, 0, 52, 300, 512)
+    idx = wv.FlatIndex(distance="cosine", bq=True, rescore_limit=40)
+    idx.add_batch(np.arange(6000, dtype=np.uint64), data)
+    a = idx.search_by_vector_batch(queries, 10)
+    idx.set_option("bq_kernel", 1)
+    b = idx.search_by_vector_batch(queries, 10)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
     idx.close()

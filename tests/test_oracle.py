@@ -166,3 +166,22 @@ def test_generator_is_counter_based(oracle):
     assert a.min() >= -1 and a.max() < 1
     ints = oracle.gen_matrix(1, 5, 0, 100, 8)
     assert np.all(ints == np.round(ints)) and ints.max() <= 127
+
+
+def test_bq_baseline_matches_oracle_bq(oracle):
+    """The threaded BQ CPU baseline (bench cpu_baseline leg) = the BQ oracle,
+    with the reference's own hamming_bitwise_256 / dot kernels when built."""
+    n, d, k, R = 1500, 130, 10, 40
+    data = oracle.gen_matrix(0, 41, 0, n, d)
+    queries = oracle.gen_matrix(0, 42, 0, 6, d)
+    orc = oracle.OracleFlatBQ(oracle.COSINE, oracle.AVX256, d, n, R)
+    orc.add_batch(np.arange(n), data)
+    qn = np.stack([oracle.normalize(q) for q in queries])
+    uses = [False] + ([True] if oracle.ref_lib() is not None and oracle.host_has_avx512() else [])
+    for use_ref in uses:
+        ids, dd, cnt = oracle.cpu_baseline_bq(oracle.COSINE, oracle.AVX256, orc.store, orc.codes, qn, k, R, 3, use_ref)
+        for q in range(len(queries)):
+            rc, oi, od = orc.search(queries[q], k)
+            assert rc == 0
+            np.testing.assert_array_equal(ids[q, :cnt[q]], oi)
+            np.testing.assert_array_equal(dd[q, :cnt[q]].view(np.uint32), od.view(np.uint32))

@@ -94,10 +94,80 @@ __global__ __launch_bounds__(256) void k_bq_blockmin(const uint64_t* __restrict_
     }
 }
 
+// Block minima, LDS-broadcast form (words <= NW <= 32).  Block = 256 queries
+// (lane = query, its NW-word code in VGPRs) x a span of 256-row tiles.  Each
+// tile is staged once into LDS row-major ([row][NW] u64, zero padded) from the
+// word-major store (2 KiB coalesced per word), then every wave walks the 256
+// rows reading each row with uniform-address ds_read_b128 (broadcast, no bank
+// conflicts) against its 64 query codes in registers: per row and word
+// 2 x v_xor_b32 + 2 x v_bcnt_u32_b32, the running minimum per lane, and one
+// store per (query, tile).
+template <int NW>
+__global__ __launch_bounds__(256, 2) void k_bq_blockmin_lds(const uint64_t* __restrict__ codes, int64_t ccap,
+                                                            int words, const uint32_t* __restrict__ valid,
+                                                            int64_t nslots, const uint64_t* __restrict__ qcodes,
+                                                            int64_t ldq, const int32_t* __restrict__ qlist, int nlist,
+                                                            int64_t nblk, int64_t blk_per_span,
+                                                            float* __restrict__ bmin) {
+    __shared__ __attribute__((aligned(16))) uint64_t tile[BQBLK * NW];
+    __shared__ uint32_t vb[BQBLK / 32];
+    const int t = threadIdx.x;
+    const int f = blockIdx.y * 256 + t;
+    const bool fq = f < nlist;
+    uint32_t qlo[NW], qhi[NW];
+    {
+        const int qr = qlist[fq ? f : nlist - 1];
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const uint64_t v = w < words ? qcodes[(int64_t)w * ldq + qr] : 0ull;
+            qlo[w] = (uint32_t)v;
+            qhi[w] = (uint32_t)(v >> 32);
+        }
+    }
+    const int64_t b0 = (int64_t)blockIdx.x * blk_per_span;
+    int64_t b1 = b0 + blk_per_span;
+    if (b1 > nblk) b1 = nblk;
+    for (int64_t blk = b0; blk < b1; blk++) {
+        const int64_t s = blk * BQBLK + t;
+        __syncthreads();  // previous tile consumed
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+            tile[t * NW + w] = (w < words && s < nslots) ? codes[(int64_t)w * ccap + s] : 0ull;
+        if (t < BQBLK / 32) {
+            const int64_t wi = blk * (BQBLK / 32) + t;
+            vb[t] = (wi * 32 < nslots) ? valid[wi] : 0u;
+        }
+        __syncthreads();
+        uint32_t mn = 0xFFFFFFFFu;
+        for (int r0 = 0; r0 < BQBLK; r0 += 32) {
+            const uint32_t vbits = vb[r0 >> 5];
+            if (vbits == 0) continue;
+#pragma unroll 2
+            for (int r = 0; r < 32; r++) {
+                const uint4* rp = reinterpret_cast<const uint4*>(&tile[(r0 + r) * NW]);
+                uint32_t acc = 0;
+#pragma unroll
+                for (int c = 0; c < NW / 2; c++) {
+                    const uint4 v = rp[c];
+                    acc += __builtin_popcount(qlo[2 * c] ^ v.x);
+                    acc += __builtin_popcount(qhi[2 * c] ^ v.y);
+                    acc += __builtin_popcount(qlo[2 * c + 1] ^ v.z);
+                    acc += __builtin_popcount(qhi[2 * c + 1] ^ v.w);
+                }
+                if ((vbits >> r) & 1u) mn = min(mn, acc);
+            }
+        }
+        if (fq) bmin[(int64_t)f * nblk + blk] = mn == 0xFFFFFFFFu ? __builtin_inff() : (float)mn;
+    }
+}
+
 // Exact replay of the R-heap of searchByVectorQuantized (one wave per listed
 // query), then the max-first pop of the whole heap (flat/index.go:485-487).
 // out_slot[li * R + i] = slot of the i-th popped item, out_n[li] = heap length.
+// A visited block's 256 distances are recomputed with all loads issued up
+// front (NW > 0: words <= NW known at compile time; NW == 0: generic loop).
 // Dynamic LDS: [R] u64 ids | [64] f32 | [R] f32 dists | len.
+template <int NW>
 __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ codes, int64_t ccap, int words,
                                                   const uint32_t* __restrict__ valid, int64_t nslots,
                                                   const uint64_t* __restrict__ qcodes, int64_t ldq,
@@ -129,26 +199,54 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
             top = len > 0 ? hd[0] : 0.f;
             if (!(len < R || top > bmj)) continue;
             const int64_t r0 = (b0 + j) * BQBLK;
-            for (int sub = 0; sub < BQBLK; sub += 64) {
-                const int64_t s = r0 + sub + lane;
-                const bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
-                uint32_t h = 0;
-                if (ok)
-                    for (int w = 0; w < words; w++) h += (uint32_t)__popcll(codes[(int64_t)w * ccap + s] ^ qc[(int64_t)w * ldq]);
-                const float dist = (float)h;
+            float dist[BQBLK / 64];
+            bool okv[BQBLK / 64];
+#pragma unroll
+            for (int sub = 0; sub < BQBLK / 64; sub++) {
+                const int64_t s = r0 + sub * 64 + lane;
+                okv[sub] = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
+            }
+            if (NW > 0) {
+                uint64_t x[BQBLK / 64][NW > 0 ? NW : 1];
+#pragma unroll
+                for (int sub = 0; sub < BQBLK / 64; sub++)
+#pragma unroll
+                    for (int w = 0; w < (NW > 0 ? NW : 1); w++)
+                        x[sub][w] = (okv[sub] && w < words) ? codes[(int64_t)w * ccap + r0 + sub * 64 + lane] : 0ull;
+#pragma unroll
+                for (int sub = 0; sub < BQBLK / 64; sub++) {
+                    uint32_t h = 0;
+#pragma unroll
+                    for (int w = 0; w < (NW > 0 ? NW : 1); w++)
+                        h += (uint32_t)__popcll(x[sub][w] ^ (w < words ? qc[(int64_t)w * ldq] : 0ull));
+                    dist[sub] = (float)h;
+                }
+            } else {
+#pragma unroll
+                for (int sub = 0; sub < BQBLK / 64; sub++) {
+                    uint32_t h = 0;
+                    if (okv[sub])
+                        for (int w = 0; w < words; w++)
+                            h += (uint32_t)__popcll(codes[(int64_t)w * ccap + r0 + sub * 64 + lane] ^ qc[(int64_t)w * ldq]);
+                    dist[sub] = (float)h;
+                }
+            }
+#pragma unroll
+            for (int sub = 0; sub < BQBLK / 64; sub++) {
                 len = *s_len;
                 top = len > 0 ? hd[0] : 0.f;
-                uint64_t mask = __ballot(ok && (len < R || top > dist));
+                uint64_t mask = __ballot(okv[sub] && (len < R || top > dist[sub]));
                 if (mask == 0) continue;
-                s_d[lane] = dist;
+                s_d[lane] = dist[sub];
                 __syncthreads();
                 if (lane == 0) {
                     ReplayHeap hp{hid, hd, *s_len};
+                    const int64_t sb = r0 + sub * 64;
                     while (mask) {
                         const int jj = __builtin_ctzll(mask);
                         mask &= mask - 1;
                         const float dj = s_d[jj];
-                        const uint64_t sj = (uint64_t)(s - lane + jj);
+                        const uint64_t sj = (uint64_t)(sb + jj);
                         if (hp.len < R) rh_insert(hp, sj, dj);
                         else if (hp.dist[0] > dj) { uint64_t a; float b; rh_pop(hp, &a, &b); rh_insert(hp, sj, dj); }
                     }

@@ -125,7 +125,7 @@ struct wv_index {
 
     DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident;
 
-    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3;
+    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     wv_stats stats{};
 };
@@ -433,6 +433,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "timing") idx->timing = (int)value;
     else if (k == "cbuf") idx->cbuf_opt = (int)value;
     else if (k == "kernel") idx->kernel_opt = (int)value;
+    else if (k == "bq_kernel") idx->bq_kernel = (int)value;
     else return set_err(WV_ERR_INVALID, "unknown option %s", key);
     return WV_OK;
 }
@@ -555,23 +556,64 @@ static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     HIPCHK(idx->cslot.ensure((size_t)nq * R * sizeof(uint32_t)));
     HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
     HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
-    if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
     const size_t lds_r = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
-    if (lds_r > 64 * 1024)
-        HIPCHK(hipFuncSetAttribute((const void*)k_bq_replay, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_r));
+    // compile-time word count for the LDS-broadcast block-minima kernel and
+    // the replay's unrolled loads (words <= 32, i.e. d <= 2048); else generic
+    const int nw = words <= 2 ? 2 : words <= 4 ? 4 : words <= 8 ? 8 : words <= 12 ? 12 : words <= 16 ? 16
+                 : words <= 24 ? 24 : words <= 32 ? 32 : 0;
+    const bool generic = nw == 0 || idx->bq_kernel == 1;
     for (int64_t g0 = 0; g0 < nq; g0 += G) {
         const int F = (int)std::min<int64_t>(G, nq - g0);
-        dim3 grid((unsigned)nblk, (unsigned)((F + QPB - 1) / QPB));
-        k_bq_blockmin<QPB><<<grid, 256, 0, s>>>(idx->codes, idx->cap, words, valid, nslots, idx->qcodes.as<uint64_t>(),
-                                                nq, qlist + g0, F, nblk, idx->bqmin.as<float>());
+        // timing (bench roofline): the block-minima pass of the first group
+        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
+        const uint64_t* qc = idx->qcodes.as<uint64_t>();
+        float* bm = idx->bqmin.as<float>();
+        if (generic) {
+            dim3 grid((unsigned)nblk, (unsigned)((F + QPB - 1) / QPB));
+            k_bq_blockmin<QPB><<<grid, 256, 0, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq, qlist + g0, F,
+                                                    nblk, bm);
+        } else {
+            const int64_t qg = (F + 255) / 256;
+            const int64_t spans = std::max<int64_t>(1, std::min<int64_t>(nblk, (2048 + qg - 1) / qg));
+            const int64_t bps = (nblk + spans - 1) / spans;
+            dim3 grid((unsigned)((nblk + bps - 1) / bps), (unsigned)qg);
+#define WV_BM(NWV) k_bq_blockmin_lds<NWV><<<grid, 256, 0, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq, qlist + g0, F, nblk, bps, bm)
+            switch (nw) {
+            case 2: WV_BM(2); break;
+            case 4: WV_BM(4); break;
+            case 8: WV_BM(8); break;
+            case 12: WV_BM(12); break;
+            case 16: WV_BM(16); break;
+            case 24: WV_BM(24); break;
+            default: WV_BM(32); break;
+            }
+#undef WV_BM
+        }
         HIPCHK(hipGetLastError());
-        k_bq_replay<<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots,
-                                                  idx->qcodes.as<uint64_t>(), nq, qlist + g0, F,
-                                                  idx->bqmin.as<float>(), nblk, R,
-                                                  idx->cslot.as<uint32_t>() + g0 * R, idx->cn.as<int32_t>() + g0);
+        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
+#define WV_RP(NWV)                                                                                              \
+    do {                                                                                                        \
+        if (lds_r > 64 * 1024)                                                                                  \
+            HIPCHK(hipFuncSetAttribute((const void*)k_bq_replay<NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                       (int)lds_r));                                                            \
+        k_bq_replay<NWV><<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq,      \
+                                                        qlist + g0, F, bm, nblk, R,                             \
+                                                        idx->cslot.as<uint32_t>() + g0 * R,                     \
+                                                        idx->cn.as<int32_t>() + g0);                            \
+    } while (0)
+        switch (generic ? 0 : nw) {
+        case 2: WV_RP(2); break;
+        case 4: WV_RP(4); break;
+        case 8: WV_RP(8); break;
+        case 12: WV_RP(12); break;
+        case 16: WV_RP(16); break;
+        case 24: WV_RP(24); break;
+        case 32: WV_RP(32); break;
+        default: WV_RP(0); break;
+        }
+#undef WV_RP
         HIPCHK(hipGetLastError());
     }
-    if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
     const int64_t npairs = nq * R;
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
 #define WV_RS(M, V) k_rescore<M, V><<<(unsigned)((npairs + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, Qn, idx->dims, idx->cslot.as<uint32_t>(), (int)nq, R, idx->candE.as<float>())
