@@ -43,6 +43,9 @@ extern "C" {
 /* compression: flatent.UserConfig (entities/vectorindex/flat/config.go:43-82) */
 #define WV_COMPRESSION_NONE 0
 #define WV_COMPRESSION_BQ 1
+/* PQ: ProductQuantizer (compressionhelpers/product_quantization.go) with the
+ * KMeans encoder; searched like hnsw.flatSearch (hnsw/flat_search.go:28-141) */
+#define WV_COMPRESSION_PQ 2
 
 /* which reference SIMD kernel's fp32 accumulation order to reproduce
  * (distancer/l2_amd64.go:19-26: AVX-512 only if AMX-BF16 && AVX512) */
@@ -62,6 +65,11 @@ typedef struct wv_config {
     int32_t variant;         /* WV_VARIANT_*                                          */
     uint64_t id_base;        /* first doc id of this shard: slot = id - id_base       */
     const char *root_path;   /* only used in error texts (flat/index.go:837)          */
+    /* PQ only (ent.PQConfig, entities/vectorindex/hnsw/pq_config.go) */
+    int32_t pq_segments;     /* m: must divide dims                                   */
+    int32_t pq_centroids;    /* ks <= 256                                             */
+    int32_t pq_training_limit; /* rows used by Fit (<= 0: all)                        */
+    int32_t pq_rescore;      /* 1: rescore the limit candidates with fp32 (h.rescore) */
 } wv_config;
 
 const char *wv_last_error(void);
@@ -103,6 +111,25 @@ int wv_index_search_by_vector_distance(wv_index *idx, const float *query, int64_
                                        int64_t max_limit, const uint64_t *allow_ids, int64_t n_allow,
                                        int32_t allow_mode, uint64_t *out_ids, float *out_dists,
                                        int32_t *out_count);
+
+/* ProductQuantizer.Fit (product_quantization.go:378-424) on the stored rows
+ * (the first pq_training_limit present rows in id order), one KMeansEncoder per
+ * segment (kmeans_encoder.go:48-65: random init, graph pruning, 10 iterations,
+ * delta 0.01) with PCG seed `seed + segment` (the reference seeds from
+ * rand.Uint64()); then Encode of every stored row.  Later Adds are encoded. */
+int wv_index_pq_fit(wv_index *idx, uint64_t seed);
+/* NewProductQuantizerWithEncoders (:193-203): install centers [m][ks][ds], encode rows */
+int wv_index_pq_set_centers(wv_index *idx, const float *centers, int64_t n_floats);
+/* the trained codebook [m][ks][ds] (KMeansEncoder.ExposeDataForRestore order) */
+int wv_index_pq_centers(wv_index *idx, float *out, int64_t n_floats);
+/* codes of slots [0, n) as [n][m] bytes (ProductQuantizer.Encode of the stored rows) */
+int wv_index_pq_codes(wv_index *idx, uint8_t *out, int64_t n);
+/* out[4] = {m, ks, ds, trained} */
+int wv_index_pq_info(wv_index *idx, int32_t *out);
+/* PQDistancer.Distance (product_quantization.go:360-368) of `query` (as given)
+ * against n codes [n][m]: LUT (DistanceLookUpTable) sums + Wrap */
+int wv_index_pq_distance(wv_index *idx, const float *query, int64_t d, const uint8_t *codes, int64_t n,
+                         float *out);
 
 /* Device-resident batch search for sharded / benchmark callers.
  * mode 0: like SearchByVector (kout = k, tie cases resolved by heap replay).

@@ -49,6 +49,18 @@ int or_flat_search_bq(int metric, int variant, const float *store, const uint8_t
 int or_filter_by_distance(const uint64_t *ids, const float *dists, int n, float target,
                           uint64_t *out_ids, float *out_dists);
 
+/* pq.c: product quantizer (see its header) */
+void or_pcg_stream(uint64_t s1, uint64_t s2, int cnt, uint64_t *out);
+void or_random_subset(uint64_t seed, long n, int k, long *out);
+int or_kmeans_fit(const float *data, long n, long d, int seg, int ds, int k, uint64_t seed, int variant,
+                  int iteration_threshold, float delta_threshold, int brute_force, float *centers);
+void or_pq_encode(const float *centers, int m, int k, int ds, int variant, const float *vec, uint8_t *code);
+void or_pq_lut(int metric, const float *centers, int m, int k, int ds, const float *query, float *lut);
+float or_pq_adc(int metric, const float *lut, int m, int k, const uint8_t *code);
+int or_pq_flat_search(int metric, int variant, const float *centers, int m, int ks, int ds, const uint8_t *codes,
+                      const float *store, const uint8_t *present, long nslots, const float *query, int k, int limit,
+                      int rescore, uint64_t *out_ids, float *out_dists, int *out_n);
+
 uint64_t or_gen_bits(uint64_t seed, uint64_t row, uint64_t col);
 float or_gen_value(int kind, uint64_t seed, uint64_t row, uint64_t col);
 void or_gen_matrix(int kind, uint64_t seed, uint64_t row0, long rows, long d, float *out);

@@ -61,6 +61,19 @@ def lib() -> C.CDLL:
         o.bl_flat_search_batch.restype = C.c_int
         o.bl_flat_search_batch.argtypes = [C.c_int, C.c_int, C.c_int, pf, C.c_long, C.c_long, pf, C.c_long, C.c_int,
                                            C.c_int, pu, pf, pi]
+        pl = C.POINTER(C.c_long)
+        o.or_pcg_stream.argtypes = [C.c_uint64, C.c_uint64, C.c_int, pu]
+        o.or_random_subset.argtypes = [C.c_uint64, C.c_long, C.c_int, pl]
+        o.or_kmeans_fit.restype = C.c_int
+        o.or_kmeans_fit.argtypes = [pf, C.c_long, C.c_long, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
+                                    C.c_float, C.c_int, pf]
+        o.or_pq_encode.argtypes = [pf, C.c_int, C.c_int, C.c_int, C.c_int, pf, pb]
+        o.or_pq_lut.argtypes = [C.c_int, pf, C.c_int, C.c_int, C.c_int, pf, pf]
+        o.or_pq_adc.restype = C.c_float
+        o.or_pq_adc.argtypes = [C.c_int, pf, C.c_int, C.c_int, pb]
+        o.or_pq_flat_search.restype = C.c_int
+        o.or_pq_flat_search.argtypes = [C.c_int, C.c_int, pf, C.c_int, C.c_int, C.c_int, pb, pf, pb, C.c_long, pf,
+                                        C.c_int, C.c_int, C.c_int, pu, pf, pi]
         o.bl_flat_search_bq_batch.restype = C.c_int
         o.bl_flat_search_bq_batch.argtypes = [C.c_int, C.c_int, C.c_int, pf, pu, C.c_long, C.c_long, pf, C.c_long,
                                               C.c_int, C.c_int, C.c_int, pu, pf, pi]
@@ -223,6 +236,69 @@ def cpu_baseline_bq(metric: int, variant: int, store: np.ndarray, codes: np.ndar
     if rc != 0:
         raise RuntimeError("baseline failed")
     return ids, dd, cnt
+
+
+# ---- product quantizer (oracle/pq.c) ----
+def pcg_stream(s1: int, s2: int, cnt: int) -> np.ndarray:
+    out = np.zeros(cnt, dtype=np.uint64)
+    lib().or_pcg_stream(s1, s2, cnt, out.ctypes.data_as(pu))
+    return out
+
+
+def random_subset(seed: int, n: int, k: int) -> np.ndarray:
+    out = np.zeros(k, dtype=np.int64)
+    lib().or_random_subset(seed, n, k, out.ctypes.data_as(C.POINTER(C.c_long)))
+    return out
+
+
+def pq_fit(data: np.ndarray, m: int, ks: int, seed: int, variant: int = AVX256, iterations: int = 10,
+           delta: float = 0.01, brute_force: bool = False) -> np.ndarray:
+    """ProductQuantizer.Fit with the KMeans encoder; segment s seeded seed+s.
+    Returns centers [m][ks][ds]."""
+    data = np.ascontiguousarray(data, dtype=np.float32)
+    n, d = data.shape
+    ds = d // m
+    out = np.zeros((m, ks, ds), dtype=np.float32)
+    for s in range(m):
+        rc = lib().or_kmeans_fit(f(data), n, d, s, ds, ks, (seed + s) & (2**64 - 1), variant, iterations, delta,
+                                 1 if brute_force else 0, f(out[s]))
+        if rc < 0:
+            raise ValueError("not enough data to fit k-means")
+    return out
+
+
+def pq_encode(centers: np.ndarray, vec: np.ndarray, variant: int = AVX256) -> np.ndarray:
+    m, ks, ds = centers.shape
+    c = np.ascontiguousarray(centers, dtype=np.float32)
+    v = np.ascontiguousarray(vec, dtype=np.float32)
+    out = np.zeros(m, dtype=np.uint8)
+    lib().or_pq_encode(f(c), m, ks, ds, variant, f(v), out.ctypes.data_as(pb))
+    return out
+
+
+def pq_distance(metric: int, centers: np.ndarray, query: np.ndarray, code: np.ndarray) -> float:
+    m, ks, ds = centers.shape
+    c = np.ascontiguousarray(centers, dtype=np.float32)
+    lut = np.zeros((m, ks), dtype=np.float32)
+    lib().or_pq_lut(metric, f(c), m, ks, ds, f(np.ascontiguousarray(query, dtype=np.float32)), f(lut))
+    return lib().or_pq_adc(metric, f(lut), m, ks, np.ascontiguousarray(code, dtype=np.uint8).ctypes.data_as(pb))
+
+
+def pq_flat_search(metric: int, variant: int, centers: np.ndarray, codes: np.ndarray, store: np.ndarray,
+                   present: np.ndarray, query: np.ndarray, k: int, limit: int, rescore: bool):
+    """hnsw.flatSearch (one worker) over PQ codes (+ h.rescore).  query/store
+    normalised already for cosine."""
+    m, ks, ds = centers.shape
+    ids = np.zeros(max(k, limit, 1) + 1, dtype=np.uint64)
+    dd = np.zeros(max(k, limit, 1) + 1, dtype=np.float32)
+    n = C.c_int(0)
+    lib().or_pq_flat_search(metric, variant, f(np.ascontiguousarray(centers, np.float32)), m, ks, ds,
+                            np.ascontiguousarray(codes, np.uint8).ctypes.data_as(pb),
+                            f(np.ascontiguousarray(store, np.float32)),
+                            np.ascontiguousarray(present, np.uint8).ctypes.data_as(pb), len(present),
+                            f(np.ascontiguousarray(query, np.float32)), k, limit, 1 if rescore else 0,
+                            ids.ctypes.data_as(pu), f(dd), C.byref(n))
+    return ids[: n.value].copy(), dd[: n.value].copy()
 
 
 def gen_matrix(kind: int, seed: int, row0: int, rows: int, d: int) -> np.ndarray:

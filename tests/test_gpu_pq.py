@@ -1,0 +1,121 @@
+"""GPU parity of the product quantizer and the PQ brute-force search vs the
+oracle (oracle/pq.c): k-means codebooks, codes, ADC distances and search
+results bit-exact for the same PCG seed.  MI355X only (marker gpu)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = {"avx256": 1, "avx512": 2}
+
+
+def gen(oracle, kind, seed, rows, d):
+    return oracle.gen_matrix(kind, seed, 0, rows, d)
+
+
+def stored_rows(oracle, metric, data):
+    if metric == oracle.COSINE:
+        return np.stack([oracle.normalize(x) for x in data])
+    return data.copy()
+
+
+@pytest.mark.parametrize("metric,kind,n,d,m,ks,limit,variant", [
+    ("l2-squared", 0, 3000, 32, 8, 64, 100000, "avx256"),   # ds = 4 (scalar SingleDist path)
+    ("cosine", 0, 4000, 64, 8, 256, 100000, "avx256"),      # ds = 8 (SIMD path), ks = 256
+    ("dot", 0, 2500, 60, 15, 32, 2000, "avx512"),           # ds = 4, training limit < n
+    ("l2-squared", 1, 2000, 24, 6, 16, 100000, "avx256"),   # integer data: duplicate points / ties
+    ("cosine", 0, 1500, 96, 4, 64, 100000, "avx512"),       # ds = 24
+])
+def test_pq_fit_codes_distance_match_oracle(wv, oracle, metric, kind, n, d, m, ks, limit, variant):
+    data = gen(oracle, kind, 61, n, d)
+    idx = wv.FlatIndex(distance=metric, variant=variant,
+                       pq={"segments": m, "centroids": ks, "trainingLimit": limit, "rescore": True})
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    idx.pq_fit(seed=1234)
+    assert idx.compressed()
+    got = idx.pq_centers()
+    om = oracle.METRIC[metric]
+    store = stored_rows(oracle, om, data)
+    exp = oracle.pq_fit(store[:min(n, limit)], m, ks, seed=1234, variant=VARIANTS[variant])
+    np.testing.assert_array_equal(got.view(np.uint32), exp.view(np.uint32))
+    codes = idx.pq_codes(n)
+    ecodes = np.stack([oracle.pq_encode(exp, x, VARIANTS[variant]) for x in store])
+    np.testing.assert_array_equal(codes, ecodes)
+    q = gen(oracle, kind, 62, 1, d)[0]
+    gd = idx.pq_distance(q, codes[:500])
+    ed = np.array([oracle.pq_distance(om, exp, q, c) for c in codes[:500]], np.float32)
+    np.testing.assert_array_equal(gd.view(np.uint32), ed.view(np.uint32))
+    idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,rescore,k,rl", [
+    ("l2-squared", 0, True, 10, 64),
+    ("cosine", 0, True, 10, 100),
+    ("dot", 0, False, 10, -1),
+    ("l2-squared", 1, True, 7, 40),     # integer data: ADC ties -> heap order
+    ("l2-squared", 1, False, 20, -1),
+])
+def test_pq_search_matches_oracle(wv, oracle, metric, kind, rescore, k, rl):
+    n, d, m, ks = 5000, 32, 8, 32
+    data = gen(oracle, kind, 71, n, d)
+    idx = wv.FlatIndex(distance=metric, variant="avx256", rescore_limit=rl,
+                       pq={"segments": m, "centroids": ks, "rescore": rescore})
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    idx.pq_fit(seed=77)
+    centers = idx.pq_centers()
+    codes = idx.pq_codes(n)
+    om = oracle.METRIC[metric]
+    store = stored_rows(oracle, om, data)
+    present = np.ones(n, np.uint8)
+    queries = gen(oracle, kind, 72, 16, d)
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    for qi in range(len(queries)):
+        qv = oracle.normalize(queries[qi]) if om == oracle.COSINE else queries[qi]
+        oi, od = oracle.pq_flat_search(om, 1, centers, codes, store, present, qv, k, max(rl, k), rescore)
+        np.testing.assert_array_equal(ids[qi, :counts[qi]], oi, err_msg=f"q{qi}")
+        np.testing.assert_array_equal(dists[qi, :counts[qi]].view(np.uint32), od.view(np.uint32), err_msg=f"q{qi}")
+    idx.close()
+
+
+def test_pq_add_after_fit_and_set_centers(wv, oracle):
+    n, d, m, ks = 2000, 16, 4, 16
+    data = gen(oracle, 0, 81, n, d)
+    a = wv.FlatIndex(distance="l2-squared", pq={"segments": m, "centroids": ks})
+    a.add_batch(np.arange(n, dtype=np.uint64), data)
+    a.pq_fit(seed=5)
+    more = gen(oracle, 0, 82, 300, d)
+    a.add_batch(np.arange(n, n + 300, dtype=np.uint64), more)  # encoded on Add
+    c = a.pq_centers()
+    exp = np.stack([oracle.pq_encode(c, x) for x in more])
+    np.testing.assert_array_equal(a.pq_codes(n + 300)[n:], exp)
+    b = wv.FlatIndex(distance="l2-squared", pq={"segments": m, "centroids": ks})
+    b.add_batch(np.arange(n + 300, dtype=np.uint64), np.concatenate([data, more]))
+    b.pq_set_centers(c)  # NewProductQuantizerWithEncoders
+    np.testing.assert_array_equal(b.pq_codes(n + 300), a.pq_codes(n + 300))
+    q = gen(oracle, 0, 83, 4, d)
+    for x, y in zip(a.search_by_vector_batch(q, 10), b.search_by_vector_batch(q, 10)):
+        np.testing.assert_array_equal(x, y)
+    a.close()
+    b.close()
+
+
+def test_pq_errors(wv, oracle):
+    data = gen(oracle, 0, 91, 100, 30)
+    idx = wv.FlatIndex(distance="l2-squared", pq={"segments": 7, "centroids": 16})
+    idx.add_batch(np.arange(100, dtype=np.uint64), data)
+    with pytest.raises(wv.WeaviateError, match="segments should be an integer divisor of dimensions"):
+        idx.pq_fit()
+    idx.close()
+    idx = wv.FlatIndex(distance="l2-squared", pq={"segments": 5, "centroids": 300})
+    idx.add_batch(np.arange(100, dtype=np.uint64), data)
+    with pytest.raises(wv.WeaviateError, match="centroids should not be higher than 256"):
+        idx.pq_fit()
+    idx.close()
+    idx = wv.FlatIndex(distance="l2-squared", pq={"segments": 5, "centroids": 256})
+    idx.add_batch(np.arange(100, dtype=np.uint64), data)
+    with pytest.raises(wv.WeaviateError, match="not enough data to fit k-means"):
+        idx.pq_fit()
+    # before Fit the index searches uncompressed
+    ids, _ = idx.search_by_vector(data[3], 1)
+    assert ids[0] == 3
+    idx.close()

@@ -30,6 +30,7 @@ VARIANT_AVX512 = 2
 
 COMPRESSION_NONE = 0
 COMPRESSION_BQ = 1
+COMPRESSION_PQ = 2
 
 
 class WvConfig(C.Structure):
@@ -42,6 +43,10 @@ class WvConfig(C.Structure):
         ("variant", C.c_int32),
         ("id_base", C.c_uint64),
         ("root_path", C.c_char_p),
+        ("pq_segments", C.c_int32),
+        ("pq_centroids", C.c_int32),
+        ("pq_training_limit", C.c_int32),
+        ("pq_rescore", C.c_int32),
     ]
 
 
@@ -88,6 +93,12 @@ SIGNATURES = {
     "wv_normalize_batch": (C.c_int, [i32, pf32, i64, i64, pf32]),
     "wv_gen_device": (C.c_int, [i32, i32, u64, u64, i64, i64, P, P]),
     "wv_index_stats": (C.c_int, [P, C.POINTER(WvStats)]),
+    "wv_index_pq_fit": (C.c_int, [P, u64]),
+    "wv_index_pq_set_centers": (C.c_int, [P, pf32, i64]),
+    "wv_index_pq_centers": (C.c_int, [P, pf32, i64]),
+    "wv_index_pq_codes": (C.c_int, [P, C.POINTER(C.c_uint8), i64]),
+    "wv_index_pq_info": (C.c_int, [P, pi32]),
+    "wv_index_pq_distance": (C.c_int, [P, pf32, i64, C.POINTER(C.c_uint8), i64, pf32]),
     "wv_index_set_option": (C.c_int, [P, C.c_char_p, i64]),
 }
 

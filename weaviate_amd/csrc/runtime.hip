@@ -24,6 +24,7 @@
 #include "../../include/wv_knn.h"
 #include "kernels.hip"
 #include "bq_kernels.hip"
+#include "pq_kernels.hip"
 
 using namespace wv;
 
@@ -119,11 +120,16 @@ struct wv_index {
     uint32_t* d_maxn2 = nullptr;
     uint64_t* codes = nullptr;   // BQ: [words][cap] word-major codes of the stored rows
     int words = 0;
+    // PQ (compressionhelpers.ProductQuantizer): codebook [m][ks][ds], codes
+    // [ceil(m/4)][cap] u32 (4 segment bytes per word, see pq_kernels.hip)
+    int pq_m = 0, pq_ks = 0, pq_ds = 0, pq_training_limit = 0, pq_rescore = 1, pq_trained = 0;
+    float* pq_centers = nullptr;
+    uint32_t* pq_codes = nullptr;
     std::vector<uint8_t> h_present;
     uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
     int64_t npresent = 0;
 
-    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident;
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN;
 
     int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -137,7 +143,8 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     if (!cfg || !out) return set_err(WV_ERR_INVALID, "invalid config: nil");
     if (cfg->metric < 0 || cfg->metric > WV_METRIC_HAMMING)
         return set_err(WV_ERR_INVALID, "invalid config: unknown distance metric %d", cfg->metric);
-    if (cfg->compression != WV_COMPRESSION_NONE && cfg->compression != WV_COMPRESSION_BQ)
+    if (cfg->compression != WV_COMPRESSION_NONE && cfg->compression != WV_COMPRESSION_BQ &&
+        cfg->compression != WV_COMPRESSION_PQ)
         return set_err(WV_ERR_UNSUPPORTED, "invalid config: unsupported compression %d", cfg->compression);
     HIPCHK(hipSetDevice(cfg->device));
     wv_index* idx = new wv_index();
@@ -148,6 +155,12 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     idx->device = cfg->device;
     idx->id_base = cfg->id_base;
     idx->root_path = cfg->root_path ? cfg->root_path : "";
+    if (cfg->compression == WV_COMPRESSION_PQ) {
+        idx->pq_m = cfg->pq_segments;
+        idx->pq_ks = cfg->pq_centroids;
+        idx->pq_training_limit = cfg->pq_training_limit;
+        idx->pq_rescore = cfg->pq_rescore;
+    }
     if (cfg->dims > 0) { idx->dims = cfg->dims; idx->dpad = (int)round_up(cfg->dims, BK); }
     hipError_t e = hipStreamCreateWithFlags(&idx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&idx->d_maxn2, sizeof(uint32_t));
@@ -169,13 +182,15 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
-                    &idx->cn, &idx->ident})
+                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN})
         b->release();
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
     if (idx->present) hipFree(idx->present);
     if (idx->d_maxn2) hipFree(idx->d_maxn2);
     if (idx->codes) hipFree(idx->codes);
+    if (idx->pq_centers) hipFree(idx->pq_centers);
+    if (idx->pq_codes) hipFree(idx->pq_codes);
     if (idx->ev0) hipEventDestroy(idx->ev0);
     if (idx->ev1) hipEventDestroy(idx->ev1);
     if (idx->stream) hipStreamDestroy(idx->stream);
@@ -221,6 +236,18 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         idx->codes = cd;
         idx->words = words;
     }
+    if (idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0) {
+        const int pw = (idx->pq_m + 3) / 4;
+        uint32_t* pc = nullptr;
+        HIPCHK(hipMalloc(&pc, (size_t)pw * nc * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(pc, 0, (size_t)pw * nc * sizeof(uint32_t), idx->stream));
+        if (idx->cap > 0 && idx->pq_codes)
+            HIPCHK(hipMemcpy2DAsync(pc, (size_t)nc * sizeof(uint32_t), idx->pq_codes, (size_t)idx->cap * sizeof(uint32_t),
+                                    (size_t)idx->cap * sizeof(uint32_t), pw, hipMemcpyDeviceToDevice, idx->stream));
+        HIPCHK(hipStreamSynchronize(idx->stream));
+        if (idx->pq_codes) hipFree(idx->pq_codes);
+        idx->pq_codes = pc;
+    }
     idx->X = X;
     idx->xnorm2 = xn;
     idx->present = pr;
@@ -257,6 +284,15 @@ extern "C" int wv_index_validate_before_insert(wv_index* idx, int64_t d) {
     return validate_insert(idx, d);
 }
 
+// ProductQuantizer.Encode of stored rows (slots list, or slots [0, n))
+static void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots) {
+    if (n <= 0) return;
+    const size_t lds = (size_t)idx->pq_ks * idx->pq_ds * sizeof(float);
+    dim3 grid((unsigned)((n + 255) / 256), (unsigned)idx->pq_m);
+    k_pq_encode<<<grid, 256, lds, idx->stream>>>(idx->X, idx->dpad, n, d_slots, idx->pq_ks, idx->pq_ds,
+                                                 idx->pq_centers, idx->variant, idx->pq_codes, idx->cap);
+}
+
 static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const uint32_t* d_slots) {
     dim3 grid((unsigned)((n + 255) / 256));
     switch (idx->metric) {
@@ -269,6 +305,7 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
                                                           idx->present, idx->d_maxn2);
         break;
     }
+    if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) launch_pq_encode(idx, n, d_slots);
     if (idx->compression == WV_COMPRESSION_BQ) {  // Preload: quantizer.Encode of the stored row (flat/index.go:376)
         const int64_t nt = n * idx->words;
         k_bq_encode_rows<<<(unsigned)((nt + 255) / 256), 256, 0, idx->stream>>>(idx->X, idx->dpad, n, idx->dims, d_slots,
@@ -640,6 +677,402 @@ static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     return WV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// product quantizer
+// ---------------------------------------------------------------------------
+
+// Go math/rand/v2 PCG-DXSM + Rand.IntN / Float64 / Shuffle (the Go standard
+// library's published algorithm), as kmeans.temporaryData.init seeds it:
+// rand.New(rand.NewPCG(seed, 0x385ab5285169b1ac)) (kmeans/kmeans.go:50).
+struct GoPCG {
+    uint64_t hi, lo;
+    uint64_t next_u64() {
+        const uint64_t mulHi = 2549297995355413924ULL, mulLo = 4865540595714422341ULL;
+        const uint64_t incHi = 6364136223846793005ULL, incLo = 1442695040888963407ULL;
+        __uint128_t m = (__uint128_t)lo * mulLo;
+        uint64_t h = (uint64_t)(m >> 64), l = (uint64_t)m;
+        h += hi * mulLo + lo * mulHi;
+        __uint128_t sum = (__uint128_t)l + incLo;
+        l = (uint64_t)sum;
+        h = h + incHi + (uint64_t)(sum >> 64);
+        lo = l;
+        hi = h;
+        const uint64_t cheapMul = 0xda942042e4dd58b5ULL;  // DXSM output
+        h ^= h >> 32;
+        h *= cheapMul;
+        h ^= h >> 48;
+        h *= (l | 1);
+        return h;
+    }
+    uint64_t u64n(uint64_t n) {
+        if ((n & (n - 1)) == 0) return next_u64() & (n - 1);
+        __uint128_t m = (__uint128_t)next_u64() * n;
+        uint64_t h = (uint64_t)(m >> 64), l = (uint64_t)m;
+        if (l < n) {
+            const uint64_t thresh = (0 - n) % n;
+            while (l < thresh) {
+                m = (__uint128_t)next_u64() * n;
+                h = (uint64_t)(m >> 64);
+                l = (uint64_t)m;
+            }
+        }
+        return h;
+    }
+    double f64() { return (double)((next_u64() << 11) >> 11) / 9007199254740992.0; }
+};
+
+// kmeans.randomSubset (kmeans/kmeans.go:238-274)
+static std::vector<int64_t> random_subset(GoPCG& r, int64_t n, int k) {
+    std::vector<int64_t> out((size_t)k);
+    if (k > n / 2) {  // r.Perm(n)[:k]
+        std::vector<int64_t> p((size_t)n);
+        for (int64_t i = 0; i < n; i++) p[i] = i;
+        for (int64_t i = n - 1; i > 0; i--) std::swap(p[i], p[(size_t)r.u64n((uint64_t)(i + 1))]);
+        std::copy(p.begin(), p.begin() + k, out.begin());
+        return out;
+    }
+    std::unordered_map<int64_t, double> rank;
+    std::vector<int64_t> keys;
+    while ((int)rank.size() < k) {  // m[r.IntN(n)] = r.Float64()
+        const int64_t i = (int64_t)r.u64n((uint64_t)n);
+        const double v = r.f64();
+        if (!rank.count(i)) keys.push_back(i);
+        rank[i] = v;
+    }
+    std::stable_sort(keys.begin(), keys.end(), [&](int64_t a, int64_t b) { return rank[a] < rank[b]; });
+    std::copy(keys.begin(), keys.end(), out.begin());
+    return out;
+}
+
+// NewProductQuantizer validation (product_quantization.go:206-239)
+static int pq_validate(wv_index* idx) {
+    if (idx->pq_m <= 0) return set_err(WV_ERR_INVALID, "segments cannot be 0 nor negative");
+    if (idx->pq_ks > 256)
+        return set_err(WV_ERR_INVALID, "centroids should not be higher than 256. Attempting to use %d", idx->pq_ks);
+    if (idx->pq_ks <= 0) return set_err(WV_ERR_INVALID, "centroids must be positive");
+    if (idx->dims == 0) return set_err(WV_ERR_INVALID, "pq: dimensions not set yet");
+    if (idx->dims % idx->pq_m != 0) return set_err(WV_ERR_INVALID, "segments should be an integer divisor of dimensions");
+    idx->pq_ds = idx->dims / idx->pq_m;
+    if (idx->pq_ds > 32) return set_err(WV_ERR_UNSUPPORTED, "pq: segment length %d > 32", idx->pq_ds);
+    return WV_OK;
+}
+
+static int pq_alloc(wv_index* idx) {
+    if (!idx->pq_centers)
+        HIPCHK(hipMalloc(&idx->pq_centers, (size_t)idx->pq_m * idx->pq_ks * idx->pq_ds * sizeof(float)));
+    if (!idx->pq_codes && idx->cap > 0) {
+        const int pw = (idx->pq_m + 3) / 4;
+        HIPCHK(hipMalloc(&idx->pq_codes, (size_t)pw * idx->cap * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(idx->pq_codes, 0, (size_t)pw * idx->cap * sizeof(uint32_t), idx->stream));
+    }
+    return WV_OK;
+}
+
+static int pq_encode_all(wv_index* idx) {
+    launch_pq_encode(idx, idx->hiwater, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    idx->pq_trained = 1;
+    return WV_OK;
+}
+
+extern "C" int wv_index_pq_fit(wv_index* idx, uint64_t seed) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->compression != WV_COMPRESSION_PQ) return set_err(WV_ERR_INVALID, "pq_fit: index is not PQ-compressed");
+    int rc = pq_validate(idx);
+    if (rc) return rc;
+    const int m = idx->pq_m, K = idx->pq_ks, ds = idx->pq_ds;
+    hipStream_t s = idx->stream;
+    // training data: ProductQuantizer.Fit truncates to trainingLimit (:379-381)
+    std::vector<uint32_t> tslots;
+    for (int64_t sl = 0; sl < idx->hiwater; sl++)
+        if (idx->h_present[sl]) tslots.push_back((uint32_t)sl);
+    int64_t n = (int64_t)tslots.size();
+    if (idx->pq_training_limit > 0 && n > idx->pq_training_limit) n = idx->pq_training_limit;
+    if (n < K) return set_err(WV_ERR_INVALID, "not enough data to fit k-means");  // kmeans.go:459-461
+    rc = pq_alloc(idx);
+    if (rc) return rc;
+    // T = the n training rows (gathered, dpad stride)
+    DBuf T, sub, asg, nbi, nbd, chg, act;
+    const int64_t ldt = idx->dpad;
+    HIPCHK(T.ensure((size_t)n * ldt * sizeof(float)));
+    {
+        // contiguous copy when the first n present slots are 0..n-1, else a gather
+        bool contiguous = true;
+        for (int64_t i = 0; i < n; i++)
+            if (tslots[i] != (uint32_t)i) { contiguous = false; break; }
+        if (contiguous) {
+            HIPCHK(hipMemcpyAsync(T.p, idx->X, (size_t)n * ldt * sizeof(float), hipMemcpyDeviceToDevice, s));
+        } else {
+            for (int64_t i = 0; i < n; i++)
+                HIPCHK(hipMemcpyAsync(T.as<float>() + i * ldt, idx->X + (int64_t)tslots[i] * ldt, ldt * sizeof(float),
+                                      hipMemcpyDeviceToDevice, s));
+        }
+    }
+    float* C = idx->pq_centers;
+    const size_t lds_c = (size_t)K * ds * sizeof(float);
+    if (K == 1) {  // computeCentroid (kmeans.go:447-452): every row in cluster 0
+        HIPCHK(asg.ensure((size_t)m * n * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(asg.p, 0, (size_t)m * n * sizeof(uint32_t), s));
+        const size_t lds_u = (size_t)K * ds * sizeof(double) + KM_T * sizeof(uint32_t) + (size_t)KM_T * ds * sizeof(float);
+        k_km_update_centers<<<m, KM_T, lds_u, s>>>(T.as<float>(), ldt, n, K, ds, asg.as<uint32_t>(), nullptr, C);
+        HIPCHK(hipGetLastError());
+        return pq_encode_all(idx);
+    }
+    // initializeRandom (:279-299): per segment its own PCG stream
+    std::vector<int64_t> hsub((size_t)m * K);
+    for (int sg = 0; sg < m; sg++) {
+        GoPCG r{seed + (uint64_t)sg, 0x385ab5285169b1acULL};
+        std::vector<int64_t> ss = random_subset(r, n, K);
+        std::copy(ss.begin(), ss.end(), hsub.begin() + (size_t)sg * K);
+    }
+    HIPCHK(sub.ensure(hsub.size() * sizeof(int64_t)));
+    HIPCHK(hipMemcpyAsync(sub.p, hsub.data(), hsub.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    {
+        const int64_t tot = (int64_t)m * K * ds;
+        k_km_gather_centers<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(T.as<float>(), ldt, sub.as<int64_t>(), m, K, ds,
+                                                                          C);
+    }
+    HIPCHK(asg.ensure((size_t)m * n * sizeof(uint32_t)));
+    HIPCHK(nbi.ensure((size_t)m * K * (K - 1) * sizeof(uint32_t)));
+    HIPCHK(nbd.ensure((size_t)m * K * (K - 1) * sizeof(float)));
+    HIPCHK(chg.ensure((size_t)m * sizeof(unsigned long long)));
+    HIPCHK(act.ensure((size_t)m * sizeof(int32_t)));
+    const int iteration_threshold = 10;  // KMeansEncoder.Fit: km.IterationThreshold = 10
+    const float delta_threshold = 0.01f; // km.DeltaThreshold = 0.01
+    std::vector<int32_t> active((size_t)m, iteration_threshold > 1 ? 1 : 0);
+    HIPCHK(hipMemcpyAsync(act.p, active.data(), (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const dim3 rgrid((unsigned)((n + 255) / 256), (unsigned)m);
+    if (lds_c > 64 * 1024) {
+        HIPCHK(hipFuncSetAttribute((const void*)k_km_assign_brute, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
+        HIPCHK(hipFuncSetAttribute((const void*)k_km_assign_prune, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
+        HIPCHK(hipFuncSetAttribute((const void*)k_pq_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
+    }
+    const size_t lds_u = (size_t)K * ds * sizeof(double) + KM_T * sizeof(uint32_t) + (size_t)KM_T * ds * sizeof(float);
+    if (lds_u > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_km_update_centers, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_u));
+    k_km_assign_brute<<<rgrid, 256, lds_c, s>>>(T.as<float>(), ldt, n, K, ds, C, idx->variant, nullptr, asg.as<uint32_t>());
+    k_km_update_centers<<<m, KM_T, lds_u, s>>>(T.as<float>(), ldt, n, K, ds, asg.as<uint32_t>(), nullptr, C);
+    HIPCHK(hipGetLastError());
+    int iterations = 1;  // initializeRandom counts as the first iteration (Metrics.update)
+    std::vector<unsigned long long> hchg((size_t)m);
+    while (iterations < iteration_threshold) {
+        bool any = false;
+        for (int sg = 0; sg < m; sg++) any = any || active[sg];
+        if (!any) break;
+        k_km_neighbors<<<dim3((unsigned)K, (unsigned)m), KM_T, 0, s>>>(C, K, ds, idx->variant, act.as<int32_t>(),
+                                                                       nbi.as<uint32_t>(), nbd.as<float>());
+        HIPCHK(hipMemsetAsync(chg.p, 0, (size_t)m * sizeof(unsigned long long), s));
+        k_km_assign_prune<<<rgrid, 256, lds_c, s>>>(T.as<float>(), ldt, n, K, ds, C, idx->variant, nbi.as<uint32_t>(),
+                                                    nbd.as<float>(), act.as<int32_t>(), asg.as<uint32_t>(),
+                                                    chg.as<unsigned long long>());
+        k_km_update_centers<<<m, KM_T, lds_u, s>>>(T.as<float>(), ldt, n, K, ds, asg.as<uint32_t>(), act.as<int32_t>(),
+                                                   C);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(hchg.data(), chg.p, (size_t)m * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        iterations++;
+        for (int sg = 0; sg < m; sg++) {
+            // kmeans.go:490: float32(changes) <= DeltaThreshold * float32(n)
+            if (active[sg] && ((float)hchg[sg] <= delta_threshold * (float)n || iterations >= iteration_threshold))
+                active[sg] = 0;
+        }
+        HIPCHK(hipMemcpyAsync(act.p, active.data(), (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    T.release(); sub.release(); asg.release(); nbi.release(); nbd.release(); chg.release(); act.release();
+    return pq_encode_all(idx);
+}
+
+extern "C" int wv_index_pq_set_centers(wv_index* idx, const float* centers, int64_t n_floats) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->compression != WV_COMPRESSION_PQ) return set_err(WV_ERR_INVALID, "pq: index is not PQ-compressed");
+    int rc = pq_validate(idx);
+    if (rc) return rc;
+    if (n_floats != (int64_t)idx->pq_m * idx->pq_ks * idx->pq_ds) return set_err(WV_ERR_INVALID, "pq: codebook size mismatch");
+    rc = pq_alloc(idx);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(idx->pq_centers, centers, (size_t)n_floats * sizeof(float), hipMemcpyHostToDevice, idx->stream));
+    return pq_encode_all(idx);
+}
+
+extern "C" int wv_index_pq_centers(wv_index* idx, float* out, int64_t n_floats) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (!idx->pq_trained) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (n_floats != (int64_t)idx->pq_m * idx->pq_ks * idx->pq_ds) return set_err(WV_ERR_INVALID, "pq: codebook size mismatch");
+    HIPCHK(hipMemcpyAsync(out, idx->pq_centers, (size_t)n_floats * sizeof(float), hipMemcpyDeviceToHost, idx->stream));
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    return WV_OK;
+}
+
+extern "C" int wv_index_pq_codes(wv_index* idx, uint8_t* out, int64_t n) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (!idx->pq_trained) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (n > idx->cap) return set_err(WV_ERR_INVALID, "pq_codes: n beyond capacity");
+    const int pw = (idx->pq_m + 3) / 4;
+    std::vector<uint32_t> h((size_t)pw * n);
+    HIPCHK(hipMemcpy2DAsync(h.data(), (size_t)n * sizeof(uint32_t), idx->pq_codes, (size_t)idx->cap * sizeof(uint32_t),
+                            (size_t)n * sizeof(uint32_t), pw, hipMemcpyDeviceToHost, idx->stream));
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    for (int64_t r = 0; r < n; r++)
+        for (int sg = 0; sg < idx->pq_m; sg++) out[r * idx->pq_m + sg] = (uint8_t)(h[(size_t)(sg >> 2) * n + r] >> (8 * (sg & 3)));
+    return WV_OK;
+}
+
+extern "C" int wv_index_pq_info(wv_index* idx, int32_t* out) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    out[0] = idx->pq_m; out[1] = idx->pq_ks; out[2] = idx->pq_ds; out[3] = idx->pq_trained;
+    return WV_OK;
+}
+
+extern "C" int wv_index_pq_distance(wv_index* idx, const float* query, int64_t d, const uint8_t* codes, int64_t n,
+                                    float* out) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (!idx->pq_trained) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (d != idx->dims) return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    if (n <= 0) return WV_OK;
+    hipStream_t s = idx->stream;
+    const int m = idx->pq_m, K = idx->pq_ks, pw = (m + 3) / 4;
+    DBuf Q, L, Cd, E, B, ql;
+    HIPCHK(Q.ensure((size_t)d * sizeof(float)));
+    HIPCHK(hipMemcpyAsync(Q.p, query, (size_t)d * sizeof(float), hipMemcpyHostToDevice, s));
+    HIPCHK(L.ensure((size_t)m * K * sizeof(float)));
+    k_pq_lut<<<(unsigned)(((int64_t)m * K + 255) / 256), 256, 0, s>>>(Q.as<float>(), d, 1, m, K, idx->pq_ds,
+                                                                      idx->metric == WV_METRIC_L2_SQUARED ? L2 : DOT,
+                                                                      idx->pq_centers, L.as<float>());
+    // pack the given codes [n][m] into the plane layout
+    const int64_t ld = round_up(n, 256);
+    std::vector<uint32_t> h((size_t)pw * ld, 0);
+    for (int64_t r = 0; r < n; r++)
+        for (int sg = 0; sg < m; sg++) h[(size_t)(sg >> 2) * ld + r] |= (uint32_t)codes[r * m + sg] << (8 * (sg & 3));
+    HIPCHK(Cd.ensure(h.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(Cd.p, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    std::vector<uint32_t> ones((size_t)(ld / 32), 0xFFFFFFFFu);
+    DBuf V;
+    HIPCHK(V.ensure(ones.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(V.p, ones.data(), ones.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIPCHK(E.ensure((size_t)ld * sizeof(float)));
+    HIPCHK(B.ensure((size_t)(ld / 256) * sizeof(float)));
+    int32_t zero = 0;
+    HIPCHK(ql.ensure(sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(ql.p, &zero, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const int wrapm = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+    dim3 grid((unsigned)((n + 256 * PQ_RPT - 1) / (256 * PQ_RPT)), 1);
+    k_pq_adc<<<grid, 256, (size_t)PQ_CH * K * sizeof(float), s>>>(Cd.as<uint32_t>(), ld, m, K, V.as<uint32_t>(), n,
+                                                                  L.as<float>(), ql.as<int32_t>(), wrapm, ld,
+                                                                  E.as<float>(), B.as<float>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, E.p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// hnsw.flatSearch over the PQ codes (flat_search.go:28-141, one worker) with
+// optional h.rescore (search.go:1047-1110, one worker).  limit = rescore ?
+// max(rescore_limit, k) : k.  Outputs [nq][k].
+static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
+                     const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+    if (qd != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)qd, idx->dims);
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    const int rescore = idx->pq_rescore ? 1 : 0;
+    const int R = rescore && idx->rescore_limit > k ? idx->rescore_limit : k;
+    if (R > 8192) return set_err(WV_ERR_UNSUPPORTED, "limit %d > 8192", R);
+    const int64_t nq_pad = round_up(nq, QB);
+    int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
+    if (rc) return rc;
+    const float* Qn = idx->qn.as<float>();
+    const int m = idx->pq_m, K = idx->pq_ks;
+    idx->stats.queries += (uint64_t)nq;
+    idx->stats.batches++;
+    HIPCHK(idx->lut.ensure((size_t)nq * m * K * sizeof(float)));
+    k_pq_lut<<<(unsigned)((nq * m * K + 255) / 256), 256, 0, s>>>(Qn, idx->dpad, nq, m, K, idx->pq_ds,
+                                                                   idx->metric == WV_METRIC_L2_SQUARED ? L2 : DOT,
+                                                                   idx->pq_centers, idx->lut.as<float>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(idx->ident.ensure((size_t)nq * sizeof(int32_t)));
+    {
+        std::vector<int32_t> id((size_t)nq);
+        for (int64_t i = 0; i < nq; i++) id[i] = (int32_t)i;
+        HIPCHK(hipMemcpyAsync(idx->ident.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    const int32_t* qlist = idx->ident.as<int32_t>();
+    const int64_t nslots = idx->hiwater;
+    const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
+    const int64_t G = std::max<int64_t>(1, std::min<int64_t>(nq, (2ll << 30) / (ld * 4)));
+    HIPCHK(idx->rE.ensure((size_t)G * ld * sizeof(float)));
+    HIPCHK(idx->rB.ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+    HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
+    HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
+    HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
+    const int wrapm = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+    const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
+    const size_t lds_rep = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
+    if (lds_rep > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rep));
+    for (int64_t g0 = 0; g0 < nq; g0 += G) {
+        const int F = (int)std::min<int64_t>(G, nq - g0);
+        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
+        dim3 grid((unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)), (unsigned)F);
+        k_pq_adc<<<grid, 256, lds_adc, s>>>(idx->pq_codes, idx->cap, m, K, valid, nslots, idx->lut.as<float>(),
+                                            qlist + g0, wrapm, ld, idx->rE.as<float>(), idx->rB.as<float>());
+        HIPCHK(hipGetLastError());
+        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
+        // the worker heap (addResult == insertToHeap) in id order, extracted ascending
+        k_replay_scan<<<F, 64, lds_rep, s>>>(idx->rE.as<float>(), idx->rB.as<float>(), valid, nslots, ld, qlist + g0, F,
+                                             R, idx->id_base, nullptr, nullptr, nullptr, 1, 0, R,
+                                             idx->ascI.as<uint64_t>() + g0 * R, idx->ascD.as<float>() + g0 * R,
+                                             idx->ascN.as<int32_t>() + g0);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(idx->cslot.ensure((size_t)nq * R * sizeof(uint32_t)));
+    HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
+    const size_t lds_f = (size_t)R * (sizeof(uint64_t) + sizeof(float)) + 16;
+    if (lds_f > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_pq_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
+    k_pq_finish<<<(unsigned)nq, 64, lds_f, s>>>(idx->ascI.as<uint64_t>(), idx->ascD.as<float>(), idx->ascN.as<int32_t>(),
+                                                qlist, (int)nq, R, k, rescore, idx->id_base, o_ids, o_d, o_n,
+                                                idx->cslot.as<uint32_t>(), idx->cn.as<int32_t>());
+    HIPCHK(hipGetLastError());
+    if (rescore) {
+        HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
+        const int64_t npairs = nq * R;
+        const bool v5 = idx->variant == WV_VARIANT_AVX512;
+#define WV_RS(M, V) k_rescore<M, V><<<(unsigned)((npairs + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, Qn, idx->dims, idx->cslot.as<uint32_t>(), (int)nq, R, idx->candE.as<float>())
+        switch (idx->metric) {
+        case WV_METRIC_L2_SQUARED: if (v5) WV_RS(L2, AVX512); else WV_RS(L2, AVX256); break;
+        case WV_METRIC_DOT: if (v5) WV_RS(DOT, AVX512); else WV_RS(DOT, AVX256); break;
+        default: if (v5) WV_RS(COSINE, AVX512); else WV_RS(COSINE, AVX256); break;
+        }
+#undef WV_RS
+        const size_t lds_q = (size_t)(k + 1) * (sizeof(uint64_t) + sizeof(float)) + 16;
+        if (lds_q > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute((const void*)k_pq_rescore_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
+        k_pq_rescore_final<<<(unsigned)nq, 64, lds_q, s>>>(idx->cslot.as<uint32_t>(), idx->candE.as<float>(),
+                                                           idx->cn.as<int32_t>(), qlist, (int)nq, R, k, idx->id_base,
+                                                           o_ids, o_d, o_n);
+        HIPCHK(hipGetLastError());
+    }
+    if (idx->timing) {
+        HIPCHK(hipStreamSynchronize(s));
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
+        idx->stats.last_select_ms = ms;
+    }
+    return WV_OK;
+}
+
 // Core batch search on device queries.  Outputs [nq][kout] device arrays.
 // mode 0: kout = k, flagged queries resolved by replay; mode 1: kout = k+1,
 // flags left for the caller.  n_valid = number of scan candidates.
@@ -656,6 +1089,10 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     if (idx->compression == WV_COMPRESSION_BQ) {
         if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "bq: shard-candidate mode not available");
         return search_bq(idx, s, d_qraw, nq, qd, k, valid, o_ids, o_d, o_n);
+    }
+    if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) {
+        if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "pq: shard-candidate mode not available");
+        return search_pq(idx, s, d_qraw, nq, qd, k, valid, o_ids, o_d, o_n);
     }
     // SingleDist length check on the first candidate: distancer/l2.go:47-50 etc.
     if (qd != idx->dims)

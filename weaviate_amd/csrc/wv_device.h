@@ -60,11 +60,16 @@ __device__ __forceinline__ float reduce_ymm4(const float (&acc)[4][8]) {
     return lo + hi;
 }
 
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+template <bool ALIGNED = true>
+__device__ __forceinline__ float4 ld4(const float* p) {
+    if (ALIGNED) return *reinterpret_cast<const float4*>(p);
+    return make_float4(p[0], p[1], p[2], p[3]);
+}
 
 // Raw kernel value (l2 sum or dot sum) with the reference accumulation order.
-// q and x must be 16-byte aligned (rows are padded to multiples of 32 floats).
-template <int METRIC, int VARIANT>
+// ALIGNED: q and x are 16-byte aligned (rows padded to multiples of 32 floats);
+// otherwise (PQ segments at arbitrary offsets) the same order with scalar loads.
+template <int METRIC, int VARIANT, bool ALIGNED = true>
 __device__ float exact_raw(const float* __restrict__ q, const float* __restrict__ x, int n) {
     float sum = 0.f;
     if (n < 8) {
@@ -89,8 +94,8 @@ __device__ float exact_raw(const float* __restrict__ q, const float* __restrict_
             for (int r = 0; r < 8; r++) {
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
-                    float4 a = ld4(q + e + 16 * r + 4 * c);
-                    float4 b = ld4(x + e + 16 * r + 4 * c);
+                    float4 a = ld4<ALIGNED>(q + e + 16 * r + 4 * c);
+                    float4 b = ld4<ALIGNED>(x + e + 16 * r + 4 * c);
                     acc5[r][4 * c + 0] = elem_step<METRIC>(acc5[r][4 * c + 0], a.x, b.x);
                     acc5[r][4 * c + 1] = elem_step<METRIC>(acc5[r][4 * c + 1], a.y, b.y);
                     acc5[r][4 * c + 2] = elem_step<METRIC>(acc5[r][4 * c + 2], a.z, b.z);
@@ -120,8 +125,8 @@ __device__ float exact_raw(const float* __restrict__ q, const float* __restrict_
         for (int j = 0; j < 4; j++) {
 #pragma unroll
             for (int c = 0; c < 2; c++) {
-                float4 a = ld4(q + e + 8 * j + 4 * c);
-                float4 b = ld4(x + e + 8 * j + 4 * c);
+                float4 a = ld4<ALIGNED>(q + e + 8 * j + 4 * c);
+                float4 b = ld4<ALIGNED>(x + e + 8 * j + 4 * c);
                 acc[j][4 * c + 0] = elem_step<METRIC>(acc[j][4 * c + 0], a.x, b.x);
                 acc[j][4 * c + 1] = elem_step<METRIC>(acc[j][4 * c + 1], a.y, b.y);
                 acc[j][4 * c + 2] = elem_step<METRIC>(acc[j][4 * c + 2], a.z, b.z);

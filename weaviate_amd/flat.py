@@ -64,19 +64,25 @@ class FlatIndex:
     ValidateBeforeInsert, ContainsDoc, AlreadyIndexed."""
 
     def __init__(self, distance: str = "cosine", dims: int = 0, device: int = 0, variant: str = "auto",
-                 root_path: str = "", id_base: int = 0, bq: bool = False, rescore_limit: int = -1):
+                 root_path: str = "", id_base: int = 0, bq: bool = False, rescore_limit: int = -1,
+                 pq: Optional[dict] = None):
         if distance not in DISTANCES:
             raise WeaviateError(_lib.WV_ERR_INVALID, f"unrecognized or unsupported distance metric {distance!r}")
         self._l = _lib.load()
         self._root = root_path.encode()
-        cfg = _lib.WvConfig(DISTANCES[distance], int(dims),
-                            _lib.COMPRESSION_BQ if bq else _lib.COMPRESSION_NONE, int(rescore_limit), int(device),
-                            VARIANTS[variant], int(id_base), self._root)
+        # pq: ent.PQConfig subset {"segments", "centroids" (256), "trainingLimit" (100000), "rescore" (True)}
+        pqc = dict(pq or {})
+        comp = _lib.COMPRESSION_BQ if bq else _lib.COMPRESSION_PQ if pq is not None else _lib.COMPRESSION_NONE
+        cfg = _lib.WvConfig(DISTANCES[distance], int(dims), comp, int(rescore_limit), int(device),
+                            VARIANTS[variant], int(id_base), self._root, int(pqc.get("segments", 0)),
+                            int(pqc.get("centroids", 256)), int(pqc.get("trainingLimit", 100000)),
+                            1 if pqc.get("rescore", True) else 0)
         h = C.c_void_p()
         check(self._l.wv_index_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self.metric = DISTANCES[distance]
         self.bq = bool(bq)
+        self.pq = pq is not None
         self.rescore_limit = int(rescore_limit)
         self.device = device
         self.id_base = id_base
@@ -105,8 +111,43 @@ class FlatIndex:
     def distancer_type(self) -> str:  # Provider.Type()
         return PROVIDER_TYPE[self.metric]
 
-    def compressed(self) -> bool:  # flat.Compressed (flat/index.go): BQ quantizer built at New
-        return self.bq
+    def compressed(self) -> bool:  # flat.Compressed (flat/index.go): BQ quantizer built at New; PQ once fit
+        return self.bq or (self.pq and self.pq_info()["trained"])
+
+    # -- product quantizer (compressionhelpers.ProductQuantizer) -----------
+    def pq_info(self) -> dict:
+        out = (C.c_int32 * 4)()
+        check(self._l.wv_index_pq_info(self._h, out))
+        return {"segments": out[0], "centroids": out[1], "ds": out[2], "trained": bool(out[3])}
+
+    def pq_fit(self, seed: int = 0) -> None:
+        """ProductQuantizer.Fit on the stored rows + Encode of every row."""
+        check(self._l.wv_index_pq_fit(self._h, int(seed) & (2**64 - 1)))
+
+    def pq_centers(self) -> np.ndarray:
+        i = self.pq_info()
+        out = np.zeros((i["segments"], i["centroids"], i["ds"]), dtype=np.float32)
+        check(self._l.wv_index_pq_centers(self._h, _fptr(out), out.size))
+        return out
+
+    def pq_set_centers(self, centers) -> None:
+        c = np.ascontiguousarray(centers, dtype=np.float32)
+        check(self._l.wv_index_pq_set_centers(self._h, _fptr(c), c.size))
+
+    def pq_codes(self, n: int) -> np.ndarray:
+        m = self.pq_info()["segments"]
+        out = np.zeros((n, m), dtype=np.uint8)
+        check(self._l.wv_index_pq_codes(self._h, out.ctypes.data_as(C.POINTER(C.c_uint8)), n))
+        return out
+
+    def pq_distance(self, query, codes) -> np.ndarray:
+        """PQDistancer.Distance of `query` (as given) against code rows."""
+        q = np.ascontiguousarray(query, dtype=np.float32)
+        c = np.ascontiguousarray(codes, dtype=np.uint8)
+        out = np.zeros(c.shape[0], dtype=np.float32)
+        check(self._l.wv_index_pq_distance(self._h, _fptr(q), q.size, c.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                           c.shape[0], _fptr(out)))
+        return out
 
     def reserve(self, nslots: int) -> None:
         check(self._l.wv_index_reserve(self._h, int(nslots)))
