@@ -44,6 +44,15 @@ BQ_ROWS_PER_GPU = 6_250_000
 BQ_DIMS = 1536
 BQ_RESCORE = 200
 
+# BASELINE configs[4]: PQ GIST-shaped 10M x 960, 240 segments x 256 centroids,
+# k-means trained on a 100k sample, ADC search
+PQ_ROWS = 10_000_000
+PQ_DIMS = 960
+PQ_SEGMENTS = 240
+PQ_CENTROIDS = 256
+PQ_TRAIN = 100_000
+LDS_LOOKUP_PEAK_T = 19.7       # 256 CU x 32 dwords/clk (128 B/clk LDS) x 2.4 GHz
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
@@ -106,14 +115,37 @@ def cpu_baseline_bq(n_sample: int, nq: int, threads: int, n_full: int):
     }
 
 
+def cpu_baseline_pq(index, n_sample: int, nq: int, threads: int, n_full: int):
+    """CPU PQ flat search (oracle/baseline.c: DistanceLookUpTable + LookUp +
+    flatSearch heap, restated) on the same codebook and codes; one query per
+    thread.  There is no reference kernel to call: the Go LookUp loop is pure Go."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc  # test infrastructure, used only for this baseline leg
+    centers = index.pq_centers()
+    codes = index.pq_codes(n_sample)
+    queries = orc.gen_matrix(2, SEED_QUERY, 0, nq, PQ_DIMS)
+    t0 = time.perf_counter()
+    orc.cpu_baseline_pq(orc.L2, centers, codes, queries, K, threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": nq / dt * n_sample / n_full,
+        "unit": "queries/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{nq} queries x {n_sample} rows, LUT + ADC (m={PQ_SEGMENTS}) + heap, oracle C restatement, "
+                   f"{dt:.1f} s, QPS scaled by {n_sample}/{n_full}"),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c3", "bq"], default="c3",
-                    help="c3: 10M x 768 cosine exact (default, the headline); bq: BQ 1536-d shard of configs[3]")
+    ap.add_argument("--workload", choices=["c3", "bq", "pq"], default="c3",
+                    help="c3: 10M x 768 cosine exact (default, the headline); bq: BQ 1536-d shard of configs[3]; "
+                         "pq: configs[4] PQ 10M x 960 (k-means fit timed once, ADC search timed per step)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
@@ -141,31 +173,44 @@ def main():
     lib = _lib.load()
 
     bq = args.workload == "bq"
-    if bq and world > 1:
-        raise SystemExit("--workload bq: sharded BQ search is not available yet (1 GPU = one configs[3] shard)")
-    dims = BQ_DIMS if bq else DIMS
-    n_total = args.n if args.n is not None else (BQ_ROWS_PER_GPU if bq else N_TOTAL)
+    pq = args.workload == "pq"
+    if (bq or pq) and world > 1:
+        raise SystemExit(f"--workload {args.workload}: sharded search is not available yet (1 GPU)")
+    dims = BQ_DIMS if bq else PQ_DIMS if pq else DIMS
+    n_total = args.n if args.n is not None else (BQ_ROWS_PER_GPU if bq else PQ_ROWS if pq else N_TOTAL)
     n_local = (n_total + world - 1) // world
     id0 = rank * n_local
     n_local = max(0, min(n_local, n_total - id0))
-    B = args.batch
+    B = args.batch if args.batch is not None else (256 if pq else 2048)
+    gen_kind = 2 if pq else 0  # GIST-shaped U[0,1) for PQ, U[-1,1) otherwise
 
     # ---- build the shard: generate + add in 1M-row chunks (device resident) ----
     t_build = time.perf_counter()
-    index = wv.FlatIndex(distance="cosine", dims=dims, device=local_rank, variant="avx256", id_base=id0,
-                         bq=bq, rescore_limit=BQ_RESCORE if bq else -1)
+    index = wv.FlatIndex(distance="l2-squared" if pq else "cosine", dims=dims, device=local_rank, variant="avx256", id_base=id0,
+                         bq=bq, rescore_limit=BQ_RESCORE if bq else -1,
+                         pq={"segments": PQ_SEGMENTS, "centroids": PQ_CENTROIDS, "trainingLimit": PQ_TRAIN,
+                             "rescore": False} if pq else None)
     index.reserve(n_local)
     chunk = 1_000_000
     stage = torch.empty((min(chunk, max(n_local, 1)), dims), dtype=torch.float32, device=dev)
     for r0 in range(0, n_local, chunk):
         m = min(chunk, n_local - r0)
-        _lib.check(lib.wv_gen_device(local_rank, 0, SEED_CORPUS, id0 + r0, m, dims, stage.data_ptr(), None))
+        _lib.check(lib.wv_gen_device(local_rank, gen_kind, SEED_CORPUS, id0 + r0, m, dims, stage.data_ptr(), None))
         _lib.check(lib.wv_index_add_range_device(index._h, id0 + r0, stage.data_ptr(), m, dims))
     del stage
     queries = torch.empty((B, dims), dtype=torch.float32, device=dev)
-    _lib.check(lib.wv_gen_device(local_rank, 0, SEED_QUERY, 0, B, dims, queries.data_ptr(), None))
+    _lib.check(lib.wv_gen_device(local_rank, gen_kind, SEED_QUERY, 0, B, dims, queries.data_ptr(), None))
     torch.cuda.synchronize()
     log(f"[rank {rank}] shard ids [{id0}, {id0 + n_local}) built in {time.perf_counter() - t_build:.1f} s")
+    fit_s = None
+    if pq:
+        torch.cuda.synchronize()
+        t_fit = time.perf_counter()
+        index.pq_fit(seed=SEED_CORPUS)
+        torch.cuda.synchronize()
+        fit_s = time.perf_counter() - t_fit
+        log(f"[rank {rank}] pq fit ({PQ_SEGMENTS} x k-means k={PQ_CENTROIDS} on {PQ_TRAIN} rows) + encode "
+            f"{n_local} rows: {fit_s:.2f} s")
     index.set_option("timing", 1)
 
     out_ids = torch.empty((B, K), dtype=torch.int64, device=dev)
@@ -215,7 +260,19 @@ def main():
     total_q = B * args.steps
     value = total_q / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    if bq:
+    if pq:
+        # dominant kernel k_pq_adc: one LUT lookup (LDS gather) + fp32 add per
+        # (query, row, segment); the codes of a tile are shared by the group's
+        # queries through L2
+        ld = (n_local + 255) // 256 * 256
+        f0 = max(1, min(B, (2 << 30) // (ld * 4)))  # queries in the timed first group (search_pq grouping)
+        lookups = float(f0) * n_local * PQ_SEGMENTS
+        achieved = lookups / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
+        roof = {"bound": "lds", "kernel": "k_pq_adc", "achieved": achieved, "peak": LDS_LOOKUP_PEAK_T,
+                "unit": "T lookups/s", "frac": achieved / LDS_LOOKUP_PEAK_T, "launch_ms": sel_avg,
+                "note": "launch_ms = first query group of the batch",
+                "traffic": args.traffic_bytes}
+    elif bq:
         # dominant kernel k_bq_blockmin: VALU-bound integer work, per (query,
         # row) pair and 64-bit code word 2 v_xor_b32 + 2 v_bcnt_u32_b32
         words = (dims + 63) // 64
@@ -240,14 +297,20 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                if bq:
+                if pq:
+                    cpu = cpu_baseline_pq(index, min(args.cpu_rows, n_total), args.cpu_queries or 256,
+                                          args.cpu_threads, n_total)
+                elif bq:
                     cpu = cpu_baseline_bq(min(args.cpu_rows, n_total), args.cpu_queries or 4096, args.cpu_threads,
                                           n_total)
                 else:
                     cpu = cpu_baseline(min(args.cpu_rows, n_total), args.cpu_queries or 1024, args.cpu_threads)
             except Exception as e:  # baseline failure must not hide the GPU number
                 log(f"cpu baseline failed: {e}")
-        if bq:
+        if pq:
+            workload = (f"PQ {dims}-d l2-squared, m={PQ_SEGMENTS} x ks={PQ_CENTROIDS} trained on {PQ_TRAIN} rows "
+                        f"(fit {fit_s:.2f} s), ADC flat search k={K} (BASELINE configs[4])")
+        elif bq:
             workload = (f"BQ {dims}-d cosine, k={K}, rescore R={BQ_RESCORE}: one {n_total}-row shard of "
                         "BASELINE configs[3] (50M x 1536 over 8 GPUs)")
         else:
@@ -263,7 +326,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "u64 hamming + f32 rescoring" if bq else "f32",
+            "dtype": "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else "f32",
             "data": "synthetic (counter-based U[-1,1) generator, seed 1 corpus / 2 queries)",
             "config": {
                 "workload": workload,

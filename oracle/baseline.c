@@ -155,3 +155,47 @@ int bl_flat_search_bq_batch(int metric, int variant, int use_ref, const float *s
     free(th); free(jobs);
     return 0;
 }
+
+/* ---- PQ: flatSearch over PQ codes (hnsw/flat_search.go, one worker), one query per thread ---- */
+typedef struct {
+    int metric, k, m, ks, ds;
+    const float *centers; const uint8_t *codes; long n;
+    const float *queries; long nq;
+    uint64_t *out_ids; float *out_dists; int *out_n;
+    int tid, nthreads;
+} pq_job_t;
+
+static void *pq_worker(void *arg) {
+    pq_job_t *j = (pq_job_t *)arg;
+    float *lut = (float *)malloc(sizeof(float) * (size_t)j->m * j->ks);
+    or_heap h, r;
+    h.id = (uint64_t *)malloc(sizeof(uint64_t) * (j->k + 1)); h.dist = (float *)malloc(sizeof(float) * (j->k + 1));
+    r.id = (uint64_t *)malloc(sizeof(uint64_t) * (j->k + 1)); r.dist = (float *)malloc(sizeof(float) * (j->k + 1));
+    for (long qi = j->tid; qi < j->nq; qi += j->nthreads) {
+        const float *q = j->queries + (size_t)qi * j->m * j->ds;
+        or_pq_lut(j->metric, j->centers, j->m, j->ks, j->ds, q, lut);
+        h.len = 0; r.len = 0;
+        for (long s = 0; s < j->n; s++)
+            or_insert_to_heap(&h, j->k, (uint64_t)s, or_pq_adc(j->metric, lut, j->m, j->ks, j->codes + (size_t)s * j->m));
+        while (h.len > 0) { uint64_t id; float dd; or_heap_pop(&h, &id, &dd); or_insert_to_heap(&r, j->k, id, dd); }
+        j->out_n[qi] = or_extract_heap(&r, j->out_ids + (size_t)qi * j->k, j->out_dists + (size_t)qi * j->k);
+    }
+    free(lut); free(h.id); free(h.dist); free(r.id); free(r.dist);
+    return NULL;
+}
+
+int bl_pq_search_batch(int metric, const float *centers, int m, int ks, int ds, const uint8_t *codes, long n,
+                       const float *queries, long nq, int k, int nthreads, uint64_t *out_ids, float *out_dists,
+                       int *out_n) {
+    if (nthreads < 1) nthreads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+    pq_job_t *jobs = (pq_job_t *)malloc(sizeof(pq_job_t) * nthreads);
+    for (int t = 0; t < nthreads; t++) {
+        pq_job_t jj = {metric, k, m, ks, ds, centers, codes, n, queries, nq, out_ids, out_dists, out_n, t, nthreads};
+        jobs[t] = jj;
+        pthread_create(&th[t], NULL, pq_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th); free(jobs);
+    return 0;
+}

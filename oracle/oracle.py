@@ -74,6 +74,9 @@ def lib() -> C.CDLL:
         o.or_pq_flat_search.restype = C.c_int
         o.or_pq_flat_search.argtypes = [C.c_int, C.c_int, pf, C.c_int, C.c_int, C.c_int, pb, pf, pb, C.c_long, pf,
                                         C.c_int, C.c_int, C.c_int, pu, pf, pi]
+        o.bl_pq_search_batch.restype = C.c_int
+        o.bl_pq_search_batch.argtypes = [C.c_int, pf, C.c_int, C.c_int, C.c_int, pb, C.c_long, pf, C.c_long, C.c_int,
+                                         C.c_int, pu, pf, pi]
         o.bl_flat_search_bq_batch.restype = C.c_int
         o.bl_flat_search_bq_batch.argtypes = [C.c_int, C.c_int, C.c_int, pf, pu, C.c_long, C.c_long, pf, C.c_long,
                                               C.c_int, C.c_int, C.c_int, pu, pf, pi]
@@ -299,6 +302,21 @@ def pq_flat_search(metric: int, variant: int, centers: np.ndarray, codes: np.nda
                             f(np.ascontiguousarray(query, np.float32)), k, limit, 1 if rescore else 0,
                             ids.ctypes.data_as(pu), f(dd), C.byref(n))
     return ids[: n.value].copy(), dd[: n.value].copy()
+
+
+def cpu_baseline_pq(metric: int, centers: np.ndarray, codes: np.ndarray, queries: np.ndarray, k: int, nthreads: int):
+    """Threaded CPU PQ flat search (oracle/baseline.c): LUT + ADC + heap per query."""
+    m, ks, ds = centers.shape
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    queries = np.ascontiguousarray(queries, dtype=np.float32)
+    nq = queries.shape[0]
+    ids = np.zeros((nq, k), dtype=np.uint64)
+    dd = np.zeros((nq, k), dtype=np.float32)
+    cnt = np.zeros(nq, dtype=np.int32)
+    lib().bl_pq_search_batch(metric, f(np.ascontiguousarray(centers, np.float32)), m, ks, ds, codes.ctypes.data_as(pb),
+                             codes.shape[0], f(queries), nq, k, nthreads, ids.ctypes.data_as(pu), f(dd),
+                             cnt.ctypes.data_as(pi))
+    return ids, dd, cnt
 
 
 def gen_matrix(kind: int, seed: int, row0: int, rows: int, d: int) -> np.ndarray:

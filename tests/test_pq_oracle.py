@@ -78,3 +78,16 @@ def test_adc_equals_lut_sum_and_wrap(oracle):  # product_quantization.go:85-104,
             s = np.float32(s + acc)
         want = s if metric == oracle.L2 else -s if metric == oracle.DOT else max(np.float32(1) - s, np.float32(0))
         assert oracle.pq_distance(metric, c, q, code) == np.float32(want)
+
+
+def test_pq_cpu_baseline_equals_oracle_search(oracle):
+    rng = np.random.default_rng(6)
+    data = rng.random((800, 16), dtype=np.float32)
+    c = oracle.pq_fit(data, 4, 16, seed=3)
+    codes = np.stack([oracle.pq_encode(c, x) for x in data])
+    qs = rng.random((5, 16), dtype=np.float32)
+    ids, dd, cnt = oracle.cpu_baseline_pq(oracle.L2, c, codes, qs, 10, 2)
+    for i in range(5):
+        oi, od = oracle.pq_flat_search(oracle.L2, 1, c, codes, data, np.ones(800, np.uint8), qs[i], 10, 10, False)
+        np.testing.assert_array_equal(ids[i, :cnt[i]], oi)
+        np.testing.assert_array_equal(dd[i, :cnt[i]], od)

@@ -17,13 +17,20 @@
 //                         block minima for the heap replay (k_replay_scan)
 //   k_pq_finish           flatSearch's merge of the worker heap into the result
 //                         heap (pop order), optional rescoring, extraction
-// Codes live segment-word-major: codes[(s / 4) * ccap + slot] holds segments
-// 4(s/4) .. 4(s/4)+3 of row `slot` as bytes (coalesced dword per lane).
+// Codes live in 256-row tiles of 16-segment groups: the 16 code bytes of
+// segments [16g, 16g+16) of row r are the uint4 at ((r/256) * G16 + g) * 256 +
+// r%256 (G16 = ceil(m/16)), so 64 lanes on consecutive rows read 1 KiB
+// contiguous per group (pq_code_word gives the u32 holding segment s).
 #pragma once
 
 namespace wv {
 
 constexpr int KM_T = 256;  // threads per k-means workgroup; k <= 256 (NewProductQuantizer)
+
+// u32 index of the word holding segment s of row r (byte s % 4)
+__host__ __device__ __forceinline__ int64_t pq_code_word(int64_t r, int s, int g16) {
+    return ((((r >> 8) * g16 + (s >> 4)) << 8) + (r & 255)) * 4 + ((s >> 2) & 3);
+}
 
 __device__ __forceinline__ float l2_seg(const float* a, const float* b, int ds, int variant) {
     return variant == AVX512 ? exact_raw<L2, AVX512, false>(a, b, ds) : exact_raw<L2, AVX256, false>(a, b, ds);
@@ -187,12 +194,16 @@ __global__ __launch_bounds__(KM_T) void k_km_update_centers(const float* __restr
 
 // KMeansEncoder.Encode over all segments: thread per (row, segment); centers of
 // the segment in LDS; L2 SingleDist(segment, centroid), strict <.
-// rows[slot * ld ...] -> codes[(s/4) * ccap + slot] byte (s % 4).
+// rows[slot * ld ...] -> codes[slot * mwp + s/4] byte (s % 4).
+// DS > 0: the row's segment is held in registers (compile-time length; the
+// AVX-512 kernel differs from AVX2 only for n >= 128, so ds <= 32 needs no
+// variant); DS == 0: generic length.
+template <int DS>
 __global__ __launch_bounds__(256) void k_pq_encode(const float* __restrict__ rows, int64_t ld, int64_t n,
                                                    const uint32_t* __restrict__ slots, int k, int ds,
                                                    const float* __restrict__ centers, int variant,
-                                                   uint32_t* __restrict__ codes, int64_t ccap) {
-    extern __shared__ float csm[];
+                                                   uint32_t* __restrict__ codes, int g16) {
+    extern __shared__ __attribute__((aligned(16))) float csm[];
     const int s = blockIdx.y;
     const float* cs = centers + (int64_t)s * k * ds;
     for (int i = threadIdx.x; i < k * ds; i += blockDim.x) csm[i] = cs[i];
@@ -203,11 +214,21 @@ __global__ __launch_bounds__(256) void k_pq_encode(const float* __restrict__ row
     const float* x = rows + slot * ld + (int64_t)s * ds;
     float mn = 3.40282346638528859811704183484516925440e+38f;
     uint32_t idx = 0;
-    for (int c = 0; c < k; c++) {
-        const float d = l2_seg(x, csm + c * ds, ds, variant);
-        if (d < mn) { mn = d; idx = (uint32_t)c; }
+    if (DS > 0) {
+        float xr[DS > 0 ? DS : 1];
+#pragma unroll
+        for (int j = 0; j < DS; j++) xr[j] = x[j];
+        for (int c = 0; c < k; c++) {
+            const float d = exact_raw<L2, AVX256, false>(xr, csm + c * DS, DS);
+            if (d < mn) { mn = d; idx = (uint32_t)c; }
+        }
+    } else {
+        for (int c = 0; c < k; c++) {
+            const float d = l2_seg(x, csm + c * ds, ds, variant);
+            if (d < mn) { mn = d; idx = (uint32_t)c; }
+        }
     }
-    unsigned char* b = reinterpret_cast<unsigned char*>(codes + (int64_t)(s >> 2) * ccap + slot);
+    unsigned char* b = reinterpret_cast<unsigned char*>(codes + pq_code_word(slot, s, g16));
     b[s & 3] = (unsigned char)idx;
 }
 
@@ -239,23 +260,30 @@ __device__ __forceinline__ float pq_wrap(int metric, float x) {
     return w < 0.f ? 0.f : w;
 }
 
-// ADC over a row tile for listed query f = blockIdx.y: rows tile0 + 256 r + t,
+// ADC over a row tile blockIdx.y for listed query f = blockIdx.x (queries
+// fastest: the blocks of one tile run together and share its codes in L2): rows tile0 + 256 r + t,
 // r < PQ_RPT.  LUT chunks of PQ_CH segments staged through LDS in segment
 // order (the running sums stay in registers, so the fp32 addition order is
 // the reference's).  Writes E[f][row] (+inf for invalid rows) and the 256-row
 // block minima used by k_replay_scan.
-constexpr int PQ_RPT = 16;
+constexpr int PQ_RPT = 8;
 constexpr int PQ_CH = 32;
-__global__ __launch_bounds__(256) void k_pq_adc(const uint32_t* __restrict__ codes, int64_t ccap, int m, int k,
-                                                const uint32_t* __restrict__ valid, int64_t nslots,
-                                                const float* __restrict__ lut, const int32_t* __restrict__ qlist,
-                                                int metric, int64_t ld, float* __restrict__ E,
-                                                float* __restrict__ bmin) {
+template <int KC>  // KC = ks when 256 (LDS offsets become immediates), 0 = runtime k
+__global__ __launch_bounds__(256, 2) void k_pq_adc(const uint32_t* __restrict__ codes, int g16, int m, int kk,
+                                                   const uint32_t* __restrict__ valid, int64_t nslots,
+                                                   const float* __restrict__ lut, const int32_t* __restrict__ qlist,
+                                                   int metric, int64_t ld, float* __restrict__ E,
+                                                   float* __restrict__ bmin) {
     extern __shared__ float lsm[];  // [PQ_CH][k]
     __shared__ float red[4][PQ_RPT];
+    const int k = KC > 0 ? KC : kk;
     const int t = threadIdx.x;
-    const int f = blockIdx.y;
-    const int64_t tile0 = (int64_t)blockIdx.x * 256 * PQ_RPT;
+    const int f = blockIdx.x;
+    const int64_t tile0 = (int64_t)blockIdx.y * 256 * PQ_RPT;
+    // this block's PQ_RPT 256-row code tiles: uint4 (tile r, group g, lane t) at (r * g16 + g) * 256 + t
+    const uint4* cbase = reinterpret_cast<const uint4*>(codes) + (int64_t)blockIdx.y * PQ_RPT * g16 * 256;
+    const int64_t rem64 = nslots - tile0;
+    const int rem = rem64 < 256 * PQ_RPT ? (int)rem64 : 256 * PQ_RPT;  // rows of this tile that exist
     const float* L = lut + (int64_t)qlist[f] * m * k;
     float sum[PQ_RPT];
 #pragma unroll
@@ -265,26 +293,54 @@ __global__ __launch_bounds__(256) void k_pq_adc(const uint32_t* __restrict__ cod
         __syncthreads();
         for (int i = t; i < ns * k; i += 256) lsm[i] = L[(int64_t)s0 * k + i];
         __syncthreads();
+#pragma unroll 1
+        for (int c16 = 0; c16 < ns; c16 += 16) {
+            const float* lc = lsm + c16 * k;
+            const int g = (s0 + c16) >> 4;
+            const int nv = ns - c16 < 16 ? ns - c16 : 16;
+            if (nv == 16) {
 #pragma unroll
-        for (int r = 0; r < PQ_RPT; r++) {
-            const int64_t row = tile0 + 256 * r + t;
-            if (row >= nslots) continue;
-            float acc = sum[r];
-            for (int sw = 0; sw < ns; sw += 4) {  // s0 is a multiple of 4
-                const uint32_t w = codes[(int64_t)((s0 + sw) >> 2) * ccap + row];
-                const int lim = ns - sw < 4 ? ns - sw : 4;
-                for (int b = 0; b < lim; b++) acc = acc + lsm[(sw + b) * k + ((w >> (8 * b)) & 0xFFu)];
+                for (int rb = 0; rb < PQ_RPT; rb += 4) {
+                    uint4 cw[4];
+#pragma unroll
+                    for (int rr = 0; rr < 4; rr++) {
+                        const int r = rb + rr;
+                        cw[rr] = 256 * r + t < rem ? cbase[(uint32_t)((r * g16 + g) * 256 + t)] : make_uint4(0u, 0u, 0u, 0u);
+                    }
+#pragma unroll
+                    for (int rr = 0; rr < 4; rr++) {
+                        float acc = sum[rb + rr];
+                        const uint32_t wv4[4] = {cw[rr].x, cw[rr].y, cw[rr].z, cw[rr].w};
+#pragma unroll
+                        for (int w = 0; w < 4; w++)
+#pragma unroll
+                            for (int b = 0; b < 4; b++) acc = acc + lc[(4 * w + b) * k + ((wv4[w] >> (8 * b)) & 0xFFu)];
+                        sum[rb + rr] = acc;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < PQ_RPT; r++) {
+                    const uint4 c4 = 256 * r + t < rem ? cbase[(uint32_t)((r * g16 + g) * 256 + t)] : make_uint4(0u, 0u, 0u, 0u);
+                    const uint32_t wv4[4] = {c4.x, c4.y, c4.z, c4.w};
+                    float acc = sum[r];
+#pragma unroll 1
+                    for (int j = 0; j < nv; j++) acc = acc + lc[j * k + ((wv4[j >> 2] >> (8 * (j & 3))) & 0xFFu)];
+                    sum[r] = acc;
+                }
             }
-            sum[r] = acc;
         }
     }
     const int lane = t & 63, wv = t >> 6;
+    const int64_t lrem = ld - tile0;
+    float* Ef = E + (int64_t)f * ld + tile0;
 #pragma unroll
     for (int r = 0; r < PQ_RPT; r++) {
-        const int64_t row = tile0 + 256 * r + t;
-        const bool ok = row < nslots && ((valid[row >> 5] >> (row & 31)) & 1u);
+        const int lr = 256 * r + t;
+        const int64_t row = tile0 + lr;
+        const bool ok = lr < rem && ((valid[row >> 5] >> (row & 31)) & 1u);
         const float e = ok ? pq_wrap(metric, sum[r]) : __builtin_inff();
-        if (row < ld) E[(int64_t)f * ld + row] = e;
+        if (lr < lrem) Ef[lr] = e;
         float mm = e;
         for (int o = 32; o > 0; o >>= 1) mm = fminf(mm, __shfl_xor(mm, o));
         if (lane == 0) red[wv][r] = mm;

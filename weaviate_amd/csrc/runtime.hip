@@ -98,6 +98,10 @@ struct DBuf {
 };
 
 static inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+// u32 words per row of the PQ code store (256-row tiles of 16-segment groups,
+// pq_kernels.hip); cap is a multiple of 256
+static inline int64_t pq_mwp(int m) { return (int64_t)((m + 15) / 16) * 4; }
+static inline int pq_g16(int m) { return (m + 15) / 16; }
 
 struct wv_index {
     std::mutex mu;
@@ -237,13 +241,13 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         idx->words = words;
     }
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0) {
-        const int pw = (idx->pq_m + 3) / 4;
+        const int64_t mw = pq_mwp(idx->pq_m);
         uint32_t* pc = nullptr;
-        HIPCHK(hipMalloc(&pc, (size_t)pw * nc * sizeof(uint32_t)));
-        HIPCHK(hipMemsetAsync(pc, 0, (size_t)pw * nc * sizeof(uint32_t), idx->stream));
+        HIPCHK(hipMalloc(&pc, (size_t)mw * nc * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(pc, 0, (size_t)mw * nc * sizeof(uint32_t), idx->stream));
         if (idx->cap > 0 && idx->pq_codes)
-            HIPCHK(hipMemcpy2DAsync(pc, (size_t)nc * sizeof(uint32_t), idx->pq_codes, (size_t)idx->cap * sizeof(uint32_t),
-                                    (size_t)idx->cap * sizeof(uint32_t), pw, hipMemcpyDeviceToDevice, idx->stream));
+            HIPCHK(hipMemcpyAsync(pc, idx->pq_codes, (size_t)mw * idx->cap * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                  idx->stream));
         HIPCHK(hipStreamSynchronize(idx->stream));
         if (idx->pq_codes) hipFree(idx->pq_codes);
         idx->pq_codes = pc;
@@ -289,8 +293,16 @@ static void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots) 
     if (n <= 0) return;
     const size_t lds = (size_t)idx->pq_ks * idx->pq_ds * sizeof(float);
     dim3 grid((unsigned)((n + 255) / 256), (unsigned)idx->pq_m);
-    k_pq_encode<<<grid, 256, lds, idx->stream>>>(idx->X, idx->dpad, n, d_slots, idx->pq_ks, idx->pq_ds,
-                                                 idx->pq_centers, idx->variant, idx->pq_codes, idx->cap);
+#define WV_PE(DSV) k_pq_encode<DSV><<<grid, 256, lds, idx->stream>>>(idx->X, idx->dpad, n, d_slots, idx->pq_ks, idx->pq_ds, idx->pq_centers, idx->variant, idx->pq_codes, pq_g16(idx->pq_m))
+    switch (idx->pq_ds) {
+    case 1: WV_PE(1); break;
+    case 2: WV_PE(2); break;
+    case 4: WV_PE(4); break;
+    case 8: WV_PE(8); break;
+    case 16: WV_PE(16); break;
+    default: WV_PE(0); break;
+    }
+#undef WV_PE
 }
 
 static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const uint32_t* d_slots) {
@@ -761,9 +773,9 @@ static int pq_alloc(wv_index* idx) {
     if (!idx->pq_centers)
         HIPCHK(hipMalloc(&idx->pq_centers, (size_t)idx->pq_m * idx->pq_ks * idx->pq_ds * sizeof(float)));
     if (!idx->pq_codes && idx->cap > 0) {
-        const int pw = (idx->pq_m + 3) / 4;
-        HIPCHK(hipMalloc(&idx->pq_codes, (size_t)pw * idx->cap * sizeof(uint32_t)));
-        HIPCHK(hipMemsetAsync(idx->pq_codes, 0, (size_t)pw * idx->cap * sizeof(uint32_t), idx->stream));
+        const int64_t mw = pq_mwp(idx->pq_m);
+        HIPCHK(hipMalloc(&idx->pq_codes, (size_t)mw * idx->cap * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(idx->pq_codes, 0, (size_t)mw * idx->cap * sizeof(uint32_t), idx->stream));
     }
     return WV_OK;
 }
@@ -848,7 +860,9 @@ extern "C" int wv_index_pq_fit(wv_index* idx, uint64_t seed) {
     if (lds_c > 64 * 1024) {
         HIPCHK(hipFuncSetAttribute((const void*)k_km_assign_brute, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
         HIPCHK(hipFuncSetAttribute((const void*)k_km_assign_prune, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
-        HIPCHK(hipFuncSetAttribute((const void*)k_pq_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
+        for (const void* f : {(const void*)k_pq_encode<0>, (const void*)k_pq_encode<1>, (const void*)k_pq_encode<2>,
+                              (const void*)k_pq_encode<4>, (const void*)k_pq_encode<8>, (const void*)k_pq_encode<16>})
+            HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
     }
     const size_t lds_u = (size_t)K * ds * sizeof(double) + KM_T * sizeof(uint32_t) + (size_t)KM_T * ds * sizeof(float);
     if (lds_u > 64 * 1024)
@@ -916,14 +930,15 @@ extern "C" int wv_index_pq_codes(wv_index* idx, uint8_t* out, int64_t n) {
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
     if (!idx->pq_trained) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
-    if (n > idx->cap) return set_err(WV_ERR_INVALID, "pq_codes: n beyond capacity");
-    const int pw = (idx->pq_m + 3) / 4;
-    std::vector<uint32_t> h((size_t)pw * n);
-    HIPCHK(hipMemcpy2DAsync(h.data(), (size_t)n * sizeof(uint32_t), idx->pq_codes, (size_t)idx->cap * sizeof(uint32_t),
-                            (size_t)n * sizeof(uint32_t), pw, hipMemcpyDeviceToHost, idx->stream));
+    if (round_up(n, 256) > idx->cap) return set_err(WV_ERR_INVALID, "pq_codes: n beyond capacity");
+    const int64_t mw = pq_mwp(idx->pq_m);
+    const int64_t npad = round_up(n, 256);
+    std::vector<uint32_t> h((size_t)mw * npad);
+    HIPCHK(hipMemcpyAsync(h.data(), idx->pq_codes, (size_t)mw * npad * sizeof(uint32_t), hipMemcpyDeviceToHost, idx->stream));
     HIPCHK(hipStreamSynchronize(idx->stream));
     for (int64_t r = 0; r < n; r++)
-        for (int sg = 0; sg < idx->pq_m; sg++) out[r * idx->pq_m + sg] = (uint8_t)(h[(size_t)(sg >> 2) * n + r] >> (8 * (sg & 3)));
+        for (int sg = 0; sg < idx->pq_m; sg++)
+            out[r * idx->pq_m + sg] = (uint8_t)(h[(size_t)pq_code_word(r, sg, pq_g16(idx->pq_m))] >> (8 * (sg & 3)));
     return WV_OK;
 }
 
@@ -943,7 +958,8 @@ extern "C" int wv_index_pq_distance(wv_index* idx, const float* query, int64_t d
     if (d != idx->dims) return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
     if (n <= 0) return WV_OK;
     hipStream_t s = idx->stream;
-    const int m = idx->pq_m, K = idx->pq_ks, pw = (m + 3) / 4;
+    const int m = idx->pq_m, K = idx->pq_ks;
+    const int64_t mw = pq_mwp(m);
     DBuf Q, L, Cd, E, B, ql;
     HIPCHK(Q.ensure((size_t)d * sizeof(float)));
     HIPCHK(hipMemcpyAsync(Q.p, query, (size_t)d * sizeof(float), hipMemcpyHostToDevice, s));
@@ -953,9 +969,9 @@ extern "C" int wv_index_pq_distance(wv_index* idx, const float* query, int64_t d
                                                                       idx->pq_centers, L.as<float>());
     // pack the given codes [n][m] into the plane layout
     const int64_t ld = round_up(n, 256);
-    std::vector<uint32_t> h((size_t)pw * ld, 0);
+    std::vector<uint32_t> h((size_t)mw * ld, 0);
     for (int64_t r = 0; r < n; r++)
-        for (int sg = 0; sg < m; sg++) h[(size_t)(sg >> 2) * ld + r] |= (uint32_t)codes[r * m + sg] << (8 * (sg & 3));
+        for (int sg = 0; sg < m; sg++) h[(size_t)pq_code_word(r, sg, pq_g16(m))] |= (uint32_t)codes[r * m + sg] << (8 * (sg & 3));
     HIPCHK(Cd.ensure(h.size() * sizeof(uint32_t)));
     HIPCHK(hipMemcpyAsync(Cd.p, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     std::vector<uint32_t> ones((size_t)(ld / 32), 0xFFFFFFFFu);
@@ -968,10 +984,15 @@ extern "C" int wv_index_pq_distance(wv_index* idx, const float* query, int64_t d
     HIPCHK(ql.ensure(sizeof(int32_t)));
     HIPCHK(hipMemcpyAsync(ql.p, &zero, sizeof(int32_t), hipMemcpyHostToDevice, s));
     const int wrapm = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
-    dim3 grid((unsigned)((n + 256 * PQ_RPT - 1) / (256 * PQ_RPT)), 1);
-    k_pq_adc<<<grid, 256, (size_t)PQ_CH * K * sizeof(float), s>>>(Cd.as<uint32_t>(), ld, m, K, V.as<uint32_t>(), n,
-                                                                  L.as<float>(), ql.as<int32_t>(), wrapm, ld,
-                                                                  E.as<float>(), B.as<float>());
+    dim3 grid(1, (unsigned)((n + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
+    if (K == 256)
+        k_pq_adc<256><<<grid, 256, (size_t)PQ_CH * K * sizeof(float), s>>>(Cd.as<uint32_t>(), pq_g16(m), m, K, V.as<uint32_t>(), n,
+                                                                       L.as<float>(), ql.as<int32_t>(), wrapm, ld,
+                                                                       E.as<float>(), B.as<float>());
+    else
+        k_pq_adc<0><<<grid, 256, (size_t)PQ_CH * K * sizeof(float), s>>>(Cd.as<uint32_t>(), pq_g16(m), m, K, V.as<uint32_t>(), n,
+                                                                     L.as<float>(), ql.as<int32_t>(), wrapm, ld,
+                                                                     E.as<float>(), B.as<float>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, E.p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -1024,9 +1045,13 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     for (int64_t g0 = 0; g0 < nq; g0 += G) {
         const int F = (int)std::min<int64_t>(G, nq - g0);
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
-        dim3 grid((unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)), (unsigned)F);
-        k_pq_adc<<<grid, 256, lds_adc, s>>>(idx->pq_codes, idx->cap, m, K, valid, nslots, idx->lut.as<float>(),
-                                            qlist + g0, wrapm, ld, idx->rE.as<float>(), idx->rB.as<float>());
+        dim3 grid((unsigned)F, (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
+        if (K == 256)
+            k_pq_adc<256><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots, idx->lut.as<float>(),
+                                                     qlist + g0, wrapm, ld, idx->rE.as<float>(), idx->rB.as<float>());
+        else
+            k_pq_adc<0><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots, idx->lut.as<float>(),
+                                                   qlist + g0, wrapm, ld, idx->rE.as<float>(), idx->rB.as<float>());
         HIPCHK(hipGetLastError());
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
         // the worker heap (addResult == insertToHeap) in id order, extracted ascending
