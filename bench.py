@@ -137,6 +137,22 @@ def cpu_baseline_pq(index, n_sample: int, nq: int, threads: int, n_full: int):
     }
 
 
+def measured_traffic(workload: str, n_local: int, dims: int, batch: int):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass
+    (profiles/*_pmc_<workload>.json, tools/pmc_traffic.sh) when it was taken on
+    this exact configuration; None otherwise."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{workload}.json"))):
+        try:
+            rec = json.load(open(path))
+        except Exception:
+            continue
+        if (rec.get("corpus_rows"), rec.get("dims"), rec.get("query_batch")) == (n_local, dims, batch):
+            best = rec.get("hbm_bytes_per_launch")
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", choices=["c3", "bq", "pq"], default="c3",
@@ -260,6 +276,8 @@ def main():
     total_q = B * args.steps
     value = total_q / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    if args.traffic_bytes is None:
+        args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B)
     if pq:
         # dominant kernel k_pq_adc: one LUT lookup (LDS gather) + fp32 add per
         # (query, row, segment); the codes of a tile are shared by the group's
