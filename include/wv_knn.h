@@ -186,8 +186,16 @@ typedef struct wv_stats {
 } wv_stats;
 int wv_index_stats(wv_index *idx, wv_stats *out);
 
+/* Diagnostic hook (tests): the last MFMA batch's candidates [nq][KP]:
+ * approximate distances A, exact distances E, slots I (0xFFFFFFFF = none), and
+ * per-query the eps of k_finalize's exactness proof.  Call with A == NULL to
+ * get *KP only. */
+int wv_index_debug_candidates(wv_index *idx, float *A, float *E, uint32_t *I, float *eps, int64_t nq, int32_t *KP);
+
 /* tuning / testing knobs: "margin" (extra candidates, default 8),
  * "force_replay" (1 = resolve every query by heap replay), "spans" (0 = auto),
+ * "kernel" (select kernel: 4 = bf16x3 MFMA (default for the exact fp32 path),
+ * 3 = f32 MFMA ring, 2/1 older f32 forms), "bq_kernel" (1 = generic BQ kernels),
  * "timing" (1 = record kernel times with HIP events) */
 int wv_index_set_option(wv_index *idx, const char *key, int64_t value);
 

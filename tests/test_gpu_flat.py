@@ -198,7 +198,7 @@ def test_search_by_vector_distance(wv, oracle):
     assert len(ids) == 31
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("kernel", [1, 2, 3, 4])
 @pytest.mark.parametrize("metric,kind,n,d,k", [("cosine", 0, 9000, 768, 10), ("l2-squared", 0, 7000, 96, 24),
                                                ("dot", 1, 5000, 64, 5)])
 def test_select_kernel_variants(wv, oracle, kernel, metric, kind, n, d, k):
@@ -289,4 +289,25 @@ def test_bq_generic_kernels_equal_lds_kernels(wv, oracle):
     b = idx.search_by_vector_batch(queries, 10)
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
+    idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,d", [("cosine", 0, 768), ("l2-squared", 0, 128), ("dot", 0, 300),
+                                           ("l2-squared", 2, 960)])
+def test_bf16x3_error_within_proof_bound(wv, oracle, metric, kind, d):
+    """The approximate distances of the bf16x3 select kernel (candidates A)
+    stay within the eps the exactness proof uses."""
+    n = 20000
+    data = gen(oracle, kind, 91, n, d)
+    queries = gen(oracle, kind, 92, 256, d)
+    idx = wv.FlatIndex(distance=metric, variant="avx256")
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    idx.search_by_vector_batch(queries, 10)
+    A, E, I, eps = idx.debug_candidates(len(queries))
+    ok = I != 0xFFFFFFFF
+    err = np.abs(A[ok].astype(np.float64) - E[ok].astype(np.float64))
+    bound = np.broadcast_to(eps[:, None], A.shape)[ok]
+    ratio = (err / bound).max()
+    print(f"bf16x3 max |A-E| / eps = {ratio:.4f}")
+    assert (err <= bound).all(), f"max err/eps = {ratio}"
     idx.close()

@@ -93,6 +93,7 @@ SIGNATURES = {
     "wv_normalize_batch": (C.c_int, [i32, pf32, i64, i64, pf32]),
     "wv_gen_device": (C.c_int, [i32, i32, u64, u64, i64, i64, P, P]),
     "wv_index_stats": (C.c_int, [P, C.POINTER(WvStats)]),
+    "wv_index_debug_candidates": (C.c_int, [P, pf32, pf32, C.POINTER(C.c_uint32), pf32, i64, pi32]),
     "wv_index_pq_fit": (C.c_int, [P, u64]),
     "wv_index_pq_set_centers": (C.c_int, [P, pf32, i64]),
     "wv_index_pq_centers": (C.c_int, [P, pf32, i64]),

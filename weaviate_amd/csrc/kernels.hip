@@ -98,6 +98,11 @@ struct SelectArgs {
     int qgroup;               // query blocks per XCD cell (divides nqb)
     float* outA;              // [nq_pad][nspans][KP]
     uint32_t* outI;
+    // bf16x3 kernel (k_mfma_select_bf3): hi/lo bf16 planes of X and Q
+    const uint16_t* Xh;       // [cap][dpad]
+    const uint16_t* Xl;
+    const uint16_t* Qh;       // [nq_pad][dpad]
+    const uint16_t* Ql;
 };
 
 template <int R>

@@ -1,0 +1,259 @@
+// kernels_bf3.hip -- the approximate-distance select kernel on bf16 MFMA with
+// a three-term split ("bf16x3"): every fp32 value v is stored as
+// vh = bf16(v) and vl = bf16(v - vh), and
+//     q.x  ~  qh.xh + qh.xl + ql.xh       (three v_mfma_f32_32x32x16_bf16)
+// whose error against the exact dot product is bounded by
+//     (3.05 * 2^-16 + gamma'_{3d+16}) * sum|q_i||x_i|,
+// so k_finalize's exactness proof carries over with a wider eps.  Per 32x32
+// block and 16 k this is 3 x 32 MFMA cycles instead of 8 x 64 for the f32-in
+// MFMA (5.3x less matrix-core time).
+//
+// Structure = k_mfma_select3 (8 waves, 128-query x 256-row tiles, 3-deep LDS
+// ring filled by global_load_lds_dwordx4, one barrier per BK=32 slice, the
+// same fused top-KP selection epilogue).  A ring slot holds, per plane, the
+// BK=32 slice of every row as 64 B = four 16-B chunks (8 bf16 each); chunk c
+// of row r sits at physical chunk c ^ ((r >> 2) & 3), which makes the
+// 16-lane ds_read_b128 groups (16 consecutive rows) conflict-free.
+#pragma once
+
+namespace wv {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int SLOT_BF3 = (BN3 + QB) * BK * 2 * 2;  // bytes per ring slot: 2 planes x bf16 = 48 KiB
+
+__device__ __forceinline__ int swz_bf3(int r) { return (r >> 2) & 3; }
+
+__device__ __forceinline__ bf16x8_t lds_ld8bf(const unsigned char* p) {
+    bf16x8_t v;
+    const unsigned off = (unsigned)(size_t)((__attribute__((address_space(3))) const unsigned char*)p);
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(off));
+    return v;
+}
+
+template <int METRIC, int R>
+__global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int KP = a.KP;
+    const int C = a.C;
+    unsigned char* ring = reinterpret_cast<unsigned char*>(smem);  // [NBUF3][SLOT_BF3]
+    float* thr = reinterpret_cast<float*>(ring + NBUF3 * SLOT_BF3);  // QB
+    int* cnt = reinterpret_cast<int*>(thr + QB);                     // QB
+    int* flags = cnt + QB;                                           // 4
+    float* cbA = reinterpret_cast<float*>(flags + 4);                // QB*C
+    uint32_t* cbI = reinterpret_cast<uint32_t*>(cbA + QB * C);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;          // 0..7
+    const int wq = wave & 1, wx = wave >> 1;   // 2 query halves x 4 row quarters
+    const int li = lane & 31, lh = lane >> 5;
+
+    const int total = a.nqb * a.nspans;
+    const int b = blockIdx.x;
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int QG = a.qgroup;
+    const int cell = logical / QG, qi = logical % QG;
+    const int group = cell / a.nspans;
+    const int span = cell % a.nspans;
+    const int qb = group * QG + qi;
+    const int q0 = qb * QB;
+
+    for (int jq = 0; jq < QB / 8; jq++) {
+        const int q = wave + 8 * jq;
+        if (q0 + q >= a.nq) continue;
+        const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
+        for (int e = lane; e < KP; e += 64) { a.outA[base + e] = __builtin_inff(); a.outI[base + e] = NO_ID; }
+    }
+    if (tid < QB) { thr[tid] = __builtin_inff(); cnt[tid] = 0; }
+    if (tid == 0) { flags[0] = 0; flags[1] = 0; }
+
+    const int64_t t0 = (int64_t)span * a.tiles_per_span;
+    int64_t t1 = t0 + a.tiles_per_span;
+    if (t1 > a.ntiles) t1 = a.ntiles;
+    const int nk = a.dpad / BK;
+    const int64_t total_steps = t1 > t0 ? (t1 - t0) * nk : 0;
+
+    // DMA pieces (1 KiB = 16 rows x 64 B) of this wave per slice: 2 of Xh, 2 of
+    // Xl (rows 32w .. 32w+31), 1 of Qh, 1 of Ql (rows 16w .. 16w+15).  Lane L
+    // writes LDS row L>>2, physical chunk L&3 = logical chunk (L&3) ^ swz(row).
+    const int prow = lane >> 2, pchunk = lane & 3;
+    const int64_t ldb = (int64_t)a.dpad * 2;  // bytes per row of a plane
+    auto issue = [&](int64_t step) {
+        const int64_t tile = t0 + step / nk;
+        const int kb = (int)(step % nk);
+        unsigned char* slot = ring + (int)(step % NBUF3) * SLOT_BF3;
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+            const int row = 32 * wave + 16 * p + prow;
+            const int c = pchunk ^ swz_bf3(row);
+            const int64_t off = (tile * BN3 + row) * ldb + kb * 64 + 16 * c;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned char*>(a.Xh) + off,
+                                             (lds_ptr_t)(slot + (32 * wave + 16 * p) * 64), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned char*>(a.Xl) + off,
+                                             (lds_ptr_t)(slot + BN3 * 64 + (32 * wave + 16 * p) * 64), 16, 0, 0);
+        }
+        {
+            const int row = 16 * wave + prow;
+            const int c = pchunk ^ swz_bf3(row);
+            const int64_t off = (int64_t)(q0 + row) * ldb + kb * 64 + 16 * c;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned char*>(a.Qh) + off,
+                                             (lds_ptr_t)(slot + 2 * BN3 * 64 + (16 * wave) * 64), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned char*>(a.Ql) + off,
+                                             (lds_ptr_t)(slot + 2 * BN3 * 64 + QB * 64 + (16 * wave) * 64), 16, 0, 0);
+        }
+    };
+
+    f32x16 acc[2][2];
+    int epoch = 0;
+    if (total_steps > 0) issue(0);
+    if (total_steps > 1) issue(1);
+
+    for (int64_t step = 0; step < total_steps; step++) {
+        const int64_t tile = t0 + step / nk;
+        const int kb = (int)(step % nk);
+        if (step + 1 < total_steps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // everyone's pieces landed; slot (step+2)%3 is free
+        __builtin_amdgcn_sched_barrier(0);
+        if (step + 2 < total_steps) issue(step + 2);
+        const unsigned char* cur = ring + (int)(step % NBUF3) * SLOT_BF3;
+        if (kb == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+        }
+        // all 16 fragment reads up front (invisible to hipcc's waitcnt logic);
+        // k16 step 0's MFMAs wait for its 8 reads
+        bf16x8_t XH[2][2], XL[2][2], QH[2][2], QL[2][2];  // [kk][block]
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int xr = 64 * wx + 32 * i + li;
+                const int qr = 64 * wq + 32 * i + li;
+                const int xc = (2 * kk + lh) ^ swz_bf3(xr);
+                const int qc = (2 * kk + lh) ^ swz_bf3(qr);
+                XH[kk][i] = lds_ld8bf(cur + xr * 64 + 16 * xc);
+                XL[kk][i] = lds_ld8bf(cur + BN3 * 64 + xr * 64 + 16 * xc);
+                QH[kk][i] = lds_ld8bf(cur + 2 * BN3 * 64 + qr * 64 + 16 * qc);
+                QL[kk][i] = lds_ld8bf(cur + 2 * BN3 * 64 + QB * 64 + qr * 64 + 16 * qc);
+            }
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            if (kk == 0) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XH[kk][i], QH[kk][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XH[kk][i], QL[kk][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XL[kk][i], QH[kk][j], acc[i][j], 0, 0, 0);
+                }
+        }
+
+        if (kb == nk - 1) {
+            // ---------------- epilogue: selection over this 128 x 256 tile (as k_mfma_select3) ----------------
+            const int64_t row0 = tile * BN3;
+            float qn[2];
+            int qidx[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                qidx[j] = 64 * wq + 32 * j + li;
+                qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
+            }
+            const uint32_t* vb = a.valid + (row0 >> 5);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    bool ok = (vb[rt >> 5] >> (rt & 31)) & 1u;
+                    float xn = (METRIC == L2) ? a.xnorm2[row0 + rt] : 0.f;
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        float dot = acc[i][j][r];
+                        float v;
+                        if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
+                        else if (METRIC == DOT) v = -dot;
+                        else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
+                        bool qok = (q0 + qidx[j]) < a.nq;
+                        acc[i][j][r] = (ok && qok) ? v : __builtin_inff();
+                    }
+                }
+            }
+            uint64_t pending = ~0ull;
+            for (;;) {
+                ++epoch;
+                float th[2] = {thr[qidx[0]], thr[qidx[1]]};
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+#pragma unroll
+                        for (int j = 0; j < 2; j++) {
+                            const int vi = (i * 16 + r) * 2 + j;
+                            if (!((pending >> vi) & 1ull)) continue;
+                            float v = acc[i][j][r];
+                            if (v < th[j]) {
+                                int slot = atomicAdd(&cnt[qidx[j]], 1);
+                                if (slot < C) {
+                                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                                    cbA[qidx[j] * C + slot] = v;
+                                    cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
+                                    pending &= ~(1ull << vi);
+                                }
+                                flags[0] = epoch;
+                            } else {
+                                pending &= ~(1ull << vi);
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                if (flags[0] != epoch) break;
+                for (int jq = 0; jq < QB / 8; jq++) {
+                    const int q = wave + 8 * jq;
+                    const int c = cnt[q];
+                    if (c == 0) continue;
+                    const int nc = c < C ? c : C;
+                    const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
+                    merge_query_list<R>(a.outA + base, a.outI + base, cbA + q * C, cbI + q * C, KP, C, nc, lane,
+                                        &thr[q]);
+                    if (lane == 0) {
+                        if (c > C) flags[1] = epoch;
+                        cnt[q] = 0;
+                    }
+                }
+                __syncthreads();
+                if (flags[1] != epoch) break;
+            }
+        }
+    }
+}
+
+// bf16 hi/lo split of fp32 rows: hi = bf16(v) (round to nearest even),
+// lo = bf16(v - hi) (v - hi is exact in fp32).  Thread per element of the
+// listed rows (slots) or of rows [0, n).
+__global__ void k_split_bf16(const float* __restrict__ src, int64_t n, int dpad, const uint32_t* __restrict__ slots,
+                             uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * dpad) return;
+    const int64_t r = i / dpad;
+    const int c = (int)(i % dpad);
+    const int64_t row = slots ? (int64_t)slots[r] : r;
+    const int64_t o = row * dpad + c;
+    const float v = src[o];
+    const __bf16 h = (__bf16)v;
+    const float hf = (float)h;
+    const __bf16 l = (__bf16)(v - hf);
+    hi[o] = __builtin_bit_cast(uint16_t, h);
+    lo[o] = __builtin_bit_cast(uint16_t, l);
+}
+
+}  // namespace wv

@@ -25,6 +25,7 @@
 #include "kernels.hip"
 #include "bq_kernels.hip"
 #include "pq_kernels.hip"
+#include "kernels_bf3.hip"
 
 using namespace wv;
 
@@ -129,11 +130,18 @@ struct wv_index {
     int pq_m = 0, pq_ks = 0, pq_ds = 0, pq_training_limit = 0, pq_rescore = 1, pq_trained = 0;
     float* pq_centers = nullptr;
     uint32_t* pq_codes = nullptr;
+    // bf16 hi/lo planes of X for k_mfma_select_bf3 ([cap][dpad] each)
+    int use_bf3 = 0;
+    float last_eps_scale = 0.f, last_eps_base = 0.f;  // exactness-proof eps of the last MFMA batch (debug hook)
+    int64_t last_nq = 0;
+    int last_KP = 0;
+    uint16_t* Xh = nullptr;
+    uint16_t* Xl = nullptr;
     std::vector<uint8_t> h_present;
     uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
     int64_t npresent = 0;
 
-    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN;
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, qh, ql;
 
     int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -159,6 +167,9 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     idx->device = cfg->device;
     idx->id_base = cfg->id_base;
     idx->root_path = cfg->root_path ? cfg->root_path : "";
+    // bf16x3 select kernel for the exact fp32 path (kernels_bf3.hip)
+    idx->use_bf3 = (cfg->compression == WV_COMPRESSION_NONE && cfg->metric != WV_METRIC_HAMMING) ? 1 : 0;
+    idx->kernel_opt = idx->use_bf3 ? 4 : 3;
     if (cfg->compression == WV_COMPRESSION_PQ) {
         idx->pq_m = cfg->pq_segments;
         idx->pq_ks = cfg->pq_centroids;
@@ -186,7 +197,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
-                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN})
+                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql})
         b->release();
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
@@ -195,6 +206,8 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->codes) hipFree(idx->codes);
     if (idx->pq_centers) hipFree(idx->pq_centers);
     if (idx->pq_codes) hipFree(idx->pq_codes);
+    if (idx->Xh) hipFree(idx->Xh);
+    if (idx->Xl) hipFree(idx->Xl);
     if (idx->ev0) hipEventDestroy(idx->ev0);
     if (idx->ev1) hipEventDestroy(idx->ev1);
     if (idx->stream) hipStreamDestroy(idx->stream);
@@ -239,6 +252,24 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         if (idx->codes) hipFree(idx->codes);
         idx->codes = cd;
         idx->words = words;
+    }
+    if (idx->use_bf3) {
+        uint16_t *xh = nullptr, *xl = nullptr;
+        const size_t pb = (size_t)nc * idx->dpad * sizeof(uint16_t);
+        HIPCHK(hipMalloc(&xh, pb));
+        HIPCHK(hipMalloc(&xl, pb));
+        HIPCHK(hipMemsetAsync(xh, 0, pb, idx->stream));
+        HIPCHK(hipMemsetAsync(xl, 0, pb, idx->stream));
+        if (idx->cap > 0 && idx->Xh) {
+            const size_t ob = (size_t)idx->cap * idx->dpad * sizeof(uint16_t);
+            HIPCHK(hipMemcpyAsync(xh, idx->Xh, ob, hipMemcpyDeviceToDevice, idx->stream));
+            HIPCHK(hipMemcpyAsync(xl, idx->Xl, ob, hipMemcpyDeviceToDevice, idx->stream));
+        }
+        HIPCHK(hipStreamSynchronize(idx->stream));
+        if (idx->Xh) hipFree(idx->Xh);
+        if (idx->Xl) hipFree(idx->Xl);
+        idx->Xh = xh;
+        idx->Xl = xl;
     }
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0) {
         const int64_t mw = pq_mwp(idx->pq_m);
@@ -316,6 +347,11 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
         k_prepare_rows<L2><<<grid, 256, 0, idx->stream>>>(d_in, n, idx->dims, d_slots, idx->X, idx->dpad, idx->xnorm2,
                                                           idx->present, idx->d_maxn2);
         break;
+    }
+    if (idx->use_bf3) {
+        const int64_t ne = n * idx->dpad;
+        k_split_bf16<<<(unsigned)((ne + 255) / 256), 256, 0, idx->stream>>>(idx->X, n, idx->dpad, d_slots, idx->Xh,
+                                                                           idx->Xl);
     }
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) launch_pq_encode(idx, n, d_slots);
     if (idx->compression == WV_COMPRESSION_BQ) {  // Preload: quantizer.Encode of the stored row (flat/index.go:376)
@@ -487,6 +523,30 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     return WV_OK;
 }
 
+extern "C" int wv_index_debug_candidates(wv_index* idx, float* A, float* E, uint32_t* I, float* eps, int64_t nq,
+                                         int32_t* KP) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (nq != idx->last_nq || idx->last_KP == 0) return set_err(WV_ERR_INVALID, "debug_candidates: no matching batch");
+    *KP = idx->last_KP;
+    const size_t m = (size_t)nq * idx->last_KP;
+    if (A) {
+        HIPCHK(hipMemcpyAsync(A, idx->candA.p, m * sizeof(float), hipMemcpyDeviceToHost, idx->stream));
+        HIPCHK(hipMemcpyAsync(E, idx->candE.p, m * sizeof(float), hipMemcpyDeviceToHost, idx->stream));
+        HIPCHK(hipMemcpyAsync(I, idx->candI.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, idx->stream));
+        std::vector<float> qn2((size_t)nq);
+        HIPCHK(hipMemcpyAsync(qn2.data(), idx->qn2.p, (size_t)nq * sizeof(float), hipMemcpyDeviceToHost, idx->stream));
+        HIPCHK(hipStreamSynchronize(idx->stream));
+        for (int64_t q = 0; q < nq; q++) {  // k_finalize's eps
+            const float qn = std::sqrt(qn2[q]);
+            if (idx->metric == WV_METRIC_L2_SQUARED) { float t = qn + idx->last_eps_base; eps[q] = idx->last_eps_scale * t * t; }
+            else eps[q] = idx->last_eps_scale * (qn * idx->last_eps_base + 1.f);
+        }
+    }
+    return WV_OK;
+}
+
 extern "C" int wv_index_stats(wv_index* idx, wv_stats* out) {
     if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
     std::lock_guard<std::mutex> g(idx->mu);
@@ -557,6 +617,13 @@ static int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, in
     else
         k_copy_pad_rows<<<(unsigned)((nq * idx->dpad + 255) / 256), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
     k_row_norm2<<<(unsigned)((nq_pad + 3) / 4), 256, 0, s>>>(Qn, nq_pad, idx->dpad, idx->qn2.as<float>());
+    if (idx->use_bf3) {
+        HIPCHK(idx->qh.ensure((size_t)nq_pad * idx->dpad * sizeof(uint16_t)));
+        HIPCHK(idx->ql.ensure((size_t)nq_pad * idx->dpad * sizeof(uint16_t)));
+        const int64_t ne = nq_pad * idx->dpad;
+        k_split_bf16<<<(unsigned)((ne + 255) / 256), 256, 0, s>>>(Qn, nq_pad, idx->dpad, nullptr, idx->qh.as<uint16_t>(),
+                                                                 idx->ql.as<uint16_t>());
+    }
     HIPCHK(hipGetLastError());
     return WV_OK;
 }
@@ -1136,8 +1203,8 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     int32_t* flags = o_flags ? o_flags : idx->oF.as<int32_t>();
 
     if (mfma_ok) {
-        const int kver = idx->kernel_opt;
-        const int64_t bn = kver == 3 ? BN3 : BN;
+        const int kver = (idx->kernel_opt == 4 && !idx->use_bf3) ? 3 : idx->kernel_opt;
+        const int64_t bn = kver >= 3 ? BN3 : BN;
         const int64_t ntiles = (idx->hiwater + bn - 1) / bn;
         const int nqb = (int)(nq_pad / QB);
         int qgroup = 1;
@@ -1145,7 +1212,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
             if (nqb % g == 0) { qgroup = g; break; }
         // ~1024 workgroups (2 per CU resident, 2 waves of them); keep the
         // workgroup count a multiple of 8 for the XCD mapping when possible
-        const int64_t target_wg = kver == 3 ? 768 : 1024;
+        const int64_t target_wg = kver >= 3 ? 768 : 1024;
         int64_t nspans = idx->spans_opt > 0 ? idx->spans_opt : std::max<int64_t>(8, (target_wg + nqb - 1) / nqb);
         nspans = std::min<int64_t>(nspans, ntiles);
         int64_t tps = (ntiles + nspans - 1) / nspans;
@@ -1160,12 +1227,14 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         a.Q = Qn; a.qnorm2 = idx->qn2.as<float>(); a.nq = (int)nq; a.dpad = idx->dpad;
         a.tiles_per_span = (int)tps; a.nspans = (int)nspans; a.nqb = nqb; a.KP = KP; a.qgroup = qgroup;
         a.outA = idx->spanA.as<float>(); a.outI = idx->spanI.as<uint32_t>();
+        a.Xh = idx->Xh; a.Xl = idx->Xl; a.Qh = idx->qh.as<uint16_t>(); a.Ql = idx->ql.as<uint16_t>();
         // candidate buffer: as large as fits two workgroups per CU (<= 80 KiB each)
         const bool v2 = kver == 2;
-        const int64_t fixed = kver == 3 ? (int64_t)(NBUF3 * STG3 + QB * 2 + 4) * (int64_t)sizeof(float)
+        const int64_t fixed = kver == 4 ? (int64_t)NBUF3 * SLOT_BF3 + (int64_t)(QB * 2 + 4) * (int64_t)sizeof(float)
+                              : kver == 3 ? (int64_t)(NBUF3 * STG3 + QB * 2 + 4) * (int64_t)sizeof(float)
                               : v2 ? (int64_t)(2 * (BN + QB) * BK + QB * 2 + 4) * (int64_t)sizeof(float)
                                    : (int64_t)(2 * QB * LDSROW + QB * KP * 2 + QB * 2 + 4) * (int64_t)sizeof(float);
-        const int64_t budget = kver == 3 ? 160 * 1024 : 80 * 1024;
+        const int64_t budget = kver >= 3 ? 160 * 1024 : 80 * 1024;
         int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(4, (budget - fixed) / (QB * 8)));
         if (idx->cbuf_opt > 0) C = std::min(64 - KP, idx->cbuf_opt);
         size_t lds = (size_t)(fixed + (int64_t)QB * C * 8);
@@ -1182,7 +1251,18 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select3<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
         k_mfma_select3<M, 1><<<grid, 512, lds, s>>>(a);                                                   \
     } while (0)
-        if (kver == 3) {
+#define WV_SELB(M)                                                                                         \
+    do {                                                                                                   \
+        HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select_bf3<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_mfma_select_bf3<M, 1><<<grid, 512, lds, s>>>(a);                                                 \
+    } while (0)
+        if (kver == 4) {
+            switch (idx->metric) {
+            case WV_METRIC_L2_SQUARED: WV_SELB(L2); break;
+            case WV_METRIC_DOT: WV_SELB(DOT); break;
+            default: WV_SELB(COSINE); break;
+            }
+        } else if (kver == 3) {
             switch (idx->metric) {
             case WV_METRIC_L2_SQUARED: WV_SEL3(L2); break;
             case WV_METRIC_DOT: WV_SEL3(DOT); break;
@@ -1195,6 +1275,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
             default: if (v2) WV_SEL(k_mfma_select2, COSINE); else WV_SEL(k_mfma_select, COSINE); break;
             }
         }
+#undef WV_SELB
 #undef WV_SEL3
 #undef WV_SEL
         HIPCHK(hipGetLastError());
@@ -1217,8 +1298,21 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         HIPCHK(hipStreamSynchronize(s));
         float maxn2;
         memcpy(&maxn2, &mx, sizeof(float));
-        const float eps_scale = (float)(2.0 * gamma_n(idx->dpad + 4) * 1.05 + 1e-12);
+        // bf16x3 (kver 4): + 2 x (3.05 * 2^-16 split error + gamma'_h accumulation).  Each
+        // product passes through at most h = 3*dpad/16 + 16 additions (the 3*dpad/16 chained
+        // MFMAs that add into the accumulator, plus at most 16 inside one MFMA's 16-product
+        // sum), so the recursive-summation bound is gamma_h * sum|terms| for any internal
+        // order; u' = 2^-22 (4x the fp32 unit roundoff) assumes nothing about the rounding mode.
+        const double u4 = 2.384185791015625e-07;
+        const double hdep = 3.0 * idx->dpad / 16.0 + 16.0;
+        const double g3 = hdep * u4 / (1.0 - hdep * u4);
+        const double extra = kver == 4 ? 2.0 * (3.05 * 1.52587890625e-05 + g3) : 0.0;
+        const float eps_scale = (float)((2.0 * gamma_n(idx->dpad + 4) + extra) * 1.05 + 1e-12);
         const float eps_base = (float)(std::sqrt((double)maxn2) * (1.0 + 1e-6));
+        idx->last_eps_scale = eps_scale;
+        idx->last_eps_base = eps_base;
+        idx->last_nq = nq;
+        idx->last_KP = KP;
         k_finalize<1><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(
             idx->candA.as<float>(), idx->candI.as<uint32_t>(), idx->candE.as<float>(), idx->qn2.as<float>(), (int)nq,
             KP, k, kout, eps_scale, eps_base, idx->metric == WV_METRIC_L2_SQUARED ? L2 : DOT, idx->id_base, o_ids,

@@ -114,6 +114,18 @@ class FlatIndex:
     def compressed(self) -> bool:  # flat.Compressed (flat/index.go): BQ quantizer built at New; PQ once fit
         return self.bq or (self.pq and self.pq_info()["trained"])
 
+    def debug_candidates(self, nq: int):
+        """Diagnostic: (A, E, slots, eps) of the last MFMA batch (see wv_knn.h)."""
+        kp = C.c_int32()
+        check(self._l.wv_index_debug_candidates(self._h, None, None, None, None, int(nq), C.byref(kp)))
+        A = np.zeros((nq, kp.value), np.float32)
+        E = np.zeros_like(A)
+        I = np.zeros((nq, kp.value), np.uint32)
+        eps = np.zeros(nq, np.float32)
+        check(self._l.wv_index_debug_candidates(self._h, _fptr(A), _fptr(E), I.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                _fptr(eps), int(nq), C.byref(kp)))
+        return A, E, I, eps
+
     # -- product quantizer (compressionhelpers.ProductQuantizer) -----------
     def pq_info(self) -> dict:
         out = (C.c_int32 * 4)()
