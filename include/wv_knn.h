@@ -151,6 +151,28 @@ int wv_index_replay(wv_index *idx, const float *d_queries, int64_t nq, int64_t d
                     const int32_t *h_in_len, int32_t extract, uint64_t *h_out_ids, float *h_out_dists,
                     int32_t *h_out_len);
 
+/* Sharded BQ search (flat.searchByVectorQuantized over contiguous id-range
+ * shards): the reference R-heap (flat/index.go:470-487) runs
+ * across the shards in id order.
+ * 1. wv_index_bq_begin: every shard, in parallel: encode the queries
+ *    (normalised for cosine) and compute this shard's hamming block minima.
+ * 2. wv_index_bq_replay: shard r continues the heaps of shard r-1 (device
+ *    [nq][R] ids/dists in layout order + [nq] lengths; NULL = empty heaps);
+ *    pop = 0 writes the heap states, pop = 1 (last shard) the candidates in
+ *    the reference's pop order.  R = max(rescore_limit, k).
+ * 3. wv_index_bq_rescore: exact SingleDist of the candidates this shard holds
+ *    into d_E (other entries untouched).
+ * 4. wv_bq_final: the rescoring heap (:525-531) over the candidates, with E
+ *    gathered [world][nq][R]: the entry of an id comes from shard
+ *    min(id / id_stride, world - 1).  Outputs [nq][k]. */
+int wv_index_bq_begin(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k, void *stream);
+int wv_index_bq_replay(wv_index *idx, const uint64_t *d_in_ids, const float *d_in_dists, const int32_t *d_in_len,
+                       int32_t pop, uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_len, void *stream);
+int wv_index_bq_rescore(wv_index *idx, const uint64_t *d_ids, const int32_t *d_len, float *d_E, void *stream);
+int wv_bq_final(int32_t device, int64_t nq, int32_t R, int32_t k, int32_t world, uint64_t id_stride,
+                const uint64_t *d_ids, const int32_t *d_len, const float *d_E, uint64_t *d_out_ids, float *d_out_dists,
+                int32_t *d_out_counts, void *stream);
+
 /* Merge shard-local candidate lists (mode-1 search outputs of G shards, each
  * [nq x (k+1)], gathered shard-major on this device) into the final top-k by
  * (distance, id); d_out_flags[q]=1 when a shard flagged q or the merged top

@@ -1,0 +1,162 @@
+"""CPU, world_size 2 and 3 (gloo): the sharded BQ protocol of
+weaviate_amd/sharded.py (per-rank block minima -> R-heap replay chained across
+the ranks in id order -> per-rank rescoring -> all-gather -> rescoring heap)
+reproduces the single BQ index (flat.searchByVectorQuantized) exactly,
+including hamming tie order.  The per-rank engine is an oracle-backed stand-in
+(test infrastructure); the GPU kernels behind the same interface are covered
+by the gpu-marked tests.
+"""
+import ctypes as C
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _H(C.Structure):
+    _fields_ = [("id", C.POINTER(C.c_uint64)), ("dist", C.POINTER(C.c_float)), ("len", C.c_int)]
+
+
+class OracleBQShardBackend:
+    """Stand-in for GpuBQShardBackend over rows [begin, end) of the corpus."""
+
+    def __init__(self, orc, metric, corpus, begin, end, rescore_limit):
+        self.o = orc
+        self.metric = metric
+        self.n, self.d = corpus.shape
+        self.store = corpus.copy()
+        if metric == orc.COSINE:
+            orc.lib().or_normalize_rows(orc.f(self.store), self.n, self.d)
+        self.codes = np.stack([orc.bq_encode(x) for x in self.store])
+        self.begin, self.end = begin, end
+        self.rescore_limit = rescore_limit
+        lib = orc.lib()
+        lib.or_insert_to_heap.argtypes = [C.POINTER(_H), C.c_int, C.c_uint64, C.c_float]
+        lib.or_heap_pop.argtypes = [C.POINTER(_H), C.POINTER(C.c_uint64), C.POINTER(C.c_float)]
+
+    def R(self, k):
+        return max(self.rescore_limit, k)
+
+    def bq_begin(self, q, k):
+        self.k = k
+        qn = q.numpy()
+        self.q = np.stack([self.o.normalize(x) if self.metric == self.o.COSINE else x for x in qn])
+        self.qc = np.stack([self.o.bq_encode(x) for x in self.q])
+
+    def _heap(self, R):
+        hid = np.zeros(R + 1, np.uint64)
+        hd = np.zeros(R + 1, np.float32)
+        return hid, hd, _H(hid.ctypes.data_as(C.POINTER(C.c_uint64)), hd.ctypes.data_as(C.POINTER(C.c_float)), 0)
+
+    def bq_replay(self, state, pop):
+        lib = self.o.lib()
+        R = self.R(self.k)
+        nq = self.q.shape[0]
+        oi = np.zeros((nq, R), np.int64)
+        od = np.zeros((nq, R), np.float32)
+        on = np.zeros(nq, np.int32)
+        for i in range(nq):
+            hid, hd, h = self._heap(R)
+            if state is not None:
+                ln = int(state[2][i])
+                hid[:ln] = state[0][i, :ln].numpy().astype(np.uint64)
+                hd[:ln] = state[1][i, :ln].numpy()
+                h.len = ln
+            for s in range(self.begin, self.end):
+                dist_ = self.o.hamming_bitwise(self.codes[s], self.qc[i])
+                lib.or_insert_to_heap(C.byref(h), R, s, dist_)
+            n = h.len
+            if pop:
+                for j in range(n):
+                    a, b = C.c_uint64(), C.c_float()
+                    lib.or_heap_pop(C.byref(h), C.byref(a), C.byref(b))
+                    oi[i, j], od[i, j] = a.value, b.value
+            else:
+                oi[i, :n] = hid[:n].astype(np.int64)
+                od[i, :n] = hd[:n]
+            on[i] = n
+        return torch.from_numpy(oi), torch.from_numpy(od), torch.from_numpy(on)
+
+    def bq_rescore(self, ids, ln):
+        ids, ln = ids.numpy(), ln.numpy()
+        E = np.zeros(ids.shape, np.float32)
+        for i in range(ids.shape[0]):
+            for j in range(ln[i]):
+                s = int(ids[i, j])
+                if self.begin <= s < self.end:
+                    E[i, j] = self.o.single_dist(self.metric, 1, self.q[i], self.store[s])
+        return torch.from_numpy(E)
+
+    def bq_final(self, world, id_stride, ids, ln, E_all):
+        lib = self.o.lib()
+        ids, ln, E_all = ids.numpy(), ln.numpy(), E_all.numpy()
+        nq = ids.shape[0]
+        k = self.k
+        oi = np.zeros((nq, k), np.int64)
+        od = np.zeros((nq, k), np.float32)
+        on = np.zeros(nq, np.int32)
+        for i in range(nq):
+            hid, hd, h = self._heap(k)
+            for j in range(ln[i]):
+                idv = int(ids[i, j])
+                owner = min(idv // id_stride, world - 1)
+                lib.or_insert_to_heap(C.byref(h), k, idv, float(E_all[owner, i, j]))
+            m = h.len
+            for j in range(m - 1, -1, -1):
+                a, b = C.c_uint64(), C.c_float()
+                lib.or_heap_pop(C.byref(h), C.byref(a), C.byref(b))
+                oi[i, j], od[i, j] = a.value, b.value
+            on[i] = m
+        return torch.from_numpy(oi), torch.from_numpy(od), torch.from_numpy(on)
+
+
+def _worker(rank, world, port, metric, kind, n, d, nq, k, rl, outpath):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle as orc
+    from weaviate_amd.sharded import ShardedBQSearch
+    corpus = orc.gen_matrix(kind, 5, 0, n, d)
+    queries = orc.gen_matrix(kind, 6, 0, nq, d)
+    per = (n + world - 1) // world
+    b = OracleBQShardBackend(orc, metric, corpus, rank * per, min(n, (rank + 1) * per), rl)
+    s = ShardedBQSearch(b, torch.device("cpu"), per)
+    oi, od, on = s.search(torch.from_numpy(queries), k)
+    if rank == 0:
+        np.savez(outpath, ids=oi.numpy(), dists=od.numpy(), counts=on.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,metric,kind,d,rl", [(2, 2, 0, 130, 40), (3, 0, 0, 64, 25), (2, 2, 1, 70, 30),
+                                                   (3, 1, 2, 100, -1)])
+def test_sharded_bq_matches_single_index(tmp_path, oracle, world, metric, kind, d, rl):
+    n, nq, k = 450, 6, 10
+    out = str(tmp_path / "res.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), metric, kind, n, d, nq, k, rl, out), nprocs=world,
+                       join=True, start_method="spawn")
+    r = np.load(out)
+    corpus = oracle.gen_matrix(kind, 5, 0, n, d)
+    queries = oracle.gen_matrix(kind, 6, 0, nq, d)
+    ref = oracle.OracleFlatBQ(metric, 1, d, n, rl)
+    ref.add_batch(np.arange(n), corpus)
+    for q in range(nq):
+        rc, ids, dd = ref.search(queries[q], k)
+        c = int(r["counts"][q])
+        np.testing.assert_array_equal(r["ids"][q, :c].astype(np.uint64), ids, err_msg=f"q{q}")
+        np.testing.assert_array_equal(r["dists"][q, :c].view(np.uint32), dd.view(np.uint32))

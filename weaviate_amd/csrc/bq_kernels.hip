@@ -173,7 +173,10 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
                                                   const uint64_t* __restrict__ qcodes, int64_t ldq,
                                                   const int32_t* __restrict__ qlist, int nlist,
                                                   const float* __restrict__ bmin, int64_t nblk, int R,
-                                                  uint32_t* __restrict__ out_slot, int32_t* __restrict__ out_n) {
+                                                  uint64_t id_base, const uint64_t* __restrict__ in_ids,
+                                                  const float* __restrict__ in_d, const int32_t* __restrict__ in_len,
+                                                  int pop, uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
+                                                  int32_t* __restrict__ out_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
     float* s_d = reinterpret_cast<float*>(hid + R);
@@ -184,7 +187,10 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
     if (li >= nlist) return;
     const uint64_t* qc = qcodes + qlist[li];  // word w at qc[w * ldq]
     const float* Bq = bmin + (int64_t)li * nblk;
-    if (lane == 0) *s_len = 0;
+    // heap state handed over by the previous shard (layout order), or empty
+    const int len0 = in_len ? in_len[li] : 0;
+    for (int i = lane; i < len0; i += 64) { hid[i] = in_ids[(int64_t)li * R + i]; hd[i] = in_d[(int64_t)li * R + i]; }
+    if (lane == 0) *s_len = len0;
     __syncthreads();
     for (int64_t b0 = 0; b0 < nblk; b0 += 64) {
         const float bm = (b0 + lane < nblk) ? Bq[b0 + lane] : __builtin_inff();
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
                         const int jj = __builtin_ctzll(mask);
                         mask &= mask - 1;
                         const float dj = s_d[jj];
-                        const uint64_t sj = (uint64_t)(sb + jj);
+                        const uint64_t sj = id_base + (uint64_t)(sb + jj);
                         if (hp.len < R) rh_insert(hp, sj, dj);
                         else if (hp.dist[0] > dj) { uint64_t a; float b; rh_pop(hp, &a, &b); rh_insert(hp, sj, dj); }
                     }
@@ -259,23 +265,47 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
     if (lane == 0) {
         ReplayHeap hp{hid, hd, *s_len};
         const int n = hp.len;
-        for (int i = 0; i < n; i++) {
-            uint64_t a; float b;
-            rh_pop(hp, &a, &b);
-            out_slot[(int64_t)li * R + i] = (uint32_t)a;
+        if (pop) {  // pop order (max first) = idsSlice of flat/index.go:485-487
+            for (int i = 0; i < n; i++) {
+                uint64_t a; float b;
+                rh_pop(hp, &a, &b);
+                out_ids[(int64_t)li * R + i] = a;
+                out_d[(int64_t)li * R + i] = b;
+            }
+        } else {  // the heap state itself, for the next shard
+            for (int i = 0; i < n; i++) { out_ids[(int64_t)li * R + i] = hid[i]; out_d[(int64_t)li * R + i] = hd[i]; }
         }
-        for (int i = n; i < R; i++) out_slot[(int64_t)li * R + i] = NO_ID;
         out_n[li] = n;
     }
+}
+
+// Exact-order SingleDist of candidate ids (lane per (listed query, entry)):
+// ids [nlist][R] global, entries i < cnt[li]; only ids this shard holds
+// (id_base <= id < id_base + nslots) are written.  Q row = qlist[li].
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(64) void k_rescore_ids(const float* __restrict__ X, int dpad, const float* __restrict__ Q,
+                                                    int d, const uint64_t* __restrict__ ids,
+                                                    const int32_t* __restrict__ cnt, const int32_t* __restrict__ qlist,
+                                                    int nlist, int R, uint64_t id_base, int64_t nslots,
+                                                    float* __restrict__ outE) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (int64_t)nlist * R) return;
+    const int li = (int)(p / R), i = (int)(p % R);
+    if (i >= cnt[li]) return;
+    const uint64_t id = ids[p];
+    if (id < id_base || id - id_base >= (uint64_t)nslots) return;
+    outE[p] = exact_dist<METRIC, VARIANT>(Q + (int64_t)qlist[li] * dpad, X + (int64_t)(id - id_base) * dpad, d);
 }
 
 // Rescoring heap (flat/index.go:525-531): the candidates, in pop order, go
 // through insertToHeap(heap, k, id, dist); extractHeap gives the result.
 // One wave per listed query; lane 0 runs the heap in LDS ([k] u64 | [k] f32).
-__global__ __launch_bounds__(64) void k_bq_final(const uint32_t* __restrict__ cand_slot,
+// world > 1: candE is [world][nlist][R] (each shard's exact distances of the
+// ids it holds); the entry of id comes from shard min(id / id_stride, world-1).
+__global__ __launch_bounds__(64) void k_bq_final(const uint64_t* __restrict__ cand_ids,
                                                  const float* __restrict__ candE,
                                                  const int32_t* __restrict__ cand_n, const int32_t* __restrict__ qlist,
-                                                 int nlist, int R, int k, uint64_t id_base,
+                                                 int nlist, int R, int k, int world, uint64_t id_stride,
                                                  uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
                                                  int32_t* __restrict__ out_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
@@ -287,8 +317,10 @@ __global__ __launch_bounds__(64) void k_bq_final(const uint32_t* __restrict__ ca
     ReplayHeap hp{hid, hd, 0};
     const int n = cand_n[li];
     for (int i = 0; i < n; i++) {
-        const uint64_t id = id_base + cand_slot[(int64_t)li * R + i];
-        const float dist = candE[(int64_t)li * R + i];
+        const uint64_t id = cand_ids[(int64_t)li * R + i];
+        uint64_t owner = 0;
+        if (world > 1) { owner = id / id_stride; if (owner > (uint64_t)(world - 1)) owner = world - 1; }
+        const float dist = candE[(int64_t)owner * nlist * R + (int64_t)li * R + i];
         if (hp.len < k) rh_insert(hp, id, dist);
         else if (hp.dist[0] > dist) { uint64_t a; float b; rh_pop(hp, &a, &b); rh_insert(hp, id, dist); }
     }

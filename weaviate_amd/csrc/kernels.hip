@@ -103,6 +103,7 @@ struct SelectArgs {
     const uint16_t* Xl;
     const uint16_t* Qh;       // [nq_pad][dpad]
     const uint16_t* Ql;
+    int dbg;                  // timing experiments only: 1 = skip selection, 2 = skip MFMA + selection
 };
 
 template <int R>

@@ -77,47 +77,54 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
     // DMA pieces (1 KiB = 16 rows x 64 B) of this wave per slice: 2 of Xh, 2 of
     // Xl (rows 32w .. 32w+31), 1 of Qh, 1 of Ql (rows 16w .. 16w+15).  Lane L
     // writes LDS row L>>2, physical chunk L&3 = logical chunk (L&3) ^ swz(row).
+    // Per-lane source offsets are fixed; a slice adds kb*64 B, a tile BN3 rows.
     const int prow = lane >> 2, pchunk = lane & 3;
     const int64_t ldb = (int64_t)a.dpad * 2;  // bytes per row of a plane
-    auto issue = [&](int64_t step) {
-        const int64_t tile = t0 + step / nk;
-        const int kb = (int)(step % nk);
-        unsigned char* slot = ring + (int)(step % NBUF3) * SLOT_BF3;
+    int64_t xoff[2];
+#pragma unroll
+    for (int p = 0; p < 2; p++) {
+        const int row = 32 * wave + 16 * p + prow;
+        xoff[p] = (int64_t)row * ldb + 16 * (pchunk ^ swz_bf3(row));
+    }
+    const int64_t qoff = (int64_t)(q0 + 16 * wave + prow) * ldb + 16 * (pchunk ^ swz_bf3(16 * wave + prow));
+    const unsigned char* Xh8 = reinterpret_cast<const unsigned char*>(a.Xh);
+    const unsigned char* Xl8 = reinterpret_cast<const unsigned char*>(a.Xl);
+    const unsigned char* Qh8 = reinterpret_cast<const unsigned char*>(a.Qh);
+    const unsigned char* Ql8 = reinterpret_cast<const unsigned char*>(a.Ql);
+    // issue position (tile, kb, slot) runs two slices ahead of the compute position
+    int64_t itile = t0;
+    int ikb = 0, islot = 0;
+    auto issue = [&]() {
+        unsigned char* slot = ring + islot * SLOT_BF3;
+        const int64_t tb = itile * BN3 * ldb + ikb * 64;
 #pragma unroll
         for (int p = 0; p < 2; p++) {
-            const int row = 32 * wave + 16 * p + prow;
-            const int c = pchunk ^ swz_bf3(row);
-            const int64_t off = (tile * BN3 + row) * ldb + kb * 64 + 16 * c;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned char*>(a.Xh) + off,
-                                             (lds_ptr_t)(slot + (32 * wave + 16 * p) * 64), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned char*>(a.Xl) + off,
-                                             (lds_ptr_t)(slot + BN3 * 64 + (32 * wave + 16 * p) * 64), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(Xh8 + tb + xoff[p], (lds_ptr_t)(slot + (32 * wave + 16 * p) * 64), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(Xl8 + tb + xoff[p], (lds_ptr_t)(slot + BN3 * 64 + (32 * wave + 16 * p) * 64),
+                                             16, 0, 0);
         }
-        {
-            const int row = 16 * wave + prow;
-            const int c = pchunk ^ swz_bf3(row);
-            const int64_t off = (int64_t)(q0 + row) * ldb + kb * 64 + 16 * c;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned char*>(a.Qh) + off,
-                                             (lds_ptr_t)(slot + 2 * BN3 * 64 + (16 * wave) * 64), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned char*>(a.Ql) + off,
-                                             (lds_ptr_t)(slot + 2 * BN3 * 64 + QB * 64 + (16 * wave) * 64), 16, 0, 0);
-        }
+        __builtin_amdgcn_global_load_lds(Qh8 + ikb * 64 + qoff, (lds_ptr_t)(slot + 2 * BN3 * 64 + (16 * wave) * 64), 16,
+                                         0, 0);
+        __builtin_amdgcn_global_load_lds(Ql8 + ikb * 64 + qoff,
+                                         (lds_ptr_t)(slot + 2 * BN3 * 64 + QB * 64 + (16 * wave) * 64), 16, 0, 0);
+        if (++ikb == nk) { ikb = 0; itile++; }
+        if (++islot == NBUF3) islot = 0;
     };
 
     f32x16 acc[2][2];
     int epoch = 0;
-    if (total_steps > 0) issue(0);
-    if (total_steps > 1) issue(1);
+    if (total_steps > 0) issue();
+    if (total_steps > 1) issue();
 
+    int64_t tile = t0;
+    int kb = 0, cslot = 0;
     for (int64_t step = 0; step < total_steps; step++) {
-        const int64_t tile = t0 + step / nk;
-        const int kb = (int)(step % nk);
         if (step + 1 < total_steps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();   // everyone's pieces landed; slot (step+2)%3 is free
         __builtin_amdgcn_sched_barrier(0);
-        if (step + 2 < total_steps) issue(step + 2);
-        const unsigned char* cur = ring + (int)(step % NBUF3) * SLOT_BF3;
+        if (step + 2 < total_steps) issue();
+        const unsigned char* cur = ring + cslot * SLOT_BF3;
         if (kb == 0) {
 #pragma unroll
             for (int i = 0; i < 2; i++)
@@ -144,6 +151,7 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
             }
 #pragma unroll
         for (int kk = 0; kk < 2; kk++) {
+            if (a.dbg == 2) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); break; }
             if (kk == 0) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
             else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
@@ -156,8 +164,12 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XL[kk][i], QH[kk][j], acc[i][j], 0, 0, 0);
                 }
         }
+        const bool last_k = kb == nk - 1;
+        if (++cslot == NBUF3) cslot = 0;
+        if (++kb == nk) kb = 0;
 
-        if (kb == nk - 1) {
+        if (last_k && a.dbg) tile++;
+        if (last_k && !a.dbg) {
             // ---------------- epilogue: selection over this 128 x 256 tile (as k_mfma_select3) ----------------
             const int64_t row0 = tile * BN3;
             float qn[2];
@@ -167,30 +179,46 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                 qidx[j] = 64 * wq + 32 * j + li;
                 qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
             }
+            // rows 64wx + 32i + [0, 32) of the tile share one word of the valid bitmap
             const uint32_t* vb = a.valid + (row0 >> 5);
+            const uint32_t vbw[2] = {vb[2 * wx], vb[2 * wx + 1]};
+            // the candidate mask against the current thresholds is built
+            // branch-free; a wave with no candidate skips the selection loop
+            uint64_t pending = 0;
+            {
+                const float th0[2] = {thr[qidx[0]], thr[qidx[1]]};
 #pragma unroll
-            for (int i = 0; i < 2; i++) {
+                for (int i = 0; i < 2; i++) {
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    bool ok = (vb[rt >> 5] >> (rt & 31)) & 1u;
-                    float xn = (METRIC == L2) ? a.xnorm2[row0 + rt] : 0.f;
+                    for (int r = 0; r < 16; r++) {
+                        const int rr = (r & 3) + 8 * (r >> 2) + 4 * lh;  // row within the 32-row block
+                        const bool ok = (vbw[i] >> rr) & 1u;
+                        const float xn = (METRIC == L2) ? a.xnorm2[row0 + 64 * wx + 32 * i + rr] : 0.f;
 #pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        float dot = acc[i][j][r];
-                        float v;
-                        if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
-                        else if (METRIC == DOT) v = -dot;
-                        else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
-                        bool qok = (q0 + qidx[j]) < a.nq;
-                        acc[i][j][r] = (ok && qok) ? v : __builtin_inff();
+                        for (int j = 0; j < 2; j++) {
+                            const float dot = acc[i][j][r];
+                            float v;
+                            if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
+                            else if (METRIC == DOT) v = -dot;
+                            else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
+                            const bool qok = (q0 + qidx[j]) < a.nq;
+                            v = (ok && qok) ? v : __builtin_inff();
+                            acc[i][j][r] = v;
+                            const int vi = (i * 16 + r) * 2 + j;
+                            pending |= (uint64_t)(v < th0[j]) << vi;
+                        }
                     }
                 }
             }
-            uint64_t pending = ~0ull;
+            // Candidates accumulate in the LDS buffer across tiles; the lists
+            // (global) are merged only when a buffer overflows or at the span's
+            // last tile.  Stale thresholds only admit more candidates, never
+            // drop one of the KP best.
+            const bool last_tile = tile == t1 - 1;
             for (;;) {
                 ++epoch;
                 float th[2] = {thr[qidx[0]], thr[qidx[1]]};
+                if (__any(pending != 0))
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
 #pragma unroll
@@ -207,8 +235,9 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                                     cbA[qidx[j] * C + slot] = v;
                                     cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
                                     pending &= ~(1ull << vi);
+                                } else {
+                                    flags[1] = epoch;  // overflow: merge, then retry
                                 }
-                                flags[0] = epoch;
                             } else {
                                 pending &= ~(1ull << vi);
                             }
@@ -216,7 +245,8 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                     }
                 }
                 __syncthreads();
-                if (flags[0] != epoch) break;
+                const bool overflow = flags[1] == epoch;
+                if (!overflow && !last_tile) break;
                 for (int jq = 0; jq < QB / 8; jq++) {
                     const int q = wave + 8 * jq;
                     const int c = cnt[q];
@@ -225,14 +255,12 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                     const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
                     merge_query_list<R>(a.outA + base, a.outI + base, cbA + q * C, cbI + q * C, KP, C, nc, lane,
                                         &thr[q]);
-                    if (lane == 0) {
-                        if (c > C) flags[1] = epoch;
-                        cnt[q] = 0;
-                    }
+                    if (lane == 0) cnt[q] = 0;
                 }
                 __syncthreads();
-                if (flags[1] != epoch) break;
+                if (!overflow) break;
             }
+            tile++;
         }
     }
 }

@@ -125,6 +125,8 @@ struct wv_index {
     uint32_t* d_maxn2 = nullptr;
     uint64_t* codes = nullptr;   // BQ: [words][cap] word-major codes of the stored rows
     int words = 0;
+    int64_t bq_nq = 0;           // BQ batch in flight (bq_begin): queries and R
+    int bq_R = 0;
     // PQ (compressionhelpers.ProductQuantizer): codebook [m][ks][ds], codes
     // [ceil(m/4)][cap] u32 (4 segment bytes per word, see pq_kernels.hip)
     int pq_m = 0, pq_ks = 0, pq_ds = 0, pq_training_limit = 0, pq_rescore = 1, pq_trained = 0;
@@ -143,7 +145,7 @@ struct wv_index {
 
     DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, qh, ql;
 
-    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0;
+    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0, sel_dbg = 0, qgroup_opt = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     wv_stats stats{};
 };
@@ -519,6 +521,8 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "cbuf") idx->cbuf_opt = (int)value;
     else if (k == "kernel") idx->kernel_opt = (int)value;
     else if (k == "bq_kernel") idx->bq_kernel = (int)value;
+    else if (k == "sel_dbg") idx->sel_dbg = (int)value;
+    else if (k == "qgroup") idx->qgroup_opt = (int)value;
     else return set_err(WV_ERR_INVALID, "unknown option %s", key);
     return WV_OK;
 }
@@ -630,8 +634,11 @@ static int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, in
 
 // searchByVectorQuantized (flat/index.go:460-532) for BQ indexes, every query
 // through the exact R-heap replay (bq_kernels.hip).  Outputs [nq][k].
-static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
-                     const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+// Phase 1 of the BQ search: validation, query normalisation + codes, identity
+// query list.  Returns R (searchTimeRescore) via *R_out and the query group
+// size (block-minima buffer bounded to 1 GiB) via *G_out.
+static int bq_begin(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, int* R_out,
+                    int64_t* G_out) {
     // query code length vs stored code length: HammingBitwise (distancer/hamming.go:63-66)
     if ((qd + 63) / 64 != idx->words) return set_err(WV_ERR_VECTOR_LENGTH, "both vectors should have the same len");
     // the rescoring SingleDist then checks the float lengths (distancer/errors.go:16)
@@ -665,26 +672,39 @@ static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
         for (int64_t i = 0; i < nq; i++) id[i] = (int32_t)i;
         HIPCHK(hipMemcpyAsync(idx->ident.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
     }
-    const int32_t* qlist = idx->ident.as<int32_t>();
     constexpr int QPB = 16;
-    const int64_t G = std::max<int64_t>(QPB, std::min<int64_t>(round_up(nq, QPB), ((1ll << 30) / (nblk * 4)) / QPB * QPB));
-    HIPCHK(idx->bqmin.ensure((size_t)G * nblk * sizeof(float)));
-    HIPCHK(idx->cslot.ensure((size_t)nq * R * sizeof(uint32_t)));
-    HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
-    HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
-    const size_t lds_r = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
-    // compile-time word count for the LDS-broadcast block-minima kernel and
-    // the replay's unrolled loads (words <= 32, i.e. d <= 2048); else generic
+    *G_out = std::max<int64_t>(QPB, std::min<int64_t>(round_up(nq, QPB), ((1ll << 30) / (nblk * 4)) / QPB * QPB));
+    *R_out = R;
+    HIPCHK(idx->bqmin.ensure((size_t)(*G_out) * nblk * sizeof(float)));
+    idx->bq_nq = nq;
+    idx->bq_R = R;
+    return WV_OK;
+}
+
+// compile-time word count for the LDS-broadcast block-minima kernel and the
+// replay's unrolled loads (words <= 32, i.e. d <= 2048); 0 = generic kernels
+static int bq_nw(wv_index* idx) {
+    const int words = idx->words;
     const int nw = words <= 2 ? 2 : words <= 4 ? 4 : words <= 8 ? 8 : words <= 12 ? 12 : words <= 16 ? 16
                  : words <= 24 ? 24 : words <= 32 ? 32 : 0;
-    const bool generic = nw == 0 || idx->bq_kernel == 1;
-    for (int64_t g0 = 0; g0 < nq; g0 += G) {
-        const int F = (int)std::min<int64_t>(G, nq - g0);
-        // timing (bench roofline): the block-minima pass of the first group
-        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
-        const uint64_t* qc = idx->qcodes.as<uint64_t>();
-        float* bm = idx->bqmin.as<float>();
-        if (generic) {
+    return idx->bq_kernel == 1 ? 0 : nw;
+}
+
+// Phase 1b: block minima of query group [g0, g0 + F) into idx->bqmin
+static int bq_blockmin(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t g0, int F) {
+    constexpr int QPB = 16;
+    const int64_t nq = idx->bq_nq;
+    const int64_t nslots = idx->hiwater;
+    const int64_t nblk = std::max<int64_t>((nslots + BQBLK - 1) / BQBLK, 1);
+    const int words = idx->words;
+    const int nw = bq_nw(idx);
+    const int32_t* qlist = idx->ident.as<int32_t>();
+    // timing (bench roofline): the block-minima pass of the first group
+    if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
+    const uint64_t* qc = idx->qcodes.as<uint64_t>();
+    float* bm = idx->bqmin.as<float>();
+    {
+        if (nw == 0) {
             dim3 grid((unsigned)nblk, (unsigned)((F + QPB - 1) / QPB));
             k_bq_blockmin<QPB><<<grid, 256, 0, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq, qlist + g0, F,
                                                     nblk, bm);
@@ -707,32 +727,59 @@ static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
         }
         HIPCHK(hipGetLastError());
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
+    }
+    return WV_OK;
+}
+
+// Phase 2: the R-heap replay of query group [g0, g0 + F) over this shard, from
+// heap states in_* (NULL = empty) [F][R]; pop = 1 writes the popped
+// candidates (pop order), 0 the heap states.  Ids are global (id_base + slot).
+static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t g0, int F, const uint64_t* in_ids,
+                     const float* in_d, const int32_t* in_len, int pop, uint64_t* out_ids, float* out_d,
+                     int32_t* out_n) {
+    const int64_t nq = idx->bq_nq;
+    const int R = idx->bq_R;
+    const int64_t nslots = idx->hiwater;
+    const int64_t nblk = std::max<int64_t>((nslots + BQBLK - 1) / BQBLK, 1);
+    const int words = idx->words;
+    const int nw = bq_nw(idx);
+    const int32_t* qlist = idx->ident.as<int32_t>();
+    const uint64_t* qc = idx->qcodes.as<uint64_t>();
+    const float* bm = idx->bqmin.as<float>();
+    const size_t lds_r = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
 #define WV_RP(NWV)                                                                                              \
     do {                                                                                                        \
         if (lds_r > 64 * 1024)                                                                                  \
             HIPCHK(hipFuncSetAttribute((const void*)k_bq_replay<NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                        (int)lds_r));                                                            \
         k_bq_replay<NWV><<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq,      \
-                                                        qlist + g0, F, bm, nblk, R,                             \
-                                                        idx->cslot.as<uint32_t>() + g0 * R,                     \
-                                                        idx->cn.as<int32_t>() + g0);                            \
+                                                        qlist + g0, F, bm, nblk, R, idx->id_base, in_ids, in_d, \
+                                                        in_len, pop, out_ids, out_d, out_n);                    \
     } while (0)
-        switch (generic ? 0 : nw) {
-        case 2: WV_RP(2); break;
-        case 4: WV_RP(4); break;
-        case 8: WV_RP(8); break;
-        case 12: WV_RP(12); break;
-        case 16: WV_RP(16); break;
-        case 24: WV_RP(24); break;
-        case 32: WV_RP(32); break;
-        default: WV_RP(0); break;
-        }
-#undef WV_RP
-        HIPCHK(hipGetLastError());
+    switch (nw) {
+    case 2: WV_RP(2); break;
+    case 4: WV_RP(4); break;
+    case 8: WV_RP(8); break;
+    case 12: WV_RP(12); break;
+    case 16: WV_RP(16); break;
+    case 24: WV_RP(24); break;
+    case 32: WV_RP(32); break;
+    default: WV_RP(0); break;
     }
+#undef WV_RP
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
+// Phase 3: exact distances of the candidate ids this shard holds
+static int bq_rescore(wv_index* idx, hipStream_t s, const uint64_t* ids, const int32_t* cnt, float* E) {
+    const int64_t nq = idx->bq_nq;
+    const int R = idx->bq_R;
     const int64_t npairs = nq * R;
+    const float* Qn = idx->qn.as<float>();
+    const int32_t* qlist = idx->ident.as<int32_t>();
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
-#define WV_RS(M, V) k_rescore<M, V><<<(unsigned)((npairs + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, Qn, idx->dims, idx->cslot.as<uint32_t>(), (int)nq, R, idx->candE.as<float>())
+#define WV_RS(M, V) k_rescore_ids<M, V><<<(unsigned)((npairs + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, Qn, idx->dims, ids, cnt, qlist, (int)nq, R, idx->id_base, idx->hiwater, E)
     switch (idx->metric) {
     case WV_METRIC_L2_SQUARED: if (v5) WV_RS(L2, AVX512); else WV_RS(L2, AVX256); break;
     case WV_METRIC_DOT: if (v5) WV_RS(DOT, AVX512); else WV_RS(DOT, AVX256); break;
@@ -741,12 +788,44 @@ static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     }
 #undef WV_RS
     HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
+// Phase 4: insertToHeap(heap, k, ...) in pop order + extractHeap
+static int bq_final(hipStream_t s, int64_t nq, int R, int k, int world, uint64_t id_stride, const int32_t* qlist,
+                    const uint64_t* ids, const int32_t* cnt, const float* E, uint64_t* o_ids, float* o_d,
+                    int32_t* o_n) {
     const size_t lds_f = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
     if (lds_f > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_bq_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
-    k_bq_final<<<(unsigned)nq, 64, lds_f, s>>>(idx->cslot.as<uint32_t>(), idx->candE.as<float>(), idx->cn.as<int32_t>(),
-                                               qlist, (int)nq, R, k, idx->id_base, o_ids, o_d, o_n);
+    k_bq_final<<<(unsigned)nq, 64, lds_f, s>>>(ids, E, cnt, qlist, (int)nq, R, k, world, id_stride, o_ids, o_d, o_n);
     HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
+static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
+                     const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+    int R = 0;
+    int64_t G = 0;
+    int rc = bq_begin(idx, s, d_qraw, nq, qd, k, &R, &G);
+    if (rc) return rc;
+    HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
+    HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
+    HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
+    for (int64_t g0 = 0; g0 < nq; g0 += G) {
+        const int F = (int)std::min<int64_t>(G, nq - g0);
+        rc = bq_blockmin(idx, s, valid, g0, F);
+        if (rc) return rc;
+        rc = bq_replay(idx, s, valid, g0, F, nullptr, nullptr, nullptr, 1, idx->ascI.as<uint64_t>() + g0 * R,
+                       idx->ascD.as<float>() + g0 * R, idx->cn.as<int32_t>() + g0);
+        if (rc) return rc;
+    }
+    rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->cn.as<int32_t>(), idx->candE.as<float>());
+    if (rc) return rc;
+    rc = bq_final(s, nq, R, k, 1, 0, idx->ident.as<int32_t>(), idx->ascI.as<uint64_t>(), idx->cn.as<int32_t>(),
+                  idx->candE.as<float>(), o_ids, o_d, o_n);
+    if (rc) return rc;
     if (idx->timing) {
         HIPCHK(hipStreamSynchronize(s));
         float ms = 0.f;
@@ -754,6 +833,72 @@ static int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
         idx->stats.last_select_ms = ms;
     }
     return WV_OK;
+}
+
+// ---- sharded BQ (weaviate_amd/sharded.py ShardedBQSearch) ----
+extern "C" int wv_index_bq_begin(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                 void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->compression != WV_COMPRESSION_BQ) return set_err(WV_ERR_INVALID, "bq_begin: index is not BQ-compressed");
+    hipStream_t s = stream ? (hipStream_t)stream : idx->stream;
+    int R = 0;
+    int64_t G = 0;
+    int rc = bq_begin(idx, s, d_queries, nq, d, k, &R, &G);
+    if (rc) return rc;
+    if (G < nq) return set_err(WV_ERR_UNSUPPORTED, "bq_begin: batch of %lld queries exceeds one block-minima group",
+                               (long long)nq);
+    rc = bq_blockmin(idx, s, idx->present, 0, (int)nq);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_index_bq_replay(wv_index* idx, const uint64_t* d_in_ids, const float* d_in_d,
+                                  const int32_t* d_in_len, int32_t pop, uint64_t* d_out_ids, float* d_out_d,
+                                  int32_t* d_out_len, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->bq_nq <= 0) return set_err(WV_ERR_INVALID, "bq_replay: no batch begun");
+    hipStream_t s = stream ? (hipStream_t)stream : idx->stream;
+    int rc = bq_replay(idx, s, idx->present, 0, (int)idx->bq_nq, d_in_ids, d_in_d, d_in_len, pop, d_out_ids, d_out_d,
+                       d_out_len);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_index_bq_rescore(wv_index* idx, const uint64_t* d_ids, const int32_t* d_len, float* d_E,
+                                   void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->bq_nq <= 0) return set_err(WV_ERR_INVALID, "bq_rescore: no batch begun");
+    hipStream_t s = stream ? (hipStream_t)stream : idx->stream;
+    int rc = bq_rescore(idx, s, d_ids, d_len, d_E);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_bq_final(int32_t device, int64_t nq, int32_t R, int32_t k, int32_t world, uint64_t id_stride,
+                           const uint64_t* d_ids, const int32_t* d_len, const float* d_E, uint64_t* d_out_ids,
+                           float* d_out_d, int32_t* d_out_n, void* stream) {
+    HIPCHK(hipSetDevice(device));
+    if (nq <= 0) return WV_OK;
+    if (k <= 0 || R < k || world < 1) return set_err(WV_ERR_INVALID, "bq_final: invalid k / R / world");
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<int32_t> id((size_t)nq);
+    for (int64_t i = 0; i < nq; i++) id[i] = (int32_t)i;
+    DBuf ql;
+    HIPCHK(ql.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(ql.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    int rc = bq_final(s, nq, R, k, world, id_stride, ql.as<int32_t>(), d_ids, d_len, d_E, d_out_ids, d_out_d, d_out_n);
+    HIPCHK(hipStreamSynchronize(s));  // ql is freed on return
+    ql.release();
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -1210,6 +1355,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         int qgroup = 1;
         for (int g : {4, 2, 1})
             if (nqb % g == 0) { qgroup = g; break; }
+        if (idx->qgroup_opt > 0 && nqb % idx->qgroup_opt == 0) qgroup = idx->qgroup_opt;
         // ~1024 workgroups (2 per CU resident, 2 waves of them); keep the
         // workgroup count a multiple of 8 for the XCD mapping when possible
         const int64_t target_wg = kver >= 3 ? 768 : 1024;
@@ -1228,6 +1374,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         a.tiles_per_span = (int)tps; a.nspans = (int)nspans; a.nqb = nqb; a.KP = KP; a.qgroup = qgroup;
         a.outA = idx->spanA.as<float>(); a.outI = idx->spanI.as<uint32_t>();
         a.Xh = idx->Xh; a.Xl = idx->Xl; a.Qh = idx->qh.as<uint16_t>(); a.Ql = idx->ql.as<uint16_t>();
+        a.dbg = idx->sel_dbg;
         // candidate buffer: as large as fits two workgroups per CU (<= 80 KiB each)
         const bool v2 = kver == 2;
         const int64_t fixed = kver == 4 ? (int64_t)NBUF3 * SLOT_BF3 + (int64_t)(QB * 2 + 4) * (int64_t)sizeof(float)

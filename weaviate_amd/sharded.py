@@ -82,6 +82,92 @@ class GpuShardBackend:
         return oi, od, on
 
 
+class GpuBQShardBackend(GpuShardBackend):
+    """Rank-local BQ engine (wv_index_bq_* entry points, include/wv_knn.h)."""
+
+    def R(self, k: int) -> int:
+        return max(int(self.index.rescore_limit), k)
+
+    def _s(self):
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def bq_begin(self, q: torch.Tensor, k: int):
+        nq, d = q.shape
+        self.nq, self.k = nq, k
+        self._check(self._l.wv_index_bq_begin(self.index._h, q.data_ptr(), nq, d, k, self._s()))
+
+    def bq_replay(self, state, pop: bool):
+        R = self.R(self.k)
+        ids = torch.empty((self.nq, R), dtype=torch.int64, device=self.dev)
+        dd = torch.empty((self.nq, R), dtype=torch.float32, device=self.dev)
+        ln = torch.empty(self.nq, dtype=torch.int32, device=self.dev)
+        si, sd, sl = (None, None, None) if state is None else (state[0].data_ptr(), state[1].data_ptr(),
+                                                               state[2].data_ptr())
+        self._check(self._l.wv_index_bq_replay(self.index._h, si, sd, sl, 1 if pop else 0, ids.data_ptr(),
+                                               dd.data_ptr(), ln.data_ptr(), self._s()))
+        return ids, dd, ln
+
+    def bq_rescore(self, ids, ln):
+        E = torch.zeros(ids.shape, dtype=torch.float32, device=self.dev)
+        self._check(self._l.wv_index_bq_rescore(self.index._h, ids.data_ptr(), ln.data_ptr(), E.data_ptr(),
+                                                self._s()))
+        return E
+
+    def bq_final(self, world: int, id_stride: int, ids, ln, E_all):
+        nq, R = ids.shape
+        oi = torch.empty((nq, self.k), dtype=torch.int64, device=self.dev)
+        od = torch.empty((nq, self.k), dtype=torch.float32, device=self.dev)
+        on = torch.empty(nq, dtype=torch.int32, device=self.dev)
+        self._check(self._l.wv_bq_final(self.device, nq, R, self.k, world, id_stride, ids.data_ptr(), ln.data_ptr(),
+                                        E_all.data_ptr(), oi.data_ptr(), od.data_ptr(), on.data_ptr(), self._s()))
+        return oi, od, on
+
+
+class ShardedBQSearch:
+    """BQ-compressed search over contiguous id-range shards (one per rank) with
+    the single index's exact semantics (flat/index.go:460-532):
+      1. every rank: query codes + hamming block minima of its shard (parallel,
+         the expensive VALU pass);
+      2. the R-heap is replayed across the ranks in id order: rank r continues
+         rank r-1's heap states (broadcast over RCCL, B*R*16 bytes), the last
+         rank pops it in the reference's pop order;
+      3. every rank rescores the candidates it holds (exact SingleDist),
+         all-gather of the [B][R] distance tiles;
+      4. the rescoring heap (insertToHeap in pop order, extractHeap)."""
+
+    def __init__(self, backend, device: torch.device, id_stride: int):
+        self.b = backend
+        self.dev = device
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.id_stride = int(id_stride)
+
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        return ShardedFlatSearch._all_gather(self, t)
+
+    def search(self, q: torch.Tensor, k: int):
+        nq = q.shape[0]
+        R = self.b.R(k)
+        self.b.bq_begin(q, k)
+        state = None
+        for r in range(self.world):
+            last = r == self.world - 1
+            if self.rank == r:
+                ids, dd, ln = self.b.bq_replay(state, last)
+            else:
+                ids = torch.empty((nq, R), dtype=torch.int64, device=self.dev)
+                dd = torch.empty((nq, R), dtype=torch.float32, device=self.dev)
+                ln = torch.empty(nq, dtype=torch.int32, device=self.dev)
+            dist.broadcast(ids, src=r)
+            dist.broadcast(dd, src=r)
+            dist.broadcast(ln, src=r)
+            state = (ids, dd, ln)
+        ids, _, ln = state
+        E = self.b.bq_rescore(ids, ln)
+        E_all = self._all_gather(E)
+        return self.b.bq_final(self.world, self.id_stride, ids, ln, E_all)
+
+
 class ShardedFlatSearch:
     """search(queries) over all ranks of the default process group."""
 
