@@ -191,10 +191,12 @@ def main():
 
     bq = args.workload == "bq"
     pq = args.workload == "pq"
-    if (bq or pq) and world > 1:
+    if pq and world > 1:
         raise SystemExit(f"--workload {args.workload}: sharded search is not available yet (1 GPU)")
     dims = BQ_DIMS if bq else PQ_DIMS if pq else DIMS
-    n_total = args.n if args.n is not None else (BQ_ROWS_PER_GPU if bq else PQ_ROWS if pq else N_TOTAL)
+    # c3 / pq: a fixed corpus split over the ranks (strong scaling); bq: configs[3]
+    # is 50M rows over 8 GPUs, i.e. a 6.25M-row shard per GPU (weak scaling)
+    n_total = args.n if args.n is not None else (BQ_ROWS_PER_GPU * world if bq else PQ_ROWS if pq else N_TOTAL)
     n_local = (n_total + world - 1) // world
     id0 = rank * n_local
     n_local = max(0, min(n_local, n_total - id0))
@@ -234,7 +236,13 @@ def main():
     out_d = torch.empty((B, K), dtype=torch.float32, device=dev)
     out_n = torch.empty(B, dtype=torch.int32, device=dev)
 
-    if world > 1:
+    if world > 1 and bq:
+        from weaviate_amd.sharded import GpuBQShardBackend, ShardedBQSearch
+        searcher = ShardedBQSearch(GpuBQShardBackend(index, local_rank), dev, (n_total + world - 1) // world)
+
+        def step():
+            return searcher.search(queries, K)
+    elif world > 1:
         from weaviate_amd.sharded import GpuShardBackend, ShardedFlatSearch
         searcher = ShardedFlatSearch(GpuShardBackend(index, local_rank), dev)
 
@@ -349,7 +357,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if bq else "strong",
             "vs_baseline": None,
             "dtype": "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else "f32",
             "data": "synthetic (counter-based U[-1,1) generator, seed 1 corpus / 2 queries)",
@@ -360,7 +368,8 @@ def main():
                 "k": K,
                 "query_batch": B,
                 "parallelism": f"corpus sharded over {world} GPU(s), contiguous id ranges"
-                               + (", RCCL all-gather merge" if world > 1 else ""),
+                               + ((", R-heap replay chained over RCCL broadcasts + all-gather rescoring" if bq
+                                   else ", RCCL all-gather merge") if world > 1 else ""),
                 "replayed_queries": int(replays),
             },
             "roofline": roof,

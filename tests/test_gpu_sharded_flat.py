@@ -1,0 +1,50 @@
+"""GPU: the sharded exact-search protocol of weaviate_amd.sharded.ShardedFlatSearch
+(mode-1 shard search -> gather -> wv_merge_shards -> cross-shard heap replay of
+flagged queries) with the shards as separate indexes on one GPU; the RCCL
+all-gather / broadcasts become local hand-overs.  Must equal the single index."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shards,metric,kind,n,d,k", [(2, "cosine", 0, 12000, 768, 10),
+                                                     (3, "l2-squared", 1, 6000, 64, 10),   # integer data: ties
+                                                     (4, "dot", 0, 5000, 100, 24)])
+def test_sharded_flat_protocol_equals_single_index(wv, oracle, shards, metric, kind, n, d, k):
+    from weaviate_amd.sharded import GpuShardBackend
+    dev = torch.device("cuda", 0)
+    data = oracle.gen_matrix(kind, 41, 0, n, d)
+    queries = oracle.gen_matrix(kind, 42, 0, 200, d)
+    per = (n + shards - 1) // shards
+    backs = []
+    for r in range(shards):
+        lo, hi = r * per, min(n, (r + 1) * per)
+        idx = wv.FlatIndex(distance=metric, id_base=lo, variant="avx256")
+        idx.add_batch(np.arange(lo, hi, dtype=np.uint64), data[lo:hi])
+        backs.append(GpuShardBackend(idx, 0))
+    q = torch.from_numpy(queries).to(dev)
+    parts = [b.local_search(q, k) for b in backs]
+    gi, gd, gc, gf = (torch.stack([p[j] for p in parts]) for j in range(4))
+    oi, od, on, of = backs[0].merge(shards, k, gi, gd, gc, gf)
+    flagged = torch.nonzero(of).flatten().cpu().numpy()
+    oi, od, on = oi.cpu().numpy(), od.cpu().numpy(), on.cpu().numpy()
+    if flagged.size:
+        state = None
+        for r, b in enumerate(backs):
+            state = b.replay(q, flagged, state, k, r == shards - 1)
+        fi, fd, fn = state
+        oi[flagged] = fi.view(np.int64)
+        od[flagged] = fd
+        on[flagged] = fn
+    single = wv.FlatIndex(distance=metric, variant="avx256")
+    single.add_batch(np.arange(n, dtype=np.uint64), data)
+    si, sd, sn = single.search_by_vector_batch(queries, k)
+    for i in range(len(queries)):
+        assert on[i] == sn[i]
+        np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), si[i, :sn[i]], err_msg=f"q{i}")
+        np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), sd[i, :sn[i]].view(np.uint32))
+    for b in backs:
+        b.index.close()
+    single.close()

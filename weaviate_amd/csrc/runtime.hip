@@ -851,7 +851,12 @@ extern "C" int wv_index_bq_begin(wv_index* idx, const float* d_queries, int64_t 
                                (long long)nq);
     rc = bq_blockmin(idx, s, idx->present, 0, (int)nq);
     if (rc) return rc;
-    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    if (!stream || idx->timing) HIPCHK(hipStreamSynchronize(s));
+    if (idx->timing) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
+        idx->stats.last_select_ms = ms;
+    }
     return WV_OK;
 }
 
