@@ -198,7 +198,7 @@ def test_search_by_vector_distance(wv, oracle):
     assert len(ids) == 31
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3, 4])
+@pytest.mark.parametrize("kernel", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("metric,kind,n,d,k", [("cosine", 0, 9000, 768, 10), ("l2-squared", 0, 7000, 96, 24),
                                                ("dot", 1, 5000, 64, 5)])
 def test_select_kernel_variants(wv, oracle, kernel, metric, kind, n, d, k):

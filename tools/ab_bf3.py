@@ -30,7 +30,7 @@ fl = torch.empty(B, dtype=torch.int32, device=dev)
 idx.set_option("timing", 1)
 for k, v in opts:
     idx.set_option(k, int(v))
-for dbg in (0, 1, 2):
+for dbg in [int(x) for x in os.environ.get('DBGS', '0,1,2').split(',')]:
     idx.set_option("sel_dbg", dbg)
     ms = []
     for it in range(4):

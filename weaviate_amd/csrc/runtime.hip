@@ -1340,7 +1340,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     if (qd != idx->dims)
         return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)qd, idx->dims);
     if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
-    const int64_t nq_pad = round_up(nq, QB);
+    const int64_t nq_pad = round_up(nq, QBW);  // 256: the wide bf16x3 tile; a multiple of QB
     int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
     if (rc) return rc;
     const float* Qn = idx->qn.as<float>();
@@ -1353,10 +1353,11 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     int32_t* flags = o_flags ? o_flags : idx->oF.as<int32_t>();
 
     if (mfma_ok) {
-        const int kver = (idx->kernel_opt == 4 && !idx->use_bf3) ? 3 : idx->kernel_opt;
+        const int kver = (idx->kernel_opt >= 4 && !idx->use_bf3) ? 3 : idx->kernel_opt;
         const int64_t bn = kver >= 3 ? BN3 : BN;
         const int64_t ntiles = (idx->hiwater + bn - 1) / bn;
-        const int nqb = (int)(nq_pad / QB);
+        const int qtile = kver == 5 ? QBW : QB;
+        const int nqb = (int)(round_up(nq, qtile) / qtile);
         int qgroup = 1;
         for (int g : {4, 2, 1})
             if (nqb % g == 0) { qgroup = g; break; }
@@ -1382,14 +1383,15 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         a.dbg = idx->sel_dbg;
         // candidate buffer: as large as fits two workgroups per CU (<= 80 KiB each)
         const bool v2 = kver == 2;
-        const int64_t fixed = kver == 4 ? (int64_t)NBUF3 * SLOT_BF3 + (int64_t)(QB * 2 + 4) * (int64_t)sizeof(float)
+        const int64_t fixed = kver == 5 ? (int64_t)NBUFW * SLOT_BW + (int64_t)(QBW * 2 + 4) * (int64_t)sizeof(float)
+                              : kver == 4 ? (int64_t)NBUF3 * SLOT_BF3 + (int64_t)(QB * 2 + 4) * (int64_t)sizeof(float)
                               : kver == 3 ? (int64_t)(NBUF3 * STG3 + QB * 2 + 4) * (int64_t)sizeof(float)
                               : v2 ? (int64_t)(2 * (BN + QB) * BK + QB * 2 + 4) * (int64_t)sizeof(float)
                                    : (int64_t)(2 * QB * LDSROW + QB * KP * 2 + QB * 2 + 4) * (int64_t)sizeof(float);
         const int64_t budget = kver >= 3 ? 160 * 1024 : 80 * 1024;
-        int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(4, (budget - fixed) / (QB * 8)));
+        int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(4, (budget - fixed) / (qtile * 8)));
         if (idx->cbuf_opt > 0) C = std::min(64 - KP, idx->cbuf_opt);
-        size_t lds = (size_t)(fixed + (int64_t)QB * C * 8);
+        size_t lds = (size_t)(fixed + (int64_t)qtile * C * 8);
         a.C = C;
         dim3 grid((unsigned)(nqb * nspans));
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
@@ -1408,7 +1410,18 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select_bf3<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
         k_mfma_select_bf3<M, 1><<<grid, 512, lds, s>>>(a);                                                 \
     } while (0)
-        if (kver == 4) {
+#define WV_SELW(M)                                                                                         \
+    do {                                                                                                   \
+        HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select_bf3w<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_mfma_select_bf3w<M, 1><<<grid, 512, lds, s>>>(a);                                                \
+    } while (0)
+        if (kver == 5) {
+            switch (idx->metric) {
+            case WV_METRIC_L2_SQUARED: WV_SELW(L2); break;
+            case WV_METRIC_DOT: WV_SELW(DOT); break;
+            default: WV_SELW(COSINE); break;
+            }
+        } else if (kver == 4) {
             switch (idx->metric) {
             case WV_METRIC_L2_SQUARED: WV_SELB(L2); break;
             case WV_METRIC_DOT: WV_SELB(DOT); break;
@@ -1427,6 +1440,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
             default: if (v2) WV_SEL(k_mfma_select2, COSINE); else WV_SEL(k_mfma_select, COSINE); break;
             }
         }
+#undef WV_SELW
 #undef WV_SELB
 #undef WV_SEL3
 #undef WV_SEL
@@ -1458,7 +1472,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         const double u4 = 2.384185791015625e-07;
         const double hdep = 3.0 * idx->dpad / 16.0 + 16.0;
         const double g3 = hdep * u4 / (1.0 - hdep * u4);
-        const double extra = kver == 4 ? 2.0 * (3.05 * 1.52587890625e-05 + g3) : 0.0;
+        const double extra = kver >= 4 ? 2.0 * (3.05 * 1.52587890625e-05 + g3) : 0.0;
         const float eps_scale = (float)((2.0 * gamma_n(idx->dpad + 4) + extra) * 1.05 + 1e-12);
         const float eps_base = (float)(std::sqrt((double)maxn2) * (1.0 + 1e-6));
         idx->last_eps_scale = eps_scale;
