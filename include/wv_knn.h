@@ -46,6 +46,14 @@ extern "C" {
 /* PQ: ProductQuantizer (compressionhelpers/product_quantization.go) with the
  * KMeans encoder; searched like hnsw.flatSearch (hnsw/flat_search.go:28-141) */
 #define WV_COMPRESSION_PQ 2
+/* flat's rotational quantizers (flat/quantizer.go:31-36, :85-99): "rq-8" =
+ * RotationalQuantizer (compressionhelpers/rotational_quantization.go) with 8
+ * bits, "rq-1" = BinaryRotationalQuantizer (binary_rotational_quantization.go);
+ * both seeded with DefaultFastRotationSeed (fast_rotation.go:27), created at the
+ * first Add (flat/index.go:338-360), searched by searchByVectorQuantized
+ * (:460-532) with rescore_limit = RQ.RescoreLimit */
+#define WV_COMPRESSION_RQ8 3
+#define WV_COMPRESSION_RQ1 4
 
 /* which reference SIMD kernel's fp32 accumulation order to reproduce
  * (distancer/l2_amd64.go:19-26: AVX-512 only if AMX-BF16 && AVX512) */
@@ -130,6 +138,23 @@ int wv_index_pq_info(wv_index *idx, int32_t *out);
  * against n codes [n][m]: LUT (DistanceLookUpTable) sums + Wrap */
 int wv_index_pq_distance(wv_index *idx, const float *query, int64_t d, const uint8_t *codes, int64_t n,
                          float *out);
+
+/* Rotational quantizer state: out[4] = {bits (8 / 1 / 0), rotation output dim D,
+ * code length in bytes (rq-8: 16 + D, rq-1: 8 * (1 + D/64)), created} */
+int wv_index_rq_info(wv_index *idx, int32_t *out);
+/* codes of slots [0, n) in the reference's compressed-bucket formats
+ * (flat/index.go:201-232 stores quantizer.Encode output): rq-8 RQCode
+ * [lower|step|codeSum|norm2 as big-endian float32][D bytes]
+ * (rotational_quantization.go:95-155); rq-1 RQOneBitCode little-endian u64
+ * words [step (low 32) | squaredNorm (high 32)][D/64 sign words]
+ * (binary_rotational_quantization.go:92-148).  out: n * code length bytes. */
+int wv_index_rq_codes(wv_index *idx, void *out, int64_t n);
+/* the quantized distance the scan uses (flat/index.go:536-560: rq-8
+ * DistanceBetweenCompressedVectors(candidate, EncodeBytes(query)); rq-1
+ * NewDistancer(query).Distance(candidate)) of nq queries (normalised for
+ * cosine like SearchByVector) against slots [0, n): out [nq][n], +inf where a
+ * slot holds no vector */
+int wv_index_rq_distances(wv_index *idx, const float *queries, int64_t nq, int64_t d, float *out, int64_t n);
 
 /* Device-resident batch search for sharded / benchmark callers.
  * mode 0: like SearchByVector (kout = k, tie cases resolved by heap replay).

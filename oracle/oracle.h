@@ -49,6 +49,12 @@ int or_flat_search_bq(int metric, int variant, const float *store, const uint8_t
 int or_filter_by_distance(const uint64_t *ids, const float *dists, int n, float target,
                           uint64_t *out_ids, float *out_dists);
 
+/* pq.c: Go math/rand/v2 PCG-DXSM restatement shared with rq.c */
+typedef struct { uint64_t hi, lo; } pcg_t;
+uint64_t pcg_u64(pcg_t *p);
+uint64_t pcg_u64n(pcg_t *p, uint64_t n);
+double pcg_f64(pcg_t *p);
+
 /* pq.c: product quantizer (see its header) */
 void or_pcg_stream(uint64_t s1, uint64_t s2, int cnt, uint64_t *out);
 void or_random_subset(uint64_t seed, long n, int k, long *out);
@@ -60,6 +66,28 @@ float or_pq_adc(int metric, const float *lut, int m, int k, const uint8_t *code)
 int or_pq_flat_search(int metric, int variant, const float *centers, int m, int ks, int ds, const uint8_t *codes,
                       const float *store, const uint8_t *present, long nslots, const float *query, int k, int limit,
                       int rescore, uint64_t *out_ids, float *out_dists, int *out_n);
+
+/* rq.c: rotational quantization rq-8 / rq-1 (see its header) */
+typedef struct or_rq or_rq;
+or_rq *or_rq_new(int bits, int metric, int dims, uint64_t seed);
+void or_rq_free(or_rq *r);
+int or_rq_out_dim(const or_rq *r);
+void or_rq_tables(const or_rq *r, uint16_t *sI, uint16_t *sJ, float *signs, float *rounding);
+void or_fwht64(float *x);
+void or_fwht256(float *x);
+void or_rq_rotate(const or_rq *r, const float *x, long n, float *rx);
+void or_rq8_encode(const or_rq *r, int variant, const float *x, long n, uint8_t *code);
+float or_rq8_distance(const or_rq *r, const uint8_t *cx, const uint8_t *cy);
+void or_brq_encode(const or_rq *r, const float *x, long n, uint64_t *code);
+void or_brq_encode_query(const or_rq *r, const float *x, long n, float *step_out, float *sqn_out, int *dim_out,
+                         uint64_t *planes);
+float or_brq_distance(const or_rq *r, float qstep, float qsqn, int qdim, const uint64_t *planes,
+                      const uint64_t *cx);
+int or_flat_search_rq(const or_rq *r, int variant, const float *store, const uint8_t *present, const void *codes,
+                      long nslots, long d, const float *query, long qd, int k, int rescore_limit,
+                      const uint8_t *allow, int allow_empty, uint64_t *out_ids, float *out_dists, int *out_n);
+void or_rq_query_distances(const or_rq *r, int variant, const void *codes, long nslots, const float *query, long qd,
+                           float *out);
 
 uint64_t or_gen_bits(uint64_t seed, uint64_t row, uint64_t col);
 float or_gen_value(int kind, uint64_t seed, uint64_t row, uint64_t col);

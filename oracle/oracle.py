@@ -68,6 +68,28 @@ def lib() -> C.CDLL:
         o.or_kmeans_fit.argtypes = [pf, C.c_long, C.c_long, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
                                     C.c_float, C.c_int, pf]
         o.or_pq_encode.argtypes = [pf, C.c_int, C.c_int, C.c_int, C.c_int, pf, pb]
+        vp = C.c_void_p
+        o.or_rq_new.restype = vp
+        o.or_rq_new.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64]
+        o.or_rq_free.argtypes = [vp]
+        o.or_rq_out_dim.restype = C.c_int
+        o.or_rq_out_dim.argtypes = [vp]
+        p16 = C.POINTER(C.c_uint16)
+        o.or_rq_tables.argtypes = [vp, p16, p16, pf, pf]
+        o.or_fwht64.argtypes = [pf]
+        o.or_fwht256.argtypes = [pf]
+        o.or_rq_rotate.argtypes = [vp, pf, C.c_long, pf]
+        o.or_rq8_encode.argtypes = [vp, C.c_int, pf, C.c_long, pb]
+        o.or_rq8_distance.restype = C.c_float
+        o.or_rq8_distance.argtypes = [vp, pb, pb]
+        o.or_brq_encode.argtypes = [vp, pf, C.c_long, pu]
+        o.or_brq_encode_query.argtypes = [vp, pf, C.c_long, pf, pf, pi, pu]
+        o.or_brq_distance.restype = C.c_float
+        o.or_brq_distance.argtypes = [vp, C.c_float, C.c_float, C.c_int, pu, pu]
+        o.or_flat_search_rq.restype = C.c_int
+        o.or_flat_search_rq.argtypes = [vp, C.c_int, pf, pb, vp, C.c_long, C.c_long, pf, C.c_long, C.c_int, C.c_int,
+                                        pb, C.c_int, pu, pf, pi]
+        o.or_rq_query_distances.argtypes = [vp, C.c_int, vp, C.c_long, pf, C.c_long, pf]
         o.or_pq_lut.argtypes = [C.c_int, pf, C.c_int, C.c_int, C.c_int, pf, pf]
         o.or_pq_adc.restype = C.c_float
         o.or_pq_adc.argtypes = [C.c_int, pf, C.c_int, C.c_int, pb]
@@ -317,6 +339,116 @@ def cpu_baseline_pq(metric: int, centers: np.ndarray, codes: np.ndarray, queries
                              codes.shape[0], f(queries), nq, k, nthreads, ids.ctypes.data_as(pu), f(dd),
                              cnt.ctypes.data_as(pi))
     return ids, dd, cnt
+
+
+DEFAULT_FAST_ROTATION_SEED = 0x535AB5105169B1DF  # compressionhelpers/fast_rotation.go:27
+
+
+class RQ:
+    """Rotational quantizer restatement (oracle/rq.c): bits 8 = RotationalQuantizer
+    (rotational_quantization.go), bits 1 = BinaryRotationalQuantizer
+    (binary_rotational_quantization.go), with flat's seed and rounds."""
+
+    def __init__(self, bits: int, metric: int, dims: int, seed: int = DEFAULT_FAST_ROTATION_SEED):
+        self.bits, self.metric, self.dims = bits, metric, dims
+        self.h = lib().or_rq_new(bits, metric, dims, seed)
+        if not self.h:
+            raise ValueError("unsupported rq configuration")
+        self.D = lib().or_rq_out_dim(self.h)
+        self.W = self.D // 64
+        self.code_len = (16 + self.D) if bits == 8 else (1 + self.W)  # bytes / u64 words
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_rq_free(self.h)
+            self.h = None
+
+    def tables(self):
+        sI = np.zeros((3, self.D // 2), np.uint16)
+        sJ = np.zeros((3, self.D // 2), np.uint16)
+        sg = np.zeros((3, self.D), np.float32)
+        rd = np.zeros(self.D, np.float32)
+        p16 = C.POINTER(C.c_uint16)
+        lib().or_rq_tables(self.h, sI.ctypes.data_as(p16), sJ.ctypes.data_as(p16), f(sg), f(rd))
+        return sI, sJ, sg, rd
+
+    def rotate(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float32)
+        out = np.zeros(self.D, np.float32)
+        lib().or_rq_rotate(self.h, f(x), x.size, f(out))
+        return out
+
+    def encode(self, x: np.ndarray, variant: int = AVX256) -> np.ndarray:
+        """rq-8: RQCode bytes [16 + D]; rq-1: RQOneBitCode words [1 + D/64]"""
+        x = np.ascontiguousarray(x, np.float32)
+        if self.bits == 8:
+            out = np.zeros(self.code_len, np.uint8)
+            lib().or_rq8_encode(self.h, variant, f(x), x.size, out.ctypes.data_as(pb))
+        else:
+            out = np.zeros(self.code_len, np.uint64)
+            lib().or_brq_encode(self.h, f(x), x.size, out.ctypes.data_as(pu))
+        return out
+
+    def encode_query(self, x: np.ndarray):
+        """rq-1 encodeQuery -> (step, squared norm, dim, planes [5][W])"""
+        x = np.ascontiguousarray(x, np.float32)
+        planes = np.zeros((5, self.W), np.uint64)
+        st, sq, dim = C.c_float(0), C.c_float(0), C.c_int(0)
+        lib().or_brq_encode_query(self.h, f(x), x.size, C.byref(st), C.byref(sq), C.byref(dim),
+                                  planes.ctypes.data_as(pu))
+        return st.value, sq.value, dim.value, planes
+
+    def distance(self, cx: np.ndarray, query) -> float:
+        """rq-8: DistanceBetweenCompressedVectors(cx, cy=query code);
+        rq-1: BinaryRQDistancer.Distance(cx) with query = encode_query(...)"""
+        if self.bits == 8:
+            return lib().or_rq8_distance(self.h, np.ascontiguousarray(cx, np.uint8).ctypes.data_as(pb),
+                                         np.ascontiguousarray(query, np.uint8).ctypes.data_as(pb))
+        st, sq, dim, planes = query
+        return lib().or_brq_distance(self.h, st, sq, dim, np.ascontiguousarray(planes, np.uint64).ctypes.data_as(pu),
+                                     np.ascontiguousarray(cx, np.uint64).ctypes.data_as(pu))
+
+
+class OracleFlatRQ(OracleFlat):
+    """Oracle flat index with rq-8 / rq-1 compression (flat/index.go:338-360 creates
+    the quantizer at the first Add; :460-532 searches)."""
+
+    def __init__(self, bits: int, metric: int, variant: int, d: int, nslots: int, rescore_limit: int = -1):
+        super().__init__(metric, variant, d, nslots)
+        self.rescore_limit = rescore_limit
+        self.rq = RQ(bits, metric, d)
+        dt = np.uint8 if bits == 8 else np.uint64
+        self.codes = np.zeros((nslots, self.rq.code_len), dtype=dt)
+
+    def add_batch(self, ids, vecs):
+        super().add_batch(ids, vecs)
+        for i in ids:
+            self.codes[int(i)] = self.rq.encode(self.store[int(i)], self.variant)
+
+    def query_distances(self, query) -> np.ndarray:
+        q = np.ascontiguousarray(query, dtype=np.float32)
+        out = np.zeros(len(self.present), np.float32)
+        lib().or_rq_query_distances(self.rq.h, self.variant, self.codes.ctypes.data, len(self.present), f(q), q.size,
+                                    f(out))
+        return out
+
+    def search(self, query, k, allow=None):
+        q = np.ascontiguousarray(query, dtype=np.float32)
+        ids = np.zeros(max(k, 1), dtype=np.uint64)
+        dd = np.zeros(max(k, 1), dtype=np.float32)
+        n = C.c_int(0)
+        allow_bm = None
+        allow_empty = 0
+        if allow is not None:
+            allow_bm = np.zeros(len(self.present), dtype=np.uint8)
+            a = [int(x) for x in allow if int(x) < len(self.present)]
+            allow_bm[a] = 1
+            allow_empty = 1 if len(list(allow)) == 0 else 0
+        rc = lib().or_flat_search_rq(self.rq.h, self.variant, f(self.store), self.present.ctypes.data_as(pb),
+                                     self.codes.ctypes.data, len(self.present), self.d, f(q), q.size, k,
+                                     self.rescore_limit, allow_bm.ctypes.data_as(pb) if allow_bm is not None else None,
+                                     allow_empty, ids.ctypes.data_as(pu), f(dd), C.byref(n))
+        return rc, ids[: n.value].copy(), dd[: n.value].copy()
 
 
 def gen_matrix(kind: int, seed: int, row0: int, rows: int, d: int) -> np.ndarray:

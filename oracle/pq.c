@@ -25,7 +25,6 @@
 #include "oracle.h"
 
 /* ---- Go math/rand/v2 ------------------------------------------------------ */
-typedef struct { uint64_t hi, lo; } pcg_t;
 
 /* pcg.go: state = state * mul + inc (128-bit LCG) */
 static void pcg_next(pcg_t *p, uint64_t *ohi, uint64_t *olo) {
@@ -44,7 +43,7 @@ static void pcg_next(pcg_t *p, uint64_t *ohi, uint64_t *olo) {
 }
 
 /* pcg.go Uint64: DXSM output */
-static uint64_t pcg_u64(pcg_t *p) {
+uint64_t pcg_u64(pcg_t *p) {
     uint64_t hi, lo;
     pcg_next(p, &hi, &lo);
     const uint64_t cheapMul = 0xda942042e4dd58b5ULL;
@@ -56,7 +55,7 @@ static uint64_t pcg_u64(pcg_t *p) {
 }
 
 /* rand.go uint64n (64-bit platform): power of two mask, else Lemire */
-static uint64_t pcg_u64n(pcg_t *p, uint64_t n) {
+uint64_t pcg_u64n(pcg_t *p, uint64_t n) {
     if ((n & (n - 1)) == 0) return pcg_u64(p) & (n - 1);
     __uint128_t m = (__uint128_t)pcg_u64(p) * n;
     uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
@@ -71,7 +70,7 @@ static uint64_t pcg_u64n(pcg_t *p, uint64_t n) {
     return hi;
 }
 
-static double pcg_f64(pcg_t *p) { return (double)((pcg_u64(p) << 11) >> 11) / 9007199254740992.0; }
+double pcg_f64(pcg_t *p) { return (double)((pcg_u64(p) << 11) >> 11) / 9007199254740992.0; }
 
 /* exported for tests: first `cnt` Uint64 draws of NewPCG(s1, s2) */
 void or_pcg_stream(uint64_t s1, uint64_t s2, int cnt, uint64_t *out) {

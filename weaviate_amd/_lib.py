@@ -31,6 +31,8 @@ VARIANT_AVX512 = 2
 COMPRESSION_NONE = 0
 COMPRESSION_BQ = 1
 COMPRESSION_PQ = 2
+COMPRESSION_RQ8 = 3
+COMPRESSION_RQ1 = 4
 
 
 class WvConfig(C.Structure):
@@ -104,6 +106,9 @@ SIGNATURES = {
     "wv_index_pq_codes": (C.c_int, [P, C.POINTER(C.c_uint8), i64]),
     "wv_index_pq_info": (C.c_int, [P, pi32]),
     "wv_index_pq_distance": (C.c_int, [P, pf32, i64, C.POINTER(C.c_uint8), i64, pf32]),
+    "wv_index_rq_info": (C.c_int, [P, pi32]),
+    "wv_index_rq_codes": (C.c_int, [P, P, i64]),
+    "wv_index_rq_distances": (C.c_int, [P, pf32, i64, i64, pf32, i64]),
     "wv_index_set_option": (C.c_int, [P, C.c_char_p, i64]),
 }
 

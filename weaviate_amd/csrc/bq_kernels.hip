@@ -297,7 +297,8 @@ __global__ __launch_bounds__(64) void k_rescore_ids(const float* __restrict__ X,
     outE[p] = exact_dist<METRIC, VARIANT>(Q + (int64_t)qlist[li] * dpad, X + (int64_t)(id - id_base) * dpad, d);
 }
 
-// Rescoring heap (flat/index.go:525-531): the candidates, in pop order, go
+// Rescoring heap (flat/index.go:525-531): the candidates, in pop order (asc = 1:
+// stored ascending, i.e. extractHeap order, read back to front), go
 // through insertToHeap(heap, k, id, dist); extractHeap gives the result.
 // One wave per listed query; lane 0 runs the heap in LDS ([k] u64 | [k] f32).
 // world > 1: candE is [world][nlist][R] (each shard's exact distances of the
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(64) void k_bq_final(const uint64_t* __restrict__ ca
                                                  const int32_t* __restrict__ cand_n, const int32_t* __restrict__ qlist,
                                                  int nlist, int R, int k, int world, uint64_t id_stride,
                                                  uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
-                                                 int32_t* __restrict__ out_n) {
+                                                 int32_t* __restrict__ out_n, int asc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(fsm);
     float* hd = reinterpret_cast<float*>(hid + k);
@@ -316,7 +317,8 @@ __global__ __launch_bounds__(64) void k_bq_final(const uint64_t* __restrict__ ca
     const int q = qlist[li];
     ReplayHeap hp{hid, hd, 0};
     const int n = cand_n[li];
-    for (int i = 0; i < n; i++) {
+    for (int ii = 0; ii < n; ii++) {
+        const int i = asc ? n - 1 - ii : ii;  // asc: candidates extracted ascending, pop order = reversed
         const uint64_t id = cand_ids[(int64_t)li * R + i];
         uint64_t owner = 0;
         if (world > 1) { owner = id / id_stride; if (owner > (uint64_t)(world - 1)) owner = world - 1; }

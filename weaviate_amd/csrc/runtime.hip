@@ -26,6 +26,7 @@
 #include "bq_kernels.hip"
 #include "pq_kernels.hip"
 #include "kernels_bf3.hip"
+#include "rq_kernels.hip"
 
 using namespace wv;
 
@@ -139,11 +140,19 @@ struct wv_index {
     int last_KP = 0;
     uint16_t* Xh = nullptr;
     uint16_t* Xl = nullptr;
+    // rq-8 / rq-1 (rq_kernels.hip): rotation tables built at the first Add
+    // (initializeDimensionsAndRQ, flat/index.go:338-360), codes + meta per slot
+    int rq_bits = 0, rq_D = 0, rq_ready = 0;
+    uint16_t* rq_src = nullptr;   // [3][D]
+    float* rq_sign = nullptr;     // [3][D]
+    float* rq_round = nullptr;    // [D] (rq-1)
+    void* rq_codes = nullptr;     // rq-8: tiled [cap][D] bytes; rq-1: [D/64][cap] u64
+    float4* rq_meta = nullptr;    // [cap]
     std::vector<uint8_t> h_present;
     uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
     int64_t npresent = 0;
 
-    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, qh, ql;
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, qh, ql, rqq, rqm;
 
     int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0, sel_dbg = 0, qgroup_opt = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -158,8 +167,15 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     if (cfg->metric < 0 || cfg->metric > WV_METRIC_HAMMING)
         return set_err(WV_ERR_INVALID, "invalid config: unknown distance metric %d", cfg->metric);
     if (cfg->compression != WV_COMPRESSION_NONE && cfg->compression != WV_COMPRESSION_BQ &&
-        cfg->compression != WV_COMPRESSION_PQ)
+        cfg->compression != WV_COMPRESSION_PQ && cfg->compression != WV_COMPRESSION_RQ8 &&
+        cfg->compression != WV_COMPRESSION_RQ1)
         return set_err(WV_ERR_UNSUPPORTED, "invalid config: unsupported compression %d", cfg->compression);
+    // distancerIndicatorsAndError (rotational_quantization.go:41-55)
+    if ((cfg->compression == WV_COMPRESSION_RQ8 || cfg->compression == WV_COMPRESSION_RQ1) &&
+        cfg->metric == WV_METRIC_HAMMING)
+        return set_err(WV_ERR_UNSUPPORTED, "Distance not supported yet hamming");
+    if (cfg->dims > RQ_MAXD - 64 && (cfg->compression == WV_COMPRESSION_RQ8 || cfg->compression == WV_COMPRESSION_RQ1))
+        return set_err(WV_ERR_UNSUPPORTED, "rq: dimensions > %d not supported", RQ_MAXD - 64);
     HIPCHK(hipSetDevice(cfg->device));
     wv_index* idx = new wv_index();
     idx->metric = cfg->metric;
@@ -172,6 +188,8 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     // bf16x3 select kernel for the exact fp32 path (kernels_bf3.hip)
     idx->use_bf3 = (cfg->compression == WV_COMPRESSION_NONE && cfg->metric != WV_METRIC_HAMMING) ? 1 : 0;
     idx->kernel_opt = idx->use_bf3 ? 4 : 3;
+    if (cfg->compression == WV_COMPRESSION_RQ8) idx->rq_bits = 8;
+    if (cfg->compression == WV_COMPRESSION_RQ1) idx->rq_bits = 1;
     if (cfg->compression == WV_COMPRESSION_PQ) {
         idx->pq_m = cfg->pq_segments;
         idx->pq_ks = cfg->pq_centroids;
@@ -199,7 +217,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
-                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql})
+                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm})
         b->release();
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
@@ -210,6 +228,8 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->pq_codes) hipFree(idx->pq_codes);
     if (idx->Xh) hipFree(idx->Xh);
     if (idx->Xl) hipFree(idx->Xl);
+    for (void* p : {(void*)idx->rq_src, (void*)idx->rq_sign, (void*)idx->rq_round, idx->rq_codes, (void*)idx->rq_meta})
+        if (p) hipFree(p);
     if (idx->ev0) hipEventDestroy(idx->ev0);
     if (idx->ev1) hipEventDestroy(idx->ev1);
     if (idx->stream) hipStreamDestroy(idx->stream);
@@ -272,6 +292,31 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         if (idx->Xl) hipFree(idx->Xl);
         idx->Xh = xh;
         idx->Xl = xl;
+    }
+    if (idx->rq_ready) {
+        const size_t cb = idx->rq_bits == 8 ? (size_t)nc * idx->rq_D : (size_t)(idx->rq_D / 64) * nc * sizeof(uint64_t);
+        void* cd = nullptr;
+        float4* md = nullptr;
+        HIPCHK(hipMalloc(&cd, cb));
+        HIPCHK(hipMalloc(&md, (size_t)nc * sizeof(float4)));
+        HIPCHK(hipMemsetAsync(cd, 0, cb, idx->stream));
+        HIPCHK(hipMemsetAsync(md, 0, (size_t)nc * sizeof(float4), idx->stream));
+        if (idx->cap > 0 && idx->rq_codes) {
+            if (idx->rq_bits == 8)  // tiles of 256 rows are contiguous: the old tiles are a prefix
+                HIPCHK(hipMemcpyAsync(cd, idx->rq_codes, (size_t)idx->cap * idx->rq_D, hipMemcpyDeviceToDevice,
+                                      idx->stream));
+            else
+                HIPCHK(hipMemcpy2DAsync(cd, (size_t)nc * sizeof(uint64_t), idx->rq_codes,
+                                        (size_t)idx->cap * sizeof(uint64_t), (size_t)idx->cap * sizeof(uint64_t),
+                                        idx->rq_D / 64, hipMemcpyDeviceToDevice, idx->stream));
+            HIPCHK(hipMemcpyAsync(md, idx->rq_meta, (size_t)idx->cap * sizeof(float4), hipMemcpyDeviceToDevice,
+                                  idx->stream));
+        }
+        HIPCHK(hipStreamSynchronize(idx->stream));
+        if (idx->rq_codes) hipFree(idx->rq_codes);
+        if (idx->rq_meta) hipFree(idx->rq_meta);
+        idx->rq_codes = cd;
+        idx->rq_meta = md;
     }
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0) {
         const int64_t mw = pq_mwp(idx->pq_m);
@@ -338,6 +383,24 @@ static void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots) 
 #undef WV_PE
 }
 
+// rq-8 / rq-1 encode of n rows (rows[slot * ld], slot = slots[r] or r) into the
+// data layout (query = 0) or the group-tiled query layout (query = 1)
+static void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t ld, int64_t n,
+                             const uint32_t* d_slots, int query, void* codes, int64_t cap, float4* meta) {
+    if (n <= 0) return;
+    const size_t lds = 2 * (size_t)idx->rq_D * sizeof(float);
+    const bool v5 = idx->variant == WV_VARIANT_AVX512;
+#define WV_RQE(B, V, Q) k_rq_encode<B, V, Q><<<(unsigned)n, 256, lds, s>>>(rows, ld, n, idx->dims, d_slots, idx->rq_D, idx->rq_src, idx->rq_sign, idx->rq_round, codes, cap, meta)
+    if (idx->rq_bits == 8) {
+        if (query) { if (v5) WV_RQE(8, AVX512, 1); else WV_RQE(8, AVX256, 1); }
+        else { if (v5) WV_RQE(8, AVX512, 0); else WV_RQE(8, AVX256, 0); }
+    } else {
+        if (query) WV_RQE(1, AVX256, 1);
+        else WV_RQE(1, AVX256, 0);
+    }
+#undef WV_RQE
+}
+
 static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const uint32_t* d_slots) {
     dim3 grid((unsigned)((n + 255) / 256));
     switch (idx->metric) {
@@ -356,12 +419,16 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
                                                                            idx->Xl);
     }
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) launch_pq_encode(idx, n, d_slots);
+    if (idx->rq_ready)  // Preload: quantizer.EncodeBytes / EncodeUint64 of the stored row (flat/index.go:844-865)
+        launch_rq_encode(idx, idx->stream, idx->X, idx->dpad, n, d_slots, 0, idx->rq_codes, idx->cap, idx->rq_meta);
     if (idx->compression == WV_COMPRESSION_BQ) {  // Preload: quantizer.Encode of the stored row (flat/index.go:376)
         const int64_t nt = n * idx->words;
         k_bq_encode_rows<<<(unsigned)((nt + 255) / 256), 256, 0, idx->stream>>>(idx->X, idx->dpad, n, idx->dims, d_slots,
                                                                                  idx->codes, idx->cap);
     }
 }
+
+static int rq_init(wv_index* idx);
 
 // rows: host pointer to n x d floats; ids: host doc ids
 static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs, int64_t n, int64_t d) {
@@ -371,6 +438,10 @@ static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs
         if (d > (1 << 20)) return set_err(WV_ERR_INVALID, "dimensions too large: %lld", (long long)d);
         idx->dims = (int)d;
         idx->dpad = (int)round_up(d, BK);
+    }
+    if (idx->rq_bits && !idx->rq_ready) {
+        rc = rq_init(idx);
+        if (rc) return rc;
     }
     // upsert semantics of the replace bucket: the last write of an id wins.
     std::unordered_map<uint64_t, int64_t> last;
@@ -445,6 +516,10 @@ extern "C" int wv_index_add_range_device(wv_index* idx, uint64_t first_id, const
     int rc = validate_insert(idx, d);
     if (rc) return rc;
     if (idx->dims == 0) { idx->dims = (int)d; idx->dpad = (int)round_up(d, BK); }
+    if (idx->rq_bits && !idx->rq_ready) {
+        rc = rq_init(idx);
+        if (rc) return rc;
+    }
     if (first_id < idx->id_base) return set_err(WV_ERR_INVALID, "id below shard id_base");
     int64_t s0 = (int64_t)(first_id - idx->id_base);
     rc = ensure_capacity(idx, s0 + n);
@@ -798,7 +873,7 @@ static int bq_final(hipStream_t s, int64_t nq, int R, int k, int world, uint64_t
     const size_t lds_f = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
     if (lds_f > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_bq_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
-    k_bq_final<<<(unsigned)nq, 64, lds_f, s>>>(ids, E, cnt, qlist, (int)nq, R, k, world, id_stride, o_ids, o_d, o_n);
+    k_bq_final<<<(unsigned)nq, 64, lds_f, s>>>(ids, E, cnt, qlist, (int)nq, R, k, world, id_stride, o_ids, o_d, o_n, 0);
     HIPCHK(hipGetLastError());
     return WV_OK;
 }
@@ -1315,6 +1390,262 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     return WV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// rotational quantization: flat "rq-8" / "rq-1" (flat/quantizer.go:85-99)
+// ---------------------------------------------------------------------------
+static constexpr uint64_t kDefaultFastRotationSeed = 0x535ab5105169b1dfULL;  // fast_rotation.go:27
+
+// NewFastRotation (fast_rotation.go:72-90) -> per-round gather tables, and the
+// rq-1 rounding vector (binary_rotational_quantization.go:52-56); then the code
+// store for the current capacity.
+static int rq_init(wv_index* idx) {
+    const int in_dim = (idx->rq_bits == 1 && idx->dims < 256) ? 256 : idx->dims;  // minCodeBits
+    int D = 64;
+    while (D < in_dim) D += 64;
+    if (D > RQ_MAXD) return set_err(WV_ERR_UNSUPPORTED, "rq: output dimension %d > %d", D, RQ_MAXD);
+    std::vector<uint16_t> src((size_t)RQ_ROUNDS * D);
+    std::vector<float> sign((size_t)RQ_ROUNDS * D), rnd((size_t)D);
+    GoPCG r{kDefaultFastRotationSeed, 0x385ab5285169b1acULL};
+    std::vector<int> perm((size_t)D);
+    for (int rd = 0; rd < RQ_ROUNDS; rd++) {
+        for (int i = 0; i < D; i++) perm[i] = i;  // rng.Perm(n): Shuffle with uint64n
+        for (int i = D - 1; i > 0; i--) std::swap(perm[i], perm[(size_t)r.u64n((uint64_t)(i + 1))]);
+        std::vector<float> sg((size_t)D);
+        for (int i = 0; i < D; i++) sg[i] = r.f64() < 0.5 ? -1.0f : 1.0f;  // randomSigns
+        // swap (I, J): new[I] = sign[I] * old[J], new[J] = sign[J] * old[I]
+        for (int p = 0; p < D / 2; p++) {
+            const int a = perm[2 * p], b = perm[2 * p + 1];
+            src[(size_t)rd * D + a] = (uint16_t)b;
+            src[(size_t)rd * D + b] = (uint16_t)a;
+        }
+        for (int i = 0; i < D; i++) sign[(size_t)rd * D + i] = sg[i];
+    }
+    if (idx->rq_bits == 1) {
+        GoPCG rr{kDefaultFastRotationSeed, 0x4f8ebf70e130707fULL};
+        for (int i = 0; i < D; i++) {  // rng.Float32(): float32(Uint32()<<8>>8) / 2^24
+            const uint32_t u = (uint32_t)(rr.next_u64() >> 32);
+            rnd[i] = (float)((u << 8) >> 8) / 16777216.0f;
+        }
+    }
+    HIPCHK(hipMalloc(&idx->rq_src, src.size() * sizeof(uint16_t)));
+    HIPCHK(hipMalloc(&idx->rq_sign, sign.size() * sizeof(float)));
+    HIPCHK(hipMalloc(&idx->rq_round, rnd.size() * sizeof(float)));
+    HIPCHK(hipMemcpy(idx->rq_src, src.data(), src.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(idx->rq_sign, sign.data(), sign.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(idx->rq_round, rnd.data(), rnd.size() * sizeof(float), hipMemcpyHostToDevice));
+    idx->rq_D = D;
+    idx->rq_ready = 1;
+    if (idx->cap > 0) {  // store already sized (reserve): allocate the codes for it
+        const size_t cb = idx->rq_bits == 8 ? (size_t)idx->cap * D : (size_t)(D / 64) * idx->cap * sizeof(uint64_t);
+        HIPCHK(hipMalloc(&idx->rq_codes, cb));
+        HIPCHK(hipMalloc(&idx->rq_meta, (size_t)idx->cap * sizeof(float4)));
+        HIPCHK(hipMemset(idx->rq_codes, 0, cb));
+        HIPCHK(hipMemset(idx->rq_meta, 0, (size_t)idx->cap * sizeof(float4)));
+    }
+    return WV_OK;
+}
+
+// encode nq prepared query rows (idx->qn, normalised for cosine) into idx->rqq / rqm
+static int rq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq) {
+    const int64_t nq32 = round_up(nq, RQ_QPB);
+    const size_t qb = idx->rq_bits == 8 ? (size_t)nq32 * idx->rq_D : (size_t)nq32 * 5 * (idx->rq_D / 64) * sizeof(uint64_t);
+    HIPCHK(idx->rqq.ensure(qb));
+    HIPCHK(idx->rqm.ensure((size_t)nq32 * sizeof(float4)));
+    if (nq32 > nq) {  // padded group members: zero codes (their results are never written)
+        HIPCHK(hipMemsetAsync(idx->rqq.p, 0, qb, s));
+        HIPCHK(hipMemsetAsync(idx->rqm.p, 0, (size_t)nq32 * sizeof(float4), s));
+    }
+    launch_rq_encode(idx, s, idx->qn.as<float>(), idx->dpad, nq, nullptr, 1, idx->rqq.p, 0, idx->rqm.as<float4>());
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
+// quantized distances of queries [q0, q0 + F) (q0 % RQ_QPB == 0) -> E [F][ld], bmin
+static int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int F, int64_t ld, float* E,
+                   float* bmin) {
+    const int64_t nslots = idx->hiwater;
+    const float fl2 = idx->metric == WV_METRIC_L2_SQUARED ? 1.f : 0.f;
+    const float fcos = idx->metric == WV_METRIC_COSINE_DOT ? 1.f : 0.f;
+    dim3 grid((unsigned)((F + RQ_QPB - 1) / RQ_QPB), (unsigned)(ld / 256));
+    if (idx->rq_bits == 8)
+        k_rq8_dist<<<grid, 256, 0, s>>>(reinterpret_cast<const uint4*>(idx->rq_codes), idx->rq_meta, idx->rq_D, valid,
+                                        nslots, idx->rqq.as<uint4>(), idx->rqm.as<float4>(), q0, F, fl2, fcos, ld, E,
+                                        bmin);
+    else
+        k_rq1_dist<<<grid, 256, 0, s>>>(reinterpret_cast<const uint64_t*>(idx->rq_codes), idx->cap, idx->rq_meta,
+                                        idx->rq_D / 64, valid, nslots, idx->rqq.as<uint64_t>(), idx->rqm.as<float4>(),
+                                        q0, F, fl2, fcos, ld, E, bmin);
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
+// flat.searchByVectorQuantized (flat/index.go:460-532) for rq-8 / rq-1: exact
+// quantized distances + block minima (k_rq*_dist), the R-heap replayed in id
+// order (k_replay_scan, extracted ascending = reversed pop order), fp32
+// rescoring of the candidates (k_rescore_ids) and the k-heap fed in pop order
+// (k_bq_final with asc = 1).
+static int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
+                     const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+    if (qd != idx->dims)  // SingleDist of the rescoring (distancer/errors.go:16)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)qd, idx->dims);
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    if (!idx->rq_ready) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    const int R = idx->rescore_limit > k ? idx->rescore_limit : k;  // searchTimeRescore (:413-421)
+    if (R > 8192) return set_err(WV_ERR_UNSUPPORTED, "rescore limit %d > 8192", R);
+    const int64_t nq_pad = round_up(nq, QB);
+    int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
+    if (rc) return rc;
+    rc = rq_encode_queries(idx, s, nq);
+    if (rc) return rc;
+    idx->stats.queries += (uint64_t)nq;
+    idx->stats.batches++;
+    idx->stats.replayed_queries += (uint64_t)nq;
+    HIPCHK(idx->ident.ensure((size_t)nq * sizeof(int32_t)));
+    {
+        std::vector<int32_t> id((size_t)nq);
+        for (int64_t i = 0; i < nq; i++) id[i] = (int32_t)i;
+        HIPCHK(hipMemcpyAsync(idx->ident.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    const int32_t* qlist = idx->ident.as<int32_t>();
+    const int64_t nslots = idx->hiwater;
+    const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
+    // query groups: multiples of RQ_QPB, distance buffer bounded to 4 GiB
+    int64_t G = ((4ll << 30) / (ld * 4)) / RQ_QPB * RQ_QPB;
+    G = std::max<int64_t>(RQ_QPB, std::min<int64_t>(G, round_up(nq, RQ_QPB)));
+    HIPCHK(idx->rE.ensure((size_t)G * ld * sizeof(float)));
+    HIPCHK(idx->rB.ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+    HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
+    HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
+    HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
+    const size_t lds_rep = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
+    if (lds_rep > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rep));
+    for (int64_t g0 = 0; g0 < nq; g0 += G) {
+        const int F = (int)std::min<int64_t>(G, nq - g0);
+        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
+        rc = rq_dist(idx, s, valid, g0, F, ld, idx->rE.as<float>(), idx->rB.as<float>());
+        if (rc) return rc;
+        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
+        k_replay_scan<<<F, 64, lds_rep, s>>>(idx->rE.as<float>(), idx->rB.as<float>(), valid, nslots, ld, qlist + g0, F,
+                                             R, idx->id_base, nullptr, nullptr, nullptr, 1, 0, R,
+                                             idx->ascI.as<uint64_t>() + g0 * R, idx->ascD.as<float>() + g0 * R,
+                                             idx->ascN.as<int32_t>() + g0);
+        HIPCHK(hipGetLastError());
+    }
+    idx->bq_nq = nq;
+    idx->bq_R = R;
+    rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
+    if (rc) return rc;
+    const size_t lds_f = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
+    if (lds_f > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_bq_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
+    k_bq_final<<<(unsigned)nq, 64, lds_f, s>>>(idx->ascI.as<uint64_t>(), idx->candE.as<float>(), idx->ascN.as<int32_t>(),
+                                               qlist, (int)nq, R, k, 1, 0, o_ids, o_d, o_n, 1);
+    HIPCHK(hipGetLastError());
+    if (idx->timing) {
+        HIPCHK(hipStreamSynchronize(s));
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
+        idx->stats.last_select_ms = ms;
+    }
+    return WV_OK;
+}
+
+extern "C" int wv_index_rq_info(wv_index* idx, int32_t* out) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    out[0] = idx->rq_bits;
+    out[1] = idx->rq_D;
+    out[2] = idx->rq_bits == 8 ? 16 + idx->rq_D : idx->rq_bits == 1 ? 8 * (1 + idx->rq_D / 64) : 0;
+    out[3] = idx->rq_ready;
+    return WV_OK;
+}
+
+static inline void put_be32(uint8_t* b, float x) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    b[0] = (uint8_t)(u >> 24); b[1] = (uint8_t)(u >> 16); b[2] = (uint8_t)(u >> 8); b[3] = (uint8_t)u;
+}
+
+// codes of slots [0, n) in the reference's compressed-bucket formats:
+// rq-8 RQCode (rotational_quantization.go:95-155, BE floats + bytes),
+// rq-1 RQOneBitCode words (binary_rotational_quantization.go:92-148, LE u64)
+extern "C" int wv_index_rq_codes(wv_index* idx, void* out, int64_t n) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (!idx->rq_ready) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (n < 0 || n > idx->cap) return set_err(WV_ERR_INVALID, "rq_codes: n out of range");
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    const int D = idx->rq_D, W = D / 64;
+    std::vector<float4> meta((size_t)std::max<int64_t>(n, 1));
+    if (n) HIPCHK(hipMemcpy(meta.data(), idx->rq_meta, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
+    if (idx->rq_bits == 8) {
+        const int64_t ntile = (n + 255) / 256;
+        std::vector<uint8_t> tiled((size_t)std::max<int64_t>(ntile * 256 * D, 1));
+        if (n) HIPCHK(hipMemcpy(tiled.data(), idx->rq_codes, (size_t)ntile * 256 * D, hipMemcpyDeviceToHost));
+        uint8_t* o = (uint8_t*)out;
+        const int nch = D / 16;
+        for (int64_t s = 0; s < n; s++) {
+            uint8_t* c = o + (size_t)s * (16 + D);
+            put_be32(c + 0, meta[s].x);
+            put_be32(c + 4, meta[s].y);
+            put_be32(c + 8, meta[s].z);
+            put_be32(c + 12, meta[s].w);
+            for (int ch = 0; ch < nch; ch++)
+                memcpy(c + 16 + ch * 16, &tiled[((size_t)((s >> 8) * nch + ch) * 256 + (s & 255)) * 16], 16);
+        }
+    } else {
+        std::vector<uint64_t> words((size_t)W * std::max<int64_t>(n, 1));
+        if (n)
+            HIPCHK(hipMemcpy2D(words.data(), (size_t)n * sizeof(uint64_t), idx->rq_codes, (size_t)idx->cap * sizeof(uint64_t),
+                               (size_t)n * sizeof(uint64_t), W, hipMemcpyDeviceToHost));
+        uint64_t* o = (uint64_t*)out;
+        for (int64_t s = 0; s < n; s++) {
+            uint32_t st, sq;
+            memcpy(&st, &meta[s].x, 4);
+            memcpy(&sq, &meta[s].y, 4);
+            o[(size_t)s * (1 + W)] = ((uint64_t)sq << 32) | st;
+            for (int w = 0; w < W; w++) o[(size_t)s * (1 + W) + 1 + w] = words[(size_t)w * n + s];
+        }
+    }
+    return WV_OK;
+}
+
+// quantized distances (the distancer the scan uses) of nq queries against
+// slots [0, n): out [nq][n], +inf for slots without a vector
+extern "C" int wv_index_rq_distances(wv_index* idx, const float* queries, int64_t nq, int64_t d, float* out,
+                                     int64_t n) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (!idx->rq_ready) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (d != idx->dims) return set_err(WV_ERR_VECTOR_LENGTH, "vector lengths don't match");
+    if (n < 0 || n > idx->hiwater || nq <= 0) return set_err(WV_ERR_INVALID, "rq_distances: bad sizes");
+    hipStream_t s = idx->stream;
+    HIPCHK(idx->qraw.ensure((size_t)nq * d * sizeof(float)));
+    HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
+    int rc = prepare_queries(idx, s, idx->qraw.as<float>(), nq, round_up(nq, QB));
+    if (rc) return rc;
+    rc = rq_encode_queries(idx, s, nq);
+    if (rc) return rc;
+    const int64_t ld = std::max<int64_t>(round_up(idx->hiwater, EBLK), EBLK);
+    const int64_t nq32 = round_up(nq, RQ_QPB);
+    DBuf E, B;
+    HIPCHK(E.ensure((size_t)nq32 * ld * sizeof(float)));
+    HIPCHK(B.ensure((size_t)nq32 * (ld / EBLK) * sizeof(float)));
+    rc = rq_dist(idx, s, idx->present, 0, (int)nq, ld, E.as<float>(), B.as<float>());
+    if (rc) return rc;
+    if (n > 0)
+        HIPCHK(hipMemcpy2DAsync(out, (size_t)n * sizeof(float), E.p, (size_t)ld * sizeof(float), (size_t)n * sizeof(float),
+                                nq, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    E.release();
+    B.release();
+    return WV_OK;
+}
+
 // Core batch search on device queries.  Outputs [nq][kout] device arrays.
 // mode 0: kout = k, flagged queries resolved by replay; mode 1: kout = k+1,
 // flags left for the caller.  n_valid = number of scan candidates.
@@ -1331,6 +1662,10 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     if (idx->compression == WV_COMPRESSION_BQ) {
         if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "bq: shard-candidate mode not available");
         return search_bq(idx, s, d_qraw, nq, qd, k, valid, o_ids, o_d, o_n);
+    }
+    if (idx->rq_bits) {
+        if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "rq: shard-candidate mode not available");
+        return search_rq(idx, s, d_qraw, nq, qd, k, valid, o_ids, o_d, o_n);
     }
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) {
         if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "pq: shard-candidate mode not available");

@@ -65,14 +65,21 @@ class FlatIndex:
 
     def __init__(self, distance: str = "cosine", dims: int = 0, device: int = 0, variant: str = "auto",
                  root_path: str = "", id_base: int = 0, bq: bool = False, rescore_limit: int = -1,
-                 pq: Optional[dict] = None):
+                 pq: Optional[dict] = None, rq: Optional[dict] = None):
         if distance not in DISTANCES:
             raise WeaviateError(_lib.WV_ERR_INVALID, f"unrecognized or unsupported distance metric {distance!r}")
         self._l = _lib.load()
         self._root = root_path.encode()
         # pq: ent.PQConfig subset {"segments", "centroids" (256), "trainingLimit" (100000), "rescore" (True)}
         pqc = dict(pq or {})
-        comp = _lib.COMPRESSION_BQ if bq else _lib.COMPRESSION_PQ if pq is not None else _lib.COMPRESSION_NONE
+        # rq: flatent RQ config subset {"bits": 8 | 1} (entities/vectorindex/flat/config.go:27, :199-201);
+        # its RescoreLimit is `rescore_limit`
+        rqc = dict(rq or {})
+        if rq is not None and int(rqc.get("bits", 8)) not in (1, 8):
+            raise WeaviateError(_lib.WV_ERR_INVALID, "rq bits must be 1 or 8")
+        comp = (_lib.COMPRESSION_BQ if bq else _lib.COMPRESSION_PQ if pq is not None
+                else (_lib.COMPRESSION_RQ8 if int(rqc.get("bits", 8)) == 8 else _lib.COMPRESSION_RQ1)
+                if rq is not None else _lib.COMPRESSION_NONE)
         cfg = _lib.WvConfig(DISTANCES[distance], int(dims), comp, int(rescore_limit), int(device),
                             VARIANTS[variant], int(id_base), self._root, int(pqc.get("segments", 0)),
                             int(pqc.get("centroids", 256)), int(pqc.get("trainingLimit", 100000)),
@@ -83,6 +90,7 @@ class FlatIndex:
         self.metric = DISTANCES[distance]
         self.bq = bool(bq)
         self.pq = pq is not None
+        self.rq = rq is not None
         self.rescore_limit = int(rescore_limit)
         self.device = device
         self.id_base = id_base
@@ -112,7 +120,31 @@ class FlatIndex:
         return PROVIDER_TYPE[self.metric]
 
     def compressed(self) -> bool:  # flat.Compressed (flat/index.go): BQ quantizer built at New; PQ once fit
-        return self.bq or (self.pq and self.pq_info()["trained"])
+        return self.bq or (self.pq and self.pq_info()["trained"]) or (self.rq and self.rq_info()["created"])
+
+    # -- rotational quantization (flat "rq-8" / "rq-1") ---------------------
+    def rq_info(self) -> dict:
+        out = np.zeros(4, np.int32)
+        check(self._l.wv_index_rq_info(self._h, _iptr(out)))
+        return {"bits": int(out[0]), "output_dim": int(out[1]), "code_bytes": int(out[2]), "created": bool(out[3])}
+
+    def rq_codes(self, n: int) -> np.ndarray:
+        """Codes of slots [0, n) in the reference formats: rq-8 uint8 [n][16 + D]
+        (RQCode), rq-1 uint64 [n][1 + D/64] (RQOneBitCode)."""
+        info = self.rq_info()
+        if info["bits"] == 8:
+            out = np.zeros((n, info["code_bytes"]), np.uint8)
+        else:
+            out = np.zeros((n, info["code_bytes"] // 8), np.uint64)
+        check(self._l.wv_index_rq_codes(self._h, out.ctypes.data, int(n)))
+        return out
+
+    def rq_distances(self, queries, n: int) -> np.ndarray:
+        """Quantized scan distances of queries [nq][d] against slots [0, n)."""
+        q = np.ascontiguousarray(np.atleast_2d(queries), dtype=np.float32)
+        out = np.zeros((q.shape[0], n), np.float32)
+        check(self._l.wv_index_rq_distances(self._h, _fptr(q), q.shape[0], q.shape[1], _fptr(out), int(n)))
+        return out
 
     def debug_candidates(self, nq: int):
         """Diagnostic: (A, E, slots, eps) of the last MFMA batch (see wv_knn.h)."""
