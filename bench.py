@@ -138,18 +138,19 @@ def cpu_baseline_pq(index, n_sample: int, nq: int, threads: int, n_full: int):
     }
 
 
-def measured_traffic(workload: str, n_local: int, dims: int, batch: int):
+def measured_traffic(workload: str, n_local: int, dims: int, batch: int, kernel: str = None):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
     (profiles/*_pmc_<workload>.json, tools/pmc_traffic.sh) when it was taken on
     this exact configuration; None otherwise."""
     import glob
     best = None
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{workload}.json"))):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{workload}*.json"))):
         try:
             rec = json.load(open(path))
         except Exception:
             continue
-        if (rec.get("corpus_rows"), rec.get("dims"), rec.get("query_batch")) == (n_local, dims, batch):
+        if (rec.get("corpus_rows"), rec.get("dims"), rec.get("query_batch")) == (n_local, dims, batch) and \
+                (kernel is None or rec.get("kernel") == kernel):
             best = rec.get("hbm_bytes_per_launch")
     return best
 
@@ -285,8 +286,10 @@ def main():
     total_q = B * args.steps
     value = total_q / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    # the fp32 path's select kernel: 256 x 256 tiles above 128 queries (runtime.hip auto choice)
+    sel_kernel = "k_mfma_select_bf3w" if B > 128 else "k_mfma_select_bf3"
     if args.traffic_bytes is None:
-        args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B)
+        args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B, None if (pq or bq) else sel_kernel)
     if pq:
         # dominant kernel k_pq_adc: one LUT lookup (LDS gather) + fp32 add per
         # (query, row, segment); the codes of a tile are shared by the group's
@@ -310,7 +313,7 @@ def main():
                 "hbm_GBps": n_local * words * 8 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
                 "traffic": args.traffic_bytes}
     else:
-        # roofline of the dominant kernel (k_mfma_select_bf3): algorithmic flops
+        # roofline of the dominant kernel (k_mfma_select_bf3w): algorithmic flops
         # per launch = 2 * B * n_local * d (one FMA per element pair), over its
         # measured average duration (HIP events on the stream it runs on).  The
         # kernel computes each fp32 product as 3 bf16 MFMA products (bf16x3
@@ -319,7 +322,7 @@ def main():
         flops = 2.0 * B * n_local * dims
         achieved = flops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
         peak = MFMA_BF16_PEAK_TFLOPS / 3.0
-        roof = {"bound": "mfma", "kernel": "k_mfma_select_bf3", "achieved": achieved, "peak": peak,
+        roof = {"bound": "mfma", "kernel": sel_kernel, "achieved": achieved, "peak": peak,
                 "unit": "TFLOP/s (fp32-product equivalent)", "frac": achieved / peak, "launch_ms": sel_avg,
                 "mfma": "v_mfma_f32_32x32x16_bf16, 3 per fp32 product (hi*hi + hi*lo + lo*hi)",
                 "executed_bf16_tflops": 3.0 * achieved, "f32_mfma_peak_equivalent_frac": achieved / MFMA_F32_PEAK_TFLOPS,

@@ -104,6 +104,7 @@ struct SelectArgs {
     const uint16_t* Qh;       // [nq_pad][dpad]
     const uint16_t* Ql;
     int dbg;                  // timing experiments only: 1 = skip selection, 2 = skip MFMA + selection
+    int opt;                  // kernel tuning bits (option sel_opt), reserved for experiments
 };
 
 template <int R>

@@ -36,6 +36,48 @@ __device__ __forceinline__ bf16x8_t lds_ld8bf(const unsigned char* p) {
     return v;
 }
 
+// Epilogue LDS traffic in inline asm: the LDS-DMA ring (global_load_lds)
+// counts as pending LDS writes for the compiler, which then puts vmcnt(0) --
+// a full drain of the ring -- before every LDS atomic/store and on every
+// __syncthreads fence.  The candidate buffer, counters and flags are never a
+// DMA target, so LDS ordering (lgkmcnt) is all these accesses need.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)((__attribute__((address_space(3))) const void*)p);
+}
+__device__ __forceinline__ int lds_add_rtn(int* p, int v) {
+    int r;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_addr(p)), "v"(v) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_st(void* p, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(p)), "v"(v) : "memory");
+}
+// workgroup barrier ordering LDS only (no vmcnt drain of the DMA ring)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// wave-uniform 8-byte read through the scalar cache (address 8-B aligned)
+__device__ __forceinline__ uint64_t sload_u64(const void* p) {
+    // p is wave-uniform but derived from threadIdx: move it to SGPRs
+    const uint64_t pi = (uint64_t)p;
+    const uint64_t up = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pi >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pi);
+    uint64_t v;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(up) : "memory");
+    return v;
+}
+
+// ds_read_b128 at LDS byte address base + OFF (immediate offset field)
+template <int OFF>
+__device__ __forceinline__ bf16x8_t lds_ld8bf_o(unsigned base) {
+    bf16x8_t v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(OFF));
+    return v;
+}
+
 template <int METRIC, int R>
 __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -50,7 +92,7 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;          // 0..7
+    const int wave = tid >> 6;  // 0..7
     const int wq = wave & 1, wx = wave >> 1;   // 2 query halves x 4 row quarters
     const int li = lane & 31, lh = lane >> 5;
 
@@ -191,8 +233,10 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                 qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
             }
             // rows 64wx + 32i + [0, 32) of the tile share one word of the valid bitmap
-            const uint32_t* vb = a.valid + (row0 >> 5);
-            const uint32_t vbw[2] = {vb[2 * wx], vb[2 * wx + 1]};
+            // scalar read: a vector load here would be retired by the
+            // compiler's vmcnt(0), which also drains the DMA ring
+            const uint64_t vb2 = sload_u64(a.valid + (row0 >> 5) + 2 * wx);
+            const uint32_t vbw[2] = {(uint32_t)vb2, (uint32_t)(vb2 >> 32)};
             // the candidate mask against the current thresholds is built
             // branch-free; a wave with no candidate skips the selection loop
             uint64_t pending = 0;
@@ -240,14 +284,14 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                             if (!((pending >> vi) & 1ull)) continue;
                             float v = acc[i][j][r];
                             if (v < th[j]) {
-                                int slot = atomicAdd(&cnt[qidx[j]], 1);
+                                int slot = lds_add_rtn(&cnt[qidx[j]], 1);
                                 if (slot < C) {
                                     int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                                    cbA[qidx[j] * C + slot] = v;
-                                    cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
+                                    lds_st(&cbA[qidx[j] * C + slot], __float_as_uint(v));
+                                    lds_st(&cbI[qidx[j] * C + slot], (uint32_t)(row0 + rt));
                                     pending &= ~(1ull << vi);
                                 } else {
-                                    flags[1] = epoch;  // overflow: merge, then retry
+                                    lds_st(&flags[1], (uint32_t)epoch);  // overflow: merge, then retry
                                 }
                             } else {
                                 pending &= ~(1ull << vi);
@@ -255,7 +299,7 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                         }
                     }
                 }
-                __syncthreads();
+                lds_barrier();
                 const bool overflow = flags[1] == epoch;
                 if (!overflow && !last_tile) break;
                 for (int jq = 0; jq < QB / 8; jq++) {
@@ -268,7 +312,7 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3(SelectArgs a) {
                                         &thr[q]);
                     if (lane == 0) cnt[q] = 0;
                 }
-                __syncthreads();
+                lds_barrier();
                 if (!overflow) break;
             }
             tile++;
@@ -304,7 +348,7 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3w(SelectArgs a) {
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;                 // 0..7
+    const int wave = tid >> 6;  // 0..7
     const int wq = wave & 1, wx = wave >> 1;   // 2 query halves (128) x 4 row quarters (64)
     const int li = lane & 31, lh = lane >> 5;
 
@@ -339,24 +383,30 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3w(SelectArgs a) {
     const int64_t tile_b = (int64_t)(a.dpad >> 4) * 8192;  // bytes per 256-row tile of a plane (bf3_plane_index)
     const int row = 32 * wave + prow;
     const int xoff = row * 32 + 16 * (pchunk ^ swz_bw(row));
-    const int64_t qoff = (int64_t)(q0 >> 8) * tile_b + xoff;  // q0 is a multiple of 256
-    const unsigned char* Xh8 = reinterpret_cast<const unsigned char*>(a.Xh);
-    const unsigned char* Xl8 = reinterpret_cast<const unsigned char*>(a.Xl);
-    const unsigned char* Qh8 = reinterpret_cast<const unsigned char*>(a.Qh);
-    const unsigned char* Ql8 = reinterpret_cast<const unsigned char*>(a.Ql);
-    int itile = t0;
-    int ikb = 0, islot = 0;
+    // the query tile's plane base is wave-uniform (q0 is a multiple of 256):
+    // the only per-lane DMA state is xoff
+    // Lean per-slice state (the scalar work between two slices' MFMAs is
+    // exposed: both waves of a SIMD reach it together after the barrier).
+    // In the tiled planes slice g of the span starts at (t0*nk + g) * 8 KiB
+    // of X and at (g mod nk) * 8 KiB of the query tile.
+    const unsigned char* Xh8 = reinterpret_cast<const unsigned char*>(a.Xh) + (int64_t)t0 * tile_b;
+    const unsigned char* Xl8 = reinterpret_cast<const unsigned char*>(a.Xl) + (int64_t)t0 * tile_b;
+    const unsigned char* Qh8 = reinterpret_cast<const unsigned char*>(a.Qh) + (int64_t)(q0 >> 8) * tile_b;
+    const unsigned char* Ql8 = reinterpret_cast<const unsigned char*>(a.Ql) + (int64_t)(q0 >> 8) * tile_b;
+    const unsigned ring_a = lds_addr(ring) + (unsigned)(32 * wave) * 32u;
+    uint32_t xg = 0, qg = 0;  // byte offsets of the next slice to issue (X, query tile)
+    int islot = 0;
+    const uint32_t qwrap = (uint32_t)nk * 8192u;
     auto issue = [&]() {
-        unsigned char* slot = ring + islot * SLOT_BW;
-        const int64_t tb = (int64_t)itile * tile_b + ikb * 8192;
-        __builtin_amdgcn_global_load_lds(Xh8 + tb + xoff, (lds_ptr_t)(slot + (32 * wave) * 32), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(Xl8 + tb + xoff, (lds_ptr_t)(slot + BN3 * 32 + (32 * wave) * 32), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(Qh8 + ikb * 8192 + qoff, (lds_ptr_t)(slot + 2 * BN3 * 32 + (32 * wave) * 32), 16,
-                                         0, 0);
-        __builtin_amdgcn_global_load_lds(Ql8 + ikb * 8192 + qoff,
-                                         (lds_ptr_t)(slot + 2 * BN3 * 32 + QBW * 32 + (32 * wave) * 32), 16, 0, 0);
-        if (++ikb == nk) { ikb = 0; itile++; }
-        if (++islot == NBUFW) islot = 0;
+        const unsigned sa = ring_a + (unsigned)islot * SLOT_BW;
+        __builtin_amdgcn_global_load_lds(Xh8 + xg + xoff, (lds_ptr_t)(size_t)sa, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(Xl8 + xg + xoff, (lds_ptr_t)(size_t)(sa + BN3 * 32), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(Qh8 + qg + xoff, (lds_ptr_t)(size_t)(sa + 2 * BN3 * 32), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(Ql8 + qg + xoff, (lds_ptr_t)(size_t)(sa + 2 * BN3 * 32 + QBW * 32), 16, 0, 0);
+        xg += 8192u;
+        qg += 8192u;
+        if (qg == qwrap) qg = 0;
+        islot = (islot + 1) & (NBUFW - 1);
     };
 
     f32x16 acc[2][4];
@@ -366,6 +416,7 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3w(SelectArgs a) {
 
     int tile = t0;
     int kb = 0, cslot = 0;
+
     for (int step = 0; step < total_steps; step++) {
         // slices step+1, step+2 may stay in flight (4 pieces each)
         if (step + 2 < total_steps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -383,29 +434,33 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3w(SelectArgs a) {
 #pragma unroll
                     for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
         }
-        // X fragments stay for the slice; Q fragments of query blocks (0,1)
-        // then (2,3) reuse the same registers (128 accumulators leave room
-        // for 32 fragment registers at 2 waves per SIMD)
-        bf16x8_t XH[2], XL[2], QH[2], QL[2];
-        if (a.dbg != 3)
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const int xr = 64 * wx + 32 * i + li;
-            const int xc = lh ^ swz_bw(xr);
-            XH[i] = lds_ld8bf(cur + xr * 32 + 16 * xc);
-            XL[i] = lds_ld8bf(cur + BN3 * 32 + xr * 32 + 16 * xc);
-        }
+        // All 12 fragment reads of the slice are issued up front: X (4) and
+        // query blocks 0-1 (4) are waited for before the first 12 MFMAs,
+        // blocks 2-3 (4) land behind them.  Row r = 32*blk + li of any block
+        // has swizzle (li >> 3) & 1, so every fragment address is one per-lane
+        // VGPR plus an immediate offset (no address registers live across the
+        // loop: spills here forced vmcnt(0) on the DMA ring).
+        const unsigned lane_off = (unsigned)(li * 32 + 16 * (lh ^ ((li >> 3) & 1)));
+        const unsigned cur_a = (unsigned)(size_t)((__attribute__((address_space(3))) const unsigned char*)cur);
+        const unsigned xa = cur_a + 2048u * wx + lane_off;
+        const unsigned qa = cur_a + 2u * BN3 * 32 + 4096u * wq + lane_off;
+        bf16x8_t XH[2], XL[2], QH[4], QL[4];
+        XH[0] = lds_ld8bf_o<0>(xa);
+        XH[1] = lds_ld8bf_o<1024>(xa);
+        XL[0] = lds_ld8bf_o<BN3 * 32>(xa);
+        XL[1] = lds_ld8bf_o<BN3 * 32 + 1024>(xa);
+        QH[0] = lds_ld8bf_o<0>(qa);
+        QH[1] = lds_ld8bf_o<1024>(qa);
+        QL[0] = lds_ld8bf_o<QBW * 32>(qa);
+        QL[1] = lds_ld8bf_o<QBW * 32 + 1024>(qa);
+        QH[2] = lds_ld8bf_o<2048>(qa);
+        QH[3] = lds_ld8bf_o<3072>(qa);
+        QL[2] = lds_ld8bf_o<QBW * 32 + 2048>(qa);
+        QL[3] = lds_ld8bf_o<QBW * 32 + 3072>(qa);
 #pragma unroll
         for (int jh = 0; jh < 2; jh++) {
-            if (a.dbg == 3) break;
-#pragma unroll
-            for (int jj = 0; jj < 2; jj++) {
-                const int qr = 128 * wq + 32 * (2 * jh + jj) + li;
-                const int qc = lh ^ swz_bw(qr);
-                QH[jj] = lds_ld8bf(cur + 2 * BN3 * 32 + qr * 32 + 16 * qc);
-                QL[jj] = lds_ld8bf(cur + 2 * BN3 * 32 + QBW * 32 + qr * 32 + 16 * qc);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (jh == 0) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             if (a.dbg == 2) continue;
 #pragma unroll
@@ -413,9 +468,9 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3w(SelectArgs a) {
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
                     const int j = 2 * jh + jj;
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XH[i], QH[jj], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XH[i], QL[jj], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XL[i], QH[jj], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XH[i], QH[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XH[i], QL[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XL[i], QH[j], acc[i][j], 0, 0, 0);
                 }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -433,33 +488,31 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3w(SelectArgs a) {
                 qidx[j] = 128 * wq + 32 * j + li;
                 qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
             }
-            const uint32_t* vb = a.valid + (row0 >> 5);
-            const uint32_t vbw[2] = {vb[2 * wx], vb[2 * wx + 1]};
-            uint64_t pending[2] = {0ull, 0ull};  // bit (i*16 + r)*4 + j over [i][r][j] (128 values)
-            {
-                float th0[4];
+            // scalar read: a vector load here would be retired by the
+            // compiler's vmcnt(0), which also drains the DMA ring
+            const uint64_t vb2 = sload_u64(a.valid + (row0 >> 5) + 2 * wx);
+            const uint32_t vbw[2] = {(uint32_t)vb2, (uint32_t)(vb2 >> 32)};
+            // No pending bitmask (its 128 single-bit constants were hoisted
+            // out of the main loop and pushed it into scratch): a value is a
+            // candidate while it is below its query's threshold, and an
+            // inserted value is set to +inf in its accumulator.  Thresholds
+            // only decrease, so this admits exactly the values the mask did.
 #pragma unroll
-                for (int j = 0; j < 4; j++) th0[j] = thr[qidx[j]];
+            for (int i = 0; i < 2; i++) {
 #pragma unroll
-                for (int i = 0; i < 2; i++) {
+                for (int r = 0; r < 16; r++) {
+                    const int rr = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const bool ok = (vbw[i] >> rr) & 1u;
+                    const float xn = (METRIC == L2) ? a.xnorm2[row0 + 64 * wx + 32 * i + rr] : 0.f;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        const int rr = (r & 3) + 8 * (r >> 2) + 4 * lh;
-                        const bool ok = (vbw[i] >> rr) & 1u;
-                        const float xn = (METRIC == L2) ? a.xnorm2[row0 + 64 * wx + 32 * i + rr] : 0.f;
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const float dot = acc[i][j][r];
-                            float v;
-                            if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
-                            else if (METRIC == DOT) v = -dot;
-                            else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
-                            const bool qok = (q0 + qidx[j]) < a.nq;
-                            v = (ok && qok) ? v : __builtin_inff();
-                            acc[i][j][r] = v;
-                            const int vi = (i * 16 + r) * 4 + j;
-                            pending[vi >> 6] |= (uint64_t)(v < th0[j]) << (vi & 63);
-                        }
+                    for (int j = 0; j < 4; j++) {
+                        const float dot = acc[i][j][r];
+                        float v;
+                        if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
+                        else if (METRIC == DOT) v = -dot;
+                        else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
+                        const bool qok = (q0 + qidx[j]) < a.nq;
+                        acc[i][j][r] = (ok && qok) ? v : __builtin_inff();
                     }
                 }
             }
@@ -469,33 +522,36 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3w(SelectArgs a) {
                 float th[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) th[j] = thr[qidx[j]];
-                if (__any((pending[0] | pending[1]) != 0))
+                bool anyc = false;
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++)
+#pragma unroll
+                        for (int j = 0; j < 4; j++) anyc |= acc[i][j][r] < th[j];
+                if (__any(anyc))
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
 #pragma unroll
                     for (int r = 0; r < 16; r++) {
 #pragma unroll
                         for (int j = 0; j < 4; j++) {
-                            const int vi = (i * 16 + r) * 4 + j;
-                            if (!((pending[vi >> 6] >> (vi & 63)) & 1ull)) continue;
                             const float v = acc[i][j][r];
                             if (v < th[j]) {
-                                const int slot = atomicAdd(&cnt[qidx[j]], 1);
+                                const int slot = lds_add_rtn(&cnt[qidx[j]], 1);
                                 if (slot < C) {
                                     const int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                                    cbA[qidx[j] * C + slot] = v;
-                                    cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
-                                    pending[vi >> 6] &= ~(1ull << (vi & 63));
+                                    lds_st(&cbA[qidx[j] * C + slot], __float_as_uint(v));
+                                    lds_st(&cbI[qidx[j] * C + slot], (uint32_t)(row0 + rt));
+                                    acc[i][j][r] = __builtin_inff();
                                 } else {
-                                    flags[1] = epoch;
+                                    lds_st(&flags[1], (uint32_t)epoch);
                                 }
-                            } else {
-                                pending[vi >> 6] &= ~(1ull << (vi & 63));
                             }
                         }
                     }
                 }
-                __syncthreads();
+                lds_barrier();
                 const bool overflow = flags[1] == epoch;
                 if (!overflow && !last_tile) break;
                 for (int jq = 0; jq < QBW / 8; jq++) {
@@ -508,7 +564,7 @@ __global__ __launch_bounds__(512, 2) void k_mfma_select_bf3w(SelectArgs a) {
                                         &thr[q]);
                     if (lane == 0) cnt[q] = 0;
                 }
-                __syncthreads();
+                lds_barrier();
                 if (!overflow) break;
             }
             tile++;

@@ -154,7 +154,7 @@ struct wv_index {
 
     DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, qh, ql, rqq, rqm;
 
-    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0, sel_dbg = 0, qgroup_opt = 0;
+    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0, sel_dbg = 0, qgroup_opt = 0, sel_opt = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     wv_stats stats{};
 };
@@ -187,7 +187,7 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     idx->root_path = cfg->root_path ? cfg->root_path : "";
     // bf16x3 select kernel for the exact fp32 path (kernels_bf3.hip)
     idx->use_bf3 = (cfg->compression == WV_COMPRESSION_NONE && cfg->metric != WV_METRIC_HAMMING) ? 1 : 0;
-    idx->kernel_opt = idx->use_bf3 ? 4 : 3;
+    idx->kernel_opt = 0;  // auto: bf16x3 256x256 (5) for batches > 128 queries, else 128x256 (4); f32 (3) without planes
     if (cfg->compression == WV_COMPRESSION_RQ8) idx->rq_bits = 8;
     if (cfg->compression == WV_COMPRESSION_RQ1) idx->rq_bits = 1;
     if (cfg->compression == WV_COMPRESSION_PQ) {
@@ -598,6 +598,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "bq_kernel") idx->bq_kernel = (int)value;
     else if (k == "sel_dbg") idx->sel_dbg = (int)value;
     else if (k == "qgroup") idx->qgroup_opt = (int)value;
+    else if (k == "sel_opt") idx->sel_opt = (int)value;
     else return set_err(WV_ERR_INVALID, "unknown option %s", key);
     return WV_OK;
 }
@@ -1688,7 +1689,9 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     int32_t* flags = o_flags ? o_flags : idx->oF.as<int32_t>();
 
     if (mfma_ok) {
-        const int kver = (idx->kernel_opt >= 4 && !idx->use_bf3) ? 3 : idx->kernel_opt;
+        int kver = idx->kernel_opt;
+        if (kver == 0) kver = idx->use_bf3 ? (nq > QB ? 5 : 4) : 3;
+        if (kver >= 4 && !idx->use_bf3) kver = 3;
         const int64_t bn = kver >= 3 ? BN3 : BN;
         const int64_t ntiles = (idx->hiwater + bn - 1) / bn;
         const int qtile = kver == 5 ? QBW : QB;
@@ -1699,8 +1702,16 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         if (idx->qgroup_opt > 0 && nqb % idx->qgroup_opt == 0) qgroup = idx->qgroup_opt;
         // ~1024 workgroups (2 per CU resident, 2 waves of them); keep the
         // workgroup count a multiple of 8 for the XCD mapping when possible
-        const int64_t target_wg = kver >= 3 ? 768 : 1024;
+        // (k_mfma_select_bf3w: one 1024-wide wave of resident workgroups, 256
+        // = one per CU, measured fastest; its 32-bit span offsets need a span
+        // below 4 GiB of one plane)
+        const int64_t target_wg = kver == 5 ? 256 : kver >= 3 ? 768 : 1024;
         int64_t nspans = idx->spans_opt > 0 ? idx->spans_opt : std::max<int64_t>(8, (target_wg + nqb - 1) / nqb);
+        if (kver == 5) {
+            const int64_t tile_bytes = (int64_t)(idx->dpad / 16) * 8192;
+            const int64_t max_tps = ((int64_t)1 << 32) / tile_bytes - 1;
+            nspans = std::max<int64_t>(nspans, (ntiles + max_tps - 1) / max_tps);
+        }
         nspans = std::min<int64_t>(nspans, ntiles);
         int64_t tps = (ntiles + nspans - 1) / nspans;
         nspans = (ntiles + tps - 1) / tps;
@@ -1716,6 +1727,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         a.outA = idx->spanA.as<float>(); a.outI = idx->spanI.as<uint32_t>();
         a.Xh = idx->Xh; a.Xl = idx->Xl; a.Qh = idx->qh.as<uint16_t>(); a.Ql = idx->ql.as<uint16_t>();
         a.dbg = idx->sel_dbg;
+        a.opt = idx->sel_opt;
         // candidate buffer: as large as fits two workgroups per CU (<= 80 KiB each)
         const bool v2 = kver == 2;
         const int64_t fixed = kver == 5 ? (int64_t)NBUFW * SLOT_BW + (int64_t)(QBW * 2 + 4) * (int64_t)sizeof(float)
