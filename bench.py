@@ -138,6 +138,31 @@ def cpu_baseline_pq(index, n_sample: int, nq: int, threads: int, n_full: int):
     }
 
 
+def cpu_baseline_rq(bits: int, n_sample: int, nq: int, threads: int, n_full: int):
+    """CPU rq-8 / rq-1 flat search (oracle/rq.c restating flat.searchByVectorQuantized
+    with the rotational quantizers) on the first n_sample rows of the same
+    corpus, one query per thread (ctypes releases the GIL)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc  # test infrastructure, used only for this baseline leg
+    from concurrent.futures import ThreadPoolExecutor
+    corpus = orc.gen_matrix(0, SEED_CORPUS, 0, n_sample, DIMS)
+    flat = orc.OracleFlatRQ(bits, orc.COSINE, orc.AVX256, DIMS, n_sample, BQ_RESCORE)
+    flat.add_batch(np.arange(n_sample, dtype=np.uint64), corpus)
+    queries = orc.gen_matrix(0, SEED_QUERY, 0, nq, DIMS)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda i: flat.search(queries[i], K), range(nq)))
+    dt = time.perf_counter() - t0
+    return {
+        "value": nq / dt * n_sample / n_full,
+        "unit": "queries/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{nq} queries x {n_sample} rows, rq-{bits} R={BQ_RESCORE} heap + fp32 rescoring, oracle C "
+                   f"restatement (oracle/rq.c), {dt:.1f} s, QPS scaled by {n_sample}/{n_full}"),
+    }
+
+
 def measured_traffic(workload: str, n_local: int, dims: int, batch: int, kernel: str = None):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
     (profiles/*_pmc_<workload>.json, tools/pmc_traffic.sh) when it was taken on
@@ -157,9 +182,10 @@ def measured_traffic(workload: str, n_local: int, dims: int, batch: int, kernel:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c3", "bq", "pq"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "bq", "pq", "rq8", "rq1"], default="c3",
                     help="c3: 10M x 768 cosine exact (default, the headline); bq: BQ 1536-d shard of configs[3]; "
-                         "pq: configs[4] PQ 10M x 960 (k-means fit timed once, ADC search timed per step)")
+                         "pq: configs[4] PQ 10M x 960 (k-means fit timed once, ADC search timed per step); "
+                         "rq8 / rq1: flat's rotational quantizers on the c3 corpus, R=200 rescoring")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -192,7 +218,8 @@ def main():
 
     bq = args.workload == "bq"
     pq = args.workload == "pq"
-    if pq and world > 1:
+    rq_bits = {"rq8": 8, "rq1": 1}.get(args.workload, 0)
+    if (pq or rq_bits) and world > 1:
         raise SystemExit(f"--workload {args.workload}: sharded search is not available yet (1 GPU)")
     dims = BQ_DIMS if bq else PQ_DIMS if pq else DIMS
     # c3 / pq: a fixed corpus split over the ranks (strong scaling); bq: configs[3]
@@ -207,7 +234,8 @@ def main():
     # ---- build the shard: generate + add in 1M-row chunks (device resident) ----
     t_build = time.perf_counter()
     index = wv.FlatIndex(distance="l2-squared" if pq else "cosine", dims=dims, device=local_rank, variant="avx256", id_base=id0,
-                         bq=bq, rescore_limit=BQ_RESCORE if bq else -1,
+                         bq=bq, rescore_limit=BQ_RESCORE if (bq or rq_bits) else -1,
+                         rq={"bits": rq_bits} if rq_bits else None,
                          pq={"segments": PQ_SEGMENTS, "centroids": PQ_CENTROIDS, "trainingLimit": PQ_TRAIN,
                              "rescore": False} if pq else None)
     index.reserve(n_local)
@@ -289,8 +317,27 @@ def main():
     # the fp32 path's select kernel: 256 x 256 tiles above 128 queries (runtime.hip auto choice)
     sel_kernel = "k_mfma_select_bf3w" if B > 128 else "k_mfma_select_bf3"
     if args.traffic_bytes is None:
-        args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B, None if (pq or bq) else sel_kernel)
-    if pq:
+        args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B,
+                                              None if (pq or bq or rq_bits) else sel_kernel)
+    if rq_bits:
+        # dominant kernel k_rq8_dist / k_rq1_dist, timed on the first query
+        # group of the batch (search_rq: groups of RQ_QPB multiples whose
+        # distance rows fit 4 GiB).  rq-8: one v_dot4_u32_u8 per 4 code bytes
+        # and (query, row); rq-1: per 64-bit word and (query, row) 5 bit planes
+        # x (2 v_xor_b32 + 2 v_bcnt_u32_b32).  The kernel also writes the
+        # 4-byte quantized distance of every (query, row) pair.
+        D = (dims + 63) // 64 * 64
+        ld = max((n_local + 255) // 256 * 256, 256)
+        f0 = int(index.stats().get("last_group_queries", 0)) or min(B, max(32, ((4 << 30) // (ld * 4)) // 32 * 32))
+        ops = float(f0) * n_local * (D / 4 if rq_bits == 8 else (D / 64) * 5 * 4)
+        achieved = ops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
+        kname = "k_rq8_dist" if rq_bits == 8 else "k_rq1_dist"
+        roof = {"bound": "valu", "kernel": kname, "achieved": achieved, "peak": VALU_PEAK_TOPS,
+                "unit": "Tops/s (int32 lane-ops)", "frac": achieved / VALU_PEAK_TOPS, "launch_ms": sel_avg,
+                "note": f"launch_ms = first query group ({f0} queries) of the batch",
+                "hbm_write_GBps": f0 * ld * 4 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
+                "traffic": args.traffic_bytes}
+    elif pq:
         # dominant kernel k_pq_adc: one LUT lookup (LDS gather) + fp32 add per
         # (query, row, segment); the codes of a tile are shared by the group's
         # queries through L2
@@ -333,7 +380,10 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                if pq:
+                if rq_bits:
+                    cpu = cpu_baseline_rq(rq_bits, min(args.cpu_rows, 200_000), args.cpu_queries or 512,
+                                          args.cpu_threads, n_total)
+                elif pq:
                     cpu = cpu_baseline_pq(index, min(args.cpu_rows, n_total), args.cpu_queries or 256,
                                           args.cpu_threads, n_total)
                 elif bq:
@@ -343,7 +393,10 @@ def main():
                     cpu = cpu_baseline(min(args.cpu_rows, n_total), args.cpu_queries or 1024, args.cpu_threads)
             except Exception as e:  # baseline failure must not hide the GPU number
                 log(f"cpu baseline failed: {e}")
-        if pq:
+        if rq_bits:
+            workload = (f"rq-{rq_bits} (flat rotational quantization) {dims}-d cosine, k={K}, rescore R={BQ_RESCORE}, "
+                        f"on the BASELINE configs[2] corpus ({n_total} rows)")
+        elif pq:
             workload = (f"PQ {dims}-d l2-squared, m={PQ_SEGMENTS} x ks={PQ_CENTROIDS} trained on {PQ_TRAIN} rows "
                         f"(fit {fit_s:.2f} s), ADC flat search k={K} (BASELINE configs[4])")
         elif bq:
@@ -362,7 +415,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if bq else "strong",
             "vs_baseline": None,
-            "dtype": "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else "f32",
+            "dtype": ("u8 codes (v_dot4) + f32 rescoring" if rq_bits == 8 else
+                      "u64 codes x 5-bit query planes + f32 rescoring" if rq_bits == 1 else
+                      "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else "f32"),
             "data": "synthetic (counter-based U[-1,1) generator, seed 1 corpus / 2 queries)",
             "config": {
                 "workload": workload,

@@ -230,6 +230,7 @@ typedef struct wv_stats {
     uint64_t mfma_launches;
     double last_select_ms;   /* k_mfma_select time of the last batch (HIP events) */
     double last_total_ms;
+    uint64_t last_group_queries; /* queries in the timed (first) group of the last quantized batch */
 } wv_stats;
 int wv_index_stats(wv_index *idx, wv_stats *out);
 

@@ -60,6 +60,7 @@ class WvStats(C.Structure):
         ("mfma_launches", C.c_uint64),
         ("last_select_ms", C.c_double),
         ("last_total_ms", C.c_double),
+        ("last_group_queries", C.c_uint64),
     ]
 
 

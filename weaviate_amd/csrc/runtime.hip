@@ -156,6 +156,11 @@ struct wv_index {
 
     int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0, sel_dbg = 0, qgroup_opt = 0, sel_opt = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // replay stream: the quantized searches' one-wave-per-query heap replays
+    // run there, beside the next query group's full-GPU distance kernel
+    hipStream_t aux = nullptr;
+    hipEvent_t evd[2] = {nullptr, nullptr}, evr[2] = {nullptr, nullptr};
+    DBuf rE2, rB2;
     wv_stats stats{};
 };
 
@@ -217,8 +222,13 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
-                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm})
+                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm,
+                    &idx->rE2, &idx->rB2})
         b->release();
+    if (idx->aux) hipStreamSynchronize(idx->aux);
+    for (hipEvent_t e : {idx->evd[0], idx->evd[1], idx->evr[0], idx->evr[1]})
+        if (e) hipEventDestroy(e);
+    if (idx->aux) hipStreamDestroy(idx->aux);
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
     if (idx->present) hipFree(idx->present);
@@ -1485,6 +1495,19 @@ static int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t 
 // order (k_replay_scan, extracted ascending = reversed pop order), fp32
 // rescoring of the candidates (k_rescore_ids) and the k-heap fed in pop order
 // (k_bq_final with asc = 1).
+// bytes already held by the first distance buffer (counted as available
+// when sizing the groups: ensure() reuses it)
+static size_t Eb0_bytes(const wv_index* idx) { return idx->rE.bytes; }
+
+// replay stream + events (created at the first quantized search that uses them)
+static int ensure_aux(wv_index* idx) {
+    if (idx->aux) return WV_OK;
+    HIPCHK(hipStreamCreateWithFlags(&idx->aux, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&idx->evd[0], &idx->evd[1], &idx->evr[0], &idx->evr[1]})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return WV_OK;
+}
+
 static int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
                      const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
     if (qd != idx->dims)  // SingleDist of the rescoring (distancer/errors.go:16)
@@ -1510,11 +1533,27 @@ static int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     const int32_t* qlist = idx->ident.as<int32_t>();
     const int64_t nslots = idx->hiwater;
     const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
-    // query groups: multiples of RQ_QPB, distance buffer bounded to 4 GiB
-    int64_t G = ((4ll << 30) / (ld * 4)) / RQ_QPB * RQ_QPB;
+    // query groups: multiples of RQ_QPB, two distance buffers of up to
+    // 16 GiB each (a quarter of the free HBM at most).  A replay wave's time
+    // does not shrink with the group (one wave per query), so groups are as
+    // large as memory allows.  Group i's distances (whole GPU, stream s)
+    // overlap group i-1's replay (stream aux); buffer i&1 is reused once
+    // replay i-2 has finished with it.
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const int64_t have = (int64_t)(Eb0_bytes(idx) + free_b / 4);
+    const int64_t budget = std::max<int64_t>(std::min<int64_t>(16ll << 30, have), 1ll << 30);
+    int64_t G = (budget / (ld * 4)) / RQ_QPB * RQ_QPB;
     G = std::max<int64_t>(RQ_QPB, std::min<int64_t>(G, round_up(nq, RQ_QPB)));
-    HIPCHK(idx->rE.ensure((size_t)G * ld * sizeof(float)));
-    HIPCHK(idx->rB.ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+    idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(G, nq);
+    rc = ensure_aux(idx);
+    if (rc) return rc;
+    DBuf* Eb[2] = {&idx->rE, &idx->rE2};
+    DBuf* Bb[2] = {&idx->rB, &idx->rB2};
+    for (int b = 0; b < 2; b++) {
+        HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
+        HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+    }
     HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
     HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
     HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
@@ -1522,18 +1561,26 @@ static int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     const size_t lds_rep = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
     if (lds_rep > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rep));
-    for (int64_t g0 = 0; g0 < nq; g0 += G) {
+    int64_t gi = 0;
+    for (int64_t g0 = 0; g0 < nq; g0 += G, gi++) {
         const int F = (int)std::min<int64_t>(G, nq - g0);
+        const int b = (int)(gi & 1);
+        if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
-        rc = rq_dist(idx, s, valid, g0, F, ld, idx->rE.as<float>(), idx->rB.as<float>());
+        rc = rq_dist(idx, s, valid, g0, F, ld, Eb[b]->as<float>(), Bb[b]->as<float>());
         if (rc) return rc;
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
-        k_replay_scan<<<F, 64, lds_rep, s>>>(idx->rE.as<float>(), idx->rB.as<float>(), valid, nslots, ld, qlist + g0, F,
-                                             R, idx->id_base, nullptr, nullptr, nullptr, 1, 0, R,
-                                             idx->ascI.as<uint64_t>() + g0 * R, idx->ascD.as<float>() + g0 * R,
-                                             idx->ascN.as<int32_t>() + g0);
+        HIPCHK(hipEventRecord(idx->evd[b], s));
+        HIPCHK(hipStreamWaitEvent(idx->aux, idx->evd[b], 0));
+        k_replay_scan<<<F, 64, lds_rep, idx->aux>>>(Eb[b]->as<float>(), Bb[b]->as<float>(), valid, nslots, ld,
+                                                    qlist + g0, F, R, idx->id_base, nullptr, nullptr, nullptr, 1, 0,
+                                                    R, idx->ascI.as<uint64_t>() + g0 * R,
+                                                    idx->ascD.as<float>() + g0 * R, idx->ascN.as<int32_t>() + g0);
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
     }
+    // join: the rescoring on s reads every group's heap
+    for (int b = 0; b < 2 && b < gi; b++) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
     idx->bq_nq = nq;
     idx->bq_R = R;
     rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
