@@ -342,7 +342,7 @@ def main():
         # (query, row, segment); the codes of a tile are shared by the group's
         # queries through L2
         ld = (n_local + 255) // 256 * 256
-        f0 = max(1, min(B, (2 << 30) // (ld * 4)))  # queries in the timed first group (search_pq grouping)
+        f0 = int(index.stats().get("last_group_queries", 0)) or max(1, min(B, (2 << 30) // (ld * 4)))  # timed first group
         lookups = float(f0) * n_local * PQ_SEGMENTS
         achieved = lookups / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
         roof = {"bound": "lds", "kernel": "k_pq_adc", "achieved": achieved, "peak": LDS_LOOKUP_PEAK_T,

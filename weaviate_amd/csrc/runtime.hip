@@ -1305,6 +1305,19 @@ extern "C" int wv_index_pq_distance(wv_index* idx, const float* query, int64_t d
 // hnsw.flatSearch over the PQ codes (flat_search.go:28-141, one worker) with
 // optional h.rescore (search.go:1047-1110, one worker).  limit = rescore ?
 // max(rescore_limit, k) : k.  Outputs [nq][k].
+// bytes already held by the first distance buffer (counted as available
+// when sizing the groups: ensure() reuses it)
+static size_t Eb0_bytes(const wv_index* idx) { return idx->rE.bytes; }
+
+// replay stream + events (created at the first quantized search that uses them)
+static int ensure_aux(wv_index* idx) {
+    if (idx->aux) return WV_OK;
+    HIPCHK(hipStreamCreateWithFlags(&idx->aux, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&idx->evd[0], &idx->evd[1], &idx->evr[0], &idx->evr[1]})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return WV_OK;
+}
+
 static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
                      const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
     if (qd != idx->dims)
@@ -1334,9 +1347,22 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     const int32_t* qlist = idx->ident.as<int32_t>();
     const int64_t nslots = idx->hiwater;
     const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
-    const int64_t G = std::max<int64_t>(1, std::min<int64_t>(nq, (2ll << 30) / (ld * 4)));
-    HIPCHK(idx->rE.ensure((size_t)G * ld * sizeof(float)));
-    HIPCHK(idx->rB.ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+    // groups sized to the free HBM, replay on the aux stream beside the next
+    // group's ADC kernel (as search_rq)
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const int64_t have = (int64_t)(Eb0_bytes(idx) + free_b / 4);
+    const int64_t budget = std::max<int64_t>(std::min<int64_t>(16ll << 30, have), 1ll << 30);
+    const int64_t G = std::max<int64_t>(1, std::min<int64_t>(nq, budget / (ld * 4)));
+    idx->stats.last_group_queries = (uint64_t)G;
+    rc = ensure_aux(idx);
+    if (rc) return rc;
+    DBuf* Eb[2] = {&idx->rE, &idx->rE2};
+    DBuf* Bb[2] = {&idx->rB, &idx->rB2};
+    for (int b = 0; b < 2; b++) {
+        HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
+        HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+    }
     HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
     HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
     HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
@@ -1345,25 +1371,33 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     const size_t lds_rep = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
     if (lds_rep > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rep));
-    for (int64_t g0 = 0; g0 < nq; g0 += G) {
+    int64_t gi = 0;
+    for (int64_t g0 = 0; g0 < nq; g0 += G, gi++) {
         const int F = (int)std::min<int64_t>(G, nq - g0);
+        const int b = (int)(gi & 1);
+        float* E = Eb[b]->as<float>();
+        float* Bm = Bb[b]->as<float>();
+        if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
         dim3 grid((unsigned)F, (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
         if (K == 256)
             k_pq_adc<256><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots, idx->lut.as<float>(),
-                                                     qlist + g0, wrapm, ld, idx->rE.as<float>(), idx->rB.as<float>());
+                                                     qlist + g0, wrapm, ld, E, Bm);
         else
             k_pq_adc<0><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots, idx->lut.as<float>(),
-                                                   qlist + g0, wrapm, ld, idx->rE.as<float>(), idx->rB.as<float>());
+                                                   qlist + g0, wrapm, ld, E, Bm);
         HIPCHK(hipGetLastError());
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
+        HIPCHK(hipEventRecord(idx->evd[b], s));
+        HIPCHK(hipStreamWaitEvent(idx->aux, idx->evd[b], 0));
         // the worker heap (addResult == insertToHeap) in id order, extracted ascending
-        k_replay_scan<<<F, 64, lds_rep, s>>>(idx->rE.as<float>(), idx->rB.as<float>(), valid, nslots, ld, qlist + g0, F,
-                                             R, idx->id_base, nullptr, nullptr, nullptr, 1, 0, R,
-                                             idx->ascI.as<uint64_t>() + g0 * R, idx->ascD.as<float>() + g0 * R,
-                                             idx->ascN.as<int32_t>() + g0);
+        k_replay_scan<<<F, 64, lds_rep, idx->aux>>>(E, Bm, valid, nslots, ld, qlist + g0, F, R, idx->id_base, nullptr,
+                                                    nullptr, nullptr, 1, 0, R, idx->ascI.as<uint64_t>() + g0 * R,
+                                                    idx->ascD.as<float>() + g0 * R, idx->ascN.as<int32_t>() + g0);
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
     }
+    for (int b = 0; b < 2 && b < gi; b++) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
     HIPCHK(idx->cslot.ensure((size_t)nq * R * sizeof(uint32_t)));
     HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
     const size_t lds_f = (size_t)R * (sizeof(uint64_t) + sizeof(float)) + 16;
@@ -1495,19 +1529,6 @@ static int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t 
 // order (k_replay_scan, extracted ascending = reversed pop order), fp32
 // rescoring of the candidates (k_rescore_ids) and the k-heap fed in pop order
 // (k_bq_final with asc = 1).
-// bytes already held by the first distance buffer (counted as available
-// when sizing the groups: ensure() reuses it)
-static size_t Eb0_bytes(const wv_index* idx) { return idx->rE.bytes; }
-
-// replay stream + events (created at the first quantized search that uses them)
-static int ensure_aux(wv_index* idx) {
-    if (idx->aux) return WV_OK;
-    HIPCHK(hipStreamCreateWithFlags(&idx->aux, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&idx->evd[0], &idx->evd[1], &idx->evr[0], &idx->evr[1]})
-        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    return WV_OK;
-}
-
 static int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
                      const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
     if (qd != idx->dims)  // SingleDist of the rescoring (distancer/errors.go:16)
