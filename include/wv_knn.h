@@ -247,6 +247,36 @@ int wv_index_debug_candidates(wv_index *idx, float *A, float *E, uint32_t *I, fl
  * "timing" (1 = record kernel times with HIP events) */
 int wv_index_set_option(wv_index *idx, const char *key, int64_t value);
 
+/* ---- LSM on-disk format: restore from flat's vectors bucket ----------------
+ * Host-only (no GPU call).  Replace-strategy segment files as written by
+ * lsmkv (segmentindex/header.go:24-42, segment_serialization.go:34-166,
+ * segmentindex/segment_file.go:274-341 for the v1 CRC32 trailer).
+ * validate_checksum != 0 checks the trailer of version >= 1 segments
+ * (the bucket option enableChecksumValidation, segment.go:262-272). */
+
+/* out[6] = level, version, secondary index count, strategy, indexStart, file size */
+int wv_lsm_segment_header(const char *path, int32_t validate_checksum, int64_t *out);
+
+/* Walk the data region [16, indexStart) node by node (ParseReplaceNode).
+ * Fills up to cap entries (any array may be NULL): node [start, end) offsets,
+ * tombstone flag, key as a big-endian uint64 when the key is 8 bytes (else
+ * UINT64_MAX).  *out_n = number of nodes.  Non-replace strategy -> error
+ * "unsupported strategy in segment: ...". */
+int wv_lsm_segment_scan(const char *path, int32_t validate_checksum, int64_t *node_start, int64_t *node_end,
+                        uint8_t *tombstone, uint64_t *key_id, int64_t cap, int64_t *out_n);
+
+/* Replaces the startup path of flat.New → initBuckets → PostStartup
+ * (flat/index.go:236-282, 867-1033): segments of the vectors bucket, oldest
+ * first; key = big-endian uint64 id, value = d little-endian float32
+ * (flat/index.go:204-208, 317-336).  Newest entry per key wins, tombstones
+ * delete.  Live vectors are normalised/encoded and uploaded exactly as by
+ * wv_index_add_batch (compressed codes are re-derived from the fp32 values,
+ * which the BQ/RQ encoders determine uniquely).  out[3] (may be NULL) = live
+ * vectors uploaded, tombstoned keys, nodes read.  AlreadyIndexed becomes the
+ * live count (flat/index.go:278-279). */
+int wv_index_load_segments(wv_index *idx, const char *const *paths, int32_t n_paths, int32_t validate_checksum,
+                           int64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

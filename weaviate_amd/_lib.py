@@ -111,6 +111,10 @@ SIGNATURES = {
     "wv_index_rq_codes": (C.c_int, [P, P, i64]),
     "wv_index_rq_distances": (C.c_int, [P, pf32, i64, i64, pf32, i64]),
     "wv_index_set_option": (C.c_int, [P, C.c_char_p, i64]),
+    "wv_lsm_segment_header": (C.c_int, [C.c_char_p, i32, C.POINTER(C.c_int64)]),
+    "wv_lsm_segment_scan": (C.c_int, [C.c_char_p, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                      C.POINTER(C.c_uint8), pu64, i64, C.POINTER(C.c_int64)]),
+    "wv_index_load_segments": (C.c_int, [P, C.POINTER(C.c_char_p), i32, i32, C.POINTER(C.c_int64)]),
 }
 
 _lib = None

@@ -9,6 +9,7 @@
 //   xnorm2  [cap]              sum of squares per stored row (approx. L2 path)
 //   present [cap/32] u32       bitmap of slots holding a vector (LSM key exists)
 // cap is a multiple of 128 (the MFMA tile) so tiles never read out of bounds.
+#include <cerrno>
 #include <cpuid.h>
 #include <stdarg.h>
 
@@ -2195,3 +2196,6 @@ extern "C" int wv_gen_device(int32_t device, int32_t kind, uint64_t seed, uint64
     if (!stream) HIPCHK(hipStreamSynchronize(nullptr));
     return WV_OK;
 }
+
+// LSM segment restore (host-only; uses add_rows_locked / wv_index_delete above)
+#include "lsm_segment.hip"

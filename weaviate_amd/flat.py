@@ -230,6 +230,15 @@ class FlatIndex:
         a = np.ascontiguousarray(ids, dtype=np.uint64)
         check(self._l.wv_index_delete(self._h, _uptr(a), a.size))
 
+    def load_segments(self, paths: Sequence[str], validate_checksum: bool = True) -> dict:
+        """Restore from the vectors bucket's LSM segments, oldest first
+        (initBuckets + PostStartup, flat/index.go:236-282, 867-1033); see
+        wv_index_load_segments in include/wv_knn.h."""
+        arr = (C.c_char_p * max(len(paths), 1))(*[str(p).encode() for p in paths])
+        out = (C.c_int64 * 3)()
+        check(self._l.wv_index_load_segments(self._h, arr, len(paths), int(bool(validate_checksum)), out))
+        return {"loaded": out[0], "tombstoned": out[1], "nodes": out[2]}
+
     def contains_doc(self, id: int) -> bool:  # flat/index.go:1035-1055
         return bool(self._l.wv_index_contains_doc(self._h, int(id)))
 
@@ -331,3 +340,28 @@ def normalize_batch(vecs, device: int = 0) -> np.ndarray:
     out = np.zeros_like(v)
     check(lib.wv_normalize_batch(device, _fptr(v), v.shape[0], v.shape[1], _fptr(out)))
     return out
+
+
+def lsm_segment_header(path: str, validate_checksum: bool = True) -> dict:
+    """segmentindex.ParseHeader (+ ValidateChecksum for v1) of one segment file."""
+    out = (C.c_int64 * 6)()
+    check(_lib.load().wv_lsm_segment_header(str(path).encode(), int(bool(validate_checksum)), out))
+    return dict(zip(("level", "version", "secondary_indices", "strategy", "index_start", "size"), list(out)))
+
+
+def lsm_segment_scan(path: str, validate_checksum: bool = True) -> dict:
+    """Walk a replace-strategy segment's nodes (ParseReplaceNode,
+    lsmkv/segment_serialization.go:106-166): offsets, tombstones, BE uint64 keys."""
+    lib = _lib.load()
+    n = C.c_int64(0)
+    bpath = str(path).encode()
+    check(lib.wv_lsm_segment_scan(bpath, int(bool(validate_checksum)), None, None, None, None, 0, C.byref(n)))
+    m = n.value
+    start = np.zeros(m, np.int64)
+    end = np.zeros(m, np.int64)
+    tomb = np.zeros(m, np.uint8)
+    keys = np.zeros(m, np.uint64)
+    check(lib.wv_lsm_segment_scan(bpath, int(bool(validate_checksum)),
+                                  start.ctypes.data_as(C.POINTER(C.c_int64)), end.ctypes.data_as(C.POINTER(C.c_int64)),
+                                  tomb.ctypes.data_as(C.POINTER(C.c_uint8)), _uptr(keys), m, C.byref(n)))
+    return {"start": start, "end": end, "tombstone": tomb.astype(bool), "key_id": keys}
