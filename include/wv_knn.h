@@ -114,6 +114,21 @@ int wv_index_search_by_vector_batch(wv_index *idx, const float *queries, int64_t
                                     const uint64_t *allow_ids, int64_t n_allow, int32_t allow_mode,
                                     uint64_t *out_ids, float *out_dists, int32_t *out_counts);
 
+/* flat.SearchByVector for ONE query (flat/index.go:423-448), the call a
+ * goroutine makes (shard_read.go:415-424).  Thread-safe; concurrent callers on
+ * one index are coalesced into batched launches (micro-batcher, batcher.hip):
+ * a caller that finds no batch running leads the next one, waiting up to the
+ * "batch_window_us" option (default 0) for company, at most "batch_max"
+ * (default 4096) queries per launch; requests with an allow list, or another
+ * d or k, run as their own group.  Results and errors equal those of a
+ * one-query wv_index_search_by_vector_batch.  out_ids/out_dists capacity k. */
+int wv_index_search_by_vector(wv_index *idx, const float *query, int64_t d, int32_t k, const uint64_t *allow_ids,
+                              int64_t n_allow, int32_t allow_mode, uint64_t *out_ids, float *out_dists,
+                              int32_t *out_count);
+
+/* out[3] = single-query calls, batched launches, largest batch so far */
+int wv_index_batcher_stats(wv_index *idx, int64_t *out);
+
 /* flat.SearchByVectorDistance (flat/index.go:699-761); out_* capacity >= 100 */
 int wv_index_search_by_vector_distance(wv_index *idx, const float *query, int64_t d, float target_distance,
                                        int64_t max_limit, const uint64_t *allow_ids, int64_t n_allow,
@@ -244,7 +259,8 @@ int wv_index_debug_candidates(wv_index *idx, float *A, float *E, uint32_t *I, fl
  * "force_replay" (1 = resolve every query by heap replay), "spans" (0 = auto),
  * "kernel" (select kernel: 4 = bf16x3 MFMA (default for the exact fp32 path),
  * 3 = f32 MFMA ring, 2/1 older f32 forms), "bq_kernel" (1 = generic BQ kernels),
- * "timing" (1 = record kernel times with HIP events) */
+ * "timing" (1 = record kernel times with HIP events), "batch_window_us" /
+ * "batch_max" (micro-batcher, see wv_index_search_by_vector) */
 int wv_index_set_option(wv_index *idx, const char *key, int64_t value);
 
 /* ---- LSM on-disk format: restore from flat's vectors bucket ----------------

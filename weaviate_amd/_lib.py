@@ -114,6 +114,8 @@ SIGNATURES = {
     "wv_lsm_segment_header": (C.c_int, [C.c_char_p, i32, C.POINTER(C.c_int64)]),
     "wv_lsm_segment_scan": (C.c_int, [C.c_char_p, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                       C.POINTER(C.c_uint8), pu64, i64, C.POINTER(C.c_int64)]),
+    "wv_index_search_by_vector": (C.c_int, [P, pf32, i64, i32, pu64, i64, i32, pu64, pf32, pi32]),
+    "wv_index_batcher_stats": (C.c_int, [P, C.POINTER(C.c_int64)]),
     "wv_index_load_segments": (C.c_int, [P, C.POINTER(C.c_char_p), i32, i32, C.POINTER(C.c_int64)]),
 }
 

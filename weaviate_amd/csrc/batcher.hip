@@ -1,0 +1,142 @@
+// Micro-batcher for concurrent single-query searches (host only, included by
+// runtime.hip).
+//
+// Weaviate calls SearchByVector once per query from many goroutines at once
+// (shard_read.go:415-424, flat/index.go:423-448).  One fp32 query alone
+// streams the whole corpus (HBM-bound, SURVEY §8d C3: 3.84 ms at 10M x 768),
+// while a batch of B queries costs the same HBM pass plus MFMA work.  So
+// concurrent callers are coalesced: leader/follower, no background thread.
+// A caller enqueues its request; if no batch is running it becomes the
+// leader, optionally waits batch_window_us for company, takes every pending
+// request, groups them by (d, k) (one allow list = its own group, since the
+// batch entry point takes one allow list), runs each group through
+// wv_index_search_by_vector_batch and hands every follower its rows.  Requests
+// that arrive while a batch runs form the next batch.  Results are identical
+// to individual calls: each query of a batch is searched independently.
+#include <chrono>
+#include <condition_variable>
+
+struct wv_batch_req {
+    const float* q;
+    int64_t d;
+    int32_t k;
+    const uint64_t* allow_ids;
+    int64_t n_allow;
+    int32_t allow_mode;
+    uint64_t* out_ids;
+    float* out_dists;
+    int32_t* out_count;
+    int rc = WV_OK;
+    std::string err;
+    bool done = false;
+};
+
+struct wv_batcher {
+    std::mutex m;
+    std::condition_variable cv;         // followers: their batch is done / leader slot free
+    std::condition_variable cv_window;  // the leader waiting out batch_window_us
+    std::vector<wv_batch_req*> pending;
+    bool busy = false, in_window = false;
+    int64_t calls = 0, launches = 0, max_batch_seen = 0;
+};
+
+static void batcher_free(wv_batcher* b) { delete b; }
+
+static wv_batcher* get_batcher(wv_index* idx) {
+    static std::mutex create_mu;
+    std::lock_guard<std::mutex> g(create_mu);
+    if (!idx->batcher) idx->batcher = new wv_batcher();
+    return idx->batcher;
+}
+
+// Runs one group of requests sharing (d, k, allow) as one batch call.
+static void run_group(wv_index* idx, std::vector<wv_batch_req*>& grp) {
+    const int64_t n = (int64_t)grp.size();
+    const int64_t d = grp[0]->d;
+    const int32_t k = grp[0]->k;
+    std::vector<float> q((size_t)(n * std::max<int64_t>(d, 0)));
+    for (int64_t i = 0; i < n; i++) memcpy(&q[(size_t)(i * d)], grp[i]->q, (size_t)d * sizeof(float));
+    const int32_t kk = std::max(k, 0);
+    std::vector<uint64_t> ids((size_t)(n * kk) + 1);
+    std::vector<float> dists((size_t)(n * kk) + 1);
+    std::vector<int32_t> cnt((size_t)n);
+    int rc = wv_index_search_by_vector_batch(idx, q.data(), n, d, k, grp[0]->allow_ids, grp[0]->n_allow,
+                                             grp[0]->allow_mode, ids.data(), dists.data(), cnt.data());
+    std::string err = rc ? std::string(wv_last_error()) : std::string();
+    for (int64_t i = 0; i < n; i++) {
+        wv_batch_req* r = grp[i];
+        r->rc = rc;
+        if (rc) { r->err = err; continue; }
+        *r->out_count = cnt[i];
+        memcpy(r->out_ids, &ids[(size_t)(i * kk)], (size_t)cnt[i] * sizeof(uint64_t));
+        memcpy(r->out_dists, &dists[(size_t)(i * kk)], (size_t)cnt[i] * sizeof(float));
+    }
+}
+
+static void run_batch(wv_index* idx, std::vector<wv_batch_req*>& batch) {
+    // group by (d, k) for allow-free requests; allow-list requests alone
+    std::vector<std::vector<wv_batch_req*>> groups;
+    for (wv_batch_req* r : batch) {
+        bool placed = false;
+        if (r->allow_mode == 0) {
+            for (auto& g : groups)
+                if (g[0]->allow_mode == 0 && g[0]->d == r->d && g[0]->k == r->k) { g.push_back(r); placed = true; break; }
+        }
+        if (!placed) groups.push_back({r});
+    }
+    for (auto& g : groups) run_group(idx, g);
+}
+
+extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int64_t d, int32_t k,
+                                         const uint64_t* allow_ids, int64_t n_allow, int32_t allow_mode,
+                                         uint64_t* out_ids, float* out_dists, int32_t* out_count) {
+    if (!idx || !out_count) return set_err(WV_ERR_INVALID, "nil argument");
+    if (d > 0 && !query) return set_err(WV_ERR_INVALID, "nil query");
+    wv_batcher* b = get_batcher(idx);
+    wv_batch_req req{query, d, k, allow_ids, n_allow, allow_mode, out_ids, out_dists, out_count};
+    std::unique_lock<std::mutex> lk(b->m);
+    b->calls++;
+    b->pending.push_back(&req);
+    // only a leader inside its batch window wants to hear about arrivals (waking
+    // every waiting follower per arrival would cost O(callers^2) wakeups)
+    if (b->in_window) b->cv_window.notify_one();
+    while (!req.done) {
+        if (!b->busy) {
+            // become the leader for the next batch
+            b->busy = true;
+            const int64_t window = idx->batch_window_us;
+            if (window > 0 && (int64_t)b->pending.size() < idx->batch_max) {
+                b->in_window = true;
+                b->cv_window.wait_for(lk, std::chrono::microseconds(window),
+                                      [&] { return (int64_t)b->pending.size() >= idx->batch_max; });
+                b->in_window = false;
+            }
+            std::vector<wv_batch_req*> batch;
+            const size_t take = std::min(b->pending.size(), (size_t)std::max<int64_t>(idx->batch_max, 1));
+            batch.assign(b->pending.begin(), b->pending.begin() + take);
+            b->pending.erase(b->pending.begin(), b->pending.begin() + take);
+            b->launches++;
+            b->max_batch_seen = std::max<int64_t>(b->max_batch_seen, (int64_t)batch.size());
+            lk.unlock();
+            run_batch(idx, batch);
+            lk.lock();
+            for (wv_batch_req* r : batch) r->done = true;
+            b->busy = false;
+            b->cv.notify_all();
+        } else {
+            b->cv.wait(lk);
+        }
+    }
+    if (req.rc) return set_err(req.rc, "%s", req.err.c_str());
+    return WV_OK;
+}
+
+extern "C" int wv_index_batcher_stats(wv_index* idx, int64_t* out) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    wv_batcher* b = get_batcher(idx);
+    std::lock_guard<std::mutex> g(b->m);
+    out[0] = b->calls;
+    out[1] = b->launches;
+    out[2] = b->max_batch_seen;
+    return WV_OK;
+}

@@ -106,6 +106,9 @@ static inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * 
 static inline int64_t pq_mwp(int m) { return (int64_t)((m + 15) / 16) * 4; }
 static inline int pq_g16(int m) { return (m + 15) / 16; }
 
+struct wv_batcher;
+static void batcher_free(wv_batcher* b);
+
 struct wv_index {
     std::mutex mu;
     int metric = WV_METRIC_COSINE_DOT;
@@ -163,6 +166,9 @@ struct wv_index {
     hipEvent_t evd[2] = {nullptr, nullptr}, evr[2] = {nullptr, nullptr};
     DBuf rE2, rB2;
     wv_stats stats{};
+    // micro-batcher of concurrent single-query searches (batcher.hip)
+    wv_batcher* batcher = nullptr;
+    int64_t batch_window_us = 0, batch_max = 4096;
 };
 
 // ---------------------------------------------------------------------------
@@ -218,6 +224,7 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
 
 extern "C" void wv_index_destroy(wv_index* idx) {
     if (!idx) return;
+    batcher_free(idx->batcher);
     hipSetDevice(idx->device);
     if (idx->stream) hipStreamSynchronize(idx->stream);
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
@@ -600,6 +607,8 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     if (!idx || !key) return set_err(WV_ERR_INVALID, "nil argument");
     std::lock_guard<std::mutex> g(idx->mu);
     std::string k(key);
+    if (k == "batch_window_us") { if (value < 0 || value > 1000000) return set_err(WV_ERR_INVALID, "batch_window_us out of range"); idx->batch_window_us = value; return WV_OK; }
+    if (k == "batch_max") { if (value < 1) return set_err(WV_ERR_INVALID, "batch_max out of range"); idx->batch_max = value; return WV_OK; }
     if (k == "margin") { if (value < 2 || value > 30) return set_err(WV_ERR_INVALID, "margin out of range"); idx->margin = (int)value; }
     else if (k == "force_replay") idx->force_replay = (int)value;
     else if (k == "spans") idx->spans_opt = (int)value;
@@ -2199,3 +2208,6 @@ extern "C" int wv_gen_device(int32_t device, int32_t kind, uint64_t seed, uint64
 
 // LSM segment restore (host-only; uses add_rows_locked / wv_index_delete above)
 #include "lsm_segment.hip"
+
+// micro-batcher of concurrent single-query SearchByVector calls
+#include "batcher.hip"

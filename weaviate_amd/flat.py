@@ -267,10 +267,24 @@ class FlatIndex:
         return ids, dists, counts
 
     def search_by_vector(self, vector, k: int, allow: Optional[AllowList] = None):
-        """flat.SearchByVector: (ids, dists) ascending, len <= k."""
-        ids, dists, counts = self.search_by_vector_batch(np.asarray(vector, dtype=np.float32)[None, :], k, allow)
-        n = int(counts[0])
-        return ids[0, :n].copy(), dists[0, :n].copy()
+        """flat.SearchByVector: (ids, dists) ascending, len <= k.  One query per
+        call, safe to call from many threads at once: concurrent calls are
+        coalesced into batched launches by the C side's micro-batcher
+        (wv_index_search_by_vector)."""
+        v = np.ascontiguousarray(vector, dtype=np.float32).ravel()
+        kk = max(int(k), 1)
+        ids = np.zeros(kk, dtype=np.uint64)
+        dists = np.zeros(kk, dtype=np.float32)
+        n = C.c_int32(0)
+        ap, na, mode, _keep = _allow_args(allow)
+        check(self._l.wv_index_search_by_vector(self._h, _fptr(v), v.size, int(k), ap, na, mode, _uptr(ids),
+                                                _fptr(dists), C.byref(n)))
+        return ids[:n.value].copy(), dists[:n.value].copy()
+
+    def batcher_stats(self) -> dict:
+        out = (C.c_int64 * 3)()
+        check(self._l.wv_index_batcher_stats(self._h, out))
+        return {"calls": out[0], "launches": out[1], "max_batch": out[2]}
 
     def search_by_vector_distance(self, vector, target_distance: float, max_limit: int,
                                   allow: Optional[AllowList] = None):
