@@ -257,7 +257,8 @@ int wv_index_debug_candidates(wv_index *idx, float *A, float *E, uint32_t *I, fl
 
 /* tuning / testing knobs: "margin" (extra candidates, default 8),
  * "force_replay" (1 = resolve every query by heap replay), "spans" (0 = auto),
- * "kernel" (select kernel: 4 = bf16x3 MFMA (default for the exact fp32 path),
+ * "kernel" (select kernel: 6 = HBM-streaming GEMV (default for batches <= "gemv_max",
+ * default 8), 4 = bf16x3 MFMA (default for the exact fp32 path),
  * 3 = f32 MFMA ring, 2/1 older f32 forms), "bq_kernel" (1 = generic BQ kernels),
  * "timing" (1 = record kernel times with HIP events), "batch_window_us" /
  * "batch_max" (micro-batcher, see wv_index_search_by_vector) */

@@ -198,7 +198,7 @@ def test_search_by_vector_distance(wv, oracle):
     assert len(ids) == 31
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("kernel", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("metric,kind,n,d,k", [("cosine", 0, 9000, 768, 10), ("l2-squared", 0, 7000, 96, 24),
                                                ("dot", 1, 5000, 64, 5)])
 def test_select_kernel_variants(wv, oracle, kernel, metric, kind, n, d, k):
@@ -209,6 +209,29 @@ def test_select_kernel_variants(wv, oracle, kernel, metric, kind, n, d, k):
     ids, dists, counts = idx.search_by_vector_batch(queries, k)
     for qi in range(0, len(queries), 7):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
+
+
+@pytest.mark.parametrize("metric,kind,n,d,k,nq", [
+    ("cosine", 0, 30000, 768, 10, 1), ("cosine", 0, 30000, 768, 10, 8), ("l2-squared", 0, 20000, 100, 24, 3),
+    ("dot", 2, 12000, 40, 5, 5), ("l2-squared", 1, 8000, 2500, 10, 6), ("cosine", 0, 5000, 1536, 32 - 8, 2)])
+def test_gemv_small_batches(wv, oracle, metric, kind, n, d, k, nq):
+    """Batches <= gemv_max take k_gemv_select (the HBM-streaming GEMV path) by default."""
+    data = gen(oracle, kind, 91, n, d)
+    queries = gen(oracle, kind, 92, nq, d)
+    idx, orc = build_pair(wv, oracle, metric, "avx256", data)
+    idx.delete(*range(3, n, 17))
+    orc.delete(list(range(3, n, 17)))
+    before = idx.stats()["replayed_queries"]
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    for qi in range(nq):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
+    if kind == 0:  # continuous data: the fp32 error bound proves every query, no replay
+        assert idx.stats()["replayed_queries"] == before
+    allow = list(range(5, n, 3))
+    ids, dists, counts = idx.search_by_vector_batch(queries, k, allow=wv.AllowList(allow))
+    for qi in range(nq):
+        assert_same(orc.search(queries[qi], k, allow=allow), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"a{qi}")
+    idx.close()
 
 
 # ---------------------------------------------------------------------------

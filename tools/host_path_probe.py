@@ -26,7 +26,15 @@ def main():
     torch.cuda.synchronize()
     q = qd.cpu().numpy()
     idx.set_option("timing", 1)
-    for b in [1, 64, 111, 128, 205, 256]:
+    batches = [int(x) for x in os.environ.get("BATCHES", "1,64,111,128,205,256").split(",")]
+    runs = [(int(x), None) for x in os.environ.get("KERNELS", "0").split(",")]
+    runs += [(6, int(w)) for w in os.environ.get("GEMV_WGS", "").split(",") if w]
+    for kern, wg in runs:
+      idx.set_option("kernel", kern)
+      if wg:
+          idx.set_option("gemv_wg", wg)
+      print(f"kernel option {kern} gemv_wg {wg}", flush=True)
+      for b in batches:
         idx.search_by_vector_batch(q[:b], 10)
         ts = []
         for _ in range(3):
@@ -34,7 +42,7 @@ def main():
             idx.search_by_vector_batch(q[:b], 10)
             ts.append(time.perf_counter() - t0)
         st = idx.stats()
-        print(f"B={b}: host-path {min(ts)*1e3:.2f} ms  select {st['last_select_ms']:.2f} ms  total {st['last_total_ms']:.2f} ms  replayed {st['replayed_queries']}", flush=True)
+        print(f"  B={b}: host-path {min(ts)*1e3:.2f} ms  select {st['last_select_ms']:.2f} ms  total {st['last_total_ms']:.2f} ms  replayed {st['replayed_queries']}", flush=True)
 
 
 if __name__ == "__main__":

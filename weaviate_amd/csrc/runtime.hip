@@ -28,6 +28,7 @@
 #include "pq_kernels.hip"
 #include "kernels_bf3.hip"
 #include "rq_kernels.hip"
+#include "gemv_kernels.hip"
 
 using namespace wv;
 
@@ -165,10 +166,12 @@ struct wv_index {
     hipStream_t aux = nullptr;
     hipEvent_t evd[2] = {nullptr, nullptr}, evr[2] = {nullptr, nullptr};
     DBuf rE2, rB2;
+    DBuf gmA, gmI;  // GEMV path: first level of the two-level span merge
     wv_stats stats{};
     // micro-batcher of concurrent single-query searches (batcher.hip)
     wv_batcher* batcher = nullptr;
     int64_t batch_window_us = 0, batch_max = 4096;
+    int gemv_max = 8, gemv_wg = 1024;  // batches up to this many queries take the GEMV select kernel (kver 6)
 };
 
 // ---------------------------------------------------------------------------
@@ -231,7 +234,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
                     &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm,
-                    &idx->rE2, &idx->rB2})
+                    &idx->rE2, &idx->rB2, &idx->gmA, &idx->gmI})
         b->release();
     if (idx->aux) hipStreamSynchronize(idx->aux);
     for (hipEvent_t e : {idx->evd[0], idx->evd[1], idx->evr[0], idx->evr[1]})
@@ -608,6 +611,8 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     std::lock_guard<std::mutex> g(idx->mu);
     std::string k(key);
     if (k == "batch_window_us") { if (value < 0 || value > 1000000) return set_err(WV_ERR_INVALID, "batch_window_us out of range"); idx->batch_window_us = value; return WV_OK; }
+    if (k == "gemv_wg") { if (value < 8 || value > 65536) return set_err(WV_ERR_INVALID, "gemv_wg out of range"); idx->gemv_wg = (int)value; return WV_OK; }
+    if (k == "gemv_max") { if (value < 0 || value > 4096) return set_err(WV_ERR_INVALID, "gemv_max out of range"); idx->gemv_max = (int)value; return WV_OK; }
     if (k == "batch_max") { if (value < 1) return set_err(WV_ERR_INVALID, "batch_max out of range"); idx->batch_max = value; return WV_OK; }
     if (k == "margin") { if (value < 2 || value > 30) return set_err(WV_ERR_INVALID, "margin out of range"); idx->margin = (int)value; }
     else if (k == "force_replay") idx->force_replay = (int)value;
@@ -1768,11 +1773,16 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
 
     if (mfma_ok) {
         int kver = idx->kernel_opt;
-        if (kver == 0) kver = idx->use_bf3 ? (nq > QB ? 5 : 4) : 3;
-        if (kver >= 4 && !idx->use_bf3) kver = 3;
+        if (kver == 0) kver = nq <= idx->gemv_max ? 6 : idx->use_bf3 ? (nq > QB ? 5 : 4) : 3;
+        if ((kver == 4 || kver == 5) && !idx->use_bf3) kver = 3;
+        const bool gemv = kver == 6;
+        // GEMV: QG queries per workgroup staged in LDS (<= 64 KiB of query rows)
+        // (the smallest of 1/2/4/8 covering nq: padded query columns cost FMAs and LDS reads)
+        int gqg = nq <= 1 ? 1 : nq <= 2 ? 2 : nq <= 4 ? 4 : 8;
+        while (gqg > 1 && (int64_t)gqg * idx->dpad * 4 > 65536) gqg >>= 1;
         const int64_t bn = kver >= 3 ? BN3 : BN;
         const int64_t ntiles = (idx->hiwater + bn - 1) / bn;
-        const int qtile = kver == 5 ? QBW : QB;
+        const int qtile = gemv ? gqg : kver == 5 ? QBW : QB;
         const int nqb = (int)(round_up(nq, qtile) / qtile);
         int qgroup = 1;
         for (int g : {4, 2, 1})
@@ -1783,7 +1793,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         // (k_mfma_select_bf3w: one 1024-wide wave of resident workgroups, 256
         // = one per CU, measured fastest; its 32-bit span offsets need a span
         // below 4 GiB of one plane)
-        const int64_t target_wg = kver == 5 ? 256 : kver >= 3 ? 768 : 1024;
+        const int64_t target_wg = gemv ? idx->gemv_wg : kver == 5 ? 256 : kver >= 3 ? 768 : 1024;
         int64_t nspans = idx->spans_opt > 0 ? idx->spans_opt : std::max<int64_t>(8, (target_wg + nqb - 1) / nqb);
         if (kver == 5) {
             const int64_t tile_bytes = (int64_t)(idx->dpad / 16) * 8192;
@@ -1817,6 +1827,10 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(4, (budget - fixed) / (qtile * 8)));
         if (idx->cbuf_opt > 0) C = std::min(64 - KP, idx->cbuf_opt);
         size_t lds = (size_t)(fixed + (int64_t)qtile * C * 8);
+        if (gemv) {  // a 32-row chunk adds <= 32 candidates per query: C = 64 - KP >= 32 never overflows
+            C = 64 - KP;
+            lds = (size_t)((int64_t)gqg * idx->dpad + (int64_t)gqg * KP * 2 + (int64_t)gqg * C * 2 + gqg * 2 + 3) * sizeof(float);
+        }
         a.C = C;
         dim3 grid((unsigned)(nqb * nspans));
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
@@ -1840,7 +1854,25 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select_bf3w<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
         k_mfma_select_bf3w<M, 1><<<grid, 512, lds, s>>>(a);                                                \
     } while (0)
-        if (kver == 5) {
+#define WV_GEMV(M, G)                                                                                      \
+    do {                                                                                                   \
+        HIPCHK(hipFuncSetAttribute((const void*)k_gemv_select<M, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_gemv_select<M, G><<<grid, 256, lds, s>>>(a);                                                     \
+    } while (0)
+#define WV_GEMVQ(M)                                          \
+    do {                                                     \
+        if (gqg == 8) WV_GEMV(M, 8);                         \
+        else if (gqg == 4) WV_GEMV(M, 4);                    \
+        else if (gqg == 2) WV_GEMV(M, 2);                    \
+        else WV_GEMV(M, 1);                                  \
+    } while (0)
+        if (gemv) {
+            switch (idx->metric) {
+            case WV_METRIC_L2_SQUARED: WV_GEMVQ(L2); break;
+            case WV_METRIC_DOT: WV_GEMVQ(DOT); break;
+            default: WV_GEMVQ(COSINE); break;
+            }
+        } else if (kver == 5) {
             switch (idx->metric) {
             case WV_METRIC_L2_SQUARED: WV_SELW(L2); break;
             case WV_METRIC_DOT: WV_SELW(DOT); break;
@@ -1865,6 +1897,8 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
             default: if (v2) WV_SEL(k_mfma_select2, COSINE); else WV_SEL(k_mfma_select, COSINE); break;
             }
         }
+#undef WV_GEMVQ
+#undef WV_GEMV
 #undef WV_SELW
 #undef WV_SELB
 #undef WV_SEL3
@@ -1872,8 +1906,23 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         HIPCHK(hipGetLastError());
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
         idx->stats.mfma_launches++;
-        k_merge_spans<1><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(a.outA, a.outI, (int)nq, (int)nspans, KP,
-                                                                   idx->candA.as<float>(), idx->candI.as<uint32_t>());
+        int G = 1;  // GEMV: ~1024 spans per query -> merge in two levels (G groups of nspans/G)
+        if (gemv)
+            for (int g = 32; g >= 2; g--)
+                if (nspans % g == 0 && nspans / g >= 2) { G = g; break; }
+        if (gemv && G > 1) {
+            HIPCHK(idx->gmA.ensure((size_t)nq * G * KP * sizeof(float)));
+            HIPCHK(idx->gmI.ensure((size_t)nq * G * KP * sizeof(uint32_t)));
+            k_merge_spans<2><<<(unsigned)((nq * G + 3) / 4), 256, 0, s>>>(a.outA, a.outI, (int)(nq * G), (int)(nspans / G),
+                                                                           KP, idx->gmA.as<float>(), idx->gmI.as<uint32_t>());
+            k_merge_spans<2><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(idx->gmA.as<float>(), idx->gmI.as<uint32_t>(), (int)nq,
+                                                                       G, KP, idx->candA.as<float>(), idx->candI.as<uint32_t>());
+        } else if (gemv)
+            k_merge_spans<2><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(a.outA, a.outI, (int)nq, (int)nspans, KP,
+                                                                       idx->candA.as<float>(), idx->candI.as<uint32_t>());
+        else
+            k_merge_spans<1><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(a.outA, a.outI, (int)nq, (int)nspans, KP,
+                                                                       idx->candA.as<float>(), idx->candI.as<uint32_t>());
         const int64_t npairs = nq * KP;
         const bool v5 = idx->variant == WV_VARIANT_AVX512;
 #define WV_RS(M, V) k_rescore<M, V><<<(unsigned)((npairs + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, Qn, idx->dims, idx->candI.as<uint32_t>(), (int)nq, KP, idx->candE.as<float>())
@@ -1897,7 +1946,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         const double u4 = 2.384185791015625e-07;
         const double hdep = 3.0 * idx->dpad / 16.0 + 16.0;
         const double g3 = hdep * u4 / (1.0 - hdep * u4);
-        const double extra = kver >= 4 ? 2.0 * (3.05 * 1.52587890625e-05 + g3) : 0.0;
+        const double extra = (kver == 4 || kver == 5) ? 2.0 * (3.05 * 1.52587890625e-05 + g3) : 0.0;
         const float eps_scale = (float)((2.0 * gamma_n(idx->dpad + 4) + extra) * 1.05 + 1e-12);
         const float eps_base = (float)(std::sqrt((double)maxn2) * (1.0 + 1e-6));
         idx->last_eps_scale = eps_scale;
