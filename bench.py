@@ -39,6 +39,8 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (spec, MI355X_MICROARCH
 # 32-lane/clk rate (78.6 T) is the f32 FMA rate; v_xor_b32 / v_bcnt_u32_b32 issue
 # at 4 cycles per wave64 (measured: k_bq_blockmin_lds sustains 33.6 T instr-lane-ops/s).
 VALU_PEAK_TOPS = 39.3
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+GEMV_MAX = 8                   # runtime.hip default "gemv_max": batches up to 8 queries take k_gemv_select
 
 # BASELINE configs[3]: BQ 50M x 1536 over 8 GPUs -> one GPU holds a 6.25M-row shard
 BQ_ROWS_PER_GPU = 6_250_000
@@ -315,7 +317,7 @@ def main():
     value = total_q / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     # the fp32 path's select kernel: 256 x 256 tiles above 128 queries (runtime.hip auto choice)
-    sel_kernel = "k_mfma_select_bf3w" if B > 128 else "k_mfma_select_bf3"
+    sel_kernel = "k_mfma_select_bf3w" if B > 128 else "k_gemv_select" if B <= GEMV_MAX else "k_mfma_select_bf3"
     if args.traffic_bytes is None:
         args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B,
                                               None if (pq or bq or rq_bits) else sel_kernel)
@@ -358,6 +360,16 @@ def main():
         roof = {"bound": "valu", "kernel": "k_bq_blockmin", "achieved": achieved, "peak": VALU_PEAK_TOPS,
                 "unit": "Tops/s (int32 lane-ops)", "frac": achieved / VALU_PEAK_TOPS, "launch_ms": sel_avg,
                 "hbm_GBps": n_local * words * 8 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
+                "traffic": args.traffic_bytes}
+    elif sel_kernel == "k_gemv_select":
+        # batches <= GEMV_MAX queries: the HBM-streaming GEMV (runtime.hip,
+        # gemv_kernels.hip) -- algorithmic bytes per launch = one pass over the
+        # shard's fp32 rows (N_local x d x 4 B) + the queries, over its measured
+        # average duration (HIP events on its stream)
+        nbytes = float(n_local) * dims * 4 + B * dims * 4
+        achieved = nbytes / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0
+        roof = {"bound": "hbm", "kernel": sel_kernel, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "launch_ms": sel_avg,
                 "traffic": args.traffic_bytes}
     else:
         # roofline of the dominant kernel (k_mfma_select_bf3w): algorithmic flops
