@@ -1,0 +1,36 @@
+"""BASELINE configs[1] probe: SIFT-shaped 1M x 128 integer-valued fp32 (U{0..127}),
+l2-squared, k=100, query batches through the host-buffer batch path.
+k + margin > 32 exceeds the select kernels' candidate lists, so every query is
+resolved by the exact heap replay: this measures that path."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    import weaviate_amd as wv
+    from weaviate_amd import _lib
+    lib = _lib.load()
+    n, d, k = 1_000_000, 128, 100
+    idx = wv.FlatIndex(distance="l2-squared", dims=d, variant="avx256")
+    idx.reserve(n)
+    stage = torch.empty((n, d), dtype=torch.float32, device="cuda")
+    _lib.check(lib.wv_gen_device(0, 1, 1, 0, n, d, stage.data_ptr(), None))
+    _lib.check(lib.wv_index_add_range_device(idx._h, 0, stage.data_ptr(), n, d))
+    qd = torch.empty((10000, d), dtype=torch.float32, device="cuda")
+    _lib.check(lib.wv_gen_device(0, 1, 2, 0, 10000, d, qd.data_ptr(), None))
+    torch.cuda.synchronize()
+    q = qd.cpu().numpy()
+    for nq in [int(x) for x in os.environ.get("NQ", "100,1000,10000").split(",")]:
+        r0 = idx.stats()["replayed_queries"]
+        t0 = time.perf_counter()
+        idx.search_by_vector_batch(q[:nq], k)
+        el = time.perf_counter() - t0
+        print(f"nq={nq}: {el*1e3:.1f} ms  {nq/el:.0f} QPS  replayed {idx.stats()['replayed_queries'] - r0}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
