@@ -24,6 +24,7 @@ def main():
     _lib.check(lib.wv_gen_device(0, 1, 2, 0, 10000, d, qd.data_ptr(), None))
     torch.cuda.synchronize()
     q = qd.cpu().numpy()
+    idx.set_option("exact_multi", int(os.environ.get("EXACT_MULTI", "1")))
     for nq in [int(x) for x in os.environ.get("NQ", "100,1000,10000").split(",")]:
         r0 = idx.stats()["replayed_queries"]
         t0 = time.perf_counter()

@@ -984,6 +984,119 @@ __global__ __launch_bounds__(256) void k_exact_rows(const float* __restrict__ X,
     }
 }
 
+// (1b) k_exact_rows for QF queries per thread (the AVX2 accumulation order,
+//      i.e. VARIANT AVX256, or AVX512 below 128 dims where both orders agree):
+//      the thread's row is loaded once per 32-float block and stepped into the
+//      QF queries' accumulators, cutting the uncoalesced row loads QF-fold.
+//      Same order of operations per (query, row) as exact_raw's
+//      32-block / 8-block / scalar-tail paths and reduce_ymm4.
+template <int METRIC, int QF>
+__device__ __forceinline__ void exact_raw_avx256_multi(const float* const (&q)[QF], const float* __restrict__ x, int n,
+                                                       float (&out)[QF]) {
+    float sum[QF];
+    float acc[QF][4][8];
+#pragma unroll
+    for (int f = 0; f < QF; f++) {
+        sum[f] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int l = 0; l < 8; l++) acc[f][j][l] = 0.f;
+    }
+    if (n < 8) {
+        for (int i = 0; i < n; i++) {
+            const float xv = x[i];
+#pragma unroll
+            for (int f = 0; f < QF; f++) sum[f] = scalar_step<METRIC>(sum[f], q[f][i], xv);
+        }
+#pragma unroll
+        for (int f = 0; f < QF; f++) out[f] = sum[f];
+        return;
+    }
+    int e = 0;
+    while (n - e >= 32) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const float4 b = ld4(x + e + 8 * j + 4 * c);
+#pragma unroll
+                for (int f = 0; f < QF; f++) {
+                    const float4 a = ld4(q[f] + e + 8 * j + 4 * c);
+                    acc[f][j][4 * c + 0] = elem_step<METRIC>(acc[f][j][4 * c + 0], a.x, b.x);
+                    acc[f][j][4 * c + 1] = elem_step<METRIC>(acc[f][j][4 * c + 1], a.y, b.y);
+                    acc[f][j][4 * c + 2] = elem_step<METRIC>(acc[f][j][4 * c + 2], a.z, b.z);
+                    acc[f][j][4 * c + 3] = elem_step<METRIC>(acc[f][j][4 * c + 3], a.w, b.w);
+                }
+            }
+        }
+        e += 32;
+    }
+    while (n - e >= 8) {
+#pragma unroll
+        for (int l = 0; l < 8; l++) {
+            const float xv = x[e + l];
+#pragma unroll
+            for (int f = 0; f < QF; f++) acc[f][0][l] = elem_step<METRIC>(acc[f][0][l], q[f][e + l], xv);
+        }
+        e += 8;
+    }
+    for (; e < n; e++) {
+        const float xv = x[e];
+#pragma unroll
+        for (int f = 0; f < QF; f++) sum[f] = scalar_step<METRIC>(sum[f], q[f][e], xv);
+    }
+#pragma unroll
+    for (int f = 0; f < QF; f++) out[f] = sum[f] + reduce_ymm4(acc[f]);
+}
+
+template <int METRIC, int QF>
+__global__ __launch_bounds__(256) void k_exact_rows_multi(const float* __restrict__ X, int dpad,
+                                                          const uint32_t* __restrict__ valid, int64_t nslots,
+                                                          const float* __restrict__ Q, int d,
+                                                          const int32_t* __restrict__ qlist, int F, int64_t ld,
+                                                          float* __restrict__ E, float* __restrict__ bmin) {
+    __shared__ float red[4][QF];
+    const int FB = (F + QF - 1) / QF;
+    const int fb = blockIdx.x % FB;
+    const int64_t blk = blockIdx.x / FB;
+    const int64_t s = blk * EBLK + threadIdx.x;
+    const float* qv[QF];
+#pragma unroll
+    for (int f = 0; f < QF; f++) {
+        const int ff = fb * QF + f < F ? fb * QF + f : fb * QF;  // duplicate a real query, never written
+        qv[f] = Q + (int64_t)qlist[ff] * dpad;
+    }
+    float e[QF];
+#pragma unroll
+    for (int f = 0; f < QF; f++) e[f] = __builtin_inff();
+    const bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
+    if (ok) {
+        float r[QF];
+        exact_raw_avx256_multi<METRIC == L2 ? L2 : DOT, QF>(qv, X + s * dpad, d, r);
+#pragma unroll
+        for (int f = 0; f < QF; f++) {
+            if (METRIC == L2) e[f] = r[f];
+            else if (METRIC == DOT) e[f] = -r[f];
+            else { const float p = 1.f - r[f]; e[f] = p < 0.f ? 0.f : p; }
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < QF; f++) {
+        const int ff = fb * QF + f;
+        if (ff < F && s < ld) E[(int64_t)ff * ld + s] = e[f];
+        float m = e[f];
+        for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][f] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x < QF) {
+        const int f = threadIdx.x;
+        const int ff = fb * QF + f;
+        if (ff < F) bmin[(int64_t)ff * (ld / EBLK) + blk] = fminf(fminf(red[0][f], red[1][f]), fminf(red[2][f], red[3][f]));
+    }
+}
+
 // (2) exact replay of the reference heap (priorityqueue NewMax +
 //     insertToHeap, flat/index.go:578-688) over the precomputed distances, in
 //     id order, one wave per listed query.  A 256-row block is skipped when the

@@ -171,7 +171,7 @@ struct wv_index {
     // micro-batcher of concurrent single-query searches (batcher.hip)
     wv_batcher* batcher = nullptr;
     int64_t batch_window_us = 0, batch_max = 4096;
-    int gemv_max = 8, gemv_wg = 1024;  // batches up to this many queries take the GEMV select kernel (kver 6)
+    int gemv_max = 8, gemv_wg = 1024, exact_multi = 1;  // batches up to this many queries take the GEMV select kernel (kver 6)
 };
 
 // ---------------------------------------------------------------------------
@@ -611,6 +611,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     std::lock_guard<std::mutex> g(idx->mu);
     std::string k(key);
     if (k == "batch_window_us") { if (value < 0 || value > 1000000) return set_err(WV_ERR_INVALID, "batch_window_us out of range"); idx->batch_window_us = value; return WV_OK; }
+    if (k == "exact_multi") { idx->exact_multi = value ? 1 : 0; return WV_OK; }
     if (k == "gemv_wg") { if (value < 8 || value > 65536) return set_err(WV_ERR_INVALID, "gemv_wg out of range"); idx->gemv_wg = (int)value; return WV_OK; }
     if (k == "gemv_max") { if (value < 0 || value > 4096) return set_err(WV_ERR_INVALID, "gemv_max out of range"); idx->gemv_max = (int)value; return WV_OK; }
     if (k == "batch_max") { if (value < 1) return set_err(WV_ERR_INVALID, "batch_max out of range"); idx->batch_max = value; return WV_OK; }
@@ -689,6 +690,17 @@ static int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const
         if (nslots > 0 && Qn) {
             const unsigned grid = (unsigned)(F * (ld / EBLK));
 #define WV_EX(M, V) k_exact_rows<M, V><<<grid, EBLK, 0, s>>>(idx->X, idx->dpad, valid, nslots, Qn, idx->dims, d_qlist + g0, F, ld, idx->rE.as<float>(), idx->rB.as<float>())
+            // AVX2 order (or AVX-512 below 128 dims, the same order): 4 queries per thread
+            const bool multi = idx->metric != WV_METRIC_HAMMING && (!v5 || idx->dims < 128) && idx->exact_multi;
+            const unsigned gridm = (unsigned)(((F + 3) / 4) * (ld / EBLK));
+#define WV_EXM(M) k_exact_rows_multi<M, 4><<<gridm, EBLK, 0, s>>>(idx->X, idx->dpad, valid, nslots, Qn, idx->dims, d_qlist + g0, F, ld, idx->rE.as<float>(), idx->rB.as<float>())
+            if (multi) {
+                switch (idx->metric) {
+                case WV_METRIC_L2_SQUARED: WV_EXM(L2); break;
+                case WV_METRIC_DOT: WV_EXM(DOT); break;
+                default: WV_EXM(COSINE); break;
+                }
+            } else
             switch (idx->metric) {
             case WV_METRIC_L2_SQUARED: if (v5) WV_EX(L2, AVX512); else WV_EX(L2, AVX256); break;
             case WV_METRIC_DOT: if (v5) WV_EX(DOT, AVX512); else WV_EX(DOT, AVX256); break;
@@ -696,6 +708,7 @@ static int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const
             default: WV_EX(HAMMING, AVX256); break;
             }
 #undef WV_EX
+#undef WV_EXM
             HIPCHK(hipGetLastError());
         }
         const bool raw = !extract;
