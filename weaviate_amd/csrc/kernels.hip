@@ -1057,16 +1057,20 @@ __global__ __launch_bounds__(256) void k_exact_rows_multi(const float* __restric
                                                           const int32_t* __restrict__ qlist, int F, int64_t ld,
                                                           float* __restrict__ E, float* __restrict__ bmin) {
     __shared__ float red[4][QF];
+    extern __shared__ __attribute__((aligned(16))) float qs[];  // [QF][dpad]: broadcast ds_reads, not VMEM
     const int FB = (F + QF - 1) / QF;
     const int fb = blockIdx.x % FB;
     const int64_t blk = blockIdx.x / FB;
     const int64_t s = blk * EBLK + threadIdx.x;
+    for (int i = threadIdx.x; i < QF * dpad; i += 256) {
+        const int f = i / dpad;
+        const int ff = fb * QF + f < F ? fb * QF + f : fb * QF;  // duplicate a real query, never written
+        qs[i] = Q[(int64_t)qlist[ff] * dpad + (i - f * dpad)];
+    }
+    __syncthreads();
     const float* qv[QF];
 #pragma unroll
-    for (int f = 0; f < QF; f++) {
-        const int ff = fb * QF + f < F ? fb * QF + f : fb * QF;  // duplicate a real query, never written
-        qv[f] = Q + (int64_t)qlist[ff] * dpad;
-    }
+    for (int f = 0; f < QF; f++) qv[f] = qs + f * dpad;
     float e[QF];
 #pragma unroll
     for (int f = 0; f < QF; f++) e[f] = __builtin_inff();

@@ -691,9 +691,11 @@ static int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const
             const unsigned grid = (unsigned)(F * (ld / EBLK));
 #define WV_EX(M, V) k_exact_rows<M, V><<<grid, EBLK, 0, s>>>(idx->X, idx->dpad, valid, nslots, Qn, idx->dims, d_qlist + g0, F, ld, idx->rE.as<float>(), idx->rB.as<float>())
             // AVX2 order (or AVX-512 below 128 dims, the same order): 4 queries per thread
-            const bool multi = idx->metric != WV_METRIC_HAMMING && (!v5 || idx->dims < 128) && idx->exact_multi;
+            const bool multi = idx->metric != WV_METRIC_HAMMING && (!v5 || idx->dims < 128) && idx->exact_multi &&
+                               (int64_t)idx->dpad * 16 <= 65536;
+            const size_t lds_q = (size_t)4 * idx->dpad * sizeof(float);
             const unsigned gridm = (unsigned)(((F + 3) / 4) * (ld / EBLK));
-#define WV_EXM(M) k_exact_rows_multi<M, 4><<<gridm, EBLK, 0, s>>>(idx->X, idx->dpad, valid, nslots, Qn, idx->dims, d_qlist + g0, F, ld, idx->rE.as<float>(), idx->rB.as<float>())
+#define WV_EXM(M) k_exact_rows_multi<M, 4><<<gridm, EBLK, lds_q, s>>>(idx->X, idx->dpad, valid, nslots, Qn, idx->dims, d_qlist + g0, F, ld, idx->rE.as<float>(), idx->rB.as<float>())
             if (multi) {
                 switch (idx->metric) {
                 case WV_METRIC_L2_SQUARED: WV_EXM(L2); break;
