@@ -25,10 +25,12 @@ def assert_same(oracle_res, ids, dists, ctx=""):
                                   np.asarray(od, np.float32).view(np.uint32), err_msg=f"{ctx}: dists")
 
 
-def build_pair(wv, oracle, metric_name, variant, data, ids=None, dims=0):
+def build_pair(wv, oracle, metric_name, variant, data, ids=None, dims=0, options=None):
     n, d = data.shape
     ids = np.arange(n, dtype=np.uint64) if ids is None else ids
     idx = wv.FlatIndex(distance=metric_name, variant=variant, dims=dims)
+    for key, val in (options or {}).items():
+        idx.set_option(key, val)
     idx.add_batch(ids, data)
     orc = oracle.OracleFlat(oracle.METRIC[metric_name], VARIANTS[variant], d, int(ids.max()) + 1)
     orc.add_batch(ids, data)
@@ -198,16 +200,19 @@ def test_search_by_vector_distance(wv, oracle):
     assert len(ids) == 31
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("kernel", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("metric,kind,n,d,k", [("cosine", 0, 9000, 768, 10), ("l2-squared", 0, 7000, 96, 24),
                                                ("dot", 1, 5000, 64, 5)])
 def test_select_kernel_variants(wv, oracle, kernel, metric, kind, n, d, k):
+    """Every select kernel (1-6 legacy f32 / bf16x3 / GEMV, 7 = block keys)
+    against the oracle on every query."""
     data = gen(oracle, kind, 81, n, d)
     queries = gen(oracle, kind, 82, 300, d)   # > 2 query blocks, ragged last block
-    idx, orc = build_pair(wv, oracle, metric, "avx256", data)
+    idx, orc = build_pair(wv, oracle, metric, "avx256", data,
+                          options={"bf3_planes": 1} if kernel in (4, 5) else None)
     idx.set_option("kernel", kernel)
     ids, dists, counts = idx.search_by_vector_batch(queries, k)
-    for qi in range(0, len(queries), 7):
+    for qi in range(len(queries)):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
 
 
@@ -324,7 +329,9 @@ def test_bf16x3_error_within_proof_bound(wv, oracle, metric, kind, d):
     data = gen(oracle, kind, 91, n, d)
     queries = gen(oracle, kind, 92, 256, d)
     idx = wv.FlatIndex(distance=metric, variant="avx256")
+    idx.set_option("bf3_planes", 1)
     idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    idx.set_option("kernel", 5)
     idx.search_by_vector_batch(queries, 10)
     A, E, I, eps = idx.debug_candidates(len(queries))
     ok = I != 0xFFFFFFFF

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -29,6 +30,7 @@
 #include "kernels_bf3.hip"
 #include "rq_kernels.hip"
 #include "gemv_kernels.hip"
+#include "qs_kernels.hip"
 
 using namespace wv;
 
@@ -138,8 +140,18 @@ struct wv_index {
     int pq_m = 0, pq_ks = 0, pq_ds = 0, pq_training_limit = 0, pq_rescore = 1, pq_trained = 0;
     float* pq_centers = nullptr;
     uint32_t* pq_codes = nullptr;
-    // bf16 hi/lo planes of X for k_mfma_select_bf3 ([cap][dpad] each)
+    // bf16 hi/lo planes of X for k_mfma_select_bf3 ([cap][dpad] each): built
+    // only when option bf3_planes is set before the first Add
     int use_bf3 = 0;
+    // bf16 hi plane of X for the block-key path (qs_kernels.hip): [cap][dpb],
+    // dpb = dims rounded up to 128, built when dpb <= QS_MAX_DPB
+    int use_qs = 0, qs_planes = 0, dpb = 0;
+    uint16_t* Xb = nullptr;
+    uint32_t* qsmax = nullptr;      // device [4]: max |x - x_h|^2, max |x_h|^2 (float bits), non-finite flag
+    uint32_t* qscount = nullptr;    // device [4]: [0] replayed queries (cumulative), [1] this batch's flagged
+    int has_nonfinite = 0;          // host mirror of qsmax[2]
+    uint64_t replayed_host = 0;     // replays counted on the host (legacy paths)
+    int timed = 0;                  // ev0/ev1 bracket the last batch's dominant kernel
     float last_eps_scale = 0.f, last_eps_base = 0.f;  // exactness-proof eps of the last MFMA batch (debug hook)
     int64_t last_nq = 0;
     int last_KP = 0;
@@ -166,6 +178,7 @@ struct wv_index {
     hipStream_t aux = nullptr;
     hipEvent_t evd[2] = {nullptr, nullptr}, evr[2] = {nullptr, nullptr};
     DBuf rE2, rB2;
+    DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList;
     DBuf gmA, gmI;  // GEMV path: first level of the two-level span merge
     wv_stats stats{};
     // micro-batcher of concurrent single-query searches (batcher.hip)
@@ -177,6 +190,16 @@ struct wv_index {
 // ---------------------------------------------------------------------------
 // create / destroy / capacity
 // ---------------------------------------------------------------------------
+constexpr int QS_MAX_DPB = 768;  // k_qs_blockkey keeps 32 queries x dpb bf16 in VGPRs
+
+// dims fixed (config or first Add, initializeDimensionsAndRQ flat/index.go:338-360)
+static void set_dims(wv_index* idx, int64_t d) {
+    idx->dims = (int)d;
+    idx->dpad = (int)round_up(d, BK);
+    idx->dpb = (int)round_up(d, 128);
+    idx->qs_planes = (idx->use_qs && idx->dpb <= QS_MAX_DPB) ? 1 : 0;
+}
+
 extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     if (!cfg || !out) return set_err(WV_ERR_INVALID, "invalid config: nil");
     if (cfg->metric < 0 || cfg->metric > WV_METRIC_HAMMING)
@@ -200,9 +223,11 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     idx->device = cfg->device;
     idx->id_base = cfg->id_base;
     idx->root_path = cfg->root_path ? cfg->root_path : "";
-    // bf16x3 select kernel for the exact fp32 path (kernels_bf3.hip)
-    idx->use_bf3 = (cfg->compression == WV_COMPRESSION_NONE && cfg->metric != WV_METRIC_HAMMING) ? 1 : 0;
-    idx->kernel_opt = 0;  // auto: bf16x3 256x256 (5) for batches > 128 queries, else 128x256 (4); f32 (3) without planes
+    // block-key path for the exact fp32 search (qs_kernels.hip); the bf16x3
+    // select kernels (kernels_bf3.hip) need option bf3_planes before the first Add
+    idx->use_qs = (cfg->compression == WV_COMPRESSION_NONE && cfg->metric != WV_METRIC_HAMMING) ? 1 : 0;
+    idx->use_bf3 = 0;
+    idx->kernel_opt = 0;  // auto: the block-key path (7) when the planes exist, else the legacy select kernels
     if (cfg->compression == WV_COMPRESSION_RQ8) idx->rq_bits = 8;
     if (cfg->compression == WV_COMPRESSION_RQ1) idx->rq_bits = 1;
     if (cfg->compression == WV_COMPRESSION_PQ) {
@@ -211,10 +236,14 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
         idx->pq_training_limit = cfg->pq_training_limit;
         idx->pq_rescore = cfg->pq_rescore;
     }
-    if (cfg->dims > 0) { idx->dims = cfg->dims; idx->dpad = (int)round_up(cfg->dims, BK); }
+    if (cfg->dims > 0) set_dims(idx, cfg->dims);
     hipError_t e = hipStreamCreateWithFlags(&idx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&idx->d_maxn2, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(idx->d_maxn2, 0, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&idx->qsmax, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(idx->qsmax, 0, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&idx->qscount, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(idx->qscount, 0, 4 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipEventCreate(&idx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&idx->ev1);
     if (e != hipSuccess) {
@@ -234,7 +263,8 @@ extern "C" void wv_index_destroy(wv_index* idx) {
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
                     &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm,
-                    &idx->rE2, &idx->rB2, &idx->gmA, &idx->gmI})
+                    &idx->rE2, &idx->rB2, &idx->gmA, &idx->gmI, &idx->qsQb, &idx->qsInfo, &idx->qsKey, &idx->qsCand,
+                    &idx->qsNc, &idx->qsEps, &idx->qsFlags, &idx->qsList})
         b->release();
     if (idx->aux) hipStreamSynchronize(idx->aux);
     for (hipEvent_t e : {idx->evd[0], idx->evd[1], idx->evr[0], idx->evr[1]})
@@ -249,6 +279,9 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->pq_codes) hipFree(idx->pq_codes);
     if (idx->Xh) hipFree(idx->Xh);
     if (idx->Xl) hipFree(idx->Xl);
+    if (idx->Xb) hipFree(idx->Xb);
+    if (idx->qsmax) hipFree(idx->qsmax);
+    if (idx->qscount) hipFree(idx->qscount);
     for (void* p : {(void*)idx->rq_src, (void*)idx->rq_sign, (void*)idx->rq_round, idx->rq_codes, (void*)idx->rq_meta})
         if (p) hipFree(p);
     if (idx->ev0) hipEventDestroy(idx->ev0);
@@ -257,103 +290,130 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     delete idx;
 }
 
-// grow the id-indexed store to hold `need` slots (requires dims set)
+// grow the id-indexed store to hold `need` slots (requires dims set).
+// Transactional: every new buffer is allocated and filled first; only then are
+// the old ones freed and the new ones committed.  On any failure the partial
+// new buffers are freed and the index is left exactly as it was.
 static int ensure_capacity(wv_index* idx, int64_t need) {
     if (need <= idx->cap) return WV_OK;
     int64_t nc = std::max<int64_t>(need, idx->cap * 2);
     nc = round_up(std::max<int64_t>(nc, 1024), BN3);
+    const int64_t oc = idx->cap;
+    hipStream_t s = idx->stream;
+    std::vector<void*> fresh;
+    auto alloc = [&](void** p, size_t bytes) -> hipError_t {
+        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 256));
+        if (e == hipSuccess) fresh.push_back(*p);
+        else *p = nullptr;
+        return e;
+    };
     float* X = nullptr;
     float* xn = nullptr;
     uint32_t* pr = nullptr;
-    HIPCHK(hipMalloc(&X, (size_t)nc * idx->dpad * sizeof(float)));
-    HIPCHK(hipMalloc(&xn, (size_t)nc * sizeof(float)));
-    HIPCHK(hipMalloc(&pr, (size_t)(nc / 32) * sizeof(uint32_t)));
-    HIPCHK(hipMemsetAsync(pr, 0, (size_t)(nc / 32) * sizeof(uint32_t), idx->stream));
-    HIPCHK(hipMemsetAsync(xn, 0, (size_t)nc * sizeof(float), idx->stream));
-    HIPCHK(hipMemsetAsync(X + (size_t)idx->cap * idx->dpad, 0, (size_t)(nc - idx->cap) * idx->dpad * sizeof(float),
-                          idx->stream));
-    if (idx->cap > 0) {
-        HIPCHK(hipMemcpyAsync(X, idx->X, (size_t)idx->cap * idx->dpad * sizeof(float), hipMemcpyDeviceToDevice,
-                              idx->stream));
-        HIPCHK(hipMemcpyAsync(xn, idx->xnorm2, (size_t)idx->cap * sizeof(float), hipMemcpyDeviceToDevice, idx->stream));
-        HIPCHK(hipMemcpyAsync(pr, idx->present, (size_t)(idx->cap / 32) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                              idx->stream));
-    }
-    HIPCHK(hipStreamSynchronize(idx->stream));
-    if (idx->X) hipFree(idx->X);
-    if (idx->xnorm2) hipFree(idx->xnorm2);
-    if (idx->present) hipFree(idx->present);
-    if (idx->compression == WV_COMPRESSION_BQ) {
-        const int words = (idx->dims + 63) / 64;
-        uint64_t* cd = nullptr;
-        HIPCHK(hipMalloc(&cd, (size_t)words * nc * sizeof(uint64_t)));
-        HIPCHK(hipMemsetAsync(cd, 0, (size_t)words * nc * sizeof(uint64_t), idx->stream));
-        if (idx->cap > 0)  // word-major: copy each word plane
-            HIPCHK(hipMemcpy2DAsync(cd, (size_t)nc * sizeof(uint64_t), idx->codes, (size_t)idx->cap * sizeof(uint64_t),
-                                    (size_t)idx->cap * sizeof(uint64_t), words, hipMemcpyDeviceToDevice, idx->stream));
-        HIPCHK(hipStreamSynchronize(idx->stream));
-        if (idx->codes) hipFree(idx->codes);
-        idx->codes = cd;
-        idx->words = words;
-    }
+    uint64_t* cd = nullptr;
+    uint16_t *xh = nullptr, *xl = nullptr, *xb = nullptr;
+    void* rqc = nullptr;
+    float4* rqm = nullptr;
+    uint32_t* pc = nullptr;
+    const int words = (idx->dims + 63) / 64;
+    const size_t rq_cb = idx->rq_bits == 8 ? (size_t)nc * idx->rq_D : (size_t)(idx->rq_D / 64) * nc * sizeof(uint64_t);
+    const int64_t pq_w = idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0 ? pq_mwp(idx->pq_m) : 0;
+    const size_t plane_b = (size_t)nc * idx->dpad * sizeof(uint16_t);
+    const size_t qs_b = (size_t)nc * idx->dpb * sizeof(uint16_t);
+    hipError_t e = hipSuccess;
+    const char* what = "";
+#define WV_STEP(W, X_)                        \
+    do {                                      \
+        if (e == hipSuccess) { what = W; e = (X_); } \
+    } while (0)
+    WV_STEP("X", alloc((void**)&X, (size_t)nc * idx->dpad * sizeof(float)));
+    WV_STEP("xnorm2", alloc((void**)&xn, (size_t)nc * sizeof(float)));
+    WV_STEP("present", alloc((void**)&pr, (size_t)(nc / 32) * sizeof(uint32_t)));
+    if (idx->compression == WV_COMPRESSION_BQ) WV_STEP("bq codes", alloc((void**)&cd, (size_t)words * nc * sizeof(uint64_t)));
     if (idx->use_bf3) {
-        uint16_t *xh = nullptr, *xl = nullptr;
-        const size_t pb = (size_t)nc * idx->dpad * sizeof(uint16_t);
-        HIPCHK(hipMalloc(&xh, pb));
-        HIPCHK(hipMalloc(&xl, pb));
-        HIPCHK(hipMemsetAsync(xh, 0, pb, idx->stream));
-        HIPCHK(hipMemsetAsync(xl, 0, pb, idx->stream));
-        if (idx->cap > 0 && idx->Xh) {
-            const size_t ob = (size_t)idx->cap * idx->dpad * sizeof(uint16_t);
-            HIPCHK(hipMemcpyAsync(xh, idx->Xh, ob, hipMemcpyDeviceToDevice, idx->stream));
-            HIPCHK(hipMemcpyAsync(xl, idx->Xl, ob, hipMemcpyDeviceToDevice, idx->stream));
-        }
-        HIPCHK(hipStreamSynchronize(idx->stream));
-        if (idx->Xh) hipFree(idx->Xh);
-        if (idx->Xl) hipFree(idx->Xl);
-        idx->Xh = xh;
-        idx->Xl = xl;
+        WV_STEP("bf16 hi plane", alloc((void**)&xh, plane_b));
+        WV_STEP("bf16 lo plane", alloc((void**)&xl, plane_b));
     }
+    if (idx->qs_planes) WV_STEP("bf16 block-key plane", alloc((void**)&xb, qs_b));
     if (idx->rq_ready) {
-        const size_t cb = idx->rq_bits == 8 ? (size_t)nc * idx->rq_D : (size_t)(idx->rq_D / 64) * nc * sizeof(uint64_t);
-        void* cd = nullptr;
-        float4* md = nullptr;
-        HIPCHK(hipMalloc(&cd, cb));
-        HIPCHK(hipMalloc(&md, (size_t)nc * sizeof(float4)));
-        HIPCHK(hipMemsetAsync(cd, 0, cb, idx->stream));
-        HIPCHK(hipMemsetAsync(md, 0, (size_t)nc * sizeof(float4), idx->stream));
-        if (idx->cap > 0 && idx->rq_codes) {
-            if (idx->rq_bits == 8)  // tiles of 256 rows are contiguous: the old tiles are a prefix
-                HIPCHK(hipMemcpyAsync(cd, idx->rq_codes, (size_t)idx->cap * idx->rq_D, hipMemcpyDeviceToDevice,
-                                      idx->stream));
-            else
-                HIPCHK(hipMemcpy2DAsync(cd, (size_t)nc * sizeof(uint64_t), idx->rq_codes,
-                                        (size_t)idx->cap * sizeof(uint64_t), (size_t)idx->cap * sizeof(uint64_t),
-                                        idx->rq_D / 64, hipMemcpyDeviceToDevice, idx->stream));
-            HIPCHK(hipMemcpyAsync(md, idx->rq_meta, (size_t)idx->cap * sizeof(float4), hipMemcpyDeviceToDevice,
-                                  idx->stream));
+        WV_STEP("rq codes", alloc(&rqc, rq_cb));
+        WV_STEP("rq meta", alloc((void**)&rqm, (size_t)nc * sizeof(float4)));
+    }
+    if (pq_w) WV_STEP("pq codes", alloc((void**)&pc, (size_t)pq_w * nc * sizeof(uint32_t)));
+    // zero the new tails, copy the old contents
+    WV_STEP("memset", hipMemsetAsync(pr, 0, (size_t)(nc / 32) * sizeof(uint32_t), s));
+    WV_STEP("memset", hipMemsetAsync(xn, 0, (size_t)nc * sizeof(float), s));
+    WV_STEP("memset", hipMemsetAsync(X + (size_t)oc * idx->dpad, 0, (size_t)(nc - oc) * idx->dpad * sizeof(float), s));
+    if (oc > 0) {
+        WV_STEP("copy", hipMemcpyAsync(X, idx->X, (size_t)oc * idx->dpad * sizeof(float), hipMemcpyDeviceToDevice, s));
+        WV_STEP("copy", hipMemcpyAsync(xn, idx->xnorm2, (size_t)oc * sizeof(float), hipMemcpyDeviceToDevice, s));
+        WV_STEP("copy", hipMemcpyAsync(pr, idx->present, (size_t)(oc / 32) * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    }
+    if (cd) {
+        WV_STEP("memset", hipMemsetAsync(cd, 0, (size_t)words * nc * sizeof(uint64_t), s));
+        if (oc > 0 && idx->codes)  // word-major: copy each word plane
+            WV_STEP("copy", hipMemcpy2DAsync(cd, (size_t)nc * sizeof(uint64_t), idx->codes, (size_t)oc * sizeof(uint64_t),
+                                             (size_t)oc * sizeof(uint64_t), words, hipMemcpyDeviceToDevice, s));
+    }
+    if (xh) {
+        WV_STEP("memset", hipMemsetAsync(xh, 0, plane_b, s));
+        WV_STEP("memset", hipMemsetAsync(xl, 0, plane_b, s));
+        if (oc > 0 && idx->Xh) {  // 256-row tiles: the old tiles are a prefix
+            const size_t ob = (size_t)oc * idx->dpad * sizeof(uint16_t);
+            WV_STEP("copy", hipMemcpyAsync(xh, idx->Xh, ob, hipMemcpyDeviceToDevice, s));
+            WV_STEP("copy", hipMemcpyAsync(xl, idx->Xl, ob, hipMemcpyDeviceToDevice, s));
         }
-        HIPCHK(hipStreamSynchronize(idx->stream));
+    }
+    if (xb) {
+        WV_STEP("memset", hipMemsetAsync(xb, 0, qs_b, s));
+        if (oc > 0 && idx->Xb)
+            WV_STEP("copy", hipMemcpyAsync(xb, idx->Xb, (size_t)oc * idx->dpb * sizeof(uint16_t), hipMemcpyDeviceToDevice, s));
+    }
+    if (rqc) {
+        WV_STEP("memset", hipMemsetAsync(rqc, 0, rq_cb, s));
+        WV_STEP("memset", hipMemsetAsync(rqm, 0, (size_t)nc * sizeof(float4), s));
+        if (oc > 0 && idx->rq_codes) {
+            if (idx->rq_bits == 8)  // tiles of 256 rows are contiguous: the old tiles are a prefix
+                WV_STEP("copy", hipMemcpyAsync(rqc, idx->rq_codes, (size_t)oc * idx->rq_D, hipMemcpyDeviceToDevice, s));
+            else
+                WV_STEP("copy", hipMemcpy2DAsync(rqc, (size_t)nc * sizeof(uint64_t), idx->rq_codes,
+                                                 (size_t)oc * sizeof(uint64_t), (size_t)oc * sizeof(uint64_t),
+                                                 idx->rq_D / 64, hipMemcpyDeviceToDevice, s));
+            WV_STEP("copy", hipMemcpyAsync(rqm, idx->rq_meta, (size_t)oc * sizeof(float4), hipMemcpyDeviceToDevice, s));
+        }
+    }
+    if (pc) {
+        WV_STEP("memset", hipMemsetAsync(pc, 0, (size_t)pq_w * nc * sizeof(uint32_t), s));
+        if (oc > 0 && idx->pq_codes)
+            WV_STEP("copy", hipMemcpyAsync(pc, idx->pq_codes, (size_t)pq_w * oc * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    }
+    const hipError_t es = hipStreamSynchronize(s);
+    if (e == hipSuccess && es != hipSuccess) { e = es; what = "sync"; }
+#undef WV_STEP
+    if (e != hipSuccess) {
+        for (void* p : fresh) hipFree(p);
+        (void)hipGetLastError();
+        return set_err(WV_ERR_HIP, "ensure_capacity(%lld slots): %s: %s", (long long)nc, what, hipGetErrorString(e));
+    }
+    // commit
+    auto swap_in = [](auto*& cur, auto* nw) {
+        if (!nw) return;
+        if (cur) hipFree(cur);
+        cur = nw;
+    };
+    swap_in(idx->X, X);
+    swap_in(idx->xnorm2, xn);
+    swap_in(idx->present, pr);
+    if (cd) { swap_in(idx->codes, cd); idx->words = words; }
+    swap_in(idx->Xh, xh);
+    swap_in(idx->Xl, xl);
+    swap_in(idx->Xb, xb);
+    if (rqc) {
         if (idx->rq_codes) hipFree(idx->rq_codes);
-        if (idx->rq_meta) hipFree(idx->rq_meta);
-        idx->rq_codes = cd;
-        idx->rq_meta = md;
+        idx->rq_codes = rqc;
+        swap_in(idx->rq_meta, rqm);
     }
-    if (idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0) {
-        const int64_t mw = pq_mwp(idx->pq_m);
-        uint32_t* pc = nullptr;
-        HIPCHK(hipMalloc(&pc, (size_t)mw * nc * sizeof(uint32_t)));
-        HIPCHK(hipMemsetAsync(pc, 0, (size_t)mw * nc * sizeof(uint32_t), idx->stream));
-        if (idx->cap > 0 && idx->pq_codes)
-            HIPCHK(hipMemcpyAsync(pc, idx->pq_codes, (size_t)mw * idx->cap * sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                                  idx->stream));
-        HIPCHK(hipStreamSynchronize(idx->stream));
-        if (idx->pq_codes) hipFree(idx->pq_codes);
-        idx->pq_codes = pc;
-    }
-    idx->X = X;
-    idx->xnorm2 = xn;
-    idx->present = pr;
+    swap_in(idx->pq_codes, pc);
     idx->cap = nc;
     idx->h_present.resize((size_t)nc, 0);
     return WV_OK;
@@ -439,6 +499,9 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
         k_split_bf16<<<(unsigned)((ne + 255) / 256), 256, 0, idx->stream>>>(idx->X, n, idx->dpad, d_slots, idx->Xh,
                                                                            idx->Xl);
     }
+    if (idx->qs_planes)  // bf16 hi plane + residual-norm maxima of the block-key path
+        k_rows_split<<<(unsigned)((n + 3) / 4), 256, 0, idx->stream>>>(idx->X, idx->dpad, idx->dpb, n, d_slots, idx->Xb,
+                                                                       idx->qsmax);
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) launch_pq_encode(idx, n, d_slots);
     if (idx->rq_ready)  // Preload: quantizer.EncodeBytes / EncodeUint64 of the stored row (flat/index.go:844-865)
         launch_rq_encode(idx, idx->stream, idx->X, idx->dpad, n, d_slots, 0, idx->rq_codes, idx->cap, idx->rq_meta);
@@ -451,14 +514,34 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
 
 static int rq_init(wv_index* idx);
 
+// host mirror of the device non-finite flag (rows with NaN/Inf route the exact
+// search to the all-rows path); called after a synchronised Add
+static int refresh_nonfinite(wv_index* idx) {
+    if (!idx->qs_planes || idx->has_nonfinite) return WV_OK;
+    uint32_t f = 0;
+    HIPCHK(hipMemcpy(&f, idx->qsmax + 2, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    idx->has_nonfinite = f ? 1 : 0;
+    return WV_OK;
+}
+
+// shared by the host and device insert entry points: dims (lazily fixed by
+// the first Add), id range of the slot store
+static int validate_rows(wv_index* idx, int64_t d, uint64_t first_slot, uint64_t last_slot) {
+    int rc = validate_insert(idx, d);
+    if (rc) return rc;
+    if (idx->dims == 0 && d > (1 << 20)) return set_err(WV_ERR_INVALID, "dimensions too large: %lld", (long long)d);
+    if (first_slot > last_slot || last_slot >= (1ull << 32) - BN)
+        return set_err(WV_ERR_INVALID, "id %llu out of range", (unsigned long long)last_slot);
+    return WV_OK;
+}
+
 // rows: host pointer to n x d floats; ids: host doc ids
 static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs, int64_t n, int64_t d) {
     int rc = validate_insert(idx, d);
     if (rc) return rc;
     if (idx->dims == 0) {  // initOnce: initializeDimensionsAndRQ (flat/index.go:338-360)
         if (d > (1 << 20)) return set_err(WV_ERR_INVALID, "dimensions too large: %lld", (long long)d);
-        idx->dims = (int)d;
-        idx->dpad = (int)round_up(d, BK);
+        set_dims(idx, d);
     }
     if (idx->rq_bits && !idx->rq_ready) {
         rc = rq_init(idx);
@@ -509,7 +592,7 @@ static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs
         }
     }
     idx->count += (uint64_t)n;
-    return WV_OK;
+    return refresh_nonfinite(idx);
 }
 
 extern "C" int wv_index_add(wv_index* idx, uint64_t id, const float* vec, int64_t d) {
@@ -532,17 +615,19 @@ extern "C" int wv_index_add_range_device(wv_index* idx, uint64_t first_id, const
                                          int64_t d) {
     if (!idx) return set_err(WV_ERR_INVALID, "nil index");
     if (n == 0) return set_err(WV_ERR_INSERT, "insertBatch called with empty lists");
+    if (n < 0 || !d_vecs) return set_err(WV_ERR_INSERT, "ids and vectors sizes does not match");
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
-    int rc = validate_insert(idx, d);
+    if (first_id < idx->id_base) return set_err(WV_ERR_INVALID, "id below shard id_base");
+    const uint64_t s0u = first_id - idx->id_base;
+    int rc = validate_rows(idx, d, s0u, s0u + (uint64_t)n - 1);
     if (rc) return rc;
-    if (idx->dims == 0) { idx->dims = (int)d; idx->dpad = (int)round_up(d, BK); }
+    if (idx->dims == 0) set_dims(idx, d);
     if (idx->rq_bits && !idx->rq_ready) {
         rc = rq_init(idx);
         if (rc) return rc;
     }
-    if (first_id < idx->id_base) return set_err(WV_ERR_INVALID, "id below shard id_base");
-    int64_t s0 = (int64_t)(first_id - idx->id_base);
+    const int64_t s0 = (int64_t)s0u;
     rc = ensure_capacity(idx, s0 + n);
     if (rc) return rc;
     std::vector<uint32_t> hs((size_t)n);
@@ -557,7 +642,7 @@ extern "C" int wv_index_add_range_device(wv_index* idx, uint64_t first_id, const
     }
     idx->hiwater = std::max<int64_t>(idx->hiwater, s0 + n);
     idx->count += (uint64_t)n;
-    return WV_OK;
+    return refresh_nonfinite(idx);
 }
 
 // flat.Delete (flat/index.go:392-411): drop the key; count is not decremented
@@ -620,7 +705,20 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "spans") idx->spans_opt = (int)value;
     else if (k == "timing") idx->timing = (int)value;
     else if (k == "cbuf") idx->cbuf_opt = (int)value;
-    else if (k == "kernel") idx->kernel_opt = (int)value;
+    else if (k == "kernel") {
+        if (value < 0 || value > 7) return set_err(WV_ERR_INVALID, "kernel out of range (0-7)");
+        idx->kernel_opt = (int)value;
+    } else if (k == "bf3_planes") {
+        // the bf16x3 select kernels' hi/lo planes are built at Add: only before the first one
+        if (idx->cap > 0 && (value != 0) != (idx->use_bf3 != 0))
+            return set_err(WV_ERR_INVALID, "bf3_planes must be set before the first Add");
+        idx->use_bf3 = value ? 1 : 0;
+    } else if (k == "qs") {
+        if (idx->cap > 0 && (value != 0) != (idx->use_qs != 0))
+            return set_err(WV_ERR_INVALID, "qs must be set before the first Add");
+        idx->use_qs = value ? 1 : 0;
+        if (idx->dims) set_dims(idx, idx->dims);
+    }
     else if (k == "bq_kernel") idx->bq_kernel = (int)value;
     else if (k == "sel_dbg") idx->sel_dbg = (int)value;
     else if (k == "qgroup") idx->qgroup_opt = (int)value;
@@ -656,7 +754,21 @@ extern "C" int wv_index_debug_candidates(wv_index* idx, float* A, float* E, uint
 extern "C" int wv_index_stats(wv_index* idx, wv_stats* out) {
     if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
     std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    // device-side counters and timings of the block-key path are read here,
+    // never inside the search pipeline
+    uint32_t dev_replays = 0;
+    if (idx->qscount) {
+        HIPCHK(hipStreamSynchronize(idx->stream));
+        HIPCHK(hipMemcpy(&dev_replays, idx->qscount, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
+    if (idx->timed) {
+        HIPCHK(hipEventSynchronize(idx->ev1));
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, idx->ev0, idx->ev1) == hipSuccess) idx->stats.last_select_ms = ms;
+    }
     *out = idx->stats;
+    out->replayed_queries = idx->stats.replayed_queries + dev_replays;
     return WV_OK;
 }
 
@@ -1745,6 +1857,133 @@ extern "C" int wv_index_rq_distances(wv_index* idx, const float* queries, int64_
     return WV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// exact search on the block-key path (qs_kernels.hip).
+// Queries already prepared (idx->qn, qn2).  Outputs [nq][kout]; mode 1 leaves
+// flags (nonzero = not proven) for the caller, mode 0 replays them.  No host
+// synchronisation: the eps inputs, flag lists and counts stay on the device.
+// ---------------------------------------------------------------------------
+static int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : 0; }
+
+static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid,
+                     uint64_t* o_ids, float* o_d, int32_t* o_n, int32_t* o_flags) {
+    const int kout = mode == 1 ? k + 1 : k;
+    const int NK = idx->dpb / 16;
+    const int RB = qs_rb(NK);
+    const int R = qs_R(k);
+    const int L = 64 * (R - 1);
+    const int64_t nslots = std::max<int64_t>(1, (idx->hiwater + 32 * RB - 1) / (32 * RB));
+    const int64_t nb = nslots * RB;  // 32-row blocks scanned = key row length
+    const int64_t ldk = nb;
+    // query chunks of 256-multiples whose key rows fit 4 GiB
+    const int64_t qmax = std::max<int64_t>(QS_QPB, ((4ll << 30) / (ldk * 4)) / QS_QPB * QS_QPB);
+    const int64_t qc = std::min<int64_t>(round_up(nq, QS_QPB), qmax);
+    HIPCHK(idx->qsQb.ensure((size_t)qc * idx->dpb * sizeof(uint16_t)));
+    HIPCHK(idx->qsInfo.ensure((size_t)qc * sizeof(float4)));
+    HIPCHK(idx->qsKey.ensure((size_t)qc * ldk * sizeof(float)));
+    HIPCHK(idx->qsCand.ensure((size_t)qc * L * sizeof(uint32_t)));
+    HIPCHK(idx->qsNc.ensure((size_t)qc * sizeof(int32_t)));
+    HIPCHK(idx->qsEps.ensure((size_t)qc * sizeof(float)));
+    HIPCHK(idx->qsList.ensure((size_t)qc * sizeof(int32_t)));
+    if (!o_flags) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
+    const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16;
+    if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
+    // error-bound constants: reference-order fp32 (gamma_{dpb+8}) and the MFMA's
+    // fp32 accumulation over NK chained 16-deep products (u' = 2^-22)
+    const double u4 = 2.384185791015625e-07;
+    const double hdep = NK + 16.0;
+    const float gacc = (float)(hdep * u4 / (1.0 - hdep * u4));
+    const float gd = (float)gamma_n(idx->dpb + 8);
+    const int metric = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+    const bool v5 = idx->variant == WV_VARIANT_AVX512;
+    const float* Qn_all = idx->qn.as<float>();
+    idx->timed = 0;
+    for (int64_t c0 = 0; c0 < nq; c0 += qc) {
+        const int64_t cn = std::min<int64_t>(qc, nq - c0);
+        const int64_t cn_pad = round_up(cn, QS_QPB);
+        const float* Qn = Qn_all + c0 * idx->dpad;
+        float4* qinfo = idx->qsInfo.as<float4>();
+        k_query_split<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dpb, cn, cn_pad,
+                                                                   idx->qsQb.as<uint16_t>(), qinfo);
+        // ---- block keys (the dominant kernel) ----
+        QsArgs a;
+        a.Xb = reinterpret_cast<const unsigned char*>(idx->Xb);
+        a.xnorm2 = idx->xnorm2;
+        a.valid = valid;
+        a.Qb = reinterpret_cast<const unsigned char*>(idx->qsQb.p);
+        a.key = idx->qsKey.as<float>();
+        a.ldk = ldk;
+        a.nslots = nslots;
+        a.nqg = (int)(cn_pad / QS_QPB);
+        int64_t nspans = 256 / std::gcd(256, a.nqg);
+        while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
+        if (idx->spans_opt > 0) nspans = idx->spans_opt;
+        nspans = std::max<int64_t>(1, std::min<int64_t>(nspans, nslots));
+        const int64_t sps = (nslots + nspans - 1) / nspans;
+        a.slots_per_span = (int)sps;
+        a.nspans = (int)((nslots + sps - 1) / sps);
+        const bool l2 = metric == L2;
+        const size_t lds = (size_t)QS_NBUF * RB * NK * 1024 + (l2 ? (size_t)QS_NBUF * RB * 128 : 0);
+        dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
+        const bool time_it = idx->timing && c0 == 0;
+        if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
+#define WV_QS(NKV, L2V)                                                                                        \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_qs_blockkey<NKV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_qs_blockkey<NKV, L2V><<<grid, 512, lds, s>>>(a);                                                     \
+    } while (0)
+#define WV_QSN(L2V)                                    \
+    switch (NK) {                                      \
+    case 8: WV_QS(8, L2V); break;                      \
+    case 16: WV_QS(16, L2V); break;                    \
+    case 24: WV_QS(24, L2V); break;                    \
+    case 32: WV_QS(32, L2V); break;                    \
+    case 40: WV_QS(40, L2V); break;                    \
+    default: WV_QS(48, L2V); break;                    \
+    }
+        if (l2) { WV_QSN(true); } else { WV_QSN(false); }
+#undef WV_QSN
+#undef WV_QS
+        HIPCHK(hipGetLastError());
+        if (time_it) { HIPCHK(hipEventRecord(idx->ev1, s)); idx->timed = 1; }
+        idx->stats.mfma_launches++;
+        // ---- candidate blocks, exact rows, proof ----
+        int32_t* flags = o_flags ? o_flags + c0 : idx->qsFlags.as<int32_t>();
+        const unsigned gw = (unsigned)((cn + 3) / 4);
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>())
+        if (R == 2) WV_SELR(2); else if (R == 4) WV_SELR(4); else WV_SELR(8);
+#undef WV_SELR
+#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<gw, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags)
+#define WV_EXM(RV)                                                          \
+    switch (metric) {                                                       \
+    case L2: if (v5) WV_EXR(RV, L2, AVX512); else WV_EXR(RV, L2, AVX256); break;   \
+    case DOT: if (v5) WV_EXR(RV, DOT, AVX512); else WV_EXR(RV, DOT, AVX256); break; \
+    default: if (v5) WV_EXR(RV, COSINE, AVX512); else WV_EXR(RV, COSINE, AVX256); break; \
+    }
+        if (R == 2) { WV_EXM(2); } else if (R == 4) { WV_EXM(4); } else { WV_EXM(8); }
+#undef WV_EXM
+#undef WV_EXR
+        HIPCHK(hipGetLastError());
+        if (mode == 1) continue;
+        // ---- flagged queries: the exact heap replay, bounded by the block keys ----
+        HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
+        k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount);
+#define WV_RP(M, V)                                                                                             \
+    do {                                                                                                        \
+        if (rlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); \
+        k_blk_replay<M, V><<<(unsigned)cn, 64, rlds, s>>>(a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsList.as<int32_t>(), idx->qscount, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0); \
+    } while (0)
+        switch (metric) {
+        case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;
+        case DOT: if (v5) WV_RP(DOT, AVX512); else WV_RP(DOT, AVX256); break;
+        default: if (v5) WV_RP(COSINE, AVX512); else WV_RP(COSINE, AVX256); break;
+        }
+#undef WV_RP
+        HIPCHK(hipGetLastError());
+    }
+    return WV_OK;
+}
+
 // Core batch search on device queries.  Outputs [nq][kout] device arrays.
 // mode 0: kout = k, flagged queries resolved by replay; mode 1: kout = k+1,
 // flags left for the caller.  n_valid = number of scan candidates.
@@ -1778,6 +2017,13 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
     if (rc) return rc;
     const float* Qn = idx->qn.as<float>();
+    // block-key path (default): planes built, finite corpus, list sizes that fit
+    if (idx->qs_planes && !idx->has_nonfinite && (idx->kernel_opt == 0 || idx->kernel_opt == 7) && !idx->force_replay &&
+        qs_R(k) > 0 && idx->metric != WV_METRIC_HAMMING) {
+        idx->stats.queries += (uint64_t)nq;
+        idx->stats.batches++;
+        return search_qs(idx, s, nq, k, mode, valid, o_ids, o_d, o_n, o_flags);
+    }
     const int KP = k + idx->margin;
     const bool mfma_ok = KP <= 32 && idx->metric != WV_METRIC_HAMMING && !idx->force_replay;
     idx->stats.queries += (uint64_t)nq;
@@ -1787,7 +2033,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     int32_t* flags = o_flags ? o_flags : idx->oF.as<int32_t>();
 
     if (mfma_ok) {
-        int kver = idx->kernel_opt;
+        int kver = idx->kernel_opt == 7 ? 0 : idx->kernel_opt;
         if (kver == 0) kver = nq <= idx->gemv_max ? 6 : idx->use_bf3 ? (nq > QB ? 5 : 4) : 3;
         if ((kver == 4 || kver == 5) && !idx->use_bf3) kver = 3;
         const bool gemv = kver == 6;
