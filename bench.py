@@ -5,11 +5,12 @@ Workload (BASELINE.json configs[2], the config north_star's target is quoted
 on): 10M x 768 fp32 vectors, cosine ("cosine-dot"), k = 10, corpus sharded
 over the N GPUs of one node by contiguous doc-id ranges (N=1: the whole 10M
 corpus on one GPU).  One step = one batch of B queries through the full
-SearchByVector pipeline (query normalisation, fused MFMA distance + top-k
-selection, exact-order rescoring, exactness proof, heap replay of any flagged
-query, and for N>1 the RCCL all-gather + merge).  Inputs are synthetic
-(counter-based generator, identical on CPU and GPU) and resident in HBM before
-timing starts.
+SearchByVector pipeline (query normalisation, bf16 block-key MFMA pass,
+candidate-block selection, exact-order distances of the candidate rows,
+exactness proof, bounded heap replay of any flagged query, and for N>1 the
+RCCL all-gather + merge).  Inputs are synthetic (counter-based generator,
+identical on CPU and GPU) and resident in HBM before timing starts.
+--workload c1 / c2 run BASELINE configs[0] / [1] the same way.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -34,6 +35,16 @@ K = 10
 SEED_CORPUS = 1
 SEED_QUERY = 2
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+# exact flat workloads: BASELINE configs[0] (c1), [1] (c2), [2] (c3, the headline)
+FLAT = {
+    "c1": dict(n=100_000, d=128, metric="l2-squared", k=10, batch=1000, kind=0,
+               name="Flat index exact kNN, 100k x 128 U(-1,1) fp32, l2-squared, k=10, 1k queries (BASELINE configs[0])"),
+    "c2": dict(n=1_000_000, d=128, metric="l2-squared", k=100, batch=10_000, kind=1,
+               name="SIFT-shaped 1M x 128 integer-valued fp32 U{0..127}, l2-squared, k=100, 10k-query batch "
+                    "(BASELINE configs[1])"),
+    "c3": dict(n=10_000_000, d=768, metric="cosine", k=10, batch=2048, kind=0,
+               name="10M x 768 fp32 cosine, k=10, exact flat search (BASELINE configs[2])"),
+}
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (spec, MI355X_MICROARCH.md)
 # 32-bit integer VALU lane-ops/s: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  The
 # 32-lane/clk rate (78.6 T) is the f32 FMA rate; v_xor_b32 / v_bcnt_u32_b32 issue
@@ -61,31 +72,61 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n_sample: int, nq: int, threads: int):
-    """Reference CPU flat scan on the host cores: the reference's own AVX2 dot
-    kernel (oracle/_ref, compiled from /root/reference) when the host can run
-    it, else the oracle's scalar restatement; one query per thread."""
+def host_info() -> dict:
+    """nproc (CPUs this process may run on), the CPU model, and the kernel
+    variant the reference would pick on this host: AVX-512 only with
+    AMX-BF16 && AVX512 (distancer/l2_amd64.go:19-26), else AVX2."""
+    nproc = len(os.sched_getaffinity(0))
+    model, flags = "", ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name") and not model:
+                model = line.split(":", 1)[1].strip()
+            if line.startswith("flags") and not flags:
+                flags = line + " "
+    except OSError:
+        pass
+    variant = "avx512" if (" amx_bf16 " in flags and " avx512f " in flags) else "avx256"
+    return {"nproc": nproc, "cpu_model": model, "variant": variant}
+
+
+def cpu_baseline(n_sample: int, nq: int, threads: int, spec=None):
+    """Reference CPU flat scan on the host cores: the reference's own SIMD
+    kernels (oracle/_ref, compiled from /root/reference) when the host can run
+    them, else the oracle's scalar restatement; one query per thread, the
+    kernel variant the reference's dispatch rule picks on this host."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc  # test infrastructure, used only for this baseline leg
+    spec = spec or FLAT["c3"]
+    info = host_info()
     use_ref = orc.ref_lib() is not None and orc.host_has_avx512()
-    corpus = orc.gen_matrix(0, SEED_CORPUS, 0, n_sample, DIMS)
-    orc.lib().or_normalize_rows(orc.f(corpus), n_sample, DIMS)
-    queries = orc.gen_matrix(0, SEED_QUERY, 0, nq, DIMS)
-    orc.lib().or_normalize_rows(orc.f(queries), nq, DIMS)
+    d, k, kind = spec["d"], spec["k"], spec["kind"]
+    metric = orc.METRIC[spec["metric"]]
+    variant = orc.AVX512 if info["variant"] == "avx512" else orc.AVX256
+    corpus = orc.gen_matrix(kind, SEED_CORPUS, 0, n_sample, d)
+    queries = orc.gen_matrix(kind, SEED_QUERY, 0, nq, d)
+    if metric == orc.COSINE:
+        orc.lib().or_normalize_rows(orc.f(corpus), n_sample, d)
+        orc.lib().or_normalize_rows(orc.f(queries), nq, d)
     t0 = time.perf_counter()
-    orc.cpu_baseline(orc.COSINE, orc.AVX256, corpus, queries, K, threads, use_ref)
+    orc.cpu_baseline(metric, variant, corpus, queries, k, threads, use_ref)
     dt = time.perf_counter() - t0
     qps_sample = nq / dt
     # the scan is linear in N: extrapolate to the full corpus
-    qps_full = qps_sample * n_sample / N_TOTAL
+    qps_full = qps_sample * n_sample / spec["n"]
+    kname = ("l2" if metric == orc.L2 else "dot") + ("_512" if variant == orc.AVX512 else "_256")
     return {
         "value": qps_full,
         "unit": "queries/s",
         "cores": threads,
         "kind": "reference" if use_ref else "port",
-        "sample": (f"{nq} queries x {n_sample} rows (first rows of the same corpus), cosine k=10, "
-                   f"{'reference dot_256 AVX2 kernel (oracle/_ref)' if use_ref else 'oracle scalar restatement'} "
-                   f"+ NewMax heap scan, {dt:.1f} s, QPS scaled by {n_sample}/{N_TOTAL}"),
+        "nproc": info["nproc"],
+        "cpu_model": info["cpu_model"],
+        "variant": info["variant"],
+        "sample": (f"{nq} queries x {n_sample} rows (first rows of the same corpus), {spec['metric']} k={k}, "
+                   f"{'reference ' + kname + ' kernel (oracle/_ref)' if use_ref else 'oracle scalar restatement'} "
+                   f"+ NewMax heap scan, {threads} threads, {dt:.1f} s"
+                   + (f", QPS scaled by {n_sample}/{spec['n']}" if n_sample != spec["n"] else "")),
     }
 
 
@@ -184,8 +225,9 @@ def measured_traffic(workload: str, n_local: int, dims: int, batch: int, kernel:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c3", "bq", "pq", "rq8", "rq1"], default="c3",
-                    help="c3: 10M x 768 cosine exact (default, the headline); bq: BQ 1536-d shard of configs[3]; "
+    ap.add_argument("--workload", choices=["c3", "c1", "c2", "bq", "pq", "rq8", "rq1"], default="c3",
+                    help="c3: 10M x 768 cosine exact (default, the headline); c1 / c2: BASELINE configs[0] / [1]; "
+                         "bq: BQ 1536-d shard of configs[3]; "
                          "pq: configs[4] PQ 10M x 960 (k-means fit timed once, ADC search timed per step); "
                          "rq8 / rq1: flat's rotational quantizers on the c3 corpus, R=200 rescoring")
     ap.add_argument("--gpus", type=int, default=1)
@@ -196,10 +238,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-queries", type=int, default=None)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None, help="default: nproc (all CPUs this process may use)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per k_mfma_select launch from the rocprofv3 PMC pass")
     args = ap.parse_args()
+    if args.cpu_threads is None:
+        args.cpu_threads = len(os.sched_getaffinity(0))
 
     import torch
     import torch.distributed as dist
@@ -221,21 +265,26 @@ def main():
     bq = args.workload == "bq"
     pq = args.workload == "pq"
     rq_bits = {"rq8": 8, "rq1": 1}.get(args.workload, 0)
+    flat = FLAT.get(args.workload)  # exact fp32 flat search (c1 / c2 / c3)
     if (pq or rq_bits) and world > 1:
         raise SystemExit(f"--workload {args.workload}: sharded search is not available yet (1 GPU)")
-    dims = BQ_DIMS if bq else PQ_DIMS if pq else DIMS
-    # c3 / pq: a fixed corpus split over the ranks (strong scaling); bq: configs[3]
+    dims = BQ_DIMS if bq else PQ_DIMS if pq else flat["d"] if flat else DIMS
+    K_ = flat["k"] if flat else K
+    # flat / pq: a fixed corpus split over the ranks (strong scaling); bq: configs[3]
     # is 50M rows over 8 GPUs, i.e. a 6.25M-row shard per GPU (weak scaling)
-    n_total = args.n if args.n is not None else (BQ_ROWS_PER_GPU * world if bq else PQ_ROWS if pq else N_TOTAL)
+    n_total = args.n if args.n is not None else (BQ_ROWS_PER_GPU * world if bq else PQ_ROWS if pq
+                                                 else flat["n"] if flat else N_TOTAL)
     n_local = (n_total + world - 1) // world
     id0 = rank * n_local
     n_local = max(0, min(n_local, n_total - id0))
-    B = args.batch if args.batch is not None else (256 if pq else 2048)
-    gen_kind = 2 if pq else 0  # GIST-shaped U[0,1) for PQ, U[-1,1) otherwise
+    B = args.batch if args.batch is not None else (256 if pq else flat["batch"] if flat else 2048)
+    # GIST-shaped U[0,1) for PQ, SIFT-shaped integers for c2, U[-1,1) otherwise
+    gen_kind = 2 if pq else flat["kind"] if flat else 0
+    metric_name = "l2-squared" if pq else flat["metric"] if flat else "cosine"
 
     # ---- build the shard: generate + add in 1M-row chunks (device resident) ----
     t_build = time.perf_counter()
-    index = wv.FlatIndex(distance="l2-squared" if pq else "cosine", dims=dims, device=local_rank, variant="avx256", id_base=id0,
+    index = wv.FlatIndex(distance=metric_name, dims=dims, device=local_rank, variant="avx256", id_base=id0,
                          bq=bq, rescore_limit=BQ_RESCORE if (bq or rq_bits) else -1,
                          rq={"bits": rq_bits} if rq_bits else None,
                          pq={"segments": PQ_SEGMENTS, "centroids": PQ_CENTROIDS, "trainingLimit": PQ_TRAIN,
@@ -263,8 +312,8 @@ def main():
             f"{n_local} rows: {fit_s:.2f} s")
     index.set_option("timing", 1)
 
-    out_ids = torch.empty((B, K), dtype=torch.int64, device=dev)
-    out_d = torch.empty((B, K), dtype=torch.float32, device=dev)
+    out_ids = torch.empty((B, K_), dtype=torch.int64, device=dev)
+    out_d = torch.empty((B, K_), dtype=torch.float32, device=dev)
     out_n = torch.empty(B, dtype=torch.int32, device=dev)
 
     if world > 1 and bq:
@@ -272,17 +321,17 @@ def main():
         searcher = ShardedBQSearch(GpuBQShardBackend(index, local_rank), dev, (n_total + world - 1) // world)
 
         def step():
-            return searcher.search(queries, K)
+            return searcher.search(queries, K_)
     elif world > 1:
         from weaviate_amd.sharded import GpuShardBackend, ShardedFlatSearch
         searcher = ShardedFlatSearch(GpuShardBackend(index, local_rank), dev)
 
         def step():
-            return searcher.search(queries, K)
+            return searcher.search(queries, K_)
     else:
         def step():
             s = torch.cuda.current_stream(dev).cuda_stream
-            _lib.check(lib.wv_index_search_device(index._h, queries.data_ptr(), B, dims, K, 0, out_ids.data_ptr(),
+            _lib.check(lib.wv_index_search_device(index._h, queries.data_ptr(), B, dims, K_, 0, out_ids.data_ptr(),
                                                   out_d.data_ptr(), out_n.data_ptr(), None, s))
 
     for _ in range(args.warmup):
@@ -291,12 +340,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    sel_ms = []
+    sel_ms, tot_ms = [], []
     replays0 = index.stats()["replayed_queries"]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        sel_ms.append(index.stats()["last_select_ms"])
+        st = index.stats()
+        sel_ms.append(st["last_select_ms"])
+        tot_ms.append(st["last_total_ms"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -316,8 +367,9 @@ def main():
     total_q = B * args.steps
     value = total_q / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    # the fp32 path's select kernel: 256 x 256 tiles above 128 queries (runtime.hip auto choice)
-    sel_kernel = "k_mfma_select_bf3w" if B > 128 else "k_gemv_select" if B <= GEMV_MAX else "k_mfma_select_bf3"
+    # the exact fp32 path's dominant kernel: the bf16 block-key pass (runtime.hip auto choice)
+    sel_kernel = "k_qs_blockkey"
+    total_avg = float(np.mean(tot_ms)) if tot_ms else 0.0
     if args.traffic_bytes is None:
         args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B,
                                               None if (pq or bq or rq_bits) else sel_kernel)
@@ -361,30 +413,20 @@ def main():
                 "unit": "Tops/s (int32 lane-ops)", "frac": achieved / VALU_PEAK_TOPS, "launch_ms": sel_avg,
                 "hbm_GBps": n_local * words * 8 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
                 "traffic": args.traffic_bytes}
-    elif sel_kernel == "k_gemv_select":
-        # batches <= GEMV_MAX queries: the HBM-streaming GEMV (runtime.hip,
-        # gemv_kernels.hip) -- algorithmic bytes per launch = one pass over the
-        # shard's fp32 rows (N_local x d x 4 B) + the queries, over its measured
-        # average duration (HIP events on its stream)
-        nbytes = float(n_local) * dims * 4 + B * dims * 4
-        achieved = nbytes / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0
-        roof = {"bound": "hbm", "kernel": sel_kernel, "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "launch_ms": sel_avg,
-                "traffic": args.traffic_bytes}
     else:
-        # roofline of the dominant kernel (k_mfma_select_bf3w): algorithmic flops
-        # per launch = 2 * B * n_local * d (one FMA per element pair), over its
-        # measured average duration (HIP events on the stream it runs on).  The
-        # kernel computes each fp32 product as 3 bf16 MFMA products (bf16x3
-        # split), so its peak for this work is the dense bf16
-        # MFMA peak / 3.
+        # roofline of the dominant kernel (k_qs_blockkey): one
+        # bf16 MFMA product per (query, row, dim): algorithmic flops per launch
+        # = 2 * B * n_local * d, over its measured average duration (HIP events
+        # on the stream it runs on), against the dense bf16 MFMA peak.
         flops = 2.0 * B * n_local * dims
         achieved = flops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
-        peak = MFMA_BF16_PEAK_TFLOPS / 3.0
+        peak = MFMA_BF16_PEAK_TFLOPS
         roof = {"bound": "mfma", "kernel": sel_kernel, "achieved": achieved, "peak": peak,
-                "unit": "TFLOP/s (fp32-product equivalent)", "frac": achieved / peak, "launch_ms": sel_avg,
-                "mfma": "v_mfma_f32_32x32x16_bf16, 3 per fp32 product (hi*hi + hi*lo + lo*hi)",
-                "executed_bf16_tflops": 3.0 * achieved, "f32_mfma_peak_equivalent_frac": achieved / MFMA_F32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": achieved / peak, "launch_ms": sel_avg,
+                "mfma": "v_mfma_f32_32x32x16_bf16 (bf16 in, fp32 accumulate): block keys = per-32-row minima of "
+                        "the approximate distance; every returned distance is the reference-order fp32 value",
+                "pipeline_ms": total_avg,
+                "f32_mfma_peak_equivalent_frac": achieved / MFMA_F32_PEAK_TFLOPS,
                 "traffic": args.traffic_bytes}
 
     result = None
@@ -402,7 +444,12 @@ def main():
                     cpu = cpu_baseline_bq(min(args.cpu_rows, n_total), args.cpu_queries or 4096, args.cpu_threads,
                                           n_total)
                 else:
-                    cpu = cpu_baseline(min(args.cpu_rows, n_total), args.cpu_queries or 1024, args.cpu_threads)
+                    spec = dict(flat)
+                    spec["n"] = n_total
+                    # c1 is small enough to time in full (every query, every row)
+                    rows = n_total if args.workload == "c1" else min(args.cpu_rows, n_total)
+                    nqc = args.cpu_queries or (B if args.workload == "c1" else 1024)
+                    cpu = cpu_baseline(rows, nqc, args.cpu_threads, spec)
             except Exception as e:  # baseline failure must not hide the GPU number
                 log(f"cpu baseline failed: {e}")
         if rq_bits:
@@ -415,7 +462,7 @@ def main():
             workload = (f"BQ {dims}-d cosine, k={K}, rescore R={BQ_RESCORE}: one {n_total}-row shard of "
                         "BASELINE configs[3] (50M x 1536 over 8 GPUs)")
         else:
-            workload = "10M x 768 fp32 cosine, k=10, exact flat search (BASELINE configs[2])"
+            workload = flat["name"]
         result = {
             "metric": METRIC,
             "value": value,
@@ -429,13 +476,16 @@ def main():
             "vs_baseline": None,
             "dtype": ("u8 codes (v_dot4) + f32 rescoring" if rq_bits == 8 else
                       "u64 codes x 5-bit query planes + f32 rescoring" if rq_bits == 1 else
-                      "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else "f32"),
-            "data": "synthetic (counter-based U[-1,1) generator, seed 1 corpus / 2 queries)",
+                      "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else
+                      "f32 (exact result; bf16 MFMA block-key filter)"),
+            "data": ("synthetic (counter-based integer U{0..127} generator, seed 1 corpus / 2 queries)" if gen_kind == 1
+                     else "synthetic (counter-based U[0,1) generator, seed 1 corpus / 2 queries)" if gen_kind == 2
+                     else "synthetic (counter-based U[-1,1) generator, seed 1 corpus / 2 queries)"),
             "config": {
                 "workload": workload,
                 "corpus_rows": n_total,
                 "dims": dims,
-                "k": K,
+                "k": K_,
                 "query_batch": B,
                 "parallelism": f"corpus sharded over {world} GPU(s), contiguous id ranges"
                                + ((", R-heap replay chained over RCCL broadcasts + all-gather rescoring" if bq

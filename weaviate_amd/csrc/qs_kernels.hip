@@ -53,6 +53,7 @@ struct QsArgs {
     int slots_per_span;
     int nspans;
     int nqg;                   // query groups of 256
+    int dbg;                   // reserved for timing experiments
 };
 
 __device__ __forceinline__ uint32_t sload_u32(const void* p) {
@@ -77,11 +78,13 @@ __device__ __forceinline__ void qs_wait_vm(int y) {
 }
 
 template <int N>
+__device__ __forceinline__ void qs_wait_vm_c() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int N>
 __device__ __forceinline__ void qs_wait_lgkm() {
-    if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else if constexpr (N == 1) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
-    else if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
 }
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
@@ -99,7 +102,10 @@ __device__ __forceinline__ f32x4_t lds_ld4f_o(unsigned base) {
 // with S = sum_k bf16(q_k) bf16(x_k) (fp32 MFMA accumulation); a block with no
 // valid row gets +inf.
 // ---------------------------------------------------------------------------
-template <int NK, bool ISL2>
+// DBG (timing experiments only, never the product path): bit 0 drops the
+// MFMAs, bit 1 the LDS-DMA pieces (every wait then vmcnt(0)), bit 2 the
+// A-fragment LDS reads of the one-block schedule
+template <int NK, bool ISL2, int DBG = 0>
 __global__ __launch_bounds__(512, 2) void k_qs_blockkey(QsArgs a) {
     constexpr int RB = qs_rb(NK);
     constexpr int SLOT = RB * NK * 1024;        // bytes per ring slot
@@ -118,10 +124,26 @@ __global__ __launch_bounds__(512, 2) void k_qs_blockkey(QsArgs a) {
     const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
     const int span = logical / a.nqg, grp = logical % a.nqg;
 
-    // this wave's 32 queries as MFMA B fragments for all of d: lane (li, lh)
-    // holds query wave*32+li, columns 16c + 8lh .. +7 of chunk c
+    // One 32-row block per slot (d > 384) runs the 16x16x32 schedule below
+    // (IL), smaller d the 32x32x16 schedule with several blocks per slot.
+    constexpr bool IL = RB == 1;
+    // this wave's 32 queries as MFMA B fragments for all of d.
+    //  32x32x16: Qf[c] for 16-column chunk c: lane (li, lh) holds query
+    //            wave*32+li, columns 16c + 8lh .. +7;
+    //  16x16x32: Qf[2c+n] for 32-column chunk c and query half n: lane
+    //            (j = lane&15, kq = lane>>4) holds query wave*32+16n+j,
+    //            columns 32c + 8kq .. +7.
     bf16x8_t Qf[NK];
-    {
+    if constexpr (IL) {
+        const int j = lane & 15, kq = lane >> 4;
+        const unsigned char* qp =
+            a.Qb + (int64_t)grp * TILE_B + (kq >> 1) * 8192 + (wave * 32 + j) * 32 + 16 * (kq & 1);
+#pragma unroll
+        for (int c = 0; c < NK / 2; c++)
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                Qf[2 * c + n] = *reinterpret_cast<const bf16x8_t*>(qp + (2 * c) * 8192 + n * 16 * 32);
+    } else {
         const unsigned char* qp = a.Qb + (int64_t)grp * TILE_B + (wave * 32 + li) * 32 + 16 * lh;
 #pragma unroll
         for (int c = 0; c < NK; c++) Qf[c] = *reinterpret_cast<const bf16x8_t*>(qp + c * 8192);
@@ -138,60 +160,254 @@ __global__ __launch_bounds__(512, 2) void k_qs_blockkey(QsArgs a) {
     // LDS-DMA: lane L writes bytes [16L, 16L+16) of a 1 KiB piece = row L>>1,
     // physical half L&1, holding source half (L&1) ^ ((row>>3)&1): the
     // 16-lane groups of ds_read_b128 are then conflict-free
+    // (the 16x16x32 schedule reads the image unswizzled: its 16-lane groups
+    // are conflict-free on the linear layout)
     const int prow = lane >> 1;
-    const uint32_t src_lane = (uint32_t)(prow * 32 + 16 * ((lane & 1) ^ ((prow >> 3) & 1)));
+    const uint32_t src_lane = IL ? (uint32_t)(16 * lane) : (uint32_t)(prow * 32 + 16 * ((lane & 1) ^ ((prow >> 3) & 1)));
     const unsigned ring = lds_addr(qsm);
-    const unsigned xnring = ring + QS_NBUF * SLOT;  // L2: [NBUF][RB*32] floats
-    const int P0 = P + ((ISL2 && wave == 0) ? 1 : 0);
+    // per-wave rings with 4 entries (step & 3: never the entry being refilled
+    // while an epilogue reads it): valid words [8][4][4] u32, L2 norms
+    // [8][4][RB*32] floats.  Every wave loads its own copy, so every wave
+    // issues the same number of vector-memory ops per step (one compile-time
+    // vmcnt for the steady state).
+    const unsigned vring = ring + QS_NBUF * SLOT + (unsigned)wave * 64u;
+    const unsigned xnring = ring + QS_NBUF * SLOT + 512u + (unsigned)wave * (unsigned)(4 * RB * 128);
+    constexpr int P0 = P + (ISL2 ? 2 : 1);  // vector-memory ops per step group, per wave
     // the span's rows through one buffer resource (the host keeps a span's
     // plane bytes below 4 GiB): per piece an SGPR offset + the lane's VGPR
     const int64_t tile0 = (s0 * RB * 32) >> 8;
     const __amdgpu_buffer_rsrc_t xrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.Xb + tile0 * TILE_B), (short)0, -1, 0x00020000);
-    auto issue = [&](int64_t gs, int slot) {
+    // piece i of this wave: block rb_i of the slot, k chunk c_i -> source
+    // offset K_i from the slot's first block, LDS offset Ld_i in the slot
+    // source offset of the next group to issue: ((gb>>3) - tile0) * TILE_B + (gb&7) * 1024
+    int64_t igb = s0 * RB;
+    uint32_t ioff = (uint32_t)(((igb >> 3) - tile0) * TILE_B + (igb & 7) * 1024);
+    auto issue = [&](int t, int slot) {
         const unsigned sb = ring + (unsigned)(slot * SLOT);
 #pragma unroll
         for (int i = 0; i < P; i++) {
             const int p = wave + 8 * i;
             const int rb = p / NK, c = p % NK;
-            const int64_t gb = gs * RB + rb;
-            const uint32_t so = (uint32_t)(((gb >> 3) - tile0) * TILE_B + (int64_t)c * 8192 + (gb & 7) * 1024);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(size_t)(sb + (unsigned)((rb * NK + c) * 1024)), 16,
-                                                     src_lane, so, 0, 0);
+                                                     src_lane, ioff + (uint32_t)(rb * 1024 + c * 8192), 0, 0);
         }
-        if (ISL2 && wave == 0) {
-            if (lane < RB * 8)
-                __builtin_amdgcn_global_load_lds(a.xnorm2 + gs * RB * 32 + 4 * lane,
-                                                 (lds_ptr_t)(size_t)(xnring + (unsigned)(slot * RB * 128)), 16, 0, 0);
-        }
+        if (lane < RB)
+            __builtin_amdgcn_global_load_lds(a.valid + igb + lane, (lds_ptr_t)(size_t)(vring + (unsigned)((t & 3) * 16)), 4, 0, 0);
+        if (ISL2 && lane < RB * 8)
+            __builtin_amdgcn_global_load_lds(a.xnorm2 + igb * 32 + 4 * lane,
+                                             (lds_ptr_t)(size_t)(xnring + (unsigned)((t & 3) * RB * 128)), 16, 0, 0);
+        igb += RB;
+        ioff += RB * 1024;
+        if ((igb & 7) == 0) ioff += (uint32_t)(TILE_B - 8192);
     };
-
-    if (nsteps > 0) issue(s0, 0);
-    if (nsteps > 1) issue(s0 + 1, 1);
 
     const unsigned lane_off = (unsigned)(li * 32 + 16 * (lh ^ ((li >> 3) & 1)));
     const int64_t qrow = (int64_t)grp * QS_QPB + wave * 32 + li;
     float* krow = a.key + qrow * a.ldk;
-    int slot = 0;
-    for (int step = 0; step < nsteps; step++) {
-        // ops issued after slot `step`'s pieces: the stores of the two
-        // previous steps and slot step+1's pieces (issue order, vmcnt counts both)
-        const int y = (step >= 1 ? RB : 0) + (step >= 2 ? RB : 0) + (step + 1 < nsteps ? P0 : 0);
-        qs_wait_vm(y);
-        __builtin_amdgcn_s_barrier();  // every wave's pieces of this slot landed; slot step+2 is free
+    bf16x8_t A[4];
+    if (nsteps > 0) {
+        issue(0, 0);
+        if (nsteps > 1) issue(1, 1);
+        qs_wait_vm(nsteps > 1 ? P0 : 0);  // group 0 landed, group 1 may stay in flight
+        __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (step + 2 < nsteps) issue(s0 + step + 2, slot == 0 ? 2 : slot - 1);
-        const unsigned sb = ring + (unsigned)(slot * SLOT) + lane_off;
+        if constexpr (!IL) {  // the one-block schedule issues group 2 in its first chain
+            if (nsteps > 2) issue(2, 2);
+            const unsigned sb0 = ring + lane_off;
+            A[0] = lds_ld8bf_o<0>(sb0);
+            A[1] = lds_ld8bf_o<1024>(sb0);
+            A[2] = lds_ld8bf_o<2048>(sb0);
+            A[3] = lds_ld8bf_o<3072>(sb0);
+        }
+    }
+    // ---------------------------------------------------------------------
+    // One 32-row block per slot (d > 384): the epilogue of block t-1 and the
+    // DMA of group t+2 run as fillers between block t's MFMAs, so the matrix
+    // pipe never waits for them; one barrier per block.
+    // ---------------------------------------------------------------------
+    // ---------------------------------------------------------------------
+    // One 32-row block per slot (d > 384), v_mfma_f32_16x16x32_bf16: per
+    // 32-column chunk c, two row halves m x two query halves n.  The DMA of
+    // group t+2 and the previous block's key store run as fillers between
+    // block t's MFMAs; one barrier per block.
+    // ---------------------------------------------------------------------
+    if constexpr (IL) {
+        constexpr int NC = NK / 2;
+        // lane (i = lane&15, kq = lane>>4) reads row 16m+i, columns 32c+8kq..+7
+        // = piece 2c + (kq>>1), half kq&1 of the linear image
+        const unsigned l16 = (unsigned)(((lane >> 5) & 1) * 1024 + (lane & 15) * 32 + 16 * ((lane >> 4) & 1));
+        auto issue_piece = [&](int j, int t, int slot) {
+            if (j < P) {
+                if constexpr (DBG & 2) return;
+                const int c = wave + 8 * j;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(size_t)(ring + (unsigned)(slot * SLOT + c * 1024)),
+                                                         16, src_lane, ioff + (uint32_t)(c * 8192), 0, 0);
+            } else if (j == P) {
+                if (lane == 0)
+                    __builtin_amdgcn_global_load_lds(a.valid + igb, (lds_ptr_t)(size_t)(vring + (unsigned)((t & 3) * 16)), 4,
+                                                     0, 0);
+            } else {
+                if (lane < 8)
+                    __builtin_amdgcn_global_load_lds(a.xnorm2 + igb * 32 + 4 * lane,
+                                                     (lds_ptr_t)(size_t)(xnring + (unsigned)((t & 3) * 128)), 16, 0, 0);
+            }
+            if (j == P0 - 1) {
+                igb += 1;
+                ioff += 1024;
+                if ((igb & 7) == 0) ioff += (uint32_t)(TILE_B - 8192);
+            }
+        };
+        bf16x8_t B2[2][2];  // A fragments [chunk & 1][m]
+        if (nsteps > 0) {
+            const unsigned sb0 = ring + l16;
+            B2[0][0] = lds_ld8bf_o<0>(sb0);
+            B2[0][1] = lds_ld8bf_o<512>(sb0);
+        }
+        // per query half n: the block's key before the cross-lane combine
+        float mp0 = 0.f, mp1 = 0.f;
+        int64_t gbp = 0;
+        int cur = 0;
+        auto finish = [&]() {
+            // lanes g*16 + j (g = 0..3) hold partial keys of query 16n + j
+            float m0 = mp0, m1 = mp1;
+            const auto a0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m0), __float_as_uint(m0), false, false);
+            const auto a1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
+            m0 = ISL2 ? fminf(m0, __uint_as_float(a0[1])) : fmaxf(m0, __uint_as_float(a0[1]));
+            m1 = ISL2 ? fminf(m1, __uint_as_float(a1[1])) : fmaxf(m1, __uint_as_float(a1[1]));
+            const auto b0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m0), false, false);
+            const auto b1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
+            m0 = ISL2 ? fminf(m0, __uint_as_float(b0[1])) : fmaxf(m0, __uint_as_float(b0[1]));
+            m1 = ISL2 ? fminf(m1, __uint_as_float(b1[1])) : fmaxf(m1, __uint_as_float(b1[1]));
+            // lanes 0-15: queries j (n = 0) in m0, 16 + j in m1 -> lanes 16-31 take m1
+            const auto c01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m1), false, false);
+            const float m = __uint_as_float(c01[0]);
+            if (lane < 32) krow[gbp] = ISL2 ? m : -m;
+        };
+        for (int t = 0; t < nsteps; t++) {
+            const int nxt = cur == QS_NBUF - 1 ? 0 : cur + 1;
+            const int gslot = cur == 0 ? QS_NBUF - 1 : cur - 1;  // slot of group t+2
+            const unsigned sb = ring + (unsigned)(cur * SLOT) + l16;
+            const bool dma = t + 2 < nsteps;
+            const unsigned sm = (unsigned)(t & 3);
+            f32x4_t acc[2][2];
+#pragma unroll
+            for (int m = 0; m < 2; m++)
+#pragma unroll
+                for (int n = 0; n < 2; n++) acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            uint32_t vwv = 0;
+            f32x4_t x0, x1;
+            // extra LDS reads (valid word, L2 norms) issued in chunk XC: the next
+            // chunk's wait leaves them in flight, later waits retire them
+            constexpr int XC = NC - 4;
+            constexpr int XE = ISL2 ? 3 : 1;
+            static_for<0, NC>([&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                if constexpr (c + 1 < NC && !(DBG & 4)) {
+                    B2[(c + 1) & 1][0] = lds_ld8bf_o<(2 * (c + 1)) * 1024>(sb);
+                    B2[(c + 1) & 1][1] = lds_ld8bf_o<(2 * (c + 1)) * 1024 + 512>(sb);
+                }
+                qs_wait_lgkm<(c + 1 < NC ? 2 : 0) + (c == XC + 1 ? XE : 0)>();
+                asm volatile("" : "+v"(B2[c & 1][0]), "+v"(B2[c & 1][1]));
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (!(DBG & 1)) {
+#pragma unroll
+                    for (int m = 0; m < 2; m++)
+#pragma unroll
+                        for (int n = 0; n < 2; n++)
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B2[c & 1][m], Qf[2 * c + n], acc[m][n], 0, 0, 0);
+                }
+                // DMA of group t+2: one piece per chunk
+                if constexpr (c < P0) {
+                    if (dma) issue_piece(c, t + 2, gslot);
+                }
+                // previous block: cross-lane combine + key store
+                if constexpr (c == P0 + 1) {
+                    if (t > 0) finish();
+                }
+                if constexpr (c == XC) {
+                    asm volatile("ds_read_b32 %0, %1" : "=v"(vwv) : "v"(vring + sm * 16u));
+                    if constexpr (ISL2) {
+                        // rows 4g..4g+3 and 16+4g..+3 of the block, g = lane>>4
+                        const unsigned xb = xnring + sm * 128u + (unsigned)(16 * ((lane >> 4) & 3));
+                        x0 = lds_ld4f_o<0>(xb);
+                        x1 = lds_ld4f_o<64>(xb);
+                    }
+                }
+            });
+            // retired by the chunk waits after XC + 1
+            if constexpr (ISL2) asm volatile("" : "+v"(vwv), "+v"(x0), "+v"(x1));
+            else asm volatile("" : "+v"(vwv));
+            {
+                const uint32_t vw = __builtin_amdgcn_readfirstlane(vwv);
+                // acc[m][n][r] is row 16m + 4g + r (g = lane>>4) of query 16n + (lane&15)
+                const uint32_t vl = vw >> (4 * ((lane >> 4) & 3));
+                float mn[2];
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    if constexpr (ISL2) {
+                        float m = __builtin_inff();
+#pragma unroll
+                        for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                            for (int r = 0; r < 4; r++) {
+                                const float v = fmaf(-2.f, acc[mm][n][r], mm ? x1[r] : x0[r]);
+                                m = fminf(m, ((vl >> (16 * mm + r)) & 1u) ? v : __builtin_inff());
+                            }
+                        mn[n] = m;
+                    } else if (vw == 0xFFFFFFFFu) {
+                        float m = fmaxf(fmaxf(acc[0][n][0], acc[0][n][1]), fmaxf(acc[0][n][2], acc[0][n][3]));
+                        m = fmaxf(m, fmaxf(fmaxf(acc[1][n][0], acc[1][n][1]), fmaxf(acc[1][n][2], acc[1][n][3])));
+                        mn[n] = m;
+                    } else {
+                        float m = -__builtin_inff();
+#pragma unroll
+                        for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                            for (int r = 0; r < 4; r++)
+                                m = fmaxf(m, ((vl >> (16 * mm + r)) & 1u) ? acc[mm][n][r] : -__builtin_inff());
+                        mn[n] = m;
+                    }
+                }
+                mp0 = mn[0];
+                mp1 = mn[1];
+                gbp = s0 + t;
+            }
+            // ---- end of the block: the next group must have landed (every wave) ----
+            if (t + 1 < nsteps) {
+                // vector-memory ops of this wave after group t+1, in issue order:
+                // store(t-2), the pieces of group t+2, store(t-1)
+                if constexpr (DBG & 2) {
+                    qs_wait_vm_c<0>();
+                } else if (t >= 2 && t + 2 < nsteps) {
+                    qs_wait_vm_c<P0 + 2>();
+                } else {
+                    const int y = (t >= 1 ? 1 : 0) + (t >= 2 ? 1 : 0) + (t + 2 < nsteps ? P0 : 0);
+                    qs_wait_vm(y);
+                }
+                __builtin_amdgcn_s_barrier();  // slot t is free; slot t+1 has landed for every wave
+                __builtin_amdgcn_sched_barrier(0);
+                const unsigned sbn = ring + (unsigned)(nxt * SLOT) + l16;
+                B2[0][0] = lds_ld8bf_o<0>(sbn);
+                B2[0][1] = lds_ld8bf_o<512>(sbn);
+            }
+            cur = nxt;
+        }
+        if (nsteps > 0) finish();
+        return;
+    }
+    int cur = 0;
+    for (int t = 0; t < nsteps; t++) {
+        const int nxt = cur == QS_NBUF - 1 ? 0 : cur + 1;
+        const unsigned sb = ring + (unsigned)(cur * SLOT) + lane_off;
+        const unsigned sbn = ring + (unsigned)(nxt * SLOT) + lane_off;
+        const unsigned sm = (unsigned)(t & 3);
         static_for<0, RB>([&](auto rbc) {
             constexpr int rb = decltype(rbc)::value;
+            // ---- the block's 32 rows x this wave's 32 queries: NK MFMAs, A fragments 4 ahead ----
             f32x16 acc;
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[r] = 0.f;
-            bf16x8_t A[4];
-            A[0] = lds_ld8bf_o<(rb * NK + 0) * 1024>(sb);
-            A[1] = lds_ld8bf_o<(rb * NK + 1) * 1024>(sb);
-            A[2] = lds_ld8bf_o<(rb * NK + 2) * 1024>(sb);
-            A[3] = lds_ld8bf_o<(rb * NK + 3) * 1024>(sb);
             static_for<0, NK>([&](auto cc) {
                 constexpr int c = decltype(cc)::value;
                 qs_wait_lgkm<(NK - 1 - c) < 3 ? (NK - 1 - c) : 3>();
@@ -200,35 +416,62 @@ __global__ __launch_bounds__(512, 2) void k_qs_blockkey(QsArgs a) {
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[c & 3], Qf[c], acc, 0, 0, 0);
                 if constexpr (c + 4 < NK) A[c & 3] = lds_ld8bf_o<(rb * NK + c + 4) * 1024>(sb);
             });
+            // ---- end of the slot: the next group must have landed (every wave) ----
+            if constexpr (rb == RB - 1) {
+                if (t + 1 < nsteps) {
+                    // ops of this wave issued after group t+1, in issue order (vmcnt
+                    // counts the LDS-DMA pieces and the key stores together)
+                    if (t >= 2 && t + 2 < nsteps) {
+                        qs_wait_vm_c<2 * RB + P0>();  // steady state
+                    } else {
+                        const int y = (RB - 1) + (t >= 1 ? RB : 0) + (t >= 2 ? 1 : 0) + (t + 2 < nsteps ? P0 : 0);
+                        qs_wait_vm(y);
+                    }
+                    __builtin_amdgcn_s_barrier();  // slot t is free: every wave's chain over it is done
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (t + 3 < nsteps) issue(t + 3, cur);
+                }
+            }
             // ---- epilogue: the block's key for this lane's query ----
-            const int64_t gb = (s0 + step) * RB + rb;
-            const uint32_t vw = sload_u32(a.valid + gb);
-            // rows of acc[r]: (r&3) + 8(r>>2) + 4lh; the valid word shifted by 4lh
-            // leaves a compile-time bit position per r
-            const uint32_t vl = vw >> (4 * lh);
+            const int64_t gb = (s0 + t) * RB + rb;
+            uint32_t vwv;
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(vwv) : "v"(vring + sm * 16u), "i"(rb * 4));
             float m;
             if constexpr (ISL2) {
-                const unsigned xb = xnring + (unsigned)(slot * RB * 128 + rb * 128 + 16 * lh);
+                const unsigned xb = xnring + sm * (unsigned)(RB * 128) + (unsigned)(rb * 128 + 16 * lh);
+                f32x4_t x0 = lds_ld4f_o<0>(xb), x1 = lds_ld4f_o<32>(xb), x2 = lds_ld4f_o<64>(xb), x3 = lds_ld4f_o<96>(xb);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vwv), "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+                const uint32_t vw = __builtin_amdgcn_readfirstlane(vwv);
+                const uint32_t vl = vw >> (4 * lh);
+                const float xn[16] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3],
+                                      x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
                 m = __builtin_inff();
-                static_for<0, 4>([&](auto gg) {
-                    constexpr int g = decltype(gg)::value;
-                    f32x4_t x = lds_ld4f_o<32 * g>(xb);
-                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x));
 #pragma unroll
-                    for (int t = 0; t < 4; t++) {
-                        const float v = fmaf(-2.f, acc[4 * g + t], x[t]);
-                        m = fminf(m, v);
-                        if (vw != 0xFFFFFFFFu) acc[4 * g + t] = ((vl >> (8 * g + t)) & 1u) ? v : __builtin_inff();
-                    }
-                });
-                if (vw != 0xFFFFFFFFu) {  // partial block: min over the valid rows only
-                    m = __builtin_inff();
-#pragma unroll
-                    for (int r = 0; r < 16; r++) m = fminf(m, acc[r]);
+                for (int r = 0; r < 16; r++) {
+                    float v = fmaf(-2.f, acc[r], xn[r]);
+                    if (vw != 0xFFFFFFFFu) v = ((vl >> ((r & 3) + 8 * (r >> 2))) & 1u) ? v : __builtin_inff();
+                    m = fminf(m, v);
                 }
+                // next block's first fragments (after the epilogue reads: registers)
+                const unsigned pb = rb + 1 < RB ? sb : sbn;
+                constexpr int pr = rb + 1 < RB ? rb + 1 : 0;
+                A[0] = lds_ld8bf_o<(pr * NK + 0) * 1024>(pb);
+                A[1] = lds_ld8bf_o<(pr * NK + 1) * 1024>(pb);
+                A[2] = lds_ld8bf_o<(pr * NK + 2) * 1024>(pb);
+                A[3] = lds_ld8bf_o<(pr * NK + 3) * 1024>(pb);
                 const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
                 m = fminf(m, __uint_as_float(sw[1]));
             } else {
+                // next block's first fragments, in flight during the epilogue
+                const unsigned pb = rb + 1 < RB ? sb : sbn;
+                constexpr int pr = rb + 1 < RB ? rb + 1 : 0;
+                A[0] = lds_ld8bf_o<(pr * NK + 0) * 1024>(pb);
+                A[1] = lds_ld8bf_o<(pr * NK + 1) * 1024>(pb);
+                A[2] = lds_ld8bf_o<(pr * NK + 2) * 1024>(pb);
+                A[3] = lds_ld8bf_o<(pr * NK + 3) * 1024>(pb);
+                asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(vwv));
+                const uint32_t vw = __builtin_amdgcn_readfirstlane(vwv);
+                const uint32_t vl = vw >> (4 * lh);
                 m = -__builtin_inff();
                 if (vw == 0xFFFFFFFFu) {
 #pragma unroll
@@ -243,8 +486,9 @@ __global__ __launch_bounds__(512, 2) void k_qs_blockkey(QsArgs a) {
             }
             if (lh == 0) krow[gb] = m;
         });
-        slot = slot == QS_NBUF - 1 ? 0 : slot + 1;
+        cur = nxt;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last (unused) prefetch
 }
 
 // ---------------------------------------------------------------------------
@@ -458,11 +702,12 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
     }
 }
 
-// k_blk_exact<R, METRIC, VARIANT>: wave per query over its candidate blocks
-// (two blocks per pass: lanes 0-31 and 32-63, lane = row).  Reference-order
-// SingleDist of every valid row, top-(k+1) by (distance, id); proof = the
-// first min(k+1, n) are strictly increasing (the reference heap then holds
-// exactly the k smallest and extractHeap returns them ascending).
+// k_blk_exact<R, METRIC, VARIANT>: one workgroup (4 waves) per query over its
+// candidate blocks (each wave two blocks per pass: lanes 0-31 and 32-63, lane
+// = row).  Reference-order SingleDist of every valid row, top-(k+1) by
+// (distance, id) per wave, merged by wave 0; proof = the first min(k+1, n)
+// are strictly increasing (the reference heap then holds exactly the k
+// smallest and extractHeap returns them ascending).
 template <int R, int METRIC, int VARIANT>
 __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
                                                    int64_t nrows, const float* __restrict__ Qn, int d,
@@ -473,9 +718,12 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     constexpr int L = 64 * (R - 1);
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
+    __shared__ float lk[3][L];
+    __shared__ uint32_t lid[3][L];
+    __shared__ int snv[4];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int q = blockIdx.x * 4 + w;
+    const int q = blockIdx.x;
     if (q >= nq) return;
     if (flags[q]) return;  // overflowed selection: the replay resolves it
     const int nc = ncand[q];
@@ -484,7 +732,7 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     WaveTopL<R> t;
     t.init();
     int nvalid = 0;
-    for (int j0 = 0; j0 < nc; j0 += 2) {
+    for (int j0 = 2 * w; j0 < nc; j0 += 8) {
         const int j = j0 + lh;
         bool ok = false;
         int64_t row = 0;
@@ -498,6 +746,21 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         t.offer(ok ? e : __builtin_inff(), ok ? (uint32_t)row : NO_ID, sbk[w], sbi[w], lane);
     }
     t.merge(sbk[w], sbi[w], lane);
+    if (w > 0) {
+#pragma unroll
+        for (int r = 0; r < R - 1; r++) {
+            lk[w - 1][r * 64 + lane] = t.key[r];
+            lid[w - 1][r * 64 + lane] = t.id[r];
+        }
+    }
+    if (lane == 0) snv[w] = nvalid;
+    __syncthreads();
+    if (w > 0) return;
+    // wave 0: merge the other waves' lists into its own
+    for (int w2 = 0; w2 < 3; w2++)
+        for (int r = 0; r < R - 1; r++) t.offer(lk[w2][r * 64 + lane], lid[w2][r * 64 + lane], sbk[0], sbi[0], lane);
+    t.merge(sbk[0], sbi[0], lane);
+    nvalid = snv[0] + snv[1] + snv[2] + snv[3];
     const int m = (k + 1) < nvalid ? (k + 1) : nvalid;
     bool inc = true;
 #pragma unroll
@@ -575,12 +838,37 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     const int li = lane & 31, lh = lane >> 5;
     if (lane == 0) *s_len = 0;
     __syncthreads();
-    for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+    // block keys in rounds of 64 * RU: all loads of a round in flight at once,
+    // parked in LDS; a round with no visitable block is skipped whole
+    constexpr int RU = 16;
+    float* skey = hd + k + 4;  // [RU * 64]
+    for (int64_t r0 = 0; r0 < nb; r0 += 64 * RU) {
+        float kvr[RU];
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+            const int64_t bb = r0 + u * 64 + lane;
+            kvr[u] = bb < nb ? kr[bb] : __builtin_inff();
+        }
+        {
+            const int len0 = *s_len;
+            const float top0 = len0 > 0 ? hd[0] : 0.f;
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < RU; u++) {
+                const int64_t bb = r0 + u * 64 + lane;
+                const bool has = bb < nb && (noskip || kvr[u] < __builtin_inff());
+                const float lb = noskip ? -__builtin_inff() : qs_key_to_a(metric, kvr[u], qi.x) - eps;
+                any |= has && (len0 < k || top0 > lb);
+                skey[u * 64 + lane] = kvr[u];
+            }
+            if (!__any(any)) continue;
+        }
+    for (int64_t b0 = r0; b0 < r0 + 64 * RU && b0 < nb; b0 += 64) {
         const int64_t bb = b0 + lane;
         float lb = __builtin_inff();
         bool has = false;
         if (bb < nb) {
-            const float kv = kr[bb];
+            const float kv = skey[(b0 - r0) + lane];
             has = noskip || kv < __builtin_inff();
             lb = noskip ? -__builtin_inff() : qs_key_to_a(metric, kv, qi.x) - eps;
         }
@@ -623,6 +911,7 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
             }
             __syncthreads();
         }
+    }
     }
     if (lane == 0) {
         ReplayHeap h{hid, hd, *s_len};

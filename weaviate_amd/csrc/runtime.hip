@@ -152,6 +152,8 @@ struct wv_index {
     int has_nonfinite = 0;          // host mirror of qsmax[2]
     uint64_t replayed_host = 0;     // replays counted on the host (legacy paths)
     int timed = 0;                  // ev0/ev1 bracket the last batch's dominant kernel
+    int timed_total = 0;            // evt0/evt1 bracket the last batch's whole block-key pipeline
+    hipEvent_t evt0 = nullptr, evt1 = nullptr;
     float last_eps_scale = 0.f, last_eps_base = 0.f;  // exactness-proof eps of the last MFMA batch (debug hook)
     int64_t last_nq = 0;
     int last_KP = 0;
@@ -246,6 +248,8 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     if (e == hipSuccess) e = hipMemset(idx->qscount, 0, 4 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipEventCreate(&idx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&idx->ev1);
+    if (e == hipSuccess) e = hipEventCreate(&idx->evt0);
+    if (e == hipSuccess) e = hipEventCreate(&idx->evt1);
     if (e != hipSuccess) {
         delete idx;
         return set_err(WV_ERR_HIP, "create: %s", hipGetErrorString(e));
@@ -286,6 +290,8 @@ extern "C" void wv_index_destroy(wv_index* idx) {
         if (p) hipFree(p);
     if (idx->ev0) hipEventDestroy(idx->ev0);
     if (idx->ev1) hipEventDestroy(idx->ev1);
+    if (idx->evt0) hipEventDestroy(idx->evt0);
+    if (idx->evt1) hipEventDestroy(idx->evt1);
     if (idx->stream) hipStreamDestroy(idx->stream);
     delete idx;
 }
@@ -766,6 +772,11 @@ extern "C" int wv_index_stats(wv_index* idx, wv_stats* out) {
         HIPCHK(hipEventSynchronize(idx->ev1));
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, idx->ev0, idx->ev1) == hipSuccess) idx->stats.last_select_ms = ms;
+    }
+    if (idx->timed_total) {
+        HIPCHK(hipEventSynchronize(idx->evt1));
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, idx->evt0, idx->evt1) == hipSuccess) idx->stats.last_total_ms = ms;
     }
     *out = idx->stats;
     out->replayed_queries = idx->stats.replayed_queries + dev_replays;
@@ -1886,7 +1897,7 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     HIPCHK(idx->qsEps.ensure((size_t)qc * sizeof(float)));
     HIPCHK(idx->qsList.ensure((size_t)qc * sizeof(int32_t)));
     if (!o_flags) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
-    const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16;
+    const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
     if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
     // error-bound constants: reference-order fp32 (gamma_{dpb+8}) and the MFMA's
     // fp32 accumulation over NK chained 16-deep products (u' = 2^-22)
@@ -1898,6 +1909,8 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
     const float* Qn_all = idx->qn.as<float>();
     idx->timed = 0;
+    idx->timed_total = 0;
+    if (idx->timing) HIPCHK(hipEventRecord(idx->evt0, s));
     for (int64_t c0 = 0; c0 < nq; c0 += qc) {
         const int64_t cn = std::min<int64_t>(qc, nq - c0);
         const int64_t cn_pad = round_up(cn, QS_QPB);
@@ -1914,16 +1927,22 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         a.key = idx->qsKey.as<float>();
         a.ldk = ldk;
         a.nslots = nslots;
+        a.dbg = idx->sel_dbg;
         a.nqg = (int)(cn_pad / QS_QPB);
         int64_t nspans = 256 / std::gcd(256, a.nqg);
         while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
         if (idx->spans_opt > 0) nspans = idx->spans_opt;
+        {   // a span's plane bytes (+ one tile of slack) must stay below 4 GiB (32-bit buffer offsets)
+            const int64_t slot_b = (int64_t)RB * 32 * idx->dpb * 2;
+            const int64_t max_sps = ((1ll << 32) - 2 * 256ll * idx->dpb * 2) / slot_b;
+            nspans = std::max<int64_t>(nspans, (nslots + max_sps - 1) / max_sps);
+        }
         nspans = std::max<int64_t>(1, std::min<int64_t>(nspans, nslots));
         const int64_t sps = (nslots + nspans - 1) / nspans;
         a.slots_per_span = (int)sps;
         a.nspans = (int)((nslots + sps - 1) / sps);
         const bool l2 = metric == L2;
-        const size_t lds = (size_t)QS_NBUF * RB * NK * 1024 + (l2 ? (size_t)QS_NBUF * RB * 128 : 0);
+        const size_t lds = (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
         dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
         const bool time_it = idx->timing && c0 == 0;
         if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
@@ -1931,6 +1950,11 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     do {                                                                                                       \
         HIPCHK(hipFuncSetAttribute((const void*)k_qs_blockkey<NKV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
         k_qs_blockkey<NKV, L2V><<<grid, 512, lds, s>>>(a);                                                     \
+    } while (0)
+#define WV_QS3(NKV, L2V, D)                                                                                    \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_qs_blockkey<NKV, L2V, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_qs_blockkey<NKV, L2V, D><<<grid, 512, lds, s>>>(a);                                                  \
     } while (0)
 #define WV_QSN(L2V)                                    \
     switch (NK) {                                      \
@@ -1941,8 +1965,19 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     case 40: WV_QS(40, L2V); break;                    \
     default: WV_QS(48, L2V); break;                    \
     }
-        if (l2) { WV_QSN(true); } else { WV_QSN(false); }
+        if (idx->sel_dbg > 0 && !l2 && NK == 48) {  // timing experiments (k_qs_blockkey DBG)
+            switch (idx->sel_dbg) {
+            case 1: WV_QS3(48, false, 1); break;
+            case 2: WV_QS3(48, false, 2); break;
+            case 3: WV_QS3(48, false, 3); break;
+            case 4: WV_QS3(48, false, 4); break;
+            case 5: WV_QS3(48, false, 5); break;
+            case 6: WV_QS3(48, false, 6); break;
+            default: WV_QS3(48, false, 7); break;
+            }
+        } else if (l2) { WV_QSN(true); } else { WV_QSN(false); }
 #undef WV_QSN
+#undef WV_QS3
 #undef WV_QS
         HIPCHK(hipGetLastError());
         if (time_it) { HIPCHK(hipEventRecord(idx->ev1, s)); idx->timed = 1; }
@@ -1953,7 +1988,7 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
 #define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>())
         if (R == 2) WV_SELR(2); else if (R == 4) WV_SELR(4); else WV_SELR(8);
 #undef WV_SELR
-#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<gw, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags)
+#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \
     case L2: if (v5) WV_EXR(RV, L2, AVX512); else WV_EXR(RV, L2, AVX256); break;   \
@@ -1980,6 +2015,10 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         }
 #undef WV_RP
         HIPCHK(hipGetLastError());
+    }
+    if (idx->timing) {
+        HIPCHK(hipEventRecord(idx->evt1, s));
+        idx->timed_total = 1;
     }
     return WV_OK;
 }
