@@ -72,10 +72,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cgroup_cpus():
+    """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_info() -> dict:
-    """nproc (CPUs this process may run on), the CPU model, and the kernel
-    variant the reference would pick on this host: AVX-512 only with
-    AMX-BF16 && AVX512 (distancer/l2_amd64.go:19-26), else AVX2."""
+    """nproc (CPUs this process may run on), the cgroup CPU quota, the CPU
+    model, and the kernel variant the reference would pick on this host:
+    AVX-512 only with AMX-BF16 && AVX512 (distancer/l2_amd64.go:19-26), else AVX2."""
     nproc = len(os.sched_getaffinity(0))
     model, flags = "", ""
     try:
@@ -87,7 +98,7 @@ def host_info() -> dict:
     except OSError:
         pass
     variant = "avx512" if (" amx_bf16 " in flags and " avx512f " in flags) else "avx256"
-    return {"nproc": nproc, "cpu_model": model, "variant": variant}
+    return {"nproc": nproc, "cgroup_cpus": cgroup_cpus(), "cpu_model": model, "variant": variant}
 
 
 def cpu_baseline(n_sample: int, nq: int, threads: int, spec=None):
@@ -121,6 +132,7 @@ def cpu_baseline(n_sample: int, nq: int, threads: int, spec=None):
         "cores": threads,
         "kind": "reference" if use_ref else "port",
         "nproc": info["nproc"],
+        "cgroup_cpus": info["cgroup_cpus"],
         "cpu_model": info["cpu_model"],
         "variant": info["variant"],
         "sample": (f"{nq} queries x {n_sample} rows (first rows of the same corpus), {spec['metric']} k={k}, "
@@ -243,7 +255,10 @@ def main():
                     help="HBM bytes per k_mfma_select launch from the rocprofv3 PMC pass")
     args = ap.parse_args()
     if args.cpu_threads is None:
-        args.cpu_threads = len(os.sched_getaffinity(0))
+        # every CPU this process may use: nproc, capped by a cgroup quota (more
+        # threads than the quota only time-slice the same cores)
+        quota = cgroup_cpus()
+        args.cpu_threads = len(os.sched_getaffinity(0)) if quota is None else min(quota, len(os.sched_getaffinity(0)))
 
     import torch
     import torch.distributed as dist

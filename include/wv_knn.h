@@ -255,13 +255,21 @@ int wv_index_stats(wv_index *idx, wv_stats *out);
  * get *KP only. */
 int wv_index_debug_candidates(wv_index *idx, float *A, float *E, uint32_t *I, float *eps, int64_t nq, int32_t *KP);
 
-/* tuning / testing knobs: "margin" (extra candidates, default 8),
- * "force_replay" (1 = resolve every query by heap replay), "spans" (0 = auto),
- * "kernel" (select kernel: 6 = HBM-streaming GEMV (default for batches <= "gemv_max",
- * default 8), 4 = bf16x3 MFMA (default for the exact fp32 path),
- * 3 = f32 MFMA ring, 2/1 older f32 forms), "bq_kernel" (1 = generic BQ kernels),
- * "timing" (1 = record kernel times with HIP events), "batch_window_us" /
- * "batch_max" (micro-batcher, see wv_index_search_by_vector) */
+/* Diagnostic hook (tests) of the block-key path: query q of the last batch
+ * (first query chunk): its smallest approximate distance of every 32-row block
+ * (A space, +inf for a block without a valid row) into A[*nb] and its error
+ * bound eps(q).  Call with A == NULL to read *nb only. */
+int wv_index_debug_blockkeys(wv_index *idx, int64_t q, float *A, float *eps, int64_t *nb);
+
+/* tuning / testing knobs: "margin" (extra candidates of the legacy select
+ * kernels, default 8), "force_replay" (1 = resolve every query by heap
+ * replay), "spans" (0 = auto), "kernel" (0 = auto: 7 = bf16 block-key path
+ * (qs_kernels.hip, the default for the exact fp32 search up to 768 dims),
+ * 6 = HBM-streaming GEMV, 5/4 = bf16x3 MFMA select (need "bf3_planes" = 1
+ * before the first Add), 3 = f32 MFMA ring, 2/1 older f32 forms),
+ * "bq_kernel" (1 = generic BQ kernels), "timing" (1 = record kernel times
+ * with HIP events), "batch_window_us" / "batch_max" (micro-batcher, see
+ * wv_index_search_by_vector) */
 int wv_index_set_option(wv_index *idx, const char *key, int64_t value);
 
 /* ---- LSM on-disk format: restore from flat's vectors bucket ----------------

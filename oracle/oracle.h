@@ -89,6 +89,13 @@ int or_flat_search_rq(const or_rq *r, int variant, const float *store, const uin
 void or_rq_query_distances(const or_rq *r, int variant, const void *codes, long nslots, const float *query, long qd,
                            float *out);
 
+/* scale.c: oracles at full BASELINE sizes over the regenerated corpus */
+int or_gen_dists(int kind, uint64_t seed, long n, long d, int metric, int variant, const float *queries, long nq,
+                 int nthreads, float *out);
+int or_heap_scan(const float *dists, long n, int k, uint64_t *out_ids, float *out_dists);
+int or_bq_search_gen(int kind, uint64_t seed, long n, long d, int metric, int variant, const float *queries, long nq,
+                     int k, int rescore_limit, int nthreads, uint64_t *out_ids, float *out_d, int *out_n);
+
 uint64_t or_gen_bits(uint64_t seed, uint64_t row, uint64_t col);
 float or_gen_value(int kind, uint64_t seed, uint64_t row, uint64_t col);
 void or_gen_matrix(int kind, uint64_t seed, uint64_t row0, long rows, long d, float *out);

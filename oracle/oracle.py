@@ -54,6 +54,14 @@ def lib() -> C.CDLL:
         o.or_filter_by_distance.restype = C.c_int
         o.or_filter_by_distance.argtypes = [pu, pf, C.c_int, C.c_float, pu, pf]
         o.or_gen_matrix.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_long, C.c_long, pf]
+        o.or_gen_dists.restype = C.c_int
+        o.or_gen_dists.argtypes = [C.c_int, C.c_uint64, C.c_long, C.c_long, C.c_int, C.c_int, pf, C.c_long, C.c_int,
+                                   pf]
+        o.or_heap_scan.restype = C.c_int
+        o.or_heap_scan.argtypes = [pf, C.c_long, C.c_int, pu, pf]
+        o.or_bq_search_gen.restype = C.c_int
+        o.or_bq_search_gen.argtypes = [C.c_int, C.c_uint64, C.c_long, C.c_long, C.c_int, C.c_int, pf, C.c_long,
+                                       C.c_int, C.c_int, C.c_int, pu, pf, pi]
         o.or_gen_value.restype = C.c_float
         o.or_gen_value.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64]
         o.bl_set_ref_kernels.argtypes = [C.c_void_p] * 4
@@ -277,18 +285,26 @@ def random_subset(seed: int, n: int, k: int) -> np.ndarray:
 
 
 def pq_fit(data: np.ndarray, m: int, ks: int, seed: int, variant: int = AVX256, iterations: int = 10,
-           delta: float = 0.01, brute_force: bool = False) -> np.ndarray:
-    """ProductQuantizer.Fit with the KMeans encoder; segment s seeded seed+s.
-    Returns centers [m][ks][ds]."""
+           delta: float = 0.01, brute_force: bool = False, nthreads: int = 1) -> np.ndarray:
+    """ProductQuantizer.Fit with the KMeans encoder; segment s seeded seed+s
+    (the segments are independent problems: nthreads fit them concurrently,
+    as the reference's Fit does).  Returns centers [m][ks][ds]."""
     data = np.ascontiguousarray(data, dtype=np.float32)
     n, d = data.shape
     ds = d // m
     out = np.zeros((m, ks, ds), dtype=np.float32)
-    for s in range(m):
-        rc = lib().or_kmeans_fit(f(data), n, d, s, ds, ks, (seed + s) & (2**64 - 1), variant, iterations, delta,
-                                 1 if brute_force else 0, f(out[s]))
-        if rc < 0:
-            raise ValueError("not enough data to fit k-means")
+
+    def one(s):
+        return lib().or_kmeans_fit(f(data), n, d, s, ds, ks, (seed + s) & (2**64 - 1), variant, iterations, delta,
+                                   1 if brute_force else 0, f(out[s]))
+    if nthreads > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(nthreads) as ex:
+            rcs = list(ex.map(one, range(m)))
+    else:
+        rcs = [one(s) for s in range(m)]
+    if min(rcs) < 0:
+        raise ValueError("not enough data to fit k-means")
     return out
 
 
@@ -478,4 +494,42 @@ def cpu_baseline(metric: int, variant: int, store: np.ndarray, queries: np.ndarr
                                 f(queries), nq, k, nthreads, ids.ctypes.data_as(pu), f(dd), cnt.ctypes.data_as(pi))
     if rc != 0:
         raise RuntimeError("baseline failed")
+    return ids, dd, cnt
+
+
+# ---------------------------------------------------------------------------
+# full-size oracles over the regenerated corpus (oracle/scale.c)
+# ---------------------------------------------------------------------------
+def gen_dists(kind: int, seed: int, n: int, d: int, metric: int, variant: int, queries: np.ndarray,
+              nthreads: int = 16) -> np.ndarray:
+    """SingleDist of each prepared query (normalised for cosine) to rows [0, n)
+    of the generated corpus, rows prepared as flat.Add does.  [nq][n] float32."""
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    out = np.empty((q.shape[0], n), dtype=np.float32)
+    lib().or_gen_dists(kind, seed, n, d, metric, variant, f(q), q.shape[0], nthreads, f(out))
+    return out
+
+
+def heap_scan(dists: np.ndarray, k: int):
+    """The reference heap (insertToHeap in id order + extractHeap) over one
+    query's precomputed distances of rows [0, n)."""
+    dd = np.ascontiguousarray(dists, dtype=np.float32)
+    ids = np.zeros(k, np.uint64)
+    od = np.zeros(k, np.float32)
+    m = lib().or_heap_scan(f(dd), dd.size, k, ids.ctypes.data_as(pu), f(od))
+    return ids[:m], od[:m]
+
+
+def bq_search_gen(kind: int, seed: int, n: int, d: int, metric: int, variant: int, queries: np.ndarray, k: int,
+                  rescore_limit: int, nthreads: int = 16):
+    """searchByVectorQuantized of raw queries over the generated corpus."""
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    nq = q.shape[0]
+    ids = np.zeros((nq, k), np.uint64)
+    dd = np.zeros((nq, k), np.float32)
+    cnt = np.zeros(nq, np.int32)
+    rc = lib().or_bq_search_gen(kind, seed, n, d, metric, variant, f(q), nq, k, rescore_limit, nthreads,
+                                ids.ctypes.data_as(pu), f(dd), cnt.ctypes.data_as(pi))
+    if rc != 0:
+        raise RuntimeError("bq_search_gen failed")
     return ids, dd, cnt

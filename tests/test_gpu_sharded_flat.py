@@ -41,10 +41,18 @@ def test_sharded_flat_protocol_equals_single_index(wv, oracle, shards, metric, k
     single = wv.FlatIndex(distance=metric, variant="avx256")
     single.add_batch(np.arange(n, dtype=np.uint64), data)
     si, sd, sn = single.search_by_vector_batch(queries, k)
+    om = oracle.METRIC[metric]
+    orc = oracle.OracleFlat(om, 1, d, n)
+    orc.add_batch(np.arange(n), data)
     for i in range(len(queries)):
         assert on[i] == sn[i]
         np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), si[i, :sn[i]], err_msg=f"q{i}")
         np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), sd[i, :sn[i]].view(np.uint32))
+        # and the reference heap over the whole corpus (oracle/oracle.c or_flat_search)
+        rc, ei, ed = orc.search(queries[i], k)
+        assert rc == 0 and on[i] == len(ei)
+        np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), ei, err_msg=f"q{i} vs oracle")
+        np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), ed.view(np.uint32), err_msg=f"q{i} vs oracle")
     for b in backs:
         b.index.close()
     single.close()

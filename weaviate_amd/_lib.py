@@ -97,6 +97,7 @@ SIGNATURES = {
     "wv_gen_device": (C.c_int, [i32, i32, u64, u64, i64, i64, P, P]),
     "wv_index_stats": (C.c_int, [P, C.POINTER(WvStats)]),
     "wv_index_debug_candidates": (C.c_int, [P, pf32, pf32, C.POINTER(C.c_uint32), pf32, i64, pi32]),
+    "wv_index_debug_blockkeys": (C.c_int, [P, i64, pf32, pf32, C.POINTER(C.c_int64)]),
     "wv_index_bq_begin": (C.c_int, [P, P, i64, i64, i32, P]),
     "wv_index_bq_replay": (C.c_int, [P, P, P, P, i32, P, P, P, P]),
     "wv_index_bq_rescore": (C.c_int, [P, P, P, P, P]),

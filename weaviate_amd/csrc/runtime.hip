@@ -153,6 +153,7 @@ struct wv_index {
     uint64_t replayed_host = 0;     // replays counted on the host (legacy paths)
     int timed = 0;                  // ev0/ev1 bracket the last batch's dominant kernel
     int timed_total = 0;            // evt0/evt1 bracket the last batch's whole block-key pipeline
+    int64_t qs_last_nq = 0, qs_last_nb = 0, qs_last_ldk = 0;  // first chunk of the last block-key batch (debug hook)
     hipEvent_t evt0 = nullptr, evt1 = nullptr;
     float last_eps_scale = 0.f, last_eps_base = 0.f;  // exactness-proof eps of the last MFMA batch (debug hook)
     int64_t last_nq = 0;
@@ -753,6 +754,32 @@ extern "C" int wv_index_debug_candidates(wv_index* idx, float* A, float* E, uint
             if (idx->metric == WV_METRIC_L2_SQUARED) { float t = qn + idx->last_eps_base; eps[q] = idx->last_eps_scale * t * t; }
             else eps[q] = idx->last_eps_scale * (qn * idx->last_eps_base + 1.f);
         }
+    }
+    return WV_OK;
+}
+
+extern "C" int wv_index_debug_blockkeys(wv_index* idx, int64_t q, float* A, float* eps, int64_t* nb) {
+    if (!idx || !nb) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->qs_last_nq <= 0 || q < 0 || q >= idx->qs_last_nq)
+        return set_err(WV_ERR_INVALID, "debug_blockkeys: no such query in the last block-key batch");
+    *nb = idx->qs_last_nb;
+    if (!A) return WV_OK;
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    std::vector<float> key((size_t)idx->qs_last_nb);
+    float4 qi;
+    HIPCHK(hipMemcpy(key.data(), idx->qsKey.as<float>() + q * idx->qs_last_ldk, key.size() * sizeof(float),
+                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&qi, idx->qsInfo.as<float4>() + q, sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(eps, idx->qsEps.as<float>() + q, sizeof(float), hipMemcpyDeviceToHost));
+    for (size_t b = 0; b < key.size(); b++) {  // qs_key_to_a, host side (same fp32 ops)
+        const float kv = key[b];
+        float a;
+        if (idx->metric == WV_METRIC_L2_SQUARED) a = kv + qi.x;
+        else if (idx->metric == WV_METRIC_DOT) a = kv;
+        else { const float p = 1.f + kv; a = p < 0.f ? 0.f : p; }
+        A[b] = a;
     }
     return WV_OK;
 }
@@ -1914,6 +1941,7 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     for (int64_t c0 = 0; c0 < nq; c0 += qc) {
         const int64_t cn = std::min<int64_t>(qc, nq - c0);
         const int64_t cn_pad = round_up(cn, QS_QPB);
+        if (c0 == 0) { idx->qs_last_nq = cn == nq ? cn : 0; idx->qs_last_nb = nb; idx->qs_last_ldk = ldk; }
         const float* Qn = Qn_all + c0 * idx->dpad;
         float4* qinfo = idx->qsInfo.as<float4>();
         k_query_split<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dpb, cn, cn_pad,

@@ -158,6 +158,16 @@ class FlatIndex:
                                                 _fptr(eps), int(nq), C.byref(kp)))
         return A, E, I, eps
 
+    def debug_blockkeys(self, q: int):
+        """Diagnostic: (A_block[nb], eps) of query q of the last block-key batch
+        (see wv_index_debug_blockkeys in include/wv_knn.h)."""
+        nb = C.c_int64(0)
+        check(self._l.wv_index_debug_blockkeys(self._h, int(q), None, None, C.byref(nb)))
+        A = np.zeros(nb.value, np.float32)
+        eps = np.zeros(1, np.float32)
+        check(self._l.wv_index_debug_blockkeys(self._h, int(q), _fptr(A), _fptr(eps), C.byref(nb)))
+        return A, float(eps[0])
+
     # -- product quantizer (compressionhelpers.ProductQuantizer) -----------
     def pq_info(self) -> dict:
         out = (C.c_int32 * 4)()
