@@ -106,6 +106,34 @@ int wv_index_contains_doc(wv_index *idx, uint64_t id);
 uint64_t wv_index_already_indexed(wv_index *idx);
 int32_t wv_index_dims(wv_index *idx);
 
+/* ---- the rest of db.VectorIndex (adapters/repos/db/vector_index.go:25-54) -- */
+/* flat.Iterate (flat/index.go:1057-1079): fn(id, user) for every stored id in
+ * ascending order until fn returns 0 (snapshot taken under the index lock; fn
+ * runs without it). */
+int wv_index_iterate(wv_index *idx, int (*fn)(uint64_t id, void *user), void *user);
+/* flat.QueryVectorDistancer(query).DistanceFunc(id) for n ids
+ * (flat/index.go:1160-1240): SingleDist(normalised query, stored row); with
+ * option "cache" = 1 on a BQ / RQ index, the quantized distance of the cached
+ * code (createDistanceCalcQuantized, :534-566).  Missing ids fail as the
+ * reference's empty bucket read does ("<qd> vs 0: vector lengths don't
+ * match").  out_rc (may be NULL): per-id status; NULL returns the first
+ * failure. */
+int wv_index_query_distances(wv_index *idx, const float *query, int64_t qd, const uint64_t *ids, int64_t n,
+                             float *out, int32_t *out_rc);
+/* flat.Preload (flat/index.go:844-865): compressed index -> the row's code is
+ * stored (rows and codes live together here; AlreadyIndexed unchanged);
+ * uncompressed -> no-op. */
+int wv_index_preload(wv_index *idx, uint64_t id, const float *vec, int64_t d);
+/* flat.UpdateUserConfig (flat/index.go:763-776): applies the rescore limit
+ * (extractCompressionRescore, :170-180). */
+int wv_index_update_user_config(wv_index *idx, const wv_config *updated);
+/* flat.ValidateUserConfigUpdate (flat/index.go:1106-1154): distance, pq, bq,
+ * rq, rq.bits immutable -> "<name> is immutable: attempted change from ..." */
+int wv_validate_user_config_update(const wv_config *initial, const wv_config *updated);
+/* flat.CompressionStats (flat/index.go:1246-1249): UncompressedStats{} ->
+ * type "none", ratio 1.0 */
+int wv_index_compression_stats(wv_index *idx, char *type_out, int64_t type_cap, double *ratio);
+
 /* flat.SearchByVector (flat/index.go:423-448 + :578-688) for nq queries.
  * allow_mode 0: allow list nil; 1: allow list = allow_ids[0..n_allow) (may be
  * empty -> empty results, flat/index.go:590-594).
@@ -269,7 +297,8 @@ int wv_index_debug_blockkeys(wv_index *idx, int64_t q, float *A, float *eps, int
  * before the first Add), 3 = f32 MFMA ring, 2/1 older f32 forms),
  * "bq_kernel" (1 = generic BQ kernels), "timing" (1 = record kernel times
  * with HIP events), "batch_window_us" / "batch_max" (micro-batcher, see
- * wv_index_search_by_vector) */
+ * wv_index_search_by_vector), "cache" (BQ.Cache / RQ.Cache, default 0: see
+ * wv_index_query_distances) */
 int wv_index_set_option(wv_index *idx, const char *key, int64_t value);
 
 /* ---- LSM on-disk format: restore from flat's vectors bucket ----------------

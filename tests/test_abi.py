@@ -47,3 +47,21 @@ def test_variant_rule_matches_reference_dispatch(wv):
     expect = 2 if ("amx_bf16" in flags and "avx512f" in flags) else 1
     assert lib.wv_resolve_variant(0) == expect
     assert lib.wv_resolve_variant(1) == 1 and lib.wv_resolve_variant(2) == 2
+
+
+def test_validate_user_config_update_host_only(wv):
+    """flat.ValidateUserConfigUpdate (flat/index.go:1106-1154): host logic, no GPU."""
+    import pytest
+    from weaviate_amd.flat import validate_user_config_update as v
+    base = dict(distance="cosine", bq=True, rescore_limit=10)
+    v(base, dict(base, rescore_limit=300))  # rescore is mutable
+    with pytest.raises(wv.WeaviateError, match='distance is immutable: attempted change from "cosine" to "l2-squared"'):
+        v(base, dict(base, distance="l2-squared"))
+    with pytest.raises(wv.WeaviateError, match='bq is immutable: attempted change from "true" to "false"'):
+        v(base, dict(base, bq=False))
+    with pytest.raises(wv.WeaviateError, match='pq is immutable: attempted change from "false" to "true"'):
+        v(dict(distance="dot"), dict(distance="dot", pq={"segments": 4}))
+    with pytest.raises(wv.WeaviateError, match='rq is immutable: attempted change from "false" to "true"'):
+        v(dict(distance="dot"), dict(distance="dot", rq={"bits": 8}))
+    with pytest.raises(wv.WeaviateError, match='rq.bits is immutable: attempted change from "8" to "1"'):
+        v(dict(distance="dot", rq={"bits": 8}), dict(distance="dot", rq={"bits": 1}))

@@ -124,6 +124,14 @@ def test_large_k_replay_path(wv, oracle):
     ids, dists, counts = idx.search_by_vector_batch(queries, 100)
     for qi in range(len(queries)):
         assert_same(orc.search(queries[qi], 100), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
+    # k in the thousands: the replay heap needs more than the default 64 KiB LDS
+    for k in (3000, 6000):
+        ids, dists, counts = idx.search_by_vector_batch(queries[:3], k)
+        for qi in range(3):
+            assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"k{k} q{qi}")
+    # beyond the LDS heap: a clear error, not a launch failure
+    with pytest.raises(wv.WeaviateError, match="exceeds the exact replay heap limit"):
+        idx.search_by_vector_batch(queries[:1], 20000)
 
 
 def test_allow_list_delete_upsert(wv, oracle):

@@ -10,14 +10,17 @@ import lsm  # oracle/lsm.py (test infrastructure)
 pytestmark = pytest.mark.gpu
 
 
-def _segments(tmp_path, oracle, n, d, kind=0):
-    base = oracle.gen_matrix(kind, 31, 0, n, d)
-    upd = oracle.gen_matrix(kind, 32, 0, n // 5, d)
+def _segments(tmp_path, oracle, n, d, kind=0, normalized=False):
+    """normalized: the bucket holds what flat.Add stored for cosine -- rows
+    already through distancer.Normalize (flat/index.go:376-378)."""
+    prep = (lambda m: np.stack([oracle.normalize(x) for x in m])) if normalized else (lambda m: m)
+    base = prep(oracle.gen_matrix(kind, 31, 0, n, d))
+    upd = prep(oracle.gen_matrix(kind, 32, 0, n // 5, d))
     ids = np.arange(n, dtype=np.uint64) * 3 + 5          # sparse ids
     up_ids = ids[::5][: len(upd)]
     dead = np.setdiff1d(ids[1::11], up_ids)  # one node per key within a segment
     revived = dead[::4]
-    rv = oracle.gen_matrix(kind, 33, 0, len(revived), d)
+    rv = prep(oracle.gen_matrix(kind, 33, 0, len(revived), d))
     blobs = [
         lsm.write_segment(lsm.vector_entries(ids[: n // 2], base[: n // 2]), version=0),
         lsm.write_segment(lsm.vector_entries(ids[n // 2:], base[n // 2:]), version=1, level=1),
@@ -41,7 +44,8 @@ def _segments(tmp_path, oracle, n, d, kind=0):
     ("dot", True, 5000, 200, 10),
 ])
 def test_load_segments_search_equals_oracle(wv, oracle, tmp_path, metric, bq, n, d, k):
-    paths, state, live_ids, live_vecs = _segments(tmp_path, oracle, n, d)
+    M = oracle.METRIC[metric]
+    paths, state, live_ids, live_vecs = _segments(tmp_path, oracle, n, d, normalized=M == oracle.COSINE)
     kw = {"bq": True, "rescore_limit": 60} if bq else {}
     idx = wv.FlatIndex(distance=metric, variant="avx256", **kw)
     info = idx.load_segments(paths)
@@ -50,12 +54,15 @@ def test_load_segments_search_equals_oracle(wv, oracle, tmp_path, metric, bq, n,
     assert idx.already_indexed() == len(live_ids) and idx.dims == d
     for key, v in list(state.items())[:50]:
         assert idx.contains_doc(key) == (v is not None)
-    M = oracle.METRIC[metric]
     if bq:
         orc = oracle.OracleFlatBQ(M, 1, d, int(max(state)) + 1, 60)
     else:
         orc = oracle.OracleFlat(M, 1, d, int(max(state)) + 1)
-    orc.add_batch(live_ids, live_vecs)
+    if M == oracle.COSINE:  # the oracle holds the bucket's bytes exactly (no second normalisation)
+        orc.store[live_ids.astype(np.int64)] = live_vecs
+        orc.present[live_ids.astype(np.int64)] = 1
+    else:
+        orc.add_batch(live_ids, live_vecs)
     queries = oracle.gen_matrix(0, 34, 0, 16, d)
     ids, dists, counts = idx.search_by_vector_batch(queries, k)
     for q in range(len(queries)):

@@ -65,6 +65,8 @@ class WvStats(C.Structure):
 
 
 P = C.c_void_p
+# flat.Iterate callback: int fn(uint64_t id, void *user)
+ITERATE_FN = C.CFUNCTYPE(C.c_int, C.c_uint64, C.c_void_p)
 i32, i64, u64, f32 = C.c_int32, C.c_int64, C.c_uint64, C.c_float
 pf32 = C.POINTER(C.c_float)
 pu64 = C.POINTER(C.c_uint64)
@@ -85,6 +87,12 @@ SIGNATURES = {
     "wv_index_contains_doc": (C.c_int, [P, u64]),
     "wv_index_already_indexed": (u64, [P]),
     "wv_index_dims": (i32, [P]),
+    "wv_index_iterate": (C.c_int, [P, P, P]),
+    "wv_index_query_distances": (C.c_int, [P, pf32, i64, pu64, i64, pf32, pi32]),
+    "wv_index_preload": (C.c_int, [P, u64, pf32, i64]),
+    "wv_index_update_user_config": (C.c_int, [P, C.POINTER(WvConfig)]),
+    "wv_validate_user_config_update": (C.c_int, [C.POINTER(WvConfig), C.POINTER(WvConfig)]),
+    "wv_index_compression_stats": (C.c_int, [P, C.c_char_p, i64, C.POINTER(C.c_double)]),
     "wv_index_search_by_vector_batch": (C.c_int, [P, pf32, i64, i64, i32, pu64, i64, i32, pu64, pf32, pi32]),
     "wv_index_search_by_vector_distance": (C.c_int, [P, pf32, i64, f32, i64, pu64, i64, i32, pu64, pf32, pi32]),
     "wv_index_search_device": (C.c_int, [P, P, i64, i64, i32, i32, P, P, P, P, P]),

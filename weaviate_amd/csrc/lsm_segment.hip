@@ -275,7 +275,9 @@ extern "C" int wv_index_load_segments(wv_index* idx, const char* const* paths, i
                 }
                 memcpy(&buf[(j - c0) * d], maps[e.seg].p + e.value_off, (size_t)d * 4);  // LE host
             }
-            rc = add_rows_locked(idx, ids.data(), buf.data(), (int64_t)(c1 - c0), d);
+            // the bucket holds the stored bytes (normalised by Add for cosine):
+            // upload as they are (PostStartup / restore reads them unchanged)
+            rc = add_rows_locked(idx, ids.data(), buf.data(), (int64_t)(c1 - c0), d, true);
             if (rc) return rc;
             loaded += (int64_t)(c1 - c0);
         }

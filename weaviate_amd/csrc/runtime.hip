@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <atomic>
 #include <numeric>
 #include <string>
 #include <unordered_map>
@@ -118,6 +119,7 @@ struct wv_index {
     int variant = WV_VARIANT_AVX256;
     int compression = WV_COMPRESSION_NONE;
     int rescore_limit = -1;
+    int cache_opt = 0;  // BQ.Cache / RQ.Cache (flatent UserConfig): QueryVectorDistancer reads codes
     int device = 0;
     uint64_t id_base = 0;
     std::string root_path;
@@ -186,7 +188,8 @@ struct wv_index {
     wv_stats stats{};
     // micro-batcher of concurrent single-query searches (batcher.hip)
     wv_batcher* batcher = nullptr;
-    int64_t batch_window_us = 0, batch_max = 4096;
+    // written by set_option under mu, read by the batcher leader without it
+    std::atomic<int64_t> batch_window_us{0}, batch_max{4096};
     int gemv_max = 8, gemv_wg = 1024, exact_multi = 1;  // batches up to this many queries take the GEMV select kernel (kver 6)
 };
 
@@ -489,9 +492,12 @@ static void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, in
 #undef WV_RQE
 }
 
-static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const uint32_t* d_slots) {
+// as_stored: the rows are the stored bytes already (LSM segment restore: flat.Add
+// normalised them before storeVector, flat/index.go:376-378), so cosine rows are
+// copied as they are -- fp32 normalisation is not idempotent.
+static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const uint32_t* d_slots, bool as_stored = false) {
     dim3 grid((unsigned)((n + 255) / 256));
-    switch (idx->metric) {
+    switch (as_stored ? WV_METRIC_L2_SQUARED : idx->metric) {
     case WV_METRIC_COSINE_DOT:
         k_prepare_rows<COSINE><<<grid, 256, 0, idx->stream>>>(d_in, n, idx->dims, d_slots, idx->X, idx->dpad,
                                                               idx->xnorm2, idx->present, idx->d_maxn2);
@@ -543,7 +549,8 @@ static int validate_rows(wv_index* idx, int64_t d, uint64_t first_slot, uint64_t
 }
 
 // rows: host pointer to n x d floats; ids: host doc ids
-static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs, int64_t n, int64_t d) {
+static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs, int64_t n, int64_t d,
+                           bool as_stored = false) {
     int rc = validate_insert(idx, d);
     if (rc) return rc;
     if (idx->dims == 0) {  // initOnce: initializeDimensionsAndRQ (flat/index.go:338-360)
@@ -589,7 +596,7 @@ static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs
         HIPCHK(idx->slots.ensure(m * sizeof(uint32_t)));
         HIPCHK(hipMemcpyAsync(idx->stage.p, hbuf.data(), m * d * sizeof(float), hipMemcpyHostToDevice, idx->stream));
         HIPCHK(hipMemcpyAsync(idx->slots.p, hslots.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, idx->stream));
-        launch_prepare(idx, idx->stage.as<float>(), (int64_t)m, idx->slots.as<uint32_t>());
+        launch_prepare(idx, idx->stage.as<float>(), (int64_t)m, idx->slots.as<uint32_t>(), as_stored);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(idx->stream));
         for (size_t j = 0; j < m; j++) {
@@ -727,6 +734,10 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
         if (idx->dims) set_dims(idx, idx->dims);
     }
     else if (k == "bq_kernel") idx->bq_kernel = (int)value;
+    else if (k == "cache") {  // BQ.Cache / RQ.Cache: QueryVectorDistancer uses the cached codes
+        if (value != 0 && value != 1) return set_err(WV_ERR_INVALID, "cache must be 0 or 1");
+        idx->cache_opt = (int)value;
+    }
     else if (k == "sel_dbg") idx->sel_dbg = (int)value;
     else if (k == "qgroup") idx->qgroup_opt = (int)value;
     else if (k == "sel_opt") idx->sel_opt = (int)value;
@@ -834,6 +845,10 @@ static int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const
     HIPCHK(idx->rE.ensure((size_t)G * ld * sizeof(float)));
     HIPCHK(idx->rB.ensure((size_t)G * (ld / EBLK) * sizeof(float)));
     const size_t lds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16;
+    if (lds > 160 * 1024)
+        return set_err(WV_ERR_INVALID, "k=%d exceeds the exact replay heap limit of %d results", k,
+                       (int)((160 * 1024 - 272) / 12));
+    HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
     for (int64_t g0 = 0; g0 < nlist; g0 += G) {
         const int F = (int)std::min<int64_t>(G, nlist - g0);
@@ -2585,6 +2600,9 @@ extern "C" int wv_gen_device(int32_t device, int32_t kind, uint64_t seed, uint64
 
 // LSM segment restore (host-only; uses add_rows_locked / wv_index_delete above)
 #include "lsm_segment.hip"
+
+// Iterate, QueryVectorDistancer, Preload, UpdateUserConfig, CompressionStats
+#include "vector_index.hip"
 
 // micro-batcher of concurrent single-query SearchByVector calls
 #include "batcher.hip"

@@ -58,6 +58,35 @@ def _allow_args(allow: Optional[AllowList]):
     return _uptr(ids), ids.size, 1, ids
 
 
+def make_config(distance: str = "cosine", dims: int = 0, device: int = 0, variant: str = "auto",
+                root_path: bytes = b"", id_base: int = 0, bq: bool = False, rescore_limit: int = -1,
+                pq: Optional[dict] = None, rq: Optional[dict] = None) -> "_lib.WvConfig":
+    """flatent.UserConfig subset -> wv_config (include/wv_knn.h)."""
+    if distance not in DISTANCES:
+        raise WeaviateError(_lib.WV_ERR_INVALID, f"unrecognized or unsupported distance metric {distance!r}")
+    # pq: ent.PQConfig subset {"segments", "centroids" (256), "trainingLimit" (100000), "rescore" (True)}
+    pqc = dict(pq or {})
+    # rq: flatent RQ config subset {"bits": 8 | 1} (entities/vectorindex/flat/config.go:27, :199-201);
+    # its RescoreLimit is `rescore_limit`
+    rqc = dict(rq or {})
+    if rq is not None and int(rqc.get("bits", 8)) not in (1, 8):
+        raise WeaviateError(_lib.WV_ERR_INVALID, "rq bits must be 1 or 8")
+    comp = (_lib.COMPRESSION_BQ if bq else _lib.COMPRESSION_PQ if pq is not None
+            else (_lib.COMPRESSION_RQ8 if int(rqc.get("bits", 8)) == 8 else _lib.COMPRESSION_RQ1)
+            if rq is not None else _lib.COMPRESSION_NONE)
+    return _lib.WvConfig(DISTANCES[distance], int(dims), comp, int(rescore_limit), int(device),
+                         VARIANTS[variant], int(id_base), root_path, int(pqc.get("segments", 0)),
+                         int(pqc.get("centroids", 256)), int(pqc.get("trainingLimit", 100000)),
+                         1 if pqc.get("rescore", True) else 0)
+
+
+def validate_user_config_update(initial: dict, updated: dict) -> None:
+    """flat.ValidateUserConfigUpdate (flat/index.go:1106-1154); dicts of
+    make_config keyword arguments.  Raises WeaviateError on an immutable change."""
+    a, b = make_config(**initial), make_config(**updated)
+    check(_lib.load().wv_validate_user_config_update(C.byref(a), C.byref(b)))
+
+
 class FlatIndex:
     """flat.New (flat/index.go:76-125) with the VectorIndex surface used on the
     hot path: Add, AddBatch, Delete, SearchByVector, SearchByVectorDistance,
@@ -66,24 +95,11 @@ class FlatIndex:
     def __init__(self, distance: str = "cosine", dims: int = 0, device: int = 0, variant: str = "auto",
                  root_path: str = "", id_base: int = 0, bq: bool = False, rescore_limit: int = -1,
                  pq: Optional[dict] = None, rq: Optional[dict] = None):
-        if distance not in DISTANCES:
-            raise WeaviateError(_lib.WV_ERR_INVALID, f"unrecognized or unsupported distance metric {distance!r}")
         self._l = _lib.load()
         self._root = root_path.encode()
-        # pq: ent.PQConfig subset {"segments", "centroids" (256), "trainingLimit" (100000), "rescore" (True)}
-        pqc = dict(pq or {})
-        # rq: flatent RQ config subset {"bits": 8 | 1} (entities/vectorindex/flat/config.go:27, :199-201);
-        # its RescoreLimit is `rescore_limit`
-        rqc = dict(rq or {})
-        if rq is not None and int(rqc.get("bits", 8)) not in (1, 8):
-            raise WeaviateError(_lib.WV_ERR_INVALID, "rq bits must be 1 or 8")
-        comp = (_lib.COMPRESSION_BQ if bq else _lib.COMPRESSION_PQ if pq is not None
-                else (_lib.COMPRESSION_RQ8 if int(rqc.get("bits", 8)) == 8 else _lib.COMPRESSION_RQ1)
-                if rq is not None else _lib.COMPRESSION_NONE)
-        cfg = _lib.WvConfig(DISTANCES[distance], int(dims), comp, int(rescore_limit), int(device),
-                            VARIANTS[variant], int(id_base), self._root, int(pqc.get("segments", 0)),
-                            int(pqc.get("centroids", 256)), int(pqc.get("trainingLimit", 100000)),
-                            1 if pqc.get("rescore", True) else 0)
+        self._cfg_args = dict(distance=distance, dims=dims, device=device, variant=variant, root_path=self._root,
+                              id_base=id_base, bq=bq, rescore_limit=rescore_limit, pq=pq, rq=rq)
+        cfg = make_config(**self._cfg_args)
         h = C.c_void_p()
         check(self._l.wv_index_create(C.byref(cfg), C.byref(h)))
         self._h = h
@@ -260,6 +276,48 @@ class FlatIndex:
         return int(self._l.wv_index_dims(self._h))
 
     # -- search path ------------------------------------------------------
+    # -- rest of db.VectorIndex (vector_index.go:25-54) -----------------------
+    def iterate(self, fn) -> None:
+        """flat.Iterate (flat/index.go:1057-1079): fn(id) -> bool, ascending ids."""
+        cb = _lib.ITERATE_FN(lambda i, _u: 1 if fn(int(i)) else 0)
+        check(self._l.wv_index_iterate(self._h, C.cast(cb, C.c_void_p), None))
+
+    def query_vector_distances(self, query, ids, per_id_status: bool = False):
+        """flat.QueryVectorDistancer(query).DistanceFunc over ids
+        (flat/index.go:1160-1240).  per_id_status: -> (dists, rc[]) instead of
+        raising on the first missing id."""
+        q = np.ascontiguousarray(query, dtype=np.float32).ravel()
+        i = np.ascontiguousarray(ids, dtype=np.uint64).ravel()
+        out = np.zeros(i.size, np.float32)
+        rc = np.zeros(i.size, np.int32) if per_id_status else None
+        check(self._l.wv_index_query_distances(self._h, _fptr(q), q.size, i.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                               i.size, _fptr(out), _iptr(rc) if rc is not None else None))
+        return (out, rc) if per_id_status else out
+
+    def query_vector_distancer(self, query):
+        """-> DistanceFunc(id) like common.QueryVectorDistancer."""
+        return lambda doc_id: float(self.query_vector_distances(query, [doc_id])[0])
+
+    def preload(self, id: int, vector) -> None:  # flat/index.go:844-865
+        v = np.ascontiguousarray(vector, dtype=np.float32).ravel()
+        check(self._l.wv_index_preload(self._h, int(id), _fptr(v), v.size))
+
+    def update_user_config(self, **updated) -> None:
+        """flat.UpdateUserConfig (flat/index.go:763-776), after
+        ValidateUserConfigUpdate against the current config."""
+        new = dict(self._cfg_args, **updated)
+        validate_user_config_update(self._cfg_args, new)
+        cfg = make_config(**new)
+        check(self._l.wv_index_update_user_config(self._h, C.byref(cfg)))
+        self._cfg_args = new
+        self.rescore_limit = int(new["rescore_limit"])
+
+    def compression_stats(self) -> dict:  # flat/index.go:1246-1249
+        buf = C.create_string_buffer(32)
+        ratio = C.c_double(0)
+        check(self._l.wv_index_compression_stats(self._h, buf, 32, C.byref(ratio)))
+        return {"type": buf.value.decode(), "ratio": ratio.value}
+
     def search_by_vector_batch(self, queries, k: int, allow: Optional[AllowList] = None):
         """SearchByVector for each row of `queries` (flat/index.go:423-448).
         Returns (ids[nq,k] uint64, dists[nq,k] float32, counts[nq] int32)."""
