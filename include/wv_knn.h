@@ -203,7 +203,7 @@ int wv_index_rq_distances(wv_index *idx, const float *queries, int64_t nq, int64
  * mode 0: like SearchByVector (kout = k, tie cases resolved by heap replay).
  * mode 1: shard-local candidates: kout = k+1 verified results per query and
  *         d_flags[q] = 1 where the query needs the cross-shard replay.
- * stream: hipStream_t to order against (NULL = the index's own stream). */
+ * stream: hipStream_t to order against (NULL = the null stream). */
 int wv_index_search_device(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k, int32_t mode,
                            uint64_t *d_ids, float *d_dists, int32_t *d_counts, int32_t *d_flags, void *stream);
 
@@ -218,6 +218,17 @@ int wv_index_replay(wv_index *idx, const float *d_queries, int64_t nq, int64_t d
                     const int32_t *h_qlist, int32_t nlist, const uint64_t *h_in_ids, const float *h_in_dists,
                     const int32_t *h_in_len, int32_t extract, uint64_t *h_out_ids, float *h_out_dists,
                     int32_t *h_out_len);
+/* wv_index_replay on device buffers, ordered on `stream` (NULL = the null
+ * stream), no host synchronisation: d_qlist[nlist], heap states
+ * d_in_* / d_out_* [nlist x k] in layout order (d_in_len NULL = empty heaps);
+ * extract=1 writes ascending results by list position.  When the index's last
+ * search was wv_index_search_device over the same nq queries (no write since),
+ * its block keys bound the scan (only blocks that can insert are visited);
+ * otherwise every row's exact distance is computed. */
+int wv_index_replay_device(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k,
+                           const int32_t *d_qlist, int32_t nlist, const uint64_t *d_in_ids, const float *d_in_dists,
+                           const int32_t *d_in_len, int32_t extract, uint64_t *d_out_ids, float *d_out_dists,
+                           int32_t *d_out_len, void *stream);
 
 /* Sharded BQ search (flat.searchByVectorQuantized over contiguous id-range
  * shards): the reference R-heap (flat/index.go:470-487) runs

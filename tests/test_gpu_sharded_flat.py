@@ -9,10 +9,15 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("stale", [False, True])
 @pytest.mark.parametrize("shards,metric,kind,n,d,k", [(2, "cosine", 0, 12000, 768, 10),
                                                      (3, "l2-squared", 1, 6000, 64, 10),   # integer data: ties
-                                                     (4, "dot", 0, 5000, 100, 24)])
-def test_sharded_flat_protocol_equals_single_index(wv, oracle, shards, metric, kind, n, d, k):
+                                                     (4, "dot", 0, 5000, 100, 24),
+                                                     (2, "l2-squared", 1, 20000, 32, 100)])
+def test_sharded_flat_protocol_equals_single_index(wv, oracle, shards, metric, kind, n, d, k, stale):
+    """stale=False: each shard's replay is bounded by the block keys of its
+    local search (k_blk_replay with a handed-over heap); stale=True: another
+    search in between invalidates them, every row is scanned (run_replay)."""
     from weaviate_amd.sharded import GpuShardBackend
     dev = torch.device("cuda", 0)
     data = oracle.gen_matrix(kind, 41, 0, n, d)
@@ -28,16 +33,19 @@ def test_sharded_flat_protocol_equals_single_index(wv, oracle, shards, metric, k
     parts = [b.local_search(q, k) for b in backs]
     gi, gd, gc, gf = (torch.stack([p[j] for p in parts]) for j in range(4))
     oi, od, on, of = backs[0].merge(shards, k, gi, gd, gc, gf)
-    flagged = torch.nonzero(of).flatten().cpu().numpy()
-    oi, od, on = oi.cpu().numpy(), od.cpu().numpy(), on.cpu().numpy()
-    if flagged.size:
+    if stale:
+        for b in backs:
+            b.index.search_by_vector_batch(queries[:1], 1)
+    flagged = torch.nonzero(of).flatten().to(torch.int32)
+    if kind == 1:
+        assert flagged.numel() > 0  # integer data: the replay chain must run
+    if flagged.numel():
         state = None
         for r, b in enumerate(backs):
             state = b.replay(q, flagged, state, k, r == shards - 1)
-        fi, fd, fn = state
-        oi[flagged] = fi.view(np.int64)
-        od[flagged] = fd
-        on[flagged] = fn
+        rows = flagged.long()
+        oi[rows], od[rows], on[rows] = state
+    oi, od, on = oi.cpu().numpy(), od.cpu().numpy(), on.cpu().numpy()
     single = wv.FlatIndex(distance=metric, variant="avx256")
     single.add_batch(np.arange(n, dtype=np.uint64), data)
     si, sd, sn = single.search_by_vector_batch(queries, k)

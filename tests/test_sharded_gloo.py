@@ -92,6 +92,9 @@ class OracleShardBackend:
 
         class H(C.Structure):
             _fields_ = [("id", C.POINTER(C.c_uint64)), ("dist", C.POINTER(C.c_float)), ("len", C.c_int)]
+        qlist = qlist.numpy()
+        if state is not None:
+            state = (state[0].numpy().view(np.uint64), state[1].numpy(), state[2].numpy())
         nl = len(qlist)
         oi = np.zeros((nl, k), np.uint64)
         od = np.zeros((nl, k), np.float32)
@@ -118,7 +121,7 @@ class OracleShardBackend:
                 oi[li, :h.len] = hid[:h.len]
                 od[li, :h.len] = hd[:h.len]
                 on[li] = h.len
-        return oi, od, on
+        return torch.from_numpy(oi.view(np.int64)), torch.from_numpy(od), torch.from_numpy(on)
 
 
 def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath):

@@ -653,14 +653,19 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
                                                     const uint32_t* __restrict__ qsmax, const uint32_t* __restrict__ maxn2,
                                                     float gd, float gacc, uint32_t* __restrict__ cand,
                                                     int32_t* __restrict__ ncand, int32_t* __restrict__ flags,
-                                                    float* __restrict__ eps_out) {
+                                                    float* __restrict__ eps_out, const int32_t* __restrict__ qlist,
+                                                    const uint32_t* __restrict__ qcount) {
     constexpr int L = 64 * (R - 1);
     constexpr int U = 16;
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int q = blockIdx.x * 4 + w;
+    int q = blockIdx.x * 4 + w;
+    if (qlist) {  // second pass over the listed queries (qcount[1] of them)
+        if ((uint32_t)q >= qcount[1]) return;
+        q = qlist[q];
+    }
     if (q >= nq) return;
     const float4 qi = qinfo[q];
     const float eps = qs_eps(metric, qi, qsmax, maxn2, gd, gacc);
@@ -714,7 +719,8 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
                                                    const uint32_t* __restrict__ cand, const int32_t* __restrict__ ncand,
                                                    int nq, int k, int kout, uint64_t id_base, uint64_t* __restrict__ out_ids,
                                                    float* __restrict__ out_d, int32_t* __restrict__ out_n,
-                                                   int32_t* __restrict__ flags) {
+                                                   int32_t* __restrict__ flags, const int32_t* __restrict__ qlist,
+                                                   const uint32_t* __restrict__ qcount) {
     constexpr int L = 64 * (R - 1);
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
@@ -723,7 +729,11 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     __shared__ int snv[4];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int q = blockIdx.x;
+    int q = blockIdx.x;
+    if (qlist) {
+        if ((uint32_t)q >= qcount[1]) return;
+        q = qlist[q];
+    }
     if (q >= nq) return;
     if (flags[q]) return;  // overflowed selection: the replay resolves it
     const int nc = ncand[q];
@@ -788,12 +798,13 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     if (lane == 0) out_n[q] = nout;
 }
 
-// flagged queries -> list (order irrelevant: every listed query is replayed
-// independently); counters[0] += count, counters[1] = count (this batch)
+// flagged queries -> list (order irrelevant: every listed query is handled
+// independently); want = 0: every nonzero flag, else flags == want.
+// counters[0] += count, counters[1] = count (this batch)
 __global__ void k_flag_list(const int32_t* __restrict__ flags, int nq, int32_t* __restrict__ qlist,
-                            uint32_t* __restrict__ counters) {
+                            uint32_t* __restrict__ counters, int want) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool f = q < nq && flags[q] != 0;
+    const bool f = q < nq && (want ? flags[q] == want : flags[q] != 0);
     const uint64_t m = __ballot(f);
     if (m == 0) return;
     const int lane = threadIdx.x & 63;
@@ -819,16 +830,20 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
                                                    const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
                                                    int64_t nrows, const float* __restrict__ Qn, int d,
                                                    const int32_t* __restrict__ qlist, const uint32_t* __restrict__ counters,
-                                                   int k, int kout, uint64_t id_base, uint64_t* __restrict__ out_ids,
-                                                   float* __restrict__ out_d, int32_t* __restrict__ out_n) {
+                                                   int nlist, int k, int kout, uint64_t id_base,
+                                                   uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
+                                                   int32_t* __restrict__ out_n, const uint64_t* __restrict__ in_ids,
+                                                   const float* __restrict__ in_d, const int32_t* __restrict__ in_len,
+                                                   int extract, int by_list) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
     float* s_d = reinterpret_cast<float*>(hid + k);
     float* hd = s_d + 64;
     int* s_len = reinterpret_cast<int*>(hd + k);
     const int lane = threadIdx.x;
-    if ((uint32_t)blockIdx.x >= counters[1]) return;
-    const int q = qlist[blockIdx.x];
+    const int li_ = blockIdx.x;  // list position
+    if (counters ? (uint32_t)li_ >= counters[1] : li_ >= nlist) return;
+    const int q = qlist[li_];
     const int metric = METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2;
     const float4 qi = qinfo[q];
     const bool noskip = qi.w != 0.f;
@@ -836,7 +851,14 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     const float* kr = key + (int64_t)q * ldk;
     const float* qv = Qn + (int64_t)q * dpad;
     const int li = lane & 31, lh = lane >> 5;
-    if (lane == 0) *s_len = 0;
+    // the heap handed over by the previous shard (layout order), or empty
+    int len_in = in_len ? in_len[li_] : 0;
+    len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
+    for (int i = lane; i < len_in; i += 64) {
+        hid[i] = in_ids[(int64_t)li_ * k + i];
+        hd[i] = in_d[(int64_t)li_ * k + i];
+    }
+    if (lane == 0) *s_len = len_in;
     __syncthreads();
     // block keys in rounds of 64 * RU: all loads of a round in flight at once,
     // parked in LDS; a round with no visitable block is skipped whole
@@ -913,15 +935,25 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
         }
     }
     }
-    if (lane == 0) {
+    const int64_t orow = by_list ? li_ : q;
+    if (!extract) {  // hand the heap on in layout order (kout == k)
+        const int n = *s_len;
+        for (int i = lane; i < n; i += 64) {
+            out_ids[orow * kout + i] = hid[i];
+            out_d[orow * kout + i] = hd[i];
+        }
+        if (lane == 0) out_n[orow] = n;
+        return;
+    }
+    if (lane == 0) {  // extractHeap (flat/index.go:676-688): pops max-first into the tail
         ReplayHeap h{hid, hd, *s_len};
         const int n = h.len;
         for (int i = n - 1; i >= 0; i--) {
             uint64_t x; float y;
             rh_pop(h, &x, &y);
-            if (i < kout) { out_ids[(int64_t)q * kout + i] = x; out_d[(int64_t)q * kout + i] = y; }
+            if (i < kout) { out_ids[orow * kout + i] = x; out_d[orow * kout + i] = y; }
         }
-        out_n[q] = n < kout ? n : kout;
+        out_n[orow] = n < kout ? n : kout;
     }
 }
 

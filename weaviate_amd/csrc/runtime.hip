@@ -150,12 +150,17 @@ struct wv_index {
     int use_qs = 0, qs_planes = 0, dpb = 0;
     uint16_t* Xb = nullptr;
     uint32_t* qsmax = nullptr;      // device [4]: max |x - x_h|^2, max |x_h|^2 (float bits), non-finite flag
-    uint32_t* qscount = nullptr;    // device [4]: [0] replayed queries (cumulative), [1] this batch's flagged
+    uint32_t* qscount = nullptr;    // device [4]: [0] replayed queries (cumulative), [1] this batch's flagged,
+                                    // [2] overflow second passes (cumulative), [3] this batch's
     int has_nonfinite = 0;          // host mirror of qsmax[2]
     uint64_t replayed_host = 0;     // replays counted on the host (legacy paths)
     int timed = 0;                  // ev0/ev1 bracket the last batch's dominant kernel
     int timed_total = 0;            // evt0/evt1 bracket the last batch's whole block-key pipeline
     int64_t qs_last_nq = 0, qs_last_nb = 0, qs_last_ldk = 0;  // first chunk of the last block-key batch (debug hook)
+    // > 0: the block keys / eps / query planes of the last search (nq queries,
+    // one chunk, no allow list) still describe the stored rows -- the
+    // cross-shard replay may bound its scan with them.  Reset by any write or search.
+    int64_t qs_keys_nq = 0;
     hipEvent_t evt0 = nullptr, evt1 = nullptr;
     float last_eps_scale = 0.f, last_eps_base = 0.f;  // exactness-proof eps of the last MFMA batch (debug hook)
     int64_t last_nq = 0;
@@ -573,6 +578,7 @@ static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs
         last[ids[i]] = i;
         maxslot = std::max<int64_t>(maxslot, (int64_t)s);
     }
+    idx->qs_keys_nq = 0;
     rc = ensure_capacity(idx, maxslot + 1);
     if (rc) return rc;
     std::vector<int64_t> rows;
@@ -642,6 +648,7 @@ extern "C" int wv_index_add_range_device(wv_index* idx, uint64_t first_id, const
         if (rc) return rc;
     }
     const int64_t s0 = (int64_t)s0u;
+    idx->qs_keys_nq = 0;
     rc = ensure_capacity(idx, s0 + n);
     if (rc) return rc;
     std::vector<uint32_t> hs((size_t)n);
@@ -664,6 +671,7 @@ extern "C" int wv_index_delete(wv_index* idx, const uint64_t* ids, int64_t n) {
     if (!idx) return set_err(WV_ERR_INVALID, "nil index");
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
+    idx->qs_keys_nq = 0;
     bool dirty = false;
     for (int64_t i = 0; i < n; i++) {
         if (ids[i] < idx->id_base) continue;
@@ -1123,7 +1131,7 @@ extern "C" int wv_index_bq_begin(wv_index* idx, const float* d_queries, int64_t 
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
     if (idx->compression != WV_COMPRESSION_BQ) return set_err(WV_ERR_INVALID, "bq_begin: index is not BQ-compressed");
-    hipStream_t s = stream ? (hipStream_t)stream : idx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
     int R = 0;
     int64_t G = 0;
     int rc = bq_begin(idx, s, d_queries, nq, d, k, &R, &G);
@@ -1148,7 +1156,7 @@ extern "C" int wv_index_bq_replay(wv_index* idx, const uint64_t* d_in_ids, const
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
     if (idx->bq_nq <= 0) return set_err(WV_ERR_INVALID, "bq_replay: no batch begun");
-    hipStream_t s = stream ? (hipStream_t)stream : idx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
     int rc = bq_replay(idx, s, idx->present, 0, (int)idx->bq_nq, d_in_ids, d_in_d, d_in_len, pop, d_out_ids, d_out_d,
                        d_out_len);
     if (rc) return rc;
@@ -1162,7 +1170,7 @@ extern "C" int wv_index_bq_rescore(wv_index* idx, const uint64_t* d_ids, const i
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
     if (idx->bq_nq <= 0) return set_err(WV_ERR_INVALID, "bq_rescore: no batch begun");
-    hipStream_t s = stream ? (hipStream_t)stream : idx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
     int rc = bq_rescore(idx, s, d_ids, d_len, d_E);
     if (rc) return rc;
     if (!stream) HIPCHK(hipStreamSynchronize(s));
@@ -1934,10 +1942,10 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     HIPCHK(idx->qsQb.ensure((size_t)qc * idx->dpb * sizeof(uint16_t)));
     HIPCHK(idx->qsInfo.ensure((size_t)qc * sizeof(float4)));
     HIPCHK(idx->qsKey.ensure((size_t)qc * ldk * sizeof(float)));
-    HIPCHK(idx->qsCand.ensure((size_t)qc * L * sizeof(uint32_t)));
+    HIPCHK(idx->qsCand.ensure((size_t)qc * std::max(L, 448) * sizeof(uint32_t)));  // 448: the overflow pass
     HIPCHK(idx->qsNc.ensure((size_t)qc * sizeof(int32_t)));
     HIPCHK(idx->qsEps.ensure((size_t)qc * sizeof(float)));
-    HIPCHK(idx->qsList.ensure((size_t)qc * sizeof(int32_t)));
+    HIPCHK(idx->qsList.ensure((size_t)2 * qc * sizeof(int32_t)));
     if (!o_flags) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
     const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
     if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
@@ -2027,29 +2035,40 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         idx->stats.mfma_launches++;
         // ---- candidate blocks, exact rows, proof ----
         int32_t* flags = o_flags ? o_flags + c0 : idx->qsFlags.as<int32_t>();
-        const unsigned gw = (unsigned)((cn + 3) / 4);
-#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>())
-        if (R == 2) WV_SELR(2); else if (R == 4) WV_SELR(4); else WV_SELR(8);
+        int32_t* olist = idx->qsList.as<int32_t>() + qc;  // second half: the overflow list
+        // pass RV over all queries (list == nullptr) or over the listed ones
+        auto blk_pass = [&](int RV, const int32_t* list, const uint32_t* cnt) {
+            const unsigned gw = (unsigned)((cn + 3) / 4);
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt)
+            if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
 #undef WV_SELR
-#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags)
+#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags, list, cnt)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \
     case L2: if (v5) WV_EXR(RV, L2, AVX512); else WV_EXR(RV, L2, AVX256); break;   \
     case DOT: if (v5) WV_EXR(RV, DOT, AVX512); else WV_EXR(RV, DOT, AVX256); break; \
     default: if (v5) WV_EXR(RV, COSINE, AVX512); else WV_EXR(RV, COSINE, AVX256); break; \
     }
-        if (R == 2) { WV_EXM(2); } else if (R == 4) { WV_EXM(4); } else { WV_EXM(8); }
+            if (RV == 2) { WV_EXM(2); } else if (RV == 4) { WV_EXM(4); } else { WV_EXM(8); }
 #undef WV_EXM
 #undef WV_EXR
+        };
+        blk_pass(R, nullptr, nullptr);
         HIPCHK(hipGetLastError());
+        if (R < 8) {  // candidate lists that overflowed (flag 2): again with the 448-block lists
+            HIPCHK(hipMemsetAsync(idx->qscount + 3, 0, sizeof(uint32_t), s));
+            k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, olist, idx->qscount + 2, 2);
+            blk_pass(8, olist, idx->qscount + 2);
+            HIPCHK(hipGetLastError());
+        }
         if (mode == 1) continue;
         // ---- flagged queries: the exact heap replay, bounded by the block keys ----
         HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
-        k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount);
+        k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount, 0);
 #define WV_RP(M, V)                                                                                             \
     do {                                                                                                        \
         if (rlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); \
-        k_blk_replay<M, V><<<(unsigned)cn, 64, rlds, s>>>(a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsList.as<int32_t>(), idx->qscount, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0); \
+        k_blk_replay<M, V><<<(unsigned)cn, 64, rlds, s>>>(a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsList.as<int32_t>(), idx->qscount, 0, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, nullptr, nullptr, nullptr, 1, 0); \
     } while (0)
         switch (metric) {
         case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;
@@ -2063,6 +2082,7 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         HIPCHK(hipEventRecord(idx->evt1, s));
         idx->timed_total = 1;
     }
+    if (qc >= nq && valid == idx->present) idx->qs_keys_nq = nq;
     return WV_OK;
 }
 
@@ -2073,6 +2093,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
                        const uint32_t* valid, int64_t n_valid, uint64_t* o_ids, float* o_d, int32_t* o_n,
                        int32_t* o_flags) {
     const int kout = mode == 1 ? k + 1 : k;
+    idx->qs_keys_nq = 0;
     if (nq <= 0) return WV_OK;
     if (n_valid == 0 || idx->dims == 0) {
         HIPCHK(hipMemsetAsync(o_n, 0, (size_t)nq * sizeof(int32_t), s));
@@ -2428,7 +2449,7 @@ extern "C" int wv_index_search_device(wv_index* idx, const float* d_queries, int
     if (mode == 1 && !d_flags) return set_err(WV_ERR_INVALID, "mode 1 needs d_flags");
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : idx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
     int rc = search_core(idx, s, d_queries, nq, d, k, mode, idx->present, idx->npresent, d_ids, d_dists, d_counts,
                          mode == 1 ? d_flags : nullptr);
     if (rc) return rc;
@@ -2484,6 +2505,55 @@ extern "C" int wv_index_replay(wv_index* idx, const float* d_queries, int64_t nq
     HIPCHK(hipMemcpyAsync(h_out_len, outN, (size_t)nlist * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return WV_OK;
+}
+
+// wv_index_replay on device buffers (no host hops, stream-ordered).  With the
+// block keys of this index's last search over the same nq queries still valid
+// (qs_keys_nq), the scan visits only blocks that can insert (k_blk_replay);
+// otherwise every row's exact distance is computed (run_replay).
+extern "C" int wv_index_replay_device(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                      const int32_t* d_qlist, int32_t nlist, const uint64_t* d_in_ids,
+                                      const float* d_in_dists, const int32_t* d_in_len, int32_t extract,
+                                      uint64_t* d_out_ids, float* d_out_dists, int32_t* d_out_len, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0 || nlist < 0) return set_err(WV_ERR_INVALID, "invalid k / list");
+    if (nlist > 0 && (!d_qlist || !d_out_ids || !d_out_dists || !d_out_len)) return set_err(WV_ERR_INVALID, "nil buffer");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
+    if (nlist == 0) return WV_OK;
+    const bool have_data = idx->dims != 0 && idx->npresent > 0;
+    if (have_data && d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
+    const bool keyed = have_data && idx->qs_keys_nq == nq && rlds <= 160 * 1024;
+    if (keyed) {
+        const int metric = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+        const bool v5 = idx->variant == WV_VARIANT_AVX512;
+        const float* Qn = idx->qn.as<float>();  // the prepared rows of that batch
+#define WV_RP(M, V)                                                                                             \
+    do {                                                                                                        \
+        if (rlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); \
+        k_blk_replay<M, V><<<(unsigned)nlist, 64, rlds, s>>>(idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb, idx->qsEps.as<float>(), idx->qsInfo.as<float4>(), idx->X, idx->dpad, idx->present, idx->hiwater, Qn, idx->dims, d_qlist, nullptr, nlist, k, k, idx->id_base, d_out_ids, d_out_dists, d_out_len, d_in_ids, d_in_dists, d_in_len, extract, 1); \
+    } while (0)
+        switch (metric) {
+        case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;
+        case DOT: if (v5) WV_RP(DOT, AVX512); else WV_RP(DOT, AVX256); break;
+        default: if (v5) WV_RP(COSINE, AVX512); else WV_RP(COSINE, AVX256); break;
+        }
+#undef WV_RP
+        HIPCHK(hipGetLastError());
+        return WV_OK;
+    }
+    const float* Qn = nullptr;
+    if (have_data) {
+        int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QB));
+        if (rc) return rc;
+        Qn = idx->qn.as<float>();
+    }
+    // run_replay reads in-state when in_n != nullptr; list-ordered outputs
+    return run_replay(idx, s, idx->present, Qn, d_qlist, nlist, k, d_in_ids, d_in_dists, d_in_len, extract, 0, k,
+                      d_out_ids, d_out_dists, d_out_len);
 }
 
 extern "C" int wv_merge_shards(int32_t device, int32_t nshards, int64_t nq, int32_t k, const uint64_t* d_ids,

@@ -21,7 +21,6 @@ interface so the protocol can be exercised on CPU.
 """
 from __future__ import annotations
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -60,25 +59,21 @@ class GpuShardBackend:
                                             of.data_ptr(), s))
         return oi, od, on, of
 
-    def replay(self, q: torch.Tensor, qlist: np.ndarray, state, k: int, extract: bool):
-        import ctypes as C
-        nl = len(qlist)
-        ql = np.ascontiguousarray(qlist, dtype=np.int32)
-        oi = np.zeros((nl, k), dtype=np.uint64)
-        od = np.zeros((nl, k), dtype=np.float32)
-        on = np.zeros(nl, dtype=np.int32)
-        pu, pf, pi = C.POINTER(C.c_uint64), C.POINTER(C.c_float), C.POINTER(C.c_int32)
-        if state is None:
-            ii, idd, il = None, None, None
-        else:
-            si = np.ascontiguousarray(state[0], dtype=np.uint64)
-            sd = np.ascontiguousarray(state[1], dtype=np.float32)
-            sn = np.ascontiguousarray(state[2], dtype=np.int32)
-            ii, idd, il = si.ctypes.data_as(pu), sd.ctypes.data_as(pf), sn.ctypes.data_as(pi)
-        torch.cuda.current_stream(self.dev).synchronize()
-        self._check(self._l.wv_index_replay(self.index._h, q.data_ptr(), q.shape[0], q.shape[1], k,
-                                            ql.ctypes.data_as(pi), nl, ii, idd, il, 1 if extract else 0,
-                                            oi.ctypes.data_as(pu), od.ctypes.data_as(pf), on.ctypes.data_as(pi)))
+    def replay(self, q: torch.Tensor, qlist: torch.Tensor, state, k: int, extract: bool):
+        """Continue the reference heap over this shard for the listed query rows
+        (wv_index_replay_device: device tensors in and out, stream-ordered).
+        state: (ids int64 [nl, k], dists float32 [nl, k], len int32 [nl]) in
+        heap layout order, or None for empty heaps."""
+        nl = int(qlist.numel())
+        oi = torch.empty((nl, k), dtype=torch.int64, device=self.dev)
+        od = torch.empty((nl, k), dtype=torch.float32, device=self.dev)
+        on = torch.empty(nl, dtype=torch.int32, device=self.dev)
+        si, sd, sl = (None, None, None) if state is None else (state[0].data_ptr(), state[1].data_ptr(),
+                                                               state[2].data_ptr())
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        self._check(self._l.wv_index_replay_device(self.index._h, q.data_ptr(), q.shape[0], q.shape[1], k,
+                                                   qlist.data_ptr(), nl, si, sd, sl, 1 if extract else 0,
+                                                   oi.data_ptr(), od.data_ptr(), on.data_ptr(), s))
         return oi, od, on
 
 
@@ -194,22 +189,20 @@ class ShardedFlatSearch:
         gc = self._all_gather(cnt)
         gf = self._all_gather(flg)
         oi, od, on, of = self.b.merge(self.world, k, gi, gd, gc, gf)
-        flagged = torch.nonzero(of).flatten().cpu().numpy()
-        if flagged.size:
+        flagged = torch.nonzero(of).flatten().to(torch.int32)  # (the one host sync: the list length)
+        if flagged.numel():
             oi, od, on = self._replay_chain(q, k, flagged, oi, od, on)
         return oi, od, on
 
     def _replay_chain(self, q, k, qlist, oi, od, on):
-        """Exact heap replay across ranks in id order (rank 0 first)."""
-        nl = len(qlist)
+        """Exact heap replay across ranks in id order (rank 0 first); heap
+        states move rank to rank as device tensors over the collective."""
+        nl = int(qlist.numel())
         state = None
         for r in range(self.world):
             extract = r == self.world - 1
             if self.rank == r:
-                si, sd, sn = self.b.replay(q, qlist, state, k, extract)
-                ti = torch.from_numpy(si.view(np.int64)).to(self.dev)
-                td = torch.from_numpy(sd).to(self.dev)
-                tn = torch.from_numpy(sn).to(self.dev)
+                ti, td, tn = self.b.replay(q, qlist, state, k, extract)
             else:
                 ti = torch.empty((nl, k), dtype=torch.int64, device=self.dev)
                 td = torch.empty((nl, k), dtype=torch.float32, device=self.dev)
@@ -217,10 +210,10 @@ class ShardedFlatSearch:
             dist.broadcast(ti, src=r)
             dist.broadcast(td, src=r)
             dist.broadcast(tn, src=r)
-            state = (ti.cpu().numpy().view(np.uint64), td.cpu().numpy(), tn.cpu().numpy())
+            state = (ti, td, tn)
         fi, fd, fn = state
-        idx = torch.from_numpy(qlist.astype(np.int64)).to(oi.device)
-        oi[idx] = torch.from_numpy(fi.view(np.int64)).to(oi.device)
-        od[idx] = torch.from_numpy(fd).to(od.device)
-        on[idx] = torch.from_numpy(fn).to(on.device)
+        rows = qlist.to(torch.int64)
+        oi[rows] = fi
+        od[rows] = fd
+        on[rows] = fn
         return oi, od, on
