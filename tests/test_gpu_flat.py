@@ -349,3 +349,27 @@ def test_bf16x3_error_within_proof_bound(wv, oracle, metric, kind, d):
     print(f"bf16x3 max |A-E| / eps = {ratio:.4f}")
     assert (err <= bound).all(), f"max err/eps = {ratio}"
     idx.close()
+
+
+@pytest.mark.parametrize("k", [1, 10, 50, 63, 64])
+def test_block_key_replay_parallel_and_single_wave(wv, oracle, k):
+    """Integer data (exact ties everywhere): most queries go to the heap replay.
+    k < 64: k_blk_replay_par (8-wave candidate scan), else / replay_par=0: the
+    one-wave k_blk_replay; both equal the reference heap, including queries with
+    non-finite values (every block visited)."""
+    n, d = 60000, 24
+    data = gen(oracle, 1, 91, n, d)
+    queries = gen(oracle, 1, 92, 40, d)
+    queries[3, 5] = np.nan
+    queries[7, 0] = np.inf
+    res = []
+    for par in (1, 0):
+        idx, orc = build_pair(wv, oracle, "l2-squared", "avx256", data)
+        idx.set_option("replay_par", par)
+        before = idx.stats()["replayed_queries"]
+        res.append(idx.search_by_vector_batch(queries, k))
+        assert idx.stats()["replayed_queries"] - before >= 2  # at least the non-finite queries
+    for qi in range(len(queries)):
+        exp = orc.search(queries[qi], k)
+        for ids, dists, counts in res:
+            assert_same(exp, ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"k{k} q{qi}")

@@ -957,4 +957,266 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_blk_replay_par<METRIC, VARIANT>: the exact heap replay of k_blk_replay for
+// k < 64 with the block-key scan spread over 8 waves (latency: a lone flagged
+// query no longer walks every block key in one wave).
+//   1. every wave: per chunk of 1024 blocks, the lane minima of U = A + eps
+//      (16 blocks per lane) -> scratch; each is the exact-distance upper bound
+//      of one distinct row;
+//   2. wave 0: Uc[c] = k-th smallest of the minima of chunks < c and of the
+//      handed-over heap -- an upper bound of the heap top at chunk c (the heap
+//      holds the k smallest distances seen, flat/index.go:665-674);
+//   3. every wave: candidate blocks A - eps < Uc[c] (a superset of the blocks
+//      the reference scan can insert from), compacted in block order in LDS;
+//   4. wave 0: the heap replay over the candidates only, visiting a block iff
+//      the heap is short or top > A - eps (exactly k_blk_replay's rule).
+// Non-finite queries and lists beyond RP_CAP fall back to every block in 4.
+// ---------------------------------------------------------------------------
+constexpr int RP_NW = 8, RP_CH = 1024, RP_CAP = 6144, RP_MAXCH = 4096;
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(512) void k_blk_replay_par(const float* __restrict__ key, int64_t ldk, int64_t nb,
+                                                        const float* __restrict__ eps_q, const float4* __restrict__ qinfo,
+                                                        const float* __restrict__ X, int dpad,
+                                                        const uint32_t* __restrict__ valid, int64_t nrows,
+                                                        const float* __restrict__ Qn, int d,
+                                                        const int32_t* __restrict__ qlist,
+                                                        const uint32_t* __restrict__ counters, int nlist, int k, int kout,
+                                                        uint64_t id_base, uint64_t* __restrict__ out_ids,
+                                                        float* __restrict__ out_d, int32_t* __restrict__ out_n,
+                                                        const uint64_t* __restrict__ in_ids,
+                                                        const float* __restrict__ in_d,
+                                                        const int32_t* __restrict__ in_len, int extract, int by_list,
+                                                        float* __restrict__ scratch) {
+    __shared__ uint64_t hid[64];
+    __shared__ float hd[64];
+    __shared__ float s_d[64];
+    __shared__ int s_len, s_total;
+    __shared__ uint32_t scand[RP_CAP];
+    __shared__ float slb[RP_CAP];
+    __shared__ float suc[RP_MAXCH];
+    __shared__ int scc[RP_MAXCH];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int metric = METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2;
+    const int count = counters ? (int)counters[1] : nlist;
+    const int nch = (int)((nb + RP_CH - 1) / RP_CH);
+    float* sc = scratch + (int64_t)blockIdx.x * nch * 64;
+    const int li = lane & 31, lh = lane >> 5;
+    for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
+        const int q = qlist[li_];
+        const float4 qi = qinfo[q];
+        const bool noskip = qi.w != 0.f;
+        const float eps = eps_q[q];
+        const float* kr = key + (int64_t)q * ldk;
+        const float* qv = Qn + (int64_t)q * dpad;
+        int len_in = in_len ? in_len[li_] : 0;
+        len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
+        if (w == 0) {
+            if (lane < len_in) {
+                hid[lane] = in_ids[(int64_t)li_ * k + lane];
+                hd[lane] = in_d[(int64_t)li_ * k + lane];
+            }
+            if (lane == 0) s_len = len_in;
+        }
+        // 1. lane minima of the upper bounds per chunk
+        if (!noskip) {
+            for (int c = w; c < nch; c += RP_NW) {
+                float kv[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
+                    kv[u] = bb < nb ? kr[bb] : __builtin_inff();
+                }
+                float m = __builtin_inff();
+#pragma unroll
+                for (int u = 0; u < 16; u++)
+                    if (kv[u] < __builtin_inff()) m = fminf(m, qs_key_to_a(metric, kv[u], qi.x) + eps);
+                sc[(int64_t)c * 64 + lane] = m;
+            }
+        }
+        __syncthreads();
+        // 2. prefix k-th smallest -> Uc
+        if (w == 0 && !noskip) {
+            float sk[2];
+            uint32_t sid[2];
+            sk[0] = lane < len_in ? hd[lane] : __builtin_inff();
+            sid[0] = sid[1] = 0;
+            {
+                float t1[1] = {sk[0]};
+                uint32_t i1[1] = {0};
+                bitonic_sort<1>(t1, i1, lane);
+                sk[0] = t1[0];
+            }
+            float thr = __shfl(sk[0], k - 1);
+            for (int c0 = 0; c0 < nch; c0 += 16) {
+                float v[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) v[u] = c0 + u < nch ? sc[(int64_t)(c0 + u) * 64 + lane] : __builtin_inff();
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    if (c0 + u >= nch) break;
+                    if (lane == 0) suc[c0 + u] = thr;
+                    if (__any(v[u] < thr)) {
+                        sk[1] = v[u];
+                        bitonic_sort<2>(sk, sid, lane);
+                        thr = __shfl(sk[0], k - 1);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // 3a. candidate counts per chunk
+        if (!noskip) {
+            for (int c = w; c < nch; c += RP_NW) {
+                const float U = suc[c];
+                int cnt = 0;
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
+                    const float kv = bb < nb ? kr[bb] : __builtin_inff();
+                    const bool in = kv < __builtin_inff() && qs_key_to_a(metric, kv, qi.x) - eps < U;
+                    cnt += __popcll(__ballot(in));
+                }
+                if (lane == 0) scc[c] = cnt;
+            }
+        }
+        __syncthreads();
+        // 3b. exclusive scan (wave 0)
+        if (w == 0) {
+            if (noskip) {
+                if (lane == 0) s_total = RP_CAP + 1;
+            } else {
+                const int per = (nch + 63) / 64;
+                const int c0 = lane * per, c1 = c0 + per < nch ? c0 + per : nch;
+                int sum = 0;
+                for (int c = c0; c < c1; c++) sum += scc[c];
+                int incl = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(incl, o);
+                    if (lane >= o) incl += t;
+                }
+                int run = incl - sum;
+                for (int c = c0; c < c1; c++) { const int t = scc[c]; scc[c] = run; run += t; }
+                if (lane == 63) s_total = incl;
+            }
+        }
+        __syncthreads();
+        const int total = s_total;
+        // 3c. compaction in block order
+        if (total <= RP_CAP) {
+            for (int c = w; c < nch; c += RP_NW) {
+                const float U = suc[c];
+                int pos = scc[c];
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
+                    const float kv = bb < nb ? kr[bb] : __builtin_inff();
+                    const float lb = qs_key_to_a(metric, kv, qi.x) - eps;
+                    const bool in = kv < __builtin_inff() && lb < U;
+                    const uint64_t m = __ballot(in);
+                    if (in) {
+                        const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                        scand[o] = (uint32_t)bb;
+                        slb[o] = lb;
+                    }
+                    pos += __popcll(m);
+                }
+            }
+        }
+        __syncthreads();
+        // 4. the heap replay over the candidates (wave 0)
+        if (w == 0) {
+            const bool use_list = total <= RP_CAP;
+            const int64_t ncand = use_list ? total : nb;
+            for (int64_t base = 0; base < ncand; base += 64) {
+                const int64_t e = base + lane;
+                int64_t blk = 0;
+                float lb = __builtin_inff();
+                bool has = false;
+                if (e < ncand) {
+                    if (use_list) {
+                        blk = scand[e];
+                        lb = slb[e];
+                        has = true;
+                    } else {
+                        blk = e;
+                        const float kv = kr[e];
+                        has = noskip || kv < __builtin_inff();
+                        lb = noskip ? -__builtin_inff() : qs_key_to_a(metric, kv, qi.x) - eps;
+                    }
+                }
+                int len = s_len;
+                float top = len > 0 ? hd[0] : 0.f;
+                uint64_t bmask = __ballot(has && (len < k || top > lb));
+                while (bmask) {
+                    len = s_len;
+                    top = len > 0 ? hd[0] : 0.f;
+                    int j1 = -1, j2 = -1;
+                    while (bmask && j2 < 0) {
+                        const int j = __builtin_ctzll(bmask);
+                        bmask &= bmask - 1;
+                        const float lbj = __shfl(lb, j);
+                        if (!(len < k || top > lbj)) continue;
+                        if (j1 < 0) j1 = j; else j2 = j;
+                    }
+                    if (j1 < 0) break;
+                    const int64_t b1 = __shfl(blk, j1);
+                    const int64_t b2 = __shfl(blk, j2 < 0 ? j1 : j2);
+                    const bool okb = lh ? j2 >= 0 : true;
+                    const int64_t row = (lh ? b2 : b1) * 32 + li;
+                    const bool ok = okb && row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+                    const float dist = ok ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
+                    uint64_t mask = __ballot(ok && (len < k || top > dist));
+                    if (mask == 0) continue;
+                    s_d[lane] = dist;
+                    wave_sync_lds();
+                    if (lane == 0) {
+                        ReplayHeap h{hid, hd, s_len};
+                        while (mask) {
+                            const int l = __builtin_ctzll(mask);
+                            mask &= mask - 1;
+                            const float dj = s_d[l];
+                            const int64_t bj = l >= 32 ? b2 : b1;
+                            const uint64_t idj = id_base + (uint64_t)(bj * 32 + (l & 31));
+                            if (h.len < k) rh_insert(h, idj, dj);
+                            else if (h.dist[0] > dj) { uint64_t x; float y; rh_pop(h, &x, &y); rh_insert(h, idj, dj); }
+                        }
+                        s_len = h.len;
+                    }
+                    wave_sync_lds();
+                }
+            }
+            const int64_t orow = by_list ? li_ : q;
+            if (!extract) {
+                const int n = s_len;
+                if (lane < n) {
+                    out_ids[orow * kout + lane] = hid[lane];
+                    out_d[orow * kout + lane] = hd[lane];
+                }
+                if (lane == 0) out_n[orow] = n;
+            } else if (lane == 0) {
+                ReplayHeap h{hid, hd, s_len};
+                const int n = h.len;
+                for (int i = n - 1; i >= 0; i--) {
+                    uint64_t x; float y;
+                    rh_pop(h, &x, &y);
+                    if (i < kout) { out_ids[orow * kout + i] = x; out_d[orow * kout + i] = y; }
+                }
+                out_n[orow] = n < kout ? n : kout;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace wv

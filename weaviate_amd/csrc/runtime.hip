@@ -119,7 +119,8 @@ struct wv_index {
     int variant = WV_VARIANT_AVX256;
     int compression = WV_COMPRESSION_NONE;
     int rescore_limit = -1;
-    int cache_opt = 0;  // BQ.Cache / RQ.Cache (flatent UserConfig): QueryVectorDistancer reads codes
+    int cache_opt = 0;
+    int replay_par = 1;  // BQ.Cache / RQ.Cache (flatent UserConfig): QueryVectorDistancer reads codes
     int device = 0;
     uint64_t id_base = 0;
     std::string root_path;
@@ -188,7 +189,7 @@ struct wv_index {
     hipStream_t aux = nullptr;
     hipEvent_t evd[2] = {nullptr, nullptr}, evr[2] = {nullptr, nullptr};
     DBuf rE2, rB2;
-    DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList;
+    DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
     DBuf gmA, gmI;  // GEMV path: first level of the two-level span merge
     wv_stats stats{};
     // micro-batcher of concurrent single-query searches (batcher.hip)
@@ -277,7 +278,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
                     &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm,
                     &idx->rE2, &idx->rB2, &idx->gmA, &idx->gmI, &idx->qsQb, &idx->qsInfo, &idx->qsKey, &idx->qsCand,
-                    &idx->qsNc, &idx->qsEps, &idx->qsFlags, &idx->qsList})
+                    &idx->qsNc, &idx->qsEps, &idx->qsFlags, &idx->qsList, &idx->qsScratch})
         b->release();
     if (idx->aux) hipStreamSynchronize(idx->aux);
     for (hipEvent_t e : {idx->evd[0], idx->evd[1], idx->evr[0], idx->evr[1]})
@@ -742,6 +743,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
         if (idx->dims) set_dims(idx, idx->dims);
     }
     else if (k == "bq_kernel") idx->bq_kernel = (int)value;
+    else if (k == "replay_par") idx->replay_par = value ? 1 : 0;  // 0: one-wave block-key replay only
     else if (k == "cache") {  // BQ.Cache / RQ.Cache: QueryVectorDistancer uses the cached codes
         if (value != 0 && value != 1) return set_err(WV_ERR_INVALID, "cache must be 0 or 1");
         idx->cache_opt = (int)value;
@@ -1924,6 +1926,49 @@ extern "C" int wv_index_rq_distances(wv_index* idx, const float* queries, int64_
 // flags (nonzero = not proven) for the caller, mode 0 replays them.  No host
 // synchronisation: the eps inputs, flag lists and counts stay on the device.
 // ---------------------------------------------------------------------------
+// the block-key replay of listed queries: k_blk_replay_par (8 waves per query,
+// k < 64) or k_blk_replay (one wave per query).  list/count: device list and
+// its length at counters[1] (or nlist when counters == nullptr); max_list =
+// host bound of the list length (grid sizing).
+static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ldk, int64_t nb, const float* eps,
+                             const float4* qinfo, const uint32_t* valid, const float* Qn, const int32_t* list,
+                             const uint32_t* counters, int nlist, int64_t max_list, int k, int kout, uint64_t* oi,
+                             float* od, int32_t* on, const uint64_t* in_i, const float* in_d, const int32_t* in_n,
+                             int extract, int by_list) {
+    const int metric = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+    const bool v5 = idx->variant == WV_VARIANT_AVX512;
+    const int64_t nch = (nb + RP_CH - 1) / RP_CH;
+    if (max_list <= 0) return WV_OK;
+    if (k < 64 && nch <= RP_MAXCH && idx->replay_par) {
+        const int64_t grid = std::min<int64_t>(max_list, 256);
+        HIPCHK(idx->qsScratch.ensure((size_t)grid * nch * 64 * sizeof(float)));
+#define WV_RPP(M, V) k_blk_replay_par<M, V><<<(unsigned)grid, 512, 0, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, idx->qsScratch.as<float>())
+        switch (metric) {
+        case L2: if (v5) WV_RPP(L2, AVX512); else WV_RPP(L2, AVX256); break;
+        case DOT: if (v5) WV_RPP(DOT, AVX512); else WV_RPP(DOT, AVX256); break;
+        default: if (v5) WV_RPP(COSINE, AVX512); else WV_RPP(COSINE, AVX256); break;
+        }
+#undef WV_RPP
+        HIPCHK(hipGetLastError());
+        return WV_OK;
+    }
+    const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
+    if (rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
+#define WV_RP(M, V)                                                                                             \
+    do {                                                                                                        \
+        if (rlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); \
+        k_blk_replay<M, V><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list); \
+    } while (0)
+    switch (metric) {
+    case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;
+    case DOT: if (v5) WV_RP(DOT, AVX512); else WV_RP(DOT, AVX256); break;
+    default: if (v5) WV_RP(COSINE, AVX512); else WV_RP(COSINE, AVX256); break;
+    }
+#undef WV_RP
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
 static int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : 0; }
 
 static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid,
@@ -2065,18 +2110,12 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         // ---- flagged queries: the exact heap replay, bounded by the block keys ----
         HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
         k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount, 0);
-#define WV_RP(M, V)                                                                                             \
-    do {                                                                                                        \
-        if (rlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); \
-        k_blk_replay<M, V><<<(unsigned)cn, 64, rlds, s>>>(a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsList.as<int32_t>(), idx->qscount, 0, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, nullptr, nullptr, nullptr, 1, 0); \
-    } while (0)
-        switch (metric) {
-        case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;
-        case DOT: if (v5) WV_RP(DOT, AVX512); else WV_RP(DOT, AVX256); break;
-        default: if (v5) WV_RP(COSINE, AVX512); else WV_RP(COSINE, AVX256); break;
+        {
+            int rc = launch_blk_replay(idx, s, a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, valid, Qn,
+                                       idx->qsList.as<int32_t>(), idx->qscount, 0, cn, k, kout, o_ids + c0 * kout,
+                                       o_d + c0 * kout, o_n + c0, nullptr, nullptr, nullptr, 1, 0);
+            if (rc) return rc;
         }
-#undef WV_RP
-        HIPCHK(hipGetLastError());
     }
     if (idx->timing) {
         HIPCHK(hipEventRecord(idx->evt1, s));
@@ -2528,22 +2567,11 @@ extern "C" int wv_index_replay_device(wv_index* idx, const float* d_queries, int
     const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
     const bool keyed = have_data && idx->qs_keys_nq == nq && rlds <= 160 * 1024;
     if (keyed) {
-        const int metric = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
-        const bool v5 = idx->variant == WV_VARIANT_AVX512;
         const float* Qn = idx->qn.as<float>();  // the prepared rows of that batch
-#define WV_RP(M, V)                                                                                             \
-    do {                                                                                                        \
-        if (rlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); \
-        k_blk_replay<M, V><<<(unsigned)nlist, 64, rlds, s>>>(idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb, idx->qsEps.as<float>(), idx->qsInfo.as<float4>(), idx->X, idx->dpad, idx->present, idx->hiwater, Qn, idx->dims, d_qlist, nullptr, nlist, k, k, idx->id_base, d_out_ids, d_out_dists, d_out_len, d_in_ids, d_in_dists, d_in_len, extract, 1); \
-    } while (0)
-        switch (metric) {
-        case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;
-        case DOT: if (v5) WV_RP(DOT, AVX512); else WV_RP(DOT, AVX256); break;
-        default: if (v5) WV_RP(COSINE, AVX512); else WV_RP(COSINE, AVX256); break;
-        }
-#undef WV_RP
-        HIPCHK(hipGetLastError());
-        return WV_OK;
+        return launch_blk_replay(idx, s, idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb,
+                                 idx->qsEps.as<float>(), idx->qsInfo.as<float4>(), idx->present, Qn, d_qlist, nullptr,
+                                 nlist, nlist, k, k, d_out_ids, d_out_dists, d_out_len, d_in_ids, d_in_dists, d_in_len,
+                                 extract, 1);
     }
     const float* Qn = nullptr;
     if (have_data) {
