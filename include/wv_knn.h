@@ -54,6 +54,11 @@ extern "C" {
  * (:460-532) with rescore_limit = RQ.RescoreLimit */
 #define WV_COMPRESSION_RQ8 3
 #define WV_COMPRESSION_RQ1 4
+/* HNSW's scalar quantizer (compressionhelpers/scalar_quantization.go,
+ * NewHNSWSQCompressor compression.go:634-662): 8-bit codes over the trained
+ * range [b, b + a]; searched like hnsw.flatSearch (see
+ * wv_index_hnsw_flat_search) after wv_index_sq_fit / wv_index_sq_restore */
+#define WV_COMPRESSION_SQ 5
 
 /* which reference SIMD kernel's fp32 accumulation order to reproduce
  * (distancer/l2_amd64.go:19-26: AVX-512 only if AMX-BF16 && AVX512) */
@@ -198,6 +203,39 @@ int wv_index_rq_codes(wv_index *idx, void *out, int64_t n);
  * cosine like SearchByVector) against slots [0, n): out [nq][n], +inf where a
  * slot holds no vector */
 int wv_index_rq_distances(wv_index *idx, const float *queries, int64_t nq, int64_t d, float *out, int64_t n);
+
+/* ScalarQuantizer: NewScalarQuantizer (scalar_quantization.go:73-97) trained
+ * on the first training_limit stored vectors in id order (<= 0: all; the
+ * reference samples hnsw.compress's cache dump, hnsw/compress.go:31-68), then
+ * every stored vector encoded (Encode, :124-137) and later Adds encoded on
+ * insert.  Errors: empty index ("compress command cannot be executed before
+ * inserting some data", hnsw/compress.go:34-36). */
+int wv_index_sq_fit(wv_index *idx, int64_t training_limit);
+/* RestoreScalarQuantizer (scalar_quantization.go:99-112): "invalid range value
+ * while restoring SQ settings" when a == 0 */
+int wv_index_sq_restore(wv_index *idx, float a, float b);
+/* out[0] = a, out[1] = b, out[2] = ready (0/1), out[3] = bytes per code (d + 8) */
+int wv_index_sq_info(wv_index *idx, float *out);
+/* the reference's code bytes of slots [0, n): out [n][d + 8] (codes, big-endian
+ * sum, big-endian sum of squares) */
+int wv_index_sq_codes(wv_index *idx, uint8_t *out, int64_t n);
+
+/* hnsw.flatSearch (hnsw/flat_search.go:28-141, one worker: flatSearchConcurrency
+ * > 1 makes the reference's tie order nondeterministic) + h.rescore
+ * (hnsw/search.go:1047-1110, one worker) over the compressed vectors of a BQ /
+ * PQ / SQ / rq-8 / rq-1 index: the filtered brute force that
+ * hnsw.SearchByVector runs when the allow list is below flatSearchCutoff
+ * (search.go:78-92).  limit = searchTimeEF(k) (search.go:44-76; options "ef"
+ * (default -1 = dynamic), "ef_min" 100, "ef_max" 500, "ef_factor" 8) when
+ * shouldRescore (search.go:182-189: compressed, option "hnsw_rescore" = 1,
+ * and for SQ / RQ rescore_limit != 0), else k; SQ / RQ trim the results to
+ * rescore_limit before rescoring when rescore_limit >= k.  Distances:
+ * CompressorDistancer.DistanceToNode, rescoring SingleDist(query, vector).
+ * Outputs [nq][k] ascending + counts; allow_mode as
+ * wv_index_search_by_vector_batch. */
+int wv_index_hnsw_flat_search(wv_index *idx, const float *queries, int64_t nq, int64_t d, int32_t k,
+                              const uint64_t *allow_ids, int64_t n_allow, int32_t allow_mode, uint64_t *out_ids,
+                              float *out_dists, int32_t *out_counts);
 
 /* Device-resident batch search for sharded / benchmark callers.
  * mode 0: like SearchByVector (kout = k, tie cases resolved by heap replay).

@@ -67,6 +67,13 @@ int or_pq_flat_search(int metric, int variant, const float *centers, int m, int 
                       const float *store, const uint8_t *present, long nslots, const float *query, int k, int limit,
                       int rescore, uint64_t *out_ids, float *out_dists, int *out_n);
 
+/* sq.c: scalar quantizer + generic hnsw.flatSearch (see its header) */
+void or_sq_fit(const float *data, long n, long d, float *out_ab);
+void or_sq_encode(float a, float b, const float *vec, long d, uint8_t *code);
+float or_sq_distance(int metric, float a, float b, long d, const uint8_t *x, const uint8_t *y);
+int or_hnsw_flat_search(const float *cdist, const float *edist, const uint8_t *present, long nslots, int k, int limit,
+                        int rescore, int trim, uint64_t *out_ids, float *out_dists, int *out_n);
+
 /* rq.c: rotational quantization rq-8 / rq-1 (see its header) */
 typedef struct or_rq or_rq;
 or_rq *or_rq_new(int bits, int metric, int dims, uint64_t seed);

@@ -110,6 +110,12 @@ def lib() -> C.CDLL:
         o.bl_flat_search_bq_batch.restype = C.c_int
         o.bl_flat_search_bq_batch.argtypes = [C.c_int, C.c_int, C.c_int, pf, pu, C.c_long, C.c_long, pf, C.c_long,
                                               C.c_int, C.c_int, C.c_int, pu, pf, pi]
+        o.or_sq_fit.argtypes = [pf, C.c_long, C.c_long, pf]
+        o.or_sq_encode.argtypes = [C.c_float, C.c_float, pf, C.c_long, pb]
+        o.or_sq_distance.restype = C.c_float
+        o.or_sq_distance.argtypes = [C.c_int, C.c_float, C.c_float, C.c_long, pb, pb]
+        o.or_hnsw_flat_search.restype = C.c_int
+        o.or_hnsw_flat_search.argtypes = [pf, pf, pb, C.c_long, C.c_int, C.c_int, C.c_int, C.c_int, pu, pf, pi]
         _o = o
     return _o
 
@@ -533,3 +539,51 @@ def bq_search_gen(kind: int, seed: int, n: int, d: int, metric: int, variant: in
     if rc != 0:
         raise RuntimeError("bq_search_gen failed")
     return ids, dd, cnt
+
+
+# ---- scalar quantizer (oracle/sq.c) + generic hnsw.flatSearch ----------------
+class SQ:
+    """compressionhelpers.ScalarQuantizer restated (scalar_quantization.go)."""
+
+    def __init__(self, data=None, a: Optional[float] = None, b: Optional[float] = None, d: Optional[int] = None):
+        if data is not None:
+            x = np.ascontiguousarray(data, dtype=np.float32)
+            ab = np.zeros(2, np.float32)
+            lib().or_sq_fit(f(x), x.shape[0], x.shape[1], f(ab))
+            self.a, self.b, self.d = float(ab[0]), float(ab[1]), x.shape[1]
+        else:
+            self.a, self.b, self.d = float(np.float32(a)), float(np.float32(b)), int(d)
+
+    def encode(self, v) -> np.ndarray:
+        x = np.ascontiguousarray(v, dtype=np.float32).ravel()
+        out = np.zeros(x.size + 8, np.uint8)
+        lib().or_sq_encode(self.a, self.b, f(x), x.size, out.ctypes.data_as(pb))
+        return out
+
+    def distance(self, metric: int, cx: np.ndarray, cy: np.ndarray) -> float:
+        return float(lib().or_sq_distance(metric, self.a, self.b, self.d, np.ascontiguousarray(cx).ctypes.data_as(pb),
+                                          np.ascontiguousarray(cy).ctypes.data_as(pb)))
+
+
+def hnsw_flat_search(cdist: np.ndarray, edist: np.ndarray, present: np.ndarray, k: int, limit: int, rescore: bool,
+                     trim: int):
+    """hnsw.flatSearch (one worker) + h.rescore over precomputed compressor
+    distances cdist[slot] and rescoring distances edist[slot] -> (ids, dists)."""
+    cd = np.ascontiguousarray(cdist, dtype=np.float32)
+    ed = np.ascontiguousarray(edist, dtype=np.float32)
+    pr = np.ascontiguousarray(present, dtype=np.uint8)
+    ids = np.zeros(max(k, 1), np.uint64)
+    dd = np.zeros(max(k, 1), np.float32)
+    n = C.c_int(0)
+    lib().or_hnsw_flat_search(f(cd), f(ed), pr.ctypes.data_as(pb), cd.size, int(k), int(limit), int(bool(rescore)),
+                              int(trim), ids.ctypes.data_as(pu), f(dd), C.byref(n))
+    return ids[:n.value].copy(), dd[:n.value].copy()
+
+
+def search_time_ef(k: int, ef: int = -1, ef_min: int = 100, ef_max: int = 500, ef_factor: int = 8) -> int:
+    """hnsw searchTimeEF / autoEfFromK (hnsw/search.go:44-76)."""
+    if ef < 1:
+        e = k * ef_factor
+        e = ef_max if e > ef_max else ef_min if e < ef_min else e
+        return max(e, k)
+    return max(ef, k)

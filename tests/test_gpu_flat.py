@@ -351,11 +351,14 @@ def test_bf16x3_error_within_proof_bound(wv, oracle, metric, kind, d):
     idx.close()
 
 
-@pytest.mark.parametrize("k", [1, 10, 50, 63, 64])
+@pytest.mark.parametrize("k", [1, 10, 50, 63, 64, 100, 191, 200])
 def test_block_key_replay_parallel_and_single_wave(wv, oracle, k):
     """Integer data (exact ties everywhere): most queries go to the heap replay.
-    k < 64: k_blk_replay_par (8-wave candidate scan), else / replay_par=0: the
-    one-wave k_blk_replay; both equal the reference heap, including queries with
+    replay_par=3 (2, the default, for k < 64): pooled k_rp_bounds / k_rp_exact /
+    k_rp_heap, also with a one-block and a 300-block pool (queries that do not
+    fit fall back to the on-the-fly scan);
+    replay_par=1, k < 64: k_blk_replay_par; else / replay_par=0: the one-wave
+    k_blk_replay.  All equal the reference heap, including queries with
     non-finite values (every block visited)."""
     n, d = 60000, 24
     data = gen(oracle, 1, 91, n, d)
@@ -363,9 +366,11 @@ def test_block_key_replay_parallel_and_single_wave(wv, oracle, k):
     queries[3, 5] = np.nan
     queries[7, 0] = np.inf
     res = []
-    for par in (1, 0):
+    for par, pool in ((3, 0), (3, 1), (3, 300), (2, 0), (1, 0), (0, 0)):
         idx, orc = build_pair(wv, oracle, "l2-squared", "avx256", data)
         idx.set_option("replay_par", par)
+        if pool:
+            idx.set_option("rp_pool", pool)
         before = idx.stats()["replayed_queries"]
         res.append(idx.search_by_vector_batch(queries, k))
         assert idx.stats()["replayed_queries"] - before >= 2  # at least the non-finite queries
@@ -373,3 +378,20 @@ def test_block_key_replay_parallel_and_single_wave(wv, oracle, k):
         exp = orc.search(queries[qi], k)
         for ids, dists, counts in res:
             assert_same(exp, ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"k{k} q{qi}")
+
+
+@pytest.mark.parametrize("metric", ["cosine", "l2-squared", "dot"])
+def test_pooled_replay_float_data(wv, oracle, metric):
+    """Random float data: forced replay of every query through the pooled
+    k_rp_* kernels (the C3 path of a flagged query) equals the oracle."""
+    n, d, k = 50000, 96, 10
+    data = gen(oracle, 0, 93, n, d)
+    queries = gen(oracle, 0, 94, 24, d)
+    idx, orc = build_pair(wv, oracle, metric, "avx256", data)
+    idx.set_option("replay_par", 2)
+    idx.set_option("qs_force_flag", 1)
+    before = idx.stats()["replayed_queries"]
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["replayed_queries"] - before == len(queries)
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")

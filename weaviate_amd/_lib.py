@@ -33,6 +33,7 @@ COMPRESSION_BQ = 1
 COMPRESSION_PQ = 2
 COMPRESSION_RQ8 = 3
 COMPRESSION_RQ1 = 4
+COMPRESSION_SQ = 5
 
 
 class WvConfig(C.Structure):
@@ -120,6 +121,11 @@ SIGNATURES = {
     "wv_index_rq_info": (C.c_int, [P, pi32]),
     "wv_index_rq_codes": (C.c_int, [P, P, i64]),
     "wv_index_rq_distances": (C.c_int, [P, pf32, i64, i64, pf32, i64]),
+    "wv_index_sq_fit": (C.c_int, [P, i64]),
+    "wv_index_sq_restore": (C.c_int, [P, f32, f32]),
+    "wv_index_sq_info": (C.c_int, [P, pf32]),
+    "wv_index_sq_codes": (C.c_int, [P, C.POINTER(C.c_uint8), i64]),
+    "wv_index_hnsw_flat_search": (C.c_int, [P, pf32, i64, i64, i32, pu64, i64, i32, pu64, pf32, pi32]),
     "wv_index_set_option": (C.c_int, [P, C.c_char_p, i64]),
     "wv_lsm_segment_header": (C.c_int, [C.c_char_p, i32, C.POINTER(C.c_int64)]),
     "wv_lsm_segment_scan": (C.c_int, [C.c_char_p, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),

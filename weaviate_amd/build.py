@@ -23,6 +23,7 @@ SOURCES = [
     os.path.join(HERE, "csrc", "batcher.hip"),
     os.path.join(HERE, "csrc", "gemv_kernels.hip"),
     os.path.join(HERE, "csrc", "qs_kernels.hip"),
+    os.path.join(HERE, "csrc", "sq_kernels.hip"),
     os.path.join(HERE, "csrc", "wv_device.h"),
     os.path.join(REPO, "include", "wv_knn.h"),
 ]

@@ -357,7 +357,8 @@ __global__ __launch_bounds__(256, 2) void k_pq_adc(const uint32_t* __restrict__ 
 // heap's ascending extraction asc[li][0..n) is popped max-first
 // (= reverse order) into the result heap via addResult (:214-224).
 // rescore == 0: extract (fill from the back) -> out rows q = qlist[li].
-// rescore == 1: pop all into ascending ids (search.go:1058-1064) -> cand slots
+// rescore == 1: (trim > 0: Pop while Len > trim) pop all into ascending ids
+//               (search.go:1048-1064) -> cand slots
 //               [li][R] for k_rescore; cand_n[li].
 // Dynamic LDS: [R] u64 | [R] f32.
 __global__ __launch_bounds__(64) void k_pq_finish(const uint64_t* __restrict__ asc_ids,
@@ -365,7 +366,8 @@ __global__ __launch_bounds__(64) void k_pq_finish(const uint64_t* __restrict__ a
                                                   const int32_t* __restrict__ qlist, int nlist, int R, int k,
                                                   int rescore, uint64_t id_base, uint64_t* __restrict__ out_ids,
                                                   float* __restrict__ out_d, int32_t* __restrict__ out_n,
-                                                  uint32_t* __restrict__ cand_slot, int32_t* __restrict__ cand_n) {
+                                                  uint32_t* __restrict__ cand_slot, int32_t* __restrict__ cand_n,
+                                                  int trim) {
     extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(psm);
     float* hd = reinterpret_cast<float*>(hid + R);
@@ -390,13 +392,17 @@ __global__ __launch_bounds__(64) void k_pq_finish(const uint64_t* __restrict__ a
         out_n[q] = m < k ? m : k;
         return;
     }
-    for (int i = m - 1; i >= 0; i--) {
+    // SQ / RQ (search.go:1048-1057): Pop while Len > RescoreLimit (>= k)
+    if (trim > 0)
+        while (hp.len > trim) { uint64_t a; float b; rh_pop(hp, &a, &b); }
+    const int mt = hp.len;
+    for (int i = mt - 1; i >= 0; i--) {
         uint64_t a; float b;
         rh_pop(hp, &a, &b);
         cand_slot[(int64_t)li * R + i] = (uint32_t)(a - id_base);
     }
-    for (int i = m; i < R; i++) cand_slot[(int64_t)li * R + i] = NO_ID;
-    cand_n[li] = m;
+    for (int i = mt; i < R; i++) cand_slot[(int64_t)li * R + i] = NO_ID;
+    cand_n[li] = mt;
 }
 
 // h.rescore with one worker (hnsw/search.go:1067-1110): in ascending-id-list

@@ -1219,4 +1219,382 @@ __global__ __launch_bounds__(512) void k_blk_replay_par(const float* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Three-kernel form of the block-key replay (default):
+//   k_rp_bounds  8 waves per listed query: heap-top upper bounds per chunk of
+//                1024 blocks (k-th smallest of the earlier chunks' row upper
+//                bounds A + eps, and of the handed-over heap), refined inside
+//                chunk 0 per 64-block group; candidate blocks (A - eps below
+//                the bound) compacted in block order into a shared pool;
+//   k_rp_exact   the whole grid: reference-order exact distances of every
+//                row of every pooled block (no serial dependency left);
+//   k_rp_heap    one wave per listed query: insertToHeap over the pooled
+//                blocks in order, visiting a block iff the heap is short or
+//                top > A - eps (k_blk_replay's rule), distances read back
+//                from the pool in windows of 16 blocks.
+// A query whose candidates do not fit the pool, or with non-finite values,
+// replays every block with on-the-fly distances in k_rp_heap.
+// ---------------------------------------------------------------------------
+constexpr int RPW = 16;  // k_rp_heap window (blocks)
+
+// element e of a wave-sorted list of RS rows (broadcast)
+template <int RS>
+__device__ __forceinline__ float rp_key_at(const float (&key)[RS], int e) {
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < RS; r++) {
+        const float t = __shfl(key[r], e & 63);
+        if ((e >> 6) == r) v = t;
+    }
+    return v;
+}
+
+// merge 64 new values (one per lane) into the sorted list rows 0..RS-2 when any
+// is below thr; returns the new k-th smallest
+template <int RS>
+__device__ __forceinline__ float rp_offer(float (&sk)[RS], uint32_t (&sid)[RS], float v, float thr, int k, int lane) {
+    if (!__any(v < thr)) return thr;
+    sk[RS - 1] = v;
+    sid[RS - 1] = 0;
+    bitonic_sort<RS>(sk, sid, lane);
+    return rp_key_at<RS>(sk, k - 1);
+}
+
+template <int RS, int METRIC>
+__global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key, int64_t ldk, int64_t nb,
+                                                   const float* __restrict__ eps_q, const float4* __restrict__ qinfo,
+                                                   const int32_t* __restrict__ qlist, const uint32_t* __restrict__ counters,
+                                                   int nlist, int k, const float* __restrict__ in_d,
+                                                   const int32_t* __restrict__ in_len, float* __restrict__ scratch,
+                                                   uint32_t* __restrict__ pool_blk, float* __restrict__ pool_lb,
+                                                   int32_t* __restrict__ pool_q, uint32_t* __restrict__ pool_ctr,
+                                                   int64_t pool_cap, int32_t* __restrict__ rp_off,
+                                                   int32_t* __restrict__ rp_tot) {
+    __shared__ float suc[RP_MAXCH];
+    __shared__ int scc[RP_MAXCH];
+    __shared__ float sg0[16];
+    __shared__ int s_total, s_off;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int metric = METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2;
+    const int count = counters ? (int)counters[1] : nlist;
+    const int nch = (int)((nb + RP_CH - 1) / RP_CH);
+    float* sc = scratch + (int64_t)blockIdx.x * nch * 64;
+    for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
+        const int q = qlist[li_];
+        const float4 qi = qinfo[q];
+        const bool noskip = qi.w != 0.f;
+        const float eps = eps_q[q];
+        const float* kr = key + (int64_t)q * ldk;
+        int len_in = in_len ? in_len[li_] : 0;
+        len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
+        if (noskip) {  // every block, distances on the fly (k_rp_heap)
+            if (threadIdx.x == 0) { rp_off[li_] = -1; rp_tot[li_] = 0; }
+            continue;
+        }
+        // 1. per chunk, per lane: the smallest row upper bound A + eps of 16 blocks
+        for (int c = w; c < nch; c += RP_NW) {
+            float kv[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
+                kv[u] = bb < nb ? kr[bb] : __builtin_inff();
+            }
+            float m = __builtin_inff();
+#pragma unroll
+            for (int u = 0; u < 16; u++)
+                if (kv[u] < __builtin_inff()) m = fminf(m, qs_key_to_a(metric, kv[u], qi.x) + eps);
+            sc[(int64_t)c * 64 + lane] = m;
+        }
+        __syncthreads();
+        // 2. wave 0: suc[c] = k-th smallest of the handed-over heap and of the
+        //    lane minima of chunks < c (an upper bound of the heap top at chunk c)
+        if (w == 0) {
+            float sk[RS];
+            uint32_t sid[RS];
+#pragma unroll
+            for (int r = 0; r < RS; r++) {
+                const int e = r * 64 + lane;
+                sk[r] = (r < RS - 1 && e < len_in) ? in_d[(int64_t)li_ * k + e] : __builtin_inff();
+                sid[r] = 0;
+            }
+            bitonic_sort<RS>(sk, sid, lane);
+            float thr = rp_key_at<RS>(sk, k - 1);
+            for (int c0 = 0; c0 < nch; c0 += 16) {
+                float v[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) v[u] = c0 + u < nch ? sc[(int64_t)(c0 + u) * 64 + lane] : __builtin_inff();
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    if (c0 + u >= nch) break;
+                    if (lane == 0) suc[c0 + u] = thr;
+                    thr = rp_offer<RS>(sk, sid, v[u], thr, k, lane);
+                }
+            }
+            // chunk 0 per 64-block group: also bounded by the k-th smallest A + eps
+            // of its own earlier groups (the chunk-level bound is weakest there)
+            float kv[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) kv[u] = u * 64 + lane < nb ? kr[u * 64 + lane] : __builtin_inff();
+#pragma unroll
+            for (int r = 0; r < RS; r++) { sk[r] = __builtin_inff(); sid[r] = 0; }
+            float tin = __builtin_inff();
+            const float U0 = suc[0];
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                if (lane == 0) sg0[u] = fminf(U0, tin);
+                tin = rp_offer<RS>(sk, sid, kv[u] < __builtin_inff() ? qs_key_to_a(metric, kv[u], qi.x) + eps
+                                                                    : __builtin_inff(), tin, k, lane);
+            }
+        }
+        __syncthreads();
+        // 3. candidate blocks of chunk c: A - eps < bound (suc[c]; inside chunk 0
+        //    the per-group bound sg0[u]).  pass 0: counts, pass 1: compaction.
+        for (int pass = 0; pass < 2; pass++) {
+            const int off = pass ? s_off : 0;
+            if (pass == 0 || off >= 0) {
+                for (int c = w; c < nch; c += RP_NW) {
+                    float kv[16];
+#pragma unroll
+                    for (int u = 0; u < 16; u++) {
+                        const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
+                        kv[u] = bb < nb ? kr[bb] : __builtin_inff();
+                    }
+                    const float U = suc[c];
+                    int pos = pass ? off + scc[c] : 0;
+#pragma unroll
+                    for (int u = 0; u < 16; u++) {
+                        const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
+                        const float lb = qs_key_to_a(metric, kv[u], qi.x) - eps;
+                        const bool in = kv[u] < __builtin_inff() && lb < (c == 0 ? sg0[u] : U);
+                        const uint64_t m = __ballot(in);
+                        if (pass && in) {
+                            const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                            pool_blk[o] = (uint32_t)bb;
+                            pool_lb[o] = lb;
+                            pool_q[o] = li_;
+                        }
+                        pos += __popcll(m);
+                    }
+                    if (!pass && lane == 0) scc[c] = pos;
+                }
+            }
+            __syncthreads();
+            if (pass == 0 && w == 0) {  // exclusive scan of the chunk counts, pool allocation
+                const int per = (nch + 63) / 64;
+                const int c0 = lane * per, c1 = c0 + per < nch ? c0 + per : nch;
+                int sum = 0;
+                for (int c = c0; c < c1; c++) sum += scc[c];
+                int incl = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(incl, o);
+                    if (lane >= o) incl += t;
+                }
+                int run = incl - sum;
+                for (int c = c0; c < c1; c++) { const int t = scc[c]; scc[c] = run; run += t; }
+                if (lane == 63) {
+                    s_total = incl;
+                    int64_t o = incl > 0 ? (int64_t)atomicAdd(pool_ctr, (uint32_t)incl) : 0;
+                    if (o + incl > pool_cap) {  // pool exhausted: mark the claimed tail dead
+                        for (int64_t e = o; e < pool_cap; e++) pool_q[e] = -1;
+                        o = -1;
+                    }
+                    s_off = (int)o;
+                    rp_off[li_] = (int)o;
+                    rp_tot[li_] = incl;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// exact distances of the pooled blocks' rows: pool_E[e][32], valid masks pool_vm[e]
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(256) void k_rp_exact(const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
+                                                  int64_t nrows, const float* __restrict__ Qn, int d,
+                                                  const int32_t* __restrict__ qlist, const uint32_t* __restrict__ pool_blk,
+                                                  const int32_t* __restrict__ pool_q, const uint32_t* __restrict__ pool_ctr,
+                                                  int64_t pool_cap, float* __restrict__ pool_E,
+                                                  uint32_t* __restrict__ pool_vm) {
+    const int lane = threadIdx.x & 63;
+    const int li = lane & 31, lh = lane >> 5;
+    int64_t used = (int64_t)pool_ctr[0];
+    used = used < pool_cap ? used : pool_cap;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); 2 * p < used; p += nw) {
+        const int64_t e = 2 * p + lh;
+        bool ok = false;
+        float dist = 0.f;
+        if (e < used) {
+            const int lq = pool_q[e];
+            if (lq >= 0) {
+                const int q = qlist[lq];
+                const int64_t row = (int64_t)pool_blk[e] * 32 + li;
+                ok = row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+                if (ok) dist = exact_dist<METRIC, VARIANT>(Qn + (int64_t)q * dpad, X + row * dpad, d);
+                pool_E[e * 32 + li] = dist;
+            }
+        }
+        const uint64_t m = __ballot(ok);
+        if (e < used && li == 0) pool_vm[e] = (uint32_t)(m >> (32 * lh));
+    }
+}
+
+// one wave per listed query: the reference heap over the pooled blocks
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, int64_t ldk, int64_t nb,
+                                                const float* __restrict__ eps_q, const float4* __restrict__ qinfo,
+                                                const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
+                                                int64_t nrows, const float* __restrict__ Qn, int d,
+                                                const int32_t* __restrict__ qlist, const uint32_t* __restrict__ counters,
+                                                int nlist, int k, int kout, uint64_t id_base, uint64_t* __restrict__ out_ids,
+                                                float* __restrict__ out_d, int32_t* __restrict__ out_n,
+                                                const uint64_t* __restrict__ in_ids, const float* __restrict__ in_d,
+                                                const int32_t* __restrict__ in_len, int extract, int by_list,
+                                                const uint32_t* __restrict__ pool_blk, const float* __restrict__ pool_lb,
+                                                const float* __restrict__ pool_E, const uint32_t* __restrict__ pool_vm,
+                                                const int32_t* __restrict__ rp_off, const int32_t* __restrict__ rp_tot) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+    uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
+    float* hd = reinterpret_cast<float*>(hid + k);
+    float* s_d = hd + k;                 // [64]
+    float* sE = s_d + 64;                // [RPW][32]
+    int* s_len = reinterpret_cast<int*>(sE + RPW * 32);
+    const int lane = threadIdx.x;
+    const int metric = METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2;
+    const int count = counters ? (int)counters[1] : nlist;
+    const int li = lane & 31, lh = lane >> 5;
+    for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
+        const int q = qlist[li_];
+        const float* qv = Qn + (int64_t)q * dpad;
+        int len_in = in_len ? in_len[li_] : 0;
+        len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
+        for (int i = lane; i < len_in; i += 64) {
+            hid[i] = in_ids[(int64_t)li_ * k + i];
+            hd[i] = in_d[(int64_t)li_ * k + i];
+        }
+        if (lane == 0) *s_len = len_in;
+        wave_sync_lds();
+        const int off = rp_off[li_];
+        if (off >= 0) {
+            const int tot = rp_tot[li_];
+            for (int w0 = 0; w0 < tot; w0 += RPW) {
+                const int nwin = tot - w0 < RPW ? tot - w0 : RPW;
+                // the window's distances (independent of the heap state): one load round
+#pragma unroll
+                for (int j = 0; j < RPW / 2; j++) {
+                    const int e = 2 * j + lh;
+                    if (e < nwin) sE[e * 32 + li] = pool_E[(int64_t)(off + w0 + e) * 32 + li];
+                }
+                const uint32_t blk = lane < nwin ? pool_blk[off + w0 + lane] : 0u;
+                const float lb = lane < nwin ? pool_lb[off + w0 + lane] : __builtin_inff();
+                const uint32_t vm = lane < nwin ? pool_vm[off + w0 + lane] : 0u;
+                wave_sync_lds();
+                for (int j = 0; j < nwin; j++) {
+                    const int len = *s_len;
+                    const float top = len > 0 ? hd[0] : 0.f;
+                    const float lbj = __shfl(lb, j);
+                    if (!(len < k || top > lbj)) continue;
+                    const uint32_t vmj = (uint32_t)__shfl((int)vm, j);
+                    const float dist = lane < 32 ? sE[j * 32 + lane] : 0.f;
+                    const bool ok = lane < 32 && ((vmj >> lane) & 1u);
+                    uint64_t mask = __ballot(ok && (len < k || top > dist));
+                    if (mask == 0) continue;
+                    const uint32_t bj = (uint32_t)__shfl((int)blk, j);
+                    if (lane == 0) {
+                        ReplayHeap h{hid, hd, len};
+                        while (mask) {
+                            const int l = __builtin_ctzll(mask);
+                            mask &= mask - 1;
+                            const float dj = sE[j * 32 + l];
+                            const uint64_t idj = id_base + (uint64_t)bj * 32 + (uint64_t)l;
+                            if (h.len < k) rh_insert(h, idj, dj);
+                            else if (h.dist[0] > dj) { uint64_t x; float y; rh_pop(h, &x, &y); rh_insert(h, idj, dj); }
+                        }
+                        *s_len = h.len;
+                    }
+                    wave_sync_lds();
+                }
+                wave_sync_lds();  // the window buffer is rewritten next
+            }
+        } else {
+            // every block (non-finite values or pool exhausted), distances on the fly
+            const float4 qi = qinfo[q];
+            const bool noskip = qi.w != 0.f;
+            const float eps = eps_q[q];
+            const float* kr = key + (int64_t)q * ldk;
+            for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+                const int64_t bb = b0 + lane;
+                float lb = __builtin_inff();
+                bool has = false;
+                if (bb < nb) {
+                    const float kv = kr[bb];
+                    has = noskip || kv < __builtin_inff();
+                    lb = noskip ? -__builtin_inff() : qs_key_to_a(metric, kv, qi.x) - eps;
+                }
+                int len = *s_len;
+                float top = len > 0 ? hd[0] : 0.f;
+                uint64_t bmask = __ballot(has && (len < k || top > lb));
+                while (bmask) {
+                    len = *s_len;
+                    top = len > 0 ? hd[0] : 0.f;
+                    int j1 = -1, j2 = -1;
+                    while (bmask && j2 < 0) {
+                        const int j = __builtin_ctzll(bmask);
+                        bmask &= bmask - 1;
+                        const float lbj = __shfl(lb, j);
+                        if (!(len < k || top > lbj)) continue;
+                        if (j1 < 0) j1 = j; else j2 = j;
+                    }
+                    if (j1 < 0) break;
+                    const int jj = lh ? j2 : j1;
+                    const int64_t row = (b0 + jj) * 32 + li;
+                    const bool ok = jj >= 0 && row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+                    const float dist = ok ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
+                    uint64_t mask = __ballot(ok && (len < k || top > dist));
+                    if (mask == 0) continue;
+                    s_d[lane] = dist;
+                    wave_sync_lds();
+                    if (lane == 0) {
+                        ReplayHeap h{hid, hd, *s_len};
+                        while (mask) {
+                            const int l = __builtin_ctzll(mask);
+                            mask &= mask - 1;
+                            const int jb = l >= 32 ? j2 : j1;
+                            const uint64_t idj = id_base + (uint64_t)((b0 + jb) * 32 + (l & 31));
+                            const float dj = s_d[l];
+                            if (h.len < k) rh_insert(h, idj, dj);
+                            else if (h.dist[0] > dj) { uint64_t x; float y; rh_pop(h, &x, &y); rh_insert(h, idj, dj); }
+                        }
+                        *s_len = h.len;
+                    }
+                    wave_sync_lds();
+                }
+            }
+        }
+        const int64_t orow = by_list ? li_ : q;
+        if (!extract) {  // hand the heap on in layout order (kout == k)
+            const int n = *s_len;
+            for (int i = lane; i < n; i += 64) {
+                out_ids[orow * kout + i] = hid[i];
+                out_d[orow * kout + i] = hd[i];
+            }
+            if (lane == 0) out_n[orow] = n;
+        } else if (lane == 0) {  // extractHeap (flat/index.go:676-688)
+            ReplayHeap h{hid, hd, *s_len};
+            const int n = h.len;
+            for (int i = n - 1; i >= 0; i--) {
+                uint64_t x; float y;
+                rh_pop(h, &x, &y);
+                if (i < kout) { out_ids[orow * kout + i] = x; out_d[orow * kout + i] = y; }
+            }
+            out_n[orow] = n < kout ? n : kout;
+        }
+        wave_sync_lds();
+    }
+}
+
 }  // namespace wv

@@ -32,6 +32,7 @@
 #include "rq_kernels.hip"
 #include "gemv_kernels.hip"
 #include "qs_kernels.hip"
+#include "sq_kernels.hip"
 
 using namespace wv;
 
@@ -119,8 +120,11 @@ struct wv_index {
     int variant = WV_VARIANT_AVX256;
     int compression = WV_COMPRESSION_NONE;
     int rescore_limit = -1;
-    int cache_opt = 0;
-    int replay_par = 1;  // BQ.Cache / RQ.Cache (flatent UserConfig): QueryVectorDistancer reads codes
+    int cache_opt = 0;   // BQ.Cache / RQ.Cache (flatent UserConfig): QueryVectorDistancer reads codes
+    int replay_par = 2;  // block-key replay: 2 = pooled three-kernel form (k < 64), 3 = pooled for any k,
+                         // 1 = 8-wave form, 0 = one wave
+    int64_t rp_pool = 1 << 20;  // pooled replay: candidate blocks per batch (144 B each)
+    int qs_force_flag = 0;      // tests: flag every query of the block-key path (exercise the replay)
     int device = 0;
     uint64_t id_base = 0;
     std::string root_path;
@@ -176,6 +180,14 @@ struct wv_index {
     float* rq_round = nullptr;    // [D] (rq-1)
     void* rq_codes = nullptr;     // rq-8: tiled [cap][D] bytes; rq-1: [D/64][cap] u64
     float4* rq_meta = nullptr;    // [cap]
+    // scalar quantizer (sq_kernels.hip): range a, b and the Go float32 constants
+    int sq_ready = 0, sq_Dq = 0;
+    float sq_a = 0.f, sq_b = 0.f, sq_a2 = 0.f, sq_ab = 0.f, sq_ib2 = 0.f;
+    uint4* sq_codes = nullptr;    // rq-8 layout, Dq = round_up(d, 16) bytes per row
+    uint2* sq_meta = nullptr;     // [cap] {sum, sum2} of the codes
+    DBuf sqq, sqm;                // query codes / meta
+    // hnsw.flatSearch parameters (wv_index_hnsw_flat_search)
+    int hnsw_ef = -1, ef_min = 100, ef_max = 500, ef_factor = 8, hnsw_rescore = 1;
     std::vector<uint8_t> h_present;
     uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
     int64_t npresent = 0;
@@ -190,6 +202,7 @@ struct wv_index {
     hipEvent_t evd[2] = {nullptr, nullptr}, evr[2] = {nullptr, nullptr};
     DBuf rE2, rB2;
     DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
+    DBuf rpBlk, rpLb, rpQ, rpE, rpVm, rpOff, rpTot, rpCtr;  // pooled replay (k_rp_*)
     DBuf gmA, gmI;  // GEMV path: first level of the two-level span merge
     wv_stats stats{};
     // micro-batcher of concurrent single-query searches (batcher.hip)
@@ -218,7 +231,7 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
         return set_err(WV_ERR_INVALID, "invalid config: unknown distance metric %d", cfg->metric);
     if (cfg->compression != WV_COMPRESSION_NONE && cfg->compression != WV_COMPRESSION_BQ &&
         cfg->compression != WV_COMPRESSION_PQ && cfg->compression != WV_COMPRESSION_RQ8 &&
-        cfg->compression != WV_COMPRESSION_RQ1)
+        cfg->compression != WV_COMPRESSION_RQ1 && cfg->compression != WV_COMPRESSION_SQ)
         return set_err(WV_ERR_UNSUPPORTED, "invalid config: unsupported compression %d", cfg->compression);
     // distancerIndicatorsAndError (rotational_quantization.go:41-55)
     if ((cfg->compression == WV_COMPRESSION_RQ8 || cfg->compression == WV_COMPRESSION_RQ1) &&
@@ -278,12 +291,17 @@ extern "C" void wv_index_destroy(wv_index* idx) {
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
                     &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm,
                     &idx->rE2, &idx->rB2, &idx->gmA, &idx->gmI, &idx->qsQb, &idx->qsInfo, &idx->qsKey, &idx->qsCand,
-                    &idx->qsNc, &idx->qsEps, &idx->qsFlags, &idx->qsList, &idx->qsScratch})
+                    &idx->qsNc, &idx->qsEps, &idx->qsFlags, &idx->qsList, &idx->qsScratch, &idx->rpBlk, &idx->rpLb,
+                    &idx->rpQ, &idx->rpE, &idx->rpVm, &idx->rpOff, &idx->rpTot, &idx->rpCtr})
         b->release();
     if (idx->aux) hipStreamSynchronize(idx->aux);
     for (hipEvent_t e : {idx->evd[0], idx->evd[1], idx->evr[0], idx->evr[1]})
         if (e) hipEventDestroy(e);
     if (idx->aux) hipStreamDestroy(idx->aux);
+    if (idx->sq_codes) hipFree(idx->sq_codes);
+    if (idx->sq_meta) hipFree(idx->sq_meta);
+    idx->sqq.release();
+    idx->sqm.release();
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
     if (idx->present) hipFree(idx->present);
@@ -331,6 +349,8 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     void* rqc = nullptr;
     float4* rqm = nullptr;
     uint32_t* pc = nullptr;
+    uint4* sqc = nullptr;
+    uint2* sqmt = nullptr;
     const int words = (idx->dims + 63) / 64;
     const size_t rq_cb = idx->rq_bits == 8 ? (size_t)nc * idx->rq_D : (size_t)(idx->rq_D / 64) * nc * sizeof(uint64_t);
     const int64_t pq_w = idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0 ? pq_mwp(idx->pq_m) : 0;
@@ -356,6 +376,10 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         WV_STEP("rq meta", alloc((void**)&rqm, (size_t)nc * sizeof(float4)));
     }
     if (pq_w) WV_STEP("pq codes", alloc((void**)&pc, (size_t)pq_w * nc * sizeof(uint32_t)));
+    if (idx->sq_ready) {
+        WV_STEP("sq codes", alloc((void**)&sqc, (size_t)nc * idx->sq_Dq));
+        WV_STEP("sq meta", alloc((void**)&sqmt, (size_t)nc * sizeof(uint2)));
+    }
     // zero the new tails, copy the old contents
     WV_STEP("memset", hipMemsetAsync(pr, 0, (size_t)(nc / 32) * sizeof(uint32_t), s));
     WV_STEP("memset", hipMemsetAsync(xn, 0, (size_t)nc * sizeof(float), s));
@@ -403,6 +427,14 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         if (oc > 0 && idx->pq_codes)
             WV_STEP("copy", hipMemcpyAsync(pc, idx->pq_codes, (size_t)pq_w * oc * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     }
+    if (sqc) {  // 256-row tiles: the old tiles are a prefix
+        WV_STEP("memset", hipMemsetAsync(sqc, 0, (size_t)nc * idx->sq_Dq, s));
+        WV_STEP("memset", hipMemsetAsync(sqmt, 0, (size_t)nc * sizeof(uint2), s));
+        if (oc > 0 && idx->sq_codes) {
+            WV_STEP("copy", hipMemcpyAsync(sqc, idx->sq_codes, (size_t)oc * idx->sq_Dq, hipMemcpyDeviceToDevice, s));
+            WV_STEP("copy", hipMemcpyAsync(sqmt, idx->sq_meta, (size_t)oc * sizeof(uint2), hipMemcpyDeviceToDevice, s));
+        }
+    }
     const hipError_t es = hipStreamSynchronize(s);
     if (e == hipSuccess && es != hipSuccess) { e = es; what = "sync"; }
 #undef WV_STEP
@@ -430,6 +462,8 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         swap_in(idx->rq_meta, rqm);
     }
     swap_in(idx->pq_codes, pc);
+    swap_in(idx->sq_codes, sqc);
+    swap_in(idx->sq_meta, sqmt);
     idx->cap = nc;
     idx->h_present.resize((size_t)nc, 0);
     return WV_OK;
@@ -522,6 +556,10 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
         k_rows_split<<<(unsigned)((n + 3) / 4), 256, 0, idx->stream>>>(idx->X, idx->dpad, idx->dpb, n, d_slots, idx->Xb,
                                                                        idx->qsmax);
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) launch_pq_encode(idx, n, d_slots);
+    if (idx->sq_ready)  // the compressor encodes every inserted vector (hnsw insert -> compressor.Preload)
+        k_sq_encode<0><<<(unsigned)((n + 3) / 4), 256, 0, idx->stream>>>(idx->X, idx->dpad, n, idx->dims, d_slots,
+                                                                        idx->sq_Dq, idx->sq_a, idx->sq_b,
+                                                                        idx->sq_codes, idx->sq_meta);
     if (idx->rq_ready)  // Preload: quantizer.EncodeBytes / EncodeUint64 of the stored row (flat/index.go:844-865)
         launch_rq_encode(idx, idx->stream, idx->X, idx->dpad, n, d_slots, 0, idx->rq_codes, idx->cap, idx->rq_meta);
     if (idx->compression == WV_COMPRESSION_BQ) {  // Preload: quantizer.Encode of the stored row (flat/index.go:376)
@@ -743,7 +781,23 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
         if (idx->dims) set_dims(idx, idx->dims);
     }
     else if (k == "bq_kernel") idx->bq_kernel = (int)value;
-    else if (k == "replay_par") idx->replay_par = value ? 1 : 0;  // 0: one-wave block-key replay only
+    else if (k == "replay_par") {  // 2: pooled k_rp_* for k < 64 (default), 3: pooled for every k,
+                                   // 1: k_blk_replay_par for k < 64, 0: k_blk_replay only
+        if (value < 0 || value > 3) return set_err(WV_ERR_INVALID, "replay_par must be 0..3");
+        idx->replay_par = (int)value;
+    }
+    else if (k == "qs_force_flag") idx->qs_force_flag = value ? 1 : 0;
+    else if (k == "ef") idx->hnsw_ef = (int)value;  // hnsw UserConfig.EF (-1: dynamic)
+    else if (k == "ef_min") idx->ef_min = (int)value;
+    else if (k == "ef_max") idx->ef_max = (int)value;
+    else if (k == "ef_factor") idx->ef_factor = (int)value;
+    else if (k == "hnsw_rescore") idx->hnsw_rescore = value ? 1 : 0;  // 0: doNotRescore
+    else if (k == "rescore_limit") idx->rescore_limit = (int)value;
+    else if (k == "rp_pool") {  // pooled replay capacity in 32-row blocks (tests force the fallback with 1)
+        if (value < 1 || value > (1ll << 26)) return set_err(WV_ERR_INVALID, "rp_pool out of range");
+        idx->rp_pool = value;
+        idx->rpBlk.release(); idx->rpLb.release(); idx->rpQ.release(); idx->rpE.release(); idx->rpVm.release();
+    }
     else if (k == "cache") {  // BQ.Cache / RQ.Cache: QueryVectorDistancer uses the cached codes
         if (value != 0 && value != 1) return set_err(WV_ERR_INVALID, "cache must be 0 or 1");
         idx->cache_opt = (int)value;
@@ -1523,26 +1577,80 @@ static int ensure_aux(wv_index* idx) {
     return WV_OK;
 }
 
-static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
-                     const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+static int rq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq);
+static int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int F, int64_t ld, float* E,
+                   float* bmin);
+
+// SQ query codes: idx->qn (prepared, normalised for cosine) -> group-tiled sqq / sqm
+static int sq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq) {
+    const int64_t nq32 = round_up(nq, RQ_QPB);
+    HIPCHK(idx->sqq.ensure((size_t)nq32 * idx->sq_Dq));
+    HIPCHK(idx->sqm.ensure((size_t)nq32 * sizeof(uint2)));
+    if (nq32 > nq) {
+        HIPCHK(hipMemsetAsync(idx->sqq.p, 0, (size_t)nq32 * idx->sq_Dq, s));
+        HIPCHK(hipMemsetAsync(idx->sqm.p, 0, (size_t)nq32 * sizeof(uint2), s));
+    }
+    k_sq_encode<1><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(idx->qn.as<float>(), idx->dpad, nq, idx->dims, nullptr,
+                                                             idx->sq_Dq, idx->sq_a, idx->sq_b, idx->sqq.as<uint4>(),
+                                                             idx->sqm.as<uint2>());
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
+// hnsw.flatSearch over the compressed vectors (flat_search.go:28-141, one
+// worker) + optional h.rescore (search.go:1047-1110, one worker).  The
+// compressor distance of every (query, allowed row) is materialised per query
+// group (k_pq_adc / k_sq_dist / k_rq*_dist / k_bq_dist, with 256-row block
+// minima), the worker heap (addResult == insertToHeap with `limit`) is
+// replayed in id order by k_replay_scan on the aux stream beside the next
+// group's distance kernel, k_pq_finish merges it into the result heap in pop
+// order (and trims SQ / RQ to `trim`), k_rescore + k_pq_rescore_final rescore.
+// Outputs [nq][k].
+static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, int limit,
+                       int trim, int rescore, const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+    const int comp = idx->rq_bits ? WV_COMPRESSION_RQ8 : idx->compression;
+    if (comp == WV_COMPRESSION_BQ && (qd + 63) / 64 != idx->words)  // HammingBitwise (distancer/hamming.go:63-66)
+        return set_err(WV_ERR_VECTOR_LENGTH, "both vectors should have the same len");
+    if (comp == WV_COMPRESSION_SQ && qd != idx->dims)  // DistanceBetweenCompressedVectors (scalar_quantization.go:46-49)
+        return set_err(WV_ERR_INVALID, "vector lengths don't match: %lld vs %d", (long long)qd + 8, idx->dims + 8);
     if (qd != idx->dims)
         return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)qd, idx->dims);
     if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
-    const int rescore = idx->pq_rescore ? 1 : 0;
-    const int R = rescore && idx->rescore_limit > k ? idx->rescore_limit : k;
+    if (comp == WV_COMPRESSION_SQ && idx->metric == WV_METRIC_HAMMING)  // scalar_quantization.go:56
+        return set_err(WV_ERR_UNSUPPORTED, "Distance not supported yet hamming");
+    if (comp == WV_COMPRESSION_SQ && !idx->sq_ready) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (comp == WV_COMPRESSION_PQ && !idx->pq_trained) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (idx->rq_bits && !idx->rq_ready) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (limit < k) limit = k;
+    const int R = limit;
     if (R > 8192) return set_err(WV_ERR_UNSUPPORTED, "limit %d > 8192", R);
     const int64_t nq_pad = round_up(nq, QB);
     int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
     if (rc) return rc;
     const float* Qn = idx->qn.as<float>();
-    const int m = idx->pq_m, K = idx->pq_ks;
     idx->stats.queries += (uint64_t)nq;
     idx->stats.batches++;
-    HIPCHK(idx->lut.ensure((size_t)nq * m * K * sizeof(float)));
-    k_pq_lut<<<(unsigned)((nq * m * K + 255) / 256), 256, 0, s>>>(Qn, idx->dpad, nq, m, K, idx->pq_ds,
-                                                                   idx->metric == WV_METRIC_L2_SQUARED ? L2 : DOT,
-                                                                   idx->pq_centers, idx->lut.as<float>());
-    HIPCHK(hipGetLastError());
+    // per-compressor query state
+    if (comp == WV_COMPRESSION_PQ) {
+        const int m = idx->pq_m, K = idx->pq_ks;
+        HIPCHK(idx->lut.ensure((size_t)nq * m * K * sizeof(float)));
+        k_pq_lut<<<(unsigned)((nq * m * K + 255) / 256), 256, 0, s>>>(Qn, idx->dpad, nq, m, K, idx->pq_ds,
+                                                                       idx->metric == WV_METRIC_L2_SQUARED ? L2 : DOT,
+                                                                       idx->pq_centers, idx->lut.as<float>());
+        HIPCHK(hipGetLastError());
+    } else if (comp == WV_COMPRESSION_RQ8) {
+        rc = rq_encode_queries(idx, s, nq);
+        if (rc) return rc;
+    } else if (comp == WV_COMPRESSION_SQ) {
+        rc = sq_encode_queries(idx, s, nq);
+        if (rc) return rc;
+    } else if (comp == WV_COMPRESSION_BQ) {
+        HIPCHK(idx->qcodes.ensure((size_t)nq * idx->words * sizeof(uint64_t)));
+        const int64_t nt = nq * idx->words;
+        k_bq_encode_rows<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(Qn, idx->dpad, nq, idx->dims, nullptr,
+                                                                       idx->qcodes.as<uint64_t>(), nq);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(idx->ident.ensure((size_t)nq * sizeof(int32_t)));
     {
         std::vector<int32_t> id((size_t)nq);
@@ -1552,14 +1660,18 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     const int32_t* qlist = idx->ident.as<int32_t>();
     const int64_t nslots = idx->hiwater;
     const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
-    // groups sized to the free HBM, replay on the aux stream beside the next
-    // group's ADC kernel (as search_rq)
+    // query groups sized to the free HBM (two distance buffers), multiples of
+    // RQ_QPB for the thread-per-row kernels
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     const int64_t have = (int64_t)(Eb0_bytes(idx) + free_b / 4);
     const int64_t budget = std::max<int64_t>(std::min<int64_t>(16ll << 30, have), 1ll << 30);
-    const int64_t G = std::max<int64_t>(1, std::min<int64_t>(nq, budget / (ld * 4)));
-    idx->stats.last_group_queries = (uint64_t)G;
+    int64_t G = std::max<int64_t>(1, std::min<int64_t>(nq, budget / (ld * 4)));
+    if (comp != WV_COMPRESSION_PQ) {
+        G = std::max<int64_t>(RQ_QPB, G / RQ_QPB * RQ_QPB);
+        G = std::min<int64_t>(G, round_up(nq, RQ_QPB));
+    }
+    idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(G, nq);
     rc = ensure_aux(idx);
     if (rc) return rc;
     DBuf* Eb[2] = {&idx->rE, &idx->rE2};
@@ -1572,7 +1684,6 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
     HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
     const int wrapm = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
-    const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
     const size_t lds_rep = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
     if (lds_rep > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rep));
@@ -1584,13 +1695,29 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
         float* Bm = Bb[b]->as<float>();
         if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
-        dim3 grid((unsigned)F, (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
-        if (K == 256)
-            k_pq_adc<256><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots, idx->lut.as<float>(),
-                                                     qlist + g0, wrapm, ld, E, Bm);
-        else
-            k_pq_adc<0><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots, idx->lut.as<float>(),
-                                                   qlist + g0, wrapm, ld, E, Bm);
+        if (comp == WV_COMPRESSION_PQ) {
+            const int m = idx->pq_m, K = idx->pq_ks;
+            const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
+            dim3 grid((unsigned)F, (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
+            if (K == 256)
+                k_pq_adc<256><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,
+                                                         idx->lut.as<float>(), qlist + g0, wrapm, ld, E, Bm);
+            else
+                k_pq_adc<0><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,
+                                                       idx->lut.as<float>(), qlist + g0, wrapm, ld, E, Bm);
+        } else if (comp == WV_COMPRESSION_RQ8) {
+            rc = rq_dist(idx, s, valid, g0, F, ld, E, Bm);
+            if (rc) return rc;
+        } else if (comp == WV_COMPRESSION_SQ) {
+            dim3 grid((unsigned)((F + RQ_QPB - 1) / RQ_QPB), (unsigned)(ld / 256));
+            k_sq_dist<<<grid, 256, 0, s>>>(idx->sq_codes, idx->sq_meta, idx->sq_Dq, valid, nslots,
+                                           idx->sqq.as<uint4>(), idx->sqm.as<uint2>(), g0, F, wrapm, idx->sq_a2,
+                                           idx->sq_ab, idx->sq_ib2, ld, E, Bm);
+        } else {  // BQ
+            dim3 grid((unsigned)((F + RQ_QPB - 1) / RQ_QPB), (unsigned)(ld / 256));
+            k_bq_dist<<<grid, 256, 0, s>>>(idx->codes, idx->cap, idx->words, valid, nslots, idx->qcodes.as<uint64_t>(),
+                                           nq, g0, F, ld, E, Bm);
+        }
         HIPCHK(hipGetLastError());
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
         HIPCHK(hipEventRecord(idx->evd[b], s));
@@ -1610,7 +1737,7 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
         HIPCHK(hipFuncSetAttribute((const void*)k_pq_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
     k_pq_finish<<<(unsigned)nq, 64, lds_f, s>>>(idx->ascI.as<uint64_t>(), idx->ascD.as<float>(), idx->ascN.as<int32_t>(),
                                                 qlist, (int)nq, R, k, rescore, idx->id_base, o_ids, o_d, o_n,
-                                                idx->cslot.as<uint32_t>(), idx->cn.as<int32_t>());
+                                                idx->cslot.as<uint32_t>(), idx->cn.as<int32_t>(), rescore ? trim : 0);
     HIPCHK(hipGetLastError());
     if (rescore) {
         HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
@@ -1620,9 +1747,11 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
         switch (idx->metric) {
         case WV_METRIC_L2_SQUARED: if (v5) WV_RS(L2, AVX512); else WV_RS(L2, AVX256); break;
         case WV_METRIC_DOT: if (v5) WV_RS(DOT, AVX512); else WV_RS(DOT, AVX256); break;
-        default: if (v5) WV_RS(COSINE, AVX512); else WV_RS(COSINE, AVX256); break;
+        case WV_METRIC_COSINE_DOT: if (v5) WV_RS(COSINE, AVX512); else WV_RS(COSINE, AVX256); break;
+        default: WV_RS(HAMMING, AVX256); break;
         }
 #undef WV_RS
+        HIPCHK(hipGetLastError());
         const size_t lds_q = (size_t)(k + 1) * (sizeof(uint64_t) + sizeof(float)) + 16;
         if (lds_q > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void*)k_pq_rescore_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
@@ -1636,6 +1765,154 @@ static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
         float ms = 0.f;
         hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
         idx->stats.last_select_ms = ms;
+    }
+    return WV_OK;
+}
+
+// the PQ index behind SearchByVector: hnsw.flatSearch with limit =
+// max(rescore_limit, k) when rescoring (the caller's ef), else k
+static int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
+                     const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+    const int rescore = idx->pq_rescore ? 1 : 0;
+    const int R = rescore && idx->rescore_limit > k ? idx->rescore_limit : k;
+    return search_hnsw(idx, s, d_qraw, nq, qd, k, R, 0, rescore, valid, o_ids, o_d, o_n);
+}
+
+// searchTimeEF (hnsw/search.go:44-76)
+static int hnsw_search_ef(const wv_index* idx, int k) {
+    int ef = idx->hnsw_ef;
+    if (ef < 1) {  // autoEfFromK
+        ef = k * idx->ef_factor;
+        if (ef > idx->ef_max) ef = idx->ef_max;
+        else if (ef < idx->ef_min) ef = idx->ef_min;
+        if (k > ef) ef = k;
+        return ef;
+    }
+    return ef < k ? k : ef;
+}
+
+// hnsw.SearchByVector's flat branch for a compressed index: limit / trim / rescore
+static int search_hnsw_flat(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
+                            const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+    const bool sqrq = idx->compression == WV_COMPRESSION_SQ || idx->rq_bits != 0;
+    // shouldRescore (search.go:182-189); a PQ index created with pq_rescore = 0 counts as doNotRescore
+    bool rescore = idx->hnsw_rescore != 0 && !(sqrq && idx->rescore_limit == 0);
+    if (idx->compression == WV_COMPRESSION_PQ && !idx->pq_rescore) rescore = false;
+    const int limit = rescore ? hnsw_search_ef(idx, k) : k;  // flat_search.go:31-33
+    const int trim = (sqrq && idx->rescore_limit >= k) ? idx->rescore_limit : 0;
+    return search_hnsw(idx, s, d_qraw, nq, qd, k, limit, trim, rescore ? 1 : 0, valid, o_ids, o_d, o_n);
+}
+
+// ---------------------------------------------------------------------------
+// scalar quantizer (compressionhelpers/scalar_quantization.go)
+// ---------------------------------------------------------------------------
+// a, b -> the float32 constants of the distance (NewScalarQuantizer :93-95),
+// codes for the current capacity, every stored row encoded
+static int sq_set(wv_index* idx, float a, float b) {
+    const float codes2 = 65025.0f;  // codes * codes
+    float t = a * a;
+    idx->sq_a2 = t / codes2;
+    t = a * b;
+    idx->sq_ab = t / 255.0f;
+    t = b * b;
+    idx->sq_ib2 = t * (float)idx->dims;
+    idx->sq_a = a;
+    idx->sq_b = b;
+    idx->sq_Dq = (int)round_up(idx->dims, 16);
+    if (!idx->sq_codes && idx->cap > 0) {
+        HIPCHK(hipMalloc(&idx->sq_codes, (size_t)idx->cap * idx->sq_Dq));
+        HIPCHK(hipMalloc(&idx->sq_meta, (size_t)idx->cap * sizeof(uint2)));
+        HIPCHK(hipMemsetAsync(idx->sq_codes, 0, (size_t)idx->cap * idx->sq_Dq, idx->stream));
+        HIPCHK(hipMemsetAsync(idx->sq_meta, 0, (size_t)idx->cap * sizeof(uint2), idx->stream));
+    }
+    idx->sq_ready = 1;
+    if (idx->hiwater > 0) {
+        k_sq_encode<0><<<(unsigned)((idx->hiwater + 3) / 4), 256, 0, idx->stream>>>(
+            idx->X, idx->dpad, idx->hiwater, idx->dims, nullptr, idx->sq_Dq, a, b, idx->sq_codes, idx->sq_meta);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    return WV_OK;
+}
+
+extern "C" int wv_index_sq_fit(wv_index* idx, int64_t training_limit) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->compression != WV_COMPRESSION_SQ) return set_err(WV_ERR_INVALID, "sq_fit: index is not SQ-compressed");
+    if (idx->npresent == 0 || idx->dims == 0)  // hnsw/compress.go:34-36
+        return set_err(WV_ERR_INVALID, "compress command cannot be executed before inserting some data");
+    std::vector<int64_t> rows;
+    for (int64_t sl = 0; sl < idx->hiwater; sl++) {
+        if (!idx->h_present[sl]) continue;
+        rows.push_back(sl);
+        if (training_limit > 0 && (int64_t)rows.size() >= training_limit) break;
+    }
+    // NewScalarQuantizer (:73-97): b = data[0][0]; a grows with every new
+    // minimum (a += b - x) or sets to the new range (a = x - b), in float32
+    const int d = idx->dims;
+    // one copy of the slot range holding the sample (padded rows, dpad stride)
+    const int64_t span = rows.back() + 1;
+    std::vector<float> buf((size_t)span * idx->dpad);
+    HIPCHK(hipMemcpy(buf.data(), idx->X, buf.size() * sizeof(float), hipMemcpyDeviceToHost));
+    float a = 0.f, b = 0.f;
+    for (size_t i = 0; i < rows.size(); i++) {
+        const float* row = buf.data() + (size_t)rows[i] * idx->dpad;
+        if (i == 0) b = row[0];
+        for (int j = 0; j < d; j++) {
+            const float x = row[j];
+            if (x < b) {
+                const float t = b - x;
+                a = a + t;
+                b = x;
+            } else if (x - b > a) {
+                a = x - b;
+            }
+        }
+    }
+    return sq_set(idx, a, b);
+}
+
+extern "C" int wv_index_sq_restore(wv_index* idx, float a, float b) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->compression != WV_COMPRESSION_SQ) return set_err(WV_ERR_INVALID, "sq_restore: index is not SQ-compressed");
+    if (a == 0.f) return set_err(WV_ERR_INVALID, "invalid range value while restoring SQ settings");
+    if (idx->dims == 0) return set_err(WV_ERR_INVALID, "sq_restore: dimensions not set yet");
+    return sq_set(idx, a, b);
+}
+
+extern "C" int wv_index_sq_info(wv_index* idx, float* out) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    out[0] = idx->sq_a;
+    out[1] = idx->sq_b;
+    out[2] = (float)idx->sq_ready;
+    out[3] = (float)(idx->dims + 8);
+    return WV_OK;
+}
+
+extern "C" int wv_index_sq_codes(wv_index* idx, uint8_t* out, int64_t n) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (!idx->sq_ready) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
+    if (n < 0 || n > idx->cap) return set_err(WV_ERR_INVALID, "sq_codes: n out of range");
+    const int Dq = idx->sq_Dq, d = idx->dims, nch = Dq / 16;
+    std::vector<uint8_t> tiles((size_t)round_up(std::max<int64_t>(n, 1), 256) * Dq);
+    std::vector<uint2> meta((size_t)std::max<int64_t>(n, 1));
+    HIPCHK(hipMemcpy(tiles.data(), idx->sq_codes, std::min<size_t>(tiles.size(), (size_t)idx->cap * Dq), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(meta.data(), idx->sq_meta, (size_t)n * sizeof(uint2), hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < n; r++) {
+        uint8_t* o = out + r * (d + 8);
+        for (int e = 0; e < d; e++) {
+            const int c = e / 16;
+            o[e] = tiles[((size_t)((r >> 8) * nch + c) * 256 + (r & 255)) * 16 + (e & 15)];
+        }
+        const uint32_t v[2] = {meta[r].x, meta[r].y};
+        for (int w = 0; w < 2; w++)
+            for (int i = 0; i < 4; i++) o[d + 4 * w + i] = (uint8_t)(v[w] >> (24 - 8 * i));  // big endian
     }
     return WV_OK;
 }
@@ -1939,6 +2216,59 @@ static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
     const int64_t nch = (nb + RP_CH - 1) / RP_CH;
     if (max_list <= 0) return WV_OK;
+    // pooled form by default for k < 64 (few flagged queries, latency-bound);
+    // many flagged queries with large k (integer data, C2) replay faster in the
+    // one-wave kernel, which visits only blocks under the true heap top
+    const int RS = k < 64 ? 2 : k < 192 ? 4 : k < 448 ? 8 : 0;
+    if (RS && nch <= RP_MAXCH && ((idx->replay_par == 2 && k < 64) || idx->replay_par == 3)) {
+        // pooled form: bounds + candidate pool (8 waves per query), exact
+        // distances over the whole grid, one-wave heap per query
+        const int64_t pool_cap = idx->rp_pool;
+        const int64_t g1 = std::min<int64_t>(max_list, 256);
+        HIPCHK(idx->qsScratch.ensure((size_t)g1 * nch * 64 * sizeof(float)));
+        HIPCHK(idx->rpBlk.ensure((size_t)pool_cap * sizeof(uint32_t)));
+        HIPCHK(idx->rpLb.ensure((size_t)pool_cap * sizeof(float)));
+        HIPCHK(idx->rpQ.ensure((size_t)pool_cap * sizeof(int32_t)));
+        HIPCHK(idx->rpE.ensure((size_t)pool_cap * 32 * sizeof(float)));
+        HIPCHK(idx->rpVm.ensure((size_t)pool_cap * sizeof(uint32_t)));
+        HIPCHK(idx->rpOff.ensure((size_t)max_list * sizeof(int32_t)));
+        HIPCHK(idx->rpTot.ensure((size_t)max_list * sizeof(int32_t)));
+        HIPCHK(idx->rpCtr.ensure(sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(idx->rpCtr.p, 0, sizeof(uint32_t), s));
+#define WV_RPB(RSV, M) k_rp_bounds<RSV, M><<<(unsigned)g1, 512, 0, s>>>(key, ldk, nb, eps, qinfo, list, counters, nlist, k, in_d, in_n, idx->qsScratch.as<float>(), idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>())
+#define WV_RPBS(M) do { if (RS == 2) WV_RPB(2, M); else if (RS == 4) WV_RPB(4, M); else WV_RPB(8, M); } while (0)
+        switch (metric) {
+        case L2: WV_RPBS(L2); break;
+        case DOT: WV_RPBS(DOT); break;
+        default: WV_RPBS(COSINE); break;
+        }
+#undef WV_RPBS
+#undef WV_RPB
+        HIPCHK(hipGetLastError());
+#define WV_RPE(M, V) k_rp_exact<M, V><<<1024, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, idx->rpBlk.as<uint32_t>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpE.as<float>(), idx->rpVm.as<uint32_t>())
+        switch (metric) {
+        case L2: if (v5) WV_RPE(L2, AVX512); else WV_RPE(L2, AVX256); break;
+        case DOT: if (v5) WV_RPE(DOT, AVX512); else WV_RPE(DOT, AVX256); break;
+        default: if (v5) WV_RPE(COSINE, AVX512); else WV_RPE(COSINE, AVX256); break;
+        }
+#undef WV_RPE
+        HIPCHK(hipGetLastError());
+        const size_t hlds = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 64 * sizeof(float) + RPW * 32 * sizeof(float) + 16;
+        const int64_t g3 = std::min<int64_t>(max_list, 2048);
+#define WV_RPH(M, V)                                                                                            \
+    do {                                                                                                        \
+        if (hlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_rp_heap<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hlds)); \
+        k_rp_heap<M, V><<<(unsigned)g3, 64, hlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpE.as<float>(), idx->rpVm.as<uint32_t>(), idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>()); \
+    } while (0)
+        switch (metric) {
+        case L2: if (v5) WV_RPH(L2, AVX512); else WV_RPH(L2, AVX256); break;
+        case DOT: if (v5) WV_RPH(DOT, AVX512); else WV_RPH(DOT, AVX256); break;
+        default: if (v5) WV_RPH(COSINE, AVX512); else WV_RPH(COSINE, AVX256); break;
+        }
+#undef WV_RPH
+        HIPCHK(hipGetLastError());
+        return WV_OK;
+    }
     if (k < 64 && nch <= RP_MAXCH && idx->replay_par) {
         const int64_t grid = std::min<int64_t>(max_list, 256);
         HIPCHK(idx->qsScratch.ensure((size_t)grid * nch * 64 * sizeof(float)));
@@ -2106,6 +2436,7 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
             blk_pass(8, olist, idx->qscount + 2);
             HIPCHK(hipGetLastError());
         }
+        if (idx->qs_force_flag) HIPCHK(hipMemsetAsync(flags, 1, (size_t)cn * sizeof(int32_t), s));
         if (mode == 1) continue;
         // ---- flagged queries: the exact heap replay, bounded by the block keys ----
         HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
@@ -2146,6 +2477,10 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     if (idx->rq_bits) {
         if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "rq: shard-candidate mode not available");
         return search_rq(idx, s, d_qraw, nq, qd, k, valid, o_ids, o_d, o_n);
+    }
+    if (idx->compression == WV_COMPRESSION_SQ) {  // SQ exists only behind hnsw: its flat branch
+        if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "sq: shard-candidate mode not available");
+        return search_hnsw_flat(idx, s, d_qraw, nq, qd, k, valid, o_ids, o_d, o_n);
     }
     if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) {
         if (mode != 0) return set_err(WV_ERR_UNSUPPORTED, "pq: shard-candidate mode not available");
@@ -2447,6 +2782,43 @@ extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queri
     HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
     rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, valid, n_valid, idx->oIds.as<uint64_t>(),
                      idx->oD.as<float>(), idx->oN.as<int32_t>(), nullptr);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_counts, idx->oN.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_index_hnsw_flat_search(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
+                                         const uint64_t* allow_ids, int64_t n_allow, int32_t allow_mode,
+                                         uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->compression == WV_COMPRESSION_NONE)
+        return set_err(WV_ERR_UNSUPPORTED, "hnsw flat search: index is not compressed (use SearchByVector)");
+    hipStream_t s = idx->stream;
+    if (allow_mode == 1 && n_allow == 0) {
+        for (int64_t q = 0; q < nq; q++) out_counts[q] = 0;
+        return WV_OK;
+    }
+    const uint32_t* valid = nullptr;
+    int64_t n_valid = 0;
+    int rc = build_valid(idx, s, allow_ids, n_allow, allow_mode, &valid, &n_valid);
+    if (rc) return rc;
+    if (n_valid == 0 || idx->dims == 0 || nq <= 0) {
+        for (int64_t q = 0; q < nq; q++) out_counts[q] = 0;
+        return WV_OK;
+    }
+    const int kk = std::max(k, 1);
+    HIPCHK(idx->qraw.ensure((size_t)nq * d * sizeof(float)));
+    HIPCHK(idx->oIds.ensure((size_t)nq * kk * sizeof(uint64_t)));
+    HIPCHK(idx->oD.ensure((size_t)nq * kk * sizeof(float)));
+    HIPCHK(idx->oN.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
+    rc = search_hnsw_flat(idx, s, idx->qraw.as<float>(), nq, d, k, valid, idx->oIds.as<uint64_t>(),
+                          idx->oD.as<float>(), idx->oN.as<int32_t>());
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));

@@ -208,8 +208,9 @@ extern "C" int wv_index_update_user_config(wv_index* idx, const wv_config* updat
     std::lock_guard<std::mutex> g(idx->mu);
     const bool bq_rq = updated->compression == WV_COMPRESSION_BQ || updated->compression == WV_COMPRESSION_RQ8 ||
                        updated->compression == WV_COMPRESSION_RQ1;
-    // (PQ here is the hnsw flatSearch restatement: its limit follows the same field)
-    idx->rescore_limit = bq_rq || updated->compression == WV_COMPRESSION_PQ ? updated->rescore_limit : 0;
+    // (PQ / SQ here are the hnsw flatSearch restatement: limit / SQ.RescoreLimit follow the same field)
+    idx->rescore_limit = bq_rq || updated->compression == WV_COMPRESSION_PQ || updated->compression == WV_COMPRESSION_SQ
+                             ? updated->rescore_limit : 0;
     return WV_OK;
 }
 

@@ -60,7 +60,7 @@ def _allow_args(allow: Optional[AllowList]):
 
 def make_config(distance: str = "cosine", dims: int = 0, device: int = 0, variant: str = "auto",
                 root_path: bytes = b"", id_base: int = 0, bq: bool = False, rescore_limit: int = -1,
-                pq: Optional[dict] = None, rq: Optional[dict] = None) -> "_lib.WvConfig":
+                pq: Optional[dict] = None, rq: Optional[dict] = None, sq: bool = False) -> "_lib.WvConfig":
     """flatent.UserConfig subset -> wv_config (include/wv_knn.h)."""
     if distance not in DISTANCES:
         raise WeaviateError(_lib.WV_ERR_INVALID, f"unrecognized or unsupported distance metric {distance!r}")
@@ -73,7 +73,7 @@ def make_config(distance: str = "cosine", dims: int = 0, device: int = 0, varian
         raise WeaviateError(_lib.WV_ERR_INVALID, "rq bits must be 1 or 8")
     comp = (_lib.COMPRESSION_BQ if bq else _lib.COMPRESSION_PQ if pq is not None
             else (_lib.COMPRESSION_RQ8 if int(rqc.get("bits", 8)) == 8 else _lib.COMPRESSION_RQ1)
-            if rq is not None else _lib.COMPRESSION_NONE)
+            if rq is not None else _lib.COMPRESSION_SQ if sq else _lib.COMPRESSION_NONE)
     return _lib.WvConfig(DISTANCES[distance], int(dims), comp, int(rescore_limit), int(device),
                          VARIANTS[variant], int(id_base), root_path, int(pqc.get("segments", 0)),
                          int(pqc.get("centroids", 256)), int(pqc.get("trainingLimit", 100000)),
@@ -94,11 +94,11 @@ class FlatIndex:
 
     def __init__(self, distance: str = "cosine", dims: int = 0, device: int = 0, variant: str = "auto",
                  root_path: str = "", id_base: int = 0, bq: bool = False, rescore_limit: int = -1,
-                 pq: Optional[dict] = None, rq: Optional[dict] = None):
+                 pq: Optional[dict] = None, rq: Optional[dict] = None, sq: bool = False):
         self._l = _lib.load()
         self._root = root_path.encode()
         self._cfg_args = dict(distance=distance, dims=dims, device=device, variant=variant, root_path=self._root,
-                              id_base=id_base, bq=bq, rescore_limit=rescore_limit, pq=pq, rq=rq)
+                              id_base=id_base, bq=bq, rescore_limit=rescore_limit, pq=pq, rq=rq, sq=sq)
         cfg = make_config(**self._cfg_args)
         h = C.c_void_p()
         check(self._l.wv_index_create(C.byref(cfg), C.byref(h)))
@@ -107,6 +107,7 @@ class FlatIndex:
         self.bq = bool(bq)
         self.pq = pq is not None
         self.rq = rq is not None
+        self.sq = bool(sq)
         self.rescore_limit = int(rescore_limit)
         self.device = device
         self.id_base = id_base
@@ -218,6 +219,44 @@ class FlatIndex:
         check(self._l.wv_index_pq_distance(self._h, _fptr(q), q.size, c.ctypes.data_as(C.POINTER(C.c_uint8)),
                                            c.shape[0], _fptr(out)))
         return out
+
+    # -- scalar quantizer (HNSW's SQ compressor) ----------------------------
+    def sq_fit(self, training_limit: int = 0) -> None:
+        """NewScalarQuantizer over the first training_limit stored vectors (id
+        order; <= 0: all) + Encode of every stored vector."""
+        check(self._l.wv_index_sq_fit(self._h, int(training_limit)))
+
+    def sq_restore(self, a: float, b: float) -> None:  # RestoreScalarQuantizer
+        check(self._l.wv_index_sq_restore(self._h, float(a), float(b)))
+
+    def sq_info(self) -> dict:
+        out = np.zeros(4, np.float32)
+        check(self._l.wv_index_sq_info(self._h, _fptr(out)))
+        return {"a": float(out[0]), "b": float(out[1]), "ready": bool(out[2]), "code_bytes": int(out[3])}
+
+    def sq_codes(self, n: int) -> np.ndarray:
+        """Codes of slots [0, n) in the reference byte format [n][d + 8]."""
+        out = np.zeros((n, self.sq_info()["code_bytes"]), np.uint8)
+        check(self._l.wv_index_sq_codes(self._h, out.ctypes.data_as(C.POINTER(C.c_uint8)), int(n)))
+        return out
+
+    def hnsw_flat_search(self, queries, k: int, allow: Optional[AllowList] = None):
+        """hnsw.flatSearch + h.rescore over the compressed vectors (BQ / PQ / SQ /
+        RQ): wv_index_hnsw_flat_search.  Options "ef", "ef_min", "ef_max",
+        "ef_factor", "hnsw_rescore" (set_option) are the hnsw UserConfig's.
+        Returns (ids[nq,k], dists[nq,k], counts[nq])."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq, d = q.shape
+        kk = max(int(k), 1)
+        ids = np.zeros((nq, kk), dtype=np.uint64)
+        dists = np.zeros((nq, kk), dtype=np.float32)
+        counts = np.zeros(nq, dtype=np.int32)
+        ap, na, mode, _keep = _allow_args(allow)
+        check(self._l.wv_index_hnsw_flat_search(self._h, _fptr(q), nq, d, int(k), ap, na, mode, _uptr(ids),
+                                                _fptr(dists), _iptr(counts)))
+        return ids, dists, counts
 
     def reserve(self, nslots: int) -> None:
         check(self._l.wv_index_reserve(self._h, int(nslots)))
