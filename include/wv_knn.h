@@ -282,6 +282,28 @@ int wv_index_replay_device(wv_index *idx, const float *d_queries, int64_t nq, in
  * 4. wv_bq_final: the rescoring heap (:525-531) over the candidates, with E
  *    gathered [world][nq][R]: the entry of an id comes from shard
  *    min(id / id_stride, world - 1).  Outputs [nq][k]. */
+/* Sharded exact search in two phases (weaviate_amd/sharded.py):
+ * phase 1: block keys + local candidate blocks of nq device queries;
+ *   d_topA [nq][k+1] = this shard's k+1 smallest block-key A values, d_eps [nq]
+ *   its per-query error bound.  WV_ERR_UNSUPPORTED when the index is not on the
+ *   block-key path (callers then use wv_index_search_device mode 1);
+ * phase 2: given every shard's d_topA / d_eps gathered ([world][nq][k+1],
+ *   [world][nq]), cut the candidates with the global (k+1)-th smallest key and
+ *   return mode 1's outputs (kout = k+1 verified results + flags). */
+int wv_index_shard_phase1(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k, float *d_topA,
+                          float *d_eps, void *stream);
+int wv_index_shard_phase2(wv_index *idx, int32_t world, int64_t nq, const float *d_topA_all, const float *d_eps_all,
+                          int32_t k, uint64_t *d_ids, float *d_dists, int32_t *d_counts, int32_t *d_flags,
+                          void *stream);
+/* wv_index_replay_device for every query with d_flags[q] != 0 (list built on
+ * the device, no host synchronisation); states d_in_* and results d_out_*
+ * indexed by query ([nq x k], [nq]), rows of unflagged queries untouched.
+ * Needs this index's block keys of the same batch. */
+int wv_index_replay_flags_device(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k,
+                                 const int32_t *d_flags, const uint64_t *d_in_ids, const float *d_in_dists,
+                                 const int32_t *d_in_len, int32_t extract, uint64_t *d_out_ids, float *d_out_dists,
+                                 int32_t *d_out_len, void *stream);
+
 int wv_index_bq_begin(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k, void *stream);
 int wv_index_bq_replay(wv_index *idx, const uint64_t *d_in_ids, const float *d_in_dists, const int32_t *d_in_len,
                        int32_t pop, uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_len, void *stream);

@@ -64,3 +64,53 @@ def test_sharded_flat_protocol_equals_single_index(wv, oracle, shards, metric, k
     for b in backs:
         b.index.close()
     single.close()
+
+
+@pytest.mark.parametrize("shards,metric,kind,n,d,k", [(2, "cosine", 0, 12000, 768, 10),
+                                                     (3, "l2-squared", 1, 6000, 64, 10),   # integer data: ties
+                                                     (4, "dot", 0, 5000, 100, 24),
+                                                     (8, "cosine", 0, 16000, 128, 10),
+                                                     (2, "l2-squared", 1, 20000, 32, 100)])
+def test_sharded_two_phase_and_flag_chain(wv, oracle, shards, metric, kind, n, d, k):
+    """The protocol ShardedFlatSearch runs on the block-key path: phase 1 (keys
+    + each shard's k+1 smallest key values) -> gather -> phase 2 (global
+    threshold cuts the candidates, exact rows) -> packed gather -> merge ->
+    replay chain of the flagged queries with device-built lists and states
+    indexed by query.  Shards are separate indexes on one GPU; gathers and
+    broadcasts become local hand-overs.  Must equal the oracle."""
+    from weaviate_amd.sharded import GpuShardBackend, ShardedFlatSearch
+    dev = torch.device("cuda", 0)
+    data = oracle.gen_matrix(kind, 43, 0, n, d)
+    queries = oracle.gen_matrix(kind, 44, 0, 300, d)
+    per = (n + shards - 1) // shards
+    backs = []
+    for r in range(shards):
+        lo, hi = r * per, min(n, (r + 1) * per)
+        idx = wv.FlatIndex(distance=metric, id_base=lo, variant="avx256")
+        idx.add_batch(np.arange(lo, hi, dtype=np.uint64), data[lo:hi])
+        backs.append(GpuShardBackend(idx, 0))
+    q = torch.from_numpy(queries).to(dev)
+    p1 = [b.phase1(q, k) for b in backs]
+    gA = torch.stack([t for t, _ in p1])
+    gE = torch.stack([e for _, e in p1])
+    parts = [b.phase2(gA, gE, k) for b in backs]
+    gi, gd, gc, gf = (torch.stack([p[j] for p in parts]) for j in range(4))
+    oi, od, on, of = backs[0].merge(shards, k, gi, gd, gc, gf)
+    nflag = int(of.count_nonzero())
+    if kind == 1:
+        assert nflag > 0  # integer data: the replay chain must run
+    state = None
+    for r, b in enumerate(backs):
+        last = r == shards - 1
+        res = b.replay_flags(q, of, state, k, last, out=(oi, od, on) if last else None)
+        state = ShardedFlatSearch._unpack_state(ShardedFlatSearch._pack_state(*res), k)
+    oi, od, on = (t.cpu().numpy() for t in state)
+    orc = oracle.OracleFlat(oracle.METRIC[metric], 1, d, n)
+    orc.add_batch(np.arange(n), data)
+    for i in range(len(queries)):
+        rc, ei, ed = orc.search(queries[i], k)
+        assert rc == 0 and on[i] == len(ei), f"q{i}"
+        np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), ei, err_msg=f"q{i} vs oracle")
+        np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), ed.view(np.uint32), err_msg=f"q{i} vs oracle")
+    for b in backs:
+        b.index.close()

@@ -63,6 +63,57 @@ class OracleShardBackend:
             flg[i] = int(np.any(np.diff(dd[i, :m]) <= 0))
         return torch.from_numpy(ids), torch.from_numpy(dd), torch.from_numpy(cnt), torch.from_numpy(flg)
 
+    # -- two-phase form (exact distances stand in for the block keys, eps = 0) --
+    two_phase = True
+
+    def _dists(self, qv):
+        return np.array([self.o.single_dist(self.metric, 1, qv, self.store[s]) for s in range(self.begin, self.end)],
+                        np.float32)
+
+    def phase1(self, q, k):
+        qn = q.numpy()
+        nq = qn.shape[0]
+        topA = np.full((nq, k + 1), np.inf, np.float32)
+        self._d = []
+        for i in range(nq):
+            dist_ = self._dists(self._qnorm(qn[i]))
+            self._d.append(dist_)
+            srt = np.sort(dist_)[: k + 1]
+            topA[i, : len(srt)] = srt
+        return torch.from_numpy(topA), torch.zeros(nq, dtype=torch.float32)
+
+    def phase2(self, gA, gE, k):
+        gA = gA.numpy()
+        nq = gA.shape[1]
+        ids = np.zeros((nq, k + 1), np.int64)
+        dd = np.zeros((nq, k + 1), np.float32)
+        cnt = np.zeros(nq, np.int32)
+        flg = np.zeros(nq, np.int32)
+        for i in range(nq):
+            T = np.sort(gA[:, i, :].ravel())[k] + float(gE.numpy()[:, i].max()) * 2
+            dist_ = self._d[i]
+            keep = np.nonzero(dist_ <= T)[0]
+            order = keep[np.lexsort((keep, dist_[keep]))][: k + 1]
+            m = len(order)
+            ids[i, :m] = np.arange(self.begin, self.end)[order]
+            dd[i, :m] = dist_[order]
+            cnt[i] = m
+            flg[i] = int(np.any(np.diff(dd[i, :m]) <= 0))
+        return torch.from_numpy(ids), torch.from_numpy(dd), torch.from_numpy(cnt), torch.from_numpy(flg)
+
+    def replay_flags(self, q, flags, state, k, extract, out=None):
+        nq = q.shape[0]
+        ql = torch.nonzero(flags).flatten().to(torch.int32)
+        st = None if state is None else (state[0][ql.long()], state[1][ql.long()], state[2][ql.long()])
+        oi = torch.zeros((nq, k), dtype=torch.int64) if out is None else out[0]
+        od = torch.zeros((nq, k), dtype=torch.float32) if out is None else out[1]
+        on = torch.zeros(nq, dtype=torch.int32) if out is None else out[2]
+        if ql.numel():
+            ti, td, tn = self.replay(q, ql, st, k, extract)
+            rows = ql.long()
+            oi[rows], od[rows], on[rows] = ti, td, tn
+        return oi, od, on
+
     def merge(self, G, k, ids, dd, cnt, flg):
         """numpy restatement of k_merge_shards (runtime: kernels.hip)."""
         ids, dd, cnt, flg = ids.numpy(), dd.numpy(), cnt.numpy(), flg.numpy()
@@ -124,7 +175,7 @@ class OracleShardBackend:
         return torch.from_numpy(oi.view(np.int64)), torch.from_numpy(od), torch.from_numpy(on)
 
 
-def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath):
+def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath, two_phase=True):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -137,6 +188,8 @@ def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath):
     queries = orc.gen_matrix(kind, 4, 0, nq, d)
     per = (n + world - 1) // world
     b = OracleShardBackend(orc, metric, corpus, rank * per, min(n, (rank + 1) * per))
+    if not two_phase:
+        b.two_phase = False
     s = ShardedFlatSearch(b, torch.device("cpu"))
     oi, od, on = s.search(torch.from_numpy(queries), k)
     if rank == 0:
@@ -144,11 +197,12 @@ def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("two_phase", [True, False])
 @pytest.mark.parametrize("metric,kind,dup", [(0, 0, False), (0, 1, True), (2, 0, True), (1, 1, False)])
-def test_sharded_protocol_matches_single_index(tmp_path, oracle, metric, kind, dup):
+def test_sharded_protocol_matches_single_index(tmp_path, oracle, metric, kind, dup, two_phase):
     n, d, nq, k, world = 400, 8, 12, 10, 2
     out = str(tmp_path / "res.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), metric, kind, n, d, nq, k, dup, out), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), metric, kind, n, d, nq, k, dup, out, two_phase), nprocs=world,
                        join=True, start_method="spawn")
     r = np.load(out)
     corpus = oracle.gen_matrix(kind, 3, 0, n, d)

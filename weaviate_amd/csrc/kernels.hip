@@ -1206,18 +1206,31 @@ __global__ __launch_bounds__(64) void k_distance_pairs(const float* __restrict__
     out[i] = exact_dist<METRIC, VARIANT>(A + i * ld, B + i * ld, d);
 }
 
-// exact normalisation of arbitrary rows into a padded buffer (queries)
-__global__ void k_normalize_rows(const float* __restrict__ in, int64_t n, int d, float* __restrict__ out, int ld) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// exact normalisation of arbitrary rows into a padded buffer (queries):
+// distancer.Normalize (normalize.go:16-32).  One wave per row: the squares are
+// formed in parallel, the float32 sum runs serially in element order (every
+// lane adds the same readlane'd square, so the sum is wave-uniform), then the
+// divisions are parallel.
+__global__ __launch_bounds__(256) void k_normalize_rows(const float* __restrict__ in, int64_t n, int d,
+                                                        float* __restrict__ out, int ld) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
     const float* src = in + i * d;
     float* dst = out + i * ld;
     float nrm = 0.f;
-    for (int c = 0; c < d; c++) { float v = src[c]; float sq = v * v; nrm = nrm + sq; }
-    if (nrm == 0.f) { for (int c = 0; c < ld; c++) dst[c] = 0.f; return; }
-    float dv = (float)sqrt((double)nrm);
-    for (int c = 0; c < d; c++) dst[c] = src[c] / dv;
-    for (int c = d; c < ld; c++) dst[c] = 0.f;
+    for (int c0 = 0; c0 < d; c0 += 64) {
+        const float v = c0 + lane < d ? src[c0 + lane] : 0.f;
+        const float sq = v * v;
+        const int m = d - c0 < 64 ? d - c0 : 64;
+        for (int j = 0; j < m; j++) nrm = nrm + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), j));
+    }
+    if (nrm == 0.f) {
+        for (int c = lane; c < ld; c += 64) dst[c] = 0.f;
+        return;
+    }
+    const float dv = (float)sqrt((double)nrm);
+    for (int c = lane; c < ld; c += 64) dst[c] = c < d ? src[c] / dv : 0.f;
 }
 
 // hamming over uint64 words: popcount(a^b) summed, as float (distancer/hamming.go:63-68)

@@ -87,6 +87,13 @@ __device__ __forceinline__ void qs_wait_lgkm() {
     asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// LDS writes of this wave visible to its other lanes
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 template <int OFF>
 __device__ __forceinline__ f32x4_t lds_ld4f_o(unsigned base) {
@@ -654,7 +661,7 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
                                                     float gd, float gacc, uint32_t* __restrict__ cand,
                                                     int32_t* __restrict__ ncand, int32_t* __restrict__ flags,
                                                     float* __restrict__ eps_out, const int32_t* __restrict__ qlist,
-                                                    const uint32_t* __restrict__ qcount) {
+                                                    const uint32_t* __restrict__ qcount, float* __restrict__ topA) {
     constexpr int L = 64 * (R - 1);
     constexpr int U = 16;
     __shared__ float sbk[4][64];
@@ -705,6 +712,71 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
         // the L-th entry also qualifies: blocks beyond the list may too
         flags[q] = (nc >= L || qi.w != 0.f) ? 2 : 0;
     }
+    if (topA) {  // sharded phase 1: this shard's k+1 smallest block-key A values
+#pragma unroll
+        for (int r = 0; r < R - 1; r++) {
+            const int e = r * 64 + lane;
+            if (e <= k) topA[(int64_t)q * (k + 1) + e] = qs_key_to_a(metric, t.key[r], qi.x);
+        }
+    }
+}
+
+// k_blk_gthresh: sharded phase 2, wave per query.  M_g = the (k+1)-th smallest
+// of the W shards' k+1 smallest block-key A values (= the (k+1)-th smallest
+// key over the whole corpus), eps_max = the largest shard eps of the query.
+// The k+1 blocks under M_g each hold a row with E <= M_g + eps_max, so a
+// block of this shard with A > M_g + eps_max + eps cannot hold a global
+// top-(k+1) row; the candidate list (ascending by key) is cut to that prefix.
+// Queries with flag 2 (their own second pass) or more than 4096 gathered
+// values keep the local list.
+__global__ __launch_bounds__(256) void k_blk_gthresh(const float* __restrict__ topA_all, const float* __restrict__ eps_all,
+                                                     int W, int nq, int k, int metric, const float4* __restrict__ qinfo,
+                                                     const float* __restrict__ key, int64_t ldk,
+                                                     const uint32_t* __restrict__ cand, int L,
+                                                     int32_t* __restrict__ ncand, const float* __restrict__ eps_own,
+                                                     const int32_t* __restrict__ flags) {
+    __shared__ float sv[4][1024];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int q = blockIdx.x * 4 + w;
+    if (q >= nq || flags[q] == 2) return;
+    const int K1 = k + 1;
+    const int n = W * K1;
+    if (n > 1024) return;
+    float emax = 0.f;
+    for (int i = lane; i < n; i += 64) {
+        const int r = i / K1, e = i % K1;
+        sv[w][i] = topA_all[((int64_t)r * nq + q) * K1 + e];
+    }
+    for (int r = lane; r < W; r += 64) emax = fmaxf(emax, eps_all[(int64_t)r * nq + q]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) emax = fmaxf(emax, __shfl_xor(emax, o));
+    wave_sync_lds();
+    // M_g: a value v with #(< v) <= k < #(<= v)
+    float M = __builtin_inff();
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        const float v = i < n ? sv[w][i] : __builtin_inff();
+        int lt = 0, le = 0;
+        for (int j = 0; j < n; j++) {
+            const float u = sv[w][j];
+            lt += u < v ? 1 : 0;
+            le += u <= v ? 1 : 0;
+        }
+        const uint64_t hit = __ballot(i < n && lt <= k && k < le);
+        if (hit) { M = __shfl(v, __builtin_ctzll(hit)); break; }
+    }
+    if (!(M < __builtin_inff())) return;
+    const float T = M + 1.0005f * (emax + eps_own[q]);
+    const int nc = ncand[q];
+    const float qn2 = qinfo[q].x;
+    int keep = 0;
+    for (int e0 = 0; e0 < nc; e0 += 64) {
+        const int e = e0 + lane;
+        const bool in = e < nc && qs_key_to_a(metric, key[(int64_t)q * ldk + cand[(int64_t)q * L + e]], qn2) <= T;
+        keep += __popcll(__ballot(in));
+    }
+    if (lane == 0) ncand[q] = keep;
 }
 
 // k_blk_exact<R, METRIC, VARIANT>: one workgroup (4 waves) per query over its
@@ -852,11 +924,11 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     const float* qv = Qn + (int64_t)q * dpad;
     const int li = lane & 31, lh = lane >> 5;
     // the heap handed over by the previous shard (layout order), or empty
-    int len_in = in_len ? in_len[li_] : 0;
+    int len_in = in_len ? in_len[by_list ? li_ : q] : 0;
     len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
     for (int i = lane; i < len_in; i += 64) {
-        hid[i] = in_ids[(int64_t)li_ * k + i];
-        hd[i] = in_d[(int64_t)li_ * k + i];
+        hid[i] = in_ids[(int64_t)(by_list ? li_ : q) * k + i];
+        hd[i] = in_d[(int64_t)(by_list ? li_ : q) * k + i];
     }
     if (lane == 0) *s_len = len_in;
     __syncthreads();
@@ -975,11 +1047,6 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
 // ---------------------------------------------------------------------------
 constexpr int RP_NW = 8, RP_CH = 1024, RP_CAP = 6144, RP_MAXCH = 4096;
 
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <int METRIC, int VARIANT>
 __global__ __launch_bounds__(512) void k_blk_replay_par(const float* __restrict__ key, int64_t ldk, int64_t nb,
@@ -1017,12 +1084,12 @@ __global__ __launch_bounds__(512) void k_blk_replay_par(const float* __restrict_
         const float eps = eps_q[q];
         const float* kr = key + (int64_t)q * ldk;
         const float* qv = Qn + (int64_t)q * dpad;
-        int len_in = in_len ? in_len[li_] : 0;
+        int len_in = in_len ? in_len[by_list ? li_ : q] : 0;
         len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
         if (w == 0) {
             if (lane < len_in) {
-                hid[lane] = in_ids[(int64_t)li_ * k + lane];
-                hd[lane] = in_d[(int64_t)li_ * k + lane];
+                hid[lane] = in_ids[(int64_t)(by_list ? li_ : q) * k + lane];
+                hd[lane] = in_d[(int64_t)(by_list ? li_ : q) * k + lane];
             }
             if (lane == 0) s_len = len_in;
         }
@@ -1269,7 +1336,7 @@ __global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key
                                                    uint32_t* __restrict__ pool_blk, float* __restrict__ pool_lb,
                                                    int32_t* __restrict__ pool_q, uint32_t* __restrict__ pool_ctr,
                                                    int64_t pool_cap, int32_t* __restrict__ rp_off,
-                                                   int32_t* __restrict__ rp_tot) {
+                                                   int32_t* __restrict__ rp_tot, int by_list) {
     __shared__ float suc[RP_MAXCH];
     __shared__ int scc[RP_MAXCH];
     __shared__ float sg0[16];
@@ -1286,7 +1353,7 @@ __global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key
         const bool noskip = qi.w != 0.f;
         const float eps = eps_q[q];
         const float* kr = key + (int64_t)q * ldk;
-        int len_in = in_len ? in_len[li_] : 0;
+        int len_in = in_len ? in_len[by_list ? li_ : q] : 0;
         len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
         if (noskip) {  // every block, distances on the fly (k_rp_heap)
             if (threadIdx.x == 0) { rp_off[li_] = -1; rp_tot[li_] = 0; }
@@ -1315,7 +1382,7 @@ __global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key
 #pragma unroll
             for (int r = 0; r < RS; r++) {
                 const int e = r * 64 + lane;
-                sk[r] = (r < RS - 1 && e < len_in) ? in_d[(int64_t)li_ * k + e] : __builtin_inff();
+                sk[r] = (r < RS - 1 && e < len_in) ? in_d[(int64_t)(by_list ? li_ : q) * k + e] : __builtin_inff();
                 sid[r] = 0;
             }
             bitonic_sort<RS>(sk, sid, lane);
@@ -1470,11 +1537,11 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
     for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
         const int q = qlist[li_];
         const float* qv = Qn + (int64_t)q * dpad;
-        int len_in = in_len ? in_len[li_] : 0;
+        int len_in = in_len ? in_len[by_list ? li_ : q] : 0;
         len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
         for (int i = lane; i < len_in; i += 64) {
-            hid[i] = in_ids[(int64_t)li_ * k + i];
-            hd[i] = in_d[(int64_t)li_ * k + i];
+            hid[i] = in_ids[(int64_t)(by_list ? li_ : q) * k + i];
+            hd[i] = in_d[(int64_t)(by_list ? li_ : q) * k + i];
         }
         if (lane == 0) *s_len = len_in;
         wave_sync_lds();

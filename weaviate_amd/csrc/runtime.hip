@@ -203,6 +203,9 @@ struct wv_index {
     DBuf rE2, rB2;
     DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
     DBuf rpBlk, rpLb, rpQ, rpE, rpVm, rpOff, rpTot, rpCtr;  // pooled replay (k_rp_*)
+    DBuf flCtr;                      // device flag-list counters (replay_flags)
+    int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
+    int qs_phase_k = 0;
     DBuf gmA, gmI;  // GEMV path: first level of the two-level span merge
     wv_stats stats{};
     // micro-batcher of concurrent single-query searches (batcher.hip)
@@ -292,7 +295,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
                     &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm,
                     &idx->rE2, &idx->rB2, &idx->gmA, &idx->gmI, &idx->qsQb, &idx->qsInfo, &idx->qsKey, &idx->qsCand,
                     &idx->qsNc, &idx->qsEps, &idx->qsFlags, &idx->qsList, &idx->qsScratch, &idx->rpBlk, &idx->rpLb,
-                    &idx->rpQ, &idx->rpE, &idx->rpVm, &idx->rpOff, &idx->rpTot, &idx->rpCtr})
+                    &idx->rpQ, &idx->rpE, &idx->rpVm, &idx->rpOff, &idx->rpTot, &idx->rpCtr, &idx->flCtr})
         b->release();
     if (idx->aux) hipStreamSynchronize(idx->aux);
     for (hipEvent_t e : {idx->evd[0], idx->evd[1], idx->evr[0], idx->evr[1]})
@@ -962,7 +965,7 @@ static int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, in
     if (nq_pad > nq)
         HIPCHK(hipMemsetAsync(Qn + nq * idx->dpad, 0, (size_t)(nq_pad - nq) * idx->dpad * sizeof(float), s));
     if (idx->metric == WV_METRIC_COSINE_DOT)
-        k_normalize_rows<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
+        k_normalize_rows<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
     else
         k_copy_pad_rows<<<(unsigned)((nq * idx->dpad + 255) / 256), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
     k_row_norm2<<<(unsigned)((nq_pad + 3) / 4), 256, 0, s>>>(Qn, nq_pad, idx->dpad, idx->qn2.as<float>());
@@ -2235,7 +2238,7 @@ static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int
         HIPCHK(idx->rpTot.ensure((size_t)max_list * sizeof(int32_t)));
         HIPCHK(idx->rpCtr.ensure(sizeof(uint32_t)));
         HIPCHK(hipMemsetAsync(idx->rpCtr.p, 0, sizeof(uint32_t), s));
-#define WV_RPB(RSV, M) k_rp_bounds<RSV, M><<<(unsigned)g1, 512, 0, s>>>(key, ldk, nb, eps, qinfo, list, counters, nlist, k, in_d, in_n, idx->qsScratch.as<float>(), idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>())
+#define WV_RPB(RSV, M) k_rp_bounds<RSV, M><<<(unsigned)g1, 512, 0, s>>>(key, ldk, nb, eps, qinfo, list, counters, nlist, k, in_d, in_n, idx->qsScratch.as<float>(), idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>(), by_list)
 #define WV_RPBS(M) do { if (RS == 2) WV_RPB(2, M); else if (RS == 4) WV_RPB(4, M); else WV_RPB(8, M); } while (0)
         switch (metric) {
         case L2: WV_RPBS(L2); break;
@@ -2301,8 +2304,14 @@ static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int
 
 static int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : 0; }
 
+// phase 0: the whole search.  Sharded two-phase form (mode 1, one query chunk):
+// phase 1 = block keys + local candidate selection, topA [nq][k+1] = this
+// shard's k+1 smallest block-key A values (eps in idx->qsEps); phase 2 = the
+// global threshold from every shard's topA / eps (gA [W][nq][k+1], gE [W][nq],
+// k_blk_gthresh), exact distances, overflow pass.
 static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid,
-                     uint64_t* o_ids, float* o_d, int32_t* o_n, int32_t* o_flags) {
+                     uint64_t* o_ids, float* o_d, int32_t* o_n, int32_t* o_flags, int phase = 0,
+                     float* topA = nullptr, const float* gA = nullptr, const float* gE = nullptr, int W = 0) {
     const int kout = mode == 1 ? k + 1 : k;
     const int NK = idx->dpb / 16;
     const int RB = qs_rb(NK);
@@ -2321,7 +2330,8 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     HIPCHK(idx->qsNc.ensure((size_t)qc * sizeof(int32_t)));
     HIPCHK(idx->qsEps.ensure((size_t)qc * sizeof(float)));
     HIPCHK(idx->qsList.ensure((size_t)2 * qc * sizeof(int32_t)));
-    if (!o_flags) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
+    if (!o_flags || phase) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
+    if (phase && qc < nq) return set_err(WV_ERR_UNSUPPORTED, "two-phase shard search: batch exceeds one query chunk");
     const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
     if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
     // error-bound constants: reference-order fp32 (gamma_{dpb+8}) and the MFMA's
@@ -2342,6 +2352,7 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         if (c0 == 0) { idx->qs_last_nq = cn == nq ? cn : 0; idx->qs_last_nb = nb; idx->qs_last_ldk = ldk; }
         const float* Qn = Qn_all + c0 * idx->dpad;
         float4* qinfo = idx->qsInfo.as<float4>();
+        if (phase != 2)
         k_query_split<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dpb, cn, cn_pad,
                                                                    idx->qsQb.as<uint16_t>(), qinfo);
         // ---- block keys (the dominant kernel) ----
@@ -2370,6 +2381,7 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         const bool l2 = metric == L2;
         const size_t lds = (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
         dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
+        if (phase != 2) {
         const bool time_it = idx->timing && c0 == 0;
         if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
 #define WV_QS(NKV, L2V)                                                                                        \
@@ -2408,15 +2420,18 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         HIPCHK(hipGetLastError());
         if (time_it) { HIPCHK(hipEventRecord(idx->ev1, s)); idx->timed = 1; }
         idx->stats.mfma_launches++;
+        }
         // ---- candidate blocks, exact rows, proof ----
-        int32_t* flags = o_flags ? o_flags + c0 : idx->qsFlags.as<int32_t>();
+        int32_t* flags = phase ? idx->qsFlags.as<int32_t>() : o_flags ? o_flags + c0 : idx->qsFlags.as<int32_t>();
         int32_t* olist = idx->qsList.as<int32_t>() + qc;  // second half: the overflow list
-        // pass RV over all queries (list == nullptr) or over the listed ones
-        auto blk_pass = [&](int RV, const int32_t* list, const uint32_t* cnt) {
+        // select / exact pass RV over all queries (list == nullptr) or over the listed ones
+        auto sel = [&](int RV, const int32_t* list, const uint32_t* cnt, float* tA) {
             const unsigned gw = (unsigned)((cn + 3) / 4);
-#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt)
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA)
             if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
 #undef WV_SELR
+        };
+        auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt) {
 #define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags, list, cnt)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \
@@ -2428,15 +2443,25 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
 #undef WV_EXM
 #undef WV_EXR
         };
-        blk_pass(R, nullptr, nullptr);
+        if (phase != 2) sel(R, nullptr, nullptr, phase == 1 ? topA : nullptr);
+        HIPCHK(hipGetLastError());
+        if (phase == 1) continue;
+        if (phase == 2)  // the global threshold cuts this shard's candidate lists
+            k_blk_gthresh<<<(unsigned)((cn + 3) / 4), 256, 0, s>>>(gA, gE, W, (int)cn, k, metric, qinfo, a.key, ldk,
+                                                                  idx->qsCand.as<uint32_t>(), L, idx->qsNc.as<int32_t>(),
+                                                                  idx->qsEps.as<float>(), flags);
+        exa(R, nullptr, nullptr);
         HIPCHK(hipGetLastError());
         if (R < 8) {  // candidate lists that overflowed (flag 2): again with the 448-block lists
             HIPCHK(hipMemsetAsync(idx->qscount + 3, 0, sizeof(uint32_t), s));
             k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, olist, idx->qscount + 2, 2);
-            blk_pass(8, olist, idx->qscount + 2);
+            sel(8, olist, idx->qscount + 2, nullptr);
+            exa(8, olist, idx->qscount + 2);
             HIPCHK(hipGetLastError());
         }
         if (idx->qs_force_flag) HIPCHK(hipMemsetAsync(flags, 1, (size_t)cn * sizeof(int32_t), s));
+        if (phase == 2 && o_flags)
+            HIPCHK(hipMemcpyAsync(o_flags + c0, flags, (size_t)cn * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         if (mode == 1) continue;
         // ---- flagged queries: the exact heap replay, bounded by the block keys ----
         HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
@@ -2922,6 +2947,91 @@ extern "C" int wv_index_replay(wv_index* idx, const float* d_queries, int64_t nq
 // block keys of this index's last search over the same nq queries still valid
 // (qs_keys_nq), the scan visits only blocks that can insert (k_blk_replay);
 // otherwise every row's exact distance is computed (run_replay).
+// sharded two-phase exact search (weaviate_amd/sharded.py): phase 1 on the
+// block-key path only (WV_ERR_UNSUPPORTED otherwise: the caller uses mode 1)
+extern "C" int wv_index_shard_phase1(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                     float* d_topA, float* d_eps, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (!d_topA || !d_eps) return set_err(WV_ERR_INVALID, "nil buffer");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;
+    idx->qs_keys_nq = 0;
+    idx->qs_phase_nq = 0;
+    const bool qs = idx->compression == WV_COMPRESSION_NONE && idx->qs_planes && !idx->has_nonfinite &&
+                    (idx->kernel_opt == 0 || idx->kernel_opt == 7) && !idx->force_replay && qs_R(k) > 0 &&
+                    idx->metric != WV_METRIC_HAMMING && idx->dims != 0 && idx->npresent > 0 && nq > 0;
+    if (!qs) return set_err(WV_ERR_UNSUPPORTED, "two-phase shard search: not on the block-key path");
+    if (d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QBW));
+    if (rc) return rc;
+    idx->stats.queries += (uint64_t)nq;
+    idx->stats.batches++;
+    rc = search_qs(idx, s, nq, k, 1, idx->present, nullptr, nullptr, nullptr, nullptr, 1, d_topA);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(d_eps, idx->qsEps.p, (size_t)nq * sizeof(float), hipMemcpyDeviceToDevice, s));
+    idx->qs_phase_nq = nq;
+    idx->qs_phase_k = k;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_index_shard_phase2(wv_index* idx, int32_t world, int64_t nq, const float* d_topA_all,
+                                     const float* d_eps_all, int32_t k, uint64_t* d_ids, float* d_dists,
+                                     int32_t* d_counts, int32_t* d_flags, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (!d_topA_all || !d_eps_all || !d_ids || !d_dists || !d_counts || !d_flags)
+        return set_err(WV_ERR_INVALID, "nil buffer");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (idx->qs_phase_nq != nq || idx->qs_phase_k != k || world < 1)
+        return set_err(WV_ERR_INVALID, "shard phase 2 without a matching phase 1 (nq %lld, k %d)", (long long)nq, k);
+    idx->qs_phase_nq = 0;
+    int rc = search_qs(idx, s, nq, k, 1, idx->present, d_ids, d_dists, d_counts, d_flags, 2, nullptr, d_topA_all,
+                       d_eps_all, world);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// the cross-shard replay of every query with d_flags[q] != 0, list built on the
+// device; states and results indexed by query.  Needs this index's block keys
+// of the same batch (wv_index_search_device mode 1 or the two phases).
+extern "C" int wv_index_replay_flags_device(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                            const int32_t* d_flags, const uint64_t* d_in_ids, const float* d_in_dists,
+                                            const int32_t* d_in_len, int32_t extract, uint64_t* d_out_ids,
+                                            float* d_out_dists, int32_t* d_out_len, void* stream) {
+    (void)d_queries;
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0 || nq < 0 || !d_flags || !d_out_ids || !d_out_dists || !d_out_len)
+        return set_err(WV_ERR_INVALID, "invalid arguments");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (nq == 0) return WV_OK;
+    const bool have_data = idx->dims != 0 && idx->npresent > 0;
+    if (have_data && d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    if (!have_data || idx->qs_keys_nq != nq)
+        return set_err(WV_ERR_UNSUPPORTED, "replay_flags: no block keys of this batch");
+    HIPCHK(idx->flCtr.ensure(2 * sizeof(uint32_t)));
+    HIPCHK(idx->qsList.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
+    k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(d_flags, (int)nq, idx->qsList.as<int32_t>(),
+                                                              idx->flCtr.as<uint32_t>(), 0);
+    HIPCHK(hipGetLastError());
+    int rc = launch_blk_replay(idx, s, idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb, idx->qsEps.as<float>(),
+                               idx->qsInfo.as<float4>(), idx->present, idx->qn.as<float>(), idx->qsList.as<int32_t>(),
+                               idx->flCtr.as<uint32_t>(), 0, nq, k, k, d_out_ids, d_out_dists, d_out_len, d_in_ids,
+                               d_in_dists, d_in_len, extract, 0);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
 extern "C" int wv_index_replay_device(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
                                       const int32_t* d_qlist, int32_t nlist, const uint64_t* d_in_ids,
                                       const float* d_in_dists, const int32_t* d_in_len, int32_t extract,
@@ -3049,7 +3159,7 @@ extern "C" int wv_normalize_batch(int32_t device, const float* vecs, int64_t n, 
     HIPCHK(A.ensure((size_t)n * d * 4));
     HIPCHK(O.ensure((size_t)n * d * 4));
     HIPCHK(hipMemcpy(A.p, vecs, (size_t)n * d * 4, hipMemcpyHostToDevice));
-    k_normalize_rows<<<(unsigned)((n + 255) / 256), 256>>>(A.as<float>(), n, (int)d, O.as<float>(), (int)d);
+    k_normalize_rows<<<(unsigned)((n + 3) / 4), 256>>>(A.as<float>(), n, (int)d, O.as<float>(), (int)d);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpy(out, O.p, (size_t)n * d * 4, hipMemcpyDeviceToHost);
     A.release(); O.release();

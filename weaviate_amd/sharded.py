@@ -3,17 +3,22 @@
 Mirrors Weaviate's shard-local top-k + coordinator merge
 (adapters/repos/db/index.go:1928-2071) with contiguous doc-id ranges per rank,
 so the id-ordered scan of the single reference index is the concatenation of
-the rank scans in rank order.  Exactness (DESIGN.md "multi-GPU"):
+the rank scans in rank order.  Exactness:
 
-1. every rank runs the fused kernel pipeline on its range (mode 1) and emits
-   its verified top-(k+1) by exact distance, or a flag;
-2. all ranks all-gather those lists over RCCL (tiny: B*(k+1)*16 bytes/rank)
-   and merge them on-device (wv_merge_shards);
+1. every rank computes its block keys and its k+1 smallest block-key values
+   (phase 1); one all-gather of those (B*(k+2)*4 bytes per rank) gives every
+   rank the global (k+1)-th smallest key, which cuts its candidate blocks to
+   those that can hold a global top-(k+1) row; exact distances of those rows
+   give the rank's verified top-(k+1) or a flag (phase 2).  Backends without
+   the two phases run both at once (mode 1 of wv_index_search_device);
+2. one all-gather of the packed lists (B*(3(k+1)+2)*4 bytes per rank) and an
+   on-device merge (wv_merge_shards);
 3. if no rank flagged a query and the merged k+1 smallest distances are
    distinct, the merged top-k IS the reference heap's result;
 4. otherwise the reference heap is replayed exactly across the ranks in id
-   order: rank r continues the heap state handed over by rank r-1
-   (wv_index_replay), the last rank applies extractHeap.
+   order: rank r continues the heap states handed over by rank r-1 (one packed
+   broadcast per hop, states indexed by query, the flagged list built on the
+   device: no host synchronisation), the last rank applies extractHeap.
 
 The collective layer is torch.distributed (backend "nccl" = RCCL on ROCm,
 "gloo" on CPU for tests); the per-rank kernels sit behind a small backend
@@ -46,6 +51,52 @@ class GpuShardBackend:
         self._check(self._l.wv_index_search_device(self.index._h, q.data_ptr(), nq, d, k, 1, ids.data_ptr(),
                                                    dd.data_ptr(), cnt.data_ptr(), flg.data_ptr(), s))
         return ids, dd, cnt, flg
+
+    two_phase = True
+
+    def phase1(self, q: torch.Tensor, k: int):
+        """Block keys + local candidate selection; -> (topA [nq][k+1], eps [nq]).
+        Raises WeaviateError (WV_ERR_UNSUPPORTED) when the index is not on the
+        block-key path; the caller then uses local_search."""
+        nq, d = q.shape
+        topA = torch.empty((nq, k + 1), dtype=torch.float32, device=self.dev)
+        eps = torch.empty(nq, dtype=torch.float32, device=self.dev)
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        self._check(self._l.wv_index_shard_phase1(self.index._h, q.data_ptr(), nq, d, k, topA.data_ptr(),
+                                                  eps.data_ptr(), s))
+        self._nq = nq
+        return topA, eps
+
+    def phase2(self, gA: torch.Tensor, gE: torch.Tensor, k: int):
+        """Global threshold + exact distances; -> the local_search tensors."""
+        W, nq = int(gA.shape[0]), int(gA.shape[1])
+        ids = torch.empty((nq, k + 1), dtype=torch.int64, device=self.dev)
+        dd = torch.empty((nq, k + 1), dtype=torch.float32, device=self.dev)
+        cnt = torch.empty(nq, dtype=torch.int32, device=self.dev)
+        flg = torch.empty(nq, dtype=torch.int32, device=self.dev)
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        self._check(self._l.wv_index_shard_phase2(self.index._h, W, nq, gA.data_ptr(), gE.data_ptr(), k,
+                                                  ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(), flg.data_ptr(), s))
+        return ids, dd, cnt, flg
+
+    def replay_flags(self, q: torch.Tensor, flags: torch.Tensor, state, k: int, extract: bool, out=None):
+        """Continue the reference heap of every flagged query over this shard
+        (wv_index_replay_flags_device: the list is built on the device).  state
+        and result rows are indexed by query: (ids [nq, k], dists [nq, k],
+        len [nq]) in heap layout order, or None for empty heaps; `out` receives
+        the result (rows of unflagged queries are left untouched)."""
+        nq = q.shape[0]
+        if out is None:
+            out = (torch.empty((nq, k), dtype=torch.int64, device=self.dev),
+                   torch.empty((nq, k), dtype=torch.float32, device=self.dev),
+                   torch.empty(nq, dtype=torch.int32, device=self.dev))
+        si, sd, sl = (None, None, None) if state is None else (state[0].data_ptr(), state[1].data_ptr(),
+                                                               state[2].data_ptr())
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        self._check(self._l.wv_index_replay_flags_device(self.index._h, q.data_ptr(), nq, q.shape[1], k,
+                                                         flags.data_ptr(), si, sd, sl, 1 if extract else 0,
+                                                         out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), s))
+        return out
 
     def merge(self, G: int, k: int, ids, dd, cnt, flg):
         nq = cnt.shape[-1]
@@ -182,17 +233,68 @@ class ShardedFlatSearch:
         dist.all_gather(parts, t)
         return torch.stack(parts)
 
+    def _local(self, q: torch.Tensor, k: int):
+        """Phases 1-2 (or the one-shot local search) -> the rank's lists."""
+        if getattr(self.b, "two_phase", False):
+            try:
+                topA, eps = self.b.phase1(q, k)
+            except Exception as e:  # not on the block-key path: one-shot local search
+                from ._lib import WeaviateError, WV_ERR_UNSUPPORTED
+                if not (isinstance(e, WeaviateError) and e.code == WV_ERR_UNSUPPORTED):
+                    raise
+            else:
+                g = self._all_gather(torch.cat([topA, eps[:, None]], 1))  # [W, nq, k+2]
+                return self.b.phase2(g[..., : k + 1].contiguous(), g[..., k + 1].contiguous(), k)
+        return self.b.local_search(q, k)
+
     def search(self, q: torch.Tensor, k: int):
-        ids, dd, cnt, flg = self.b.local_search(q, k)
-        gi = self._all_gather(ids)
-        gd = self._all_gather(dd)
-        gc = self._all_gather(cnt)
-        gf = self._all_gather(flg)
+        ids, dd, cnt, flg = self._local(q, k)
+        nq = cnt.shape[0]
+        # one all-gather of the packed lists: ids (as 2 int32), dists, count, flag
+        packed = torch.cat([ids.contiguous().view(torch.int32).reshape(nq, 2 * (k + 1)),
+                            dd.contiguous().view(torch.int32), cnt[:, None], flg[:, None]], 1)
+        G = self._all_gather(packed)
+        k1 = k + 1
+        gi = G[..., : 2 * k1].contiguous().view(torch.int64)
+        gd = G[..., 2 * k1: 3 * k1].contiguous().view(torch.float32)
+        gc = G[..., 3 * k1].contiguous()
+        gf = G[..., 3 * k1 + 1].contiguous()
         oi, od, on, of = self.b.merge(self.world, k, gi, gd, gc, gf)
-        flagged = torch.nonzero(of).flatten().to(torch.int32)  # (the one host sync: the list length)
+        if hasattr(self.b, "replay_flags"):
+            return self._replay_chain_flags(q, k, of, oi, od, on)
+        flagged = torch.nonzero(of).flatten().to(torch.int32)  # (host sync: the list length)
         if flagged.numel():
             oi, od, on = self._replay_chain(q, k, flagged, oi, od, on)
         return oi, od, on
+
+    @staticmethod
+    def _pack_state(ti, td, tn):
+        nq, k = ti.shape
+        return torch.cat([ti.contiguous().view(torch.int32).reshape(nq, 2 * k), td.contiguous().view(torch.int32),
+                          tn[:, None]], 1)
+
+    @staticmethod
+    def _unpack_state(p, k):
+        return (p[:, : 2 * k].contiguous().view(torch.int64), p[:, 2 * k: 3 * k].contiguous().view(torch.float32),
+                p[:, 3 * k].contiguous())
+
+    def _replay_chain_flags(self, q, k, of, oi, od, on):
+        """Exact heap replay of the flagged queries across the ranks in id order
+        (rank 0 first), states indexed by query, one packed broadcast per hop;
+        the last rank extracts into the merged results."""
+        nq = of.shape[0]
+        state = None
+        for r in range(self.world):
+            last = r == self.world - 1
+            if self.rank == r:
+                res = self.b.replay_flags(q, of, state, k, last, out=(oi, od, on) if last else None)
+                buf = self._pack_state(*res)
+            else:
+                buf = torch.empty((nq, 3 * k + 1), dtype=torch.int32, device=self.dev)
+            if self.world > 1:
+                dist.broadcast(buf, src=r)
+            state = self._unpack_state(buf, k)
+        return state
 
     def _replay_chain(self, q, k, qlist, oi, od, on):
         """Exact heap replay across ranks in id order (rank 0 first); heap
