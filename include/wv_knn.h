@@ -299,6 +299,24 @@ int wv_index_shard_phase2(wv_index *idx, int32_t world, int64_t nq, const float 
  * the device, no host synchronisation); states d_in_* and results d_out_*
  * indexed by query ([nq x k], [nq]), rows of unflagged queries untouched.
  * Needs this index's block keys of the same batch. */
+/* Parallel cross-shard replay: every shard r >= 1 replays the
+ * listed queries from a full heap of k copies of T_r (an upper bound of the
+ * real heap top at its first row: the k-th smallest known bound of the shards
+ * before it) and records every insertion in id order (d_rec_* [nlist x cap],
+ * count cap + 1 = overflow); shard 0 replays from empty heaps
+ * (wv_index_replay_device).  wv_heap_merge_records then applies insertToHeap
+ * over the records of shards 1..world-1 (d_rec_* [world][nlist][cap]) on shard
+ * 0's states and extracts: equal to the serial chain; d_unresolved[li] = 1
+ * where a record overflowed (the caller replays those serially). */
+int wv_index_replay_record_device(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k,
+                                  const int32_t *d_qlist, int32_t nlist, const uint64_t *d_in_ids,
+                                  const float *d_in_dists, const int32_t *d_in_len, int32_t cap, uint64_t *d_rec_ids,
+                                  float *d_rec_dists, int32_t *d_rec_n, void *stream);
+int wv_heap_merge_records(int32_t device, int32_t nlist, int32_t k, int32_t world, int32_t cap,
+                          const uint64_t *d_st_ids, const float *d_st_dists, const int32_t *d_st_n,
+                          const uint64_t *d_rec_ids, const float *d_rec_dists, const int32_t *d_rec_n,
+                          uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_n, int32_t *d_unresolved,
+                          void *stream);
 int wv_index_replay_flags_device(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k,
                                  const int32_t *d_flags, const uint64_t *d_in_ids, const float *d_in_dists,
                                  const int32_t *d_in_len, int32_t extract, uint64_t *d_out_ids, float *d_out_dists,

@@ -114,3 +114,68 @@ def test_sharded_two_phase_and_flag_chain(wv, oracle, shards, metric, kind, n, d
         np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), ed.view(np.uint32), err_msg=f"q{i} vs oracle")
     for b in backs:
         b.index.close()
+
+
+@pytest.mark.parametrize("shards,metric,kind,n,d,k", [(3, "l2-squared", 1, 6000, 64, 10),   # integer data: ties
+                                                     (8, "cosine", 0, 16000, 128, 10),
+                                                     (4, "l2-squared", 1, 8000, 24, 50)])
+def test_sharded_parallel_replay_records(wv, oracle, shards, metric, kind, n, d, k):
+    """The parallel cross-shard replay (ShardedFlatSearch._replay_parallel):
+    shard 0 replays from empty heaps, shards r >= 1 from k copies of T_r
+    (weaviate_amd.sharded.prefix_bound) recording their insertions,
+    wv_heap_merge_records applies the records in shard order.  Must equal the
+    oracle; also with a 2-entry record cap (overflow -> serial chain)."""
+    from weaviate_amd.sharded import GpuShardBackend, fake_heaps, prefix_bound
+    dev = torch.device("cuda", 0)
+    data = oracle.gen_matrix(kind, 45, 0, n, d)
+    queries = oracle.gen_matrix(kind, 46, 0, 200, d)
+    per = (n + shards - 1) // shards
+    backs = []
+    for r in range(shards):
+        lo, hi = r * per, min(n, (r + 1) * per)
+        idx = wv.FlatIndex(distance=metric, id_base=lo, variant="avx256")
+        idx.add_batch(np.arange(lo, hi, dtype=np.uint64), data[lo:hi])
+        backs.append(GpuShardBackend(idx, 0))
+    q = torch.from_numpy(queries).to(dev)
+    orc = oracle.OracleFlat(oracle.METRIC[metric], 1, d, n)
+    orc.add_batch(np.arange(n), data)
+    for cap in (256, 2):
+        p1 = [b.phase1(q, k) for b in backs]
+        gA = torch.stack([t for t, _ in p1])
+        gE = torch.stack([e for _, e in p1])
+        parts = [b.phase2(gA, gE, k) for b in backs]
+        gi, gd, gc, gf = (torch.stack([p[j] for p in parts]) for j in range(4))
+        oi, od, on, of = backs[0].merge(shards, k, gi, gd, gc, gf)
+        ql = torch.nonzero(of).flatten()
+        F = int(ql.numel())
+        if kind == 1:
+            assert F > 0
+        ql32 = ql.to(torch.int32)
+        ti, td, tn = backs[0].replay(q, ql32, None, k, False)
+        rec = [(None, None, None)]
+        for r in range(1, shards):
+            T = prefix_bound(r, ql, k, gd, gc, gf, (gA, gE))
+            rec.append(backs[r].replay_record(q, ql32, fake_heaps(T, k), k, cap))
+        ri = torch.zeros((shards, F, cap), dtype=torch.int64, device=dev)
+        rd = torch.zeros((shards, F, cap), dtype=torch.float32, device=dev)
+        rn = torch.zeros((shards, F), dtype=torch.int32, device=dev)
+        for r in range(1, shards):
+            ri[r], rd[r], rn[r] = rec[r]
+        fi, fd, fn, un = backs[0].merge_records(shards, k, cap, (ti.contiguous(), td.contiguous(), tn), (ri, rd, rn))
+        oi[ql], od[ql], on[ql] = fi, fd, fn
+        bad = ql32[un.bool()]
+        if cap == 2 and F:
+            assert bad.numel() > 0  # tiny records overflow
+        if bad.numel():  # the serial chain for the overflowed ones
+            state = None
+            for r, b in enumerate(backs):
+                state = b.replay(q, bad, state, k, r == shards - 1)
+            oi[bad.long()], od[bad.long()], on[bad.long()] = state
+        ai, ad, an = oi.cpu().numpy(), od.cpu().numpy(), on.cpu().numpy()
+        for i in range(len(queries)):
+            rc, ei, ed = orc.search(queries[i], k)
+            assert rc == 0 and an[i] == len(ei), f"cap{cap} q{i}"
+            np.testing.assert_array_equal(ai[i, :an[i]].astype(np.uint64), ei, err_msg=f"cap{cap} q{i}")
+            np.testing.assert_array_equal(ad[i, :an[i]].view(np.uint32), ed.view(np.uint32), err_msg=f"cap{cap} q{i}")
+    for b in backs:
+        b.index.close()

@@ -114,6 +114,67 @@ class OracleShardBackend:
             oi[rows], od[rows], on[rows] = ti, td, tn
         return oi, od, on
 
+    # -- parallel replay: recorded insertions + merge (oracle heap restatement) --
+    def _heap(self, k):
+        o = self.o
+        lib = o.lib()
+        lib.or_insert_to_heap.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_float]
+        lib.or_heap_pop.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_float)]
+
+        class H(C.Structure):
+            _fields_ = [("id", C.POINTER(C.c_uint64)), ("dist", C.POINTER(C.c_float)), ("len", C.c_int)]
+        hid = np.zeros(k + 2, np.uint64)
+        hd = np.zeros(k + 2, np.float32)
+        return lib, H(hid.ctypes.data_as(C.POINTER(C.c_uint64)), hd.ctypes.data_as(C.POINTER(C.c_float)), 0), hid, hd
+
+    def replay_record(self, q, qlist, state, k, cap):
+        qn = q.numpy()
+        ql = qlist.numpy()
+        si, sd, sn = (t.numpy() for t in state)
+        nl = len(ql)
+        ri = np.zeros((nl, cap), np.int64)
+        rd = np.zeros((nl, cap), np.float32)
+        rn = np.zeros(nl, np.int32)
+        for li, qi in enumerate(ql):
+            lib, h, hid, hd = self._heap(k)
+            h.len = int(sn[li])
+            hid[:h.len] = si[li, :h.len].view(np.uint64)
+            hd[:h.len] = sd[li, :h.len]
+            dist_ = self._dists(self._qnorm(qn[qi]))
+            n = 0
+            for j, e in enumerate(dist_):
+                if h.len < k or hd[0] > e:
+                    lib.or_insert_to_heap(C.byref(h), k, self.begin + j, float(e))
+                    if n < cap:
+                        ri[li, n], rd[li, n] = self.begin + j, e
+                    n += 1
+            rn[li] = cap + 1 if n > cap else n
+        return torch.from_numpy(ri), torch.from_numpy(rd), torch.from_numpy(rn)
+
+    def merge_records(self, world, k, cap, st, rec):
+        si, sd, sn = (t.numpy() for t in st)
+        rids, rds, rns = (t.numpy() for t in rec)
+        nl = len(sn)
+        oi = np.zeros((nl, k), np.int64)
+        od = np.zeros((nl, k), np.float32)
+        on = np.zeros(nl, np.int32)
+        un = np.zeros(nl, np.int32)
+        for li in range(nl):
+            lib, h, hid, hd = self._heap(k)
+            h.len = int(sn[li])
+            hid[:h.len] = si[li, :h.len].view(np.uint64)
+            hd[:h.len] = sd[li, :h.len]
+            for r in range(1, world):
+                m = int(rns[r, li])
+                if m > cap:
+                    un[li] = 1
+                    continue
+                for j in range(m):
+                    lib.or_insert_to_heap(C.byref(h), k, int(rids[r, li, j]), float(rds[r, li, j]))
+            n = lib.or_extract_heap(C.byref(h), oi[li].view(np.uint64).ctypes.data_as(self.o.pu), self.o.f(od[li]))
+            on[li] = n
+        return torch.from_numpy(oi), torch.from_numpy(od), torch.from_numpy(on), torch.from_numpy(un)
+
     def merge(self, G, k, ids, dd, cnt, flg):
         """numpy restatement of k_merge_shards (runtime: kernels.hip)."""
         ids, dd, cnt, flg = ids.numpy(), dd.numpy(), cnt.numpy(), flg.numpy()
@@ -175,7 +236,7 @@ class OracleShardBackend:
         return torch.from_numpy(oi.view(np.int64)), torch.from_numpy(od), torch.from_numpy(on)
 
 
-def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath, two_phase=True):
+def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath, two_phase=True, replay="parallel"):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -190,6 +251,10 @@ def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath, two_phas
     b = OracleShardBackend(orc, metric, corpus, rank * per, min(n, (rank + 1) * per))
     if not two_phase:
         b.two_phase = False
+    if replay != "parallel":  # the chain on device flags, or the list chain
+        b.replay_record = None
+    if replay == "list":
+        b.replay_flags = None
     s = ShardedFlatSearch(b, torch.device("cpu"))
     oi, od, on = s.search(torch.from_numpy(queries), k)
     if rank == 0:
@@ -197,12 +262,14 @@ def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath, two_phas
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("two_phase", [True, False])
+@pytest.mark.parametrize("two_phase,replay,world", [(True, "parallel", 2), (True, "parallel", 3), (False, "parallel", 2),
+                                                   (True, "flags", 2), (False, "list", 2)])
 @pytest.mark.parametrize("metric,kind,dup", [(0, 0, False), (0, 1, True), (2, 0, True), (1, 1, False)])
-def test_sharded_protocol_matches_single_index(tmp_path, oracle, metric, kind, dup, two_phase):
-    n, d, nq, k, world = 400, 8, 12, 10, 2
+def test_sharded_protocol_matches_single_index(tmp_path, oracle, metric, kind, dup, two_phase, replay, world):
+    n, d, nq, k = 400, 8, 12, 10
     out = str(tmp_path / "res.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), metric, kind, n, d, nq, k, dup, out, two_phase), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), metric, kind, n, d, nq, k, dup, out, two_phase, replay),
+                       nprocs=world,
                        join=True, start_method="spawn")
     r = np.load(out)
     corpus = oracle.gen_matrix(kind, 3, 0, n, d)

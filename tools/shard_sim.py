@@ -1,9 +1,10 @@
 """Per-rank cost of the sharded exact search at W ranks, measured on ONE GPU:
 the C3 corpus (10M x 768 cosine) split into W contiguous id-range shards held
 as W indexes on the same device; every stage of ShardedFlatSearch is timed per
-shard with HIP events (phase 1, phase 2, merge, each replay hop), the
-collectives are not (one GPU).  Predicted step at W ranks = max_r(phase1) +
-gather + max_r(phase2) + gather + merge + sum_r(replay hop) + W broadcasts.
+shard with HIP events (phase 1, phase 2, merge, each shard's part of the
+parallel replay, the record merge), the collectives are not (one GPU).
+Predicted step at W ranks = max_r(phase1) + gather + max_r(phase2) + gather +
+merge + max_r(replay part) + gather + record merge.
 Also checks the merged results against the single-GPU search of the same
 batch (bit-exact ids and distances).  Prints one JSON line."""
 import argparse
@@ -28,7 +29,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import weaviate_amd as wv  # noqa: E402
 from weaviate_amd import _lib  # noqa: E402
-from weaviate_amd.sharded import GpuShardBackend, ShardedFlatSearch  # noqa: E402
+from weaviate_amd.sharded import GpuShardBackend, ShardedFlatSearch, fake_heaps, prefix_bound  # noqa: E402
 
 lib = _lib.load()
 dev = torch.device("cuda", 0)
@@ -85,16 +86,35 @@ for rep in range(args.reps + 1):
     gc = G[..., 3 * k1].contiguous()
     gf = G[..., 3 * k1 + 1].contiguous()
     (oi, od, on, of), tm = timed(lambda: backs[0].merge(W, k, gi, gd, gc, gf))
-    state, th = None, []
-    for r, b in enumerate(backs):
-        last = r == W - 1
-        res, ms = timed(lambda b=b, st=state, last=last: b.replay_flags(q, of, st, k, last,
-                                                                         out=(oi, od, on) if last else None))
-        state = ShardedFlatSearch._unpack_state(ShardedFlatSearch._pack_state(*res), k)
-        th.append(ms)
-    nflag = int(of.count_nonzero())
+    # parallel replay: shard 0 from empty heaps, shards >= 1 recording from T_r
+    ql = torch.nonzero(of).flatten()
+    F = int(ql.numel())
+    ql32 = ql.to(torch.int32)
+    cap = 256
+    trec = []
+    if F:
+        (ti, td, tn), t0 = timed(lambda: backs[0].replay(q, ql32, None, k, False))
+        trec.append(t0)
+        ri = torch.zeros((W, F, cap), dtype=torch.int64, device=dev)
+        rd = torch.zeros((W, F, cap), dtype=torch.float32, device=dev)
+        rn = torch.zeros((W, F), dtype=torch.int32, device=dev)
+        for r in range(1, W):
+            T = prefix_bound(r, ql, k, gd, gc, gf, (gA, gE))
+            out, ms = timed(lambda b=backs[r], T=T: b.replay_record(q, ql32, fake_heaps(T, k), k, cap))
+            ri[r], rd[r], rn[r] = out
+            trec.append(ms)
+        (fi_, fd_, fn_, un), tmr = timed(lambda: backs[0].merge_records(W, k, cap, (ti.contiguous(), td.contiguous(), tn),
+                                                                        (ri, rd, rn)))
+        assert not bool(un.any())
+        oi[ql], od[ql], on[ql] = fi_, fd_, fn_
+        nrec = [int(x) for x in rn.max(1).values.tolist()]
+    else:
+        tmr, nrec = 0.0, []
+    state = (oi, od, on)
+    th = trec
+    nflag = F
     if rep:
-        rows.append(dict(phase1=t1, phase2=t2, merge=tm, replay=th, flagged=nflag))
+        rows.append(dict(phase1=t1, phase2=t2, merge=tm, replay=th, merge_rec=tmr, flagged=nflag, max_records=nrec))
     fi, fd, fn = state
 
 # single-GPU reference of the same batch (the bench path)
@@ -124,8 +144,10 @@ def avg(key, red):
 
 
 pred = dict(phase1_max=avg("phase1", max), phase2_max=avg("phase2", max), merge=avg("merge", float),
-            replay_sum=avg("replay", sum), replay_hops=[float(x) for x in np.mean([r["replay"] for r in rows], 0)])
-pred["compute_ms"] = pred["phase1_max"] + pred["phase2_max"] + pred["merge"] + pred["replay_sum"]
+            replay_max=avg("replay", lambda v: max(v) if v else 0.0), merge_rec=avg("merge_rec", float),
+            replay_per_shard=rows[-1]["replay"],
+            max_records=rows[-1]["max_records"])
+pred["compute_ms"] = pred["phase1_max"] + pred["phase2_max"] + pred["merge"] + pred["replay_max"] + pred["merge_rec"]
 print(json.dumps(dict(world=W, n=n, d=d, batch=B, k=k, flagged=rows[-1]["flagged"], equal_to_single=same,
                       phase1=[float(x) for x in np.mean([r["phase1"] for r in rows], 0)],
                       phase2=[float(x) for x in np.mean([r["phase2"] for r in rows], 0)], **pred)), flush=True)

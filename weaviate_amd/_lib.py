@@ -101,6 +101,8 @@ SIGNATURES = {
     "wv_index_shard_phase1": (C.c_int, [P, P, i64, i64, i32, P, P, P]),
     "wv_index_shard_phase2": (C.c_int, [P, i32, i64, P, P, i32, P, P, P, P, P]),
     "wv_index_replay_flags_device": (C.c_int, [P, P, i64, i64, i32, P, P, P, P, i32, P, P, P, P]),
+    "wv_index_replay_record_device": (C.c_int, [P, P, i64, i64, i32, P, i32, P, P, P, i32, P, P, P, P]),
+    "wv_heap_merge_records": (C.c_int, [i32, i32, i32, i32, i32, P, P, P, P, P, P, P, P, P, P, P]),
     "wv_index_replay": (C.c_int, [P, P, i64, i64, i32, pi32, i32, pu64, pf32, pi32, i32, pu64, pf32, pi32]),
     "wv_merge_shards": (C.c_int, [i32, i32, i64, i32, P, P, P, P, P, P, P, P, P]),
     "wv_distance_batch": (C.c_int, [i32, i32, i32, pf32, pf32, i64, i64, pf32]),

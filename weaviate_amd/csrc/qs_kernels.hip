@@ -1523,7 +1523,9 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
                                                 const int32_t* __restrict__ in_len, int extract, int by_list,
                                                 const uint32_t* __restrict__ pool_blk, const float* __restrict__ pool_lb,
                                                 const float* __restrict__ pool_E, const uint32_t* __restrict__ pool_vm,
-                                                const int32_t* __restrict__ rp_off, const int32_t* __restrict__ rp_tot) {
+                                                const int32_t* __restrict__ rp_off, const int32_t* __restrict__ rp_tot,
+                                                uint64_t* __restrict__ rec_ids, float* __restrict__ rec_d,
+                                                int32_t* __restrict__ rec_n, int rec_cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
     float* hd = reinterpret_cast<float*>(hid + k);
@@ -1537,6 +1539,18 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
     for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
         const int q = qlist[li_];
         const float* qv = Qn + (int64_t)q * dpad;
+        const int64_t orow = by_list ? li_ : q;
+        int nrec = 0;  // recorded insertions (lane 0): the parallel cross-shard replay
+        // insertToHeap (flat/index.go:665-674) by lane 0, recording what entered
+        auto ins = [&](ReplayHeap& h, uint64_t idj, float dj) {
+            bool did = false;
+            if (h.len < k) { rh_insert(h, idj, dj); did = true; }
+            else if (h.dist[0] > dj) { uint64_t x; float y; rh_pop(h, &x, &y); rh_insert(h, idj, dj); did = true; }
+            if (did && rec_ids) {
+                if (nrec < rec_cap) { rec_ids[orow * rec_cap + nrec] = idj; rec_d[orow * rec_cap + nrec] = dj; }
+                nrec++;
+            }
+        };
         int len_in = in_len ? in_len[by_list ? li_ : q] : 0;
         len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
         for (int i = lane; i < len_in; i += 64) {
@@ -1578,8 +1592,7 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
                             mask &= mask - 1;
                             const float dj = sE[j * 32 + l];
                             const uint64_t idj = id_base + (uint64_t)bj * 32 + (uint64_t)l;
-                            if (h.len < k) rh_insert(h, idj, dj);
-                            else if (h.dist[0] > dj) { uint64_t x; float y; rh_pop(h, &x, &y); rh_insert(h, idj, dj); }
+                            ins(h, idj, dj);
                         }
                         *s_len = h.len;
                     }
@@ -1633,8 +1646,7 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
                             const int jb = l >= 32 ? j2 : j1;
                             const uint64_t idj = id_base + (uint64_t)((b0 + jb) * 32 + (l & 31));
                             const float dj = s_d[l];
-                            if (h.len < k) rh_insert(h, idj, dj);
-                            else if (h.dist[0] > dj) { uint64_t x; float y; rh_pop(h, &x, &y); rh_insert(h, idj, dj); }
+                            ins(h, idj, dj);
                         }
                         *s_len = h.len;
                     }
@@ -1642,7 +1654,7 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
                 }
             }
         }
-        const int64_t orow = by_list ? li_ : q;
+        if (rec_ids && lane == 0) rec_n[orow] = nrec > rec_cap ? rec_cap + 1 : nrec;
         if (!extract) {  // hand the heap on in layout order (kout == k)
             const int n = *s_len;
             for (int i = lane; i < n; i += 64) {
@@ -1662,6 +1674,54 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
         }
         wave_sync_lds();
     }
+}
+
+// Parallel cross-shard replay, final step (weaviate_amd/sharded.py): one wave
+// per listed query.  Start from shard 0's heap state (layout order), then apply
+// insertToHeap over every later shard's recorded insertions in shard (= id)
+// order, then extractHeap.  A shard's record holds every row that entered its
+// replay from a full heap of k copies of T_r (>= the real heap top at that
+// shard's start), a superset of the rows that enter the real heap there, so
+// this equals the serial chain.  rec_n > cap: overflowed -> unresolved[li] = 1.
+__global__ __launch_bounds__(64) void k_heap_merge_records(int nlist, int k, int W, int cap,
+                                                           const uint64_t* __restrict__ st_ids,
+                                                           const float* __restrict__ st_d,
+                                                           const int32_t* __restrict__ st_n,
+                                                           const uint64_t* __restrict__ rec_ids,
+                                                           const float* __restrict__ rec_d,
+                                                           const int32_t* __restrict__ rec_n,
+                                                           uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
+                                                           int32_t* __restrict__ out_n, int32_t* __restrict__ unresolved) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char msm[];
+    uint64_t* hid = reinterpret_cast<uint64_t*>(msm);
+    float* hd = reinterpret_cast<float*>(hid + k);
+    const int li = blockIdx.x;
+    if (li >= nlist || threadIdx.x != 0) return;
+    int n0 = st_n[li];
+    n0 = n0 < 0 ? 0 : n0 > k ? k : n0;
+    for (int i = 0; i < n0; i++) { hid[i] = st_ids[(int64_t)li * k + i]; hd[i] = st_d[(int64_t)li * k + i]; }
+    ReplayHeap h{hid, hd, n0};
+    int bad = 0;
+    for (int r = 1; r < W; r++) {
+        const int64_t base = (int64_t)r * nlist + li;
+        const int m = rec_n[base];
+        if (m > cap) { bad = 1; continue; }
+        for (int j = 0; j < m; j++) {
+            const float dj = rec_d[base * cap + j];
+            const uint64_t idj = rec_ids[base * cap + j];
+            if (h.len < k) rh_insert(h, idj, dj);
+            else if (h.dist[0] > dj) { uint64_t x; float y; rh_pop(h, &x, &y); rh_insert(h, idj, dj); }
+        }
+    }
+    unresolved[li] = bad;
+    const int n = h.len;
+    for (int i = n - 1; i >= 0; i--) {
+        uint64_t x; float y;
+        rh_pop(h, &x, &y);
+        out_ids[(int64_t)li * k + i] = x;
+        out_d[(int64_t)li * k + i] = y;
+    }
+    out_n[li] = n;
 }
 
 }  // namespace wv

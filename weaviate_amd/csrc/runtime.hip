@@ -2214,7 +2214,8 @@ static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int
                              const float4* qinfo, const uint32_t* valid, const float* Qn, const int32_t* list,
                              const uint32_t* counters, int nlist, int64_t max_list, int k, int kout, uint64_t* oi,
                              float* od, int32_t* on, const uint64_t* in_i, const float* in_d, const int32_t* in_n,
-                             int extract, int by_list) {
+                             int extract, int by_list, uint64_t* rec_i = nullptr, float* rec_d = nullptr,
+                             int32_t* rec_n = nullptr, int rec_cap = 0) {
     const int metric = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
     const int64_t nch = (nb + RP_CH - 1) / RP_CH;
@@ -2261,7 +2262,7 @@ static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int
 #define WV_RPH(M, V)                                                                                            \
     do {                                                                                                        \
         if (hlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_rp_heap<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hlds)); \
-        k_rp_heap<M, V><<<(unsigned)g3, 64, hlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpE.as<float>(), idx->rpVm.as<uint32_t>(), idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>()); \
+        k_rp_heap<M, V><<<(unsigned)g3, 64, hlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpE.as<float>(), idx->rpVm.as<uint32_t>(), idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>(), rec_i, rec_d, rec_n, rec_cap); \
     } while (0)
         switch (metric) {
         case L2: if (v5) WV_RPH(L2, AVX512); else WV_RPH(L2, AVX256); break;
@@ -2272,6 +2273,7 @@ static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int
         HIPCHK(hipGetLastError());
         return WV_OK;
     }
+    if (rec_i) return set_err(WV_ERR_UNSUPPORTED, "recorded replay needs the pooled block-key replay (k < 64)");
     if (k < 64 && nch <= RP_MAXCH && idx->replay_par) {
         const int64_t grid = std::min<int64_t>(max_list, 256);
         HIPCHK(idx->qsScratch.ensure((size_t)grid * nch * 64 * sizeof(float)));
@@ -3028,6 +3030,61 @@ extern "C" int wv_index_replay_flags_device(wv_index* idx, const float* d_querie
                                idx->flCtr.as<uint32_t>(), 0, nq, k, k, d_out_ids, d_out_dists, d_out_len, d_in_ids,
                                d_in_dists, d_in_len, extract, 0);
     if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// parallel cross-shard replay (weaviate_amd/sharded.py): this shard's replay of
+// the listed queries from heap states d_in_* (by list position), recording every
+// insertion (ids, dists [nlist][cap], counts [nlist], cap + 1 = overflow)
+extern "C" int wv_index_replay_record_device(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                             const int32_t* d_qlist, int32_t nlist, const uint64_t* d_in_ids,
+                                             const float* d_in_dists, const int32_t* d_in_len, int32_t cap,
+                                             uint64_t* d_rec_ids, float* d_rec_dists, int32_t* d_rec_n, void* stream) {
+    (void)d_queries;
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0 || nlist < 0 || cap < 1 || !d_rec_ids || !d_rec_dists || !d_rec_n)
+        return set_err(WV_ERR_INVALID, "invalid arguments");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (nlist == 0) return WV_OK;
+    const bool have_data = idx->dims != 0 && idx->npresent > 0;
+    if (!have_data) {
+        HIPCHK(hipMemsetAsync(d_rec_n, 0, (size_t)nlist * sizeof(int32_t), s));
+        return WV_OK;
+    }
+    if (d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    if (idx->qs_keys_nq != nq) return set_err(WV_ERR_UNSUPPORTED, "replay_record: no block keys of this batch");
+    HIPCHK(idx->hI.ensure((size_t)nlist * k * sizeof(uint64_t)));
+    HIPCHK(idx->hD.ensure((size_t)nlist * k * sizeof(float)));
+    HIPCHK(idx->hN.ensure((size_t)nlist * sizeof(int32_t)));
+    int rc = launch_blk_replay(idx, s, idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb, idx->qsEps.as<float>(),
+                               idx->qsInfo.as<float4>(), idx->present, idx->qn.as<float>(), d_qlist, nullptr, nlist,
+                               nlist, k, k, idx->hI.as<uint64_t>(), idx->hD.as<float>(), idx->hN.as<int32_t>(), d_in_ids,
+                               d_in_dists, d_in_len, 0, 1, d_rec_ids, d_rec_dists, d_rec_n, cap);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_heap_merge_records(int32_t device, int32_t nlist, int32_t k, int32_t world, int32_t cap,
+                                     const uint64_t* d_st_ids, const float* d_st_dists, const int32_t* d_st_n,
+                                     const uint64_t* d_rec_ids, const float* d_rec_dists, const int32_t* d_rec_n,
+                                     uint64_t* d_out_ids, float* d_out_dists, int32_t* d_out_n,
+                                     int32_t* d_unresolved, void* stream) {
+    if (k <= 0 || nlist < 0 || world < 1 || cap < 1) return set_err(WV_ERR_INVALID, "invalid arguments");
+    if (nlist == 0) return WV_OK;
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s = (hipStream_t)stream;
+    const size_t lds = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
+    if (lds > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_heap_merge_records, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_heap_merge_records<<<(unsigned)nlist, 64, lds, s>>>(nlist, k, world, cap, d_st_ids, d_st_dists, d_st_n, d_rec_ids,
+                                                          d_rec_dists, d_rec_n, d_out_ids, d_out_dists, d_out_n,
+                                                          d_unresolved);
+    HIPCHK(hipGetLastError());
     if (!stream) HIPCHK(hipStreamSynchronize(s));
     return WV_OK;
 }

@@ -351,6 +351,17 @@ class FlatIndex:
         self._cfg_args = new
         self.rescore_limit = int(new["rescore_limit"])
 
+    # upgradableIndexer of the flat index itself (flat/index.go:1251-1261)
+    def should_upgrade(self) -> tuple:
+        return False, 0
+
+    def upgrade(self, callback=None) -> None:
+        if callback is not None:
+            callback()
+
+    def upgraded(self) -> bool:
+        return False
+
     def compression_stats(self) -> dict:  # flat/index.go:1246-1249
         buf = C.create_string_buffer(32)
         ratio = C.c_double(0)

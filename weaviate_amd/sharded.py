@@ -30,6 +30,34 @@ import torch
 import torch.distributed as dist
 
 
+def prefix_bound(r: int, ql: torch.Tensor, k: int, gd, gc, gf, bounds=None) -> torch.Tensor:
+    """T_r [F] for the listed queries ql: the k-th smallest of upper bounds of
+    distinct rows of the shards before r -- exact distances from their
+    unflagged lists (gd [W, nq, k+1], counts gc, flags gf), and the block-key
+    bounds A + eps of their phase-1 keys (bounds = (gA [W, nq, k+1], gE [W, nq]));
+    +inf when fewer than k are known.  The real heap top at shard r's first
+    row is at most T_r (the heap holds the k smallest distances seen)."""
+    F = int(ql.numel())
+    k1 = gd.shape[-1]
+    ex = gd[:r][:, ql, :]
+    ok = (torch.arange(k1, device=gd.device)[None, None, :] < gc[:r][:, ql, None]) & (gf[:r][:, ql, None] == 0)
+    vals = [torch.where(ok, ex, torch.full_like(ex, float("inf"))).permute(1, 0, 2).reshape(F, -1)]
+    if bounds is not None:
+        gA, gE = bounds
+        vals.append((gA[:r][:, ql, :] + gE[:r][:, ql, None]).permute(1, 0, 2).reshape(F, -1))
+    allv = torch.cat(vals, 1)
+    if allv.shape[1] < k:
+        return torch.full((F,), float("inf"), dtype=torch.float32, device=gd.device)
+    return torch.kthvalue(allv, k, dim=1).values.contiguous()
+
+
+def fake_heaps(T: torch.Tensor, k: int):
+    """Full heaps of k copies of T (ids -1), empty where T is infinite."""
+    F = int(T.numel())
+    return (torch.full((F, k), -1, dtype=torch.int64, device=T.device), T[:, None].expand(F, k).contiguous(),
+            torch.where(torch.isfinite(T), k, 0).to(torch.int32))
+
+
 class GpuShardBackend:
     """Rank-local engine: a FlatIndex holding ids [id_base, id_base + n)."""
 
@@ -97,6 +125,36 @@ class GpuShardBackend:
                                                          flags.data_ptr(), si, sd, sl, 1 if extract else 0,
                                                          out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), s))
         return out
+
+    def replay_record(self, q: torch.Tensor, qlist: torch.Tensor, state, k: int, cap: int):
+        """This shard's replay of the listed queries from `state` (by list
+        position), recording every insertion: (ids [nl, cap], dists, n [nl]),
+        n = cap + 1 when the record overflowed."""
+        nl = int(qlist.numel())
+        ri = torch.empty((nl, cap), dtype=torch.int64, device=self.dev)
+        rd = torch.empty((nl, cap), dtype=torch.float32, device=self.dev)
+        rn = torch.empty(nl, dtype=torch.int32, device=self.dev)
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        self._check(self._l.wv_index_replay_record_device(self.index._h, q.data_ptr(), q.shape[0], q.shape[1], k,
+                                                          qlist.data_ptr(), nl, state[0].data_ptr(),
+                                                          state[1].data_ptr(), state[2].data_ptr(), cap,
+                                                          ri.data_ptr(), rd.data_ptr(), rn.data_ptr(), s))
+        return ri, rd, rn
+
+    def merge_records(self, world: int, k: int, cap: int, st, rec):
+        """Shard 0's states + the later shards' records -> extracted results
+        [nl, k] and unresolved [nl] (wv_heap_merge_records)."""
+        nl = int(st[2].numel())
+        oi = torch.empty((nl, k), dtype=torch.int64, device=self.dev)
+        od = torch.empty((nl, k), dtype=torch.float32, device=self.dev)
+        on = torch.empty(nl, dtype=torch.int32, device=self.dev)
+        un = torch.empty(nl, dtype=torch.int32, device=self.dev)
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        self._check(self._l.wv_heap_merge_records(self.device, nl, k, world, cap, st[0].data_ptr(), st[1].data_ptr(),
+                                                  st[2].data_ptr(), rec[0].data_ptr(), rec[1].data_ptr(),
+                                                  rec[2].data_ptr(), oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+                                                  un.data_ptr(), s))
+        return oi, od, on, un
 
     def merge(self, G: int, k: int, ids, dd, cnt, flg):
         nq = cnt.shape[-1]
@@ -244,10 +302,13 @@ class ShardedFlatSearch:
                     raise
             else:
                 g = self._all_gather(torch.cat([topA, eps[:, None]], 1))  # [W, nq, k+2]
-                return self.b.phase2(g[..., : k + 1].contiguous(), g[..., k + 1].contiguous(), k)
+                gA, gE = g[..., : k + 1].contiguous(), g[..., k + 1].contiguous()
+                self._bounds = (gA, gE)
+                return self.b.phase2(gA, gE, k)
         return self.b.local_search(q, k)
 
     def search(self, q: torch.Tensor, k: int):
+        self._bounds = None
         ids, dd, cnt, flg = self._local(q, k)
         nq = cnt.shape[0]
         # one all-gather of the packed lists: ids (as 2 int32), dists, count, flag
@@ -260,11 +321,46 @@ class ShardedFlatSearch:
         gc = G[..., 3 * k1].contiguous()
         gf = G[..., 3 * k1 + 1].contiguous()
         oi, od, on, of = self.b.merge(self.world, k, gi, gd, gc, gf)
-        if hasattr(self.b, "replay_flags"):
+        if getattr(self.b, "replay_record", None) is not None and k < 64:
+            return self._replay_parallel(q, k, of, oi, od, on, gd, gc, gf)
+        if getattr(self.b, "replay_flags", None) is not None:
             return self._replay_chain_flags(q, k, of, oi, od, on)
         flagged = torch.nonzero(of).flatten().to(torch.int32)  # (host sync: the list length)
         if flagged.numel():
             oi, od, on = self._replay_chain(q, k, flagged, oi, od, on)
+        return oi, od, on
+
+    def _replay_parallel(self, q, k, of, oi, od, on, gd, gc, gf):
+        """The cross-shard replay in one parallel hop: shard 0 replays its
+        range from empty heaps, every shard r >= 1 from k copies of T_r while
+        recording its insertions; one all-gather; wv_heap_merge_records applies
+        the records in shard order.  Overflowed records fall
+        back to the serial chain."""
+        ql = torch.nonzero(of).flatten()  # (host sync: the list length; ascending on every rank)
+        F = int(ql.numel())
+        if F == 0:
+            return oi, od, on
+        ql32 = ql.to(torch.int32)
+        cap = max(256, 16 * k)
+        if self.rank == 0:
+            ti, td, tn = self.b.replay(q, ql32, None, k, False)
+            ri = torch.zeros((F, cap), dtype=torch.int64, device=self.dev)
+            rd = torch.zeros((F, cap), dtype=torch.float32, device=self.dev)
+            ri[:, :k], rd[:, :k] = ti, td
+            rn = tn
+        else:
+            T = prefix_bound(self.rank, ql, k, gd, gc, gf, self._bounds)
+            ri, rd, rn = self.b.replay_record(q, ql32, fake_heaps(T, k), k, cap)
+        pk = torch.cat([ri.contiguous().view(torch.int32).reshape(F, 2 * cap), rd.contiguous().view(torch.int32),
+                        rn[:, None]], 1)
+        G = self._all_gather(pk)  # [W, F, 3 cap + 1]
+        rec = (G[..., : 2 * cap].contiguous().view(torch.int64), G[..., 2 * cap: 3 * cap].contiguous().view(torch.float32),
+               G[..., 3 * cap].contiguous())
+        st = (rec[0][0, :, :k].contiguous(), rec[1][0, :, :k].contiguous(), rec[2][0].contiguous())
+        fi, fd, fn, un = self.b.merge_records(self.world, k, cap, st, rec)
+        oi[ql], od[ql], on[ql] = fi, fd, fn
+        if bool(un.any()):  # a record overflowed: those queries replay serially
+            oi, od, on = self._replay_chain(q, k, ql32[un.bool()], oi, od, on)
         return oi, od, on
 
     @staticmethod
