@@ -35,20 +35,24 @@ def prefix_bound(r: int, ql: torch.Tensor, k: int, gd, gc, gf, bounds=None) -> t
     distinct rows of the shards before r -- exact distances from their
     unflagged lists (gd [W, nq, k+1], counts gc, flags gf), and the block-key
     bounds A + eps of their phase-1 keys (bounds = (gA [W, nq, k+1], gE [W, nq]));
-    +inf when fewer than k are known.  The real heap top at shard r's first
-    row is at most T_r (the heap holds the k smallest distances seen)."""
+    +inf when fewer than k are known.  Each source gives its own k-th smallest
+    (the two may name the same row); T_r is the smaller.  The real heap top at
+    shard r's first row is at most T_r (the heap holds the k smallest
+    distances seen)."""
     F = int(ql.numel())
     k1 = gd.shape[-1]
+    inf = torch.full((F,), float("inf"), dtype=torch.float32, device=gd.device)
+
+    def kth(v):  # k-th smallest per row; the values of one source belong to distinct rows
+        return torch.kthvalue(v, k, dim=1).values.contiguous() if v.shape[1] >= k else inf
+
     ex = gd[:r][:, ql, :]
     ok = (torch.arange(k1, device=gd.device)[None, None, :] < gc[:r][:, ql, None]) & (gf[:r][:, ql, None] == 0)
-    vals = [torch.where(ok, ex, torch.full_like(ex, float("inf"))).permute(1, 0, 2).reshape(F, -1)]
-    if bounds is not None:
+    T = kth(torch.where(ok, ex, torch.full_like(ex, float("inf"))).permute(1, 0, 2).reshape(F, -1))
+    if bounds is not None:  # a separate order statistic: a listed row may also be a block's bound row
         gA, gE = bounds
-        vals.append((gA[:r][:, ql, :] + gE[:r][:, ql, None]).permute(1, 0, 2).reshape(F, -1))
-    allv = torch.cat(vals, 1)
-    if allv.shape[1] < k:
-        return torch.full((F,), float("inf"), dtype=torch.float32, device=gd.device)
-    return torch.kthvalue(allv, k, dim=1).values.contiguous()
+        T = torch.minimum(T, kth((gA[:r][:, ql, :] + gE[:r][:, ql, None]).permute(1, 0, 2).reshape(F, -1)))
+    return T
 
 
 def fake_heaps(T: torch.Tensor, k: int):
