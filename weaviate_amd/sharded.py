@@ -44,14 +44,14 @@ def prefix_bound(r: int, ql: torch.Tensor, k: int, gd, gc, gf, bounds=None) -> t
     inf = torch.full((F,), float("inf"), dtype=torch.float32, device=gd.device)
 
     def kth(v):  # k-th smallest per row; the values of one source belong to distinct rows
-        return torch.kthvalue(v, k, dim=1).values.contiguous() if v.shape[1] >= k else inf
+        return torch.kthvalue(v, k, dim=1).values.contiguous() if v.shape[1] >= k and F > 0 else inf
 
     ex = gd[:r][:, ql, :]
     ok = (torch.arange(k1, device=gd.device)[None, None, :] < gc[:r][:, ql, None]) & (gf[:r][:, ql, None] == 0)
-    T = kth(torch.where(ok, ex, torch.full_like(ex, float("inf"))).permute(1, 0, 2).reshape(F, -1))
+    T = kth(torch.where(ok, ex, torch.full_like(ex, float("inf"))).permute(1, 0, 2).reshape(F, r * k1))
     if bounds is not None:  # a separate order statistic: a listed row may also be a block's bound row
         gA, gE = bounds
-        T = torch.minimum(T, kth((gA[:r][:, ql, :] + gE[:r][:, ql, None]).permute(1, 0, 2).reshape(F, -1)))
+        T = torch.minimum(T, kth((gA[:r][:, ql, :] + gE[:r][:, ql, None]).permute(1, 0, 2).reshape(F, r * k1)))
     return T
 
 
