@@ -3043,8 +3043,9 @@ extern "C" int wv_index_replay_record_device(wv_index* idx, const float* d_queri
                                              uint64_t* d_rec_ids, float* d_rec_dists, int32_t* d_rec_n, void* stream) {
     (void)d_queries;
     if (!idx) return set_err(WV_ERR_INVALID, "nil index");
-    if (k <= 0 || nlist < 0 || cap < 1 || !d_rec_ids || !d_rec_dists || !d_rec_n)
-        return set_err(WV_ERR_INVALID, "invalid arguments");
+    if (k <= 0 || nlist < 0 || cap < 1) return set_err(WV_ERR_INVALID, "invalid arguments");
+    if (nlist == 0) return WV_OK;
+    if (!d_qlist || !d_rec_ids || !d_rec_dists || !d_rec_n) return set_err(WV_ERR_INVALID, "nil buffer");
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
     hipStream_t s = (hipStream_t)stream;

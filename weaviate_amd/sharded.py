@@ -138,6 +138,8 @@ class GpuShardBackend:
         ri = torch.empty((nl, cap), dtype=torch.int64, device=self.dev)
         rd = torch.empty((nl, cap), dtype=torch.float32, device=self.dev)
         rn = torch.empty(nl, dtype=torch.int32, device=self.dev)
+        if nl == 0:
+            return ri, rd, rn
         s = torch.cuda.current_stream(self.dev).cuda_stream
         self._check(self._l.wv_index_replay_record_device(self.index._h, q.data_ptr(), q.shape[0], q.shape[1], k,
                                                           qlist.data_ptr(), nl, state[0].data_ptr(),
@@ -152,7 +154,9 @@ class GpuShardBackend:
         oi = torch.empty((nl, k), dtype=torch.int64, device=self.dev)
         od = torch.empty((nl, k), dtype=torch.float32, device=self.dev)
         on = torch.empty(nl, dtype=torch.int32, device=self.dev)
-        un = torch.empty(nl, dtype=torch.int32, device=self.dev)
+        un = torch.zeros(nl, dtype=torch.int32, device=self.dev)
+        if nl == 0:
+            return oi, od, on, un
         s = torch.cuda.current_stream(self.dev).cuda_stream
         self._check(self._l.wv_heap_merge_records(self.device, nl, k, world, cap, st[0].data_ptr(), st[1].data_ptr(),
                                                   st[2].data_ptr(), rec[0].data_ptr(), rec[1].data_ptr(),
