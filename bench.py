@@ -433,7 +433,9 @@ def main():
         # bf16 MFMA product per (query, row, dim): algorithmic flops per launch
         # = 2 * B * n_local * d, over its measured average duration (HIP events
         # on the stream it runs on), against the dense bf16 MFMA peak.
-        flops = 2.0 * B * n_local * dims
+        # the timed launch is the first query chunk of the batch (search_qs)
+        f0 = int(index.stats().get("last_group_queries", 0)) or B
+        flops = 2.0 * min(B, f0) * n_local * dims
         achieved = flops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
         peak = MFMA_BF16_PEAK_TFLOPS
         roof = {"bound": "mfma", "kernel": sel_kernel, "achieved": achieved, "peak": peak,

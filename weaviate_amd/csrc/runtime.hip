@@ -2322,9 +2322,10 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     const int64_t nslots = std::max<int64_t>(1, (idx->hiwater + 32 * RB - 1) / (32 * RB));
     const int64_t nb = nslots * RB;  // 32-row blocks scanned = key row length
     const int64_t ldk = nb;
-    // query chunks of 256-multiples whose key rows fit 4 GiB
-    const int64_t qmax = std::max<int64_t>(QS_QPB, ((4ll << 30) / (ldk * 4)) / QS_QPB * QS_QPB);
+    // query chunks of 256-multiples whose key rows fit 16 GiB (10M rows: 13k queries per chunk)
+    const int64_t qmax = std::max<int64_t>(QS_QPB, ((16ll << 30) / (ldk * 4)) / QS_QPB * QS_QPB);
     const int64_t qc = std::min<int64_t>(round_up(nq, QS_QPB), qmax);
+    idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(qc, nq);  // the timed block-key launch
     HIPCHK(idx->qsQb.ensure((size_t)qc * idx->dpb * sizeof(uint16_t)));
     HIPCHK(idx->qsInfo.ensure((size_t)qc * sizeof(float4)));
     HIPCHK(idx->qsKey.ensure((size_t)qc * ldk * sizeof(float)));
