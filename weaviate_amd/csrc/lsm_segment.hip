@@ -209,20 +209,25 @@ extern "C" int wv_lsm_segment_scan(const char* path, int32_t validate_checksum, 
 // out[0] = live vectors uploaded, out[1] = keys hidden by tombstones,
 // out[2] = nodes read.  AlreadyIndexed becomes the bucket's live count
 // (initBuckets: count = CountAsync, flat/index.go:278-279).
-extern "C" int wv_index_load_segments(wv_index* idx, const char* const* paths, int32_t n_paths,
-                                      int32_t validate_checksum, int64_t* out) {
-    using namespace wvlsm;
-    if (!idx || (n_paths > 0 && !paths)) return set_err(WV_ERR_INVALID, "nil argument");
-    std::vector<Mapped> maps((size_t)std::max(n_paths, 0));
-    struct Entry { int32_t seg; uint64_t value_off, value_len; bool tombstone; };
-    std::unordered_map<uint64_t, Entry> latest;
-    int64_t nodes = 0;
+namespace wvlsm {
+
+struct Entry {
+    int32_t seg;
+    uint64_t value_off, value_len;
+    bool tombstone;
+};
+
+// every node of the segments (oldest first): the newest entry of each key wins
+static int collect(const char* const* paths, int32_t n_paths, bool validate, std::vector<Mapped>& maps,
+                   std::unordered_map<uint64_t, Entry>& latest, int64_t& nodes) {
+    maps.resize((size_t)std::max(n_paths, 0));
+    nodes = 0;
     for (int32_t si = 0; si < n_paths; si++) {
         const char* path = paths[si];
         int rc = map_file(path, maps[si]);
         if (rc) return rc;
         Header h;
-        rc = parse_header(path, maps[si], validate_checksum != 0, h);
+        rc = parse_header(path, maps[si], validate, h);
         if (rc) return rc;
         rc = check_replace(h);
         if (rc) return rc;
@@ -239,12 +244,65 @@ extern "C" int wv_index_load_segments(wv_index* idx, const char* const* paths, i
             pos = nd.end;
         }
     }
-    std::vector<uint64_t> live, dead;
+    return WV_OK;
+}
+
+// float32SliceFromByteSlice (flat/index.go:331-336) of live[c0, c1) into buf;
+// every value must hold d float32 (the first live value fixes d)
+static int gather_rows(const char* const* paths, const std::vector<Mapped>& maps,
+                       std::unordered_map<uint64_t, Entry>& latest, const std::vector<uint64_t>& live, size_t c0,
+                       size_t c1, int64_t d, std::vector<float>& buf) {
+    buf.resize((c1 - c0) * (size_t)d);
+    for (size_t j = c0; j < c1; j++) {
+        const Entry& e = latest[live[j]];
+        if ((int64_t)e.value_len != d * 4) {
+            return set_err(WV_ERR_INSERT,
+                           "insert called with a vector of the wrong size: %lld. Saved length: %lld, path: %s",
+                           (long long)(e.value_len / 4), (long long)d, paths[e.seg]);
+        }
+        memcpy(&buf[(j - c0) * d], maps[e.seg].p + e.value_off, (size_t)d * 4);  // LE host
+    }
+    return WV_OK;
+}
+
+// the vector dimension of a restore: the first live value's float32 count
+static int value_dims(std::unordered_map<uint64_t, Entry>& latest, const std::vector<uint64_t>& live, int64_t& d) {
+    d = 0;
+    if (live.empty()) return WV_OK;
+    const Entry& e0 = latest[live[0]];
+    if (e0.value_len % 4)
+        return set_err(WV_ERR_INVALID, "vector value of %llu bytes is not float32-aligned",
+                       (unsigned long long)e0.value_len);
+    d = (int64_t)(e0.value_len / 4);
+    return WV_OK;
+}
+
+static void split_live(std::unordered_map<uint64_t, Entry>& latest, std::vector<uint64_t>& live,
+                       std::vector<uint64_t>& dead) {
     live.reserve(latest.size());
     for (auto& kv : latest) (kv.second.tombstone ? dead : live).push_back(kv.first);
     std::sort(live.begin(), live.end());
     std::sort(dead.begin(), dead.end());
-    int rc = WV_OK;
+}
+
+}  // namespace wvlsm
+
+#ifndef WV_LSM_HOST_ONLY
+// Restore: all segments (oldest first) of flat's vectors bucket into the index.
+// out[0] = live vectors uploaded, out[1] = keys hidden by tombstones,
+// out[2] = nodes read.  AlreadyIndexed becomes the bucket's live count
+// (initBuckets: count = CountAsync, flat/index.go:278-279).
+extern "C" int wv_index_load_segments(wv_index* idx, const char* const* paths, int32_t n_paths,
+                                      int32_t validate_checksum, int64_t* out) {
+    using namespace wvlsm;
+    if (!idx || (n_paths > 0 && !paths)) return set_err(WV_ERR_INVALID, "nil argument");
+    std::vector<Mapped> maps;
+    std::unordered_map<uint64_t, Entry> latest;
+    int64_t nodes = 0;
+    int rc = collect(paths, n_paths, validate_checksum != 0, maps, latest, nodes);
+    if (rc) return rc;
+    std::vector<uint64_t> live, dead;
+    split_live(latest, live, dead);
     if (!dead.empty()) {
         rc = wv_index_delete(idx, dead.data(), (int64_t)dead.size());
         if (rc) return rc;
@@ -252,29 +310,19 @@ extern "C" int wv_index_load_segments(wv_index* idx, const char* const* paths, i
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
     int64_t loaded = 0;
+    int64_t d = 0;
+    rc = value_dims(latest, live, d);
+    if (rc) return rc;
     if (!live.empty()) {
-        // float32SliceFromByteSlice (flat/index.go:331-336): len/4 floats; the
-        // dimension check is ValidateBeforeInsert's (add_rows_locked)
-        const Entry& e0 = latest[live[0]];
-        if (e0.value_len % 4) return set_err(WV_ERR_INVALID, "vector value of %llu bytes is not float32-aligned",
-                                             (unsigned long long)e0.value_len);
-        const int64_t d = (int64_t)(e0.value_len / 4);
+        // the dimension check is ValidateBeforeInsert's (add_rows_locked)
         const int64_t chunk = std::max<int64_t>(1, (256ll << 20) / std::max<int64_t>(d * 4, 1));
         std::vector<float> buf;
         std::vector<uint64_t> ids;
         for (size_t c0 = 0; c0 < live.size(); c0 += (size_t)chunk) {
             size_t c1 = std::min(live.size(), c0 + (size_t)chunk);
-            buf.resize((c1 - c0) * (size_t)d);
             ids.assign(live.begin() + c0, live.begin() + c1);
-            for (size_t j = c0; j < c1; j++) {
-                const Entry& e = latest[live[j]];
-                if ((int64_t)e.value_len != d * 4) {
-                    return set_err(WV_ERR_INSERT,
-                                   "insert called with a vector of the wrong size: %lld. Saved length: %lld, path: %s",
-                                   (long long)(e.value_len / 4), (long long)d, paths[e.seg]);
-                }
-                memcpy(&buf[(j - c0) * d], maps[e.seg].p + e.value_off, (size_t)d * 4);  // LE host
-            }
+            rc = gather_rows(paths, maps, latest, live, c0, c1, d, buf);
+            if (rc) return rc;
             // the bucket holds the stored bytes (normalised by Add for cosine):
             // upload as they are (PostStartup / restore reads them unchanged)
             rc = add_rows_locked(idx, ids.data(), buf.data(), (int64_t)(c1 - c0), d, true);
@@ -286,3 +334,4 @@ extern "C" int wv_index_load_segments(wv_index* idx, const char* const* paths, i
     if (out) { out[0] = loaded; out[1] = (int64_t)dead.size(); out[2] = nodes; }
     return WV_OK;
 }
+#endif
