@@ -240,6 +240,24 @@ def measured_traffic(workload: str, n_local: int, dims: int, batch: int, kernel:
     return best
 
 
+def measured_clock(workload: str, n_local: int, dims: int, batch: int, kernel: str):
+    """Effective clock and MFMA-busy fraction of the dominant kernel from the
+    committed PMC record (profiles/*_clock_<workload>*.json, tools/pmc_qs3.sh)
+    when it was taken on this exact configuration; None otherwise."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_clock_{workload}*.json"))):
+        try:
+            rec = json.load(open(path))
+        except Exception:
+            continue
+        if (rec.get("corpus_rows"), rec.get("dims"), rec.get("query_batch"), rec.get("kernel")) == \
+                (n_local, dims, batch, kernel):
+            best = {k: rec[k] for k in ("effective_clock_ghz", "mfma_busy_frac", "frac_of_peak_at_clock")}
+            best["source"] = os.path.relpath(path, REPO)
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", choices=["c3", "c1", "c2", "bq", "pq", "rq8", "rq1"], default="c3",
@@ -445,11 +463,15 @@ def main():
         peak = MFMA_BF16_PEAK_TFLOPS
         roof = {"bound": "mfma", "kernel": sel_kernel, "achieved": achieved, "peak": peak,
                 "unit": "TFLOP/s", "frac": achieved / peak, "launch_ms": sel_avg,
-                "mfma": "v_mfma_f32_32x32x16_bf16 (bf16 in, fp32 accumulate): block keys = per-32-row minima of "
-                        "the approximate distance; every returned distance is the reference-order fp32 value",
+                "mfma": ("v_mfma_f32_16x16x32_bf16" if dims > 384 else "v_mfma_f32_32x32x16_bf16")
+                        + " (bf16 in, fp32 accumulate): block keys = per-32-row minima of the approximate "
+                          "distance; every returned distance is the reference-order fp32 value",
                 "pipeline_ms": total_avg,
                 "f32_mfma_peak_equivalent_frac": achieved / MFMA_F32_PEAK_TFLOPS,
-                "traffic": args.traffic_bytes}
+                "traffic": args.traffic_bytes,
+                # DVFS: the chip holds a lower clock under this MFMA load; the PMC
+                # record gives the clock and the MFMA pipe's busy fraction
+                "pmc_clock": measured_clock(args.workload, n_local, dims, B, sel_kernel)}
 
     result = None
     if rank == 0:

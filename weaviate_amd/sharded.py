@@ -264,16 +264,12 @@ class ShardedBQSearch:
         state = None
         for r in range(self.world):
             last = r == self.world - 1
-            if self.rank == r:
-                ids, dd, ln = self.b.bq_replay(state, last)
+            if self.rank == r:  # one packed broadcast per hop: [nq][2R ids | R dists | len]
+                buf = ShardedFlatSearch._pack_state(*self.b.bq_replay(state, last))
             else:
-                ids = torch.empty((nq, R), dtype=torch.int64, device=self.dev)
-                dd = torch.empty((nq, R), dtype=torch.float32, device=self.dev)
-                ln = torch.empty(nq, dtype=torch.int32, device=self.dev)
-            dist.broadcast(ids, src=r)
-            dist.broadcast(dd, src=r)
-            dist.broadcast(ln, src=r)
-            state = (ids, dd, ln)
+                buf = torch.empty((nq, 3 * R + 1), dtype=torch.int32, device=self.dev)
+            dist.broadcast(buf, src=r)
+            state = ShardedFlatSearch._unpack_state(buf, R)
         ids, _, ln = state
         E = self.b.bq_rescore(ids, ln)
         E_all = self._all_gather(E)
