@@ -4,7 +4,7 @@
 Workload (BASELINE.json configs[2], the config north_star's target is quoted
 on): 10M x 768 fp32 vectors, cosine ("cosine-dot"), k = 10, corpus sharded
 over the N GPUs of one node by contiguous doc-id ranges (N=1: the whole 10M
-corpus on one GPU).  One step = one batch of B = 4096 queries through the
+corpus on one GPU).  One step = one batch of B = 8192 queries through the
 full SearchByVector pipeline (query normalisation, bf16 block-key MFMA pass,
 candidate-block selection, exact-order distances of the candidate rows,
 exactness proof, bounded heap replay of any flagged query; for N>1 the
@@ -44,10 +44,11 @@ FLAT = {
     "c2": dict(n=1_000_000, d=128, metric="l2-squared", k=100, batch=10_000, kind=1,
                name="SIFT-shaped 1M x 128 integer-valued fp32 U{0..127}, l2-squared, k=100, 10k-query batch "
                     "(BASELINE configs[1])"),
-    # c3: 4096 queries per step -- one block-key launch of 16 query groups per
-    # corpus span (58 % of the bf16 peak vs 55 % at 2048) and the fixed
-    # per-step costs amortised for the 8-GPU strong scaling
-    "c3": dict(n=10_000_000, d=768, metric="cosine", k=10, batch=4096, kind=0,
+    # c3: 8192 queries per step -- one block-key launch of 32 query groups per
+    # corpus span, every XCD's 32 workgroups on one span (60 % of the bf16 peak
+    # vs 58 % at 4096 and 55 % at 2048) and the fixed per-step costs amortised
+    # for the 8-GPU strong scaling
+    "c3": dict(n=10_000_000, d=768, metric="cosine", k=10, batch=8192, kind=0,
                name="10M x 768 fp32 cosine, k=10, exact flat search (BASELINE configs[2])"),
 }
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (spec, MI355X_MICROARCH.md)

@@ -1,13 +1,14 @@
 #!/bin/bash
-# busy / wait / LDS counters of the block-key kernel at B=4096 (C3), one pass per group
+# busy / wait / LDS counters of the block-key kernel on C3, one pass per group
 OUT=${1:-gpurun_out/pmcqs3}
+B=${2:-4096}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p "$OUT"
 i=0
 for grp in "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
            "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_INSTS_VALU SQ_INSTS_SALU"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp -d "$OUT/p$i" -o run --output-format csv -- python3 tools/qs_probe.py --verify 0 --batch 4096 --configs "sel_dbg=0" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $grp -d "$OUT/p$i" -o run --output-format csv -- python3 tools/qs_probe.py --verify 0 --batch $B --configs "sel_dbg=0" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   echo "pass $i ok"
 done
 python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.txt"
