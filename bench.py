@@ -272,6 +272,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the multi-GPU protocol (ShardedFlatSearch / ShardedBQSearch over RCCL) even at "
+                         "WORLD_SIZE 1 (launch under torch.distributed.run): a one-GPU check of the N>1 path")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-queries", type=int, default=None)
     ap.add_argument("--cpu-threads", type=int, default=None, help="default: nproc (all CPUs this process may use)")
@@ -294,7 +297,8 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    shard = world > 1 or args.sharded
+    if shard:
         dist.init_process_group("nccl", device_id=dev)
 
     import weaviate_amd as wv
@@ -355,13 +359,13 @@ def main():
     out_d = torch.empty((B, K_), dtype=torch.float32, device=dev)
     out_n = torch.empty(B, dtype=torch.int32, device=dev)
 
-    if world > 1 and bq:
+    if shard and bq:
         from weaviate_amd.sharded import GpuBQShardBackend, ShardedBQSearch
         searcher = ShardedBQSearch(GpuBQShardBackend(index, local_rank), dev, (n_total + world - 1) // world)
 
         def step():
             return searcher.search(queries, K_)
-    elif world > 1:
+    elif shard:
         from weaviate_amd.sharded import GpuShardBackend, ShardedFlatSearch
         searcher = ShardedFlatSearch(GpuShardBackend(index, local_rank), dev)
 
@@ -381,6 +385,8 @@ def main():
     torch.cuda.synchronize()
     sel_ms, tot_ms = [], []
     replays0 = index.stats()["replayed_queries"]
+    if shard and not bq:
+        searcher.flagged = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -393,6 +399,19 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     replays = index.stats()["replayed_queries"] - replays0
+    if shard and not bq:
+        replays = int(searcher.flagged)  # the cross-shard replay's queries (this rank's view = every rank's)
+    sharded_check = None
+    if args.sharded and world == 1 and flat:
+        # the sharded protocol at one rank must equal the single-index search
+        si, sd, sn = step()[:3]
+        s = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(lib.wv_index_search_device(index._h, queries.data_ptr(), B, dims, K_, 0, out_ids.data_ptr(),
+                                              out_d.data_ptr(), out_n.data_ptr(), None, s))
+        torch.cuda.synchronize()
+        sharded_check = bool(torch.equal(sn, out_n) and torch.equal(si.view(torch.int64), out_ids)
+                             and torch.equal(sd.view(torch.int32), out_d.view(torch.int32)))
+        log(f"sharded protocol at world 1 equals the single-index search: {sharded_check}")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -537,12 +556,13 @@ def main():
                                    else ", RCCL all-gather merge") if world > 1 else ""),
                 "replayed_queries": int(replays),
             },
+            **({"sharded_equals_single": sharded_check} if sharded_check is not None else {}),
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
     index.close()
-    if world > 1:
+    if shard:
         dist.destroy_process_group()
 
 

@@ -2346,9 +2346,11 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     const int metric = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
     const float* Qn_all = idx->qn.as<float>();
-    idx->timed = 0;
-    idx->timed_total = 0;
-    if (idx->timing) HIPCHK(hipEventRecord(idx->evt0, s));
+    if (phase != 2) {  // phase 2 keeps phase 1's block-key timing; the total spans both
+        idx->timed = 0;
+        idx->timed_total = 0;
+        if (idx->timing) HIPCHK(hipEventRecord(idx->evt0, s));
+    }
     for (int64_t c0 = 0; c0 < nq; c0 += qc) {
         const int64_t cn = std::min<int64_t>(qc, nq - c0);
         const int64_t cn_pad = round_up(cn, QS_QPB);

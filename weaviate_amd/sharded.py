@@ -284,6 +284,7 @@ class ShardedFlatSearch:
         self.dev = device
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
+        self.flagged = 0  # queries that went through the cross-shard replay (device tensor after a search)
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         t = t.contiguous()
@@ -325,6 +326,7 @@ class ShardedFlatSearch:
         gc = G[..., 3 * k1].contiguous()
         gf = G[..., 3 * k1 + 1].contiguous()
         oi, od, on, of = self.b.merge(self.world, k, gi, gd, gc, gf)
+        self.flagged = self.flagged + (of != 0).sum()  # no host sync
         if getattr(self.b, "replay_record", None) is not None and k < 64:
             return self._replay_parallel(q, k, of, oi, od, on, gd, gc, gf)
         if getattr(self.b, "replay_flags", None) is not None:
