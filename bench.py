@@ -71,7 +71,11 @@ PQ_DIMS = 960
 PQ_SEGMENTS = 240
 PQ_CENTROIDS = 256
 PQ_TRAIN = 100_000
-LDS_LOOKUP_PEAK_T = 19.7       # 256 CU x 32 dwords/clk (128 B/clk LDS) x 2.4 GHz
+# 4-byte LUT lookups from LDS: the LDS array moves 256 B/clk/CU (ds_read_b64 /
+# b128; MI355X_MICROARCH.md LDS table) -> 64 lookups/clk/CU x 256 CU x 2.4 GHz;
+# ds_read_b32 (one lookup per lane) is capped at half that (128 B/clk)
+LDS_LOOKUP_PEAK_T = 39.3
+LDS_LOOKUP_B32_T = 19.7
 
 
 def log(*a):
@@ -457,8 +461,9 @@ def main():
         f0 = int(index.stats().get("last_group_queries", 0)) or max(1, min(B, (2 << 30) // (ld * 4)))  # timed first group
         lookups = float(f0) * n_local * PQ_SEGMENTS
         achieved = lookups / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
-        roof = {"bound": "lds", "kernel": "k_pq_adc", "achieved": achieved, "peak": LDS_LOOKUP_PEAK_T,
-                "unit": "T lookups/s", "frac": achieved / LDS_LOOKUP_PEAK_T, "launch_ms": sel_avg,
+        roof = {"bound": "lds", "kernel": "k_pq_adc2 (two queries per ds_read_b64)", "achieved": achieved,
+                "peak": LDS_LOOKUP_PEAK_T, "unit": "T lookups/s", "frac": achieved / LDS_LOOKUP_PEAK_T,
+                "frac_of_b32_lookup_rate": achieved / LDS_LOOKUP_B32_T, "launch_ms": sel_avg,
                 "note": "launch_ms = first query group of the batch",
                 "traffic": args.traffic_bytes}
     elif bq:

@@ -55,19 +55,21 @@ def test_pq_fit_codes_distance_match_oracle(wv, oracle, metric, kind, n, d, m, k
     ("l2-squared", 1, True, 7, 40),     # integer data: ADC ties -> heap order
     ("l2-squared", 1, False, 20, -1),
 ])
-def test_pq_search_matches_oracle(wv, oracle, metric, kind, rescore, k, rl):
+@pytest.mark.parametrize("adc,nq", [(2, 16), (2, 15), (1, 16)])  # k_pq_adc2 (odd list: one single-query block), k_pq_adc
+def test_pq_search_matches_oracle(wv, oracle, metric, kind, rescore, k, rl, adc, nq):
     n, d, m, ks = 5000, 32, 8, 32
     data = gen(oracle, kind, 71, n, d)
     idx = wv.FlatIndex(distance=metric, variant="avx256", rescore_limit=rl,
                        pq={"segments": m, "centroids": ks, "rescore": rescore})
     idx.add_batch(np.arange(n, dtype=np.uint64), data)
     idx.pq_fit(seed=77)
+    idx.set_option("pq_adc", adc)
     centers = idx.pq_centers()
     codes = idx.pq_codes(n)
     om = oracle.METRIC[metric]
     store = stored_rows(oracle, om, data)
     present = np.ones(n, np.uint8)
-    queries = gen(oracle, kind, 72, 16, d)
+    queries = gen(oracle, kind, 72, nq, d)
     ids, dists, counts = idx.search_by_vector_batch(queries, k)
     for qi in range(len(queries)):
         qv = oracle.normalize(queries[qi]) if om == oracle.COSINE else queries[qi]

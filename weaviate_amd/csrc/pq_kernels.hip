@@ -353,6 +353,117 @@ __global__ __launch_bounds__(256, 2) void k_pq_adc(const uint32_t* __restrict__ 
     }
 }
 
+// k_pq_adc for two listed queries per workgroup (f = 2 blockIdx.x, +1): the
+// LUT chunk is staged interleaved [segment][code][2 queries], so one
+// ds_read_b64 fetches both queries' entries of a code.  A random-code lookup
+// is bank-conflict bound (ds_read_b32 and ds_read_b64 are both serviced as
+// 2 x 32 lanes with bank = code mod 32): the b64 read pays that
+// once per two lookups, and the tile's codes are read once for both queries.
+// Per query the fp32 sums keep segment order (bit-identical to k_pq_adc).
+// nf = listed queries of this launch; an odd last workgroup runs one query.
+// RPT 256-row code tiles per workgroup: PQ_RPT = 8 (16 and 32 spill to scratch
+// and ran 4x / 12x slower on C5).
+template <int KC, int RPT>
+__global__ __launch_bounds__(256, 2) void k_pq_adc2(const uint32_t* __restrict__ codes, int g16, int m, int kk,
+                                                    const uint32_t* __restrict__ valid, int64_t nslots,
+                                                    const float* __restrict__ lut, const int32_t* __restrict__ qlist,
+                                                    int nf, int metric, int64_t ld, float* __restrict__ E,
+                                                    float* __restrict__ bmin) {
+    extern __shared__ float2 lsm2[];  // [PQ_CH][k] x 2 queries
+    __shared__ float red[2][4][RPT];
+    const int k = KC > 0 ? KC : kk;
+    const int t = threadIdx.x;
+    const int f0 = 2 * blockIdx.x;
+    const bool two = f0 + 1 < nf;
+    const int64_t tile0 = (int64_t)blockIdx.y * 256 * RPT;
+    const uint4* cbase = reinterpret_cast<const uint4*>(codes) + (int64_t)blockIdx.y * RPT * g16 * 256;
+    const int64_t rem64 = nslots - tile0;
+    const int rem = rem64 < 256 * RPT ? (int)rem64 : 256 * RPT;
+    const float* L0 = lut + (int64_t)qlist[f0] * m * k;
+    const float* L1 = two ? lut + (int64_t)qlist[f0 + 1] * m * k : L0;
+    float sa[RPT], sb[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; r++) sa[r] = sb[r] = 0.f;
+    for (int s0 = 0; s0 < m; s0 += PQ_CH) {
+        const int ns = m - s0 < PQ_CH ? m - s0 : PQ_CH;
+        __syncthreads();
+        for (int i = t; i < ns * k; i += 256) lsm2[i] = make_float2(L0[(int64_t)s0 * k + i], L1[(int64_t)s0 * k + i]);
+        __syncthreads();
+#pragma unroll 1
+        for (int c16 = 0; c16 < ns; c16 += 16) {
+            const float2* lc = lsm2 + c16 * k;
+            const int g = (s0 + c16) >> 4;
+            const int nv = ns - c16 < 16 ? ns - c16 : 16;
+            if (nv == 16) {
+#pragma unroll
+                for (int rb = 0; rb < RPT; rb += 4) {
+                    uint4 cw[4];
+#pragma unroll
+                    for (int rr = 0; rr < 4; rr++) {
+                        const int r = rb + rr;
+                        cw[rr] = 256 * r + t < rem ? cbase[(uint32_t)((r * g16 + g) * 256 + t)] : make_uint4(0u, 0u, 0u, 0u);
+                    }
+#pragma unroll
+                    for (int rr = 0; rr < 4; rr++) {
+                        float a0 = sa[rb + rr], a1 = sb[rb + rr];
+                        const uint32_t wv4[4] = {cw[rr].x, cw[rr].y, cw[rr].z, cw[rr].w};
+#pragma unroll
+                        for (int w = 0; w < 4; w++)
+#pragma unroll
+                            for (int b = 0; b < 4; b++) {
+                                const float2 v = lc[(4 * w + b) * k + ((wv4[w] >> (8 * b)) & 0xFFu)];
+                                a0 = a0 + v.x;
+                                a1 = a1 + v.y;
+                            }
+                        sa[rb + rr] = a0;
+                        sb[rb + rr] = a1;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < RPT; r++) {
+                    const uint4 c4 = 256 * r + t < rem ? cbase[(uint32_t)((r * g16 + g) * 256 + t)] : make_uint4(0u, 0u, 0u, 0u);
+                    const uint32_t wv4[4] = {c4.x, c4.y, c4.z, c4.w};
+                    float a0 = sa[r], a1 = sb[r];
+#pragma unroll 1
+                    for (int j = 0; j < nv; j++) {
+                        const float2 v = lc[j * k + ((wv4[j >> 2] >> (8 * (j & 3))) & 0xFFu)];
+                        a0 = a0 + v.x;
+                        a1 = a1 + v.y;
+                    }
+                    sa[r] = a0;
+                    sb[r] = a1;
+                }
+            }
+        }
+    }
+    const int lane = t & 63, wv = t >> 6;
+    const int64_t lrem = ld - tile0;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        float* Ef = E + (int64_t)(f0 + j) * ld + tile0;
+#pragma unroll
+        for (int r = 0; r < RPT; r++) {
+            const int lr = 256 * r + t;
+            const int64_t row = tile0 + lr;
+            const bool ok = lr < rem && ((valid[row >> 5] >> (row & 31)) & 1u);
+            const float e = ok ? pq_wrap(metric, j ? sb[r] : sa[r]) : __builtin_inff();
+            if ((j == 0 || two) && lr < lrem) Ef[lr] = e;
+            float mm = e;
+            for (int o = 32; o > 0; o >>= 1) mm = fminf(mm, __shfl_xor(mm, o));
+            if (lane == 0) red[j][wv][r] = mm;
+        }
+    }
+    __syncthreads();
+    if (t < 2 * RPT) {
+        const int j = t / RPT, r = t % RPT;
+        const int64_t blk = tile0 / 256 + r;
+        if ((j == 0 || two) && blk < ld / 256)
+            bmin[(int64_t)(f0 + j) * (ld / 256) + blk] =
+                fminf(fminf(red[j][0][r], red[j][1][r]), fminf(red[j][2][r], red[j][3][r]));
+    }
+}
+
 // flatSearch tail (hnsw/flat_search.go:96-141 with one worker): the worker
 // heap's ascending extraction asc[li][0..n) is popped max-first
 // (= reverse order) into the result heap via addResult (:214-224).

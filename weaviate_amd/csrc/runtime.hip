@@ -124,6 +124,7 @@ struct wv_index {
     int replay_par = 2;  // block-key replay: 2 = pooled three-kernel form (k < 64), 3 = pooled for any k,
                          // 1 = 8-wave form, 0 = one wave
     int64_t rp_pool = 1 << 20;  // pooled replay: candidate blocks per batch (144 B each)
+    int pq_adc = 2;             // PQ ADC queries per workgroup: 2 = k_pq_adc2 (b64 LUT pairs), 1 = k_pq_adc
     int qs_force_flag = 0;      // tests: flag every query of the block-key path (exercise the replay)
     int device = 0;
     uint64_t id_base = 0;
@@ -796,6 +797,10 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "ef_factor") idx->ef_factor = (int)value;
     else if (k == "hnsw_rescore") idx->hnsw_rescore = value ? 1 : 0;  // 0: doNotRescore
     else if (k == "rescore_limit") idx->rescore_limit = (int)value;
+    else if (k == "pq_adc") {
+        if (value != 1 && value != 2) return set_err(WV_ERR_INVALID, "pq_adc must be 1 or 2");
+        idx->pq_adc = (int)value;
+    }
     else if (k == "rp_pool") {  // pooled replay capacity in 32-row blocks (tests force the fallback with 1)
         if (value < 1 || value > (1ll << 26)) return set_err(WV_ERR_INVALID, "rp_pool out of range");
         idx->rp_pool = value;
@@ -1702,7 +1707,19 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
             const int m = idx->pq_m, K = idx->pq_ks;
             const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
             dim3 grid((unsigned)F, (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
-            if (K == 256)
+            if (idx->pq_adc == 2) {  // two queries per workgroup: 2 x the LUT chunk (64 KiB at ks = 256)
+                dim3 grid2((unsigned)((F + 1) / 2), grid.y);
+#define WV_ADC2(KCV, RPTV)                                                                                   \
+    do {                                                                                                     \
+        HIPCHK(hipFuncSetAttribute((const void*)k_pq_adc2<KCV, RPTV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                   (int)(2 * lds_adc)));                                                     \
+        k_pq_adc2<KCV, RPTV><<<grid2, 256, 2 * lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,    \
+                                                             idx->lut.as<float>(), qlist + g0, F, wrapm, ld, E, Bm); \
+    } while (0)
+                if (K == 256) WV_ADC2(256, PQ_RPT);
+                else WV_ADC2(0, PQ_RPT);
+#undef WV_ADC2
+            } else if (K == 256)
                 k_pq_adc<256><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,
                                                          idx->lut.as<float>(), qlist + g0, wrapm, ld, E, Bm);
             else
