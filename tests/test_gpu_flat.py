@@ -395,3 +395,25 @@ def test_pooled_replay_float_data(wv, oracle, metric):
     assert idx.stats()["replayed_queries"] - before == len(queries)
     for qi in range(len(queries)):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")
+
+
+@pytest.mark.parametrize("metric,kind,variant,n,d,k", [("l2-squared", 1, "avx256", 40000, 128, 100),   # C2-like ties
+                                                      ("cosine", 0, "avx512", 30000, 200, 10),
+                                                      ("dot", 0, "avx256", 20000, 500, 24),
+                                                      ("l2-squared", 1, "avx256", 30000, 24, 200)])  # R = 8 lists
+def test_block_major_exact_equals_oracle(wv, oracle, metric, kind, variant, n, d, k):
+    """exact_bm=1: candidate lists inverted per 32-row block (k_inv_*), each
+    block's rows staged once (k_exact_bm), k_blk_exact reads the distances.
+    Results (fast path, proof flags and replays) equal the oracle and the
+    per-query path bit for bit."""
+    data = gen(oracle, kind, 95, n, d)
+    queries = gen(oracle, kind, 96, 300, d)
+    res = []
+    for bm in (0, 1):
+        idx, orc = build_pair(wv, oracle, metric, variant, data)
+        idx.set_option("exact_bm", bm)
+        res.append(idx.search_by_vector_batch(queries, k))
+    for qi in range(len(queries)):
+        exp = orc.search(queries[qi], k)
+        for ids, dists, counts in res:
+            assert_same(exp, ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} k{k} q{qi}")

@@ -781,7 +781,7 @@ __global__ __launch_bounds__(256) void k_blk_gthresh(const float* __restrict__ t
 
 // k_blk_exact<R, METRIC, VARIANT>: one workgroup (4 waves) per query over its
 // candidate blocks (each wave two blocks per pass: lanes 0-31 and 32-63, lane
-// = row).  Reference-order SingleDist of every valid row, top-(k+1) by
+// = row); ebuf != null: the distances come from k_exact_bm.  Reference-order SingleDist of every valid row, top-(k+1) by
 // (distance, id) per wave, merged by wave 0; proof = the first min(k+1, n)
 // are strictly increasing (the reference heap then holds exactly the k
 // smallest and extractHeap returns them ascending).
@@ -792,7 +792,8 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
                                                    int nq, int k, int kout, uint64_t id_base, uint64_t* __restrict__ out_ids,
                                                    float* __restrict__ out_d, int32_t* __restrict__ out_n,
                                                    int32_t* __restrict__ flags, const int32_t* __restrict__ qlist,
-                                                   const uint32_t* __restrict__ qcount) {
+                                                   const uint32_t* __restrict__ qcount,
+                                                   const float* __restrict__ ebuf = nullptr, int64_t ldE = 0) {
     constexpr int L = 64 * (R - 1);
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
@@ -823,7 +824,7 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
             ok = row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
         }
         float e = __builtin_inff();
-        if (ok) e = exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d);
+        if (ok) e = ebuf ? ebuf[(int64_t)q * ldE + j * 32 + li] : exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d);
         nvalid += __popcll(__ballot(ok));
         t.offer(ok ? e : __builtin_inff(), ok ? (uint32_t)row : NO_ID, sbk[w], sbi[w], lane);
     }
@@ -868,6 +869,100 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         }
     }
     if (lane == 0) out_n[q] = nout;
+}
+
+// ---------------------------------------------------------------------------
+// Block-major exact distances (rows of up to 508 floats).  Many queries list
+// the same candidate block (C2: ~60 per block); reading the block once per
+// listing query makes k_blk_exact bandwidth-bound on re-reads.  The candidate
+// lists are inverted per 32-row block (k_inv_count / k_inv_scan /
+// k_inv_scatter: pairs (query << 9 | list position)), k_exact_bm stages each
+// listed block's rows in LDS once and writes the reference-order exact
+// distance of every row for every listing query to ebuf[q][j*32 + row];
+// k_blk_exact then reads them instead of recomputing (same values, same
+// selection and proof).  Order of pairs within a block does not matter: every
+// pair writes its own slot.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_inv_count(const uint32_t* __restrict__ cand, const int32_t* __restrict__ ncand,
+                                                   const int32_t* __restrict__ flags, int nq, int L,
+                                                   uint32_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq || flags[q]) return;
+    const int nc = ncand[q];
+    for (int j = lane; j < nc; j += 64) atomicAdd(&cnt[cand[(int64_t)q * L + j]], 1u);
+}
+
+// exclusive prefix of cnt[0..nb) -> off[0..nb], cnt reset to 0 (the scatter's
+// cursors); one workgroup of 1024 threads
+__global__ __launch_bounds__(1024) void k_inv_scan(uint32_t* __restrict__ cnt, int64_t nb, uint32_t* __restrict__ off) {
+    __shared__ uint32_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (nb + 1023) / 1024;
+    const int64_t b0 = (int64_t)t * per, b1 = b0 + per < nb ? b0 + per : nb;
+    uint32_t s = 0;
+    for (int64_t b = b0; b < b1; b++) s += cnt[b];
+    part[t] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - s;
+    for (int64_t b = b0; b < b1; b++) {
+        const uint32_t c = cnt[b];
+        off[b] = run;
+        run += c;
+        cnt[b] = 0;
+    }
+    if (t == 1023) off[nb] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_inv_scatter(const uint32_t* __restrict__ cand, const int32_t* __restrict__ ncand,
+                                                     const int32_t* __restrict__ flags, int nq, int L,
+                                                     const uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
+                                                     uint32_t* __restrict__ pairs) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq || flags[q]) return;
+    const int nc = ncand[q];
+    for (int j = lane; j < nc; j += 64) {
+        const uint32_t b = cand[(int64_t)q * L + j];
+        pairs[off[b] + atomicAdd(&cur[b], 1u)] = ((uint32_t)q << 9) | (uint32_t)j;
+    }
+}
+
+// one workgroup per 32-row block; LDS rows at stride dpad + 4 floats (16-byte
+// aligned; lane = row reads conflict-free in 16-lane groups)
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(256) void k_exact_bm(const float* __restrict__ X, int dpad, int64_t nrows,
+                                                  const float* __restrict__ Qn, int d, const uint32_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ pairs, int64_t ldE,
+                                                  float* __restrict__ ebuf) {
+    extern __shared__ float4 rows4[];
+    const int64_t b = blockIdx.x;
+    const uint32_t p0 = off[b], p1 = off[b + 1];
+    if (p0 == p1) return;
+    const int t = threadIdx.x;
+    const int d4 = dpad / 4, s4 = d4 + 1;  // float4s per row in global / in LDS
+    const float4* X4 = reinterpret_cast<const float4*>(X);
+    for (int i = t; i < 32 * d4; i += 256) {
+        const int r = i / d4, c = i - r * d4;
+        const int64_t row = b * 32 + r;
+        rows4[r * s4 + c] = row < nrows ? X4[row * d4 + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const int lane = t & 63, w = t >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    const float* xr = reinterpret_cast<const float*>(rows4 + li * s4);
+    for (uint32_t p = p0 + 2 * w + lh; p < p1; p += 8) {
+        const uint32_t pr = pairs[p];
+        const int64_t q = pr >> 9;
+        const int j = (int)(pr & 511u);
+        ebuf[q * ldE + j * 32 + li] = exact_dist<METRIC, VARIANT>(Qn + q * dpad, xr, d);
+    }
 }
 
 // flagged queries -> list (order irrelevant: every listed query is handled

@@ -126,6 +126,7 @@ struct wv_index {
     int64_t rp_pool = 1 << 20;  // pooled replay: candidate blocks per batch (144 B each)
     int pq_adc = 2;             // PQ ADC queries per workgroup: 2 = k_pq_adc2 (b64 LUT pairs), 1 = k_pq_adc
     int qs_force_flag = 0;      // tests: flag every query of the block-key path (exercise the replay)
+    int exact_bm = 0;           // block-major exact distances (rows <= 508 floats): 1 on, 0 off
     int device = 0;
     uint64_t id_base = 0;
     std::string root_path;
@@ -204,6 +205,7 @@ struct wv_index {
     DBuf rE2, rB2;
     DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
     DBuf rpBlk, rpLb, rpQ, rpE, rpVm, rpOff, rpTot, rpCtr;  // pooled replay (k_rp_*)
+    DBuf bmCnt, bmOff, bmPairs, bmE;                          // block-major exact (k_inv_*, k_exact_bm)
     DBuf flCtr;                      // device flag-list counters (replay_flags)
     int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
     int qs_phase_k = 0;
@@ -791,6 +793,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
         idx->replay_par = (int)value;
     }
     else if (k == "qs_force_flag") idx->qs_force_flag = value ? 1 : 0;
+    else if (k == "exact_bm") idx->exact_bm = value ? 1 : 0;
     else if (k == "ef") idx->hnsw_ef = (int)value;  // hnsw UserConfig.EF (-1: dynamic)
     else if (k == "ef_min") idx->ef_min = (int)value;
     else if (k == "ef_max") idx->ef_max = (int)value;
@@ -2453,8 +2456,8 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
             if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
 #undef WV_SELR
         };
-        auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt) {
-#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags, list, cnt)
+        auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0) {
+#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags, list, cnt, eb, ldE)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \
     case L2: if (v5) WV_EXR(RV, L2, AVX512); else WV_EXR(RV, L2, AVX256); break;   \
@@ -2472,7 +2475,34 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
             k_blk_gthresh<<<(unsigned)((cn + 3) / 4), 256, 0, s>>>(gA, gE, W, (int)cn, k, metric, qinfo, a.key, ldk,
                                                                   idx->qsCand.as<uint32_t>(), L, idx->qsNc.as<int32_t>(),
                                                                   idx->qsEps.as<float>(), flags);
-        exa(R, nullptr, nullptr);
+        const size_t bm_lds = (size_t)32 * (idx->dpad + 4) * sizeof(float);
+        if (idx->exact_bm && bm_lds <= 64 * 1024 && nb < (1ll << 31)) {
+            // block-major exact distances: invert the candidate lists per block
+            const int64_t ldE = (int64_t)L * 32;
+            HIPCHK(idx->bmCnt.ensure((size_t)nb * sizeof(uint32_t)));
+            HIPCHK(idx->bmOff.ensure((size_t)(nb + 1) * sizeof(uint32_t)));
+            HIPCHK(idx->bmPairs.ensure((size_t)cn * L * sizeof(uint32_t)));
+            HIPCHK(idx->bmE.ensure((size_t)cn * ldE * sizeof(float)));
+            HIPCHK(hipMemsetAsync(idx->bmCnt.p, 0, (size_t)nb * sizeof(uint32_t), s));
+            const unsigned gw = (unsigned)((cn + 3) / 4);
+            k_inv_count<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
+                                           idx->bmCnt.as<uint32_t>());
+            k_inv_scan<<<1, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmOff.as<uint32_t>());
+            k_inv_scatter<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
+                                             idx->bmOff.as<uint32_t>(), idx->bmCnt.as<uint32_t>(),
+                                             idx->bmPairs.as<uint32_t>());
+#define WV_BM(M, V) k_exact_bm<M, V><<<(unsigned)nb, 256, bm_lds, s>>>(idx->X, idx->dpad, idx->hiwater, Qn, idx->dims, idx->bmOff.as<uint32_t>(), idx->bmPairs.as<uint32_t>(), ldE, idx->bmE.as<float>())
+            switch (metric) {
+            case L2: if (v5) WV_BM(L2, AVX512); else WV_BM(L2, AVX256); break;
+            case DOT: if (v5) WV_BM(DOT, AVX512); else WV_BM(DOT, AVX256); break;
+            default: if (v5) WV_BM(COSINE, AVX512); else WV_BM(COSINE, AVX256); break;
+            }
+#undef WV_BM
+            HIPCHK(hipGetLastError());
+            exa(R, nullptr, nullptr, idx->bmE.as<float>(), ldE);
+        } else {
+            exa(R, nullptr, nullptr);
+        }
         HIPCHK(hipGetLastError());
         if (R < 8) {  // candidate lists that overflowed (flag 2): again with the 448-block lists
             HIPCHK(hipMemsetAsync(idx->qscount + 3, 0, sizeof(uint32_t), s));
