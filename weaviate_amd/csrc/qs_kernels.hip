@@ -598,6 +598,14 @@ __device__ __forceinline__ float qs_key_to_a(int metric, float key, float qn2) {
     return p < 0.f ? 0.f : p;
 }
 
+// the next float toward +inf (finite x)
+__device__ __forceinline__ float qs_next_up(float x) {
+    if (!(x < __builtin_inff())) return x;
+    if (x == 0.f) return 1.4e-45f;
+    const uint32_t b = __float_as_uint(x);
+    return __uint_as_float(x > 0.f ? b + 1u : b - 1u);
+}
+
 // ---------------------------------------------------------------------------
 // wave-level streaming selection of the L = 64 (R-1) smallest (key, id) pairs:
 // list in rows 0..R-2 of the register arrays (sorted), row R-1 takes the LDS
@@ -608,18 +616,19 @@ struct WaveTopL {
     float key[R];
     uint32_t id[R];
     float thr;
+    float cap;  // values >= cap are never kept (a known upper bound of the wanted prefix)
     int cnt;
-    __device__ __forceinline__ void init() {
+    __device__ __forceinline__ void init(float cap_ = __builtin_inff()) {
 #pragma unroll
         for (int r = 0; r < R; r++) { key[r] = __builtin_inff(); id[r] = NO_ID; }
-        thr = __builtin_inff();
+        thr = cap = cap_;
         cnt = 0;
     }
     __device__ __forceinline__ void merge(const float* bk, const uint32_t* bi, int lane) {
         key[R - 1] = lane < cnt ? bk[lane] : __builtin_inff();
         id[R - 1] = lane < cnt ? bi[lane] : NO_ID;
         bitonic_sort<R>(key, id, lane);
-        thr = __shfl(key[R - 2], 63);
+        thr = fminf(__shfl(key[R - 2], 63), cap);
         cnt = 0;
     }
     // offer one value per lane; `c` = this lane's value passes (v < thr)
@@ -661,7 +670,8 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
                                                     float gd, float gacc, uint32_t* __restrict__ cand,
                                                     int32_t* __restrict__ ncand, int32_t* __restrict__ flags,
                                                     float* __restrict__ eps_out, const int32_t* __restrict__ qlist,
-                                                    const uint32_t* __restrict__ qcount, float* __restrict__ topA) {
+                                                    const uint32_t* __restrict__ qcount, float* __restrict__ topA,
+                                                    float* __restrict__ cap_out = nullptr) {
     constexpr int L = 64 * (R - 1);
     constexpr int U = 16;
     __shared__ float sbk[4][64];
@@ -709,6 +719,11 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
     if (lane == 0) {
         ncand[q] = nc;
         eps_out[q] = eps;
+        // the k+1 smallest blocks each hold a row with E <= A + eps <= M + eps, so
+        // the (k+1)-th smallest exact distance over the candidates is below cap
+        if (cap_out)
+            cap_out[q] = mk == __builtin_inff() ? __builtin_inff()
+                                                 : qs_next_up(M + 1.001f * eps);
         // the L-th entry also qualifies: blocks beyond the list may too
         flags[q] = (nc >= L || qi.w != 0.f) ? 2 : 0;
     }
@@ -793,7 +808,8 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
                                                    float* __restrict__ out_d, int32_t* __restrict__ out_n,
                                                    int32_t* __restrict__ flags, const int32_t* __restrict__ qlist,
                                                    const uint32_t* __restrict__ qcount,
-                                                   const float* __restrict__ ebuf = nullptr, int64_t ldE = 0) {
+                                                   const float* __restrict__ ebuf = nullptr, int64_t ldE = 0,
+                                                   const float* __restrict__ cap = nullptr) {
     constexpr int L = 64 * (R - 1);
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
@@ -813,7 +829,7 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     const float* qv = Qn + (int64_t)q * dpad;
     const int li = lane & 31, lh = lane >> 5;
     WaveTopL<R> t;
-    t.init();
+    t.init(cap ? cap[q] : __builtin_inff());  // only the k+1 smallest are used: nothing above cap
     int nvalid = 0;
     for (int j0 = 2 * w; j0 < nc; j0 += 8) {
         const int j = j0 + lh;

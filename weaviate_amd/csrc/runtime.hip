@@ -206,6 +206,8 @@ struct wv_index {
     DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
     DBuf rpBlk, rpLb, rpQ, rpE, rpVm, rpOff, rpTot, rpCtr;  // pooled replay (k_rp_*)
     DBuf bmCnt, bmOff, bmPairs, bmE;                          // block-major exact (k_inv_*, k_exact_bm)
+    DBuf qsCap;                                               // per query: upper bound of the (k+1)-th exact distance
+    int exact_cap = 1;                                        // k_blk_exact drops values above qsCap (phase 0)
     DBuf flCtr;                      // device flag-list counters (replay_flags)
     int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
     int qs_phase_k = 0;
@@ -794,6 +796,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     }
     else if (k == "qs_force_flag") idx->qs_force_flag = value ? 1 : 0;
     else if (k == "exact_bm") idx->exact_bm = value ? 1 : 0;
+    else if (k == "exact_cap") idx->exact_cap = value ? 1 : 0;
     else if (k == "ef") idx->hnsw_ef = (int)value;  // hnsw UserConfig.EF (-1: dynamic)
     else if (k == "ef_min") idx->ef_min = (int)value;
     else if (k == "ef_max") idx->ef_max = (int)value;
@@ -2352,6 +2355,7 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     HIPCHK(idx->qsCand.ensure((size_t)qc * std::max(L, 448) * sizeof(uint32_t)));  // 448: the overflow pass
     HIPCHK(idx->qsNc.ensure((size_t)qc * sizeof(int32_t)));
     HIPCHK(idx->qsEps.ensure((size_t)qc * sizeof(float)));
+    HIPCHK(idx->qsCap.ensure((size_t)qc * sizeof(float)));
     HIPCHK(idx->qsList.ensure((size_t)2 * qc * sizeof(int32_t)));
     if (!o_flags || phase) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
     if (phase && qc < nq) return set_err(WV_ERR_UNSUPPORTED, "two-phase shard search: batch exceeds one query chunk");
@@ -2452,12 +2456,14 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         // select / exact pass RV over all queries (list == nullptr) or over the listed ones
         auto sel = [&](int RV, const int32_t* list, const uint32_t* cnt, float* tA) {
             const unsigned gw = (unsigned)((cn + 3) / 4);
-#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA)
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>())
             if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
 #undef WV_SELR
         };
+        // phase 2 cuts the lists with the global threshold: the local cap no longer bounds them
+        const float* capv = (idx->exact_cap && phase == 0) ? idx->qsCap.as<float>() : nullptr;
         auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0) {
-#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags, list, cnt, eb, ldE)
+#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), (int)cn, k, kout, idx->id_base, o_ids + c0 * kout, o_d + c0 * kout, o_n + c0, flags, list, cnt, eb, ldE, capv)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \
     case L2: if (v5) WV_EXR(RV, L2, AVX512); else WV_EXR(RV, L2, AVX256); break;   \
