@@ -126,7 +126,7 @@ struct wv_index {
     int64_t rp_pool = 1 << 20;  // pooled replay: candidate blocks per batch (144 B each)
     int pq_adc = 2;             // PQ ADC queries per workgroup: 2 = k_pq_adc2 (b64 LUT pairs), 1 = k_pq_adc
     int qs_force_flag = 0;      // tests: flag every query of the block-key path (exercise the replay)
-    int exact_bm = 0;           // block-major exact distances (rows <= 508 floats): 1 on, 0 off
+    int exact_bm = 1;           // block-major exact distances (rows <= 508 floats): 1 on, 0 off
     int device = 0;
     uint64_t id_base = 0;
     std::string root_path;
