@@ -228,19 +228,72 @@ def cpu_baseline_rq(bits: int, n_sample: int, nq: int, threads: int, n_full: int
     }
 
 
+def verify_sample(workload: str, flat, gen_kind: int, n_total: int, dims: int, B: int, k: int, res, index,
+                  threads: int, bq_r: int = 0, world: int = 1):
+    """The bench checks its own output: a sample of the step's result rows
+    (16 queries spread over the batch; 8 for PQ) against the oracle's exact
+    scan of the regenerated corpus (oracle/scale.c; the reference heap
+    semantics of flat/index.go:578-688), bit-exact ids and distances.
+    Returns {"verified": bool, "checked": n, ...} or None when the workload
+    has no oracle check here (rq: the 10M-row rotational oracle is too large
+    for the host leg)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc  # test infrastructure: the checker, outside the timed region
+    ids, dists, counts = (t.cpu().numpy() for t in res)
+    ids = ids.view(np.uint64)
+    t0 = time.perf_counter()
+    nchk = 8 if workload == "pq" else 16
+    sample = np.unique(np.linspace(0, B - 1, nchk).astype(np.int64))
+    bad = []
+    if flat is not None:
+        metric = orc.METRIC[flat["metric"]]
+        qs = orc.gen_matrix(gen_kind, SEED_QUERY, 0, B, dims)[sample]
+        if metric == orc.COSINE:
+            qs = np.stack([orc.normalize(x) for x in qs])
+        D = orc.gen_dists(gen_kind, SEED_CORPUS, n_total, dims, metric, orc.AVX256, qs, threads)
+        exp = [orc.heap_scan(D[i], k) for i in range(len(sample))]
+        del D
+    elif workload == "bq":
+        qs = orc.gen_matrix(0, SEED_QUERY, 0, B, dims)[sample]
+        oi, od, on = orc.bq_search_gen(0, SEED_CORPUS, n_total, dims, orc.COSINE, orc.AVX256, qs, k, bq_r, threads)
+        exp = [(oi[i, :on[i]], od[i, :on[i]]) for i in range(len(sample))]
+    elif workload == "pq" and world == 1:
+        from concurrent.futures import ThreadPoolExecutor
+        centers, codes = index.pq_centers(), index.pq_codes(n_total)
+        present = np.ones(n_total, np.uint8)
+        dummy = np.zeros(1, np.float32)
+        qs = orc.gen_matrix(2, SEED_QUERY, 0, B, dims)[sample]
+        with ThreadPoolExecutor(min(threads, len(sample))) as ex:
+            exp = list(ex.map(lambda i: orc.pq_flat_search(orc.L2, orc.AVX256, centers, codes, dummy, present, qs[i],
+                                                           k, k, False), range(len(sample))))
+        del codes
+    else:
+        return None
+    for i, q in enumerate(sample):
+        ei, ed = exp[i]
+        c = int(counts[q])
+        if c != len(ei) or not np.array_equal(ids[q, :c], np.asarray(ei, np.uint64)) or \
+                not np.array_equal(np.asarray(dists[q, :c], np.float32).view(np.uint32),
+                                   np.asarray(ed, np.float32).view(np.uint32)):
+            bad.append(int(q))
+    return {"verified": not bad, "checked_queries": [int(x) for x in sample], "mismatched": bad,
+            "against": "oracle exact scan of the regenerated corpus (bit-exact ids and distances)",
+            "seconds": round(time.perf_counter() - t0, 1)}
+
+
 def measured_traffic(workload: str, n_local: int, dims: int, batch: int, kernel: str = None):
-    """HBM bytes per launch of the dominant kernel from the committed PMC pass
-    (profiles/*_pmc_<workload>.json, tools/pmc_traffic.sh) when it was taken on
-    this exact configuration; None otherwise."""
+    """HBM bytes per launch of `kernel` from a committed PMC pass
+    (profiles/*_pmc_*.json, tools/pmc_traffic.sh) taken on this exact
+    configuration and kernel; None otherwise."""
     import glob
     best = None
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{workload}*.json"))):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_*.json"))):
         try:
             rec = json.load(open(path))
         except Exception:
             continue
-        if (rec.get("corpus_rows"), rec.get("dims"), rec.get("query_batch")) == (n_local, dims, batch) and \
-                (kernel is None or rec.get("kernel") == kernel):
+        if (rec.get("corpus_rows"), rec.get("dims"), rec.get("query_batch"), rec.get("kernel")) == \
+                (n_local, dims, batch, kernel):
             best = rec.get("hbm_bytes_per_launch")
     return best
 
@@ -276,6 +329,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the self-check of sampled result rows against the oracle (outside the timed region)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU protocol (ShardedFlatSearch / ShardedBQSearch over RCCL) even at "
                          "WORLD_SIZE 1 (launch under torch.distributed.run): a one-GPU check of the N>1 path")
@@ -380,6 +435,7 @@ def main():
             s = torch.cuda.current_stream(dev).cuda_stream
             _lib.check(lib.wv_index_search_device(index._h, queries.data_ptr(), B, dims, K_, 0, out_ids.data_ptr(),
                                                   out_d.data_ptr(), out_n.data_ptr(), None, s))
+            return out_ids, out_d, out_n
 
     for _ in range(args.warmup):
         step()
@@ -392,8 +448,9 @@ def main():
     if shard and not bq:
         searcher.flagged = 0
     t0 = time.perf_counter()
+    res = None
     for _ in range(args.steps):
-        step()
+        res = step()
         st = index.stats()
         sel_ms.append(st["last_select_ms"])
         tot_ms.append(st["last_total_ms"])
@@ -432,9 +489,12 @@ def main():
     # the exact fp32 path's dominant kernel: the bf16 block-key pass (runtime.hip auto choice)
     sel_kernel = "k_qs_blockkey"
     total_avg = float(np.mean(tot_ms)) if tot_ms else 0.0
+    # the dominant kernel of each workload: its PMC record (matched on kernel
+    # name and configuration) is the only source of `traffic`
+    dom_kernel = ("k_pq_adc2" if pq else "k_bq_blockmin_lds" if bq else
+                  ("k_rq8_dist" if rq_bits == 8 else "k_rq1_dist") if rq_bits else sel_kernel)
     if args.traffic_bytes is None:
-        args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B,
-                                              None if (pq or bq or rq_bits) else sel_kernel)
+        args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B, dom_kernel)
     if rq_bits:
         # dominant kernel k_rq8_dist / k_rq1_dist, timed on the first query
         # group of the batch (search_rq: groups of RQ_QPB multiples whose
@@ -461,7 +521,7 @@ def main():
         f0 = int(index.stats().get("last_group_queries", 0)) or max(1, min(B, (2 << 30) // (ld * 4)))  # timed first group
         lookups = float(f0) * n_local * PQ_SEGMENTS
         achieved = lookups / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
-        roof = {"bound": "lds", "kernel": "k_pq_adc2 (two queries per ds_read_b64)", "achieved": achieved,
+        roof = {"bound": "lds", "kernel": "k_pq_adc2", "achieved": achieved,
                 "peak": LDS_LOOKUP_PEAK_T, "unit": "T lookups/s", "frac": achieved / LDS_LOOKUP_PEAK_T,
                 "frac_of_b32_lookup_rate": achieved / LDS_LOOKUP_B32_T, "launch_ms": sel_avg,
                 "note": "launch_ms = first query group of the batch",
@@ -472,7 +532,7 @@ def main():
         words = (dims + 63) // 64
         ops = 4.0 * B * n_local * words
         achieved = ops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
-        roof = {"bound": "valu", "kernel": "k_bq_blockmin", "achieved": achieved, "peak": VALU_PEAK_TOPS,
+        roof = {"bound": "valu", "kernel": "k_bq_blockmin_lds", "achieved": achieved, "peak": VALU_PEAK_TOPS,
                 "unit": "Tops/s (int32 lane-ops)", "frac": achieved / VALU_PEAK_TOPS, "launch_ms": sel_avg,
                 "hbm_GBps": n_local * words * 8 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
                 "traffic": args.traffic_bytes}
@@ -501,7 +561,7 @@ def main():
     result = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:  # every world size: rank 0, outside the timed region
             try:
                 if rq_bits:
                     cpu = cpu_baseline_rq(rq_bits, min(args.cpu_rows, 200_000), args.cpu_queries or 512,
@@ -521,6 +581,15 @@ def main():
                     cpu = cpu_baseline(rows, nqc, args.cpu_threads, spec)
             except Exception as e:  # baseline failure must not hide the GPU number
                 log(f"cpu baseline failed: {e}")
+        check = None
+        if not args.no_verify:
+            try:
+                check = verify_sample(args.workload, flat, gen_kind, n_total, dims, B, K_, res[:3], index,
+                                      args.cpu_threads, BQ_RESCORE, world)
+                if check is not None:
+                    log(f"self-check: {check}")
+            except Exception as e:
+                check = {"verified": False, "error": repr(e)}
         if rq_bits:
             workload = (f"rq-{rq_bits} (flat rotational quantization) {dims}-d cosine, k={K}, rescore R={BQ_RESCORE}, "
                         f"on the BASELINE configs[2] corpus ({n_total} rows)")
@@ -562,10 +631,14 @@ def main():
                 "replayed_queries": int(replays),
             },
             **({"sharded_equals_single": sharded_check} if sharded_check is not None else {}),
+            "verified": None if check is None else check["verified"],
+            "verify": check,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()  # the other ranks wait for rank 0's host legs
     index.close()
     if shard:
         dist.destroy_process_group()

@@ -88,15 +88,70 @@ def test_c2_full_integer_k100(wv, oracle):
 
 
 def test_c3_full_10m_x_768_bench_path(wv, oracle):
-    """configs[2]: 10M x 768 cosine, k=10, B=2048 through the bench's exact
-    call (wv_index_search_device, default kernel choice); 32 sampled queries
-    against the regenerated-corpus oracle, and the block-key error bound
-    |A_block - min_block E| <= eps(q) on every block of those queries."""
+    """configs[2] exactly as bench.py times it: 10M x 768 cosine, k=10, one
+    batch of B = 8192 queries (32 query groups per block-key launch, the XCD
+    order over 32 * nspans workgroups) through wv_index_search_device, default
+    kernel choice.  64 sampled queries plus every query the exactness proof
+    flagged (those go through the bounded heap replay) against the
+    regenerated-corpus oracle, and the block-key error bound
+    |A_block - min_block E| <= eps(q) on every block of the sampled queries."""
     torch = pytest.importorskip("torch")
     from weaviate_amd import _lib
     lib = _lib.load()
-    n, d, k, B = 10_000_000, 768, 10, 2048
+    n, d, k, B = 10_000_000, 768, 10, 8192
     idx = device_index(wv, torch, "cosine", 0, n, d)
+    qd = torch.empty((B, d), dtype=torch.float32, device="cuda")
+    _lib.check(lib.wv_gen_device(0, 0, 2, 0, B, d, qd.data_ptr(), None))
+    # mode 1 (the shard-candidate form) on the same batch exposes the proof's flags
+    fi = torch.empty((B, k + 1), dtype=torch.int64, device="cuda")
+    fd = torch.empty((B, k + 1), dtype=torch.float32, device="cuda")
+    fn = torch.empty(B, dtype=torch.int32, device="cuda")
+    ff = torch.empty(B, dtype=torch.int32, device="cuda")
+    _lib.check(lib.wv_index_search_device(idx._h, qd.data_ptr(), B, d, k, 1, fi.data_ptr(), fd.data_ptr(),
+                                          fn.data_ptr(), ff.data_ptr(), None))
+    flagged = np.nonzero(ff.cpu().numpy())[0]
+    oi_d = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    od_d = torch.empty((B, k), dtype=torch.float32, device="cuda")
+    on_d = torch.empty(B, dtype=torch.int32, device="cuda")
+    before = idx.stats()["replayed_queries"]
+    _lib.check(lib.wv_index_search_device(idx._h, qd.data_ptr(), B, d, k, 0, oi_d.data_ptr(), od_d.data_ptr(),
+                                          on_d.data_ptr(), None, None))
+    torch.cuda.synchronize()
+    replayed = idx.stats()["replayed_queries"] - before
+    assert replayed == len(flagged), (replayed, len(flagged))
+    ids = oi_d.cpu().numpy().view(np.uint64)
+    dists = od_d.cpu().numpy()
+    counts = on_d.cpu().numpy()
+    spread = np.arange(0, B, B // 64)[:64]
+    sample = np.unique(np.concatenate([spread, flagged]))
+    raw = oracle.gen_matrix(0, 2, 0, B, d)[sample]
+    qn = np.stack([oracle.normalize(x) for x in raw])
+    D = oracle.gen_dists(0, 1, n, d, oracle.COSINE, oracle.AVX256, qn, oracle_threads())
+    worst = 0.0
+    for i, q in enumerate(sample):
+        oi, od = oracle.heap_scan(D[i], k)
+        assert_rows(ids, dists, counts, q, oi, od, "c3")
+        if q in set(spread.tolist()):
+            A, eps = idx.debug_blockkeys(int(q))
+            bmin = D[i][: (n // 32) * 32].reshape(-1, 32).min(axis=1).astype(np.float64)
+            err = np.abs(A[: bmin.size].astype(np.float64) - bmin)
+            worst = max(worst, float(err.max() / eps))
+            assert (err <= eps).all(), f"c3 q{q}: block-key error {err.max()} > eps {eps}"
+    print(f"c3 B={B}: {len(sample)} queries checked ({len(flagged)} flagged -> replayed); "
+          f"max |A_block - min E| / eps = {worst:.4f}")
+    idx.close()
+
+
+def test_c4_bq_shard_6_25m_x_1536(wv, oracle):
+    """configs[3] per GPU as bench.py --workload bq times it: one 6.25M x 1536
+    BQ shard, hamming R=200 + fp32 rescoring, k=10, a B = 2048 batch (8 query
+    groups of 256 in k_bq_blockmin_lds); 24 queries spread over all 8 groups
+    against the regenerated-corpus BQ oracle."""
+    torch = pytest.importorskip("torch")
+    from weaviate_amd import _lib
+    lib = _lib.load()
+    n, d, k, R, B = 6_250_000, 1536, 10, 200, 2048
+    idx = device_index(wv, torch, "cosine", 0, n, d, bq=True, rescore_limit=R)
     qd = torch.empty((B, d), dtype=torch.float32, device="cuda")
     _lib.check(lib.wv_gen_device(0, 0, 2, 0, B, d, qd.data_ptr(), None))
     oi_d = torch.empty((B, k), dtype=torch.int64, device="cuda")
@@ -105,37 +160,63 @@ def test_c3_full_10m_x_768_bench_path(wv, oracle):
     _lib.check(lib.wv_index_search_device(idx._h, qd.data_ptr(), B, d, k, 0, oi_d.data_ptr(), od_d.data_ptr(),
                                           on_d.data_ptr(), None, None))
     torch.cuda.synchronize()
-    ids = oi_d.cpu().numpy().view(np.uint64)
-    dists = od_d.cpu().numpy()
-    counts = on_d.cpu().numpy()
-    sample = np.arange(0, B, B // 32)[:32]
-    raw = oracle.gen_matrix(0, 2, 0, B, d)[sample]
-    qn = np.stack([oracle.normalize(x) for x in raw])
-    D = oracle.gen_dists(0, 1, n, d, oracle.COSINE, oracle.AVX256, qn, oracle_threads())
-    worst = 0.0
+    ids, dists, counts = oi_d.cpu().numpy().view(np.uint64), od_d.cpu().numpy(), on_d.cpu().numpy()
+    sample = np.array([g * 256 + o for g in range(8) for o in (0, 131, 255)])
+    queries = oracle.gen_matrix(0, 2, 0, B, d)[sample]
+    oi, od, on = oracle.bq_search_gen(0, 1, n, d, oracle.COSINE, oracle.AVX256, queries, k, R, oracle_threads())
     for i, q in enumerate(sample):
-        oi, od = oracle.heap_scan(D[i], k)
-        assert_rows(ids, dists, counts, q, oi, od, "c3")
-        A, eps = idx.debug_blockkeys(int(q))
-        bmin = D[i][: (n // 32) * 32].reshape(-1, 32).min(axis=1).astype(np.float64)
-        err = np.abs(A[: bmin.size].astype(np.float64) - bmin)
-        worst = max(worst, float(err.max() / eps))
-        assert (err <= eps).all(), f"c3 q{q}: block-key error {err.max()} > eps {eps}"
-    print(f"c3: max |A_block - min E| / eps = {worst:.4f}")
+        assert_rows(ids, dists, counts, q, oi[i, :on[i]], od[i, :on[i]], "c4")
     idx.close()
 
 
-def test_c4_bq_shard_6_25m_x_1536(wv, oracle):
-    """configs[3] per GPU: one 6.25M x 1536 BQ shard, hamming R=200 + fp32
-    rescoring, k=10; 16 queries against the regenerated-corpus BQ oracle."""
+def test_c5_pq_full_10m_x_960_bench_batch(wv, oracle):
+    """configs[4] as bench.py --workload pq times it: 10M x 960 U[0,1) rows,
+    PQ m=240 x ks=256 trained on the first 100k rows, ADC flat search of a
+    B = 256 batch -- at 10M rows search_pq splits the batch into query groups
+    sized to the free HBM and replays group i on the aux stream beside group
+    i+1's k_pq_adc2.  Codes of sampled rows against the oracle encoder, then 8
+    queries (spread over the groups) against the oracle's flatSearch over the
+    index's full code array."""
     torch = pytest.importorskip("torch")
-    n, d, k, R, nq = 6_250_000, 1536, 10, 200, 16
-    idx = device_index(wv, torch, "cosine", 0, n, d, bq=True, rescore_limit=R)
-    queries = oracle.gen_matrix(0, 2, 0, nq, d)
-    ids, dists, counts = idx.search_by_vector_batch(queries, k)
-    oi, od, on = oracle.bq_search_gen(0, 1, n, d, oracle.COSINE, oracle.AVX256, queries, k, R, oracle_threads())
-    for q in range(nq):
-        assert_rows(ids, dists, counts, q, oi[q, :on[q]], od[q, :on[q]], "c4")
+    from concurrent.futures import ThreadPoolExecutor
+    from weaviate_amd import _lib
+    lib = _lib.load()
+    n, d, m, ks, limit, k, B = 10_000_000, 960, 240, 256, 100_000, 10, 256
+    idx = device_index(wv, torch, "l2-squared", 2, n, d,
+                       pq={"segments": m, "centroids": ks, "trainingLimit": limit, "rescore": False})
+    idx.pq_fit(seed=1)
+    centers = idx.pq_centers()
+    codes = idx.pq_codes(n)
+    rows = np.arange(0, n, n // 64)[:64]
+    data_rows = np.concatenate([oracle.gen_matrix(2, 1, int(r), 1, d) for r in rows])
+    ecodes = np.stack([oracle.pq_encode(centers, x) for x in data_rows])
+    np.testing.assert_array_equal(codes[rows], ecodes)
+    present = np.ones(n, np.uint8)
+    dummy = np.zeros(1, np.float32)
+    queries = oracle.gen_matrix(2, 2, 0, 1024, d)
+    res = {}
+    for nb in (B, 1024):  # the bench's batch, and one that needs several query groups
+        qd = torch.empty((nb, d), dtype=torch.float32, device="cuda")
+        _lib.check(lib.wv_gen_device(0, 2, 2, 0, nb, d, qd.data_ptr(), None))
+        oi_d = torch.empty((nb, k), dtype=torch.int64, device="cuda")
+        od_d = torch.empty((nb, k), dtype=torch.float32, device="cuda")
+        on_d = torch.empty(nb, dtype=torch.int32, device="cuda")
+        _lib.check(lib.wv_index_search_device(idx._h, qd.data_ptr(), nb, d, k, 0, oi_d.data_ptr(), od_d.data_ptr(),
+                                              on_d.data_ptr(), None, None))
+        torch.cuda.synchronize()
+        group = idx.stats()["last_group_queries"]
+        if nb > B:
+            assert 0 < group < nb, f"the multi-group path did not run (group of {group} queries)"
+        res[nb] = (oi_d.cpu().numpy().view(np.uint64), od_d.cpu().numpy(), on_d.cpu().numpy())
+        sample = np.linspace(0, nb - 1, 8).astype(np.int64)
+        with ThreadPoolExecutor(min(8, oracle_threads())) as ex:
+            exp = list(ex.map(lambda q: oracle.pq_flat_search(oracle.L2, 1, centers, codes, dummy, present,
+                                                              queries[q], k, k, False), sample))
+        for i, q in enumerate(sample):
+            assert_rows(*res[nb], q, exp[i][0], exp[i][1], f"c5 B={nb} (groups of {group})")
+    # a query's result does not depend on the batch or group it ran in
+    for a, b in zip(res[B], res[1024]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b)[:B])
     idx.close()
 
 

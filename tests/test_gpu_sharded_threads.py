@@ -1,0 +1,142 @@
+"""GPU: weaviate_amd.sharded.ShardedFlatSearch itself (not a restatement of its
+steps) with every rank a thread on one GPU.  The collectives are an in-process
+stand-in (FakeGroup: all_gather / broadcast through a barrier, same calls as
+torch.distributed), the per-rank engines are real GpuShardBackends over HIP
+indexes.  Covers shards off the block-key path next to shards on it: a shard
+with a non-finite row (phase 1 refused, one-shot local search, replay without
+block keys), an empty shard, and both replay forms (parallel records for
+k < 64, the device-flag chain for k >= 64).  Must equal the oracle's single
+index over the same rows (flat/index.go:578-688)."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+class FakeGroup:
+    """torch.distributed stand-in for ranks that are threads of one process."""
+
+    def __init__(self, world):
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+        self.tl = threading.local()
+
+    def get_rank(self):
+        return self.tl.rank
+
+    def get_world_size(self):
+        return self.world
+
+    def get_backend(self):
+        return "fake"
+
+    def all_gather(self, parts, t):
+        r = self.get_rank()
+        self.slots[r] = t.clone()
+        self.bar.wait()
+        for i in range(self.world):
+            parts[i].copy_(self.slots[i])
+        torch.cuda.synchronize()
+        self.bar.wait()
+
+    def broadcast(self, t, src):
+        r = self.get_rank()
+        if r == src:
+            self.slots[src] = t.clone()
+        self.bar.wait()
+        if r != src:
+            t.copy_(self.slots[src])
+        torch.cuda.synchronize()
+        self.bar.wait()
+
+
+def run_ranks(monkeypatch, backs, q, k):
+    import weaviate_amd.sharded as sh
+    g = FakeGroup(len(backs))
+    monkeypatch.setattr(sh, "dist", g)
+    out, err = [None] * len(backs), []
+
+    def rank_main(r):
+        g.tl.rank = r
+        try:
+            s = sh.ShardedFlatSearch(backs[r], torch.device("cuda", 0))
+            res = s.search(q, k)
+            torch.cuda.synchronize()
+            out[r] = tuple(t.cpu() for t in res)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            err.append(e)
+            g.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(len(backs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not any(t.is_alive() for t in th), "a rank is stuck in a collective"
+    if err:
+        raise err[0]
+    return out
+
+
+@pytest.mark.parametrize("metric,kind,d,k", [("cosine", 0, 96, 10),       # parallel record replay
+                                             ("l2-squared", 1, 32, 10),   # integer ties: many flagged queries
+                                             ("l2-squared", 1, 24, 100)])  # device-flag chain (k >= 64)
+def test_sharded_search_with_off_path_and_empty_shards(wv, oracle, monkeypatch, metric, kind, d, k):
+    per = 3000
+    layout = ["normal", "nonfinite", "empty", "normal"]
+    data = oracle.gen_matrix(kind, 51, 0, per * len(layout), d)
+    data[per + 17, 3] = np.nan  # shard 1 holds a NaN row: off the block-key path
+    queries = oracle.gen_matrix(kind, 52, 0, 160, d)
+    backs, ids_all = [], []
+    from weaviate_amd.sharded import GpuShardBackend
+    for r, kind_r in enumerate(layout):
+        lo = r * per
+        idx = wv.FlatIndex(distance=metric, dims=d, id_base=lo, variant="avx256")
+        if kind_r != "empty":
+            ids = np.arange(lo, lo + per, dtype=np.uint64)
+            idx.add_batch(ids, data[lo:lo + per])
+            ids_all.append(ids)
+        backs.append(GpuShardBackend(idx, 0))
+    q = torch.from_numpy(queries).to("cuda")
+    out = run_ranks(monkeypatch, backs, q, k)
+    ids_all = np.concatenate(ids_all)
+    orc = oracle.OracleFlat(oracle.METRIC[metric], 1, d, per * len(layout))
+    orc.add_batch(ids_all, data[ids_all.astype(np.int64)])
+    for r in range(len(backs)):  # every rank holds the merged result
+        oi, od, on = (t.numpy() for t in out[r])
+        for i in range(len(queries)):
+            rc, ei, ed = orc.search(queries[i], k)
+            assert rc == 0 and on[i] == len(ei), f"rank {r} q{i}"
+            np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), ei, err_msg=f"rank {r} q{i}")
+            np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), ed.view(np.uint32), err_msg=f"rank {r} q{i}")
+    for b in backs:
+        b.index.close()
+
+
+def test_phase2_refused_after_interleaved_add(wv, oracle):
+    """A batch's shard phase 1 ends with any Add / Delete / other query
+    preparation on the index (the keys, eps and query rows it left would be
+    stale): phase 2 is refused instead of reading them."""
+    from weaviate_amd import WeaviateError
+    from weaviate_amd.sharded import GpuShardBackend
+    n, d, k = 4000, 64, 10
+    data = oracle.gen_matrix(0, 53, 0, n + 500, d)
+    idx = wv.FlatIndex(distance="l2-squared", dims=d, variant="avx256")
+    idx.add_batch(np.arange(n, dtype=np.uint64), data[:n])
+    b = GpuShardBackend(idx, 0)
+    q = torch.from_numpy(oracle.gen_matrix(0, 54, 0, 64, d)).to("cuda")
+    for interleave in ("add", "search", "delete"):
+        topA, eps = b.phase1(q, k)
+        if interleave == "add":
+            idx.add_batch(np.arange(n, n + 500, dtype=np.uint64), data[n:])
+        elif interleave == "search":
+            idx.search_by_vector_batch(data[:2], 3)
+        else:
+            idx.delete(5)
+        with pytest.raises(WeaviateError):
+            b.phase2(topA[None], eps[None], k)
+    idx.close()

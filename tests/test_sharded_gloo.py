@@ -236,7 +236,8 @@ class OracleShardBackend:
         return torch.from_numpy(oi.view(np.int64)), torch.from_numpy(od), torch.from_numpy(on)
 
 
-def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath, two_phase=True, replay="parallel"):
+def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath, two_phase=True, replay="parallel",
+            off_rank=-1):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -251,6 +252,12 @@ def _worker(rank, world, port, metric, kind, n, d, nq, k, dup, outpath, two_phas
     b = OracleShardBackend(orc, metric, corpus, rank * per, min(n, (rank + 1) * per))
     if not two_phase:
         b.two_phase = False
+    if rank == off_rank:  # this rank's index is off the block-key path (e.g. a non-finite row)
+        from weaviate_amd._lib import WV_ERR_UNSUPPORTED, WeaviateError
+
+        def off_path(q, k):
+            raise WeaviateError(WV_ERR_UNSUPPORTED, "two-phase shard search: not on the block-key path")
+        b.phase1 = off_path
     if replay != "parallel":  # the chain on device flags, or the list chain
         b.replay_record = None
     if replay == "list":
@@ -278,6 +285,28 @@ def test_sharded_protocol_matches_single_index(tmp_path, oracle, metric, kind, d
     queries = oracle.gen_matrix(kind, 4, 0, nq, d)
     ref = oracle.OracleFlat(metric, 1, d, n)
     ref.add_batch(np.arange(n), corpus)
+    for q in range(nq):
+        rc, ids, dd = ref.search(queries[q], k)
+        c = int(r["counts"][q])
+        np.testing.assert_array_equal(r["ids"][q, :c].astype(np.uint64), ids, err_msg=f"q{q}")
+        np.testing.assert_array_equal(r["dists"][q, :c].view(np.uint32), dd.view(np.uint32))
+
+
+@pytest.mark.parametrize("replay,world,off_rank", [("parallel", 2, 1), ("parallel", 3, 0), ("flags", 3, 2)])
+def test_sharded_protocol_rank_off_block_key_path(tmp_path, oracle, replay, world, off_rank):
+    """One rank's phase 1 is refused (WV_ERR_UNSUPPORTED: its index is off the
+    block-key path): it still joins the phase-1 all-gather with +inf keys and
+    answers with the one-shot local search, the others keep the two phases;
+    no rank waits alone in a collective and the result is the single index's."""
+    n, d, nq, k, metric, kind = 400, 8, 10, 10, 0, 1
+    out = str(tmp_path / "res.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), metric, kind, n, d, nq, k, True, out, True, replay,
+                                      off_rank), nprocs=world, join=True, start_method="spawn")
+    r = np.load(out)
+    corpus = np.concatenate([oracle.gen_matrix(kind, 3, 0, n, d)[: n // 8]] * 8)
+    queries = oracle.gen_matrix(kind, 4, 0, nq, d)
+    ref = oracle.OracleFlat(metric, 1, d, corpus.shape[0])
+    ref.add_batch(np.arange(corpus.shape[0]), corpus)
     for q in range(nq):
         rc, ids, dd = ref.search(queries[q], k)
         c = int(r["counts"][q])

@@ -1114,7 +1114,10 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
                                                     const float* __restrict__ in_hd,
                                                     const int32_t* __restrict__ in_hlen, int extract,
                                                     int out_by_query, int kout, uint64_t* __restrict__ out_ids,
-                                                    float* __restrict__ out_d, int32_t* __restrict__ out_n) {
+                                                    float* __restrict__ out_d, int32_t* __restrict__ out_n,
+                                                    int in_by_query, int raw_by_query,
+                                                    uint64_t* __restrict__ rec_i, float* __restrict__ rec_d,
+                                                    int32_t* __restrict__ rec_n, int rec_cap) {
     // all LDS in the dynamic region (Guideline 17): [k] ids | [64] dists | [k] heap dists | len
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
@@ -1130,10 +1133,12 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
     if (lane == 0) {
         int len = 0;
         if (in_hlen) {
-            len = in_hlen[li];
-            for (int i = 0; i < len; i++) { hid[i] = in_hid[(int64_t)li * k + i]; hd[i] = in_hd[(int64_t)li * k + i]; }
+            const int64_t ir = in_by_query ? q : li;
+            len = in_hlen[ir];
+            for (int i = 0; i < len; i++) { hid[i] = in_hid[ir * k + i]; hd[i] = in_hd[ir * k + i]; }
         }
         *s_len = len;
+        if (rec_n) rec_n[li] = 0;
     }
     __syncthreads();
     const int64_t nblk = (nslots + EBLK - 1) / EBLK;
@@ -1167,8 +1172,15 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
                         mask &= mask - 1;
                         const float dj = s_d[jj];
                         const uint64_t idj = id_base + (uint64_t)(s - lane + jj);
+                        bool ins = true;
                         if (h.len < k) rh_insert(h, idj, dj);
                         else if (h.dist[0] > dj) { uint64_t a; float b; rh_pop(h, &a, &b); rh_insert(h, idj, dj); }
+                        else ins = false;
+                        if (ins && rec_n) {  // the parallel cross-shard replay's record (id order)
+                            const int c = rec_n[li];
+                            if (c < rec_cap) { rec_i[(int64_t)li * rec_cap + c] = idj; rec_d[(int64_t)li * rec_cap + c] = dj; }
+                            rec_n[li] = c < rec_cap ? c + 1 : rec_cap + 1;
+                        }
                     }
                     *s_len = h.len;
                 }
@@ -1189,8 +1201,9 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
             }
             out_n[row] = n < kout ? n : kout;
         } else {
-            for (int i = 0; i < h.len; i++) { out_ids[(int64_t)li * k + i] = h.id[i]; out_d[(int64_t)li * k + i] = h.dist[i]; }
-            out_n[li] = h.len;
+            const int64_t row = raw_by_query ? q : li;
+            for (int i = 0; i < h.len; i++) { out_ids[row * k + i] = h.id[i]; out_d[row * k + i] = h.dist[i]; }
+            out_n[row] = h.len;
         }
     }
 }

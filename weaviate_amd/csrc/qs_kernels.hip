@@ -742,8 +742,9 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
 // The k+1 blocks under M_g each hold a row with E <= M_g + eps_max, so a
 // block of this shard with A > M_g + eps_max + eps cannot hold a global
 // top-(k+1) row; the candidate list (ascending by key) is cut to that prefix.
-// Queries with flag 2 (their own second pass) or more than 4096 gathered
-// values keep the local list.
+// Queries with flag 2 (their own second pass) or more than 1024 gathered
+// values (W * (k+1) > 1024, e.g. k = 127 at 8 ranks) keep the local list:
+// still exact, only without the global cut.
 __global__ __launch_bounds__(256) void k_blk_gthresh(const float* __restrict__ topA_all, const float* __restrict__ eps_all,
                                                      int W, int nq, int k, int metric, const float4* __restrict__ qinfo,
                                                      const float* __restrict__ key, int64_t ldk,

@@ -220,6 +220,14 @@ struct wv_index {
     int gemv_max = 8, gemv_wg = 1024, exact_multi = 1;  // batches up to this many queries take the GEMV select kernel (kver 6)
 };
 
+// The block keys, eps and prepared query rows of the last batch (qs_keys_nq)
+// and a pending sharded phase 1 (qs_phase_nq) describe one batch on one corpus
+// state: an Add, a Delete or another batch's query preparation ends them.
+static void invalidate_batch(wv_index* idx) {
+    idx->qs_keys_nq = 0;
+    idx->qs_phase_nq = 0;
+}
+
 // ---------------------------------------------------------------------------
 // create / destroy / capacity
 // ---------------------------------------------------------------------------
@@ -625,7 +633,7 @@ static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs
         last[ids[i]] = i;
         maxslot = std::max<int64_t>(maxslot, (int64_t)s);
     }
-    idx->qs_keys_nq = 0;
+    invalidate_batch(idx);
     rc = ensure_capacity(idx, maxslot + 1);
     if (rc) return rc;
     std::vector<int64_t> rows;
@@ -695,7 +703,7 @@ extern "C" int wv_index_add_range_device(wv_index* idx, uint64_t first_id, const
         if (rc) return rc;
     }
     const int64_t s0 = (int64_t)s0u;
-    idx->qs_keys_nq = 0;
+    invalidate_batch(idx);
     rc = ensure_capacity(idx, s0 + n);
     if (rc) return rc;
     std::vector<uint32_t> hs((size_t)n);
@@ -718,7 +726,7 @@ extern "C" int wv_index_delete(wv_index* idx, const uint64_t* ids, int64_t n) {
     if (!idx) return set_err(WV_ERR_INVALID, "nil index");
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
-    idx->qs_keys_nq = 0;
+    invalidate_batch(idx);
     bool dirty = false;
     for (int64_t i = 0; i < n; i++) {
         if (ids[i] < idx->id_base) continue;
@@ -914,9 +922,13 @@ static double gamma_n(int n) {
 // (k_replay_scan), in groups bounded by a 2 GiB distance buffer.
 // in_* / raw outputs are [nlist][k] device arrays indexed by list position;
 // extract + out_by_query writes results to row qlist[i] of [nq][kout] arrays.
+// by_query = 1: in-states and raw (non-extracted) outputs are [nq][k] rows
+// indexed by query (qlist[i]) as well; rec_*: record every insertion
+// ([nlist][rec_cap] by list position, count rec_cap + 1 = overflow).
 static int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float* Qn, const int32_t* d_qlist,
                       int nlist, int k, const uint64_t* in_i, const float* in_d, const int32_t* in_n, int extract,
-                      int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on) {
+                      int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on, int by_query = 0,
+                      uint64_t* rec_i = nullptr, float* rec_d = nullptr, int32_t* rec_n = nullptr, int rec_cap = 0) {
     const int64_t nslots = idx->hiwater;
     const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
     int64_t G = std::max<int64_t>(1, std::min<int64_t>(nlist, (2ll << 30) / (ld * 4)));
@@ -957,19 +969,24 @@ static int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const
             HIPCHK(hipGetLastError());
         }
         const bool raw = !extract;
-        const int64_t ooff = (raw || !out_by_query) ? g0 : 0;
+        const int64_t ooff = by_query ? 0 : (raw || !out_by_query) ? g0 : 0;
+        const int64_t ioff = by_query ? 0 : g0;
         k_replay_scan<<<F, 64, lds, s>>>(idx->rE.as<float>(), idx->rB.as<float>(), valid, Qn ? nslots : 0, ld,
-                                         d_qlist + g0, F, k, idx->id_base, in_n ? in_i + g0 * k : nullptr,
-                                         in_n ? in_d + g0 * k : nullptr, in_n ? in_n + g0 : nullptr, extract,
-                                         out_by_query, kout, oi + ooff * (raw ? k : kout),
-                                         od + ooff * (raw ? k : kout), on + ooff);
+                                         d_qlist + g0, F, k, idx->id_base, in_n ? in_i + ioff * k : nullptr,
+                                         in_n ? in_d + ioff * k : nullptr, in_n ? in_n + ioff : nullptr, extract,
+                                         out_by_query || by_query, kout, oi + ooff * (raw ? k : kout),
+                                         od + ooff * (raw ? k : kout), on + ooff, by_query, by_query,
+                                         rec_n ? rec_i + g0 * rec_cap : nullptr, rec_n ? rec_d + g0 * rec_cap : nullptr,
+                                         rec_n ? rec_n + g0 : nullptr, rec_cap);
         HIPCHK(hipGetLastError());
     }
     return WV_OK;
 }
 
 // prepare padded (and for cosine exactly normalised) query rows + norms
+// (overwrites idx->qn: the block keys / shard phase of an earlier batch no longer apply)
 static int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t nq_pad) {
+    invalidate_batch(idx);
     HIPCHK(idx->qn.ensure((size_t)nq_pad * idx->dpad * sizeof(float)));
     HIPCHK(idx->qn2.ensure((size_t)nq_pad * sizeof(float)));
     float* Qn = idx->qn.as<float>();
@@ -1751,7 +1768,8 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         // the worker heap (addResult == insertToHeap) in id order, extracted ascending
         k_replay_scan<<<F, 64, lds_rep, idx->aux>>>(E, Bm, valid, nslots, ld, qlist + g0, F, R, idx->id_base, nullptr,
                                                     nullptr, nullptr, 1, 0, R, idx->ascI.as<uint64_t>() + g0 * R,
-                                                    idx->ascD.as<float>() + g0 * R, idx->ascN.as<int32_t>() + g0);
+                                                    idx->ascD.as<float>() + g0 * R, idx->ascN.as<int32_t>() + g0, 0, 0,
+                                                    nullptr, nullptr, nullptr, 0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
     }
@@ -2104,7 +2122,8 @@ static int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
         k_replay_scan<<<F, 64, lds_rep, idx->aux>>>(Eb[b]->as<float>(), Bb[b]->as<float>(), valid, nslots, ld,
                                                     qlist + g0, F, R, idx->id_base, nullptr, nullptr, nullptr, 1, 0,
                                                     R, idx->ascI.as<uint64_t>() + g0 * R,
-                                                    idx->ascD.as<float>() + g0 * R, idx->ascN.as<int32_t>() + g0);
+                                                    idx->ascD.as<float>() + g0 * R, idx->ascN.as<int32_t>() + g0, 0, 0,
+                                                    nullptr, nullptr, nullptr, 0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
     }
@@ -2233,6 +2252,13 @@ extern "C" int wv_index_rq_distances(wv_index* idx, const float* queries, int64_
 // k < 64) or k_blk_replay (one wave per query).  list/count: device list and
 // its length at counters[1] (or nlist when counters == nullptr); max_list =
 // host bound of the list length (grid sizing).
+// the pooled block-key replay (k_rp_*) serves this k and key row length
+// (the only block-key form that can record insertions)
+static bool blk_pooled(const wv_index* idx, int k, int64_t nb) {
+    const int64_t nch = (nb + RP_CH - 1) / RP_CH;
+    return k < 448 && nch <= RP_MAXCH && ((idx->replay_par == 2 && k < 64) || idx->replay_par == 3);
+}
+
 static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ldk, int64_t nb, const float* eps,
                              const float4* qinfo, const uint32_t* valid, const float* Qn, const int32_t* list,
                              const uint32_t* counters, int nlist, int64_t max_list, int k, int kout, uint64_t* oi,
@@ -2247,7 +2273,7 @@ static int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int
     // many flagged queries with large k (integer data, C2) replay faster in the
     // one-wave kernel, which visits only blocks under the true heap top
     const int RS = k < 64 ? 2 : k < 192 ? 4 : k < 448 ? 8 : 0;
-    if (RS && nch <= RP_MAXCH && ((idx->replay_par == 2 && k < 64) || idx->replay_par == 3)) {
+    if (blk_pooled(idx, k, nb)) {
         // pooled form: bounds + candidate pool (8 waves per query), exact
         // distances over the whole grid, one-wave heap per query
         const int64_t pool_cap = idx->rp_pool;
@@ -2482,7 +2508,11 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
                                                                   idx->qsCand.as<uint32_t>(), L, idx->qsNc.as<int32_t>(),
                                                                   idx->qsEps.as<float>(), flags);
         const size_t bm_lds = (size_t)32 * (idx->dpad + 4) * sizeof(float);
-        if (idx->exact_bm && bm_lds <= 64 * 1024 && nb < (1ll << 31)) {
+        // (bmE holds cn*L*32 floats: above a 4 GiB budget, or past the 2^23
+        // queries k_inv_scatter's packed (q << 9 | j) can name, the
+        // candidate-major k_blk_exact computes the distances itself)
+        if (idx->exact_bm && bm_lds <= 64 * 1024 && nb < (1ll << 31) && cn < (1ll << 23) &&
+            (int64_t)cn * L * 32 * 4 <= (4ll << 30)) {
             // block-major exact distances: invert the candidate lists per block
             const int64_t ldE = (int64_t)L * 32;
             HIPCHK(idx->bmCnt.ensure((size_t)nb * sizeof(uint32_t)));
@@ -3062,7 +3092,6 @@ extern "C" int wv_index_replay_flags_device(wv_index* idx, const float* d_querie
                                             const int32_t* d_flags, const uint64_t* d_in_ids, const float* d_in_dists,
                                             const int32_t* d_in_len, int32_t extract, uint64_t* d_out_ids,
                                             float* d_out_dists, int32_t* d_out_len, void* stream) {
-    (void)d_queries;
     if (!idx) return set_err(WV_ERR_INVALID, "nil index");
     if (k <= 0 || nq < 0 || !d_flags || !d_out_ids || !d_out_dists || !d_out_len)
         return set_err(WV_ERR_INVALID, "invalid arguments");
@@ -3073,14 +3102,33 @@ extern "C" int wv_index_replay_flags_device(wv_index* idx, const float* d_querie
     const bool have_data = idx->dims != 0 && idx->npresent > 0;
     if (have_data && d != idx->dims)
         return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
-    if (!have_data || idx->qs_keys_nq != nq)
-        return set_err(WV_ERR_UNSUPPORTED, "replay_flags: no block keys of this batch");
     HIPCHK(idx->flCtr.ensure(2 * sizeof(uint32_t)));
     HIPCHK(idx->qsList.ensure((size_t)nq * sizeof(int32_t)));
     HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
     k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(d_flags, (int)nq, idx->qsList.as<int32_t>(),
                                                               idx->flCtr.as<uint32_t>(), 0);
     HIPCHK(hipGetLastError());
+    if (!have_data || idx->qs_keys_nq != nq) {
+        // no block keys of this batch (empty shard, non-finite rows, k or batch
+        // off the block-key path): every row's exact distance + the id-ordered
+        // heap (run_replay, states and results by query); one host sync for the
+        // list length
+        uint32_t nl = 0;
+        HIPCHK(hipMemcpyAsync(&nl, idx->flCtr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (nl == 0) return WV_OK;
+        const float* Qn = nullptr;
+        if (have_data) {
+            int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QB));
+            if (rc) return rc;
+            Qn = idx->qn.as<float>();
+        }
+        int rc = run_replay(idx, s, idx->present, Qn, idx->qsList.as<int32_t>(), (int)nl, k, d_in_ids, d_in_dists,
+                            d_in_len, extract, 1, k, d_out_ids, d_out_dists, d_out_len, 1);
+        if (rc) return rc;
+        if (!stream) HIPCHK(hipStreamSynchronize(s));
+        return WV_OK;
+    }
     int rc = launch_blk_replay(idx, s, idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb, idx->qsEps.as<float>(),
                                idx->qsInfo.as<float4>(), idx->present, idx->qn.as<float>(), idx->qsList.as<int32_t>(),
                                idx->flCtr.as<uint32_t>(), 0, nq, k, k, d_out_ids, d_out_dists, d_out_len, d_in_ids,
@@ -3097,7 +3145,6 @@ extern "C" int wv_index_replay_record_device(wv_index* idx, const float* d_queri
                                              const int32_t* d_qlist, int32_t nlist, const uint64_t* d_in_ids,
                                              const float* d_in_dists, const int32_t* d_in_len, int32_t cap,
                                              uint64_t* d_rec_ids, float* d_rec_dists, int32_t* d_rec_n, void* stream) {
-    (void)d_queries;
     if (!idx) return set_err(WV_ERR_INVALID, "nil index");
     if (k <= 0 || nlist < 0 || cap < 1) return set_err(WV_ERR_INVALID, "invalid arguments");
     if (nlist == 0) return WV_OK;
@@ -3113,10 +3160,21 @@ extern "C" int wv_index_replay_record_device(wv_index* idx, const float* d_queri
     }
     if (d != idx->dims)
         return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
-    if (idx->qs_keys_nq != nq) return set_err(WV_ERR_UNSUPPORTED, "replay_record: no block keys of this batch");
     HIPCHK(idx->hI.ensure((size_t)nlist * k * sizeof(uint64_t)));
     HIPCHK(idx->hD.ensure((size_t)nlist * k * sizeof(float)));
     HIPCHK(idx->hN.ensure((size_t)nlist * sizeof(int32_t)));
+    if (idx->qs_keys_nq != nq || !blk_pooled(idx, k, idx->qs_last_nb)) {
+        // no block keys of this batch (or k outside the pooled replay): the
+        // all-rows exact replay records the same insertions
+        int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QB));
+        if (rc) return rc;
+        rc = run_replay(idx, s, idx->present, idx->qn.as<float>(), d_qlist, nlist, k, d_in_ids, d_in_dists, d_in_len, 0,
+                        0, k, idx->hI.as<uint64_t>(), idx->hD.as<float>(), idx->hN.as<int32_t>(), 0, d_rec_ids,
+                        d_rec_dists, d_rec_n, cap);
+        if (rc) return rc;
+        if (!stream) HIPCHK(hipStreamSynchronize(s));
+        return WV_OK;
+    }
     int rc = launch_blk_replay(idx, s, idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb, idx->qsEps.as<float>(),
                                idx->qsInfo.as<float4>(), idx->present, idx->qn.as<float>(), d_qlist, nullptr, nlist,
                                nlist, k, k, idx->hI.as<uint64_t>(), idx->hD.as<float>(), idx->hN.as<int32_t>(), d_in_ids,

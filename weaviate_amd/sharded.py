@@ -297,18 +297,29 @@ class ShardedFlatSearch:
         return torch.stack(parts)
 
     def _local(self, q: torch.Tensor, k: int):
-        """Phases 1-2 (or the one-shot local search) -> the rank's lists."""
+        """Phases 1-2 (or the one-shot local search) -> the rank's lists.
+
+        Every rank takes part in the phase-1 all-gather, also a rank whose
+        index is off the block-key path (non-finite rows, an empty shard, k or
+        a batch the path does not take): it contributes +inf keys and eps 0 --
+        no bound rows, so the global (k+1)-th key of the other ranks stays a
+        valid cut (fewer sources only weaken it) -- and answers with the
+        one-shot local search."""
         if getattr(self.b, "two_phase", False):
+            off = False
             try:
                 topA, eps = self.b.phase1(q, k)
-            except Exception as e:  # not on the block-key path: one-shot local search
+            except Exception as e:
                 from ._lib import WeaviateError, WV_ERR_UNSUPPORTED
                 if not (isinstance(e, WeaviateError) and e.code == WV_ERR_UNSUPPORTED):
                     raise
-            else:
-                g = self._all_gather(torch.cat([topA, eps[:, None]], 1))  # [W, nq, k+2]
-                gA, gE = g[..., : k + 1].contiguous(), g[..., k + 1].contiguous()
-                self._bounds = (gA, gE)
+                off = True
+                topA = torch.full((q.shape[0], k + 1), float("inf"), dtype=torch.float32, device=q.device)
+                eps = torch.zeros(q.shape[0], dtype=torch.float32, device=q.device)
+            g = self._all_gather(torch.cat([topA, eps[:, None]], 1))  # [W, nq, k+2]
+            gA, gE = g[..., : k + 1].contiguous(), g[..., k + 1].contiguous()
+            self._bounds = (gA, gE)
+            if not off:
                 return self.b.phase2(gA, gE, k)
         return self.b.local_search(q, k)
 
