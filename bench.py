@@ -328,7 +328,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--dims", type=int, default=None,
+                    help="exact flat workloads: override the row width (e.g. 1024 / 1536, the block-key w4 kernel)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--option", action="append", default=[],
+                    help="index option key=value (wv_index_set_option), e.g. qs_w4=1; repeatable")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the self-check of sampled result rows against the oracle (outside the timed region)")
     ap.add_argument("--sharded", action="store_true",
@@ -368,6 +372,9 @@ def main():
     pq = args.workload == "pq"
     rq_bits = {"rq8": 8, "rq1": 1}.get(args.workload, 0)
     flat = FLAT.get(args.workload)  # exact fp32 flat search (c1 / c2 / c3)
+    if flat is not None and args.dims is not None and args.dims != flat["d"]:
+        flat = dict(flat, d=args.dims, name=flat["name"].replace(f"x {flat['d']} ", f"x {args.dims} ")
+                    + f" at d={args.dims}")
     if (pq or rq_bits) and world > 1:
         raise SystemExit(f"--workload {args.workload}: sharded search is not available yet (1 GPU)")
     dims = BQ_DIMS if bq else PQ_DIMS if pq else flat["d"] if flat else DIMS
@@ -391,6 +398,9 @@ def main():
                          rq={"bits": rq_bits} if rq_bits else None,
                          pq={"segments": PQ_SEGMENTS, "centroids": PQ_CENTROIDS, "trainingLimit": PQ_TRAIN,
                              "rescore": False} if pq else None)
+    for kv in args.option:
+        key, val = kv.split("=", 1)
+        index.set_option(key, int(val))
     index.reserve(n_local)
     chunk = 1_000_000
     stage = torch.empty((min(chunk, max(n_local, 1)), dims), dtype=torch.float32, device=dev)
@@ -626,7 +636,8 @@ def main():
                 "k": K_,
                 "query_batch": B,
                 "parallelism": f"corpus sharded over {world} GPU(s), contiguous id ranges"
-                               + ((", R-heap replay chained over RCCL broadcasts + all-gather rescoring" if bq
+                               + ((", R-heap replay in one parallel hop (all-gathered block-minimum bounds, "
+                                   "recorded insertions, on-device merge) + all-gather rescoring" if bq
                                    else ", RCCL all-gather merge") if world > 1 else ""),
                 "replayed_queries": int(replays),
             },

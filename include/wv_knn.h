@@ -329,6 +329,21 @@ int wv_index_bq_rescore(wv_index *idx, const uint64_t *d_ids, const int32_t *d_l
 int wv_bq_final(int32_t device, int64_t nq, int32_t R, int32_t k, int32_t world, uint64_t id_stride,
                 const uint64_t *d_ids, const int32_t *d_len, const float *d_E, uint64_t *d_out_ids, float *d_out_dists,
                 int32_t *d_out_counts, void *stream);
+/* Parallel form of step 2 (replaces the serial R-heap chain of
+ * flat/index.go:470-487 across shards): wv_index_bq_bounds gives per query the
+ * R smallest 256-row block minima of this shard ([nq][R] ascending, +inf
+ * padded; each the exact hamming distance of one distinct row).  After an
+ * all-gather, shard r >= 1 replays from a full heap of R copies of T_r (the
+ * R-th smallest bound of the shards before it, >= the real heap top at its
+ * first row) and records every insertion in id order
+ * (wv_index_bq_replay_record: d_rec_* [nq][cap], count cap + 1 = overflow);
+ * shard 0 runs wv_index_bq_replay (pop = 0).  wv_heap_merge_records (k = R)
+ * applies the records on shard 0's states = the chain's final heaps, extracted
+ * ascending (pop order reversed). */
+int wv_index_bq_bounds(wv_index *idx, float *d_out, void *stream);
+int wv_index_bq_replay_record(wv_index *idx, const uint64_t *d_in_ids, const float *d_in_dists,
+                              const int32_t *d_in_len, int32_t cap, uint64_t *d_rec_ids, float *d_rec_dists,
+                              int32_t *d_rec_n, void *stream);
 
 /* Merge shard-local candidate lists (mode-1 search outputs of G shards, each
  * [nq x (k+1)], gathered shard-major on this device) into the final top-k by
@@ -412,9 +427,10 @@ int wv_lsm_segment_scan(const char *path, int32_t validate_checksum, int64_t *no
  * (flat/index.go:236-282, 867-1033): segments of the vectors bucket, oldest
  * first; key = big-endian uint64 id, value = d little-endian float32
  * (flat/index.go:204-208, 317-336).  Newest entry per key wins, tombstones
- * delete.  Live vectors are normalised/encoded and uploaded exactly as by
- * wv_index_add_batch (compressed codes are re-derived from the fp32 values,
- * which the BQ/RQ encoders determine uniquely).  out[3] (may be NULL) = live
+ * delete.  Live vectors are uploaded as stored (the bucket already holds the
+ * values Add wrote, normalised for cosine: PostStartup reads them unchanged);
+ * the compressed codes are re-derived from those fp32 values, which the
+ * BQ/RQ/PQ encoders determine uniquely.  out[3] (may be NULL) = live
  * vectors uploaded, tombstoned keys, nodes read.  AlreadyIndexed becomes the
  * live count (flat/index.go:278-279). */
 int wv_index_load_segments(wv_index *idx, const char *const *paths, int32_t n_paths, int32_t validate_checksum,

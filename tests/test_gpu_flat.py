@@ -208,20 +208,33 @@ def test_search_by_vector_distance(wv, oracle):
     assert len(ids) == 31
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("kernel", [0, 3, 6, 7])
 @pytest.mark.parametrize("metric,kind,n,d,k", [("cosine", 0, 9000, 768, 10), ("l2-squared", 0, 7000, 96, 24),
-                                               ("dot", 1, 5000, 64, 5)])
+                                               ("dot", 1, 5000, 64, 5), ("cosine", 0, 3000, 2048, 10)])
 def test_select_kernel_variants(wv, oracle, kernel, metric, kind, n, d, k):
-    """Every select kernel (1-6 legacy f32 / bf16x3 / GEMV, 7 = block keys)
-    against the oracle on every query."""
+    """Every select path (0 auto, 3 the f32 MFMA select, 6 the GEMV select,
+    7 block keys; d = 2048 has no block-key planes: 7 and 0 take the f32
+    select) against the oracle on every query."""
     data = gen(oracle, kind, 81, n, d)
     queries = gen(oracle, kind, 82, 300, d)   # > 2 query blocks, ragged last block
-    idx, orc = build_pair(wv, oracle, metric, "avx256", data,
-                          options={"bf3_planes": 1} if kernel in (4, 5) else None)
+    idx, orc = build_pair(wv, oracle, metric, "avx256", data)
     idx.set_option("kernel", kernel)
     ids, dists, counts = idx.search_by_vector_batch(queries, k)
     for qi in range(len(queries)):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
+    idx.close()
+
+
+def test_removed_select_kernels_rejected(wv, oracle):
+    """The round-1 select kernels (1, 2: f32 tiles; 4, 5: bf16x3) were removed:
+    the option refuses them, and their bf16x3 planes option is gone."""
+    idx = wv.FlatIndex(distance="cosine")
+    for kernel in (1, 2, 4, 5, 8):
+        with pytest.raises(wv.WeaviateError, match="kernel must be"):
+            idx.set_option("kernel", kernel)
+    with pytest.raises(wv.WeaviateError):
+        idx.set_option("bf3_planes", 1)
+    idx.close()
 
 
 @pytest.mark.parametrize("metric,kind,n,d,k,nq", [
@@ -329,24 +342,24 @@ def test_bq_generic_kernels_equal_lds_kernels(wv, oracle):
 
 
 @pytest.mark.parametrize("metric,kind,d", [("cosine", 0, 768), ("l2-squared", 0, 128), ("dot", 0, 300),
-                                           ("l2-squared", 2, 960)])
-def test_bf16x3_error_within_proof_bound(wv, oracle, metric, kind, d):
-    """The approximate distances of the bf16x3 select kernel (candidates A)
-    stay within the eps the exactness proof uses."""
+                                           ("l2-squared", 2, 2048)])
+def test_f32_select_error_within_proof_bound(wv, oracle, metric, kind, d):
+    """The approximate distances of the f32 MFMA select kernel (candidates A,
+    kernel 3: the fallback above 1536 dims) stay within the eps the
+    exactness proof uses."""
     n = 20000
     data = gen(oracle, kind, 91, n, d)
     queries = gen(oracle, kind, 92, 256, d)
     idx = wv.FlatIndex(distance=metric, variant="avx256")
-    idx.set_option("bf3_planes", 1)
     idx.add_batch(np.arange(n, dtype=np.uint64), data)
-    idx.set_option("kernel", 5)
+    idx.set_option("kernel", 3)
     idx.search_by_vector_batch(queries, 10)
     A, E, I, eps = idx.debug_candidates(len(queries))
     ok = I != 0xFFFFFFFF
     err = np.abs(A[ok].astype(np.float64) - E[ok].astype(np.float64))
     bound = np.broadcast_to(eps[:, None], A.shape)[ok]
     ratio = (err / bound).max()
-    print(f"bf16x3 max |A-E| / eps = {ratio:.4f}")
+    print(f"f32 select max |A-E| / eps = {ratio:.4f}")
     assert (err <= bound).all(), f"max err/eps = {ratio}"
     idx.close()
 
@@ -417,3 +430,39 @@ def test_block_major_exact_equals_oracle(wv, oracle, metric, kind, variant, n, d
         exp = orc.search(queries[qi], k)
         for ids, dists, counts in res:
             assert_same(exp, ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} k{k} q{qi}")
+
+
+@pytest.mark.parametrize("metric,kind,variant,n,d,k,options", [
+    ("cosine", 0, "avx256", 20000, 1024, 10, None),     # voyage-3 width
+    ("l2-squared", 0, "avx512", 12000, 1536, 10, None),
+    ("l2-squared", 1, "avx256", 12000, 1024, 100, None),  # integer data: ties -> the keyed replay
+    ("dot", 0, "avx256", 9000, 800, 24, None),           # dpb 1024: zero-padded columns
+    ("cosine", 0, "avx256", 8000, 1030, 10, None),       # dpb 1536: 506 zero columns
+    ("cosine", 0, "avx512", 15000, 1536, 100, None),
+    ("l2-squared", 2, "avx256", 10000, 1100, 10, None),  # dpb 1536
+])
+def test_block_keys_above_768_dims(wv, oracle, metric, kind, variant, n, d, k, options):
+    """768 < d <= 1536: k_qs_blockkey_w4 (one wave per SIMD, 128-query
+    workgroups, two column halves per ring step) feeds the same selection /
+    exact / replay pipeline.  Bit-exact against the oracle for every query,
+    and its block keys within the proof's eps of the exact block minima."""
+    data = gen(oracle, kind, 61, n, d)
+    queries = gen(oracle, kind, 62, 160, d)
+    idx, orc = build_pair(wv, oracle, metric, variant, data, options=options)
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"q{qi}")
+    sample = [0, 57, 128, 159]
+    qs = queries[sample]
+    if metric == "cosine":
+        qs = np.stack([oracle.normalize(x) for x in qs])
+    D = oracle.gen_dists(kind, 61, n, d, oracle.METRIC[metric], VARIANTS[variant], qs, 8)
+    worst = 0.0
+    for i, q in enumerate(sample):
+        A, eps = idx.debug_blockkeys(q)  # raises unless the block-key path ran
+        bmin = D[i][: (n // 32) * 32].reshape(-1, 32).min(axis=1).astype(np.float64)
+        err = np.abs(A[: bmin.size].astype(np.float64) - bmin)
+        worst = max(worst, float(err.max() / eps))
+        assert (err <= eps).all(), f"q{q}: block-key error {err.max()} > eps {eps}"
+    print(f"d={d}: max |A_block - min E| / eps = {worst:.4f}")
+    idx.close()

@@ -54,9 +54,13 @@ def test_pq_fit_codes_distance_match_oracle(wv, oracle, metric, kind, n, d, m, k
     ("dot", 0, False, 10, -1),
     ("l2-squared", 1, True, 7, 40),     # integer data: ADC ties -> heap order
     ("l2-squared", 1, False, 20, -1),
+    ("cosine", 0, True, 10, 40),        # worker heap limit 40: the candidate path with rescoring
 ])
-@pytest.mark.parametrize("adc,nq", [(2, 16), (2, 15), (1, 16)])  # k_pq_adc2 (odd list: one single-query block), k_pq_adc
-def test_pq_search_matches_oracle(wv, oracle, metric, kind, rescore, k, rl, adc, nq):
+# cand 1: block minima + candidate blocks + exact ADC of their rows (k_pq_cand; ties flagged
+# to the replay), cand 0: the full ADC matrix + replay; adc 2: k_pq_adc2 (odd list: one
+# single-query block), adc 1: k_pq_adc
+@pytest.mark.parametrize("adc,nq,cand", [(2, 16, 1), (2, 15, 1), (2, 16, 0), (1, 16, 0)])
+def test_pq_search_matches_oracle(wv, oracle, metric, kind, rescore, k, rl, adc, nq, cand):
     n, d, m, ks = 5000, 32, 8, 32
     data = gen(oracle, kind, 71, n, d)
     idx = wv.FlatIndex(distance=metric, variant="avx256", rescore_limit=rl,
@@ -64,6 +68,7 @@ def test_pq_search_matches_oracle(wv, oracle, metric, kind, rescore, k, rl, adc,
     idx.add_batch(np.arange(n, dtype=np.uint64), data)
     idx.pq_fit(seed=77)
     idx.set_option("pq_adc", adc)
+    idx.set_option("pq_cand", cand)
     centers = idx.pq_centers()
     codes = idx.pq_codes(n)
     om = oracle.METRIC[metric]

@@ -140,3 +140,78 @@ def test_phase2_refused_after_interleaved_add(wv, oracle):
         with pytest.raises(WeaviateError):
             b.phase2(topA[None], eps[None], k)
     idx.close()
+
+
+def run_bq_ranks(monkeypatch, backs, q, k, id_stride):
+    import weaviate_amd.sharded as sh
+    g = FakeGroup(len(backs))
+    monkeypatch.setattr(sh, "dist", g)
+    out, paths, err = [None] * len(backs), [None] * len(backs), []
+
+    def rank_main(r):
+        g.tl.rank = r
+        try:
+            s = sh.ShardedBQSearch(backs[r], torch.device("cuda", 0), id_stride)
+            res = s.search(q, k)
+            torch.cuda.synchronize()
+            out[r] = tuple(t.cpu() for t in res)
+            paths[r] = s.path
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            err.append(e)
+            g.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(len(backs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not any(t.is_alive() for t in th), "a rank is stuck in a collective"
+    if err:
+        raise err[0]
+    return out, paths
+
+
+@pytest.mark.parametrize("shards,metric,kind,per,d,k,rl,path", [
+    # the bounds T_r come from 256-row block minima: a finite, useful T_r needs
+    # shards of several R blocks (C4: 24k blocks of a 6.25M-row shard at R = 200)
+    (3, "cosine", 0, 52000, 1536, 10, 40, "parallel"),    # C4's width
+    (4, "l2-squared", 0, 20000, 256, 10, 16, "parallel"),
+    (2, "cosine", 1, 9000, 96, 10, 30, None)])           # integer data: ties (records may overflow -> chain)
+def test_sharded_bq_parallel_replay(wv, oracle, monkeypatch, shards, metric, kind, per, d, k, rl, path):
+    """ShardedBQSearch with GpuBQShardBackends as threads: the R-heap of
+    searchByVectorQuantized (flat/index.go:460-532) across the shards in one
+    parallel hop (wv_index_bq_bounds -> all-gather -> k copies of T_r ->
+    wv_index_bq_replay_record -> all-gather -> wv_heap_merge_records), then
+    rescoring and the final heap.  Must equal the single BQ index and the
+    oracle exactly, on every rank."""
+    from weaviate_amd.sharded import GpuBQShardBackend
+    n = per * shards
+    data = oracle.gen_matrix(kind, 71, 0, n, d)
+    queries = oracle.gen_matrix(kind, 72, 0, 300, d)
+    backs = []
+    for r in range(shards):
+        lo = r * per
+        idx = wv.FlatIndex(distance=metric, bq=True, rescore_limit=rl, id_base=lo, variant="avx256")
+        idx.add_batch(np.arange(lo, lo + per, dtype=np.uint64), data[lo:lo + per])
+        backs.append(GpuBQShardBackend(idx, 0))
+    q = torch.from_numpy(queries).to("cuda")
+    out, paths = run_bq_ranks(monkeypatch, backs, q, k, per)
+    if path is not None:
+        assert paths == [path] * shards, paths
+    single = wv.FlatIndex(distance=metric, bq=True, rescore_limit=rl, variant="avx256")
+    single.add_batch(np.arange(n, dtype=np.uint64), data)
+    si, sd, sn = single.search_by_vector_batch(queries, k)
+    orc = oracle.OracleFlatBQ(oracle.METRIC[metric], 1, d, n, rl)
+    orc.add_batch(np.arange(n), data)
+    for r in range(shards):
+        oi, od, on = (t.numpy() for t in out[r])
+        for i in range(len(queries)):
+            assert on[i] == sn[i], f"rank {r} q{i}"
+            np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), si[i, :sn[i]], err_msg=f"rank {r} q{i}")
+            np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), sd[i, :sn[i]].view(np.uint32))
+    for i in range(0, len(queries), 37):
+        rc, ids, dd = orc.search(queries[i], k)
+        np.testing.assert_array_equal(out[0][0].numpy()[i, :len(ids)].astype(np.uint64), ids, err_msg=f"q{i} vs oracle")
+    for b in backs:
+        b.index.close()
+    single.close()

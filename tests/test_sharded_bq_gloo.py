@@ -92,6 +92,68 @@ class OracleBQShardBackend:
             on[i] = n
         return torch.from_numpy(oi), torch.from_numpy(od), torch.from_numpy(on)
 
+    # -- parallel form: block-minimum bounds, recorded replay, record merge --
+    def bq_bounds(self):
+        R = self.R(self.k)
+        nq = self.q.shape[0]
+        out = np.full((nq, R), np.inf, np.float32)
+        for i in range(nq):
+            d_ = np.array([self.o.hamming_bitwise(self.codes[s], self.qc[i]) for s in range(self.begin, self.end)],
+                          np.float32)
+            mins = np.array([d_[b:b + 256].min() for b in range(0, len(d_), 256)], np.float32)
+            srt = np.sort(mins)[:R]
+            out[i, :len(srt)] = srt
+        return torch.from_numpy(out)
+
+    def bq_replay_record(self, state, cap):
+        lib = self.o.lib()
+        R = self.R(self.k)
+        nq = self.q.shape[0]
+        ri = np.zeros((nq, cap), np.int64)
+        rd = np.zeros((nq, cap), np.float32)
+        rn = np.zeros(nq, np.int32)
+        for i in range(nq):
+            hid, hd, h = self._heap(R)
+            ln = int(state[2][i])
+            hid[:ln] = state[0][i, :ln].numpy().view(np.uint64)
+            hd[:ln] = state[1][i, :ln].numpy()
+            h.len = ln
+            n = 0
+            for s in range(self.begin, self.end):
+                e = self.o.hamming_bitwise(self.codes[s], self.qc[i])
+                if h.len < R or hd[0] > e:
+                    lib.or_insert_to_heap(C.byref(h), R, s, e)
+                    if n < cap:
+                        ri[i, n], rd[i, n] = s, e
+                    n += 1
+            rn[i] = cap + 1 if n > cap else n
+        return torch.from_numpy(ri), torch.from_numpy(rd), torch.from_numpy(rn)
+
+    def merge_records(self, world, k, cap, st, rec):
+        lib = self.o.lib()
+        si, sd, sn = (t.numpy() for t in st)
+        rids, rds, rns = (t.numpy() for t in rec)
+        nl = len(sn)
+        oi = np.zeros((nl, k), np.int64)
+        od = np.zeros((nl, k), np.float32)
+        on = np.zeros(nl, np.int32)
+        un = np.zeros(nl, np.int32)
+        for li in range(nl):
+            hid, hd, h = self._heap(k)
+            h.len = int(sn[li])
+            hid[:h.len] = si[li, :h.len].view(np.uint64)
+            hd[:h.len] = sd[li, :h.len]
+            for r in range(1, world):
+                m = int(rns[r, li])
+                if m > cap:
+                    un[li] = 1
+                    continue
+                for j in range(m):
+                    lib.or_insert_to_heap(C.byref(h), k, int(rids[r, li, j]), float(rds[r, li, j]))
+            n = lib.or_extract_heap(C.byref(h), oi[li].view(np.uint64).ctypes.data_as(self.o.pu), self.o.f(od[li]))
+            on[li] = n
+        return torch.from_numpy(oi), torch.from_numpy(od), torch.from_numpy(on), torch.from_numpy(un)
+
     def bq_rescore(self, ids, ln):
         ids, ln = ids.numpy(), ln.numpy()
         E = np.zeros(ids.shape, np.float32)
@@ -125,7 +187,7 @@ class OracleBQShardBackend:
         return torch.from_numpy(oi), torch.from_numpy(od), torch.from_numpy(on)
 
 
-def _worker(rank, world, port, metric, kind, n, d, nq, k, rl, outpath):
+def _worker(rank, world, port, metric, kind, n, d, nq, k, rl, outpath, parallel=True):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -136,21 +198,31 @@ def _worker(rank, world, port, metric, kind, n, d, nq, k, rl, outpath):
     queries = orc.gen_matrix(kind, 6, 0, nq, d)
     per = (n + world - 1) // world
     b = OracleBQShardBackend(orc, metric, corpus, rank * per, min(n, (rank + 1) * per), rl)
+    if not parallel:  # the serial R-heap chain
+        b.bq_replay_record = None
     s = ShardedBQSearch(b, torch.device("cpu"), per)
     oi, od, on = s.search(torch.from_numpy(queries), k)
     if rank == 0:
-        np.savez(outpath, ids=oi.numpy(), dists=od.numpy(), counts=on.numpy())
+        np.savez(outpath, ids=oi.numpy(), dists=od.numpy(), counts=on.numpy(), path=np.array(s.path))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,metric,kind,d,rl", [(2, 2, 0, 130, 40), (3, 0, 0, 64, 25), (2, 2, 1, 70, 30),
-                                                   (3, 1, 2, 100, -1)])
-def test_sharded_bq_matches_single_index(tmp_path, oracle, world, metric, kind, d, rl):
-    n, nq, k = 450, 6, 10
+@pytest.mark.parametrize("world,metric,kind,d,rl,n,parallel", [
+    (2, 2, 0, 130, 40, 450, False), (3, 0, 0, 64, 25, 450, False), (2, 2, 1, 70, 30, 450, False),
+    (3, 1, 2, 100, -1, 450, False),
+    # parallel: each shard needs >= R 256-row blocks for a finite bound T_r
+    (2, 2, 0, 130, -1, 6000, True), (3, 0, 0, 64, 12, 9600, True), (4, 2, 1, 24, -1, 11000, True)])
+def test_sharded_bq_matches_single_index(tmp_path, oracle, world, metric, kind, d, rl, n, parallel):
+    """parallel: the one-hop recorded replay (block-minimum bounds, records,
+    merge); else the serial chain.  kind 1 (integer data) at d = 24: hamming
+    ties everywhere (records may overflow their cap: then the chain decides)."""
+    nq, k = 6, 10
     out = str(tmp_path / "res.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), metric, kind, n, d, nq, k, rl, out), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), metric, kind, n, d, nq, k, rl, out, parallel),
+                       nprocs=world, join=True, start_method="spawn")
     r = np.load(out)
+    if not parallel or kind != 1:
+        assert str(r["path"]) == ("parallel" if parallel else "chain")
     corpus = oracle.gen_matrix(kind, 5, 0, n, d)
     queries = oracle.gen_matrix(kind, 6, 0, nq, d)
     ref = oracle.OracleFlatBQ(metric, 1, d, n, rl)

@@ -5,7 +5,7 @@ TAG=${1:-r}; shift
 BARGS="$@"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/$TAG; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
+timeout -k 10 840 python -u -m pytest tests -m gpu -x -v --durations=15 --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
 echo "gpu tests rc=$rc"; tail -3 $O/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py $BARGS > $O/bench.json 2> $O/bench.err; rc=$?

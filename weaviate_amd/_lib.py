@@ -115,6 +115,8 @@ SIGNATURES = {
     "wv_index_debug_blockkeys": (C.c_int, [P, i64, pf32, pf32, C.POINTER(C.c_int64)]),
     "wv_index_bq_begin": (C.c_int, [P, P, i64, i64, i32, P]),
     "wv_index_bq_replay": (C.c_int, [P, P, P, P, i32, P, P, P, P]),
+    "wv_index_bq_bounds": (C.c_int, [P, P, P]),
+    "wv_index_bq_replay_record": (C.c_int, [P, P, P, P, i32, P, P, P, P]),
     "wv_index_bq_rescore": (C.c_int, [P, P, P, P, P]),
     "wv_bq_final": (C.c_int, [i32, i64, i32, i32, i32, u64, P, P, P, P, P, P, P]),
     "wv_index_pq_fit": (C.c_int, [P, u64]),

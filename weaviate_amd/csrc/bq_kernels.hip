@@ -176,7 +176,8 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
                                                   uint64_t id_base, const uint64_t* __restrict__ in_ids,
                                                   const float* __restrict__ in_d, const int32_t* __restrict__ in_len,
                                                   int pop, uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
-                                                  int32_t* __restrict__ out_n) {
+                                                  int32_t* __restrict__ out_n, uint64_t* __restrict__ rec_ids,
+                                                  float* __restrict__ rec_d, int32_t* __restrict__ rec_n, int cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
     float* s_d = reinterpret_cast<float*>(hid + R);
@@ -190,7 +191,10 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
     // heap state handed over by the previous shard (layout order), or empty
     const int len0 = in_len ? in_len[li] : 0;
     for (int i = lane; i < len0; i += 64) { hid[i] = in_ids[(int64_t)li * R + i]; hd[i] = in_d[(int64_t)li * R + i]; }
-    if (lane == 0) *s_len = len0;
+    if (lane == 0) {
+        *s_len = len0;
+        if (rec_n) rec_n[li] = 0;
+    }
     __syncthreads();
     for (int64_t b0 = 0; b0 < nblk; b0 += 64) {
         const float bm = (b0 + lane < nblk) ? Bq[b0 + lane] : __builtin_inff();
@@ -253,8 +257,15 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
                         mask &= mask - 1;
                         const float dj = s_d[jj];
                         const uint64_t sj = id_base + (uint64_t)(sb + jj);
+                        bool ins = true;
                         if (hp.len < R) rh_insert(hp, sj, dj);
                         else if (hp.dist[0] > dj) { uint64_t a; float b; rh_pop(hp, &a, &b); rh_insert(hp, sj, dj); }
+                        else ins = false;
+                        if (ins && rec_n) {  // the parallel cross-shard replay's record (id order)
+                            const int c = rec_n[li];
+                            if (c < cap) { rec_ids[(int64_t)li * cap + c] = sj; rec_d[(int64_t)li * cap + c] = dj; }
+                            rec_n[li] = c < cap ? c + 1 : cap + 1;
+                        }
                     }
                     *s_len = hp.len;
                 }
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
             }
         }
     }
-    if (lane == 0) {
+    if (lane == 0 && out_n) {
         ReplayHeap hp{hid, hd, *s_len};
         const int n = hp.len;
         if (pop) {  // pop order (max first) = idsSlice of flat/index.go:485-487
@@ -276,6 +287,33 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
             for (int i = 0; i < n; i++) { out_ids[(int64_t)li * R + i] = hid[i]; out_d[(int64_t)li * R + i] = hd[i]; }
         }
         out_n[li] = n;
+    }
+}
+
+// Per query the R smallest 256-row block minima of this shard, ascending
+// (+inf padded): each is the exact hamming distance of one distinct row, so
+// the R-th smallest over the shards before r bounds the R-heap's top at shard
+// r's first row (the parallel cross-shard replay, weaviate_amd/sharded.py).
+// Hamming distances are integers 0..64*words: a histogram per query in LDS.
+__global__ __launch_bounds__(256) void k_bq_bounds(const float* __restrict__ bmin, int64_t nblk, int nbins, int R,
+                                                   float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char hsm[];
+    uint32_t* hist = reinterpret_cast<uint32_t*>(hsm);
+    const int q = blockIdx.x;
+    for (int i = threadIdx.x; i < nbins; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    const float* Bq = bmin + (int64_t)q * nblk;
+    for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) {
+        const float v = Bq[b];
+        if (v < (float)nbins) atomicAdd(&hist[(int)v], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float* o = out + (int64_t)q * R;
+        int n = 0;
+        for (int v = 0; v < nbins && n < R; v++)
+            for (uint32_t c = hist[v]; c > 0 && n < R; c--) o[n++] = (float)v;
+        for (; n < R; n++) o[n] = __builtin_inff();
     }
 }
 

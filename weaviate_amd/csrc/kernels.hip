@@ -1,13 +1,16 @@
 // kernels.hip -- gfx950 kernels of the flat-index hot path.
 //
-// Pipeline for SearchByVector over a batch of queries (flat/index.go:423-448,
-// :578-688), per GPU:
+// The default exact search is the block-key path (qs_kernels.hip).  These are
+// the row preparation, the fallback select path (d > 1536, hamming-free k <= 24
+// without block keys, option kernel) and the exact replay shared by all paths
+// (flat/index.go:423-448, :578-688), per GPU:
 //   k_prepare_rows      normalise (cosine, distancer/normalize.go:16-32) and
 //                       store rows + squared norms          [Add, :362-390]
-//   k_mfma_select       f32 MFMA (v_mfma_f32_32x32x2_f32) query x corpus tiles
+//   k_mfma_select3      f32 MFMA (v_mfma_f32_32x32x2_f32) query x corpus tiles
 //                       fused with per-(query, corpus span) top-KP selection
 //                       on an approximate distance; the B x N distance matrix
-//                       is never written.
+//                       is never written (k_gemv_select: the same for <= 8
+//                       queries, gemv_kernels.hip).
 //   k_merge_spans       merge the span lists of a query       (wave per query)
 //   k_rescore           exact-order distance of the KP candidates (lane per pair)
 //   k_finalize          sort by exact distance, prove the result equals the
@@ -98,11 +101,6 @@ struct SelectArgs {
     int qgroup;               // query blocks per XCD cell (divides nqb)
     float* outA;              // [nq_pad][nspans][KP]
     uint32_t* outI;
-    // bf16x3 kernel (k_mfma_select_bf3): hi/lo bf16 planes of X and Q
-    const uint16_t* Xh;       // [cap][dpad]
-    const uint16_t* Xl;
-    const uint16_t* Qh;       // [nq_pad][dpad]
-    const uint16_t* Ql;
     int dbg;                  // timing experiments only: 1 = skip selection, 2 = skip MFMA + selection
     int opt;                  // kernel tuning bits (option sel_opt), reserved for experiments
 };
@@ -129,422 +127,9 @@ __device__ __forceinline__ void merge_query_list(float* listA, uint32_t* listI, 
     }
 }
 
-template <int METRIC, int R>
-__global__ __launch_bounds__(256, 2) void k_mfma_select(SelectArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int KP = a.KP;
-    const int C = a.C;
-    float* Xs = smem;                                   // QB*LDSROW
-    float* Qs = Xs + BN * LDSROW;                       // QB*LDSROW
-    float* listA = Qs + QB * LDSROW;                    // QB*KP
-    uint32_t* listI = reinterpret_cast<uint32_t*>(listA + QB * KP);
-    float* cbA = reinterpret_cast<float*>(listI + QB * KP);  // QB*C
-    uint32_t* cbI = reinterpret_cast<uint32_t*>(cbA + QB * C);
-    float* thr = reinterpret_cast<float*>(cbI + QB * C);     // QB
-    int* cnt = reinterpret_cast<int*>(thr + QB);             // QB
-    int* flags = cnt + QB;                                   // [0]=any, [1]=ovf
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wq = wave & 1, wx = wave >> 1;
-    const int li = lane & 31, lh = lane >> 5;
-
-    // block -> (query block, span), XCD-aware (T1): blocks b and b+8 share an
-    // XCD, so logical = (b%8)*(total/8) + b/8 gives each XCD a contiguous run
-    // of "cells"; a cell is QG query blocks x one span.  Concurrent workgroups
-    // of an XCD then share QG query blocks (L2-resident, 4 x 393 KB at d=768)
-    // and each corpus tile is read by QG workgroups through one L2.
-    const int total = a.nqb * a.nspans;
-    const int b = blockIdx.x;
-    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
-    const int QG = a.qgroup;
-    const int cell = logical / QG, qi = logical % QG;
-    const int group = cell / a.nspans;
-    const int span = cell % a.nspans;
-    const int qb = group * QG + qi;
-    const int q0 = qb * QB;
-
-    for (int i = tid; i < QB * KP; i += 256) { listA[i] = __builtin_inff(); listI[i] = NO_ID; }
-    if (tid < QB) { thr[tid] = __builtin_inff(); cnt[tid] = 0; }
-    if (tid == 0) { flags[0] = 0; flags[1] = 0; }
-
-    const int64_t t0 = (int64_t)span * a.tiles_per_span;
-    int64_t t1 = t0 + a.tiles_per_span;
-    if (t1 > a.ntiles) t1 = a.ntiles;
-    const int nk = a.dpad / BK;
-    const int64_t total_steps = t1 > t0 ? (t1 - t0) * nk : 0;
-
-    // staging: thread -> row tid>>1, 16 contiguous floats at 16*(tid&1)
-    const int srow = tid >> 1, shalf = tid & 1;
-    float4 px[4], pq[4];
-    auto prefetch = [&](int64_t step) {
-        int64_t tile = t0 + step / nk;
-        int kb = (int)(step % nk);
-        const float* xp = a.X + (tile * BN + srow) * (int64_t)a.dpad + kb * BK + 16 * shalf;
-        const float* qp = a.Q + (int64_t)(q0 + srow) * a.dpad + kb * BK + 16 * shalf;
-#pragma unroll
-        for (int c = 0; c < 4; c++) { px[c] = ld4(xp + 4 * c); pq[c] = ld4(qp + 4 * c); }
-    };
-    // a row's 32 k-values stay in order at a 36-float stride; MFMA step s
-    // takes k = s on lane half 0 and k = 16+s on lane half 1 (the k order of a
-    // sum is free), so each lane reads 16 contiguous floats.  Bank check: the
-    // 8-lane ds_write_b128 groups hit quads (r + 4h + j) mod 8, the 16-lane
-    // ds_read_b128 groups quads (9i + 4h + j) mod 16: both conflict-free.
-    auto stage = [&](float* dst, const float4 (&p)[4]) {
-        float* base = dst + srow * LDSROW + 16 * shalf;
-#pragma unroll
-        for (int c = 0; c < 4; c++) *reinterpret_cast<float4*>(base + 4 * c) = p[c];
-    };
-
-    f32x16 acc[2][2];
-    int epoch = 0;
-    if (total_steps > 0) prefetch(0);
-    __syncthreads();
-
-    for (int64_t step = 0; step < total_steps; step++) {
-        const int64_t tile = t0 + step / nk;
-        const int kb = (int)(step % nk);
-        if (kb == 0) {
-#pragma unroll
-            for (int i = 0; i < 2; i++)
-#pragma unroll
-                for (int j = 0; j < 2; j++)
-#pragma unroll
-                    for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-        }
-        __syncthreads();
-        stage(Xs, px);
-        stage(Qs, pq);
-        __syncthreads();
-        if (step + 1 < total_steps) prefetch(step + 1);
-
-        // 16 MFMA k-steps over this BK slice
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-            float fa[2][8], fb[2][8];
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-                const float* xr = Xs + (64 * wx + 32 * i + li) * LDSROW + 16 * lh + 8 * half;
-                const float* qr = Qs + (64 * wq + 32 * i + li) * LDSROW + 16 * lh + 8 * half;
-                float4 x0 = *reinterpret_cast<const float4*>(xr), x1 = *reinterpret_cast<const float4*>(xr + 4);
-                float4 y0 = *reinterpret_cast<const float4*>(qr), y1 = *reinterpret_cast<const float4*>(qr + 4);
-                fa[i][0] = x0.x; fa[i][1] = x0.y; fa[i][2] = x0.z; fa[i][3] = x0.w;
-                fa[i][4] = x1.x; fa[i][5] = x1.y; fa[i][6] = x1.z; fa[i][7] = x1.w;
-                fb[i][0] = y0.x; fb[i][1] = y0.y; fb[i][2] = y0.z; fb[i][3] = y0.w;
-                fb[i][4] = y1.x; fb[i][5] = y1.y; fb[i][6] = y1.z; fb[i][7] = y1.w;
-            }
-#pragma unroll
-            for (int s = 0; s < 8; s++)
-#pragma unroll
-                for (int i = 0; i < 2; i++)
-#pragma unroll
-                    for (int j = 0; j < 2; j++)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-        }
-
-        if (kb != nk - 1) continue;
-
-        // ---------------- epilogue: selection over this tile ----------------
-        const int64_t row0 = tile * BN;
-        // values -> distances (in place); invalid rows / padded queries -> +inf
-        float qn[2];
-        int qidx[2];
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            qidx[j] = 64 * wq + 32 * j + li;
-            qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
-        }
-        const uint32_t* vb = a.valid + (row0 >> 5);
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                bool ok = (vb[rt >> 5] >> (rt & 31)) & 1u;
-                float xn = (METRIC == L2) ? a.xnorm2[row0 + rt] : 0.f;
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    float dot = acc[i][j][r];
-                    float v;
-                    if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
-                    else if (METRIC == DOT) v = -dot;
-                    else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
-                    bool qok = (q0 + qidx[j]) < a.nq;
-                    acc[i][j][r] = (ok && qok) ? v : __builtin_inff();
-                }
-            }
-        }
-        uint64_t pending = ~0ull;
-        for (;;) {
-            ++epoch;
-            float th[2] = {thr[qidx[0]], thr[qidx[1]]};
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        const int vi = (i * 16 + r) * 2 + j;
-                        if (!((pending >> vi) & 1ull)) continue;
-                        float v = acc[i][j][r];
-                        if (v < th[j]) {
-                            int slot = atomicAdd(&cnt[qidx[j]], 1);
-                            if (slot < C) {
-                                int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                                cbA[qidx[j] * C + slot] = v;
-                                cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
-                                pending &= ~(1ull << vi);
-                            }
-                            flags[0] = epoch;
-                        } else {
-                            pending &= ~(1ull << vi);
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-            if (flags[0] != epoch) break;
-            // merge pass: wave w merges queries w, w+4, ...
-            for (int jq = 0; jq < QB / 4; jq++) {
-                const int q = wave + 4 * jq;
-                const int c = cnt[q];
-                if (c == 0) continue;
-                const int nc = c < C ? c : C;
-                merge_query_list<R>(listA + q * KP, listI + q * KP, cbA + q * C, cbI + q * C, KP, C, nc, lane,
-                                    &thr[q]);
-                if (lane == 0) {
-                    if (c > C) flags[1] = epoch;
-                    cnt[q] = 0;
-                }
-            }
-            __syncthreads();
-            if (flags[1] != epoch) break;
-        }
-    }
-
-    __syncthreads();
-    // write this span's lists
-    for (int jq = 0; jq < QB / 4; jq++) {
-        const int q = wave + 4 * jq;
-        if (q0 + q >= a.nq) continue;
-        int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
-        for (int e = lane; e < KP; e += 64) {
-            a.outA[base + e] = listA[q * KP + e];
-            a.outI[base + e] = listI[q * KP + e];
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_mfma_select2: same math as k_mfma_select, pipelined:
-//  * LDS staging double-buffered -> one barrier per BK slice; the next slice's
-//    global loads are in flight during the MFMAs and written to the other
-//    buffer afterwards;
-//  * 32-float rows with an XOR chunk swizzle f(r) = (r&3) ^ ((r>>2)&7): the
-//    8-lane ds_write_b128 groups and 16-lane ds_read_b128 groups are
-//    conflict-free (offline check in DESIGN.md);
-//  * the per-(query, span) candidate lists live in the output buffer in global
-//    memory (each entry always touched by the same thread), leaving LDS for the
-//    staging buffers, thresholds and a small candidate buffer: <= 80 KiB, two
-//    workgroups per CU.
-// ---------------------------------------------------------------------------
+// 32-float rows with an XOR chunk swizzle f(r) = (r&3) ^ ((r>>2)&7): the
+// 16-lane ds_read_b128 groups are conflict-free
 __device__ __forceinline__ int swz(int r) { return ((r & 3) ^ ((r >> 2) & 7)); }
-
-template <int METRIC, int R>
-__global__ __launch_bounds__(256, 2) void k_mfma_select2(SelectArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int STG = (BN + QB) * BK;                      // floats per staging buffer
-    const int KP = a.KP;
-    const int C = a.C;
-    float* stg = smem;                                       // [2][STG]
-    float* thr = stg + 2 * STG;                              // QB
-    int* cnt = reinterpret_cast<int*>(thr + QB);             // QB
-    int* flags = cnt + QB;                                   // 4
-    float* cbA = reinterpret_cast<float*>(flags + 4);        // QB*C
-    uint32_t* cbI = reinterpret_cast<uint32_t*>(cbA + QB * C);
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wq = wave & 1, wx = wave >> 1;
-    const int li = lane & 31, lh = lane >> 5;
-
-    const int total = a.nqb * a.nspans;
-    const int b = blockIdx.x;
-    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
-    const int QG = a.qgroup;
-    const int cell = logical / QG, qi = logical % QG;
-    const int group = cell / a.nspans;
-    const int span = cell % a.nspans;
-    const int qb = group * QG + qi;
-    const int q0 = qb * QB;
-
-    // lists: wave w owns queries w + 4j, lane e owns entry e (same thread for
-    // init, merges and the final state)
-    for (int jq = 0; jq < QB / 4; jq++) {
-        const int q = wave + 4 * jq;
-        if (q0 + q >= a.nq) continue;
-        const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
-        for (int e = lane; e < KP; e += 64) { a.outA[base + e] = __builtin_inff(); a.outI[base + e] = NO_ID; }
-    }
-    if (tid < QB) { thr[tid] = __builtin_inff(); cnt[tid] = 0; }
-    if (tid == 0) { flags[0] = 0; flags[1] = 0; }
-
-    const int64_t t0 = (int64_t)span * a.tiles_per_span;
-    int64_t t1 = t0 + a.tiles_per_span;
-    if (t1 > a.ntiles) t1 = a.ntiles;
-    const int nk = a.dpad / BK;
-    const int64_t total_steps = t1 > t0 ? (t1 - t0) * nk : 0;
-
-    const int srow = tid >> 1, shalf = tid & 1;
-    const int wsw = swz(srow & 31);
-    const int rsw = swz(li);
-    float4 px[4], pq[4];
-    auto prefetch = [&](int64_t step) {
-        int64_t tile = t0 + step / nk;
-        int kb = (int)(step % nk);
-        const float* xp = a.X + (tile * BN + srow) * (int64_t)a.dpad + kb * BK + 16 * shalf;
-        const float* qp = a.Q + (int64_t)(q0 + srow) * a.dpad + kb * BK + 16 * shalf;
-#pragma unroll
-        for (int c = 0; c < 4; c++) { px[c] = ld4(xp + 4 * c); pq[c] = ld4(qp + 4 * c); }
-    };
-    auto stage = [&](float* buf) {
-        float* xr = buf + srow * BK;
-        float* qr = buf + BN * BK + srow * BK;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const int pc = (4 * shalf + c) ^ wsw;
-            *reinterpret_cast<float4*>(xr + 4 * pc) = px[c];
-            *reinterpret_cast<float4*>(qr + 4 * pc) = pq[c];
-        }
-    };
-
-    f32x16 acc[2][2];
-    int epoch = 0;
-    if (total_steps > 0) { prefetch(0); stage(stg); }
-    __syncthreads();
-
-    for (int64_t step = 0; step < total_steps; step++) {
-        const int64_t tile = t0 + step / nk;
-        const int kb = (int)(step % nk);
-        const float* cur = stg + (step & 1) * STG;
-        if (kb == 0) {
-#pragma unroll
-            for (int i = 0; i < 2; i++)
-#pragma unroll
-                for (int j = 0; j < 2; j++)
-#pragma unroll
-                    for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-        }
-        const bool more = step + 1 < total_steps;
-        if (more) prefetch(step + 1);
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-            float fa[2][8], fb[2][8];
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-                const float* xr = cur + (64 * wx + 32 * i + li) * BK;
-                const float* qr = cur + BN * BK + (64 * wq + 32 * i + li) * BK;
-#pragma unroll
-                for (int c = 0; c < 2; c++) {
-                    const int pc = (4 * lh + 2 * half + c) ^ rsw;
-                    float4 x = *reinterpret_cast<const float4*>(xr + 4 * pc);
-                    float4 y = *reinterpret_cast<const float4*>(qr + 4 * pc);
-                    fa[i][4 * c + 0] = x.x; fa[i][4 * c + 1] = x.y; fa[i][4 * c + 2] = x.z; fa[i][4 * c + 3] = x.w;
-                    fb[i][4 * c + 0] = y.x; fb[i][4 * c + 1] = y.y; fb[i][4 * c + 2] = y.z; fb[i][4 * c + 3] = y.w;
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < 8; s++)
-#pragma unroll
-                for (int i = 0; i < 2; i++)
-#pragma unroll
-                    for (int j = 0; j < 2; j++)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-        }
-        if (more) stage(stg + ((step + 1) & 1) * STG);
-
-        if (kb == nk - 1) {
-            // ---------------- epilogue: selection over this tile ----------------
-            const int64_t row0 = tile * BN;
-            float qn[2];
-            int qidx[2];
-#pragma unroll
-            for (int j = 0; j < 2; j++) {
-                qidx[j] = 64 * wq + 32 * j + li;
-                qn[j] = (METRIC == L2) ? a.qnorm2[q0 + qidx[j]] : 0.f;
-            }
-            const uint32_t* vb = a.valid + (row0 >> 5);
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    bool ok = (vb[rt >> 5] >> (rt & 31)) & 1u;
-                    float xn = (METRIC == L2) ? a.xnorm2[row0 + rt] : 0.f;
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        float dot = acc[i][j][r];
-                        float v;
-                        if (METRIC == L2) v = (xn - 2.f * dot) + qn[j];
-                        else if (METRIC == DOT) v = -dot;
-                        else { v = 1.f - dot; v = v < 0.f ? 0.f : v; }
-                        bool qok = (q0 + qidx[j]) < a.nq;
-                        acc[i][j][r] = (ok && qok) ? v : __builtin_inff();
-                    }
-                }
-            }
-            uint64_t pending = ~0ull;
-            for (;;) {
-                ++epoch;
-                float th[2] = {thr[qidx[0]], thr[qidx[1]]};
-#pragma unroll
-                for (int i = 0; i < 2; i++) {
-#pragma unroll
-                    for (int r = 0; r < 16; r++) {
-#pragma unroll
-                        for (int j = 0; j < 2; j++) {
-                            const int vi = (i * 16 + r) * 2 + j;
-                            if (!((pending >> vi) & 1ull)) continue;
-                            float v = acc[i][j][r];
-                            if (v < th[j]) {
-                                int slot = atomicAdd(&cnt[qidx[j]], 1);
-                                if (slot < C) {
-                                    int rt = 64 * wx + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                                    cbA[qidx[j] * C + slot] = v;
-                                    cbI[qidx[j] * C + slot] = (uint32_t)(row0 + rt);
-                                    pending &= ~(1ull << vi);
-                                }
-                                flags[0] = epoch;
-                            } else {
-                                pending &= ~(1ull << vi);
-                            }
-                        }
-                    }
-                }
-                __syncthreads();
-                if (flags[0] != epoch) break;
-                for (int jq = 0; jq < QB / 4; jq++) {
-                    const int q = wave + 4 * jq;
-                    const int c = cnt[q];
-                    if (c == 0) continue;
-                    const int nc = c < C ? c : C;
-                    const int64_t base = ((int64_t)(q0 + q) * a.nspans + span) * KP;
-                    merge_query_list<R>(a.outA + base, a.outI + base, cbA + q * C, cbI + q * C, KP, C, nc, lane,
-                                        &thr[q]);
-                    if (lane == 0) {
-                        if (c > C) flags[1] = epoch;
-                        cnt[q] = 0;
-                    }
-                }
-                __syncthreads();
-                if (flags[1] != epoch) break;
-            }
-        }
-        __syncthreads();
-    }
-}
 
 // ---------------------------------------------------------------------------
 // k_mfma_select3: 8 waves, 128-query x 256-row tiles, direct global->LDS DMA

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(256, 2) void k_pq_adc2(const uint32_t* __restrict__
             const int64_t row = tile0 + lr;
             const bool ok = lr < rem && ((valid[row >> 5] >> (row & 31)) & 1u);
             const float e = ok ? pq_wrap(metric, j ? sb[r] : sa[r]) : __builtin_inff();
-            if ((j == 0 || two) && lr < lrem) Ef[lr] = e;
+            if (E && (j == 0 || two) && lr < lrem) Ef[lr] = e;  // E == nullptr: block minima only
             float mm = e;
             for (int o = 32; o > 0; o >>= 1) mm = fminf(mm, __shfl_xor(mm, o));
             if (lane == 0) red[j][wv][r] = mm;
@@ -461,6 +461,109 @@ __global__ __launch_bounds__(256, 2) void k_pq_adc2(const uint32_t* __restrict__
         if ((j == 0 || two) && blk < ld / 256)
             bmin[(int64_t)(f0 + j) * (ld / 256) + blk] =
                 fminf(fminf(red[j][0][r], red[j][1][r]), fminf(red[j][2][r], red[j][3][r]));
+    }
+}
+
+// The minima-only PQ search (no B x N distance matrix): k_pq_adc2 wrote the
+// 256-row block minima of every query, k_blk_select listed the blocks whose
+// minimum is within (a rounding-size eps of) M = the (R+1)-th smallest block
+// minimum -- every block that can hold one of the R+1 smallest ADC distances.
+// Per query (one workgroup, thread = row of a candidate block): the ADC
+// distance in segment order (bit-identical to k_pq_adc2), the rows with a
+// value <= M collected and bitonic-sorted by (value, slot) in LDS.  Strictly
+// increasing R+1 smallest values (or all of them when fewer) ARE the worker
+// heap's content in its ascending extraction (flat_search.go:96-110: the heap
+// keeps the R smallest; distinct values leave no order to the heap layout):
+// written as asc[q] for k_pq_finish.  Ties, NaN, more than PQC_MAXB candidate
+// blocks or PQC_CAP rows: flag_out[q] = 1 (the exact heap replay decides).
+constexpr int PQC_MAXB = 64;
+constexpr int PQC_CAP = 1024;
+template <int KC>
+__global__ __launch_bounds__(256) void k_pq_cand(const uint32_t* __restrict__ codes, int g16, int m, int kk,
+                                                 const uint32_t* __restrict__ valid, int64_t nslots,
+                                                 const float* __restrict__ lut, const float* __restrict__ bmin,
+                                                 int64_t ldb, const uint32_t* __restrict__ cand, int L,
+                                                 const int32_t* __restrict__ ncand, const int32_t* __restrict__ sel_flags,
+                                                 int R, int metric, uint64_t id_base, uint64_t* __restrict__ asc_ids,
+                                                 float* __restrict__ asc_d, int32_t* __restrict__ asc_n,
+                                                 int32_t* __restrict__ flag_out) {
+    __shared__ float sv[PQC_CAP];
+    __shared__ uint32_t ss[PQC_CAP];
+    __shared__ int s_cnt, s_bad;
+    __shared__ float s_M;
+    const int k = KC > 0 ? KC : kk;
+    const int q = blockIdx.x;
+    const int t = threadIdx.x;
+    const int nc = ncand[q];
+    if (sel_flags[q] != 0 || nc > PQC_MAXB || R + 1 > 64) {
+        if (t == 0) flag_out[q] = 1;
+        return;
+    }
+    if (t < 64) {  // M = the (R+1)-th smallest minimum of the candidate blocks (+inf when fewer)
+        float key[1] = {t < nc ? bmin[(int64_t)q * ldb + cand[(int64_t)q * L + t]] : __builtin_inff()};
+        uint32_t id[1] = {(uint32_t)t};
+        bitonic_sort<1>(key, id, t);
+        const float M = __shfl(key[0], R);
+        if (t == 0) { s_M = R < nc ? M : __builtin_inff(); s_cnt = 0; s_bad = 0; }
+    }
+    __syncthreads();
+    const float M = s_M;
+    const float* Lq = lut + (int64_t)q * m * k;
+    const uint4* c4 = reinterpret_cast<const uint4*>(codes);
+    for (int j = 0; j < nc; j++) {
+        const int64_t b = cand[(int64_t)q * L + j];
+        const int64_t row = b * 256 + t;
+        if (row >= nslots || !((valid[row >> 5] >> (row & 31)) & 1u)) continue;
+        float sum = 0.f;
+        for (int g = 0; g < g16; g++) {
+            const uint4 cw = c4[(b * g16 + g) * 256 + t];
+            const uint32_t w4[4] = {cw.x, cw.y, cw.z, cw.w};
+            const int nv = m - 16 * g < 16 ? m - 16 * g : 16;
+            for (int jj = 0; jj < nv; jj++) {
+                const int sgm = 16 * g + jj;
+                sum = sum + Lq[(int64_t)sgm * k + ((w4[jj >> 2] >> (8 * (jj & 3))) & 0xFFu)];
+            }
+        }
+        const float e = pq_wrap(metric, sum);
+        if (e != e) s_bad = 1;
+        if (e <= M) {
+            const int pos = atomicAdd(&s_cnt, 1);
+            if (pos < PQC_CAP) { sv[pos] = e; ss[pos] = (uint32_t)row; }
+        }
+    }
+    __syncthreads();
+    const int n = s_cnt;
+    if (n > PQC_CAP || s_bad) {
+        if (t == 0) flag_out[q] = 1;
+        return;
+    }
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    for (int i = n + t; i < p2; i += 256) { sv[i] = __builtin_inff(); ss[i] = NO_ID; }
+    __syncthreads();
+    for (int k2 = 2; k2 <= p2; k2 <<= 1)
+        for (int jj = k2 >> 1; jj > 0; jj >>= 1) {
+            for (int i = t; i < p2; i += 256) {
+                const int ixj = i ^ jj;
+                if (ixj > i) {
+                    const float a = sv[i], c = sv[ixj];
+                    const uint32_t ia = ss[i], ic = ss[ixj];
+                    const bool gt = a > c || (a == c && ia > ic);
+                    if ((i & k2) == 0 ? gt : !gt) { sv[i] = c; sv[ixj] = a; ss[i] = ic; ss[ixj] = ia; }
+                }
+            }
+            __syncthreads();
+        }
+    const int mm = n < R + 1 ? n : R + 1;
+    if (t == 0) {
+        bool strict = true;
+        for (int i = 1; i < mm; i++) strict &= sv[i - 1] < sv[i];
+        flag_out[q] = strict ? 0 : 1;
+        asc_n[q] = n < R ? n : R;
+    }
+    if (t < R && t < n) {
+        asc_ids[(int64_t)q * R + t] = id_base + ss[t];
+        asc_d[(int64_t)q * R + t] = sv[t];
     }
 }
 

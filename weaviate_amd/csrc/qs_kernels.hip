@@ -65,13 +65,14 @@ __device__ __forceinline__ uint32_t sload_u32(const void* p) {
     return v;
 }
 
-// s_waitcnt vmcnt(y) for a run-time wave-uniform y (0..23)
+// s_waitcnt vmcnt(y) for a run-time wave-uniform y (0..40; larger: vmcnt(0))
 __device__ __forceinline__ void qs_wait_vm(int y) {
 #define QS_VM(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
     switch (y) {
         QS_VM(0) QS_VM(1) QS_VM(2) QS_VM(3) QS_VM(4) QS_VM(5) QS_VM(6) QS_VM(7) QS_VM(8) QS_VM(9) QS_VM(10)
         QS_VM(11) QS_VM(12) QS_VM(13) QS_VM(14) QS_VM(15) QS_VM(16) QS_VM(17) QS_VM(18) QS_VM(19) QS_VM(20)
-        QS_VM(21) QS_VM(22) QS_VM(23)
+        QS_VM(21) QS_VM(22) QS_VM(23) QS_VM(24) QS_VM(25) QS_VM(26) QS_VM(27) QS_VM(28) QS_VM(29) QS_VM(30)
+        QS_VM(31) QS_VM(32) QS_VM(33) QS_VM(34) QS_VM(35) QS_VM(36) QS_VM(37) QS_VM(38) QS_VM(39) QS_VM(40)
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 #undef QS_VM
@@ -496,6 +497,256 @@ __global__ __launch_bounds__(512, 2) void k_qs_blockkey(QsArgs a) {
         cur = nxt;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last (unused) prefetch
+}
+
+// ---------------------------------------------------------------------------
+// k_qs_blockkey_w4<NK, L2, NB>: the same block keys for 768 < d <= 1536 (dpb
+// 1024 or 1536, NK = dpb / 16 in {64, 96}).  32 queries x dpb bf16 are NK x 4
+// registers per lane -- more than two waves per SIMD leave -- so the
+// workgroup is 4 waves, one per SIMD (512-entry register file: the stationary
+// query fragments go to AGPRs), 128 queries.  A 32-row block is staged in
+// NP = NK / 32 column parts of 512 columns (32 KiB per ring slot), one ring
+// step per part; the accumulators run across the parts and the key epilogue
+// follows the last.  NB ring slots: the DMA of the group NB - 1 steps ahead is
+// issued during a step (128 queries per workgroup read the corpus at twice
+// the per-flop rate of the 256-query k_qs_blockkey, so the L2 latency needs
+// the deeper ring).  Per 32-column chunk: 2 A reads, 4
+// v_mfma_f32_16x16x32_bf16 (2 row halves x 2 query halves), the DMA pieces
+// and the previous block's key store as fillers.
+// ---------------------------------------------------------------------------
+template <int NK, bool ISL2, int NP, int NB>
+__global__ __launch_bounds__(256, 1) void k_qs_blockkey_w4(QsArgs a) {
+    constexpr int QH = 2;                           // query halves (16 queries) per wave
+    constexpr int NCP = NK / (2 * NP);              // 32-column chunks per part
+    constexpr int SLOT = NCP * 2048;                // bytes per ring slot (32 rows x the part's columns)
+    constexpr int AF = 3;                           // A-fragment sets in flight (chunks c .. c+2)
+    constexpr int P = NCP / 2;                      // 1 KiB DMA pieces per wave per step (2 NCP / 4 waves)
+    constexpr int PX = ISL2 ? 2 : 1;                // valid word (+ the L2 norms): with a block's first part
+    constexpr int64_t TILE_B = (int64_t)NK * 8192;  // bytes per 256-row tile of a plane
+    constexpr int QPB = 64 * QH;                    // queries per workgroup
+    constexpr int XC = NCP - 4;                     // chunk of the last part that reads valid / norms
+    constexpr int XE = ISL2 ? 3 : 1;
+    static_assert(NK % (2 * NP) == 0 && NCP % 2 == 0, "parts of whole 32-column chunk pairs");
+    static_assert(P + PX + 1 < XC, "filler chunks overlap");
+    extern __shared__ __attribute__((aligned(16))) unsigned char qsm[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int total = a.nqg * a.nspans;
+    const int b = blockIdx.x;
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int span = logical / a.nqg, grp = logical % a.nqg;
+
+    // Qf[QH c + n]: lane (j = lane&15, kq = lane>>4) holds query q0 + 16n + j,
+    // columns 32c + 8kq .. +7 (the 16x16x32 B fragment)
+    bf16x8_t Qf[NK / 2 * QH];
+    const int64_t q0 = (int64_t)grp * QPB + wave * 16 * QH;
+    {
+        const int j = lane & 15, kq = lane >> 4;
+        const unsigned char* qp = a.Qb + (q0 >> 8) * TILE_B + (kq >> 1) * 8192 + ((q0 & 255) + j) * 32 + 16 * (kq & 1);
+#pragma unroll
+        for (int c = 0; c < NK / 2; c++)
+#pragma unroll
+            for (int n = 0; n < QH; n++)
+                Qf[QH * c + n] = *reinterpret_cast<const bf16x8_t*>(qp + (2 * c) * 8192 + n * 16 * 32);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the query loads retire before any LDS-DMA
+
+    const int64_t s0 = (int64_t)span * a.slots_per_span;
+    int64_t s1 = s0 + a.slots_per_span;
+    if (s1 > a.nslots) s1 = a.nslots;
+    const int nblk = s1 > s0 ? (int)(s1 - s0) : 0;
+    const int G = NP * nblk;  // ring steps
+
+    const unsigned ring = lds_addr(qsm);
+    const unsigned vring = ring + NB * SLOT + (unsigned)wave * 64u;           // [4] x 16 B valid words
+    const unsigned xnring = ring + NB * SLOT + 256u + (unsigned)wave * 512u;  // [4] x 32 floats
+    const int64_t tile0 = (s0 * 32) >> 8;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.Xb + tile0 * TILE_B), (short)0, -1, 0x00020000);
+    const uint32_t src_lane = (uint32_t)(16 * lane);
+    // the next group to issue: block igb, part ih; ioff = its block's offset in the span's buffer
+    int64_t igb = s0;
+    int ih = 0;
+    uint32_t ioff = (uint32_t)(((igb >> 3) - tile0) * TILE_B + (igb & 7) * 1024);
+    // piece j of the next group into ring slot `slot`; the group's last piece advances it
+    auto issue_piece = [&](int j, int slot, int pg) {
+        if (j < P) {
+            const int cc = wave + 4 * j;  // 16-column chunk of the part
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(size_t)(ring + (unsigned)(slot * SLOT + cc * 1024)),
+                                                     16, src_lane, ioff + (uint32_t)((ih * 2 * NCP + cc) * 8192), 0, 0);
+        } else if (j == P) {
+            if (lane == 0)
+                __builtin_amdgcn_global_load_lds(a.valid + igb, (lds_ptr_t)(size_t)(vring + (unsigned)((igb & 3) * 16)), 4,
+                                                 0, 0);
+        } else {
+            if (lane < 8)
+                __builtin_amdgcn_global_load_lds(a.xnorm2 + igb * 32 + 4 * lane,
+                                                 (lds_ptr_t)(size_t)(xnring + (unsigned)((igb & 3) * 128)), 16, 0, 0);
+        }
+        if (j == pg - 1) {
+            if (ih == NP - 1) {
+                ih = 0;
+                igb += 1;
+                ioff += 1024;
+                if ((igb & 7) == 0) ioff += (uint32_t)(TILE_B - 8192);
+            } else {
+                ih += 1;
+            }
+        }
+    };
+    auto issue_group = [&](int slot) {
+        const int pg = P + (ih == 0 ? PX : 0);
+        for (int j = 0; j < pg; j++) issue_piece(j, slot, pg);
+    };
+    // this wave's vector-memory ops issued after those of group g+1, once step
+    // g has issued its own: the groups g+2 .. g+NB-1 and the key stores of the
+    // steps from the one that issued group g+1 (store after pieces) to g
+    auto ops_after = [&](int g) {
+        int y = 0;
+        for (int j = g + 2; j <= g + NB - 1 && j < G; j++) y += P + (j % NP == 0 ? PX : 0);
+        for (int x = g + 2 - NB < 0 ? 0 : g + 2 - NB; x <= g; x++) y += (x % NP == 0 && x >= NP) ? 1 : 0;
+        return y;
+    };
+
+    // lane (i = lane&15, kq = lane>>4) reads row 16m + i, columns 32c + 8kq .. +7
+    const unsigned l16 = (unsigned)(((lane >> 5) & 1) * 1024 + (lane & 15) * 32 + 16 * ((lane >> 4) & 1));
+    // the key row this lane stores: query q0 + lane (lanes < 16 QH)
+    float* krow = a.key + (q0 + (lane < 16 * QH ? lane : 0)) * a.ldk;
+    // A fragments of chunks c, c+1, c+2 in flight: with one wave per SIMD no
+    // partner wave covers an LDS read's latency, 4 MFMAs per chunk do not
+    bf16x8_t B2[AF][2];
+    if (G > 0) {
+        for (int j = 0; j < NB - 1 && j < G; j++) issue_group(j);
+        qs_wait_vm(ops_after(0));  // group 0 landed, groups 1 .. NB-2 may stay in flight
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        B2[0][0] = lds_ld8bf_o<0>(ring + l16);
+        B2[0][1] = lds_ld8bf_o<512>(ring + l16);
+        B2[1][0] = lds_ld8bf_o<2048>(ring + l16);
+        B2[1][1] = lds_ld8bf_o<2048 + 512>(ring + l16);
+    }
+    float mp[QH];
+#pragma unroll
+    for (int n = 0; n < QH; n++) mp[n] = 0.f;
+    int64_t gbp = 0;
+    auto finish = [&]() {  // previous block: cross-lane combine (the 4 row groups) + key store
+        float m[QH];
+#pragma unroll
+        for (int n = 0; n < QH; n++) {
+            float v = mp[n];
+            const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+            v = ISL2 ? fminf(v, __uint_as_float(x[1])) : fmaxf(v, __uint_as_float(x[1]));
+            const auto y = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+            m[n] = ISL2 ? fminf(v, __uint_as_float(y[1])) : fmaxf(v, __uint_as_float(y[1]));
+        }
+        // only row 0 (lanes 0-15) of each m[n] holds all four row groups; gather
+        // those rows: lane 16n + j of the store value = query 16n + j
+        const auto c01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m[0]), __float_as_uint(m[1]), false, false);
+        const float v = __uint_as_float(c01[0]);  // rows: m0.r0, m1.r0, ..
+        if (lane < 16 * QH) krow[gbp] = ISL2 ? v : -v;
+    };
+    int cur = 0;
+    for (int tb = 0; tb < nblk; tb++) {
+        f32x4_t acc[2][QH];
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+            for (int n = 0; n < QH; n++) acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        uint32_t vwv = 0;
+        f32x4_t x0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, x1 = x0;
+        static_for<0, NP>([&](auto hh) {
+            constexpr int H = decltype(hh)::value;
+            const int g = NP * tb + H;
+            const int nxt = cur == NB - 1 ? 0 : cur + 1;
+            const int gslot = cur == 0 ? NB - 1 : cur - 1;  // slot of group g + NB - 1
+            const unsigned sb = ring + (unsigned)(cur * SLOT) + l16;
+            const bool dma = g + NB - 1 < G;
+            constexpr int PG = P + ((H + NB - 1) % NP == 0 ? PX : 0);  // ops of group g + NB - 1
+            static_for<0, NCP>([&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                if constexpr (c + 2 < NCP) {
+                    B2[(c + 2) % AF][0] = lds_ld8bf_o<(2 * (c + 2)) * 1024>(sb);
+                    B2[(c + 2) % AF][1] = lds_ld8bf_o<(2 * (c + 2)) * 1024 + 512>(sb);
+                }
+                // chunk c's reads done; those of c+1, c+2 (and the valid / norm reads
+                // issued in chunk XC, behind c+2 = XC+2's) may stay in flight
+                qs_wait_lgkm<2 * (NCP - 1 - c < 2 ? NCP - 1 - c : 2) +
+                             (H == NP - 1 && (c == XC + 1 || c == XC + 2) ? XE : 0)>();
+                asm volatile("" : "+v"(B2[c % AF][0]), "+v"(B2[c % AF][1]));
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < 2; m++)
+#pragma unroll
+                    for (int n = 0; n < QH; n++)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B2[c % AF][m], Qf[QH * (H * NCP + c) + n],
+                                                                            acc[m][n], 0, 0, 0);
+                if constexpr (c < PG) {
+                    if (dma) issue_piece(c, gslot, PG);
+                }
+                if constexpr (H == 0 && c == PG + 1) {
+                    if (tb > 0) finish();
+                }
+                if constexpr (H == NP - 1 && c == XC) {
+                    asm volatile("ds_read_b32 %0, %1" : "=v"(vwv) : "v"(vring + (unsigned)(((s0 + tb) & 3) * 16)));
+                    if constexpr (ISL2) {
+                        // rows 4g..4g+3 and 16+4g..+3 of the block, g = lane>>4
+                        const unsigned xb = xnring + (unsigned)(((s0 + tb) & 3) * 128) + (unsigned)(16 * ((lane >> 4) & 3));
+                        x0 = lds_ld4f_o<0>(xb);
+                        x1 = lds_ld4f_o<64>(xb);
+                    }
+                }
+            });
+            if constexpr (H == NP - 1) {
+                if constexpr (ISL2) asm volatile("" : "+v"(vwv), "+v"(x0), "+v"(x1));
+                else asm volatile("" : "+v"(vwv));
+                const uint32_t vw = __builtin_amdgcn_readfirstlane(vwv);
+                // acc[m][n][r] is row 16m + 4g + r (g = lane>>4) of query 16n + (lane&15)
+                const uint32_t vl = vw >> (4 * ((lane >> 4) & 3));
+#pragma unroll
+                for (int n = 0; n < QH; n++) {
+                    if constexpr (ISL2) {
+                        float m = __builtin_inff();
+#pragma unroll
+                        for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                            for (int r = 0; r < 4; r++) {
+                                const float v = fmaf(-2.f, acc[mm][n][r], mm ? x1[r] : x0[r]);
+                                m = fminf(m, ((vl >> (16 * mm + r)) & 1u) ? v : __builtin_inff());
+                            }
+                        mp[n] = m;
+                    } else if (vw == 0xFFFFFFFFu) {
+                        float m = fmaxf(fmaxf(acc[0][n][0], acc[0][n][1]), fmaxf(acc[0][n][2], acc[0][n][3]));
+                        m = fmaxf(m, fmaxf(fmaxf(acc[1][n][0], acc[1][n][1]), fmaxf(acc[1][n][2], acc[1][n][3])));
+                        mp[n] = m;
+                    } else {
+                        float m = -__builtin_inff();
+#pragma unroll
+                        for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                            for (int r = 0; r < 4; r++)
+                                m = fmaxf(m, ((vl >> (16 * mm + r)) & 1u) ? acc[mm][n][r] : -__builtin_inff());
+                        mp[n] = m;
+                    }
+                }
+                gbp = s0 + tb;
+            }
+            // ---- end of the step: group g + 1 must have landed (every wave) ----
+            if (g + 1 < G) {
+                qs_wait_vm(ops_after(g));
+                __builtin_amdgcn_s_barrier();  // slot g is free; slot g+1 has landed for every wave
+                __builtin_amdgcn_sched_barrier(0);
+                const unsigned sbn = ring + (unsigned)(nxt * SLOT) + l16;
+                B2[0][0] = lds_ld8bf_o<0>(sbn);
+                B2[0][1] = lds_ld8bf_o<512>(sbn);
+                B2[1][0] = lds_ld8bf_o<2048>(sbn);
+                B2[1][1] = lds_ld8bf_o<2048 + 512>(sbn);
+            }
+            cur = nxt;
+        });
+    }
+    if (nblk > 0) finish();
 }
 
 // ---------------------------------------------------------------------------

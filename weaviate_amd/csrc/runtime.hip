@@ -88,6 +88,10 @@ extern "C" int wv_resolve_variant(int32_t requested) {
 struct DBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { release(); }  // every device buffer of an index is freed with it
     hipError_t ensure(size_t b) {
         if (b <= bytes) return hipSuccess;
         if (p) { hipFree(p); p = nullptr; bytes = 0; }
@@ -149,9 +153,6 @@ struct wv_index {
     int pq_m = 0, pq_ks = 0, pq_ds = 0, pq_training_limit = 0, pq_rescore = 1, pq_trained = 0;
     float* pq_centers = nullptr;
     uint32_t* pq_codes = nullptr;
-    // bf16 hi/lo planes of X for k_mfma_select_bf3 ([cap][dpad] each): built
-    // only when option bf3_planes is set before the first Add
-    int use_bf3 = 0;
     // bf16 hi plane of X for the block-key path (qs_kernels.hip): [cap][dpb],
     // dpb = dims rounded up to 128, built when dpb <= QS_MAX_DPB
     int use_qs = 0, qs_planes = 0, dpb = 0;
@@ -172,8 +173,6 @@ struct wv_index {
     float last_eps_scale = 0.f, last_eps_base = 0.f;  // exactness-proof eps of the last MFMA batch (debug hook)
     int64_t last_nq = 0;
     int last_KP = 0;
-    uint16_t* Xh = nullptr;
-    uint16_t* Xl = nullptr;
     // rq-8 / rq-1 (rq_kernels.hip): rotation tables built at the first Add
     // (initializeDimensionsAndRQ, flat/index.go:338-360), codes + meta per slot
     int rq_bits = 0, rq_D = 0, rq_ready = 0;
@@ -194,7 +193,7 @@ struct wv_index {
     uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
     int64_t npresent = 0;
 
-    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, qh, ql, rqq, rqm;
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, rqq, rqm;
 
     int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0, sel_dbg = 0, qgroup_opt = 0, sel_opt = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -208,6 +207,8 @@ struct wv_index {
     DBuf bmCnt, bmOff, bmPairs, bmE;                          // block-major exact (k_inv_*, k_exact_bm)
     DBuf qsCap;                                               // per query: upper bound of the (k+1)-th exact distance
     int exact_cap = 1;                                        // k_blk_exact drops values above qsCap (phase 0)
+    int pq_cand = 1;                                          // PQ search: block minima + candidate blocks (k_pq_cand)
+    DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
     DBuf flCtr;                      // device flag-list counters (replay_flags)
     int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
     int qs_phase_k = 0;
@@ -231,13 +232,18 @@ static void invalidate_batch(wv_index* idx) {
 // ---------------------------------------------------------------------------
 // create / destroy / capacity
 // ---------------------------------------------------------------------------
-constexpr int QS_MAX_DPB = 768;  // k_qs_blockkey keeps 32 queries x dpb bf16 in VGPRs
+// k_qs_blockkey keeps 32 queries x dpb bf16 in VGPRs (two waves per SIMD) up
+// to 768 dims; k_qs_blockkey_w4 (one wave per SIMD, query fragments in the
+// 512-entry register file, dpb 1024 or 1536) up to 1536
+constexpr int QS_MAX_DPB = 1536;
+constexpr int QS_W4_DPB = 768;  // dpb above this: k_qs_blockkey_w4
 
 // dims fixed (config or first Add, initializeDimensionsAndRQ flat/index.go:338-360)
 static void set_dims(wv_index* idx, int64_t d) {
     idx->dims = (int)d;
     idx->dpad = (int)round_up(d, BK);
     idx->dpb = (int)round_up(d, 128);
+    if (idx->dpb > QS_W4_DPB) idx->dpb = (int)round_up(d, 512);  // 512-column ring parts
     idx->qs_planes = (idx->use_qs && idx->dpb <= QS_MAX_DPB) ? 1 : 0;
 }
 
@@ -267,7 +273,6 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     // block-key path for the exact fp32 search (qs_kernels.hip); the bf16x3
     // select kernels (kernels_bf3.hip) need option bf3_planes before the first Add
     idx->use_qs = (cfg->compression == WV_COMPRESSION_NONE && cfg->metric != WV_METRIC_HAMMING) ? 1 : 0;
-    idx->use_bf3 = 0;
     idx->kernel_opt = 0;  // auto: the block-key path (7) when the planes exist, else the legacy select kernels
     if (cfg->compression == WV_COMPRESSION_RQ8) idx->rq_bits = 8;
     if (cfg->compression == WV_COMPRESSION_RQ1) idx->rq_bits = 1;
@@ -305,7 +310,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
-                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->qh, &idx->ql, &idx->rqq, &idx->rqm,
+                    &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->rqq, &idx->rqm,
                     &idx->rE2, &idx->rB2, &idx->gmA, &idx->gmI, &idx->qsQb, &idx->qsInfo, &idx->qsKey, &idx->qsCand,
                     &idx->qsNc, &idx->qsEps, &idx->qsFlags, &idx->qsList, &idx->qsScratch, &idx->rpBlk, &idx->rpLb,
                     &idx->rpQ, &idx->rpE, &idx->rpVm, &idx->rpOff, &idx->rpTot, &idx->rpCtr, &idx->flCtr})
@@ -325,8 +330,6 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->codes) hipFree(idx->codes);
     if (idx->pq_centers) hipFree(idx->pq_centers);
     if (idx->pq_codes) hipFree(idx->pq_codes);
-    if (idx->Xh) hipFree(idx->Xh);
-    if (idx->Xl) hipFree(idx->Xl);
     if (idx->Xb) hipFree(idx->Xb);
     if (idx->qsmax) hipFree(idx->qsmax);
     if (idx->qscount) hipFree(idx->qscount);
@@ -361,7 +364,7 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     float* xn = nullptr;
     uint32_t* pr = nullptr;
     uint64_t* cd = nullptr;
-    uint16_t *xh = nullptr, *xl = nullptr, *xb = nullptr;
+    uint16_t* xb = nullptr;
     void* rqc = nullptr;
     float4* rqm = nullptr;
     uint32_t* pc = nullptr;
@@ -370,7 +373,6 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     const int words = (idx->dims + 63) / 64;
     const size_t rq_cb = idx->rq_bits == 8 ? (size_t)nc * idx->rq_D : (size_t)(idx->rq_D / 64) * nc * sizeof(uint64_t);
     const int64_t pq_w = idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0 ? pq_mwp(idx->pq_m) : 0;
-    const size_t plane_b = (size_t)nc * idx->dpad * sizeof(uint16_t);
     const size_t qs_b = (size_t)nc * idx->dpb * sizeof(uint16_t);
     hipError_t e = hipSuccess;
     const char* what = "";
@@ -382,10 +384,6 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     WV_STEP("xnorm2", alloc((void**)&xn, (size_t)nc * sizeof(float)));
     WV_STEP("present", alloc((void**)&pr, (size_t)(nc / 32) * sizeof(uint32_t)));
     if (idx->compression == WV_COMPRESSION_BQ) WV_STEP("bq codes", alloc((void**)&cd, (size_t)words * nc * sizeof(uint64_t)));
-    if (idx->use_bf3) {
-        WV_STEP("bf16 hi plane", alloc((void**)&xh, plane_b));
-        WV_STEP("bf16 lo plane", alloc((void**)&xl, plane_b));
-    }
     if (idx->qs_planes) WV_STEP("bf16 block-key plane", alloc((void**)&xb, qs_b));
     if (idx->rq_ready) {
         WV_STEP("rq codes", alloc(&rqc, rq_cb));
@@ -410,15 +408,6 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         if (oc > 0 && idx->codes)  // word-major: copy each word plane
             WV_STEP("copy", hipMemcpy2DAsync(cd, (size_t)nc * sizeof(uint64_t), idx->codes, (size_t)oc * sizeof(uint64_t),
                                              (size_t)oc * sizeof(uint64_t), words, hipMemcpyDeviceToDevice, s));
-    }
-    if (xh) {
-        WV_STEP("memset", hipMemsetAsync(xh, 0, plane_b, s));
-        WV_STEP("memset", hipMemsetAsync(xl, 0, plane_b, s));
-        if (oc > 0 && idx->Xh) {  // 256-row tiles: the old tiles are a prefix
-            const size_t ob = (size_t)oc * idx->dpad * sizeof(uint16_t);
-            WV_STEP("copy", hipMemcpyAsync(xh, idx->Xh, ob, hipMemcpyDeviceToDevice, s));
-            WV_STEP("copy", hipMemcpyAsync(xl, idx->Xl, ob, hipMemcpyDeviceToDevice, s));
-        }
     }
     if (xb) {
         WV_STEP("memset", hipMemsetAsync(xb, 0, qs_b, s));
@@ -469,8 +458,6 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     swap_in(idx->xnorm2, xn);
     swap_in(idx->present, pr);
     if (cd) { swap_in(idx->codes, cd); idx->words = words; }
-    swap_in(idx->Xh, xh);
-    swap_in(idx->Xl, xl);
     swap_in(idx->Xb, xb);
     if (rqc) {
         if (idx->rq_codes) hipFree(idx->rq_codes);
@@ -562,11 +549,6 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
         k_prepare_rows<L2><<<grid, 256, 0, idx->stream>>>(d_in, n, idx->dims, d_slots, idx->X, idx->dpad, idx->xnorm2,
                                                           idx->present, idx->d_maxn2);
         break;
-    }
-    if (idx->use_bf3) {
-        const int64_t ne = n * idx->dpad;
-        k_split_bf16<<<(unsigned)((ne + 255) / 256), 256, 0, idx->stream>>>(idx->X, n, idx->dpad, d_slots, idx->Xh,
-                                                                           idx->Xl);
     }
     if (idx->qs_planes)  // bf16 hi plane + residual-norm maxima of the block-key path
         k_rows_split<<<(unsigned)((n + 3) / 4), 256, 0, idx->stream>>>(idx->X, idx->dpad, idx->dpb, n, d_slots, idx->Xb,
@@ -782,14 +764,10 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "spans") idx->spans_opt = (int)value;
     else if (k == "timing") idx->timing = (int)value;
     else if (k == "cbuf") idx->cbuf_opt = (int)value;
-    else if (k == "kernel") {
-        if (value < 0 || value > 7) return set_err(WV_ERR_INVALID, "kernel out of range (0-7)");
+    else if (k == "kernel") {  // 0 auto, 3 f32 MFMA select, 6 GEMV select, 7 block keys
+        if (value != 0 && value != 3 && value != 6 && value != 7)
+            return set_err(WV_ERR_INVALID, "kernel must be 0 (auto), 3, 6 or 7");
         idx->kernel_opt = (int)value;
-    } else if (k == "bf3_planes") {
-        // the bf16x3 select kernels' hi/lo planes are built at Add: only before the first one
-        if (idx->cap > 0 && (value != 0) != (idx->use_bf3 != 0))
-            return set_err(WV_ERR_INVALID, "bf3_planes must be set before the first Add");
-        idx->use_bf3 = value ? 1 : 0;
     } else if (k == "qs") {
         if (idx->cap > 0 && (value != 0) != (idx->use_qs != 0))
             return set_err(WV_ERR_INVALID, "qs must be set before the first Add");
@@ -797,7 +775,10 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
         if (idx->dims) set_dims(idx, idx->dims);
     }
     else if (k == "bq_kernel") idx->bq_kernel = (int)value;
-    else if (k == "replay_par") {  // 2: pooled k_rp_* for k < 64 (default), 3: pooled for every k,
+    else if (k == "pq_cand") {  // 1: minima-only PQ search with candidate blocks (default), 0: full ADC matrix
+        if (value < 0 || value > 1) return set_err(WV_ERR_INVALID, "pq_cand must be 0 or 1");
+        idx->pq_cand = (int)value;
+    } else if (k == "replay_par") {  // 2: pooled k_rp_* for k < 64 (default), 3: pooled for every k,
                                    // 1: k_blk_replay_par for k < 64, 0: k_blk_replay only
         if (value < 0 || value > 3) return set_err(WV_ERR_INVALID, "replay_par must be 0..3");
         idx->replay_par = (int)value;
@@ -997,13 +978,6 @@ static int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, in
     else
         k_copy_pad_rows<<<(unsigned)((nq * idx->dpad + 255) / 256), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
     k_row_norm2<<<(unsigned)((nq_pad + 3) / 4), 256, 0, s>>>(Qn, nq_pad, idx->dpad, idx->qn2.as<float>());
-    if (idx->use_bf3) {
-        HIPCHK(idx->qh.ensure((size_t)nq_pad * idx->dpad * sizeof(uint16_t)));
-        HIPCHK(idx->ql.ensure((size_t)nq_pad * idx->dpad * sizeof(uint16_t)));
-        const int64_t ne = nq_pad * idx->dpad;
-        k_split_bf16<<<(unsigned)((ne + 255) / 256), 256, 0, s>>>(Qn, nq_pad, idx->dpad, nullptr, idx->qh.as<uint16_t>(),
-                                                                 idx->ql.as<uint16_t>());
-    }
     HIPCHK(hipGetLastError());
     return WV_OK;
 }
@@ -1110,9 +1084,12 @@ static int bq_blockmin(wv_index* idx, hipStream_t s, const uint32_t* valid, int6
 // Phase 2: the R-heap replay of query group [g0, g0 + F) over this shard, from
 // heap states in_* (NULL = empty) [F][R]; pop = 1 writes the popped
 // candidates (pop order), 0 the heap states.  Ids are global (id_base + slot).
+// rec_*: record every insertion ([F][cap], count cap + 1 = overflow); out_n
+// may then be NULL (no state written).
 static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t g0, int F, const uint64_t* in_ids,
                      const float* in_d, const int32_t* in_len, int pop, uint64_t* out_ids, float* out_d,
-                     int32_t* out_n) {
+                     int32_t* out_n, uint64_t* rec_ids = nullptr, float* rec_d = nullptr, int32_t* rec_n = nullptr,
+                     int cap = 0) {
     const int64_t nq = idx->bq_nq;
     const int R = idx->bq_R;
     const int64_t nslots = idx->hiwater;
@@ -1130,7 +1107,8 @@ static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_
                                        (int)lds_r));                                                            \
         k_bq_replay<NWV><<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq,      \
                                                         qlist + g0, F, bm, nblk, R, idx->id_base, in_ids, in_d, \
-                                                        in_len, pop, out_ids, out_d, out_n);                    \
+                                                        in_len, pop, out_ids, out_d, out_n, rec_ids, rec_d,     \
+                                                        rec_n, cap);                                            \
     } while (0)
     switch (nw) {
     case 2: WV_RP(2); break;
@@ -1246,6 +1224,44 @@ extern "C" int wv_index_bq_replay(wv_index* idx, const uint64_t* d_in_ids, const
     hipStream_t s = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
     int rc = bq_replay(idx, s, idx->present, 0, (int)idx->bq_nq, d_in_ids, d_in_d, d_in_len, pop, d_out_ids, d_out_d,
                        d_out_len);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// parallel cross-shard BQ replay: per query the R smallest block minima of this
+// shard ([nq][R] ascending, +inf padded) -- upper bounds of distinct rows
+extern "C" int wv_index_bq_bounds(wv_index* idx, float* d_out, void* stream) {
+    if (!idx || !d_out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->bq_nq <= 0) return set_err(WV_ERR_INVALID, "bq_bounds: no batch begun");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t nblk = std::max<int64_t>((idx->hiwater + BQBLK - 1) / BQBLK, 1);
+    const int nbins = idx->words * 64 + 1;
+    const size_t lds = (size_t)nbins * sizeof(uint32_t);
+    if (lds > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_bq_bounds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_bq_bounds<<<(unsigned)idx->bq_nq, 256, lds, s>>>(idx->bqmin.as<float>(), nblk, nbins, idx->bq_R, d_out);
+    HIPCHK(hipGetLastError());
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// parallel cross-shard BQ replay: this shard's R-heap replay from heap states
+// d_in_* (k copies of a bound, by query), recording every insertion in id order
+// (ids, dists [nq][cap], counts [nq]; cap + 1 = the record overflowed)
+extern "C" int wv_index_bq_replay_record(wv_index* idx, const uint64_t* d_in_ids, const float* d_in_d,
+                                         const int32_t* d_in_len, int32_t cap, uint64_t* d_rec_ids, float* d_rec_d,
+                                         int32_t* d_rec_n, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (cap < 1 || !d_rec_ids || !d_rec_d || !d_rec_n) return set_err(WV_ERR_INVALID, "invalid record buffers");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->bq_nq <= 0) return set_err(WV_ERR_INVALID, "bq_replay_record: no batch begun");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = bq_replay(idx, s, idx->present, 0, (int)idx->bq_nq, d_in_ids, d_in_d, d_in_len, 0, nullptr, nullptr,
+                       nullptr, d_rec_ids, d_rec_d, d_rec_n, cap);
     if (rc) return rc;
     if (!stream) HIPCHK(hipStreamSynchronize(s));
     return WV_OK;
@@ -1691,41 +1707,107 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     const int32_t* qlist = idx->ident.as<int32_t>();
     const int64_t nslots = idx->hiwater;
     const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
+    HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
+    HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
+    HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
+    const int wrapm = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+    // the queries the exact heap replay below takes (every query, or the ones
+    // the PQ candidate path flags), and whether its outputs go by query
+    int64_t nrep = nq;
+    int rep_by_query = 0;
+    if (comp == WV_COMPRESSION_PQ && idx->pq_cand && R + 1 <= 64) {
+        // minima-only PQ search: block minima of every query (no B x N matrix),
+        // candidate blocks, exact ADC of their rows, strict order -> asc
+        const int m = idx->pq_m, K = idx->pq_ks;
+        const int64_t nblk = ld / EBLK;
+        HIPCHK(idx->rB.ensure((size_t)nq * nblk * sizeof(float)));
+        HIPCHK(idx->pqZero.ensure((size_t)std::max<int64_t>(nq, 1) * sizeof(float4)));
+        HIPCHK(idx->qsCand.ensure((size_t)nq * 64 * sizeof(uint32_t)));
+        HIPCHK(idx->qsNc.ensure((size_t)nq * sizeof(int32_t)));
+        HIPCHK(idx->qsEps.ensure((size_t)nq * sizeof(float)));
+        HIPCHK(idx->qsFlags.ensure((size_t)nq * sizeof(int32_t)));
+        HIPCHK(idx->oF.ensure((size_t)nq * sizeof(int32_t)));
+        HIPCHK(idx->qsList.ensure((size_t)nq * sizeof(int32_t)));
+        HIPCHK(idx->flCtr.ensure(2 * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(idx->pqZero.p, 0, (size_t)std::max<int64_t>(nq, 1) * sizeof(float4), s));
+        const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
+        dim3 grid2((unsigned)((nq + 1) / 2), (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
+        if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
+#define WV_ADC2M(KCV)                                                                                        \
+    do {                                                                                                     \
+        HIPCHK(hipFuncSetAttribute((const void*)k_pq_adc2<KCV, PQ_RPT>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                   (int)(2 * lds_adc)));                                                     \
+        k_pq_adc2<KCV, PQ_RPT><<<grid2, 256, 2 * lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,  \
+                                                               idx->lut.as<float>(), qlist, (int)nq, wrapm, ld, \
+                                                               nullptr, idx->rB.as<float>());                \
+    } while (0)
+        if (K == 256) WV_ADC2M(256);
+        else WV_ADC2M(0);
+#undef WV_ADC2M
+        HIPCHK(hipGetLastError());
+        if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
+        idx->stats.last_group_queries = (uint64_t)nq;
+        // blocks whose minimum is within a rounding-size eps of the (R+1)-th
+        // smallest (DOT: the key is the value; zero norms: eps = 4u)
+        const uint32_t* z = idx->pqZero.as<uint32_t>();
+        k_blk_select<2><<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(
+            idx->rB.as<float>(), nblk, nblk, (int)nq, R, DOT, idx->pqZero.as<float4>(), z, z + 3, 0.f, 0.f,
+            idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), idx->qsEps.as<float>(),
+            nullptr, nullptr, nullptr, nullptr);
+        HIPCHK(hipGetLastError());
+        int32_t* pflag = idx->oF.as<int32_t>();
+#define WV_PQC(KCV) k_pq_cand<KCV><<<(unsigned)nq, 256, 0, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots, idx->lut.as<float>(), idx->rB.as<float>(), nblk, idx->qsCand.as<uint32_t>(), 64, idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), R, wrapm, idx->id_base, idx->ascI.as<uint64_t>(), idx->ascD.as<float>(), idx->ascN.as<int32_t>(), pflag)
+        if (K == 256) WV_PQC(256);
+        else WV_PQC(0);
+#undef WV_PQC
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
+        k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(pflag, (int)nq, idx->qsList.as<int32_t>(),
+                                                                  idx->flCtr.as<uint32_t>(), 0);
+        HIPCHK(hipGetLastError());
+        uint32_t nf = 0;
+        HIPCHK(hipMemcpyAsync(&nf, idx->flCtr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        nrep = nf;
+        rep_by_query = 1;
+        qlist = idx->qsList.as<int32_t>();
+        idx->stats.replayed_queries += nf;
+    } else if (comp == WV_COMPRESSION_PQ) {
+        idx->stats.replayed_queries += (uint64_t)nq;
+    }
     // query groups sized to the free HBM (two distance buffers), multiples of
     // RQ_QPB for the thread-per-row kernels
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     const int64_t have = (int64_t)(Eb0_bytes(idx) + free_b / 4);
     const int64_t budget = std::max<int64_t>(std::min<int64_t>(16ll << 30, have), 1ll << 30);
-    int64_t G = std::max<int64_t>(1, std::min<int64_t>(nq, budget / (ld * 4)));
+    int64_t G = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(nrep, 1), budget / (ld * 4)));
     if (comp != WV_COMPRESSION_PQ) {
         G = std::max<int64_t>(RQ_QPB, G / RQ_QPB * RQ_QPB);
         G = std::min<int64_t>(G, round_up(nq, RQ_QPB));
     }
-    idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(G, nq);
+    if (!rep_by_query) idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(G, nq);
     rc = ensure_aux(idx);
     if (rc) return rc;
     DBuf* Eb[2] = {&idx->rE, &idx->rE2};
     DBuf* Bb[2] = {&idx->rB, &idx->rB2};
-    for (int b = 0; b < 2; b++) {
-        HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
-        HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
-    }
-    HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
-    HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
-    HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
-    const int wrapm = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+    if (nrep > 0)
+        for (int b = 0; b < 2; b++) {
+            HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
+            HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+        }
     const size_t lds_rep = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
     if (lds_rep > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rep));
     int64_t gi = 0;
-    for (int64_t g0 = 0; g0 < nq; g0 += G, gi++) {
-        const int F = (int)std::min<int64_t>(G, nq - g0);
+    for (int64_t g0 = 0; g0 < nrep; g0 += G, gi++) {
+        const int F = (int)std::min<int64_t>(G, nrep - g0);
         const int b = (int)(gi & 1);
         float* E = Eb[b]->as<float>();
         float* Bm = Bb[b]->as<float>();
         if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
-        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
+        const bool time_it = idx->timing && g0 == 0 && !rep_by_query;
+        if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
         if (comp == WV_COMPRESSION_PQ) {
             const int m = idx->pq_m, K = idx->pq_ks;
             const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
@@ -1762,18 +1844,21 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
                                            nq, g0, F, ld, E, Bm);
         }
         HIPCHK(hipGetLastError());
-        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
+        if (time_it) HIPCHK(hipEventRecord(idx->ev1, s));
         HIPCHK(hipEventRecord(idx->evd[b], s));
         HIPCHK(hipStreamWaitEvent(idx->aux, idx->evd[b], 0));
         // the worker heap (addResult == insertToHeap) in id order, extracted ascending
+        // (rows by list position, or by query for the PQ candidate path's flagged list)
+        const int64_t ao = rep_by_query ? 0 : g0;
         k_replay_scan<<<F, 64, lds_rep, idx->aux>>>(E, Bm, valid, nslots, ld, qlist + g0, F, R, idx->id_base, nullptr,
-                                                    nullptr, nullptr, 1, 0, R, idx->ascI.as<uint64_t>() + g0 * R,
-                                                    idx->ascD.as<float>() + g0 * R, idx->ascN.as<int32_t>() + g0, 0, 0,
-                                                    nullptr, nullptr, nullptr, 0);
+                                                    nullptr, nullptr, 1, rep_by_query, R,
+                                                    idx->ascI.as<uint64_t>() + ao * R, idx->ascD.as<float>() + ao * R,
+                                                    idx->ascN.as<int32_t>() + ao, 0, 0, nullptr, nullptr, nullptr, 0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
     }
     for (int b = 0; b < 2 && b < gi; b++) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
+    qlist = idx->ident.as<int32_t>();
     HIPCHK(idx->cslot.ensure((size_t)nq * R * sizeof(uint32_t)));
     HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
     const size_t lds_f = (size_t)R * (sizeof(uint64_t) + sizeof(float)) + 16;
@@ -2420,7 +2505,11 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         a.ldk = ldk;
         a.nslots = nslots;
         a.dbg = idx->sel_dbg;
-        a.nqg = (int)(cn_pad / QS_QPB);
+        // k_qs_blockkey_w4 for d > 768: 128-query workgroups, a 32-row block in two
+        // column parts per ring step: dpb 1024 -> 4 slots of 32 KiB, 1536 -> 3 of 48 KiB
+        const bool w4 = idx->dpb > QS_W4_DPB;
+        const int w4_nb = NK == 64 ? 4 : 3;
+        a.nqg = (int)(cn_pad / (w4 ? 128 : QS_QPB));
         int64_t nspans = 256 / std::gcd(256, a.nqg);
         while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
         if (idx->spans_opt > 0) nspans = idx->spans_opt;
@@ -2434,7 +2523,8 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
         a.slots_per_span = (int)sps;
         a.nspans = (int)((nslots + sps - 1) / sps);
         const bool l2 = metric == L2;
-        const size_t lds = (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
+        const size_t lds = w4 ? (size_t)w4_nb * (NK / 4) * 2048 + 256 + (l2 ? (size_t)4 * 4 * 128 : 0)
+                              : (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
         dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
         if (phase != 2) {
         const bool time_it = idx->timing && c0 == 0;
@@ -2458,7 +2548,17 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
     case 40: WV_QS(40, L2V); break;                    \
     default: WV_QS(48, L2V); break;                    \
     }
-        if (idx->sel_dbg > 0 && !l2 && NK == 48) {  // timing experiments (k_qs_blockkey DBG)
+#define WV_QSW(NKV, L2V, NBV)                                                                                  \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_qs_blockkey_w4<NKV, L2V, 2, NBV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_qs_blockkey_w4<NKV, L2V, 2, NBV><<<grid, 256, lds, s>>>(a);                                          \
+    } while (0)
+#define WV_QSWN(L2V)                                   \
+    if (NK == 64) WV_QSW(64, L2V, 4); else WV_QSW(96, L2V, 3);
+        if (w4) {
+            if (l2) { WV_QSWN(true); } else { WV_QSWN(false); }
+#ifdef WV_QS_DBG  // timing experiments (k_qs_blockkey DBG bits), not in the product build
+        } else if (idx->sel_dbg > 0 && !l2 && NK == 48) {
             switch (idx->sel_dbg) {
             case 1: WV_QS3(48, false, 1); break;
             case 2: WV_QS3(48, false, 2); break;
@@ -2468,10 +2568,13 @@ static int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, 
             case 6: WV_QS3(48, false, 6); break;
             default: WV_QS3(48, false, 7); break;
             }
+#endif
         } else if (l2) { WV_QSN(true); } else { WV_QSN(false); }
 #undef WV_QSN
 #undef WV_QS3
 #undef WV_QS
+#undef WV_QSWN
+#undef WV_QSW
         HIPCHK(hipGetLastError());
         if (time_it) { HIPCHK(hipEventRecord(idx->ev1, s)); idx->timed = 1; }
         idx->stats.mfma_launches++;
@@ -2603,7 +2706,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     if (qd != idx->dims)
         return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)qd, idx->dims);
     if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
-    const int64_t nq_pad = round_up(nq, QBW);  // 256: the wide bf16x3 tile; a multiple of QB
+    const int64_t nq_pad = round_up(nq, QS_QPB);  // 256: a block-key query group; a multiple of QB
     int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
     if (rc) return rc;
     const float* Qn = idx->qn.as<float>();
@@ -2623,34 +2726,26 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     int32_t* flags = o_flags ? o_flags : idx->oF.as<int32_t>();
 
     if (mfma_ok) {
+        // kernel 3: the f32 MFMA select (k_mfma_select3); 6: the HBM-streaming GEMV
+        // select for small batches (k_gemv_select); auto picks by batch size
         int kver = idx->kernel_opt == 7 ? 0 : idx->kernel_opt;
-        if (kver == 0) kver = nq <= idx->gemv_max ? 6 : idx->use_bf3 ? (nq > QB ? 5 : 4) : 3;
-        if ((kver == 4 || kver == 5) && !idx->use_bf3) kver = 3;
+        if (kver == 0) kver = nq <= idx->gemv_max ? 6 : 3;
         const bool gemv = kver == 6;
         // GEMV: QG queries per workgroup staged in LDS (<= 64 KiB of query rows)
         // (the smallest of 1/2/4/8 covering nq: padded query columns cost FMAs and LDS reads)
         int gqg = nq <= 1 ? 1 : nq <= 2 ? 2 : nq <= 4 ? 4 : 8;
         while (gqg > 1 && (int64_t)gqg * idx->dpad * 4 > 65536) gqg >>= 1;
-        const int64_t bn = kver >= 3 ? BN3 : BN;
-        const int64_t ntiles = (idx->hiwater + bn - 1) / bn;
-        const int qtile = gemv ? gqg : kver == 5 ? QBW : QB;
+        const int64_t ntiles = (idx->hiwater + BN3 - 1) / BN3;
+        const int qtile = gemv ? gqg : QB;
         const int nqb = (int)(round_up(nq, qtile) / qtile);
         int qgroup = 1;
         for (int g : {4, 2, 1})
             if (nqb % g == 0) { qgroup = g; break; }
         if (idx->qgroup_opt > 0 && nqb % idx->qgroup_opt == 0) qgroup = idx->qgroup_opt;
-        // ~1024 workgroups (2 per CU resident, 2 waves of them); keep the
+        // ~768 workgroups for the MFMA select (2 per CU resident); keep the
         // workgroup count a multiple of 8 for the XCD mapping when possible
-        // (k_mfma_select_bf3w: one 1024-wide wave of resident workgroups, 256
-        // = one per CU, measured fastest; its 32-bit span offsets need a span
-        // below 4 GiB of one plane)
-        const int64_t target_wg = gemv ? idx->gemv_wg : kver == 5 ? 256 : kver >= 3 ? 768 : 1024;
+        const int64_t target_wg = gemv ? idx->gemv_wg : 768;
         int64_t nspans = idx->spans_opt > 0 ? idx->spans_opt : std::max<int64_t>(8, (target_wg + nqb - 1) / nqb);
-        if (kver == 5) {
-            const int64_t tile_bytes = (int64_t)(idx->dpad / 16) * 8192;
-            const int64_t max_tps = ((int64_t)1 << 32) / tile_bytes - 1;
-            nspans = std::max<int64_t>(nspans, (ntiles + max_tps - 1) / max_tps);
-        }
         nspans = std::min<int64_t>(nspans, ntiles);
         int64_t tps = (ntiles + nspans - 1) / nspans;
         nspans = (ntiles + tps - 1) / tps;
@@ -2664,18 +2759,11 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         a.Q = Qn; a.qnorm2 = idx->qn2.as<float>(); a.nq = (int)nq; a.dpad = idx->dpad;
         a.tiles_per_span = (int)tps; a.nspans = (int)nspans; a.nqb = nqb; a.KP = KP; a.qgroup = qgroup;
         a.outA = idx->spanA.as<float>(); a.outI = idx->spanI.as<uint32_t>();
-        a.Xh = idx->Xh; a.Xl = idx->Xl; a.Qh = idx->qh.as<uint16_t>(); a.Ql = idx->ql.as<uint16_t>();
         a.dbg = idx->sel_dbg;
         a.opt = idx->sel_opt;
-        // candidate buffer: as large as fits two workgroups per CU (<= 80 KiB each)
-        const bool v2 = kver == 2;
-        const int64_t fixed = kver == 5 ? (int64_t)NBUFW * SLOT_BW + (int64_t)(QBW * 2 + 4) * (int64_t)sizeof(float)
-                              : kver == 4 ? (int64_t)NBUF3 * SLOT_BF3 + (int64_t)(QB * 2 + 4) * (int64_t)sizeof(float)
-                              : kver == 3 ? (int64_t)(NBUF3 * STG3 + QB * 2 + 4) * (int64_t)sizeof(float)
-                              : v2 ? (int64_t)(2 * (BN + QB) * BK + QB * 2 + 4) * (int64_t)sizeof(float)
-                                   : (int64_t)(2 * QB * LDSROW + QB * KP * 2 + QB * 2 + 4) * (int64_t)sizeof(float);
-        const int64_t budget = kver >= 3 ? 160 * 1024 : 80 * 1024;
-        int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(4, (budget - fixed) / (qtile * 8)));
+        // candidate buffer: as large as fits the LDS left by the staging ring
+        const int64_t fixed = (int64_t)(NBUF3 * STG3 + QB * 2 + 4) * (int64_t)sizeof(float);
+        int C = (int)std::min<int64_t>(64 - KP, std::max<int64_t>(4, (160 * 1024 - fixed) / (qtile * 8)));
         if (idx->cbuf_opt > 0) C = std::min(64 - KP, idx->cbuf_opt);
         size_t lds = (size_t)(fixed + (int64_t)qtile * C * 8);
         if (gemv) {  // a 32-row chunk adds <= 32 candidates per query: C = 64 - KP >= 32 never overflows
@@ -2685,25 +2773,10 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         a.C = C;
         dim3 grid((unsigned)(nqb * nspans));
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
-#define WV_SEL(KER, M)                                                                                       \
-    do {                                                                                                     \
-        HIPCHK(hipFuncSetAttribute((const void*)KER<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-        KER<M, 1><<<grid, 256, lds, s>>>(a);                                                                 \
-    } while (0)
 #define WV_SEL3(M)                                                                                        \
     do {                                                                                                  \
         HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select3<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
         k_mfma_select3<M, 1><<<grid, 512, lds, s>>>(a);                                                   \
-    } while (0)
-#define WV_SELB(M)                                                                                         \
-    do {                                                                                                   \
-        HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select_bf3<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-        k_mfma_select_bf3<M, 1><<<grid, 512, lds, s>>>(a);                                                 \
-    } while (0)
-#define WV_SELW(M)                                                                                         \
-    do {                                                                                                   \
-        HIPCHK(hipFuncSetAttribute((const void*)k_mfma_select_bf3w<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-        k_mfma_select_bf3w<M, 1><<<grid, 512, lds, s>>>(a);                                                \
     } while (0)
 #define WV_GEMV(M, G)                                                                                      \
     do {                                                                                                   \
@@ -2723,37 +2796,16 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
             case WV_METRIC_DOT: WV_GEMVQ(DOT); break;
             default: WV_GEMVQ(COSINE); break;
             }
-        } else if (kver == 5) {
-            switch (idx->metric) {
-            case WV_METRIC_L2_SQUARED: WV_SELW(L2); break;
-            case WV_METRIC_DOT: WV_SELW(DOT); break;
-            default: WV_SELW(COSINE); break;
-            }
-        } else if (kver == 4) {
-            switch (idx->metric) {
-            case WV_METRIC_L2_SQUARED: WV_SELB(L2); break;
-            case WV_METRIC_DOT: WV_SELB(DOT); break;
-            default: WV_SELB(COSINE); break;
-            }
-        } else if (kver == 3) {
+        } else {
             switch (idx->metric) {
             case WV_METRIC_L2_SQUARED: WV_SEL3(L2); break;
             case WV_METRIC_DOT: WV_SEL3(DOT); break;
             default: WV_SEL3(COSINE); break;
             }
-        } else {
-            switch (idx->metric) {
-            case WV_METRIC_L2_SQUARED: if (v2) WV_SEL(k_mfma_select2, L2); else WV_SEL(k_mfma_select, L2); break;
-            case WV_METRIC_DOT: if (v2) WV_SEL(k_mfma_select2, DOT); else WV_SEL(k_mfma_select, DOT); break;
-            default: if (v2) WV_SEL(k_mfma_select2, COSINE); else WV_SEL(k_mfma_select, COSINE); break;
-            }
         }
 #undef WV_GEMVQ
 #undef WV_GEMV
-#undef WV_SELW
-#undef WV_SELB
 #undef WV_SEL3
-#undef WV_SEL
         HIPCHK(hipGetLastError());
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
         idx->stats.mfma_launches++;
@@ -2789,16 +2841,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         HIPCHK(hipStreamSynchronize(s));
         float maxn2;
         memcpy(&maxn2, &mx, sizeof(float));
-        // bf16x3 (kver 4): + 2 x (3.05 * 2^-16 split error + gamma'_h accumulation).  Each
-        // product passes through at most h = 3*dpad/16 + 16 additions (the 3*dpad/16 chained
-        // MFMAs that add into the accumulator, plus at most 16 inside one MFMA's 16-product
-        // sum), so the recursive-summation bound is gamma_h * sum|terms| for any internal
-        // order; u' = 2^-22 (4x the fp32 unit roundoff) assumes nothing about the rounding mode.
-        const double u4 = 2.384185791015625e-07;
-        const double hdep = 3.0 * idx->dpad / 16.0 + 16.0;
-        const double g3 = hdep * u4 / (1.0 - hdep * u4);
-        const double extra = (kver == 4 || kver == 5) ? 2.0 * (3.05 * 1.52587890625e-05 + g3) : 0.0;
-        const float eps_scale = (float)((2.0 * gamma_n(idx->dpad + 4) + extra) * 1.05 + 1e-12);
+        const float eps_scale = (float)(2.0 * gamma_n(idx->dpad + 4) * 1.05 + 1e-12);
         const float eps_base = (float)(std::sqrt((double)maxn2) * (1.0 + 1e-6));
         idx->last_eps_scale = eps_scale;
         idx->last_eps_base = eps_base;
@@ -3053,7 +3096,7 @@ extern "C" int wv_index_shard_phase1(wv_index* idx, const float* d_queries, int6
     if (d != idx->dims)
         return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
     if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
-    int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QBW));
+    int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QS_QPB));
     if (rc) return rc;
     idx->stats.queries += (uint64_t)nq;
     idx->stats.batches++;

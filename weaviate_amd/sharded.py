@@ -219,6 +219,24 @@ class GpuBQShardBackend(GpuShardBackend):
                                                dd.data_ptr(), ln.data_ptr(), self._s()))
         return ids, dd, ln
 
+    def bq_bounds(self):
+        """[nq, R] ascending: the R smallest block minima of this shard (+inf padded)."""
+        R = self.R(self.k)
+        out = torch.empty((self.nq, R), dtype=torch.float32, device=self.dev)
+        self._check(self._l.wv_index_bq_bounds(self.index._h, out.data_ptr(), self._s()))
+        return out
+
+    def bq_replay_record(self, state, cap: int):
+        """This shard's R-heap replay from `state` (by query), recording every
+        insertion: (ids [nq, cap], dists, n [nq]), n = cap + 1 on overflow."""
+        ri = torch.empty((self.nq, cap), dtype=torch.int64, device=self.dev)
+        rd = torch.empty((self.nq, cap), dtype=torch.float32, device=self.dev)
+        rn = torch.empty(self.nq, dtype=torch.int32, device=self.dev)
+        self._check(self._l.wv_index_bq_replay_record(self.index._h, state[0].data_ptr(), state[1].data_ptr(),
+                                                      state[2].data_ptr(), cap, ri.data_ptr(), rd.data_ptr(),
+                                                      rn.data_ptr(), self._s()))
+        return ri, rd, rn
+
     def bq_rescore(self, ids, ln):
         E = torch.zeros(ids.shape, dtype=torch.float32, device=self.dev)
         self._check(self._l.wv_index_bq_rescore(self.index._h, ids.data_ptr(), ln.data_ptr(), E.data_ptr(),
@@ -240,11 +258,18 @@ class ShardedBQSearch:
     the single index's exact semantics (flat/index.go:460-532):
       1. every rank: query codes + hamming block minima of its shard (parallel,
          the expensive VALU pass);
-      2. the R-heap is replayed across the ranks in id order: rank r continues
-         rank r-1's heap states (broadcast over RCCL, B*R*16 bytes), the last
-         rank pops it in the reference's pop order;
-      3. every rank rescores the candidates it holds (exact SingleDist),
-         all-gather of the [B][R] distance tiles;
+      2. the R-heap over all shards in id order, in one parallel hop (backends
+         with bq_replay_record): each rank's R smallest block minima are
+         all-gathered; rank r >= 1 replays its range from R copies of T_r (the
+         R-th smallest minimum of the ranks before it: distances of distinct
+         rows, so T_r >= the real heap top at its first row) and records every
+         insertion; rank 0 replays from empty heaps; one all-gather of the
+         records, and every rank applies them on rank 0's states in rank
+         order (wv_heap_merge_records) -- the serial chain's heaps.  A record
+         that overflows its cap sends the batch down the serial chain (rank r
+         continues rank r-1's heap states, one broadcast per hop);
+      3. every rank rescores the candidates it holds (exact SingleDist) in the
+         reference's pop order, all-gather of the [B][R] distance tiles;
       4. the rescoring heap (insertToHeap in pop order, extractHeap)."""
 
     def __init__(self, backend, device: torch.device, id_stride: int):
@@ -261,6 +286,48 @@ class ShardedBQSearch:
         nq = q.shape[0]
         R = self.b.R(k)
         self.b.bq_begin(q, k)
+        self.path = "chain"
+        if getattr(self.b, "bq_replay_record", None) is not None and self.world > 1:
+            res = self._replay_parallel(nq, R)
+            if res is not None:
+                self.path = "parallel"
+                ids, ln = res
+                E = self.b.bq_rescore(ids, ln)
+                E_all = self._all_gather(E)
+                return self.b.bq_final(self.world, self.id_stride, ids, ln, E_all)
+        return self._chain(q, nq, R)
+
+    def _replay_parallel(self, nq: int, R: int):
+        """Step 2 in one hop; -> (candidate ids in pop order [nq, R], lengths)
+        or None when a record overflowed (host sync: one flag)."""
+        cap = 2 * R
+        G = self._all_gather(self.b.bq_bounds())  # [W, nq, R]
+        if self.rank == 0:
+            ti, td, tn = self.b.bq_replay(None, False)  # heap states from empty heaps
+            ri = torch.zeros((nq, cap), dtype=torch.int64, device=self.dev)
+            rd = torch.zeros((nq, cap), dtype=torch.float32, device=self.dev)
+            ri[:, :R], rd[:, :R] = ti, td
+            rn = tn
+        else:
+            allq = torch.arange(nq, device=self.dev)
+            T = prefix_bound(self.rank, allq, R, G, torch.full((self.rank, nq), R, dtype=torch.int32, device=self.dev),
+                             torch.zeros((self.rank, nq), dtype=torch.int32, device=self.dev))
+            ri, rd, rn = self.b.bq_replay_record(fake_heaps(T, R), cap)
+        pk = torch.cat([ri.contiguous().view(torch.int32).reshape(nq, 2 * cap), rd.contiguous().view(torch.int32),
+                        rn[:, None]], 1)
+        A = self._all_gather(pk)  # [W, nq, 3 cap + 1]
+        rec = (A[..., : 2 * cap].contiguous().view(torch.int64), A[..., 2 * cap: 3 * cap].contiguous().view(torch.float32),
+               A[..., 3 * cap].contiguous())
+        st = (rec[0][0, :, :R].contiguous(), rec[1][0, :, :R].contiguous(), rec[2][0].contiguous())
+        ai, _, an, un = self.b.merge_records(self.world, R, cap, st, rec)  # extracted ascending
+        if bool(un.any()):
+            return None
+        # pop order (max first) = the ascending extraction read back to front
+        back = (an[:, None].long() - 1 - torch.arange(R, device=self.dev)[None, :]).clamp(min=0)
+        return ai.gather(1, back), an
+
+    def _chain(self, q: torch.Tensor, nq: int, R: int):
+        """Step 2 as the serial chain: rank r continues rank r-1's heaps."""
         state = None
         for r in range(self.world):
             last = r == self.world - 1
