@@ -1,14 +1,19 @@
 #!/bin/bash
-# k_qs_blockkey_w4 (d > 768): parity tests, C3 + d = 1024 / 1536 benches with kernel stats, then
-# PMC passes of the d = 1024 kernel (MFMA busy, waits, LDS, L2 hit/miss)
+# k_qs_blockkey_w4 (d > 768) + the minima-only PQ search: parity tests, benches (d = 1024 / 1536 with
+# kernel stats, C5 PQ with both search forms), then PMC passes of the d = 1024 kernel
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-w4}; mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_gpu_flat.py -m gpu -x -v -k "above_768 or select_kernel or proof_bound or removed" --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_flat.py tests/test_gpu_pq.py tests/test_gpu_hnsw_flat.py tests/test_gpu_scale.py -m gpu -x -v -k "above_768 or select_kernel or proof_bound or removed or pq" --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+summ() { python3 -c "import json,sys; r=json.load(open('$1')); print('$2', round(r['value']), 'qps', round(r['ms_per_step'],2), 'ms', r['roofline'].get('launch_ms'), r['roofline'].get('frac'), r.get('verified'))"; }
 for D in 1024 1536; do
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$D -o run --output-format csv -- python3 bench.py --dims $D --no-cpu-baseline > $O/bench_$D.json 2> $O/bench_$D.err || { tail $O/bench_$D.err; exit 1; }
-python3 -c "import json,sys; r=json.load(open('$O/bench_$D.json')); print('d=$D', round(r['value']), 'qps', round(r['ms_per_step'],2), 'ms', r['roofline'].get('launch_ms'), r['roofline'].get('frac'), r.get('verified'))"
+summ $O/bench_$D.json d=$D
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pq -o run --output-format csv -- python3 bench.py --workload pq --no-cpu-baseline > $O/bench_pq.json 2> $O/bench_pq.err || { tail $O/bench_pq.err; exit 1; }
+summ $O/bench_pq.json pq_cand
+timeout -k 10 300 python3 bench.py --workload pq --no-cpu-baseline --option pq_cand=0 > $O/bench_pq0.json 2> $O/bench_pq0.err || { tail $O/bench_pq0.err; exit 1; }
+summ $O/bench_pq0.json pq_matrix
 i=0
 for grp in "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
            "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA" \

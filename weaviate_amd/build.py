@@ -12,21 +12,13 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libwvknn.so")
-SOURCES = [
-    os.path.join(HERE, "csrc", "runtime.hip"),
-    os.path.join(HERE, "csrc", "kernels.hip"),
-    os.path.join(HERE, "csrc", "bq_kernels.hip"),
-    os.path.join(HERE, "csrc", "pq_kernels.hip"),
-    os.path.join(HERE, "csrc", "kernels_bf3.hip"),
-    os.path.join(HERE, "csrc", "rq_kernels.hip"),
-    os.path.join(HERE, "csrc", "lsm_segment.hip"),
-    os.path.join(HERE, "csrc", "batcher.hip"),
-    os.path.join(HERE, "csrc", "gemv_kernels.hip"),
-    os.path.join(HERE, "csrc", "qs_kernels.hip"),
-    os.path.join(HERE, "csrc", "sq_kernels.hip"),
-    os.path.join(HERE, "csrc", "wv_device.h"),
-    os.path.join(REPO, "include", "wv_knn.h"),
-]
+# translation units compiled in parallel (see csrc/rt_index.h) and linked into one library
+UNITS = ["runtime.hip", "qs_runtime.hip", "qs_exact.hip", "qs_replay.hip", "quant_runtime.hip"]
+SOURCES = [os.path.join(HERE, "csrc", f) for f in (
+    "runtime.hip", "qs_runtime.hip", "qs_exact.hip", "qs_replay.hip", "quant_runtime.hip", "rt_index.h", "kernels.hip", "bq_kernels.hip",
+    "pq_kernels.hip", "kernels_bf3.hip", "rq_kernels.hip", "lsm_segment.hip", "batcher.hip", "gemv_kernels.hip",
+    "qs_kernels.hip", "sq_kernels.hip", "vector_index.hip", "wv_device.h")] + [os.path.join(REPO, "include", "wv_knn.h")]
+OBJDIR = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [
     "--offload-arch=gfx950",
@@ -34,7 +26,6 @@ FLAGS = [
     "-std=c++17",
     "-ffp-contract=off",  # exact-order kernels: the only fused ops are explicit fmaf()
     "-fPIC",
-    "-shared",
     "-Wno-unused-value",
     "-Wno-unused-result",
 ]
@@ -49,7 +40,19 @@ def needs_rebuild() -> bool:
 
 def build_library(force: bool = False, verbose: bool = True) -> str:
     if force or needs_rebuild():
-        cmd = [HIPCC, *FLAGS, "-I" + os.path.join(REPO, "include"), SOURCES[0], "-o", LIB + ".tmp"]
+        os.makedirs(OBJDIR, exist_ok=True)
+        procs, objs = [], []
+        for u in UNITS:
+            obj = os.path.join(OBJDIR, u.replace(".hip", ".o"))
+            cmd = [HIPCC, *FLAGS, "-I" + os.path.join(REPO, "include"), "-c", os.path.join(HERE, "csrc", u), "-o", obj]
+            if verbose:
+                print("[weaviate_amd] " + " ".join(cmd), file=sys.stderr)
+            procs.append((u, subprocess.Popen(cmd)))
+            objs.append(obj)
+        failed = [u for u, p in procs if p.wait() != 0]
+        if failed:
+            raise subprocess.CalledProcessError(1, "hipcc " + " ".join(failed))
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
         if verbose:
             print("[weaviate_amd] " + " ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

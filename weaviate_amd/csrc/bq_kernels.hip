@@ -28,6 +28,7 @@
 #pragma once
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 constexpr int BQBLK = 256;  // rows per block minimum (== EBLK)
 
@@ -374,4 +375,5 @@ __global__ __launch_bounds__(64) void k_bq_final(const uint64_t* __restrict__ ca
     out_n[q] = m;
 }
 
+}  // namespace
 }  // namespace wv

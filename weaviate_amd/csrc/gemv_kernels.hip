@@ -19,7 +19,9 @@
 // since KP <= 32), so the candidate buffer never overflows; a merge pass runs
 // only after chunks that produced candidates.
 // ---------------------------------------------------------------------------
+#pragma once
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 template <int METRIC, int QG>
 __global__ __launch_bounds__(256) void k_gemv_select(SelectArgs a) {
@@ -144,4 +146,5 @@ __global__ __launch_bounds__(256) void k_gemv_select(SelectArgs a) {
     }
 }
 
+}  // namespace
 }  // namespace wv

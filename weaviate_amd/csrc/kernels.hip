@@ -19,12 +19,14 @@
 //   k_replay_scan       then an exact replay of the reference heap
 //                       (priorityqueue NewMax + insertToHeap) over the id-ordered
 //                       scan, skipping 256-row blocks that cannot insert.
+#pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "wv_device.h"
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -938,4 +940,5 @@ __global__ void k_gen(int kind, uint64_t seed, uint64_t row0, int64_t rows, int 
     out[i] = gen_value(kind, seed, row0 + r, c);
 }
 
+}  // namespace
 }  // namespace wv

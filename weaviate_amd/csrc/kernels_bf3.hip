@@ -11,6 +11,7 @@
 #pragma once
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 
@@ -68,4 +69,5 @@ __device__ __forceinline__ bf16x8_t lds_ld8bf_o(unsigned base) {
     return v;
 }
 
+}  // namespace
 }  // namespace wv

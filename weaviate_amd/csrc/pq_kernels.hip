@@ -24,6 +24,7 @@
 #pragma once
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 constexpr int KM_T = 256;  // threads per k-means workgroup; k <= 256 (NewProductQuantizer)
 
@@ -649,4 +650,5 @@ __global__ __launch_bounds__(64) void k_pq_rescore_final(const uint32_t* __restr
     out_n[q] = m;
 }
 
+}  // namespace
 }  // namespace wv

@@ -1,0 +1,37 @@
+// qs_exact.hip -- the block-key path's exact pass: reference-order fp32
+// distances of the candidate blocks' rows and the verified top-(k+1)
+// (k_blk_exact), and the block-major distance pass that feeds it
+// (k_exact_bm) (see rt_index.h for the unit split).
+#include "rt_index.h"
+
+// k_blk_exact<RV, METRIC, VARIANT> over the queries of one chunk (list ==
+// nullptr) or the listed ones; eb/ldE: block-major distances, capv: the per
+// query cap of the (k+1)-th exact distance (nullptr: uncapped)
+void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
+                      const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
+                      int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
+                      const float* capv) {
+#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv)
+#define WV_EXM(RV)                                                          \
+    switch (metric) {                                                       \
+    case L2: if (v5) WV_EXR(RV, L2, AVX512); else WV_EXR(RV, L2, AVX256); break;   \
+    case DOT: if (v5) WV_EXR(RV, DOT, AVX512); else WV_EXR(RV, DOT, AVX256); break; \
+    default: if (v5) WV_EXR(RV, COSINE, AVX512); else WV_EXR(RV, COSINE, AVX256); break; \
+    }
+    if (RV == 2) { WV_EXM(2); } else if (RV == 4) { WV_EXM(4); } else { WV_EXM(8); }
+#undef WV_EXM
+#undef WV_EXR
+}
+
+// k_exact_bm<METRIC, VARIANT>: every listed (query, row) distance of each
+// candidate block, one workgroup per block (the block staged in LDS once)
+void launch_exact_bm(wv_index* idx, hipStream_t s, int metric, bool v5, const float* Qn, int64_t nb, size_t bm_lds,
+                     int64_t ldE) {
+#define WV_BM(M, V) k_exact_bm<M, V><<<(unsigned)nb, 256, bm_lds, s>>>(idx->X, idx->dpad, idx->hiwater, Qn, idx->dims, idx->bmOff.as<uint32_t>(), idx->bmPairs.as<uint32_t>(), ldE, idx->bmE.as<float>())
+    switch (metric) {
+    case L2: if (v5) WV_BM(L2, AVX512); else WV_BM(L2, AVX256); break;
+    case DOT: if (v5) WV_BM(DOT, AVX512); else WV_BM(DOT, AVX256); break;
+    default: if (v5) WV_BM(COSINE, AVX512); else WV_BM(COSINE, AVX256); break;
+    }
+#undef WV_BM
+}

@@ -26,6 +26,7 @@
 #include <type_traits>
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
 template <int I, int N, class F>
@@ -2087,4 +2088,5 @@ __global__ __launch_bounds__(64) void k_heap_merge_records(int nlist, int k, int
     out_n[li] = n;
 }
 
+}  // namespace
 }  // namespace wv

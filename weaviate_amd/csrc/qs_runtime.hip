@@ -1,0 +1,500 @@
+// qs_runtime.hip -- the block-key exact search (search_qs), its bounded heap
+// replays, the sharded two-phase search and the cross-shard replay / merge
+// entry points (see rt_index.h for the unit split).
+#include "rt_index.h"
+
+int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : 0; }
+
+// phase 0: the whole search.  Sharded two-phase form (mode 1, one query chunk):
+// phase 1 = block keys + local candidate selection, topA [nq][k+1] = this
+// shard's k+1 smallest block-key A values (eps in idx->qsEps); phase 2 = the
+// global threshold from every shard's topA / eps (gA [W][nq][k+1], gE [W][nq],
+// k_blk_gthresh), exact distances, overflow pass.
+int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid,
+                     uint64_t* o_ids, float* o_d, int32_t* o_n, int32_t* o_flags, int phase,
+                     float* topA, const float* gA, const float* gE, int W) {
+    const int kout = mode == 1 ? k + 1 : k;
+    const int NK = idx->dpb / 16;
+    const int RB = qs_rb(NK);
+    const int R = qs_R(k);
+    const int L = 64 * (R - 1);
+    const int64_t nslots = std::max<int64_t>(1, (idx->hiwater + 32 * RB - 1) / (32 * RB));
+    const int64_t nb = nslots * RB;  // 32-row blocks scanned = key row length
+    const int64_t ldk = nb;
+    // query chunks of 256-multiples whose key rows fit 16 GiB (10M rows: 13k queries per chunk)
+    const int64_t qmax = std::max<int64_t>(QS_QPB, ((16ll << 30) / (ldk * 4)) / QS_QPB * QS_QPB);
+    const int64_t qc = std::min<int64_t>(round_up(nq, QS_QPB), qmax);
+    idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(qc, nq);  // the timed block-key launch
+    HIPCHK(idx->qsQb.ensure((size_t)qc * idx->dpb * sizeof(uint16_t)));
+    HIPCHK(idx->qsInfo.ensure((size_t)qc * sizeof(float4)));
+    HIPCHK(idx->qsKey.ensure((size_t)qc * ldk * sizeof(float)));
+    HIPCHK(idx->qsCand.ensure((size_t)qc * std::max(L, 448) * sizeof(uint32_t)));  // 448: the overflow pass
+    HIPCHK(idx->qsNc.ensure((size_t)qc * sizeof(int32_t)));
+    HIPCHK(idx->qsEps.ensure((size_t)qc * sizeof(float)));
+    HIPCHK(idx->qsCap.ensure((size_t)qc * sizeof(float)));
+    HIPCHK(idx->qsList.ensure((size_t)2 * qc * sizeof(int32_t)));
+    if (!o_flags || phase) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
+    if (phase && qc < nq) return set_err(WV_ERR_UNSUPPORTED, "two-phase shard search: batch exceeds one query chunk");
+    const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
+    if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
+    // error-bound constants: reference-order fp32 (gamma_{dpb+8}) and the MFMA's
+    // fp32 accumulation over NK chained 16-deep products (u' = 2^-22)
+    const double u4 = 2.384185791015625e-07;
+    const double hdep = NK + 16.0;
+    const float gacc = (float)(hdep * u4 / (1.0 - hdep * u4));
+    const float gd = (float)gamma_n(idx->dpb + 8);
+    const int metric = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+    const bool v5 = idx->variant == WV_VARIANT_AVX512;
+    const float* Qn_all = idx->qn.as<float>();
+    if (phase != 2) {  // phase 2 keeps phase 1's block-key timing; the total spans both
+        idx->timed = 0;
+        idx->timed_total = 0;
+        if (idx->timing) HIPCHK(hipEventRecord(idx->evt0, s));
+    }
+    for (int64_t c0 = 0; c0 < nq; c0 += qc) {
+        const int64_t cn = std::min<int64_t>(qc, nq - c0);
+        const int64_t cn_pad = round_up(cn, QS_QPB);
+        if (c0 == 0) { idx->qs_last_nq = cn == nq ? cn : 0; idx->qs_last_nb = nb; idx->qs_last_ldk = ldk; }
+        const float* Qn = Qn_all + c0 * idx->dpad;
+        float4* qinfo = idx->qsInfo.as<float4>();
+        if (phase != 2)
+        k_query_split<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dpb, cn, cn_pad,
+                                                                   idx->qsQb.as<uint16_t>(), qinfo);
+        // ---- block keys (the dominant kernel) ----
+        QsArgs a;
+        a.Xb = reinterpret_cast<const unsigned char*>(idx->Xb);
+        a.xnorm2 = idx->xnorm2;
+        a.valid = valid;
+        a.Qb = reinterpret_cast<const unsigned char*>(idx->qsQb.p);
+        a.key = idx->qsKey.as<float>();
+        a.ldk = ldk;
+        a.nslots = nslots;
+        a.dbg = idx->sel_dbg;
+        // k_qs_blockkey_w4 for d > 768: 128-query workgroups, a 32-row block in two
+        // column parts per ring step: dpb 1024 -> 4 slots of 32 KiB, 1536 -> 3 of 48 KiB
+        const bool w4 = idx->dpb > QS_W4_DPB;
+        const int w4_nb = NK == 64 ? 4 : 3;
+        a.nqg = (int)(cn_pad / (w4 ? 128 : QS_QPB));
+        int64_t nspans = 256 / std::gcd(256, a.nqg);
+        while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
+        if (idx->spans_opt > 0) nspans = idx->spans_opt;
+        {   // a span's plane bytes (+ one tile of slack) must stay below 4 GiB (32-bit buffer offsets)
+            const int64_t slot_b = (int64_t)RB * 32 * idx->dpb * 2;
+            const int64_t max_sps = ((1ll << 32) - 2 * 256ll * idx->dpb * 2) / slot_b;
+            nspans = std::max<int64_t>(nspans, (nslots + max_sps - 1) / max_sps);
+        }
+        nspans = std::max<int64_t>(1, std::min<int64_t>(nspans, nslots));
+        const int64_t sps = (nslots + nspans - 1) / nspans;
+        a.slots_per_span = (int)sps;
+        a.nspans = (int)((nslots + sps - 1) / sps);
+        const bool l2 = metric == L2;
+        const size_t lds = w4 ? (size_t)w4_nb * (NK / 4) * 2048 + 256 + (l2 ? (size_t)4 * 4 * 128 : 0)
+                              : (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
+        dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
+        if (phase != 2) {
+        const bool time_it = idx->timing && c0 == 0;
+        if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
+#define WV_QS(NKV, L2V)                                                                                        \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_qs_blockkey<NKV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_qs_blockkey<NKV, L2V><<<grid, 512, lds, s>>>(a);                                                     \
+    } while (0)
+#define WV_QS3(NKV, L2V, D)                                                                                    \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_qs_blockkey<NKV, L2V, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_qs_blockkey<NKV, L2V, D><<<grid, 512, lds, s>>>(a);                                                  \
+    } while (0)
+#define WV_QSN(L2V)                                    \
+    switch (NK) {                                      \
+    case 8: WV_QS(8, L2V); break;                      \
+    case 16: WV_QS(16, L2V); break;                    \
+    case 24: WV_QS(24, L2V); break;                    \
+    case 32: WV_QS(32, L2V); break;                    \
+    case 40: WV_QS(40, L2V); break;                    \
+    default: WV_QS(48, L2V); break;                    \
+    }
+#define WV_QSW(NKV, L2V, NBV)                                                                                  \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_qs_blockkey_w4<NKV, L2V, 2, NBV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_qs_blockkey_w4<NKV, L2V, 2, NBV><<<grid, 256, lds, s>>>(a);                                          \
+    } while (0)
+#define WV_QSWN(L2V)                                   \
+    if (NK == 64) WV_QSW(64, L2V, 4); else WV_QSW(96, L2V, 3);
+        if (w4) {
+            if (l2) { WV_QSWN(true); } else { WV_QSWN(false); }
+#ifdef WV_QS_DBG  // timing experiments (k_qs_blockkey DBG bits), not in the product build
+        } else if (idx->sel_dbg > 0 && !l2 && NK == 48) {
+            switch (idx->sel_dbg) {
+            case 1: WV_QS3(48, false, 1); break;
+            case 2: WV_QS3(48, false, 2); break;
+            case 3: WV_QS3(48, false, 3); break;
+            case 4: WV_QS3(48, false, 4); break;
+            case 5: WV_QS3(48, false, 5); break;
+            case 6: WV_QS3(48, false, 6); break;
+            default: WV_QS3(48, false, 7); break;
+            }
+#endif
+        } else if (l2) { WV_QSN(true); } else { WV_QSN(false); }
+#undef WV_QSN
+#undef WV_QS3
+#undef WV_QS
+#undef WV_QSWN
+#undef WV_QSW
+        HIPCHK(hipGetLastError());
+        if (time_it) { HIPCHK(hipEventRecord(idx->ev1, s)); idx->timed = 1; }
+        idx->stats.mfma_launches++;
+        }
+        // ---- candidate blocks, exact rows, proof ----
+        int32_t* flags = phase ? idx->qsFlags.as<int32_t>() : o_flags ? o_flags + c0 : idx->qsFlags.as<int32_t>();
+        int32_t* olist = idx->qsList.as<int32_t>() + qc;  // second half: the overflow list
+        // select / exact pass RV over all queries (list == nullptr) or over the listed ones
+        auto sel = [&](int RV, const int32_t* list, const uint32_t* cnt, float* tA) {
+            const unsigned gw = (unsigned)((cn + 3) / 4);
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>())
+            if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
+#undef WV_SELR
+        };
+        // phase 2 cuts the lists with the global threshold: the local cap no longer bounds them
+        const float* capv = (idx->exact_cap && phase == 0) ? idx->qsCap.as<float>() : nullptr;
+        auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0) {
+            launch_blk_exact(idx, s, RV, metric, v5, Qn, valid, (int)cn, k, kout, o_ids + c0 * kout, o_d + c0 * kout,
+                             o_n + c0, flags, list, cnt, eb, ldE, capv);
+        };
+        if (phase != 2) sel(R, nullptr, nullptr, phase == 1 ? topA : nullptr);
+        HIPCHK(hipGetLastError());
+        if (phase == 1) continue;
+        if (phase == 2)  // the global threshold cuts this shard's candidate lists
+            k_blk_gthresh<<<(unsigned)((cn + 3) / 4), 256, 0, s>>>(gA, gE, W, (int)cn, k, metric, qinfo, a.key, ldk,
+                                                                  idx->qsCand.as<uint32_t>(), L, idx->qsNc.as<int32_t>(),
+                                                                  idx->qsEps.as<float>(), flags);
+        const size_t bm_lds = (size_t)32 * (idx->dpad + 4) * sizeof(float);
+        // (bmE holds cn*L*32 floats: above a 4 GiB budget, or past the 2^23
+        // queries k_inv_scatter's packed (q << 9 | j) can name, the
+        // candidate-major k_blk_exact computes the distances itself)
+        if (idx->exact_bm && bm_lds <= 64 * 1024 && nb < (1ll << 31) && cn < (1ll << 23) &&
+            (int64_t)cn * L * 32 * 4 <= (4ll << 30)) {
+            // block-major exact distances: invert the candidate lists per block
+            const int64_t ldE = (int64_t)L * 32;
+            HIPCHK(idx->bmCnt.ensure((size_t)nb * sizeof(uint32_t)));
+            HIPCHK(idx->bmOff.ensure((size_t)(nb + 1) * sizeof(uint32_t)));
+            HIPCHK(idx->bmPairs.ensure((size_t)cn * L * sizeof(uint32_t)));
+            HIPCHK(idx->bmE.ensure((size_t)cn * ldE * sizeof(float)));
+            HIPCHK(hipMemsetAsync(idx->bmCnt.p, 0, (size_t)nb * sizeof(uint32_t), s));
+            const unsigned gw = (unsigned)((cn + 3) / 4);
+            k_inv_count<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
+                                           idx->bmCnt.as<uint32_t>());
+            k_inv_scan<<<1, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmOff.as<uint32_t>());
+            k_inv_scatter<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
+                                             idx->bmOff.as<uint32_t>(), idx->bmCnt.as<uint32_t>(),
+                                             idx->bmPairs.as<uint32_t>());
+            launch_exact_bm(idx, s, metric, v5, Qn, nb, bm_lds, ldE);
+            HIPCHK(hipGetLastError());
+            exa(R, nullptr, nullptr, idx->bmE.as<float>(), ldE);
+        } else {
+            exa(R, nullptr, nullptr);
+        }
+        HIPCHK(hipGetLastError());
+        if (R < 8) {  // candidate lists that overflowed (flag 2): again with the 448-block lists
+            HIPCHK(hipMemsetAsync(idx->qscount + 3, 0, sizeof(uint32_t), s));
+            k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, olist, idx->qscount + 2, 2);
+            sel(8, olist, idx->qscount + 2, nullptr);
+            exa(8, olist, idx->qscount + 2);
+            HIPCHK(hipGetLastError());
+        }
+        if (idx->qs_force_flag) HIPCHK(hipMemsetAsync(flags, 1, (size_t)cn * sizeof(int32_t), s));
+        if (phase == 2 && o_flags)
+            HIPCHK(hipMemcpyAsync(o_flags + c0, flags, (size_t)cn * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        if (mode == 1) continue;
+        // ---- flagged queries: the exact heap replay, bounded by the block keys ----
+        HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
+        k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount, 0);
+        {
+            int rc = launch_blk_replay(idx, s, a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, valid, Qn,
+                                       idx->qsList.as<int32_t>(), idx->qscount, 0, cn, k, kout, o_ids + c0 * kout,
+                                       o_d + c0 * kout, o_n + c0, nullptr, nullptr, nullptr, 1, 0);
+            if (rc) return rc;
+        }
+    }
+    if (idx->timing) {
+        HIPCHK(hipEventRecord(idx->evt1, s));
+        idx->timed_total = 1;
+    }
+    if (qc >= nq && valid == idx->present) idx->qs_keys_nq = nq;
+    return WV_OK;
+}
+
+extern "C" int wv_index_replay(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                               const int32_t* h_qlist, int32_t nlist, const uint64_t* h_in_ids,
+                               const float* h_in_dists, const int32_t* h_in_len, int32_t extract,
+                               uint64_t* h_out_ids, float* h_out_dists, int32_t* h_out_len) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0 || nlist < 0) return set_err(WV_ERR_INVALID, "invalid k / list");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = idx->stream;
+    if (nlist == 0) return WV_OK;
+    const bool have_data = idx->dims != 0 && idx->npresent > 0;
+    if (have_data && d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    HIPCHK(idx->hI.ensure((size_t)nlist * k * sizeof(uint64_t) * 2));
+    HIPCHK(idx->hD.ensure((size_t)nlist * k * sizeof(float) * 2));
+    HIPCHK(idx->hN.ensure((size_t)nlist * sizeof(int32_t) * 2));
+    HIPCHK(idx->qlist.ensure((size_t)nlist * sizeof(int32_t)));
+    uint64_t* inI = idx->hI.as<uint64_t>();
+    uint64_t* outI = inI + (size_t)nlist * k;
+    float* inD = idx->hD.as<float>();
+    float* outD = inD + (size_t)nlist * k;
+    int32_t* inN = idx->hN.as<int32_t>();
+    int32_t* outN = inN + nlist;
+    if (h_in_len) {
+        HIPCHK(hipMemcpyAsync(inI, h_in_ids, (size_t)nlist * k * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(inD, h_in_dists, (size_t)nlist * k * sizeof(float), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(inN, h_in_len, (size_t)nlist * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    } else {
+        HIPCHK(hipMemsetAsync(inN, 0, (size_t)nlist * sizeof(int32_t), s));
+    }
+    HIPCHK(hipMemcpyAsync(idx->qlist.p, h_qlist, (size_t)nlist * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const float* Qn = nullptr;
+    if (have_data) {
+        const int64_t nq_pad = round_up(nq, QB);
+        int rc = prepare_queries(idx, s, d_queries, nq, nq_pad);
+        if (rc) return rc;
+        Qn = idx->qn.as<float>();
+    }
+    // list-ordered output rows (out_by_query = 0); an empty shard passes the
+    // heaps through unchanged (zero tiles scanned)
+    int rc2 = run_replay(idx, s, idx->present, Qn, idx->qlist.as<int32_t>(), nlist, k, inI, inD, h_in_len ? inN : nullptr,
+                         extract, 0, k, outI, outD, outN);
+    if (rc2) return rc2;
+    HIPCHK(hipMemcpyAsync(h_out_ids, outI, (size_t)nlist * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h_out_dists, outD, (size_t)nlist * k * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h_out_len, outN, (size_t)nlist * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// wv_index_replay on device buffers (no host hops, stream-ordered).  With the
+// block keys of this index's last search over the same nq queries still valid
+// (qs_keys_nq), the scan visits only blocks that can insert (k_blk_replay);
+// otherwise every row's exact distance is computed (run_replay).
+// sharded two-phase exact search (weaviate_amd/sharded.py): phase 1 on the
+// block-key path only (WV_ERR_UNSUPPORTED otherwise: the caller uses mode 1)
+extern "C" int wv_index_shard_phase1(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                     float* d_topA, float* d_eps, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (!d_topA || !d_eps) return set_err(WV_ERR_INVALID, "nil buffer");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;
+    idx->qs_keys_nq = 0;
+    idx->qs_phase_nq = 0;
+    const bool qs = idx->compression == WV_COMPRESSION_NONE && idx->qs_planes && !idx->has_nonfinite &&
+                    (idx->kernel_opt == 0 || idx->kernel_opt == 7) && !idx->force_replay && qs_R(k) > 0 &&
+                    idx->metric != WV_METRIC_HAMMING && idx->dims != 0 && idx->npresent > 0 && nq > 0;
+    if (!qs) return set_err(WV_ERR_UNSUPPORTED, "two-phase shard search: not on the block-key path");
+    if (d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QS_QPB));
+    if (rc) return rc;
+    idx->stats.queries += (uint64_t)nq;
+    idx->stats.batches++;
+    rc = search_qs(idx, s, nq, k, 1, idx->present, nullptr, nullptr, nullptr, nullptr, 1, d_topA);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(d_eps, idx->qsEps.p, (size_t)nq * sizeof(float), hipMemcpyDeviceToDevice, s));
+    idx->qs_phase_nq = nq;
+    idx->qs_phase_k = k;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_index_shard_phase2(wv_index* idx, int32_t world, int64_t nq, const float* d_topA_all,
+                                     const float* d_eps_all, int32_t k, uint64_t* d_ids, float* d_dists,
+                                     int32_t* d_counts, int32_t* d_flags, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (!d_topA_all || !d_eps_all || !d_ids || !d_dists || !d_counts || !d_flags)
+        return set_err(WV_ERR_INVALID, "nil buffer");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (idx->qs_phase_nq != nq || idx->qs_phase_k != k || world < 1)
+        return set_err(WV_ERR_INVALID, "shard phase 2 without a matching phase 1 (nq %lld, k %d)", (long long)nq, k);
+    idx->qs_phase_nq = 0;
+    int rc = search_qs(idx, s, nq, k, 1, idx->present, d_ids, d_dists, d_counts, d_flags, 2, nullptr, d_topA_all,
+                       d_eps_all, world);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// the cross-shard replay of every query with d_flags[q] != 0, list built on the
+// device; states and results indexed by query.  Needs this index's block keys
+// of the same batch (wv_index_search_device mode 1 or the two phases).
+extern "C" int wv_index_replay_flags_device(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                            const int32_t* d_flags, const uint64_t* d_in_ids, const float* d_in_dists,
+                                            const int32_t* d_in_len, int32_t extract, uint64_t* d_out_ids,
+                                            float* d_out_dists, int32_t* d_out_len, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0 || nq < 0 || !d_flags || !d_out_ids || !d_out_dists || !d_out_len)
+        return set_err(WV_ERR_INVALID, "invalid arguments");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (nq == 0) return WV_OK;
+    const bool have_data = idx->dims != 0 && idx->npresent > 0;
+    if (have_data && d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    HIPCHK(idx->flCtr.ensure(2 * sizeof(uint32_t)));
+    HIPCHK(idx->qsList.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
+    k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(d_flags, (int)nq, idx->qsList.as<int32_t>(),
+                                                              idx->flCtr.as<uint32_t>(), 0);
+    HIPCHK(hipGetLastError());
+    if (!have_data || idx->qs_keys_nq != nq) {
+        // no block keys of this batch (empty shard, non-finite rows, k or batch
+        // off the block-key path): every row's exact distance + the id-ordered
+        // heap (run_replay, states and results by query); one host sync for the
+        // list length
+        uint32_t nl = 0;
+        HIPCHK(hipMemcpyAsync(&nl, idx->flCtr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (nl == 0) return WV_OK;
+        const float* Qn = nullptr;
+        if (have_data) {
+            int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QB));
+            if (rc) return rc;
+            Qn = idx->qn.as<float>();
+        }
+        int rc = run_replay(idx, s, idx->present, Qn, idx->qsList.as<int32_t>(), (int)nl, k, d_in_ids, d_in_dists,
+                            d_in_len, extract, 1, k, d_out_ids, d_out_dists, d_out_len, 1);
+        if (rc) return rc;
+        if (!stream) HIPCHK(hipStreamSynchronize(s));
+        return WV_OK;
+    }
+    int rc = launch_blk_replay(idx, s, idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb, idx->qsEps.as<float>(),
+                               idx->qsInfo.as<float4>(), idx->present, idx->qn.as<float>(), idx->qsList.as<int32_t>(),
+                               idx->flCtr.as<uint32_t>(), 0, nq, k, k, d_out_ids, d_out_dists, d_out_len, d_in_ids,
+                               d_in_dists, d_in_len, extract, 0);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// parallel cross-shard replay (weaviate_amd/sharded.py): this shard's replay of
+// the listed queries from heap states d_in_* (by list position), recording every
+// insertion (ids, dists [nlist][cap], counts [nlist], cap + 1 = overflow)
+extern "C" int wv_index_replay_record_device(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                             const int32_t* d_qlist, int32_t nlist, const uint64_t* d_in_ids,
+                                             const float* d_in_dists, const int32_t* d_in_len, int32_t cap,
+                                             uint64_t* d_rec_ids, float* d_rec_dists, int32_t* d_rec_n, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0 || nlist < 0 || cap < 1) return set_err(WV_ERR_INVALID, "invalid arguments");
+    if (nlist == 0) return WV_OK;
+    if (!d_qlist || !d_rec_ids || !d_rec_dists || !d_rec_n) return set_err(WV_ERR_INVALID, "nil buffer");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (nlist == 0) return WV_OK;
+    const bool have_data = idx->dims != 0 && idx->npresent > 0;
+    if (!have_data) {
+        HIPCHK(hipMemsetAsync(d_rec_n, 0, (size_t)nlist * sizeof(int32_t), s));
+        return WV_OK;
+    }
+    if (d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    HIPCHK(idx->hI.ensure((size_t)nlist * k * sizeof(uint64_t)));
+    HIPCHK(idx->hD.ensure((size_t)nlist * k * sizeof(float)));
+    HIPCHK(idx->hN.ensure((size_t)nlist * sizeof(int32_t)));
+    if (idx->qs_keys_nq != nq || !blk_pooled(idx, k, idx->qs_last_nb)) {
+        // no block keys of this batch (or k outside the pooled replay): the
+        // all-rows exact replay records the same insertions
+        int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QB));
+        if (rc) return rc;
+        rc = run_replay(idx, s, idx->present, idx->qn.as<float>(), d_qlist, nlist, k, d_in_ids, d_in_dists, d_in_len, 0,
+                        0, k, idx->hI.as<uint64_t>(), idx->hD.as<float>(), idx->hN.as<int32_t>(), 0, d_rec_ids,
+                        d_rec_dists, d_rec_n, cap);
+        if (rc) return rc;
+        if (!stream) HIPCHK(hipStreamSynchronize(s));
+        return WV_OK;
+    }
+    int rc = launch_blk_replay(idx, s, idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb, idx->qsEps.as<float>(),
+                               idx->qsInfo.as<float4>(), idx->present, idx->qn.as<float>(), d_qlist, nullptr, nlist,
+                               nlist, k, k, idx->hI.as<uint64_t>(), idx->hD.as<float>(), idx->hN.as<int32_t>(), d_in_ids,
+                               d_in_dists, d_in_len, 0, 1, d_rec_ids, d_rec_dists, d_rec_n, cap);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_heap_merge_records(int32_t device, int32_t nlist, int32_t k, int32_t world, int32_t cap,
+                                     const uint64_t* d_st_ids, const float* d_st_dists, const int32_t* d_st_n,
+                                     const uint64_t* d_rec_ids, const float* d_rec_dists, const int32_t* d_rec_n,
+                                     uint64_t* d_out_ids, float* d_out_dists, int32_t* d_out_n,
+                                     int32_t* d_unresolved, void* stream) {
+    if (k <= 0 || nlist < 0 || world < 1 || cap < 1) return set_err(WV_ERR_INVALID, "invalid arguments");
+    if (nlist == 0) return WV_OK;
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s = (hipStream_t)stream;
+    const size_t lds = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
+    if (lds > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_heap_merge_records, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_heap_merge_records<<<(unsigned)nlist, 64, lds, s>>>(nlist, k, world, cap, d_st_ids, d_st_dists, d_st_n, d_rec_ids,
+                                                          d_rec_dists, d_rec_n, d_out_ids, d_out_dists, d_out_n,
+                                                          d_unresolved);
+    HIPCHK(hipGetLastError());
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_index_replay_device(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                      const int32_t* d_qlist, int32_t nlist, const uint64_t* d_in_ids,
+                                      const float* d_in_dists, const int32_t* d_in_len, int32_t extract,
+                                      uint64_t* d_out_ids, float* d_out_dists, int32_t* d_out_len, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0 || nlist < 0) return set_err(WV_ERR_INVALID, "invalid k / list");
+    if (nlist > 0 && (!d_qlist || !d_out_ids || !d_out_dists || !d_out_len)) return set_err(WV_ERR_INVALID, "nil buffer");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
+    if (nlist == 0) return WV_OK;
+    const bool have_data = idx->dims != 0 && idx->npresent > 0;
+    if (have_data && d != idx->dims)
+        return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
+    const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
+    const bool keyed = have_data && idx->qs_keys_nq == nq && rlds <= 160 * 1024;
+    if (keyed) {
+        const float* Qn = idx->qn.as<float>();  // the prepared rows of that batch
+        return launch_blk_replay(idx, s, idx->qsKey.as<float>(), idx->qs_last_ldk, idx->qs_last_nb,
+                                 idx->qsEps.as<float>(), idx->qsInfo.as<float4>(), idx->present, Qn, d_qlist, nullptr,
+                                 nlist, nlist, k, k, d_out_ids, d_out_dists, d_out_len, d_in_ids, d_in_dists, d_in_len,
+                                 extract, 1);
+    }
+    const float* Qn = nullptr;
+    if (have_data) {
+        int rc = prepare_queries(idx, s, d_queries, nq, round_up(nq, QB));
+        if (rc) return rc;
+        Qn = idx->qn.as<float>();
+    }
+    // run_replay reads in-state when in_n != nullptr; list-ordered outputs
+    return run_replay(idx, s, idx->present, Qn, d_qlist, nlist, k, d_in_ids, d_in_dists, d_in_len, extract, 0, k,
+                      d_out_ids, d_out_dists, d_out_len);
+}
+
+extern "C" int wv_merge_shards(int32_t device, int32_t nshards, int64_t nq, int32_t k, const uint64_t* d_ids,
+                               const float* d_dists, const int32_t* d_counts, const int32_t* d_flags,
+                               uint64_t* d_out_ids, float* d_out_dists, int32_t* d_out_counts, int32_t* d_out_flags,
+                               void* stream) {
+    HIPCHK(hipSetDevice(device));
+    const int64_t n = (int64_t)nshards * (k + 1);
+    hipStream_t s = (hipStream_t)stream;
+    unsigned grid = (unsigned)((nq + 3) / 4);
+    if (n <= 64) k_merge_shards<1><<<grid, 256, 0, s>>>(nshards, nq, k, d_ids, d_dists, d_counts, d_flags, d_out_ids, d_out_dists, d_out_counts, d_out_flags);
+    else if (n <= 128) k_merge_shards<2><<<grid, 256, 0, s>>>(nshards, nq, k, d_ids, d_dists, d_counts, d_flags, d_out_ids, d_out_dists, d_out_counts, d_out_flags);
+    else if (n <= 256) k_merge_shards<4><<<grid, 256, 0, s>>>(nshards, nq, k, d_ids, d_dists, d_counts, d_flags, d_out_ids, d_out_dists, d_out_counts, d_out_flags);
+    else if (n <= 512) k_merge_shards<8><<<grid, 256, 0, s>>>(nshards, nq, k, d_ids, d_dists, d_counts, d_flags, d_out_ids, d_out_dists, d_out_counts, d_out_flags);
+    else return set_err(WV_ERR_UNSUPPORTED, "merge: nshards*(k+1) > 512");
+    HIPCHK(hipGetLastError());
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+

@@ -32,6 +32,7 @@
 #pragma once
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 constexpr int RQ_QPB = 32;      // queries per distance block (scalar operands)
 constexpr int RQ_MAXD = 4096;   // rotation output dims supported (two LDS buffers)
@@ -359,4 +360,5 @@ __global__ __launch_bounds__(256) void k_rq1_dist(const uint64_t* __restrict__ c
     rq_emit<RQ_QPB>(dist, ok, slot, f0, F, ld, tile, E, bmin, red);
 }
 
+}  // namespace
 }  // namespace wv

@@ -1,0 +1,251 @@
+// rt_index.h -- index state and helpers shared by the runtime's translation
+// units, split so their device code compiles in parallel:
+//   runtime.hip        lifecycle, Add / Delete, options, stats, the exact
+//                      search dispatch (search_core, the f32 / GEMV select
+//                      fallback, run_replay), entry points, LSM restore,
+//                      VectorIndex extras, micro-batcher
+//   qs_runtime.hip     the block-key search (search_qs), the sharded phases
+//                      and the cross-shard replay / merge entries
+//   qs_exact.hip       its exact pass (k_blk_exact, k_exact_bm)
+//   qs_replay.hip      its bounded heap replays (k_rp_*, k_blk_replay*)
+//   quant_runtime.hip  BQ, PQ (fit + search), SQ, RQ and hnsw's flat search
+// The kernel headers live in an anonymous namespace inside wv: every unit
+// compiles (and registers) the kernels it launches.
+#pragma once
+#include <cerrno>
+#include <cpuid.h>
+#include <stdarg.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <atomic>
+#include <numeric>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/wv_knn.h"
+#include "kernels.hip"
+#include "bq_kernels.hip"
+#include "pq_kernels.hip"
+#include "kernels_bf3.hip"
+#include "rq_kernels.hip"
+#include "gemv_kernels.hip"
+#include "qs_kernels.hip"
+#include "sq_kernels.hip"
+
+using namespace wv;
+
+
+// ---------------------------------------------------------------------------
+// errors (runtime.hip)
+// ---------------------------------------------------------------------------
+int set_err(int code, const char* fmt, ...);
+
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) return set_err(WV_ERR_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { release(); }  // every device buffer of an index is freed with it
+    hipError_t ensure(size_t b) {
+        if (b <= bytes) return hipSuccess;
+        if (p) { hipFree(p); p = nullptr; bytes = 0; }
+        size_t nb = std::max(b, (size_t)256);
+        hipError_t e = hipMalloc(&p, nb);
+        if (e == hipSuccess) bytes = nb;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+static inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+// u32 words per row of the PQ code store (256-row tiles of 16-segment groups,
+// pq_kernels.hip); cap is a multiple of 256
+static inline int64_t pq_mwp(int m) { return (int64_t)((m + 15) / 16) * 4; }
+static inline int pq_g16(int m) { return (m + 15) / 16; }
+
+struct wv_batcher;
+static void batcher_free(wv_batcher* b);
+
+struct wv_index {
+    std::mutex mu;
+    int metric = WV_METRIC_COSINE_DOT;
+    int variant = WV_VARIANT_AVX256;
+    int compression = WV_COMPRESSION_NONE;
+    int rescore_limit = -1;
+    int cache_opt = 0;   // BQ.Cache / RQ.Cache (flatent UserConfig): QueryVectorDistancer reads codes
+    int replay_par = 2;  // block-key replay: 2 = pooled three-kernel form (k < 64), 3 = pooled for any k,
+                         // 1 = 8-wave form, 0 = one wave
+    int64_t rp_pool = 1 << 20;  // pooled replay: candidate blocks per batch (144 B each)
+    int pq_adc = 2;             // PQ ADC queries per workgroup: 2 = k_pq_adc2 (b64 LUT pairs), 1 = k_pq_adc
+    int qs_force_flag = 0;      // tests: flag every query of the block-key path (exercise the replay)
+    int exact_bm = 1;           // block-major exact distances (rows <= 508 floats): 1 on, 0 off
+    int device = 0;
+    uint64_t id_base = 0;
+    std::string root_path;
+
+    int dims = 0, dpad = 0;
+    hipStream_t stream = nullptr;
+
+    int64_t cap = 0;       // slots allocated (multiple of BN)
+    int64_t hiwater = 0;   // 1 + highest slot ever written
+    float* X = nullptr;
+    float* xnorm2 = nullptr;
+    uint32_t* present = nullptr;
+    uint32_t* d_maxn2 = nullptr;
+    uint64_t* codes = nullptr;   // BQ: [words][cap] word-major codes of the stored rows
+    int words = 0;
+    int64_t bq_nq = 0;           // BQ batch in flight (bq_begin): queries and R
+    int bq_R = 0;
+    // PQ (compressionhelpers.ProductQuantizer): codebook [m][ks][ds], codes
+    // [ceil(m/4)][cap] u32 (4 segment bytes per word, see pq_kernels.hip)
+    int pq_m = 0, pq_ks = 0, pq_ds = 0, pq_training_limit = 0, pq_rescore = 1, pq_trained = 0;
+    float* pq_centers = nullptr;
+    uint32_t* pq_codes = nullptr;
+    // bf16 hi plane of X for the block-key path (qs_kernels.hip): [cap][dpb],
+    // dpb = dims rounded up to 128, built when dpb <= QS_MAX_DPB
+    int use_qs = 0, qs_planes = 0, dpb = 0;
+    uint16_t* Xb = nullptr;
+    uint32_t* qsmax = nullptr;      // device [4]: max |x - x_h|^2, max |x_h|^2 (float bits), non-finite flag
+    uint32_t* qscount = nullptr;    // device [4]: [0] replayed queries (cumulative), [1] this batch's flagged,
+                                    // [2] overflow second passes (cumulative), [3] this batch's
+    int has_nonfinite = 0;          // host mirror of qsmax[2]
+    uint64_t replayed_host = 0;     // replays counted on the host (legacy paths)
+    int timed = 0;                  // ev0/ev1 bracket the last batch's dominant kernel
+    int timed_total = 0;            // evt0/evt1 bracket the last batch's whole block-key pipeline
+    int64_t qs_last_nq = 0, qs_last_nb = 0, qs_last_ldk = 0;  // first chunk of the last block-key batch (debug hook)
+    // > 0: the block keys / eps / query planes of the last search (nq queries,
+    // one chunk, no allow list) still describe the stored rows -- the
+    // cross-shard replay may bound its scan with them.  Reset by any write or search.
+    int64_t qs_keys_nq = 0;
+    hipEvent_t evt0 = nullptr, evt1 = nullptr;
+    float last_eps_scale = 0.f, last_eps_base = 0.f;  // exactness-proof eps of the last MFMA batch (debug hook)
+    int64_t last_nq = 0;
+    int last_KP = 0;
+    // rq-8 / rq-1 (rq_kernels.hip): rotation tables built at the first Add
+    // (initializeDimensionsAndRQ, flat/index.go:338-360), codes + meta per slot
+    int rq_bits = 0, rq_D = 0, rq_ready = 0;
+    uint16_t* rq_src = nullptr;   // [3][D]
+    float* rq_sign = nullptr;     // [3][D]
+    float* rq_round = nullptr;    // [D] (rq-1)
+    void* rq_codes = nullptr;     // rq-8: tiled [cap][D] bytes; rq-1: [D/64][cap] u64
+    float4* rq_meta = nullptr;    // [cap]
+    // scalar quantizer (sq_kernels.hip): range a, b and the Go float32 constants
+    int sq_ready = 0, sq_Dq = 0;
+    float sq_a = 0.f, sq_b = 0.f, sq_a2 = 0.f, sq_ab = 0.f, sq_ib2 = 0.f;
+    uint4* sq_codes = nullptr;    // rq-8 layout, Dq = round_up(d, 16) bytes per row
+    uint2* sq_meta = nullptr;     // [cap] {sum, sum2} of the codes
+    DBuf sqq, sqm;                // query codes / meta
+    // hnsw.flatSearch parameters (wv_index_hnsw_flat_search)
+    int hnsw_ef = -1, ef_min = 100, ef_max = 500, ef_factor = 8, hnsw_rescore = 1;
+    std::vector<uint8_t> h_present;
+    uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
+    int64_t npresent = 0;
+
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, rqq, rqm;
+
+    int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0, sel_dbg = 0, qgroup_opt = 0, sel_opt = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // replay stream: the quantized searches' one-wave-per-query heap replays
+    // run there, beside the next query group's full-GPU distance kernel
+    hipStream_t aux = nullptr;
+    hipEvent_t evd[2] = {nullptr, nullptr}, evr[2] = {nullptr, nullptr};
+    DBuf rE2, rB2;
+    DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
+    DBuf rpBlk, rpLb, rpQ, rpE, rpVm, rpOff, rpTot, rpCtr;  // pooled replay (k_rp_*)
+    DBuf bmCnt, bmOff, bmPairs, bmE;                          // block-major exact (k_inv_*, k_exact_bm)
+    DBuf qsCap;                                               // per query: upper bound of the (k+1)-th exact distance
+    int exact_cap = 1;                                        // k_blk_exact drops values above qsCap (phase 0)
+    int pq_cand = 1;                                          // PQ search: block minima + candidate blocks (k_pq_cand)
+    DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
+    DBuf flCtr;                      // device flag-list counters (replay_flags)
+    int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
+    int qs_phase_k = 0;
+    DBuf gmA, gmI;  // GEMV path: first level of the two-level span merge
+    wv_stats stats{};
+    // micro-batcher of concurrent single-query searches (batcher.hip)
+    wv_batcher* batcher = nullptr;
+    // written by set_option under mu, read by the batcher leader without it
+    std::atomic<int64_t> batch_window_us{0}, batch_max{4096};
+    int gemv_max = 8, gemv_wg = 1024, exact_multi = 1;  // batches up to this many queries take the GEMV select kernel (kver 6)
+};
+
+// The block keys, eps and prepared query rows of the last batch (qs_keys_nq)
+// and a pending sharded phase 1 (qs_phase_nq) describe one batch on one corpus
+// state: an Add, a Delete or another batch's query preparation ends them.
+static void invalidate_batch(wv_index* idx) {
+    idx->qs_keys_nq = 0;
+    idx->qs_phase_nq = 0;
+}
+
+// ---------------------------------------------------------------------------
+// create / destroy / capacity
+// ---------------------------------------------------------------------------
+// k_qs_blockkey keeps 32 queries x dpb bf16 in VGPRs (two waves per SIMD) up
+// to 768 dims; k_qs_blockkey_w4 (one wave per SIMD, query fragments in the
+// 512-entry register file, dpb 1024 or 1536) up to 1536
+constexpr int QS_MAX_DPB = 1536;
+constexpr int QS_W4_DPB = 768;  // dpb above this: k_qs_blockkey_w4
+
+// ---------------------------------------------------------------------------
+// functions shared across the units (defined where noted)
+// ---------------------------------------------------------------------------
+// runtime.hip
+double gamma_n(int n);
+int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t nq_pad);
+int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float* Qn, const int32_t* d_qlist,
+               int nlist, int k, const uint64_t* in_i, const float* in_d, const int32_t* in_n, int extract,
+               int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on, int by_query = 0,
+               uint64_t* rec_i = nullptr, float* rec_d = nullptr, int32_t* rec_n = nullptr, int rec_cap = 0);
+void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots);
+void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t ld, int64_t n, const uint32_t* d_slots,
+                      int query, void* codes, int64_t cap, float4* meta);
+// qs_runtime.hip
+int qs_R(int k);
+int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid, uint64_t* o_ids,
+              float* o_d, int32_t* o_n, int32_t* o_flags, int phase = 0, float* topA = nullptr,
+              const float* gA = nullptr, const float* gE = nullptr, int W = 0);
+// qs_exact.hip
+void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
+                      const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
+                      int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
+                      const float* capv);
+void launch_exact_bm(wv_index* idx, hipStream_t s, int metric, bool v5, const float* Qn, int64_t nb, size_t bm_lds,
+                     int64_t ldE);
+// qs_replay.hip
+bool blk_pooled(const wv_index* idx, int k, int64_t nb);
+int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ldk, int64_t nb, const float* eps,
+                      const float4* qinfo, const uint32_t* valid, const float* Qn, const int32_t* list,
+                      const uint32_t* counters, int nlist, int64_t max_list, int k, int kout, uint64_t* oi,
+                      float* od, int32_t* on, const uint64_t* in_i, const float* in_d, const int32_t* in_n,
+                      int extract, int by_list, uint64_t* rec_i = nullptr, float* rec_d = nullptr,
+                      int32_t* rec_n = nullptr, int rec_cap = 0);
+// quant_runtime.hip
+int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, const uint32_t* valid,
+              uint64_t* o_ids, float* o_d, int32_t* o_n);
+int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, const uint32_t* valid,
+              uint64_t* o_ids, float* o_d, int32_t* o_n);
+int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, const uint32_t* valid,
+              uint64_t* o_ids, float* o_d, int32_t* o_n);
+int search_hnsw_flat(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
+                     const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n);
+int rq_init(wv_index* idx);
+int rq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq);
+int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int F, int64_t ld, float* E, float* bmin);

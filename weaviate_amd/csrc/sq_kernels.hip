@@ -21,6 +21,7 @@
 #pragma once
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 constexpr float SQ_CODES = 255.0f;  // codes (scalar_quantization.go:24)
 
@@ -160,4 +161,5 @@ __global__ __launch_bounds__(256) void k_bq_dist(const uint64_t* __restrict__ co
     rq_emit<RQ_QPB>(dist, ok, slot, f0, F, ld, tile, E, bmin, red);
 }
 
+}  // namespace
 }  // namespace wv

@@ -6,6 +6,7 @@
 #pragma once
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 // QueryVectorDistancer.DistanceFunc over listed slots (flat/index.go:1160-1240,
 // default branch: SingleDist(normalised query, stored row)).  Lane per slot;
@@ -36,6 +37,7 @@ __global__ __launch_bounds__(64) void k_bq_query_slots(const uint64_t* __restric
     out[i] = (float)c;
 }
 
+}  // namespace
 }  // namespace wv
 
 static const char* metric_name(int m) {

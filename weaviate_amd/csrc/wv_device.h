@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 namespace wv {
+namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 enum Metric : int { L2 = 0, DOT = 1, COSINE = 2, HAMMING = 3 };
 enum Variant : int { AVX256 = 1, AVX512 = 2 };
@@ -234,4 +235,5 @@ __host__ __device__ __forceinline__ float gen_value(int kind, uint64_t seed, uin
     return (float)(h >> 40) * 1.1920928955078125e-07f - 1.0f;
 }
 
+}  // namespace
 }  // namespace wv
