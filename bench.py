@@ -501,7 +501,8 @@ def main():
     total_avg = float(np.mean(tot_ms)) if tot_ms else 0.0
     # the dominant kernel of each workload: its PMC record (matched on kernel
     # name and configuration) is the only source of `traffic`
-    dom_kernel = ("k_pq_adc2" if pq else "k_bq_blockmin_lds" if bq else
+    pq_kernel = "k_pq_adc3" if pq and not any(o.replace(" ", "") == "pq_adc3=0" for o in args.option) else "k_pq_adc2"
+    dom_kernel = (pq_kernel if pq else "k_bq_blockmin_lds" if bq else
                   ("k_rq8_dist" if rq_bits == 8 else "k_rq1_dist") if rq_bits else sel_kernel)
     if args.traffic_bytes is None:
         args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B, dom_kernel)
@@ -524,14 +525,15 @@ def main():
                 "hbm_write_GBps": f0 * ld * 4 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
                 "traffic": args.traffic_bytes}
     elif pq:
-        # dominant kernel k_pq_adc: one LUT lookup (LDS gather) + fp32 add per
-        # (query, row, segment); the codes of a tile are shared by the group's
-        # queries through L2
+        # dominant kernel k_pq_adc3 (k_pq_adc2 with --option pq_adc3=0): one
+        # LUT lookup (LDS gather) + fp32 add per (query, row, segment); adc3
+        # reads 64 queries' entries of one code per 32-lane ds_read_b64 group
+        # (conflict-free), so the LDS array rate for 4-byte lookups is the peak
         ld = (n_local + 255) // 256 * 256
         f0 = int(index.stats().get("last_group_queries", 0)) or max(1, min(B, (2 << 30) // (ld * 4)))  # timed first group
         lookups = float(f0) * n_local * PQ_SEGMENTS
         achieved = lookups / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
-        roof = {"bound": "lds", "kernel": "k_pq_adc2", "achieved": achieved,
+        roof = {"bound": "lds", "kernel": pq_kernel, "achieved": achieved,
                 "peak": LDS_LOOKUP_PEAK_T, "unit": "T lookups/s", "frac": achieved / LDS_LOOKUP_PEAK_T,
                 "frac_of_b32_lookup_rate": achieved / LDS_LOOKUP_B32_T, "launch_ms": sel_avg,
                 "note": "launch_ms = first query group of the batch",

@@ -126,3 +126,51 @@ def test_pq_errors(wv, oracle):
     ids, _ = idx.search_by_vector(data[3], 1)
     assert ids[0] == 3
     idx.close()
+
+
+# k_pq_adc3 (ks = 256 only: queries on the lanes, 1024-row chunks, 64-query groups): a row
+# count off the chunk size, m off the 16-segment group, two query groups (the second
+# partial), deleted rows and an allow list (invalid rows), integer data (ADC ties); the
+# same results as k_pq_adc2 and the oracle
+@pytest.mark.parametrize("metric,kind,rescore,k,rl,allow", [
+    ("l2-squared", 0, False, 10, -1, False),
+    ("cosine", 0, True, 10, 40, False),
+    ("dot", 0, False, 12, -1, True),
+    ("l2-squared", 1, False, 20, -1, False),
+])
+def test_pq_adc3_matches_adc2_and_oracle(wv, oracle, metric, kind, rescore, k, rl, allow):
+    n, d, m, ks, nq = 3171, 96, 24, 256, 70
+    data = gen(oracle, kind, 171, n, d)
+    idx = wv.FlatIndex(distance=metric, variant="avx256", rescore_limit=rl,
+                       pq={"segments": m, "centroids": ks, "rescore": rescore})
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    idx.pq_fit(seed=17)
+    gone = list(range(5, n, 97))
+    idx.delete(*gone)
+    centers = idx.pq_centers()
+    codes = idx.pq_codes(n)
+    om = oracle.METRIC[metric]
+    store = stored_rows(oracle, om, data)
+    present = np.ones(n, np.uint8)
+    present[gone] = 0
+    al = None
+    if allow:
+        keep = [i for i in range(n) if i % 3 != 1]
+        al = wv.AllowList(keep)
+        mask = np.zeros(n, np.uint8)
+        mask[keep] = 1
+        present &= mask
+    queries = gen(oracle, kind, 172, nq, d)
+    res = {}
+    for adc3 in (1, 0):
+        idx.set_option("pq_adc3", adc3)
+        res[adc3] = idx.search_by_vector_batch(queries, k, allow=al)
+    for a, b in zip(res[1], res[0]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    ids, dists, counts = res[1]
+    for qi in list(range(0, nq, 7)) + [63, 64, nq - 1]:
+        qv = oracle.normalize(queries[qi]) if om == oracle.COSINE else queries[qi]
+        oi, od = oracle.pq_flat_search(om, 1, centers, codes, store, present, qv, k, max(rl, k), rescore)
+        np.testing.assert_array_equal(ids[qi, :counts[qi]], oi, err_msg=f"q{qi}")
+        np.testing.assert_array_equal(dists[qi, :counts[qi]].view(np.uint32), od.view(np.uint32), err_msg=f"q{qi}")
+    idx.close()

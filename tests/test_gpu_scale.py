@@ -172,11 +172,14 @@ def test_c4_bq_shard_6_25m_x_1536(wv, oracle):
 def test_c5_pq_full_10m_x_960_bench_batch(wv, oracle):
     """configs[4] as bench.py --workload pq times it: 10M x 960 U[0,1) rows,
     PQ m=240 x ks=256 trained on the first 100k rows, ADC flat search of a
-    B = 256 batch -- at 10M rows search_pq splits the batch into query groups
-    sized to the free HBM and replays group i on the aux stream beside group
-    i+1's k_pq_adc2.  Codes of sampled rows against the oracle encoder, then 8
-    queries (spread over the groups) against the oracle's flatSearch over the
-    index's full code array."""
+    B = 256 batch through the default minima-only search (k_pq_adc2 block
+    minima -> candidate blocks -> k_pq_cand, flagged queries replayed), and a
+    1024 batch both that way and through the full-matrix form (pq_cand = 0),
+    which at 10M rows splits the batch into query groups sized to the free HBM
+    and replays group i on the aux stream beside group i+1's k_pq_adc2.
+    Codes of sampled rows against the oracle encoder, then 8 queries per run
+    (spread over the groups) against the oracle's flatSearch over the index's
+    full code array."""
     torch = pytest.importorskip("torch")
     from concurrent.futures import ThreadPoolExecutor
     from weaviate_amd import _lib
@@ -195,7 +198,9 @@ def test_c5_pq_full_10m_x_960_bench_batch(wv, oracle):
     dummy = np.zeros(1, np.float32)
     queries = oracle.gen_matrix(2, 2, 0, 1024, d)
     res = {}
-    for nb in (B, 1024):  # the bench's batch, and one that needs several query groups
+    # the bench's batch and path, a larger batch, and the full-matrix multi-group form
+    for cand, nb in ((1, B), (1, 1024), (0, 1024)):
+        idx.set_option("pq_cand", cand)
         qd = torch.empty((nb, d), dtype=torch.float32, device="cuda")
         _lib.check(lib.wv_gen_device(0, 2, 2, 0, nb, d, qd.data_ptr(), None))
         oi_d = torch.empty((nb, k), dtype=torch.int64, device="cuda")
@@ -205,18 +210,22 @@ def test_c5_pq_full_10m_x_960_bench_batch(wv, oracle):
                                               on_d.data_ptr(), None, None))
         torch.cuda.synchronize()
         group = idx.stats()["last_group_queries"]
-        if nb > B:
+        if cand == 0:
             assert 0 < group < nb, f"the multi-group path did not run (group of {group} queries)"
-        res[nb] = (oi_d.cpu().numpy().view(np.uint64), od_d.cpu().numpy(), on_d.cpu().numpy())
-        sample = np.linspace(0, nb - 1, 8).astype(np.int64)
+        res[cand, nb] = (oi_d.cpu().numpy().view(np.uint64), od_d.cpu().numpy(), on_d.cpu().numpy())
+        sample = np.linspace(0, nb - 1, 8).astype(np.int64) + (3 if cand == 0 else 0)
+        sample = np.minimum(sample, nb - 1)
         with ThreadPoolExecutor(min(8, oracle_threads())) as ex:
             exp = list(ex.map(lambda q: oracle.pq_flat_search(oracle.L2, 1, centers, codes, dummy, present,
                                                               queries[q], k, k, False), sample))
         for i, q in enumerate(sample):
-            assert_rows(*res[nb], q, exp[i][0], exp[i][1], f"c5 B={nb} (groups of {group})")
-    # a query's result does not depend on the batch or group it ran in
-    for a, b in zip(res[B], res[1024]):
-        np.testing.assert_array_equal(np.asarray(a), np.asarray(b)[:B])
+            assert_rows(*res[cand, nb], q, exp[i][0], exp[i][1], f"c5 cand={cand} B={nb} (groups of {group})")
+    # a query's result depends neither on the batch, the group it ran in nor the search form
+    for other in ((1, 1024), (0, 1024)):
+        for a, b in zip(res[1, B], res[other]):
+            np.testing.assert_array_equal(np.asarray(a), np.asarray(b)[:B])
+    for a, b in zip(res[1, 1024], res[0, 1024]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
     idx.close()
 
 

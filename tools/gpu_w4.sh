@@ -14,6 +14,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pq -o run --output
 summ $O/bench_pq.json pq_cand
 timeout -k 10 300 python3 bench.py --workload pq --no-cpu-baseline --option pq_cand=0 > $O/bench_pq0.json 2> $O/bench_pq0.err || { tail $O/bench_pq0.err; exit 1; }
 summ $O/bench_pq0.json pq_matrix
+# C2 (k = 100, integer ties): one-wave replay vs the pooled replay with a pool large enough for every flagged query
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run --output-format csv -- python3 bench.py --workload c2 --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err || { tail $O/bench_c2.err; exit 1; }
+summ $O/bench_c2.json c2
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2p -o run --output-format csv -- python3 bench.py --workload c2 --no-cpu-baseline --option replay_par=3 --option rp_pool=16777216 > $O/bench_c2p.json 2> $O/bench_c2p.err || { tail $O/bench_c2p.err; exit 1; }
+summ $O/bench_c2p.json c2_pooled
 i=0
 for grp in "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
            "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA" \

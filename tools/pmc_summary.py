@@ -6,7 +6,7 @@ for path in sorted(glob.glob(os.path.join(root, "*", "run_counter_collection.csv
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(dict)
     for r in rows:
-        k = r["Kernel_Name"].split("(")[0]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     for k, v in agg.items():

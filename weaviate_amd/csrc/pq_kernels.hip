@@ -650,5 +650,202 @@ __global__ __launch_bounds__(64) void k_pq_rescore_final(const uint32_t* __restr
     out_n[q] = m;
 }
 
+
+// ---------------------------------------------------------------------------
+// k_pq_adc3: the ADC block minima with the queries on the lanes.  A random
+// code per lane (k_pq_adc2: rows on the lanes) makes every LUT read a bank
+// conflict lottery; here the 32 lanes of a ds_read_b64 group read ONE row's
+// code for 64 queries (2 per lane): 256 contiguous bytes, conflict-free, and
+// one v_pk_add_f32 adds both.  Workgroup: 8 waves x 128 rows = 1024 rows, 64
+// queries (query group blockIdx.y); lane (p = lane & 31, h = lane >> 5) keeps
+// the sums of queries 2p, 2p+1 for rows 128 w + 2 i + h, i < 64 (128 VGPRs).
+// Per segment s (in order: each fp32 sum is the reference's segment-order
+// sum, bit-identical to k_pq_adc / k_pq_adc2):
+//   LUT slot s & 1 <- lutg[G][s] (64 KiB: [code][64 queries]) by LDS-DMA,
+//   issued one segment ahead (two 64 KiB slots);
+//   codes of the segment's 1024 rows from LDS ([16 segments][1024 rows] bytes,
+//   restaged every 16 segments from the 256-row code tiles), eight rows per
+//   broadcast ds_read_b64; the LUT address = v_perm(code byte, lane base).
+// LDS reads are inline asm with counted lgkmcnt waits (the DMA would make the
+// compiler drain vmcnt before every LDS read it sees).  Writes the 256-row
+// block minima only (bmin[q][blk], +inf for invalid rows; K = 256).
+// ---------------------------------------------------------------------------
+typedef float pq_f2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void* pq_lds_t;
+
+// lutg[G][s][c][j] = lut[min(64 G + j, nq - 1)][s][c]
+__global__ void k_pq_lut_group(const float* __restrict__ lut, int nq, int m, int K, int64_t total,
+                               float* __restrict__ lutg) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int j = (int)(i & 63);
+    const int64_t r = i >> 6;
+    const int c = (int)(r % K);
+    const int64_t gs = r / K;
+    const int sg = (int)(gs % m);
+    const int64_t G = gs / m;
+    int64_t q = G * 64 + j;
+    q = q < nq ? q : nq - 1;
+    lutg[i] = lut[(q * m + sg) * K + c];
+}
+
+constexpr int PQ3_ROWS = 1024;
+constexpr int PQ3_SLOT = 65536;                          // one segment's LUT: 256 codes x 64 queries x 4 B
+constexpr int PQ3_LDS = 2 * PQ3_SLOT + 16 * PQ3_ROWS;    // two LUT slots + the codes of 16 segments
+
+__device__ __forceinline__ uint2 pq3_ld8(unsigned a) {
+    uint2 v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+template <int N>
+__device__ __forceinline__ void pq3_wait_lgkm() {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(512, 1) void k_pq_adc3(const uint32_t* __restrict__ codes, int g16, int m,
+                                                    const uint32_t* __restrict__ valid, int64_t nslots,
+                                                    const float* __restrict__ lutg, int nq, int metric,
+                                                    int64_t nblk_ld, float* __restrict__ bmin) {
+    __shared__ __attribute__((aligned(16))) unsigned char sm[PQ3_LDS];  // the kernel's only LDS: address 0
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int p = lane & 31, h = lane >> 5;
+    const int64_t row0 = (int64_t)blockIdx.x * PQ3_ROWS;
+    const int G = blockIdx.y;
+    const unsigned smb = (unsigned)(size_t)((pq_lds_t)sm);
+    const unsigned cod = smb + 2 * PQ3_SLOT;
+    // the LUT address of code c in slot b: byte 0 = 8 p, byte 1 = c, byte 2 = b (slots at 0 / 64 KiB)
+    const uint32_t selA = 0x0c020000u | ((4u + (uint32_t)h) << 8);       // code byte h   (row pairs 4j, 4j+2)
+    const uint32_t selB = 0x0c020000u | ((4u + 2u + (uint32_t)h) << 8);  // code byte 2+h (row pairs 4j+1, 4j+3)
+    const uint32_t lb0 = smb + 8u * (uint32_t)p;
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(lutg + (int64_t)G * m * 256 * 64), (short)0, -1, 0x00020000);
+    auto dma = [&](int sg) {  // LUT segment sg -> slot sg & 1: 8 KiB per wave
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const unsigned off = (unsigned)(i * 8192 + w * 1024);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (pq_lds_t)(size_t)(smb + (unsigned)((sg & 1) * PQ3_SLOT) + off),
+                                                     16, (uint32_t)(16 * lane), (uint32_t)sg * PQ3_SLOT + off, 0, 0);
+        }
+    };
+    // this thread's two rows (2 tid, 2 tid + 1) of the chunk: code uint4s of a 16-segment group
+    auto load_codes = [&](int g, uint4& c0, uint4& c1) {
+        const uint4* cb = reinterpret_cast<const uint4*>(codes);
+        const int64_t r = row0 + 2 * tid;
+        c0 = r < nslots ? cb[((r >> 8) * g16 + g) * 256 + (r & 255)] : make_uint4(0u, 0u, 0u, 0u);
+        c1 = r + 1 < nslots ? cb[(((r + 1) >> 8) * g16 + g) * 256 + ((r + 1) & 255)] : make_uint4(0u, 0u, 0u, 0u);
+    };
+    // [16][1024] bytes: segment k's byte of rows 2 tid, 2 tid + 1 as one u16
+    auto store_codes = [&](const uint4& c0, const uint4& c1) {
+        const uint32_t a[4] = {c0.x, c0.y, c0.z, c0.w}, b[4] = {c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            // low byte: row 2 tid's code k, high byte: row 2 tid + 1's
+            const uint32_t v = __builtin_amdgcn_perm(b[k >> 2], a[k >> 2], 0x0c0c0000u | (uint32_t)(k & 3) | ((uint32_t)(4 + (k & 3)) << 8));
+            *(__attribute__((address_space(3))) uint16_t*)(size_t)(cod + (unsigned)(k * PQ3_ROWS + 2 * tid)) = (uint16_t)v;
+        }
+    };
+    pq_f2 sum[64];
+#pragma unroll
+    for (int i = 0; i < 64; i++) sum[i] = pq_f2{0.f, 0.f};
+    uint4 nc0, nc1;
+    load_codes(0, nc0, nc1);
+    dma(0);
+    for (int s = 0; s < m; s++) {
+        if ((s & 15) == 0) {
+            // the group's codes: every wave is past the previous group's reads
+            __syncthreads();
+            store_codes(nc0, nc1);
+            if (s + 16 < m) load_codes((s >> 4) + 1, nc0, nc1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // slot s & 1 landed for every wave; slot (s + 1) & 1 is free
+        if (s + 1 < m) dma(s + 1);
+        // 16 broadcast reads: the codes of this wave's 128 rows
+        const unsigned crow = cod + (unsigned)((s & 15) * PQ3_ROWS + w * 128);
+        uint2 cw[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) cw[j] = pq3_ld8(crow + 8 * j);
+        pq3_wait_lgkm<0>();
+        const uint32_t lb = lb0 + (uint32_t)((s & 1) * PQ3_SLOT);
+        // 64 row pairs in batches of 8: batch t + 1's reads in flight while t's are added
+        uint2 v[2][8];
+        auto issue = [&](int t, uint2 (&dst)[8]) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = 8 * t + u;          // row pair: code dword (i >> 1) & 1 of cw[i >> 2]
+                const uint2 c = cw[i >> 2];
+                const uint32_t word = ((i >> 1) & 1) ? c.y : c.x;
+                dst[u] = pq3_ld8(__builtin_amdgcn_perm(word, lb, (i & 1) ? selB : selA));
+            }
+        };
+        issue(0, v[0]);
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            if (t + 1 < 8) issue(t + 1, v[(t + 1) & 1]);
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                if (t + 1 < 8) {
+                    switch (u) {
+                    case 0: asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(v[t & 1][0])); break;
+                    case 1: asm volatile("s_waitcnt lgkmcnt(14)" : "+v"(v[t & 1][1])); break;
+                    case 2: asm volatile("s_waitcnt lgkmcnt(13)" : "+v"(v[t & 1][2])); break;
+                    case 3: asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(v[t & 1][3])); break;
+                    case 4: asm volatile("s_waitcnt lgkmcnt(11)" : "+v"(v[t & 1][4])); break;
+                    case 5: asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(v[t & 1][5])); break;
+                    case 6: asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(v[t & 1][6])); break;
+                    default: asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(v[t & 1][7])); break;
+                    }
+                } else {
+                    switch (u) {
+                    case 0: asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(v[t & 1][0])); break;
+                    case 1: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(v[t & 1][1])); break;
+                    case 2: asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(v[t & 1][2])); break;
+                    case 3: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(v[t & 1][3])); break;
+                    case 4: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(v[t & 1][4])); break;
+                    case 5: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(v[t & 1][5])); break;
+                    case 6: asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(v[t & 1][6])); break;
+                    default: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[t & 1][7])); break;
+                    }
+                }
+                const uint2 x = v[t & 1][u];
+                sum[8 * t + u] += pq_f2{__uint_as_float(x.x), __uint_as_float(x.y)};
+            }
+        }
+    }
+    // per query: minimum over this wave's 128 rows (invalid rows +inf), then the
+    // two waves of a 256-row block through LDS (after every LUT read is done)
+    const int64_t rw = row0 + (int64_t)w * 128;
+    uint32_t vw[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) vw[k] = rw + 32 * k < nslots ? valid[(rw >> 5) + k] : 0u;
+    float m0 = __builtin_inff(), m1 = __builtin_inff();
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        const int r = 2 * i + h;  // row within the wave's 128
+        const bool ok = rw + r < nslots && ((vw[r >> 5] >> (r & 31)) & 1u);
+        if (ok) {
+            m0 = fminf(m0, pq_wrap(metric, sum[i].x));
+            m1 = fminf(m1, pq_wrap(metric, sum[i].y));
+        }
+    }
+    m0 = fminf(m0, __shfl_xor(m0, 32));
+    m1 = fminf(m1, __shfl_xor(m1, 32));
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(sm);  // [8 waves][64 queries]
+    if (h == 0) {
+        red[w * 64 + 2 * p] = m0;
+        red[w * 64 + 2 * p + 1] = m1;
+    }
+    __syncthreads();
+    if (tid < 256) {  // block b = tid >> 6 (waves 2b, 2b + 1), query j = tid & 63
+        const int b = tid >> 6, j = tid & 63;
+        const int64_t q = (int64_t)G * 64 + j;
+        const int64_t blk = row0 / 256 + b;
+        if (q < nq && blk < nblk_ld) bmin[q * nblk_ld + blk] = fminf(red[(2 * b) * 64 + j], red[(2 * b + 1) * 64 + j]);
+    }
+}
+
 }  // namespace
 }  // namespace wv

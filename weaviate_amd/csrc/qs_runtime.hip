@@ -83,6 +83,10 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             const int64_t max_sps = ((1ll << 32) - 2 * 256ll * idx->dpb * 2) / slot_b;
             nspans = std::max<int64_t>(nspans, (nslots + max_sps - 1) / max_sps);
         }
+        if (idx->spans_opt <= 0) {  // whole rounds of one workgroup per CU (10M x 1024: 5 spans = 320 groups -> 8)
+            const int64_t unit = 256 / std::gcd(256, a.nqg);
+            nspans = (nspans + unit - 1) / unit * unit;
+        }
         nspans = std::max<int64_t>(1, std::min<int64_t>(nspans, nslots));
         const int64_t sps = (nslots + nspans - 1) / nspans;
         a.slots_per_span = (int)sps;

@@ -754,7 +754,21 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         HIPCHK(hipMemsetAsync(idx->pqZero.p, 0, (size_t)std::max<int64_t>(nq, 1) * sizeof(float4), s));
         const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
         dim3 grid2((unsigned)((nq + 1) / 2), (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
+        const bool adc3 = idx->pq_adc3 && K == 256;
+        if (adc3) {  // queries on the lanes: the LUT regrouped as [64-query group][segment][code][64]
+            const int64_t ng = (nq + 63) / 64;
+            const int64_t tot = ng * m * 256 * 64;
+            HIPCHK(idx->lutg.ensure((size_t)tot * sizeof(float)));
+            k_pq_lut_group<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(idx->lut.as<float>(), (int)nq, m, K, tot,
+                                                                         idx->lutg.as<float>());
+            HIPCHK(hipGetLastError());
+        }
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
+        if (adc3) {
+            dim3 g3((unsigned)((nslots + PQ3_ROWS - 1) / PQ3_ROWS), (unsigned)((nq + 63) / 64));
+            k_pq_adc3<<<g3, 512, 0, s>>>(idx->pq_codes, pq_g16(m), m, valid, nslots, idx->lutg.as<float>(), (int)nq,
+                                         wrapm, nblk, idx->rB.as<float>());
+        } else {
 #define WV_ADC2M(KCV)                                                                                        \
     do {                                                                                                     \
         HIPCHK(hipFuncSetAttribute((const void*)k_pq_adc2<KCV, PQ_RPT>, hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -766,6 +780,7 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         if (K == 256) WV_ADC2M(256);
         else WV_ADC2M(0);
 #undef WV_ADC2M
+        }
         HIPCHK(hipGetLastError());
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
         idx->stats.last_group_queries = (uint64_t)nq;

@@ -174,6 +174,8 @@ struct wv_index {
     DBuf qsCap;                                               // per query: upper bound of the (k+1)-th exact distance
     int exact_cap = 1;                                        // k_blk_exact drops values above qsCap (phase 0)
     int pq_cand = 1;                                          // PQ search: block minima + candidate blocks (k_pq_cand)
+    int pq_adc3 = 1;                                          // minima by k_pq_adc3 (queries on the lanes), 0: k_pq_adc2
+    DBuf lutg;                                                // the LUT regrouped for k_pq_adc3 [64-query group][s][c][64]
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
     DBuf flCtr;                      // device flag-list counters (replay_flags)
     int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size

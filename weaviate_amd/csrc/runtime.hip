@@ -578,6 +578,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     if (k == "margin") { if (value < 2 || value > 30) return set_err(WV_ERR_INVALID, "margin out of range"); idx->margin = (int)value; }
     else if (k == "force_replay") idx->force_replay = (int)value;
     else if (k == "spans") idx->spans_opt = (int)value;
+    else if (k == "pq_adc3") idx->pq_adc3 = value != 0;
     else if (k == "timing") idx->timing = (int)value;
     else if (k == "cbuf") idx->cbuf_opt = (int)value;
     else if (k == "kernel") {  // 0 auto, 3 f32 MFMA select, 6 GEMV select, 7 block keys
