@@ -393,16 +393,18 @@ int wv_index_debug_candidates(wv_index *idx, float *A, float *E, uint32_t *I, fl
  * bound eps(q).  Call with A == NULL to read *nb only. */
 int wv_index_debug_blockkeys(wv_index *idx, int64_t q, float *A, float *eps, int64_t *nb);
 
-/* tuning / testing knobs: "margin" (extra candidates of the legacy select
- * kernels, default 8), "force_replay" (1 = resolve every query by heap
+/* tuning / testing knobs: "margin" (extra candidates of the f32 select
+ * kernel, default 8), "force_replay" (1 = resolve every query by heap
  * replay), "spans" (0 = auto), "kernel" (0 = auto: 7 = bf16 block-key path
- * (qs_kernels.hip, the default for the exact fp32 search up to 768 dims),
- * 6 = HBM-streaming GEMV, 5/4 = bf16x3 MFMA select (need "bf3_planes" = 1
- * before the first Add), 3 = f32 MFMA ring, 2/1 older f32 forms),
- * "bq_kernel" (1 = generic BQ kernels), "timing" (1 = record kernel times
- * with HIP events), "batch_window_us" / "batch_max" (micro-batcher, see
- * wv_index_search_by_vector), "cache" (BQ.Cache / RQ.Cache, default 0: see
- * wv_index_query_distances) */
+ * (qs_kernels.hip, the default for the exact fp32 search up to 1536 dims),
+ * 6 = HBM-streaming GEMV, 3 = f32 MFMA select; other values are rejected),
+ * "replay_par" (flagged-query replay form, default 2), "exact_bm" / "exact_cap"
+ * (block-key exact pass forms), "pq_cand" (1 = minima-only PQ search, 0 = the
+ * full ADC matrix), "pq_adc3" (1 = queries-on-lanes ADC for 256 centroids,
+ * 0 = k_pq_adc2), "bq_kernel" (1 = generic BQ kernels), "timing" (1 = record
+ * kernel times with HIP events), "batch_window_us" / "batch_max"
+ * (micro-batcher, see wv_index_search_by_vector), "cache" (BQ.Cache /
+ * RQ.Cache, default 0: see wv_index_query_distances) */
 int wv_index_set_option(wv_index *idx, const char *key, int64_t value);
 
 /* ---- LSM on-disk format: restore from flat's vectors bucket ----------------

@@ -1,7 +1,9 @@
-"""A/B of the PQ ADC kernels on the C5 shape (10M x 960, m=240, ks=256, B=256):
-k_pq_adc (pq_adc=1) vs k_pq_adc2 (pq_adc=2),
-interleaved in one process; ADC launch time (HIP events) and whole batch;
-results must be identical across settings."""
+"""A/B of the PQ ADC kernels on the C5 shape (10M x 960, m=240, ks=256, B=256),
+interleaved in one process; ADC launch time (HIP events) and whole batch.
+Default configs: k_pq_adc3 (pq_adc3=1), k_pq_adc2 (pq_adc3=0), and the adc3
+timing experiments (pq_adc3=3: no LUT DMA, 4: no per-segment barrier; their
+results are wrong by construction and are not compared).  Results of the
+other settings must be identical.  Usage: pq_probe.py [cfg ...]"""
 import os
 import sys
 import time
@@ -40,7 +42,8 @@ def run():
 
 
 ref = None
-for cfg in ["pq_adc=1", "pq_adc=2"] * 3:
+cfgs = sys.argv[1:] or ["pq_adc3=1", "pq_adc3=0", "pq_adc3=3", "pq_adc3=4"] * 2
+for cfg in cfgs:
     for kv in cfg.split(","):
         key, val = kv.split("=")
         idx.set_option(key, int(val))
@@ -54,7 +57,8 @@ for cfg in ["pq_adc=1", "pq_adc=2"] * 3:
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / 3
     got = (oi.clone(), od.clone(), on.clone())
-    if ref is None:
+    timing_only = cfg in ("pq_adc3=3", "pq_adc3=4")
+    if ref is None and not timing_only:
         ref = got
-    same = all(torch.equal(a, b) for a, b in zip(ref, got))
+    same = None if timing_only else all(torch.equal(a, b) for a, b in zip(ref, got))
     print(f"{cfg:22s} adc {min(sel):8.2f} ms  batch {dt * 1e3:8.2f} ms  QPS {B / dt:8.0f}  same {same}", flush=True)

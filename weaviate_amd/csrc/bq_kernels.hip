@@ -167,8 +167,11 @@ __global__ __launch_bounds__(256, 2) void k_bq_blockmin_lds(const uint64_t* __re
 // out_slot[li * R + i] = slot of the i-th popped item, out_n[li] = heap length.
 // A visited block's 256 distances are recomputed with all loads issued up
 // front (NW > 0: words <= NW known at compile time; NW == 0: generic loop).
-// Dynamic LDS: [R] u64 ids | [64] f32 | [R] f32 dists | len.
-template <int NW>
+// The heap is PHeap (16-byte records: one LDS round trip per sift level).
+// REC: record insertions (rec_* non-null); a separate instantiation keeps the
+// record's pointers out of the plain replay's scalar registers (the REC form
+// spilled 335 SGPRs: 26.6 ms vs 17.5 ms per C4 launch)
+template <int NW, bool REC>
 __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ codes, int64_t ccap, int words,
                                                   const uint32_t* __restrict__ valid, int64_t nslots,
                                                   const uint64_t* __restrict__ qcodes, int64_t ldq,
@@ -179,11 +182,11 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
                                                   int pop, uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
                                                   int32_t* __restrict__ out_n, uint64_t* __restrict__ rec_ids,
                                                   float* __restrict__ rec_d, int32_t* __restrict__ rec_n, int cap) {
+    // dynamic LDS: [R] heap records (PHeap) | [64] f32 | len
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
-    uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
-    float* s_d = reinterpret_cast<float*>(hid + R);
-    float* hd = s_d + 64;
-    int* s_len = reinterpret_cast<int*>(hd + R);
+    HeapRec* hr = reinterpret_cast<HeapRec*>(rsm);
+    float* s_d = reinterpret_cast<float*>(hr + R);
+    int* s_len = reinterpret_cast<int*>(s_d + 64);
     const int lane = threadIdx.x;
     const int li = blockIdx.x;
     if (li >= nlist) return;
@@ -191,23 +194,23 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
     const float* Bq = bmin + (int64_t)li * nblk;
     // heap state handed over by the previous shard (layout order), or empty
     const int len0 = in_len ? in_len[li] : 0;
-    for (int i = lane; i < len0; i += 64) { hid[i] = in_ids[(int64_t)li * R + i]; hd[i] = in_d[(int64_t)li * R + i]; }
+    for (int i = lane; i < len0; i += 64) hr[i] = hr_make(in_ids[(int64_t)li * R + i], in_d[(int64_t)li * R + i]);
     if (lane == 0) {
         *s_len = len0;
-        if (rec_n) rec_n[li] = 0;
+        if (REC) rec_n[li] = 0;
     }
     __syncthreads();
     for (int64_t b0 = 0; b0 < nblk; b0 += 64) {
         const float bm = (b0 + lane < nblk) ? Bq[b0 + lane] : __builtin_inff();
         int len = *s_len;
-        float top = len > 0 ? hd[0] : 0.f;
+        float top = len > 0 ? hr[0].d : 0.f;
         uint64_t bmask = __ballot((b0 + lane < nblk) && bm != __builtin_inff() && (len < R || top > bm));
         while (bmask) {
             const int j = __builtin_ctzll(bmask);
             bmask &= bmask - 1;
             const float bmj = __shfl(bm, j);
             len = *s_len;
-            top = len > 0 ? hd[0] : 0.f;
+            top = len > 0 ? hr[0].d : 0.f;
             if (!(len < R || top > bmj)) continue;
             const int64_t r0 = (b0 + j) * BQBLK;
             float dist[BQBLK / 64];
@@ -245,24 +248,21 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
 #pragma unroll
             for (int sub = 0; sub < BQBLK / 64; sub++) {
                 len = *s_len;
-                top = len > 0 ? hd[0] : 0.f;
+                top = len > 0 ? hr[0].d : 0.f;
                 uint64_t mask = __ballot(okv[sub] && (len < R || top > dist[sub]));
                 if (mask == 0) continue;
                 s_d[lane] = dist[sub];
                 __syncthreads();
                 if (lane == 0) {
-                    ReplayHeap hp{hid, hd, *s_len};
+                    PHeap hp{hr, *s_len};
                     const int64_t sb = r0 + sub * 64;
                     while (mask) {
                         const int jj = __builtin_ctzll(mask);
                         mask &= mask - 1;
                         const float dj = s_d[jj];
                         const uint64_t sj = id_base + (uint64_t)(sb + jj);
-                        bool ins = true;
-                        if (hp.len < R) rh_insert(hp, sj, dj);
-                        else if (hp.dist[0] > dj) { uint64_t a; float b; rh_pop(hp, &a, &b); rh_insert(hp, sj, dj); }
-                        else ins = false;
-                        if (ins && rec_n) {  // the parallel cross-shard replay's record (id order)
+                        const bool ins = ph_offer(hp, R, sj, dj);
+                        if (REC && ins) {  // the parallel cross-shard replay's record (id order)
                             const int c = rec_n[li];
                             if (c < cap) { rec_ids[(int64_t)li * cap + c] = sj; rec_d[(int64_t)li * cap + c] = dj; }
                             rec_n[li] = c < cap ? c + 1 : cap + 1;
@@ -275,17 +275,17 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
         }
     }
     if (lane == 0 && out_n) {
-        ReplayHeap hp{hid, hd, *s_len};
+        PHeap hp{hr, *s_len};
         const int n = hp.len;
         if (pop) {  // pop order (max first) = idsSlice of flat/index.go:485-487
             for (int i = 0; i < n; i++) {
                 uint64_t a; float b;
-                rh_pop(hp, &a, &b);
+                ph_pop(hp, &a, &b);
                 out_ids[(int64_t)li * R + i] = a;
                 out_d[(int64_t)li * R + i] = b;
             }
         } else {  // the heap state itself, for the next shard
-            for (int i = 0; i < n; i++) { out_ids[(int64_t)li * R + i] = hid[i]; out_d[(int64_t)li * R + i] = hd[i]; }
+            for (int i = 0; i < n; i++) { out_ids[(int64_t)li * R + i] = hr_id(hr[i]); out_d[(int64_t)li * R + i] = hr[i].d; }
         }
         out_n[li] = n;
     }

@@ -541,6 +541,89 @@ __device__ void rh_pop(ReplayHeap& h, uint64_t* id, float* dist) {
     }
 }
 
+// The same heap with each item one 16-byte LDS record (distance, id): a sift
+// level reads both children with two ds_read_b128 issued together and moves
+// one record with one ds_write_b128 -- one LDS round trip per level instead of
+// ReplayHeap's separate distance / id loads and swaps.  Comparisons and final
+// layout are rh_insert / rh_pop's (the hole moves instead of swapping, which
+// leaves the same array).  Lane 0 runs it, like ReplayHeap.
+struct __attribute__((aligned(16))) HeapRec {
+    float d;
+    uint32_t lo, hi, pad;
+};
+struct PHeap {
+    HeapRec* r;
+    int len;
+};
+// records move as one 4 x u32 vector (x = distance bits, y / z = id lo / hi):
+// ds_read_b128 / ds_write_b128, selected with v_cndmask, never an aggregate
+// copy (which the compiler put on the scratch stack)
+typedef uint32_t hr_v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint64_t hr_id(const HeapRec& x) { return ((uint64_t)x.hi << 32) | x.lo; }
+__device__ __forceinline__ HeapRec hr_make(uint64_t id, float d) {
+    HeapRec x;
+    x.d = d;
+    x.lo = (uint32_t)id;
+    x.hi = (uint32_t)(id >> 32);
+    x.pad = 0u;
+    return x;
+}
+__device__ __forceinline__ hr_v4 hr_v(uint64_t id, float d) {
+    return hr_v4{__float_as_uint(d), (uint32_t)id, (uint32_t)(id >> 32), 0u};
+}
+__device__ __forceinline__ void ph_insert(PHeap& h, uint64_t id, float v) {
+    hr_v4* r = reinterpret_cast<hr_v4*>(h.r);
+    int i = h.len++;
+    while (i != 0) {  // up while dist[i] > dist[parent]
+        const int p = (i - 1) >> 1;
+        const hr_v4 rp = r[p];
+        if (!(v > __uint_as_float(rp.x))) break;
+        r[i] = rp;
+        i = p;
+    }
+    r[i] = hr_v(id, v);
+}
+__device__ __forceinline__ void ph_pop(PHeap& h, uint64_t* id, float* dist) {
+    hr_v4* r = reinterpret_cast<hr_v4*>(h.r);
+    const hr_v4 top = r[0];
+    *id = ((uint64_t)top.z << 32) | top.y;
+    *dist = __uint_as_float(top.x);
+    const int n = --h.len;
+    const hr_v4 x = r[n];  // the last item moves to the root and sifts down
+    const float xd = __uint_as_float(x.x);
+    int i = 0;
+    for (;;) {
+        const int l = 2 * i + 1;
+        if (l >= n) break;
+        const bool hasr = l + 1 < n;
+        const hr_v4 rl = r[l];
+        const hr_v4 rr = r[hasr ? l + 1 : l];
+        const float dl = __uint_as_float(rl.x), dr = __uint_as_float(rr.x);
+        int s = i;
+        float ds = xd;
+        if (dl > ds) { s = l; ds = dl; }
+        if (hasr && dr > ds) { s = l + 1; ds = dr; }
+        if (s == i) break;
+        r[i] = s == l ? rl : rr;
+        i = s;
+    }
+    if (n > 0) r[i] = x;
+}
+// insertToHeap (flat/index.go:665-674): true when the item entered
+__device__ __forceinline__ bool ph_offer(PHeap& h, int k, uint64_t id, float v) {
+    if (h.len < k) { ph_insert(h, id, v); return true; }
+    if (h.r[0].d > v) {
+        uint64_t a;
+        float b;
+        ph_pop(h, &a, &b);
+        ph_insert(h, id, v);
+        return true;
+    }
+    return false;
+}
+// dynamic LDS of the packed replays: [k] records | [64] f32 | len (16 B)
+__host__ __device__ constexpr size_t packed_replay_lds(int k) { return (size_t)k * sizeof(HeapRec) + 64 * sizeof(float) + 16; }
+
 // (1) exact-order distances of every stored row to each listed query, plus
 //     per-256-row block minima (valid rows only).  Block b handles query
 //     f = b % F and rows [256*(b/F), +256): the F blocks of one row range are
@@ -693,6 +776,8 @@ __global__ __launch_bounds__(256) void k_exact_rows_multi(const float* __restric
 //     id order, one wave per listed query.  A 256-row block is skipped when the
 //     heap is full and !(top > block_min): no row in it can pass insertToHeap's
 //     `top.Dist > distance` test, and the top never increases.
+// PK: the heap as packed 16-byte records (PHeap, default for k <= 8192); else ReplayHeap's split arrays
+template <bool PK>
 __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E, const float* __restrict__ bmin,
                                                     const uint32_t* __restrict__ valid, int64_t nslots, int64_t ld,
                                                     const int32_t* __restrict__ qlist, int nlist, int k,
@@ -705,12 +790,14 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
                                                     int in_by_query, int raw_by_query,
                                                     uint64_t* __restrict__ rec_i, float* __restrict__ rec_d,
                                                     int32_t* __restrict__ rec_n, int rec_cap) {
-    // all LDS in the dynamic region (Guideline 17): [k] ids | [64] dists | [k] heap dists | len
+    // all LDS in the dynamic region (Guideline 17): PK: [k] records | [64] dists | len,
+    // else [k] ids | [64] dists | [k] heap dists | len
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+    HeapRec* hr = reinterpret_cast<HeapRec*>(rsm);
     uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
-    float* s_d = reinterpret_cast<float*>(hid + k);
+    float* s_d = PK ? reinterpret_cast<float*>(hr + k) : reinterpret_cast<float*>(hid + k);
     float* hd = s_d + 64;
-    int* s_len = reinterpret_cast<int*>(hd + k);
+    int* s_len = PK ? reinterpret_cast<int*>(s_d + 64) : reinterpret_cast<int*>(hd + k);
     const int lane = threadIdx.x;
     const int li = blockIdx.x;
     if (li >= nlist) return;
@@ -722,7 +809,10 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
         if (in_hlen) {
             const int64_t ir = in_by_query ? q : li;
             len = in_hlen[ir];
-            for (int i = 0; i < len; i++) { hid[i] = in_hid[ir * k + i]; hd[i] = in_hd[ir * k + i]; }
+            for (int i = 0; i < len; i++) {
+                if (PK) hr[i] = hr_make(in_hid[ir * k + i], in_hd[ir * k + i]);
+                else { hid[i] = in_hid[ir * k + i]; hd[i] = in_hd[ir * k + i]; }
+            }
         }
         *s_len = len;
         if (rec_n) rec_n[li] = 0;
@@ -732,14 +822,14 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
     for (int64_t b0 = 0; b0 < nblk; b0 += 64) {
         const float bm = (b0 + lane < nblk) ? Bq[b0 + lane] : __builtin_inff();
         int len = *s_len;
-        float top = len > 0 ? hd[0] : 0.f;
+        float top = len > 0 ? (PK ? hr[0].d : hd[0]) : 0.f;
         uint64_t bmask = __ballot((b0 + lane < nblk) && (len < k || top > bm));
         while (bmask) {
             const int j = __builtin_ctzll(bmask);
             bmask &= bmask - 1;
             const float bmj = __shfl(bm, j);
             len = *s_len;
-            top = len > 0 ? hd[0] : 0.f;
+            top = len > 0 ? (PK ? hr[0].d : hd[0]) : 0.f;
             if (!(len < k || top > bmj)) continue;
             const int64_t r0 = (b0 + j) * EBLK;
             for (int sub = 0; sub < EBLK; sub += 64) {
@@ -747,20 +837,22 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
                 const bool ok = s < nslots && ((valid[s >> 5] >> (s & 31)) & 1u);
                 const float dist = ok ? Eq[s] : 0.f;
                 len = *s_len;
-                top = len > 0 ? hd[0] : 0.f;
+                top = len > 0 ? (PK ? hr[0].d : hd[0]) : 0.f;
                 uint64_t mask = __ballot(ok && (len < k || top > dist));
                 if (mask == 0) continue;
                 s_d[lane] = dist;
                 __syncthreads();
                 if (lane == 0) {
                     ReplayHeap h{hid, hd, *s_len};
+                    PHeap ph{hr, *s_len};
                     while (mask) {
                         const int jj = __builtin_ctzll(mask);
                         mask &= mask - 1;
                         const float dj = s_d[jj];
                         const uint64_t idj = id_base + (uint64_t)(s - lane + jj);
                         bool ins = true;
-                        if (h.len < k) rh_insert(h, idj, dj);
+                        if (PK) ins = ph_offer(ph, k, idj, dj);
+                        else if (h.len < k) rh_insert(h, idj, dj);
                         else if (h.dist[0] > dj) { uint64_t a; float b; rh_pop(h, &a, &b); rh_insert(h, idj, dj); }
                         else ins = false;
                         if (ins && rec_n) {  // the parallel cross-shard replay's record (id order)
@@ -769,7 +861,7 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
                             rec_n[li] = c < rec_cap ? c + 1 : rec_cap + 1;
                         }
                     }
-                    *s_len = h.len;
+                    *s_len = PK ? ph.len : h.len;
                 }
                 __syncthreads();
             }
@@ -777,22 +869,48 @@ __global__ __launch_bounds__(64) void k_replay_scan(const float* __restrict__ E,
     }
     if (lane == 0) {
         ReplayHeap h{hid, hd, *s_len};
+        PHeap ph{hr, *s_len};
         if (extract) {
             // extractHeap (flat/index.go:676-688): pop max-first, fill from the back
-            const int n = h.len;
+            const int n = *s_len;
             const int64_t row = out_by_query ? q : li;
             for (int i = n - 1; i >= 0; i--) {
                 uint64_t a; float b;
-                rh_pop(h, &a, &b);
+                if (PK) ph_pop(ph, &a, &b);
+                else rh_pop(h, &a, &b);
                 if (i < kout) { out_ids[row * kout + i] = a; out_d[row * kout + i] = b; }
             }
             out_n[row] = n < kout ? n : kout;
         } else {
             const int64_t row = raw_by_query ? q : li;
-            for (int i = 0; i < h.len; i++) { out_ids[row * k + i] = h.id[i]; out_d[row * k + i] = h.dist[i]; }
-            out_n[row] = h.len;
+            const int n = *s_len;
+            for (int i = 0; i < n; i++) {
+                out_ids[row * k + i] = PK ? hr_id(hr[i]) : hid[i];
+                out_d[row * k + i] = PK ? hr[i].d : hd[i];
+            }
+            out_n[row] = n;
         }
     }
+}
+
+// the worker-heap replay: packed records for k <= 8192, else the split layout (up to 13.6k)
+constexpr int PACKED_REPLAY_MAX_K = 8192;
+__host__ __forceinline__ size_t replay_scan_lds(int k) {
+    return k <= PACKED_REPLAY_MAX_K ? packed_replay_lds(k)
+                                    : (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16;
+}
+template <class... A>
+static inline hipError_t launch_replay_scan(int k, unsigned grid, hipStream_t st, A... args) {
+    if (grid == 0) return hipSuccess;
+    const size_t lds = replay_scan_lds(k);
+    const void* fn = k <= PACKED_REPLAY_MAX_K ? (const void*)k_replay_scan<true> : (const void*)k_replay_scan<false>;
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    if (k <= PACKED_REPLAY_MAX_K) k_replay_scan<true><<<grid, 64, lds, st>>>(args...);
+    else k_replay_scan<false><<<grid, 64, lds, st>>>(args...);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -703,6 +703,8 @@ __device__ __forceinline__ void pq3_wait_lgkm() {
     asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// DBG (timing experiments only, wrong results): 1 = no LUT DMA in the loop, 2 = no per-segment wait + barrier
+template <int DBG>
 __global__ __launch_bounds__(512, 1) void k_pq_adc3(const uint32_t* __restrict__ codes, int g16, int m,
                                                     const uint32_t* __restrict__ valid, int64_t nslots,
                                                     const float* __restrict__ lutg, int nq, int metric,
@@ -759,9 +761,11 @@ __global__ __launch_bounds__(512, 1) void k_pq_adc3(const uint32_t* __restrict__
             store_codes(nc0, nc1);
             if (s + 16 < m) load_codes((s >> 4) + 1, nc0, nc1);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // slot s & 1 landed for every wave; slot (s + 1) & 1 is free
-        if (s + 1 < m) dma(s + 1);
+        if (DBG != 2) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // slot s & 1 landed for every wave; slot (s + 1) & 1 is free
+        }
+        if (s + 1 < m && DBG != 1) dma(s + 1);
         // 16 broadcast reads: the codes of this wave's 128 rows
         const unsigned crow = cod + (unsigned)((s & 15) * PQ3_ROWS + w * 128);
         uint2 cw[16];

@@ -1271,11 +1271,11 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
                                                    int32_t* __restrict__ out_n, const uint64_t* __restrict__ in_ids,
                                                    const float* __restrict__ in_d, const int32_t* __restrict__ in_len,
                                                    int extract, int by_list) {
+    // dynamic LDS: [k] heap records (PHeap) | [64] f32 | len (16 B) | [RU * 64] keys
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
-    uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
-    float* s_d = reinterpret_cast<float*>(hid + k);
-    float* hd = s_d + 64;
-    int* s_len = reinterpret_cast<int*>(hd + k);
+    HeapRec* hr = reinterpret_cast<HeapRec*>(rsm);
+    float* s_d = reinterpret_cast<float*>(hr + k);
+    int* s_len = reinterpret_cast<int*>(s_d + 64);
     const int lane = threadIdx.x;
     const int li_ = blockIdx.x;  // list position
     if (counters ? (uint32_t)li_ >= counters[1] : li_ >= nlist) return;
@@ -1290,16 +1290,14 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     // the heap handed over by the previous shard (layout order), or empty
     int len_in = in_len ? in_len[by_list ? li_ : q] : 0;
     len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
-    for (int i = lane; i < len_in; i += 64) {
-        hid[i] = in_ids[(int64_t)(by_list ? li_ : q) * k + i];
-        hd[i] = in_d[(int64_t)(by_list ? li_ : q) * k + i];
-    }
+    for (int i = lane; i < len_in; i += 64)
+        hr[i] = hr_make(in_ids[(int64_t)(by_list ? li_ : q) * k + i], in_d[(int64_t)(by_list ? li_ : q) * k + i]);
     if (lane == 0) *s_len = len_in;
     __syncthreads();
     // block keys in rounds of 64 * RU: all loads of a round in flight at once,
     // parked in LDS; a round with no visitable block is skipped whole
     constexpr int RU = 16;
-    float* skey = hd + k + 4;  // [RU * 64]
+    float* skey = s_d + 64 + 4;  // [RU * 64]
     for (int64_t r0 = 0; r0 < nb; r0 += 64 * RU) {
         float kvr[RU];
 #pragma unroll
@@ -1309,7 +1307,7 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
         }
         {
             const int len0 = *s_len;
-            const float top0 = len0 > 0 ? hd[0] : 0.f;
+            const float top0 = len0 > 0 ? hr[0].d : 0.f;
             bool any = false;
 #pragma unroll
             for (int u = 0; u < RU; u++) {
@@ -1331,12 +1329,12 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
             lb = noskip ? -__builtin_inff() : qs_key_to_a(metric, kv, qi.x) - eps;
         }
         int len = *s_len;
-        float top = len > 0 ? hd[0] : 0.f;
+        float top = len > 0 ? hr[0].d : 0.f;
         uint64_t bmask = __ballot(has && (len < k || top > lb));
         while (bmask) {
             // next one or two blocks still able to insert under the current top
             len = *s_len;
-            top = len > 0 ? hd[0] : 0.f;
+            top = len > 0 ? hr[0].d : 0.f;
             int j1 = -1, j2 = -1;
             while (bmask && j2 < 0) {
                 const int j = __builtin_ctzll(bmask);
@@ -1355,15 +1353,13 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
             s_d[lane] = dist;
             __syncthreads();
             if (lane == 0) {
-                ReplayHeap h{hid, hd, *s_len};
+                PHeap h{hr, *s_len};
                 while (mask) {
                     const int l = __builtin_ctzll(mask);
                     mask &= mask - 1;
                     const float dj = s_d[l];
                     const int jb = l >= 32 ? j2 : j1;
-                    const uint64_t idj = id_base + (uint64_t)((b0 + jb) * 32 + (l & 31));
-                    if (h.len < k) rh_insert(h, idj, dj);
-                    else if (h.dist[0] > dj) { uint64_t x; float y; rh_pop(h, &x, &y); rh_insert(h, idj, dj); }
+                    ph_offer(h, k, id_base + (uint64_t)((b0 + jb) * 32 + (l & 31)), dj);
                 }
                 *s_len = h.len;
             }
@@ -1375,18 +1371,18 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     if (!extract) {  // hand the heap on in layout order (kout == k)
         const int n = *s_len;
         for (int i = lane; i < n; i += 64) {
-            out_ids[orow * kout + i] = hid[i];
-            out_d[orow * kout + i] = hd[i];
+            out_ids[orow * kout + i] = hr_id(hr[i]);
+            out_d[orow * kout + i] = hr[i].d;
         }
         if (lane == 0) out_n[orow] = n;
         return;
     }
     if (lane == 0) {  // extractHeap (flat/index.go:676-688): pops max-first into the tail
-        ReplayHeap h{hid, hd, *s_len};
+        PHeap h{hr, *s_len};
         const int n = h.len;
         for (int i = n - 1; i >= 0; i--) {
             uint64_t x; float y;
-            rh_pop(h, &x, &y);
+            ph_pop(h, &x, &y);
             if (i < kout) { out_ids[orow * kout + i] = x; out_d[orow * kout + i] = y; }
         }
         out_n[orow] = n < kout ? n : kout;

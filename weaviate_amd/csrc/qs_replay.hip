@@ -87,7 +87,7 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
         HIPCHK(hipGetLastError());
         return WV_OK;
     }
-    const size_t rlds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16 + 16 * 64 * sizeof(float);
+    const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float);
     if (rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
 #define WV_RP(M, V)                                                                                             \
     do {                                                                                                        \

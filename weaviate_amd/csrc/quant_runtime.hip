@@ -121,17 +121,19 @@ static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_
     const int32_t* qlist = idx->ident.as<int32_t>();
     const uint64_t* qc = idx->qcodes.as<uint64_t>();
     const float* bm = idx->bqmin.as<float>();
-    const size_t lds_r = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
-#define WV_RP(NWV)                                                                                              \
+    const size_t lds_r = packed_replay_lds(R);
+    if (lds_r > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "rescore limit %d too large for the replay heap", R);
+#define WV_RPR(NWV, RECV)                                                                                       \
     do {                                                                                                        \
         if (lds_r > 64 * 1024)                                                                                  \
-            HIPCHK(hipFuncSetAttribute((const void*)k_bq_replay<NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                       (int)lds_r));                                                            \
-        k_bq_replay<NWV><<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq,      \
-                                                        qlist + g0, F, bm, nblk, R, idx->id_base, in_ids, in_d, \
-                                                        in_len, pop, out_ids, out_d, out_n, rec_ids, rec_d,     \
-                                                        rec_n, cap);                                            \
+            HIPCHK(hipFuncSetAttribute((const void*)k_bq_replay<NWV, RECV>,                                     \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_r));                \
+        k_bq_replay<NWV, RECV><<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq, \
+                                                              qlist + g0, F, bm, nblk, R, idx->id_base, in_ids, \
+                                                              in_d, in_len, pop, out_ids, out_d, out_n, rec_ids, \
+                                                              rec_d, rec_n, cap);                               \
     } while (0)
+#define WV_RP(NWV) do { if (rec_n) WV_RPR(NWV, true); else WV_RPR(NWV, false); } while (0)
     switch (nw) {
     case 2: WV_RP(2); break;
     case 4: WV_RP(4); break;
@@ -142,6 +144,7 @@ static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_
     case 32: WV_RP(32); break;
     default: WV_RP(0); break;
     }
+#undef WV_RPR
 #undef WV_RP
     HIPCHK(hipGetLastError());
     return WV_OK;
@@ -766,8 +769,11 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
         if (adc3) {
             dim3 g3((unsigned)((nslots + PQ3_ROWS - 1) / PQ3_ROWS), (unsigned)((nq + 63) / 64));
-            k_pq_adc3<<<g3, 512, 0, s>>>(idx->pq_codes, pq_g16(m), m, valid, nslots, idx->lutg.as<float>(), (int)nq,
-                                         wrapm, nblk, idx->rB.as<float>());
+#define WV_ADC3(DBGV) k_pq_adc3<DBGV><<<g3, 512, 0, s>>>(idx->pq_codes, pq_g16(m), m, valid, nslots, idx->lutg.as<float>(), (int)nq, wrapm, nblk, idx->rB.as<float>())
+            if (idx->pq_adc3 == 3) WV_ADC3(1);       // timing experiments only (wrong results)
+            else if (idx->pq_adc3 == 4) WV_ADC3(2);
+            else WV_ADC3(0);
+#undef WV_ADC3
         } else {
 #define WV_ADC2M(KCV)                                                                                        \
     do {                                                                                                     \
@@ -833,9 +839,6 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
             HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
             HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
         }
-    const size_t lds_rep = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
-    if (lds_rep > 64 * 1024)
-        HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rep));
     int64_t gi = 0;
     for (int64_t g0 = 0; g0 < nrep; g0 += G, gi++) {
         const int F = (int)std::min<int64_t>(G, nrep - g0);
@@ -887,11 +890,10 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         // the worker heap (addResult == insertToHeap) in id order, extracted ascending
         // (rows by list position, or by query for the PQ candidate path's flagged list)
         const int64_t ao = rep_by_query ? 0 : g0;
-        k_replay_scan<<<F, 64, lds_rep, idx->aux>>>(E, Bm, valid, nslots, ld, qlist + g0, F, R, idx->id_base, nullptr,
-                                                    nullptr, nullptr, 1, rep_by_query, R,
-                                                    idx->ascI.as<uint64_t>() + ao * R, idx->ascD.as<float>() + ao * R,
-                                                    idx->ascN.as<int32_t>() + ao, 0, 0, nullptr, nullptr, nullptr, 0);
-        HIPCHK(hipGetLastError());
+        HIPCHK(launch_replay_scan(R, (unsigned)F, idx->aux, E, Bm, valid, nslots, ld, qlist + g0, F, R, idx->id_base,
+                                  nullptr, nullptr, nullptr, 1, rep_by_query, R, idx->ascI.as<uint64_t>() + ao * R,
+                                  idx->ascD.as<float>() + ao * R, idx->ascN.as<int32_t>() + ao, 0, 0, nullptr, nullptr,
+                                  nullptr, 0));
         HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
     }
     for (int b = 0; b < 2 && b < gi; b++) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
@@ -1227,9 +1229,6 @@ int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
     HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
     HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
     HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
-    const size_t lds_rep = (size_t)R * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)R * sizeof(float) + 16;
-    if (lds_rep > 64 * 1024)
-        HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rep));
     int64_t gi = 0;
     for (int64_t g0 = 0; g0 < nq; g0 += G, gi++) {
         const int F = (int)std::min<int64_t>(G, nq - g0);
@@ -1241,12 +1240,10 @@ int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
         if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
         HIPCHK(hipEventRecord(idx->evd[b], s));
         HIPCHK(hipStreamWaitEvent(idx->aux, idx->evd[b], 0));
-        k_replay_scan<<<F, 64, lds_rep, idx->aux>>>(Eb[b]->as<float>(), Bb[b]->as<float>(), valid, nslots, ld,
-                                                    qlist + g0, F, R, idx->id_base, nullptr, nullptr, nullptr, 1, 0,
-                                                    R, idx->ascI.as<uint64_t>() + g0 * R,
-                                                    idx->ascD.as<float>() + g0 * R, idx->ascN.as<int32_t>() + g0, 0, 0,
-                                                    nullptr, nullptr, nullptr, 0);
-        HIPCHK(hipGetLastError());
+        HIPCHK(launch_replay_scan(R, (unsigned)F, idx->aux, Eb[b]->as<float>(), Bb[b]->as<float>(), valid, nslots, ld,
+                                  qlist + g0, F, R, idx->id_base, nullptr, nullptr, nullptr, 1, 0, R,
+                                  idx->ascI.as<uint64_t>() + g0 * R, idx->ascD.as<float>() + g0 * R,
+                                  idx->ascN.as<int32_t>() + g0, 0, 0, nullptr, nullptr, nullptr, 0));
         HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
     }
     // join: the rescoring on s reads every group's heap

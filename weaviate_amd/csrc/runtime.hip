@@ -578,7 +578,10 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     if (k == "margin") { if (value < 2 || value > 30) return set_err(WV_ERR_INVALID, "margin out of range"); idx->margin = (int)value; }
     else if (k == "force_replay") idx->force_replay = (int)value;
     else if (k == "spans") idx->spans_opt = (int)value;
-    else if (k == "pq_adc3") idx->pq_adc3 = value != 0;
+    else if (k == "pq_adc3") {  // 1: k_pq_adc3 (default), 0: k_pq_adc2; 3, 4: timing experiments (wrong results)
+        if (value < 0 || value > 4) return set_err(WV_ERR_INVALID, "pq_adc3 must be 0..4");
+        idx->pq_adc3 = (int)value;
+    }
     else if (k == "timing") idx->timing = (int)value;
     else if (k == "cbuf") idx->cbuf_opt = (int)value;
     else if (k == "kernel") {  // 0 auto, 3 f32 MFMA select, 6 GEMV select, 7 block keys
@@ -732,11 +735,9 @@ int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float*
     int64_t G = std::max<int64_t>(1, std::min<int64_t>(nlist, (2ll << 30) / (ld * 4)));
     HIPCHK(idx->rE.ensure((size_t)G * ld * sizeof(float)));
     HIPCHK(idx->rB.ensure((size_t)G * (ld / EBLK) * sizeof(float)));
-    const size_t lds = (size_t)k * sizeof(uint64_t) + 64 * sizeof(float) + (size_t)k * sizeof(float) + 16;
-    if (lds > 160 * 1024)
+    if (replay_scan_lds(k) > 160 * 1024)
         return set_err(WV_ERR_INVALID, "k=%d exceeds the exact replay heap limit of %d results", k,
                        (int)((160 * 1024 - 272) / 12));
-    HIPCHK(hipFuncSetAttribute((const void*)k_replay_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
     for (int64_t g0 = 0; g0 < nlist; g0 += G) {
         const int F = (int)std::min<int64_t>(G, nlist - g0);
@@ -769,14 +770,15 @@ int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float*
         const bool raw = !extract;
         const int64_t ooff = by_query ? 0 : (raw || !out_by_query) ? g0 : 0;
         const int64_t ioff = by_query ? 0 : g0;
-        k_replay_scan<<<F, 64, lds, s>>>(idx->rE.as<float>(), idx->rB.as<float>(), valid, Qn ? nslots : 0, ld,
-                                         d_qlist + g0, F, k, idx->id_base, in_n ? in_i + ioff * k : nullptr,
-                                         in_n ? in_d + ioff * k : nullptr, in_n ? in_n + ioff : nullptr, extract,
-                                         out_by_query || by_query, kout, oi + ooff * (raw ? k : kout),
-                                         od + ooff * (raw ? k : kout), on + ooff, by_query, by_query,
-                                         rec_n ? rec_i + g0 * rec_cap : nullptr, rec_n ? rec_d + g0 * rec_cap : nullptr,
-                                         rec_n ? rec_n + g0 : nullptr, rec_cap);
-        HIPCHK(hipGetLastError());
+        HIPCHK(launch_replay_scan(k, (unsigned)F, s, idx->rE.as<float>(), idx->rB.as<float>(), valid,
+                                  Qn ? nslots : (int64_t)0, ld, d_qlist + g0, F, k, idx->id_base,
+                                  in_n ? in_i + ioff * k : (const uint64_t*)nullptr,
+                                  in_n ? in_d + ioff * k : (const float*)nullptr,
+                                  in_n ? in_n + ioff : (const int32_t*)nullptr, extract, (int)(out_by_query || by_query),
+                                  kout, oi + ooff * (raw ? k : kout), od + ooff * (raw ? k : kout), on + ooff, by_query,
+                                  by_query, rec_n ? rec_i + g0 * rec_cap : (uint64_t*)nullptr,
+                                  rec_n ? rec_d + g0 * rec_cap : (float*)nullptr, rec_n ? rec_n + g0 : (int32_t*)nullptr,
+                                  rec_cap));
     }
     return WV_OK;
 }
