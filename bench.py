@@ -375,7 +375,7 @@ def main():
     if flat is not None and args.dims is not None and args.dims != flat["d"]:
         flat = dict(flat, d=args.dims, name=flat["name"].replace(f"x {flat['d']} ", f"x {args.dims} ")
                     + f" at d={args.dims}")
-    if (pq or rq_bits) and world > 1:
+    if rq_bits and world > 1:
         raise SystemExit(f"--workload {args.workload}: sharded search is not available yet (1 GPU)")
     dims = BQ_DIMS if bq else PQ_DIMS if pq else flat["d"] if flat else DIMS
     K_ = flat["k"] if flat else K
@@ -417,7 +417,14 @@ def main():
     if pq:
         torch.cuda.synchronize()
         t_fit = time.perf_counter()
-        index.pq_fit(seed=SEED_CORPUS)
+        if not shard or rank == 0:
+            index.pq_fit(seed=SEED_CORPUS)  # rank 0 holds ids [0, n_local): the first trainingLimit rows
+        if shard:  # one codebook for every shard (NewProductQuantizerWithEncoders on the others)
+            cen = torch.from_numpy(index.pq_centers()).to(dev) if rank == 0 else \
+                torch.empty((PQ_SEGMENTS, PQ_CENTROIDS, PQ_DIMS // PQ_SEGMENTS), dtype=torch.float32, device=dev)
+            dist.broadcast(cen, src=0)
+            if rank != 0:
+                index.pq_set_centers(cen.cpu().numpy())
         torch.cuda.synchronize()
         fit_s = time.perf_counter() - t_fit
         log(f"[rank {rank}] pq fit ({PQ_SEGMENTS} x k-means k={PQ_CENTROIDS} on {PQ_TRAIN} rows) + encode "
@@ -428,7 +435,13 @@ def main():
     out_d = torch.empty((B, K_), dtype=torch.float32, device=dev)
     out_n = torch.empty(B, dtype=torch.int32, device=dev)
 
-    if shard and bq:
+    if shard and pq:
+        from weaviate_amd.sharded import GpuQuantShardBackend, ShardedQuantSearch
+        searcher = ShardedQuantSearch(GpuQuantShardBackend(index, local_rank), dev, (n_total + world - 1) // world)
+
+        def step():
+            return searcher.search(queries, K_)
+    elif shard and bq:
         from weaviate_amd.sharded import GpuBQShardBackend, ShardedBQSearch
         searcher = ShardedBQSearch(GpuBQShardBackend(index, local_rank), dev, (n_total + world - 1) // world)
 
@@ -455,7 +468,7 @@ def main():
     torch.cuda.synchronize()
     sel_ms, tot_ms = [], []
     replays0 = index.stats()["replayed_queries"]
-    if shard and not bq:
+    if shard and not (bq or pq):
         searcher.flagged = 0
     t0 = time.perf_counter()
     res = None
@@ -470,10 +483,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     replays = index.stats()["replayed_queries"] - replays0
-    if shard and not bq:
+    if shard and not (bq or pq):
         replays = int(searcher.flagged)  # the cross-shard replay's queries (this rank's view = every rank's)
     sharded_check = None
-    if args.sharded and world == 1 and flat:
+    if args.sharded and world == 1 and (flat or pq):
         # the sharded protocol at one rank must equal the single-index search
         si, sd, sn = step()[:3]
         s = torch.cuda.current_stream(dev).cuda_stream
@@ -501,7 +514,9 @@ def main():
     total_avg = float(np.mean(tot_ms)) if tot_ms else 0.0
     # the dominant kernel of each workload: its PMC record (matched on kernel
     # name and configuration) is the only source of `traffic`
-    pq_kernel = "k_pq_adc3" if pq and not any(o.replace(" ", "") == "pq_adc3=0" for o in args.option) else "k_pq_adc2"
+    # the sharded PQ search (ShardedQuantSearch) computes full ADC rows with k_pq_adc2
+    pq_kernel = "k_pq_adc3" if pq and not shard and not any(o.replace(" ", "") == "pq_adc3=0" for o in args.option) \
+        else "k_pq_adc2"
     dom_kernel = (pq_kernel if pq else "k_bq_blockmin_lds" if bq else
                   ("k_rq8_dist" if rq_bits == 8 else "k_rq1_dist") if rq_bits else sel_kernel)
     if args.traffic_bytes is None:
@@ -640,6 +655,8 @@ def main():
                 "parallelism": f"corpus sharded over {world} GPU(s), contiguous id ranges"
                                + ((", R-heap replay in one parallel hop (all-gathered block-minimum bounds, "
                                    "recorded insertions, on-device merge) + all-gather rescoring" if bq
+                                   else ", worker heap in one parallel hop (block-minimum bounds, recorded "
+                                   "insertions, on-device merge), codebook trained on rank 0 and broadcast" if pq
                                    else ", RCCL all-gather merge") if world > 1 else ""),
                 "replayed_queries": int(replays),
             },

@@ -345,6 +345,47 @@ int wv_index_bq_replay_record(wv_index *idx, const uint64_t *d_in_ids, const flo
                               const int32_t *d_in_len, int32_t cap, uint64_t *d_rec_ids, float *d_rec_dists,
                               int32_t *d_rec_n, void *stream);
 
+/* Sharded hnsw flat search over compressed vectors (hnsw/flat_search.go:28-141
+ * + h.rescore, hnsw/search.go:1047-1110, the search a trained PQ index
+ * (search_pq) or an SQ index (search_hnsw_flat) runs; weaviate_amd/sharded.py
+ * ShardedQuantSearch).  Every shard holds a contiguous id range and the same
+ * quantizer (wv_index_pq_set_centers / wv_index_sq_restore).  The worker heap
+ * of limit R spans the shards in id order, exactly as BQ's R-heap above:
+ *   wv_index_quant_begin     query state + the compressed distances of every row
+ *                            of this shard to the batch (one group, <= 16 GiB)
+ *                            and their 256-row block minima; out[3] = {R, block
+ *                            count, rescore};
+ *   wv_index_quant_blockmin  the minima [nq][blocks] (each the distance of one
+ *                            distinct row: the R smallest bound the heap top);
+ *   wv_index_quant_replay    the worker heap over this shard from states d_in_*
+ *                            ([nq][R] by query, NULL = empty): extract = 1 ->
+ *                            ascending, 0 -> the state;
+ *   wv_index_quant_replay_record  the same from R copies of a bound, recording
+ *                            insertions (count cap + 1 = overflow);
+ *   wv_index_quant_finish    from the merged worker heap (ascending, global ids):
+ *                            the result without rescoring, else the rescoring
+ *                            candidates (global ids, after the SQ trim);
+ *   wv_index_quant_rescore   exact SingleDist of the candidates this shard holds;
+ *   wv_quant_rescore_final   h.rescore over the [world][nq][R] distance tiles
+ *                            (the entry of id from shard min(id / id_stride,
+ *                            world - 1)). */
+int wv_index_quant_begin(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k, int64_t *out,
+                         void *stream);
+int wv_index_quant_blockmin(wv_index *idx, float *d_out, void *stream);
+int wv_index_quant_replay(wv_index *idx, const uint64_t *d_in_ids, const float *d_in_dists, const int32_t *d_in_len,
+                          int32_t extract, uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_len, void *stream);
+int wv_index_quant_replay_record(wv_index *idx, const uint64_t *d_in_ids, const float *d_in_dists,
+                                 const int32_t *d_in_len, int32_t cap, uint64_t *d_rec_ids, float *d_rec_dists,
+                                 int32_t *d_rec_n, void *stream);
+int wv_index_quant_finish(wv_index *idx, const uint64_t *d_asc_ids, const float *d_asc_dists, const int32_t *d_asc_len,
+                          uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_counts, uint64_t *d_cand_ids,
+                          int32_t *d_cand_n, void *stream);
+int wv_index_quant_rescore(wv_index *idx, const uint64_t *d_cand_ids, const int32_t *d_cand_n, float *d_E,
+                           void *stream);
+int wv_quant_rescore_final(int32_t device, int64_t nq, int32_t R, int32_t k, int32_t world, uint64_t id_stride,
+                           const uint64_t *d_cand_ids, const int32_t *d_cand_n, const float *d_E_all,
+                           uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_counts, void *stream);
+
 /* Merge shard-local candidate lists (mode-1 search outputs of G shards, each
  * [nq x (k+1)], gathered shard-major on this device) into the final top-k by
  * (distance, id); d_out_flags[q]=1 when a shard flagged q or the merged top

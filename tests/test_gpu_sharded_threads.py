@@ -215,3 +215,88 @@ def test_sharded_bq_parallel_replay(wv, oracle, monkeypatch, shards, metric, kin
     for b in backs:
         b.index.close()
     single.close()
+
+
+def run_quant_ranks(monkeypatch, backs, q, k, id_stride):
+    import weaviate_amd.sharded as sh
+    g = FakeGroup(len(backs))
+    monkeypatch.setattr(sh, "dist", g)
+    out, paths, err = [None] * len(backs), [None] * len(backs), []
+
+    def rank_main(r):
+        g.tl.rank = r
+        try:
+            s = sh.ShardedQuantSearch(backs[r], torch.device("cuda", 0), id_stride)
+            res = s.search(q, k)
+            torch.cuda.synchronize()
+            out[r] = tuple(t.cpu() for t in res)
+            paths[r] = s.path
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            err.append(e)
+            g.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(len(backs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not any(t.is_alive() for t in th), "a rank is stuck in a collective"
+    if err:
+        raise err[0]
+    return out, paths
+
+
+@pytest.mark.parametrize("comp,shards,metric,kind,per,d,k,rl,rescore", [
+    ("pq", 3, "l2-squared", 0, 6000, 32, 10, -1, False),   # worker heap = k
+    ("pq", 2, "cosine", 0, 8000, 64, 10, 60, True),        # rescoring: owners' exact distances
+    ("pq", 4, "l2-squared", 1, 3000, 24, 7, 40, True),     # integer data: ADC ties
+    ("sq", 3, "l2-squared", 0, 5000, 48, 10, 20, True),    # SQ: ef limit, trim to the rescore limit
+    ("sq", 2, "dot", 1, 6000, 32, 10, 0, True),            # SQ rescore limit 0: no rescoring
+])
+def test_sharded_quant_equals_single_index(wv, oracle, monkeypatch, comp, shards, metric, kind, per, d, k, rl, rescore):
+    """ShardedQuantSearch with GpuQuantShardBackends as threads: hnsw's flat
+    search over PQ / SQ codes (hnsw/flat_search.go:28-141 + h.rescore) with the
+    worker heap across the shards in one parallel hop (or the chain when a
+    record overflows), the result heap and the owners' rescoring.  Every rank
+    must return the single index's result exactly (same quantizer)."""
+    from weaviate_amd.sharded import GpuQuantShardBackend
+    n = per * shards
+    data = oracle.gen_matrix(kind, 91, 0, n, d)
+    queries = oracle.gen_matrix(kind, 92, 0, 120, d)
+    kw = dict(distance=metric, variant="avx256", rescore_limit=rl)
+    if comp == "pq":
+        kw["pq"] = {"segments": d // 4, "centroids": 32, "trainingLimit": 100000, "rescore": rescore}
+    else:
+        kw["sq"] = True
+    single = wv.FlatIndex(**kw)
+    single.add_batch(np.arange(n, dtype=np.uint64), data)
+    if comp == "pq":
+        single.pq_fit(seed=3)
+        centers = single.pq_centers()
+    else:
+        single.sq_fit(2000)
+        info = single.sq_info()
+    si, sd, sn = single.search_by_vector_batch(queries, k)
+    backs = []
+    for r in range(shards):
+        lo = r * per
+        idx = wv.FlatIndex(id_base=lo, **kw)
+        idx.add_batch(np.arange(lo, lo + per, dtype=np.uint64), data[lo:lo + per])
+        if comp == "pq":
+            idx.pq_set_centers(centers)
+        else:
+            idx.sq_restore(info["a"], info["b"])
+        backs.append(GpuQuantShardBackend(idx, 0))
+    q = torch.from_numpy(queries).to("cuda")
+    out, paths = run_quant_ranks(monkeypatch, backs, q, k, per)
+    assert len(set(paths)) == 1, paths
+    for r in range(shards):
+        oi, od, on = (t.numpy() for t in out[r])
+        for i in range(len(queries)):
+            assert on[i] == sn[i], f"rank {r} q{i}"
+            np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), si[i, :sn[i]], err_msg=f"rank {r} q{i}")
+            np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), sd[i, :sn[i]].view(np.uint32),
+                                          err_msg=f"rank {r} q{i}")
+    for b in backs:
+        b.index.close()
+    single.close()

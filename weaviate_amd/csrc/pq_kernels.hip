@@ -582,7 +582,7 @@ __global__ __launch_bounds__(64) void k_pq_finish(const uint64_t* __restrict__ a
                                                   int rescore, uint64_t id_base, uint64_t* __restrict__ out_ids,
                                                   float* __restrict__ out_d, int32_t* __restrict__ out_n,
                                                   uint32_t* __restrict__ cand_slot, int32_t* __restrict__ cand_n,
-                                                  int trim) {
+                                                  int trim, uint64_t* __restrict__ cand_ids = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(psm);
     float* hd = reinterpret_cast<float*>(hid + R);
@@ -614,9 +614,13 @@ __global__ __launch_bounds__(64) void k_pq_finish(const uint64_t* __restrict__ a
     for (int i = mt - 1; i >= 0; i--) {
         uint64_t a; float b;
         rh_pop(hp, &a, &b);
-        cand_slot[(int64_t)li * R + i] = (uint32_t)(a - id_base);
+        if (cand_ids) cand_ids[(int64_t)li * R + i] = a;  // sharded: global ids (any shard)
+        else cand_slot[(int64_t)li * R + i] = (uint32_t)(a - id_base);
     }
-    for (int i = mt; i < R; i++) cand_slot[(int64_t)li * R + i] = NO_ID;
+    for (int i = mt; i < R; i++) {
+        if (cand_ids) cand_ids[(int64_t)li * R + i] = ~0ull;
+        else cand_slot[(int64_t)li * R + i] = NO_ID;
+    }
     cand_n[li] = mt;
 }
 
@@ -627,7 +631,9 @@ __global__ __launch_bounds__(64) void k_pq_rescore_final(const uint32_t* __restr
                                                          const int32_t* __restrict__ cand_n,
                                                          const int32_t* __restrict__ qlist, int nlist, int R, int k,
                                                          uint64_t id_base, uint64_t* __restrict__ out_ids,
-                                                         float* __restrict__ out_d, int32_t* __restrict__ out_n) {
+                                                         float* __restrict__ out_d, int32_t* __restrict__ out_n,
+                                                         const uint64_t* __restrict__ cand_ids = nullptr,
+                                                         int world = 1, uint64_t id_stride = 0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char qsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(qsm);
     float* hd = reinterpret_cast<float*>(hid + (k + 1));
@@ -636,7 +642,20 @@ __global__ __launch_bounds__(64) void k_pq_rescore_final(const uint32_t* __restr
     ReplayHeap hp{hid, hd, 0};
     const int n = cand_n[li];
     for (int i = 0; i < n; i++) {
-        rh_insert(hp, id_base + cand_slot[(int64_t)li * R + i], candE[(int64_t)li * R + i]);
+        // sharded (cand_ids): candE is [world][nlist][R], each shard's exact distances of
+        // the ids it holds; the entry of id comes from shard min(id / id_stride, world - 1)
+        uint64_t id;
+        float e;
+        if (cand_ids) {
+            id = cand_ids[(int64_t)li * R + i];
+            uint64_t w = id_stride ? id / id_stride : 0;
+            w = w < (uint64_t)world ? w : (uint64_t)world - 1;
+            e = candE[((int64_t)w * nlist + li) * R + i];
+        } else {
+            id = id_base + cand_slot[(int64_t)li * R + i];
+            e = candE[(int64_t)li * R + i];
+        }
+        rh_insert(hp, id, e);
         if (hp.len > k) { uint64_t a; float b; rh_pop(hp, &a, &b); }
     }
     const int q = qlist[li];

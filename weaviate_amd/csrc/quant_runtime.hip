@@ -678,8 +678,60 @@ static int sq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq) {
 // group's distance kernel, k_pq_finish merges it into the result heap in pop
 // order (and trims SQ / RQ to `trim`), k_rescore + k_pq_rescore_final rescore.
 // Outputs [nq][k].
-static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, int limit,
-                       int trim, int rescore, const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+// the compressed distances E[f][row] (+inf for invalid rows) and their 256-row
+// block minima of listed queries [g0, g0 + F) (PQ: qlist positions; the
+// thread-per-row SQ / RQ / BQ kernels index the query batch directly)
+static int hnsw_dist(wv_index* idx, hipStream_t s, int comp, const uint32_t* valid, const int32_t* qlist, int64_t nq,
+                     int64_t g0, int F, int64_t ld, float* E, float* Bm) {
+    const int64_t nslots = idx->hiwater;
+    const int wrapm = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
+    int rc = WV_OK;
+    if (comp == WV_COMPRESSION_PQ) {
+        const int m = idx->pq_m, K = idx->pq_ks;
+        const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
+        dim3 grid((unsigned)F, (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
+        if (idx->pq_adc == 2) {  // two queries per workgroup: 2 x the LUT chunk (64 KiB at ks = 256)
+            dim3 grid2((unsigned)((F + 1) / 2), grid.y);
+#define WV_ADC2(KCV, RPTV)                                                                                   \
+    do {                                                                                                     \
+        HIPCHK(hipFuncSetAttribute((const void*)k_pq_adc2<KCV, RPTV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                   (int)(2 * lds_adc)));                                                     \
+        k_pq_adc2<KCV, RPTV><<<grid2, 256, 2 * lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,    \
+                                                             idx->lut.as<float>(), qlist + g0, F, wrapm, ld, E, Bm); \
+    } while (0)
+            if (K == 256) WV_ADC2(256, PQ_RPT);
+            else WV_ADC2(0, PQ_RPT);
+#undef WV_ADC2
+        } else if (K == 256)
+            k_pq_adc<256><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,
+                                                     idx->lut.as<float>(), qlist + g0, wrapm, ld, E, Bm);
+        else
+            k_pq_adc<0><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,
+                                                   idx->lut.as<float>(), qlist + g0, wrapm, ld, E, Bm);
+    } else if (comp == WV_COMPRESSION_RQ8) {
+        rc = rq_dist(idx, s, valid, g0, F, ld, E, Bm);
+        if (rc) return rc;
+    } else if (comp == WV_COMPRESSION_SQ) {
+        dim3 grid((unsigned)((F + RQ_QPB - 1) / RQ_QPB), (unsigned)(ld / 256));
+        k_sq_dist<<<grid, 256, 0, s>>>(idx->sq_codes, idx->sq_meta, idx->sq_Dq, valid, nslots,
+                                       idx->sqq.as<uint4>(), idx->sqm.as<uint2>(), g0, F, wrapm, idx->sq_a2,
+                                       idx->sq_ab, idx->sq_ib2, ld, E, Bm);
+    } else {  // BQ
+        dim3 grid((unsigned)((F + RQ_QPB - 1) / RQ_QPB), (unsigned)(ld / 256));
+        k_bq_dist<<<grid, 256, 0, s>>>(idx->codes, idx->cap, idx->words, valid, nslots, idx->qcodes.as<uint64_t>(),
+                                       nq, g0, F, ld, E, Bm);
+    }
+    HIPCHK(hipGetLastError());
+    return rc;
+}
+
+// hnsw flat search, shared part: validation, query preparation, the
+// compressor's per-query state (LUT / codes), the identity query list.
+// *limit_io: the worker-heap limit (>= k on return); *comp_out: the compressor.
+static int hnsw_prep(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, int* limit_io,
+                     int* comp_out) {
+    int limit = *limit_io;
+    int rc = WV_OK;
     const int comp = idx->rq_bits ? WV_COMPRESSION_RQ8 : idx->compression;
     if (comp == WV_COMPRESSION_BQ && (qd + 63) / 64 != idx->words)  // HammingBitwise (distancer/hamming.go:63-66)
         return set_err(WV_ERR_VECTOR_LENGTH, "both vectors should have the same len");
@@ -695,9 +747,11 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     if (idx->rq_bits && !idx->rq_ready) return set_err(WV_ERR_QUANTIZER, "quantizer not initialized");
     if (limit < k) limit = k;
     const int R = limit;
+    *limit_io = limit;
+    *comp_out = comp;
     if (R > 8192) return set_err(WV_ERR_UNSUPPORTED, "limit %d > 8192", R);
     const int64_t nq_pad = round_up(nq, QB);
-    int rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
+    rc = prepare_queries(idx, s, d_qraw, nq, nq_pad);
     if (rc) return rc;
     const float* Qn = idx->qn.as<float>();
     idx->stats.queries += (uint64_t)nq;
@@ -729,6 +783,17 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         for (int64_t i = 0; i < nq; i++) id[i] = (int32_t)i;
         HIPCHK(hipMemcpyAsync(idx->ident.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
     }
+    (void)R;
+    return WV_OK;
+}
+
+static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, int limit,
+                       int trim, int rescore, const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
+    int comp = 0;
+    int rc = hnsw_prep(idx, s, d_qraw, nq, qd, k, &limit, &comp);
+    if (rc) return rc;
+    const int R = limit;
+    const float* Qn = idx->qn.as<float>();
     const int32_t* qlist = idx->ident.as<int32_t>();
     const int64_t nslots = idx->hiwater;
     const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
@@ -848,41 +913,8 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
         const bool time_it = idx->timing && g0 == 0 && !rep_by_query;
         if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
-        if (comp == WV_COMPRESSION_PQ) {
-            const int m = idx->pq_m, K = idx->pq_ks;
-            const size_t lds_adc = (size_t)PQ_CH * K * sizeof(float);
-            dim3 grid((unsigned)F, (unsigned)((nslots + 256 * PQ_RPT - 1) / (256 * PQ_RPT)));
-            if (idx->pq_adc == 2) {  // two queries per workgroup: 2 x the LUT chunk (64 KiB at ks = 256)
-                dim3 grid2((unsigned)((F + 1) / 2), grid.y);
-#define WV_ADC2(KCV, RPTV)                                                                                   \
-    do {                                                                                                     \
-        HIPCHK(hipFuncSetAttribute((const void*)k_pq_adc2<KCV, RPTV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                   (int)(2 * lds_adc)));                                                     \
-        k_pq_adc2<KCV, RPTV><<<grid2, 256, 2 * lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,    \
-                                                             idx->lut.as<float>(), qlist + g0, F, wrapm, ld, E, Bm); \
-    } while (0)
-                if (K == 256) WV_ADC2(256, PQ_RPT);
-                else WV_ADC2(0, PQ_RPT);
-#undef WV_ADC2
-            } else if (K == 256)
-                k_pq_adc<256><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,
-                                                         idx->lut.as<float>(), qlist + g0, wrapm, ld, E, Bm);
-            else
-                k_pq_adc<0><<<grid, 256, lds_adc, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots,
-                                                       idx->lut.as<float>(), qlist + g0, wrapm, ld, E, Bm);
-        } else if (comp == WV_COMPRESSION_RQ8) {
-            rc = rq_dist(idx, s, valid, g0, F, ld, E, Bm);
-            if (rc) return rc;
-        } else if (comp == WV_COMPRESSION_SQ) {
-            dim3 grid((unsigned)((F + RQ_QPB - 1) / RQ_QPB), (unsigned)(ld / 256));
-            k_sq_dist<<<grid, 256, 0, s>>>(idx->sq_codes, idx->sq_meta, idx->sq_Dq, valid, nslots,
-                                           idx->sqq.as<uint4>(), idx->sqm.as<uint2>(), g0, F, wrapm, idx->sq_a2,
-                                           idx->sq_ab, idx->sq_ib2, ld, E, Bm);
-        } else {  // BQ
-            dim3 grid((unsigned)((F + RQ_QPB - 1) / RQ_QPB), (unsigned)(ld / 256));
-            k_bq_dist<<<grid, 256, 0, s>>>(idx->codes, idx->cap, idx->words, valid, nslots, idx->qcodes.as<uint64_t>(),
-                                           nq, g0, F, ld, E, Bm);
-        }
+        rc = hnsw_dist(idx, s, comp, valid, qlist, nq, g0, F, ld, E, Bm);
+        if (rc) return rc;
         HIPCHK(hipGetLastError());
         if (time_it) HIPCHK(hipEventRecord(idx->ev1, s));
         HIPCHK(hipEventRecord(idx->evd[b], s));
@@ -969,6 +1001,225 @@ int search_hnsw_flat(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     const int limit = rescore ? hnsw_search_ef(idx, k) : k;  // flat_search.go:31-33
     const int trim = (sqrq && idx->rescore_limit >= k) ? idx->rescore_limit : 0;
     return search_hnsw(idx, s, d_qraw, nq, qd, k, limit, trim, rescore ? 1 : 0, valid, o_ids, o_d, o_n);
+}
+
+// ---- sharded hnsw flat search over compressed vectors (weaviate_amd/sharded.py
+// ShardedQuantSearch): every shard holds a contiguous id range with the same
+// quantizer; the worker heap (limit R) spans the shards in id order, then the
+// result heap and the rescoring follow -- the single index's search ----
+
+// the parameters the index's own SearchByVector uses: search_pq (PQ) or
+// search_hnsw_flat (SQ); RQ / BQ indexes have their own sharded forms or none
+static int quant_params(const wv_index* idx, int k, int* limit, int* trim, int* rescore) {
+    if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained && !idx->rq_bits) {
+        *rescore = idx->pq_rescore ? 1 : 0;
+        *limit = *rescore && idx->rescore_limit > k ? idx->rescore_limit : k;
+        *trim = 0;
+        return WV_OK;
+    }
+    if (idx->compression == WV_COMPRESSION_SQ && !idx->rq_bits) {
+        const bool rs = idx->hnsw_rescore != 0 && idx->rescore_limit != 0;
+        *rescore = rs ? 1 : 0;
+        *limit = rs ? hnsw_search_ef(idx, k) : k;
+        *trim = idx->rescore_limit >= k ? idx->rescore_limit : 0;
+        return WV_OK;
+    }
+    return set_err(WV_ERR_UNSUPPORTED, "quant sharding: trained PQ or SQ indexes only");
+}
+
+// phase 1: query state + the compressed distances of every row of this shard to
+// the whole batch (one group) and their 256-row block minima.
+// out[3] = {R (worker-heap limit), block count, rescore}
+extern "C" int wv_index_quant_begin(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                    int64_t* out, void* stream) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (nq <= 0) return set_err(WV_ERR_INVALID, "quant_begin: empty batch");
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    int limit = 0, trim = 0, rescore = 0, comp = 0;
+    int rc = quant_params(idx, k, &limit, &trim, &rescore);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    rc = hnsw_prep(idx, s, d_queries, nq, d, k, &limit, &comp);
+    if (rc) return rc;
+    const int64_t ld = std::max<int64_t>(round_up(idx->hiwater, EBLK), EBLK);
+    if (nq * ld * 4 > (16ll << 30))
+        return set_err(WV_ERR_UNSUPPORTED, "quant_begin: %lld queries x %lld rows exceed one 16 GiB distance group",
+                       (long long)nq, (long long)ld);
+    HIPCHK(idx->rE.ensure((size_t)nq * ld * sizeof(float)));
+    HIPCHK(idx->rB.ensure((size_t)nq * (ld / EBLK) * sizeof(float)));
+    if (idx->hiwater > 0) {
+        if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
+        rc = hnsw_dist(idx, s, comp, idx->present, idx->ident.as<int32_t>(), nq, 0, (int)nq, ld, idx->rE.as<float>(),
+                       idx->rB.as<float>());
+        if (rc) return rc;
+        if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
+        idx->stats.last_group_queries = (uint64_t)nq;
+    } else {
+        HIPCHK(hipMemsetAsync(idx->rB.p, 0x7f, (size_t)nq * (ld / EBLK) * sizeof(float), s));  // +huge: no rows
+    }
+    idx->qt_nq = nq;
+    idx->qt_ld = ld;
+    idx->qt_k = k;
+    idx->qt_R = limit;
+    idx->qt_trim = trim;
+    idx->qt_rescore = rescore;
+    idx->qt_comp = comp;
+    out[0] = limit;
+    out[1] = ld / EBLK;
+    out[2] = rescore;
+    if (!stream || (idx->timing && idx->hiwater > 0)) HIPCHK(hipStreamSynchronize(s));
+    if (idx->timing && idx->hiwater > 0) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
+        idx->stats.last_select_ms = ms;
+    }
+    return WV_OK;
+}
+
+// the block minima [nq][nblk] (each the compressed distance of one distinct row;
+// the caller's R smallest bound the worker heap across shards)
+extern "C" int wv_index_quant_blockmin(wv_index* idx, float* d_out, void* stream) {
+    if (!idx || !d_out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->qt_nq <= 0) return set_err(WV_ERR_INVALID, "quant_blockmin: no batch begun");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(d_out, idx->rB.p, (size_t)idx->qt_nq * (idx->qt_ld / EBLK) * sizeof(float),
+                          hipMemcpyDeviceToDevice, s));
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// the worker heap over this shard in id order from heap states d_in_* ([nq][R]
+// layout order by query, NULL = empty): extract = 1 -> extracted ascending
+// [nq][R], 0 -> the state; cap > 0 -> record every insertion in d_rec_*
+static int quant_replay(wv_index* idx, hipStream_t s, const uint64_t* in_i, const float* in_d, const int32_t* in_n,
+                        int extract, uint64_t* oi, float* od, int32_t* on, uint64_t* rec_i, float* rec_d,
+                        int32_t* rec_n, int cap) {
+    const int64_t nq = idx->qt_nq;
+    const int R = idx->qt_R;
+    HIPCHK(launch_replay_scan(R, (unsigned)nq, s, idx->rE.as<float>(), idx->rB.as<float>(), idx->present, idx->hiwater,
+                              idx->qt_ld, idx->ident.as<int32_t>(), (int)nq, R, idx->id_base, in_i, in_d, in_n,
+                              extract, 1, R, oi, od, on, 1, 1, rec_i, rec_d, rec_n, cap));
+    return WV_OK;
+}
+
+extern "C" int wv_index_quant_replay(wv_index* idx, const uint64_t* d_in_ids, const float* d_in_d,
+                                     const int32_t* d_in_len, int32_t extract, uint64_t* d_out_ids, float* d_out_d,
+                                     int32_t* d_out_len, void* stream) {
+    if (!idx || !d_out_ids || !d_out_d || !d_out_len) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->qt_nq <= 0) return set_err(WV_ERR_INVALID, "quant_replay: no batch begun");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = quant_replay(idx, s, d_in_ids, d_in_d, d_in_len, extract ? 1 : 0, d_out_ids, d_out_d, d_out_len, nullptr,
+                          nullptr, nullptr, 0);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+extern "C" int wv_index_quant_replay_record(wv_index* idx, const uint64_t* d_in_ids, const float* d_in_d,
+                                            const int32_t* d_in_len, int32_t cap, uint64_t* d_rec_ids,
+                                            float* d_rec_d, int32_t* d_rec_n, void* stream) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (cap < 1 || !d_rec_ids || !d_rec_d || !d_rec_n) return set_err(WV_ERR_INVALID, "invalid record buffers");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->qt_nq <= 0) return set_err(WV_ERR_INVALID, "quant_replay_record: no batch begun");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t nq = idx->qt_nq;
+    const int R = idx->qt_R;
+    HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));  // the state itself is not needed
+    HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
+    HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
+    int rc = quant_replay(idx, s, d_in_ids, d_in_d, d_in_len, 0, idx->ascI.as<uint64_t>(), idx->ascD.as<float>(),
+                          idx->ascN.as<int32_t>(), d_rec_ids, d_rec_d, d_rec_n, cap);
+    if (rc) return rc;
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// from the whole worker heap (extracted ascending [nq][R], global ids): the
+// result heap in pop order (flat_search.go) -> d_out_* [nq][k] without
+// rescoring; with rescoring the candidates after the trim, ascending id-list
+// order, as global ids d_cand_ids [nq][R] (unused slots ~0) + d_cand_n
+extern "C" int wv_index_quant_finish(wv_index* idx, const uint64_t* d_asc_ids, const float* d_asc_d,
+                                     const int32_t* d_asc_n, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n,
+                                     uint64_t* d_cand_ids, int32_t* d_cand_n, void* stream) {
+    if (!idx || !d_asc_ids || !d_asc_d || !d_asc_n) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->qt_nq <= 0) return set_err(WV_ERR_INVALID, "quant_finish: no batch begun");
+    if (idx->qt_rescore ? (!d_cand_ids || !d_cand_n) : (!d_out_ids || !d_out_d || !d_out_n))
+        return set_err(WV_ERR_INVALID, "nil output buffer");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t nq = idx->qt_nq;
+    const int R = idx->qt_R;
+    const size_t lds_f = (size_t)R * (sizeof(uint64_t) + sizeof(float)) + 16;
+    if (lds_f > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_pq_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
+    k_pq_finish<<<(unsigned)nq, 64, lds_f, s>>>(d_asc_ids, d_asc_d, d_asc_n, idx->ident.as<int32_t>(), (int)nq, R,
+                                                idx->qt_k, idx->qt_rescore, idx->id_base, d_out_ids, d_out_d, d_out_n,
+                                                nullptr, d_cand_n, idx->qt_rescore ? idx->qt_trim : 0, d_cand_ids);
+    HIPCHK(hipGetLastError());
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// exact SingleDist of the candidates this shard holds (others left as they are)
+extern "C" int wv_index_quant_rescore(wv_index* idx, const uint64_t* d_cand_ids, const int32_t* d_cand_n, float* d_E,
+                                      void* stream) {
+    if (!idx || !d_cand_ids || !d_cand_n || !d_E) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->qt_nq <= 0) return set_err(WV_ERR_INVALID, "quant_rescore: no batch begun");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t nq = idx->qt_nq;
+    const int R = idx->qt_R;
+    const int64_t npairs = nq * R;
+    const float* Qn = idx->qn.as<float>();
+    const int32_t* qlist = idx->ident.as<int32_t>();
+    const bool v5 = idx->variant == WV_VARIANT_AVX512;
+#define WV_RS(M, V) k_rescore_ids<M, V><<<(unsigned)((npairs + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, Qn, idx->dims, d_cand_ids, d_cand_n, qlist, (int)nq, R, idx->id_base, idx->hiwater, d_E)
+    switch (idx->metric) {
+    case WV_METRIC_L2_SQUARED: if (v5) WV_RS(L2, AVX512); else WV_RS(L2, AVX256); break;
+    case WV_METRIC_DOT: if (v5) WV_RS(DOT, AVX512); else WV_RS(DOT, AVX256); break;
+    case WV_METRIC_COSINE_DOT: if (v5) WV_RS(COSINE, AVX512); else WV_RS(COSINE, AVX256); break;
+    default: WV_RS(HAMMING, AVX256); break;
+    }
+#undef WV_RS
+    HIPCHK(hipGetLastError());
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// h.rescore (hnsw/search.go:1067-1110) over the candidates: d_E_all [world][nq][R],
+// the entry of id from shard min(id / id_stride, world - 1)
+extern "C" int wv_quant_rescore_final(int32_t device, int64_t nq, int32_t R, int32_t k, int32_t world,
+                                      uint64_t id_stride, const uint64_t* d_cand_ids, const int32_t* d_cand_n,
+                                      const float* d_E_all, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n,
+                                      void* stream) {
+    HIPCHK(hipSetDevice(device));
+    if (nq <= 0) return WV_OK;
+    if (k <= 0 || R < k || world < 1) return set_err(WV_ERR_INVALID, "quant_rescore_final: invalid k / R / world");
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<int32_t> id((size_t)nq);
+    for (int64_t i = 0; i < nq; i++) id[i] = (int32_t)i;
+    DBuf ql;
+    HIPCHK(ql.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(ql.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const size_t lds_q = (size_t)(k + 1) * (sizeof(uint64_t) + sizeof(float)) + 16;
+    if (lds_q > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void*)k_pq_rescore_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
+    k_pq_rescore_final<<<(unsigned)nq, 64, lds_q, s>>>(nullptr, d_E_all, d_cand_n, ql.as<int32_t>(), (int)nq, R, k, 0,
+                                                       d_out_ids, d_out_d, d_out_n, d_cand_ids, world, id_stride);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));  // ql is freed on return
+    ql.release();
+    return WV_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -343,6 +343,171 @@ class ShardedBQSearch:
         return self.b.bq_final(self.world, self.id_stride, ids, ln, E_all)
 
 
+class GpuQuantShardBackend(GpuShardBackend):
+    """Rank-local engine of the hnsw flat search over compressed vectors
+    (wv_index_quant_* entry points, include/wv_knn.h): a trained PQ or an SQ
+    index holding ids [id_base, id_base + n), the quantizer shared by all ranks."""
+
+    def _s(self):
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def quant_begin(self, q: torch.Tensor, k: int):
+        import ctypes
+        nq, d = q.shape
+        out = (ctypes.c_int64 * 3)()
+        self._check(self._l.wv_index_quant_begin(self.index._h, q.data_ptr(), nq, d, k, ctypes.addressof(out), self._s()))
+        self.nq, self.k = nq, k
+        self.R, self.nblk, self.rescore = int(out[0]), int(out[1]), bool(out[2])
+        return self.R
+
+    def quant_bounds(self):
+        """[nq, R] ascending: the R smallest block minima of this shard (+inf padded)."""
+        bm = torch.empty((self.nq, self.nblk), dtype=torch.float32, device=self.dev)
+        self._check(self._l.wv_index_quant_blockmin(self.index._h, bm.data_ptr(), self._s()))
+        out = torch.full((self.nq, self.R), float("inf"), dtype=torch.float32, device=self.dev)
+        m = min(self.R, self.nblk)
+        out[:, :m] = torch.topk(bm, m, dim=1, largest=False, sorted=True).values
+        return out
+
+    def quant_replay(self, state, extract: bool):
+        ids = torch.empty((self.nq, self.R), dtype=torch.int64, device=self.dev)
+        dd = torch.empty((self.nq, self.R), dtype=torch.float32, device=self.dev)
+        ln = torch.empty(self.nq, dtype=torch.int32, device=self.dev)
+        si, sd, sl = (None, None, None) if state is None else (state[0].data_ptr(), state[1].data_ptr(),
+                                                               state[2].data_ptr())
+        self._check(self._l.wv_index_quant_replay(self.index._h, si, sd, sl, 1 if extract else 0, ids.data_ptr(),
+                                                  dd.data_ptr(), ln.data_ptr(), self._s()))
+        return ids, dd, ln
+
+    def quant_replay_record(self, state, cap: int):
+        ri = torch.empty((self.nq, cap), dtype=torch.int64, device=self.dev)
+        rd = torch.empty((self.nq, cap), dtype=torch.float32, device=self.dev)
+        rn = torch.empty(self.nq, dtype=torch.int32, device=self.dev)
+        self._check(self._l.wv_index_quant_replay_record(self.index._h, state[0].data_ptr(), state[1].data_ptr(),
+                                                         state[2].data_ptr(), cap, ri.data_ptr(), rd.data_ptr(),
+                                                         rn.data_ptr(), self._s()))
+        return ri, rd, rn
+
+    def quant_finish(self, ai, ad, an):
+        """-> (ids, dists, counts) [nq, k] without rescoring, else the rescoring
+        candidates (global ids [nq, R], counts)."""
+        k = self.k
+        if self.rescore:
+            ci = torch.empty((self.nq, self.R), dtype=torch.int64, device=self.dev)
+            cn = torch.empty(self.nq, dtype=torch.int32, device=self.dev)
+            self._check(self._l.wv_index_quant_finish(self.index._h, ai.data_ptr(), ad.data_ptr(), an.data_ptr(),
+                                                      None, None, None, ci.data_ptr(), cn.data_ptr(), self._s()))
+            return ci, cn
+        oi = torch.empty((self.nq, k), dtype=torch.int64, device=self.dev)
+        od = torch.empty((self.nq, k), dtype=torch.float32, device=self.dev)
+        on = torch.empty(self.nq, dtype=torch.int32, device=self.dev)
+        self._check(self._l.wv_index_quant_finish(self.index._h, ai.data_ptr(), ad.data_ptr(), an.data_ptr(),
+                                                  oi.data_ptr(), od.data_ptr(), on.data_ptr(), None, None, self._s()))
+        return oi, od, on
+
+    def quant_rescore(self, ci, cn):
+        E = torch.zeros(ci.shape, dtype=torch.float32, device=self.dev)
+        self._check(self._l.wv_index_quant_rescore(self.index._h, ci.data_ptr(), cn.data_ptr(), E.data_ptr(),
+                                                   self._s()))
+        return E
+
+    def quant_rescore_final(self, world: int, id_stride: int, ci, cn, E_all):
+        nq, R = ci.shape
+        oi = torch.empty((nq, self.k), dtype=torch.int64, device=self.dev)
+        od = torch.empty((nq, self.k), dtype=torch.float32, device=self.dev)
+        on = torch.empty(nq, dtype=torch.int32, device=self.dev)
+        self._check(self._l.wv_quant_rescore_final(self.device, nq, R, self.k, world, id_stride, ci.data_ptr(),
+                                                   cn.data_ptr(), E_all.data_ptr(), oi.data_ptr(), od.data_ptr(),
+                                                   on.data_ptr(), self._s()))
+        return oi, od, on
+
+
+class ShardedQuantSearch:
+    """hnsw's flat search over compressed vectors (trained PQ, SQ;
+    hnsw/flat_search.go:28-141 + h.rescore, hnsw/search.go:1047-1110) over
+    contiguous id-range shards with the single index's exact semantics:
+      1. every rank: the compressed distances of its rows to the batch and
+         their 256-row block minima (wv_index_quant_begin, parallel);
+      2. the worker heap (limit R) over all shards in id order in one parallel
+         hop, BQ's record scheme (ShardedBQSearch): the R smallest block minima
+         of each rank are all-gathered; rank r >= 1 replays from R copies of
+         T_r and records its insertions; rank 0 replays from empty heaps; the
+         records are all-gathered and merged on rank 0's states
+         (wv_heap_merge_records).  A record over its cap sends the batch down
+         the serial chain;
+      3. the result heap in pop order; with rescoring, every rank computes the
+         exact distances of the candidates it holds, one all-gather, and
+         h.rescore picks each candidate's distance from its owner."""
+
+    def __init__(self, backend, device: torch.device, id_stride: int):
+        self.b = backend
+        self.dev = device
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.id_stride = int(id_stride)
+
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        return ShardedFlatSearch._all_gather(self, t)
+
+    def search(self, q: torch.Tensor, k: int):
+        nq = q.shape[0]
+        R = self.b.quant_begin(q, k)
+        self.path = "chain"
+        res = self._replay_parallel(nq, R) if self.world > 1 else None
+        if res is not None:
+            self.path = "parallel"
+            ai, ad, an = res
+        else:
+            ai, ad, an = self._chain(nq, R)
+        fin = self.b.quant_finish(ai, ad, an)
+        if not self.b.rescore:
+            return fin
+        ci, cn = fin
+        E_all = self._all_gather(self.b.quant_rescore(ci, cn))
+        return self.b.quant_rescore_final(self.world, self.id_stride, ci, cn, E_all)
+
+    def _replay_parallel(self, nq: int, R: int):
+        """Step 2 in one hop; -> the merged worker heaps extracted ascending, or
+        None when a record overflowed (host sync: one flag)."""
+        cap = 2 * R
+        G = self._all_gather(self.b.quant_bounds())  # [W, nq, R]
+        if self.rank == 0:
+            ti, td, tn = self.b.quant_replay(None, False)  # heap states from empty heaps
+            ri = torch.zeros((nq, cap), dtype=torch.int64, device=self.dev)
+            rd = torch.zeros((nq, cap), dtype=torch.float32, device=self.dev)
+            ri[:, :R], rd[:, :R] = ti, td
+            rn = tn
+        else:
+            allq = torch.arange(nq, device=self.dev)
+            T = prefix_bound(self.rank, allq, R, G, torch.full((self.rank, nq), R, dtype=torch.int32, device=self.dev),
+                             torch.zeros((self.rank, nq), dtype=torch.int32, device=self.dev))
+            ri, rd, rn = self.b.quant_replay_record(fake_heaps(T, R), cap)
+        pk = torch.cat([ri.contiguous().view(torch.int32).reshape(nq, 2 * cap), rd.contiguous().view(torch.int32),
+                        rn[:, None]], 1)
+        A = self._all_gather(pk)  # [W, nq, 3 cap + 1]
+        rec = (A[..., : 2 * cap].contiguous().view(torch.int64), A[..., 2 * cap: 3 * cap].contiguous().view(torch.float32),
+               A[..., 3 * cap].contiguous())
+        st = (rec[0][0, :, :R].contiguous(), rec[1][0, :, :R].contiguous(), rec[2][0].contiguous())
+        ai, ad, an, un = self.b.merge_records(self.world, R, cap, st, rec)  # extracted ascending
+        if bool(un.any()):
+            return None
+        return ai, ad, an
+
+    def _chain(self, nq: int, R: int):
+        """Step 2 as the serial chain: rank r continues rank r-1's heaps; the
+        last rank extracts (ascending)."""
+        state = None
+        for r in range(self.world):
+            last = r == self.world - 1
+            if self.rank == r:  # one packed broadcast per hop: [nq][2R ids | R dists | len]
+                buf = ShardedFlatSearch._pack_state(*self.b.quant_replay(state, last))
+            else:
+                buf = torch.empty((nq, 3 * R + 1), dtype=torch.int32, device=self.dev)
+            dist.broadcast(buf, src=r)
+            state = ShardedFlatSearch._unpack_state(buf, R)
+        return state
+
+
 class ShardedFlatSearch:
     """search(queries) over all ranks of the default process group."""
 
