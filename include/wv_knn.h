@@ -347,14 +347,15 @@ int wv_index_bq_replay_record(wv_index *idx, const uint64_t *d_in_ids, const flo
 
 /* Sharded hnsw flat search over compressed vectors (hnsw/flat_search.go:28-141
  * + h.rescore, hnsw/search.go:1047-1110, the search a trained PQ index
- * (search_pq) or an SQ index (search_hnsw_flat) runs; weaviate_amd/sharded.py
+ * (search_pq) or an SQ index (search_hnsw_flat) runs; and flat's rq-8 / rq-1
+ * searchByVectorQuantized, flat/index.go:460-532 (search_rq); weaviate_amd/sharded.py
  * ShardedQuantSearch).  Every shard holds a contiguous id range and the same
  * quantizer (wv_index_pq_set_centers / wv_index_sq_restore).  The worker heap
  * of limit R spans the shards in id order, exactly as BQ's R-heap above:
  *   wv_index_quant_begin     query state + the compressed distances of every row
  *                            of this shard to the batch (one group, <= 16 GiB)
- *                            and their 256-row block minima; out[3] = {R, block
- *                            count, rescore};
+ *                            and their 256-row block minima; out[4] = {R, block
+ *                            count, rescore, final form};
  *   wv_index_quant_blockmin  the minima [nq][blocks] (each the distance of one
  *                            distinct row: the R smallest bound the heap top);
  *   wv_index_quant_replay    the worker heap over this shard from states d_in_*
@@ -366,9 +367,13 @@ int wv_index_bq_replay_record(wv_index *idx, const uint64_t *d_in_ids, const flo
  *                            the result without rescoring, else the rescoring
  *                            candidates (global ids, after the SQ trim);
  *   wv_index_quant_rescore   exact SingleDist of the candidates this shard holds;
- *   wv_quant_rescore_final   h.rescore over the [world][nq][R] distance tiles
- *                            (the entry of id from shard min(id / id_stride,
- *                            world - 1)). */
+ *   wv_quant_rescore_final   the rescoring heap over the [world][nq][R]
+ *                            distance tiles (the entry of id from shard
+ *                            min(id / id_stride, world - 1)): form 0 =
+ *                            h.rescore, 1 = searchByVectorQuantized's heap
+ *                            (flat/index.go:525-531) for flat rq-8 / rq-1
+ *                            indexes (search_rq: every worker-heap item is a
+ *                            candidate). */
 int wv_index_quant_begin(wv_index *idx, const float *d_queries, int64_t nq, int64_t d, int32_t k, int64_t *out,
                          void *stream);
 int wv_index_quant_blockmin(wv_index *idx, float *d_out, void *stream);
@@ -382,7 +387,8 @@ int wv_index_quant_finish(wv_index *idx, const uint64_t *d_asc_ids, const float 
                           int32_t *d_cand_n, void *stream);
 int wv_index_quant_rescore(wv_index *idx, const uint64_t *d_cand_ids, const int32_t *d_cand_n, float *d_E,
                            void *stream);
-int wv_quant_rescore_final(int32_t device, int64_t nq, int32_t R, int32_t k, int32_t world, uint64_t id_stride,
+int wv_quant_rescore_final(int32_t device, int32_t form, int64_t nq, int32_t R, int32_t k, int32_t world,
+                           uint64_t id_stride,
                            const uint64_t *d_cand_ids, const int32_t *d_cand_n, const float *d_E_all,
                            uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_counts, void *stream);
 

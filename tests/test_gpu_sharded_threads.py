@@ -252,10 +252,13 @@ def run_quant_ranks(monkeypatch, backs, q, k, id_stride):
     ("pq", 4, "l2-squared", 1, 3000, 24, 7, 40, True),     # integer data: ADC ties
     ("sq", 3, "l2-squared", 0, 5000, 48, 10, 20, True),    # SQ: ef limit, trim to the rescore limit
     ("sq", 2, "dot", 1, 6000, 32, 10, 0, True),            # SQ rescore limit 0: no rescoring
+    ("rq8", 3, "cosine", 0, 6000, 64, 10, 30, True),       # flat rq-8: searchByVectorQuantized
+    ("rq1", 2, "l2-squared", 1, 7000, 64, 10, 40, True),   # flat rq-1, integer data
 ])
 def test_sharded_quant_equals_single_index(wv, oracle, monkeypatch, comp, shards, metric, kind, per, d, k, rl, rescore):
     """ShardedQuantSearch with GpuQuantShardBackends as threads: hnsw's flat
-    search over PQ / SQ codes (hnsw/flat_search.go:28-141 + h.rescore) with the
+    search over PQ / SQ codes (hnsw/flat_search.go:28-141 + h.rescore) and
+    flat's searchByVectorQuantized over rq-8 / rq-1 codes, with the
     worker heap across the shards in one parallel hop (or the chain when a
     record overflows), the result heap and the owners' rescoring.  Every rank
     must return the single index's result exactly (same quantizer)."""
@@ -266,14 +269,16 @@ def test_sharded_quant_equals_single_index(wv, oracle, monkeypatch, comp, shards
     kw = dict(distance=metric, variant="avx256", rescore_limit=rl)
     if comp == "pq":
         kw["pq"] = {"segments": d // 4, "centroids": 32, "trainingLimit": 100000, "rescore": rescore}
-    else:
+    elif comp == "sq":
         kw["sq"] = True
+    else:  # the rotation is seeded: the same on every shard
+        kw["rq"] = {"bits": 8 if comp == "rq8" else 1}
     single = wv.FlatIndex(**kw)
     single.add_batch(np.arange(n, dtype=np.uint64), data)
     if comp == "pq":
         single.pq_fit(seed=3)
         centers = single.pq_centers()
-    else:
+    elif comp == "sq":
         single.sq_fit(2000)
         info = single.sq_info()
     si, sd, sn = single.search_by_vector_batch(queries, k)
@@ -284,7 +289,7 @@ def test_sharded_quant_equals_single_index(wv, oracle, monkeypatch, comp, shards
         idx.add_batch(np.arange(lo, lo + per, dtype=np.uint64), data[lo:lo + per])
         if comp == "pq":
             idx.pq_set_centers(centers)
-        else:
+        elif comp == "sq":
             idx.sq_restore(info["a"], info["b"])
         backs.append(GpuQuantShardBackend(idx, 0))
     q = torch.from_numpy(queries).to("cuda")

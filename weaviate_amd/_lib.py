@@ -125,7 +125,7 @@ SIGNATURES = {
     "wv_index_quant_replay_record": (C.c_int, [P, P, P, P, i32, P, P, P, P]),
     "wv_index_quant_finish": (C.c_int, [P, P, P, P, P, P, P, P, P, P]),
     "wv_index_quant_rescore": (C.c_int, [P, P, P, P, P]),
-    "wv_quant_rescore_final": (C.c_int, [i32, i64, i32, i32, i32, u64, P, P, P, P, P, P, P]),
+    "wv_quant_rescore_final": (C.c_int, [i32, i32, i64, i32, i32, i32, u64, P, P, P, P, P, P, P]),
     "wv_index_pq_fit": (C.c_int, [P, u64]),
     "wv_index_pq_set_centers": (C.c_int, [P, pf32, i64]),
     "wv_index_pq_centers": (C.c_int, [P, pf32, i64]),

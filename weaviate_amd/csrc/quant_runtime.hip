@@ -173,11 +173,11 @@ static int bq_rescore(wv_index* idx, hipStream_t s, const uint64_t* ids, const i
 // Phase 4: insertToHeap(heap, k, ...) in pop order + extractHeap
 static int bq_final(hipStream_t s, int64_t nq, int R, int k, int world, uint64_t id_stride, const int32_t* qlist,
                     const uint64_t* ids, const int32_t* cnt, const float* E, uint64_t* o_ids, float* o_d,
-                    int32_t* o_n) {
+                    int32_t* o_n, int asc = 0) {
     const size_t lds_f = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
     if (lds_f > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_bq_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
-    k_bq_final<<<(unsigned)nq, 64, lds_f, s>>>(ids, E, cnt, qlist, (int)nq, R, k, world, id_stride, o_ids, o_d, o_n, 0);
+    k_bq_final<<<(unsigned)nq, 64, lds_f, s>>>(ids, E, cnt, qlist, (int)nq, R, k, world, id_stride, o_ids, o_d, o_n, asc);
     HIPCHK(hipGetLastError());
     return WV_OK;
 }
@@ -1008,28 +1008,38 @@ int search_hnsw_flat(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
 // quantizer; the worker heap (limit R) spans the shards in id order, then the
 // result heap and the rescoring follow -- the single index's search ----
 
-// the parameters the index's own SearchByVector uses: search_pq (PQ) or
-// search_hnsw_flat (SQ); RQ / BQ indexes have their own sharded forms or none
-static int quant_params(const wv_index* idx, int k, int* limit, int* trim, int* rescore) {
-    if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained && !idx->rq_bits) {
+// the parameters the index's own SearchByVector uses: search_pq (PQ),
+// search_hnsw_flat (SQ) or search_rq (flat rq-8 / rq-1: searchByVectorQuantized,
+// every worker-heap item rescored, *form = 1); BQ has ShardedBQSearch
+static int quant_params(const wv_index* idx, int k, int* limit, int* trim, int* rescore, int* form) {
+    *form = 0;
+    if (idx->rq_bits) {
+        *rescore = 1;
+        *limit = idx->rescore_limit > k ? idx->rescore_limit : k;  // searchTimeRescore (flat/index.go:413-421)
+        *trim = 0;
+        *form = 1;
+        return *limit > 8192 ? set_err(WV_ERR_UNSUPPORTED, "rescore limit %d > 8192", *limit) : WV_OK;
+    }
+    if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained) {
         *rescore = idx->pq_rescore ? 1 : 0;
         *limit = *rescore && idx->rescore_limit > k ? idx->rescore_limit : k;
         *trim = 0;
         return WV_OK;
     }
-    if (idx->compression == WV_COMPRESSION_SQ && !idx->rq_bits) {
+    if (idx->compression == WV_COMPRESSION_SQ) {
         const bool rs = idx->hnsw_rescore != 0 && idx->rescore_limit != 0;
         *rescore = rs ? 1 : 0;
         *limit = rs ? hnsw_search_ef(idx, k) : k;
         *trim = idx->rescore_limit >= k ? idx->rescore_limit : 0;
         return WV_OK;
     }
-    return set_err(WV_ERR_UNSUPPORTED, "quant sharding: trained PQ or SQ indexes only");
+    return set_err(WV_ERR_UNSUPPORTED, "quant sharding: trained PQ, SQ or RQ indexes only");
 }
 
 // phase 1: query state + the compressed distances of every row of this shard to
 // the whole batch (one group) and their 256-row block minima.
-// out[3] = {R (worker-heap limit), block count, rescore}
+// out[4] = {R (worker-heap limit), block count, rescore, final form (0: h.rescore,
+// 1: searchByVectorQuantized's rescoring heap)}
 extern "C" int wv_index_quant_begin(wv_index* idx, const float* d_queries, int64_t nq, int64_t d, int32_t k,
                                     int64_t* out, void* stream) {
     if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
@@ -1037,8 +1047,8 @@ extern "C" int wv_index_quant_begin(wv_index* idx, const float* d_queries, int64
     HIPCHK(hipSetDevice(idx->device));
     if (nq <= 0) return set_err(WV_ERR_INVALID, "quant_begin: empty batch");
     if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
-    int limit = 0, trim = 0, rescore = 0, comp = 0;
-    int rc = quant_params(idx, k, &limit, &trim, &rescore);
+    int limit = 0, trim = 0, rescore = 0, comp = 0, form = 0;
+    int rc = quant_params(idx, k, &limit, &trim, &rescore, &form);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
     rc = hnsw_prep(idx, s, d_queries, nq, d, k, &limit, &comp);
@@ -1066,9 +1076,11 @@ extern "C" int wv_index_quant_begin(wv_index* idx, const float* d_queries, int64
     idx->qt_trim = trim;
     idx->qt_rescore = rescore;
     idx->qt_comp = comp;
+    idx->qt_form = form;
     out[0] = limit;
     out[1] = ld / EBLK;
     out[2] = rescore;
+    out[3] = form;
     if (!stream || (idx->timing && idx->hiwater > 0)) HIPCHK(hipStreamSynchronize(s));
     if (idx->timing && idx->hiwater > 0) {
         float ms = 0.f;
@@ -1158,6 +1170,12 @@ extern "C" int wv_index_quant_finish(wv_index* idx, const uint64_t* d_asc_ids, c
     hipStream_t s = (hipStream_t)stream;
     const int64_t nq = idx->qt_nq;
     const int R = idx->qt_R;
+    if (idx->qt_form == 1) {  // searchByVectorQuantized: every worker-heap item is a candidate (ascending)
+        HIPCHK(hipMemcpyAsync(d_cand_ids, d_asc_ids, (size_t)nq * R * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(d_cand_n, d_asc_n, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        if (!stream) HIPCHK(hipStreamSynchronize(s));
+        return WV_OK;
+    }
     const size_t lds_f = (size_t)R * (sizeof(uint64_t) + sizeof(float)) + 16;
     if (lds_f > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_pq_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
@@ -1196,9 +1214,10 @@ extern "C" int wv_index_quant_rescore(wv_index* idx, const uint64_t* d_cand_ids,
     return WV_OK;
 }
 
-// h.rescore (hnsw/search.go:1067-1110) over the candidates: d_E_all [world][nq][R],
-// the entry of id from shard min(id / id_stride, world - 1)
-extern "C" int wv_quant_rescore_final(int32_t device, int64_t nq, int32_t R, int32_t k, int32_t world,
+// the rescoring heap over the candidates: form 0 = h.rescore (hnsw/search.go:1067-1110),
+// form 1 = searchByVectorQuantized's (flat/index.go:525-531, candidates ascending);
+// d_E_all [world][nq][R], the entry of id from shard min(id / id_stride, world - 1)
+extern "C" int wv_quant_rescore_final(int32_t device, int32_t form, int64_t nq, int32_t R, int32_t k, int32_t world,
                                       uint64_t id_stride, const uint64_t* d_cand_ids, const int32_t* d_cand_n,
                                       const float* d_E_all, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n,
                                       void* stream) {
@@ -1211,12 +1230,19 @@ extern "C" int wv_quant_rescore_final(int32_t device, int64_t nq, int32_t R, int
     DBuf ql;
     HIPCHK(ql.ensure((size_t)nq * sizeof(int32_t)));
     HIPCHK(hipMemcpyAsync(ql.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    const size_t lds_q = (size_t)(k + 1) * (sizeof(uint64_t) + sizeof(float)) + 16;
-    if (lds_q > 64 * 1024)
-        HIPCHK(hipFuncSetAttribute((const void*)k_pq_rescore_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
-    k_pq_rescore_final<<<(unsigned)nq, 64, lds_q, s>>>(nullptr, d_E_all, d_cand_n, ql.as<int32_t>(), (int)nq, R, k, 0,
-                                                       d_out_ids, d_out_d, d_out_n, d_cand_ids, world, id_stride);
-    HIPCHK(hipGetLastError());
+    if (form == 1) {
+        int rc = bq_final(s, nq, R, k, world, id_stride, ql.as<int32_t>(), d_cand_ids, d_cand_n, d_E_all, d_out_ids,
+                          d_out_d, d_out_n, 1);
+        if (rc) return rc;
+    } else {
+        const size_t lds_q = (size_t)(k + 1) * (sizeof(uint64_t) + sizeof(float)) + 16;
+        if (lds_q > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute((const void*)k_pq_rescore_final, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds_q));
+        k_pq_rescore_final<<<(unsigned)nq, 64, lds_q, s>>>(nullptr, d_E_all, d_cand_n, ql.as<int32_t>(), (int)nq, R, k,
+                                                           0, d_out_ids, d_out_d, d_out_n, d_cand_ids, world, id_stride);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipStreamSynchronize(s));  // ql is freed on return
     ql.release();
     return WV_OK;

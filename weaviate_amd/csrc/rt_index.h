@@ -115,7 +115,7 @@ struct wv_index {
     int64_t bq_nq = 0;           // BQ batch in flight (bq_begin): queries and R
     int bq_R = 0;
     int64_t qt_nq = 0, qt_ld = 0;  // sharded hnsw flat batch in flight (wv_index_quant_begin)
-    int qt_k = 0, qt_R = 0, qt_trim = 0, qt_rescore = 0, qt_comp = 0;
+    int qt_k = 0, qt_R = 0, qt_trim = 0, qt_rescore = 0, qt_comp = 0, qt_form = 0;
     // PQ (compressionhelpers.ProductQuantizer): codebook [m][ks][ds], codes
     // [ceil(m/4)][cap] u32 (4 segment bytes per word, see pq_kernels.hip)
     int pq_m = 0, pq_ks = 0, pq_ds = 0, pq_training_limit = 0, pq_rescore = 1, pq_trained = 0;

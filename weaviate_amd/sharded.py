@@ -344,9 +344,10 @@ class ShardedBQSearch:
 
 
 class GpuQuantShardBackend(GpuShardBackend):
-    """Rank-local engine of the hnsw flat search over compressed vectors
-    (wv_index_quant_* entry points, include/wv_knn.h): a trained PQ or an SQ
-    index holding ids [id_base, id_base + n), the quantizer shared by all ranks."""
+    """Rank-local engine of the search over compressed vectors (wv_index_quant_*
+    entry points, include/wv_knn.h): a trained PQ, an SQ or a flat rq-8 / rq-1
+    index holding ids [id_base, id_base + n), the quantizer shared by all ranks
+    (RQ: the same seeded rotation on every rank)."""
 
     def _s(self):
         return torch.cuda.current_stream(self.dev).cuda_stream
@@ -354,10 +355,10 @@ class GpuQuantShardBackend(GpuShardBackend):
     def quant_begin(self, q: torch.Tensor, k: int):
         import ctypes
         nq, d = q.shape
-        out = (ctypes.c_int64 * 3)()
+        out = (ctypes.c_int64 * 4)()
         self._check(self._l.wv_index_quant_begin(self.index._h, q.data_ptr(), nq, d, k, ctypes.addressof(out), self._s()))
         self.nq, self.k = nq, k
-        self.R, self.nblk, self.rescore = int(out[0]), int(out[1]), bool(out[2])
+        self.R, self.nblk, self.rescore, self.form = int(out[0]), int(out[1]), bool(out[2]), int(out[3])
         return self.R
 
     def quant_bounds(self):
@@ -416,7 +417,7 @@ class GpuQuantShardBackend(GpuShardBackend):
         oi = torch.empty((nq, self.k), dtype=torch.int64, device=self.dev)
         od = torch.empty((nq, self.k), dtype=torch.float32, device=self.dev)
         on = torch.empty(nq, dtype=torch.int32, device=self.dev)
-        self._check(self._l.wv_quant_rescore_final(self.device, nq, R, self.k, world, id_stride, ci.data_ptr(),
+        self._check(self._l.wv_quant_rescore_final(self.device, self.form, nq, R, self.k, world, id_stride, ci.data_ptr(),
                                                    cn.data_ptr(), E_all.data_ptr(), oi.data_ptr(), od.data_ptr(),
                                                    on.data_ptr(), self._s()))
         return oi, od, on
@@ -424,7 +425,9 @@ class GpuQuantShardBackend(GpuShardBackend):
 
 class ShardedQuantSearch:
     """hnsw's flat search over compressed vectors (trained PQ, SQ;
-    hnsw/flat_search.go:28-141 + h.rescore, hnsw/search.go:1047-1110) over
+    hnsw/flat_search.go:28-141 + h.rescore, hnsw/search.go:1047-1110) and
+    flat's searchByVectorQuantized over rq-8 / rq-1 codes
+    (flat/index.go:460-532: every worker-heap item rescored) over
     contiguous id-range shards with the single index's exact semantics:
       1. every rank: the compressed distances of its rows to the batch and
          their 256-row block minima (wv_index_quant_begin, parallel);
