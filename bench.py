@@ -375,8 +375,6 @@ def main():
     if flat is not None and args.dims is not None and args.dims != flat["d"]:
         flat = dict(flat, d=args.dims, name=flat["name"].replace(f"x {flat['d']} ", f"x {args.dims} ")
                     + f" at d={args.dims}")
-    if rq_bits and world > 1:
-        raise SystemExit(f"--workload {args.workload}: sharded search is not available yet (1 GPU)")
     dims = BQ_DIMS if bq else PQ_DIMS if pq else flat["d"] if flat else DIMS
     K_ = flat["k"] if flat else K
     # flat / pq: a fixed corpus split over the ranks (strong scaling); bq: configs[3]
@@ -435,7 +433,7 @@ def main():
     out_d = torch.empty((B, K_), dtype=torch.float32, device=dev)
     out_n = torch.empty(B, dtype=torch.int32, device=dev)
 
-    if shard and pq:
+    if shard and (pq or rq_bits):
         from weaviate_amd.sharded import GpuQuantShardBackend, ShardedQuantSearch
         searcher = ShardedQuantSearch(GpuQuantShardBackend(index, local_rank), dev, (n_total + world - 1) // world)
 
@@ -468,7 +466,7 @@ def main():
     torch.cuda.synchronize()
     sel_ms, tot_ms = [], []
     replays0 = index.stats()["replayed_queries"]
-    if shard and not (bq or pq):
+    if shard and not (bq or pq or rq_bits):
         searcher.flagged = 0
     t0 = time.perf_counter()
     res = None
@@ -483,10 +481,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     replays = index.stats()["replayed_queries"] - replays0
-    if shard and not (bq or pq):
+    if shard and not (bq or pq or rq_bits):
         replays = int(searcher.flagged)  # the cross-shard replay's queries (this rank's view = every rank's)
     sharded_check = None
-    if args.sharded and world == 1 and (flat or pq):
+    if args.sharded and world == 1 and (flat or pq or rq_bits):
         # the sharded protocol at one rank must equal the single-index search
         si, sd, sn = step()[:3]
         s = torch.cuda.current_stream(dev).cuda_stream
@@ -656,7 +654,8 @@ def main():
                                + ((", R-heap replay in one parallel hop (all-gathered block-minimum bounds, "
                                    "recorded insertions, on-device merge) + all-gather rescoring" if bq
                                    else ", worker heap in one parallel hop (block-minimum bounds, recorded "
-                                   "insertions, on-device merge), codebook trained on rank 0 and broadcast" if pq
+                                   "insertions, on-device merge)" + (", codebook trained on rank 0 and broadcast" if pq
+                                                                     else ", all-gather rescoring") if (pq or rq_bits)
                                    else ", RCCL all-gather merge") if world > 1 else ""),
                 "replayed_queries": int(replays),
             },

@@ -43,6 +43,17 @@ class FakeGroup:
         torch.cuda.synchronize()
         self.bar.wait()
 
+    def all_reduce(self, t, op=None):  # MIN (the only reduction the protocols use)
+        r = self.get_rank()
+        self.slots[r] = t.clone()
+        self.bar.wait()
+        m = self.slots[0].clone()
+        for i in range(1, self.world):
+            m = torch.minimum(m, self.slots[i])
+        t.copy_(m)
+        torch.cuda.synchronize()
+        self.bar.wait()
+
     def broadcast(self, t, src):
         r = self.get_rank()
         if r == src:
@@ -247,7 +258,7 @@ def run_quant_ranks(monkeypatch, backs, q, k, id_stride):
 
 
 @pytest.mark.parametrize("comp,shards,metric,kind,per,d,k,rl,rescore", [
-    ("pq", 3, "l2-squared", 0, 6000, 32, 10, -1, False),   # worker heap = k
+    ("pq", 3, "l2-squared", 0, 6000, 32, 10, -1, False),   # worker heap = k (query chunks forced: below)
     ("pq", 2, "cosine", 0, 8000, 64, 10, 60, True),        # rescoring: owners' exact distances
     ("pq", 4, "l2-squared", 1, 3000, 24, 7, 40, True),     # integer data: ADC ties
     ("sq", 3, "l2-squared", 0, 5000, 48, 10, 20, True),    # SQ: ef limit, trim to the rescore limit
@@ -292,6 +303,9 @@ def test_sharded_quant_equals_single_index(wv, oracle, monkeypatch, comp, shards
         elif comp == "sq":
             idx.sq_restore(info["a"], info["b"])
         backs.append(GpuQuantShardBackend(idx, 0))
+    if comp == "pq" and not rescore:  # rank r's distance group holds 37 + 10 r queries: chunks of 37 on every rank
+        for r, b in enumerate(backs):
+            b.max_batch = (lambda v: (lambda: v))(37 + 10 * r)
     q = torch.from_numpy(queries).to("cuda")
     out, paths = run_quant_ranks(monkeypatch, backs, q, k, per)
     assert len(set(paths)) == 1, paths

@@ -1036,6 +1036,15 @@ static int quant_params(const wv_index* idx, int k, int* limit, int* trim, int* 
     return set_err(WV_ERR_UNSUPPORTED, "quant sharding: trained PQ, SQ or RQ indexes only");
 }
 
+// the largest batch wv_index_quant_begin takes on this shard (one 16 GiB distance group)
+extern "C" int wv_index_quant_max_batch(wv_index* idx, int64_t* out) {
+    if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    const int64_t ld = std::max<int64_t>(round_up(idx->hiwater, EBLK), EBLK);
+    *out = std::max<int64_t>(1, (16ll << 30) / (ld * 4));
+    return WV_OK;
+}
+
 // phase 1: query state + the compressed distances of every row of this shard to
 // the whole batch (one group) and their 256-row block minima.
 // out[4] = {R (worker-heap limit), block count, rescore, final form (0: h.rescore,

@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import torch
 import torch.distributed as dist
+from torch.distributed import ReduceOp
 
 
 def prefix_bound(r: int, ql: torch.Tensor, k: int, gd, gc, gf, bounds=None) -> torch.Tensor:
@@ -361,6 +362,12 @@ class GpuQuantShardBackend(GpuShardBackend):
         self.R, self.nblk, self.rescore, self.form = int(out[0]), int(out[1]), bool(out[2]), int(out[3])
         return self.R
 
+    def max_batch(self) -> int:
+        import ctypes
+        out = ctypes.c_int64()
+        self._check(self._l.wv_index_quant_max_batch(self.index._h, ctypes.addressof(out)))
+        return int(out.value)
+
     def quant_bounds(self):
         """[nq, R] ascending: the R smallest block minima of this shard (+inf padded)."""
         bm = torch.empty((self.nq, self.nblk), dtype=torch.float32, device=self.dev)
@@ -453,6 +460,22 @@ class ShardedQuantSearch:
         return ShardedFlatSearch._all_gather(self, t)
 
     def search(self, q: torch.Tensor, k: int):
+        """Query chunks that every rank's distance group holds (one all-reduce
+        agrees on the size), each through steps 1-3."""
+        nq = q.shape[0]
+        mb = getattr(self.b, "max_batch", None)
+        chunk = nq
+        if mb is not None:
+            t = torch.tensor([min(int(mb()), nq)], dtype=torch.int64, device=self.dev)
+            if self.world > 1:
+                dist.all_reduce(t, op=ReduceOp.MIN)
+            chunk = max(1, int(t.item()))
+        if chunk >= nq:
+            return self._search(q, k)
+        parts = [self._search(q[i:i + chunk], k) for i in range(0, nq, chunk)]
+        return tuple(torch.cat(p) for p in zip(*parts))
+
+    def _search(self, q: torch.Tensor, k: int):
         nq = q.shape[0]
         R = self.b.quant_begin(q, k)
         self.path = "chain"
