@@ -319,3 +319,52 @@ def test_sharded_quant_equals_single_index(wv, oracle, monkeypatch, comp, shards
     for b in backs:
         b.index.close()
     single.close()
+
+
+def test_c5_sharded_pq_full_size(wv, oracle, monkeypatch):
+    """configs[4] across 4 shards (ranks as threads): 10M x 960 U[0,1) rows in
+    contiguous 2.5M-row ranges, one codebook (PQ m=240 x 256 trained on the
+    first 100k rows, distributed as bench.py --workload pq does at N > 1), the
+    bench's B = 256: ShardedQuantSearch on every rank equals the single index's
+    search (the minima-only k_pq_adc3 path) bit for bit."""
+    from weaviate_amd import _lib
+    from weaviate_amd.sharded import GpuQuantShardBackend
+    lib = _lib.load()
+    n, d, k, B, W = 10_000_000, 960, 10, 256, 4
+    per = n // W
+    pqc = {"segments": 240, "centroids": 256, "trainingLimit": 100_000, "rescore": False}
+
+    def build(lo, hi):
+        idx = wv.FlatIndex(distance="l2-squared", dims=d, variant="avx256", id_base=lo, pq=pqc)
+        idx.reserve(hi - lo)
+        stage = torch.empty((1_000_000, d), dtype=torch.float32, device="cuda")
+        for r0 in range(lo, hi, 1_000_000):
+            m = min(1_000_000, hi - r0)
+            _lib.check(lib.wv_gen_device(0, 2, 1, r0, m, d, stage.data_ptr(), None))
+            _lib.check(lib.wv_index_add_range_device(idx._h, r0, stage.data_ptr(), m, d))
+        torch.cuda.synchronize()
+        return idx
+
+    single = build(0, n)
+    single.pq_fit(seed=1)
+    centers = single.pq_centers()
+    q = torch.empty((B, d), dtype=torch.float32, device="cuda")
+    _lib.check(lib.wv_gen_device(0, 2, 2, 0, B, d, q.data_ptr(), None))
+    torch.cuda.synchronize()
+    si, sd, sn = single.search_by_vector_batch(q.cpu().numpy(), k)
+    single.close()
+    backs = []
+    for r in range(W):
+        idx = build(r * per, (r + 1) * per)
+        idx.pq_set_centers(centers)
+        backs.append(GpuQuantShardBackend(idx, 0))
+    out, paths = run_quant_ranks(monkeypatch, backs, q, k, per)
+    assert paths == ["parallel"] * W, paths
+    for r in range(W):
+        oi, od, on = (t.numpy() for t in out[r])
+        np.testing.assert_array_equal(on, sn, err_msg=f"rank {r}")
+        for i in range(B):
+            np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), si[i, :sn[i]], err_msg=f"rank {r} q{i}")
+            np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), sd[i, :sn[i]].view(np.uint32))
+    for b in backs:
+        b.index.close()

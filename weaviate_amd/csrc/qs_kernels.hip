@@ -1260,7 +1260,9 @@ __global__ void k_flag_list(const int32_t* __restrict__ flags, int nq, int32_t* 
 // skipped block cannot pass insertToHeap's `top.Dist > distance` for any row.
 // Queries with non-finite values visit every block.  Blocks are taken two at
 // a time (lanes 0-31, 32-63), inserted by lane 0 in row order.
-template <int METRIC, int VARIANT>
+// DBG = 1 (option replay_dbg, diagnostics only): per-wave clock totals of the key
+// scan, the exact distances and the heap, printed for the first listed queries
+template <int METRIC, int VARIANT, int DBG = 0>
 __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key, int64_t ldk, int64_t nb,
                                                    const float* __restrict__ eps_q, const float4* __restrict__ qinfo,
                                                    const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
@@ -1298,6 +1300,8 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     // parked in LDS; a round with no visitable block is skipped whole
     constexpr int RU = 16;
     float* skey = s_d + 64 + 4;  // [RU * 64]
+    long long t_dist = 0, t_heap = 0, t_all = DBG ? clock64() : 0;
+    int n_vis = 0, n_ins = 0;
     for (int64_t r0 = 0; r0 < nb; r0 += 64 * RU) {
         float kvr[RU];
 #pragma unroll
@@ -1347,9 +1351,12 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
             const int jj = lh ? j2 : j1;
             const int64_t row = (b0 + jj) * 32 + li;
             const bool ok = jj >= 0 && row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+            long long tc = DBG ? clock64() : 0;
             const float dist = ok ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
             uint64_t mask = __ballot(ok && (len < k || top > dist));
+            if (DBG) { t_dist += clock64() - tc; n_vis += j2 >= 0 ? 2 : 1; }
             if (mask == 0) continue;
+            if (DBG) { tc = clock64(); n_ins += __popcll(mask); }
             s_d[lane] = dist;
             __syncthreads();
             if (lane == 0) {
@@ -1364,9 +1371,13 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
                 *s_len = h.len;
             }
             __syncthreads();
+            if (DBG) t_heap += clock64() - tc;
         }
     }
     }
+    if (DBG && lane == 0 && li_ < 24)
+        printf("k_blk_replay dbg: list %d query %d visits %d offered %d heap_len %d cycles: all %lld dist %lld heap %lld\n",
+               li_, q, n_vis, n_ins, *s_len, clock64() - t_all, t_dist, t_heap);
     const int64_t orow = by_list ? li_ : q;
     if (!extract) {  // hand the heap on in layout order (kout == k)
         const int n = *s_len;

@@ -91,8 +91,9 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
     if (rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
 #define WV_RP(M, V)                                                                                             \
     do {                                                                                                        \
-        if (rlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); \
-        k_blk_replay<M, V><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list); \
+        if (rlds > 64 * 1024) { HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); } \
+        if (idx->replay_dbg) k_blk_replay<M, V, 1><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list); \
+        else k_blk_replay<M, V><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list); \
     } while (0)
     switch (metric) {
     case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;

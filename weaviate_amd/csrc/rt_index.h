@@ -175,6 +175,7 @@ struct wv_index {
     DBuf bmCnt, bmOff, bmPairs, bmE;                          // block-major exact (k_inv_*, k_exact_bm)
     DBuf qsCap;                                               // per query: upper bound of the (k+1)-th exact distance
     int exact_cap = 1;                                        // k_blk_exact drops values above qsCap (phase 0)
+    int replay_dbg = 0;                                       // k_blk_replay clock diagnostics (printf)
     int pq_cand = 1;                                          // PQ search: block minima + candidate blocks (k_pq_cand)
     int pq_adc3 = 1;                                          // minima by k_pq_adc3 (queries on the lanes), 0: k_pq_adc2
     DBuf lutg;                                                // the LUT regrouped for k_pq_adc3 [64-query group][s][c][64]

@@ -578,6 +578,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     if (k == "margin") { if (value < 2 || value > 30) return set_err(WV_ERR_INVALID, "margin out of range"); idx->margin = (int)value; }
     else if (k == "force_replay") idx->force_replay = (int)value;
     else if (k == "spans") idx->spans_opt = (int)value;
+    else if (k == "replay_dbg") idx->replay_dbg = value != 0;  // diagnostics: k_blk_replay clock totals (printf)
     else if (k == "pq_adc3") {  // 1: k_pq_adc3 (default), 0: k_pq_adc2; 3, 4: timing experiments (wrong results)
         if (value < 0 || value > 4) return set_err(WV_ERR_INVALID, "pq_adc3 must be 0..4");
         idx->pq_adc3 = (int)value;

@@ -494,8 +494,10 @@ class ShardedQuantSearch:
 
     def _replay_parallel(self, nq: int, R: int):
         """Step 2 in one hop; -> the merged worker heaps extracted ascending, or
-        None when a record overflowed (host sync: one flag)."""
-        cap = 2 * R
+        None when a record overflowed (host sync: one flag).  A small worker
+        heap (PQ without rescoring: R = k) records a few dozen insertions
+        beyond R on a shard holding that many rows under T_r: cap = 2R + 64."""
+        cap = 2 * R + 64
         G = self._all_gather(self.b.quant_bounds())  # [W, nq, R]
         if self.rank == 0:
             ti, td, tn = self.b.quant_replay(None, False)  # heap states from empty heaps
