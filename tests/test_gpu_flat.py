@@ -410,6 +410,28 @@ def test_pooled_replay_float_data(wv, oracle, metric):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")
 
 
+@pytest.mark.parametrize("metric,variant,d,k", [("l2-squared", "avx256", 128, 100), ("cosine", "avx256", 37, 10),
+                                               ("dot", "avx256", 200, 100), ("l2-squared", "avx256", 5, 10),
+                                               ("cosine", "avx512", 100, 24), ("l2-squared", "avx512", 160, 100),
+                                               ("dot", "avx256", 771, 10)])
+def test_one_wave_replay_float_data(wv, oracle, metric, variant, d, k):
+    """Random float data, every query forced through the one-wave k_blk_replay
+    (replay_par 0): the 8-lanes-per-row exact distances (AVX2 order, and the
+    AVX-512 order below 128 dims; 32-, 8-element and scalar tails) and the
+    lane-per-row form (AVX-512 from 128 dims) equal the oracle bit for bit."""
+    n = 20000
+    data = gen(oracle, 0, 97, n, d)
+    queries = gen(oracle, 0, 98, 16, d)
+    idx, orc = build_pair(wv, oracle, metric, variant, data)
+    idx.set_option("replay_par", 0)
+    idx.set_option("qs_force_flag", 1)
+    before = idx.stats()["replayed_queries"]
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["replayed_queries"] - before == len(queries)
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} d{d} q{qi}")
+
+
 @pytest.mark.parametrize("metric,kind,variant,n,d,k", [("l2-squared", 1, "avx256", 40000, 128, 100),   # C2-like ties
                                                       ("cosine", 0, "avx512", 30000, 200, 10),
                                                       ("dot", 0, "avx256", 20000, 500, 24),

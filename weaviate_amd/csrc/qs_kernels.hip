@@ -1081,6 +1081,7 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     const int nc = ncand[q];
     const float* qv = Qn + (int64_t)q * dpad;
     const int li = lane & 31, lh = lane >> 5;
+    const bool coop = exact8_ok<METRIC, VARIANT>(d);
     WaveTopL<R> t;
     t.init(cap ? cap[q] : __builtin_inff());  // only the k+1 smallest are used: nothing above cap
     int nvalid = 0;
@@ -1093,7 +1094,22 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
             ok = row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
         }
         float e = __builtin_inff();
-        if (ok) e = ebuf ? ebuf[(int64_t)q * ldE + j * 32 + li] : exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d);
+        if (ebuf) {
+            if (ok) e = ebuf[(int64_t)q * ldE + j * 32 + li];
+        } else if (coop) {  // 8 lanes per row, rows 8g + (lane >> 3) of the pass
+            const float* xp[8];
+#pragma unroll
+            for (int g = 0; g < 8; g++) {
+                const int r = 8 * g + (lane >> 3);
+                const int jg = r >= 32 && j0 + 1 < nc ? j0 + 1 : j0;
+                const int64_t rw = (int64_t)cand[(int64_t)q * L + jg] * 32 + (r & 31);
+                xp[g] = X + (rw < nrows ? rw : 0) * dpad;
+            }
+            const float dl = exact8_rows64<METRIC>(qv, xp, d, lane);
+            if (ok) e = dl;
+        } else if (ok) {
+            e = exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d);
+        }
         nvalid += __popcll(__ballot(ok));
         t.offer(ok ? e : __builtin_inff(), ok ? (uint32_t)row : NO_ID, sbk[w], sbi[w], lane);
     }
@@ -1260,6 +1276,14 @@ __global__ void k_flag_list(const int32_t* __restrict__ flags, int nq, int32_t* 
 // skipped block cannot pass insertToHeap's `top.Dist > distance` for any row.
 // Queries with non-finite values visit every block.  Blocks are taken two at
 // a time (lanes 0-31, 32-63), inserted by lane 0 in row order.
+// Row filter (Xb != null, finite query): a visited row's approximate distance
+// A_row from the bf16 planes (the block key's formula with S summed per lane,
+// error bound eps_row = qs_eps with gacc_r for that summation) is a lower
+// bound A_row - eps_row of its exact distance; only rows with
+// top > A_row - eps_row (or a short heap) get the reference-order distance.
+// A rejected row cannot pass insertToHeap's test, so the heap sees the same
+// insertions; the planes are half the fp32 bytes (C2: most visited rows are
+// rejected).
 // DBG = 1 (option replay_dbg, diagnostics only): per-wave clock totals of the key
 // scan, the exact distances and the heap, printed for the first listed queries
 template <int METRIC, int VARIANT, int DBG = 0>
@@ -1272,8 +1296,10 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
                                                    uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
                                                    int32_t* __restrict__ out_n, const uint64_t* __restrict__ in_ids,
                                                    const float* __restrict__ in_d, const int32_t* __restrict__ in_len,
-                                                   int extract, int by_list) {
-    // dynamic LDS: [k] heap records (PHeap) | [64] f32 | len (16 B) | [RU * 64] keys
+                                                   int extract, int by_list, const uint16_t* __restrict__ Xb, int dpb,
+                                                   const float* __restrict__ xn2, const uint32_t* __restrict__ qsmax,
+                                                   const uint32_t* __restrict__ maxn2, float gd, float gacc_r) {
+    // dynamic LDS: [k] heap records (PHeap) | [64] f32 | len (16 B) | [RU * 64] keys | [dpb] bf16(q) as f32
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     HeapRec* hr = reinterpret_cast<HeapRec*>(rsm);
     float* s_d = reinterpret_cast<float*>(hr + k);
@@ -1289,6 +1315,7 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     const float* kr = key + (int64_t)q * ldk;
     const float* qv = Qn + (int64_t)q * dpad;
     const int li = lane & 31, lh = lane >> 5;
+    const bool coop = exact8_ok<METRIC, VARIANT>(d);
     // the heap handed over by the previous shard (layout order), or empty
     int len_in = in_len ? in_len[by_list ? li_ : q] : 0;
     len_in = len_in < 0 ? 0 : len_in > k ? k : len_in;
@@ -1300,6 +1327,14 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     // parked in LDS; a round with no visitable block is skipped whole
     constexpr int RU = 16;
     float* skey = s_d + 64 + 4;  // [RU * 64]
+    const bool filt = Xb != nullptr && !noskip;
+    float* sqh = skey + RU * 64;  // [dpb]: bf16(q) (k_query_split's rounding), widened
+    float eps_r = 0.f;
+    if (filt) {
+        for (int c = lane; c < dpb; c += 64) sqh[c] = (float)(__bf16)(c < d ? qv[c] : 0.f);
+        eps_r = qs_eps(metric, qi, qsmax, maxn2, gd, gacc_r);
+        __syncthreads();
+    }
     long long t_dist = 0, t_heap = 0, t_all = DBG ? clock64() : 0;
     int n_vis = 0, n_ins = 0;
     for (int64_t r0 = 0; r0 < nb; r0 += 64 * RU) {
@@ -1327,6 +1362,7 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
         const int64_t bb = b0 + lane;
         float lb = __builtin_inff();
         bool has = false;
+        const uint32_t vwb = bb < nb && bb * 32 < nrows ? valid[bb] : 0u;  // the group's valid words (nb may pass the bitmap)
         if (bb < nb) {
             const float kv = skey[(b0 - r0) + lane];
             has = noskip || kv < __builtin_inff();
@@ -1350,10 +1386,69 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
             if (j1 < 0) break;
             const int jj = lh ? j2 : j1;
             const int64_t row = (b0 + jj) * 32 + li;
-            const bool ok = jj >= 0 && row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+            const uint32_t vword = __shfl(vwb, jj < 0 ? 0 : jj);
+            const bool ok = jj >= 0 && row < nrows && ((vword >> li) & 1u);
             long long tc = DBG ? clock64() : 0;
-            const float dist = ok ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
-            uint64_t mask = __ballot(ok && (len < k || top > dist));
+            float dist = 0.f;
+            bool cand = ok;  // an exact distance was computed for this lane's row
+            if (filt) {
+                bool need = ok;
+                if (ok && len >= k) {
+                    float s0 = 0.f, s1 = 0.f;
+#pragma unroll 4
+                    for (int c = 0; c < dpb; c += 16) {
+                        const uint4* xp = reinterpret_cast<const uint4*>(Xb + bf3_plane_index(row, c, dpb));
+                        const uint4 v0 = xp[0], v1 = xp[1];
+                        const float4* qp = reinterpret_cast<const float4*>(sqh + c);
+                        const float4 a0 = qp[0], a1 = qp[1], a2 = qp[2], a3 = qp[3];
+                        s0 = fmaf(__uint_as_float(v0.x << 16), a0.x, s0); s1 = fmaf(__uint_as_float(v0.x & 0xFFFF0000u), a0.y, s1);
+                        s0 = fmaf(__uint_as_float(v0.y << 16), a0.z, s0); s1 = fmaf(__uint_as_float(v0.y & 0xFFFF0000u), a0.w, s1);
+                        s0 = fmaf(__uint_as_float(v0.z << 16), a1.x, s0); s1 = fmaf(__uint_as_float(v0.z & 0xFFFF0000u), a1.y, s1);
+                        s0 = fmaf(__uint_as_float(v0.w << 16), a1.z, s0); s1 = fmaf(__uint_as_float(v0.w & 0xFFFF0000u), a1.w, s1);
+                        s0 = fmaf(__uint_as_float(v1.x << 16), a2.x, s0); s1 = fmaf(__uint_as_float(v1.x & 0xFFFF0000u), a2.y, s1);
+                        s0 = fmaf(__uint_as_float(v1.y << 16), a2.z, s0); s1 = fmaf(__uint_as_float(v1.y & 0xFFFF0000u), a2.w, s1);
+                        s0 = fmaf(__uint_as_float(v1.z << 16), a3.x, s0); s1 = fmaf(__uint_as_float(v1.z & 0xFFFF0000u), a3.y, s1);
+                        s0 = fmaf(__uint_as_float(v1.w << 16), a3.z, s0); s1 = fmaf(__uint_as_float(v1.w & 0xFFFF0000u), a3.w, s1);
+                    }
+                    const float S = s0 + s1;
+                    const float kv = METRIC == L2 ? fmaf(-2.f, S, xn2[row]) : -S;
+                    need = top > qs_key_to_a(metric, kv, qi.x) - eps_r;
+                }
+                if (coop) {  // the few rows that need it, 8 lanes per row (exact_dist8)
+                    const uint64_t nm = __ballot(need);
+                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0));
+                    const int cnt = __popcll(nm);
+                    if (need) s_d[rank] = __int_as_float((int)row);
+                    __syncthreads();
+                    for (int p0 = 0; p0 < cnt; p0 += 8) {
+                        const int gsel = p0 + (lane >> 3);
+                        const int64_t rw = (int64_t)__float_as_int(s_d[gsel < cnt ? gsel : 0]);  // spare groups repeat row 0 of the list
+                        const float* xp1[1] = {X + rw * dpad};
+                        float dv[1];
+                        exact_dist8<METRIC, 1>(qv, xp1, d, lane & 7, dv);
+                        const float dg = __shfl(dv[0], ((rank - p0) & 7) * 8);
+                        if (need && rank >= p0 && rank < p0 + 8) dist = dg;
+                    }
+                    __syncthreads();
+                } else if (need) {
+                    dist = exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d);
+                }
+                cand = need;
+            } else if (coop) {  // 8 lanes per row, rows 8g + (lane >> 3) of the pair
+                const float* xp[8];
+#pragma unroll
+                for (int g = 0; g < 8; g++) {
+                    const int r = 8 * g + (lane >> 3);
+                    const int jg = r >= 32 && j2 >= 0 ? j2 : j1;
+                    const int64_t rw = (b0 + jg) * 32 + (r & 31);
+                    xp[g] = X + (rw < nrows ? rw : 0) * dpad;
+                }
+                const float dl = exact8_rows64<METRIC>(qv, xp, d, lane);
+                dist = ok ? dl : 0.f;
+            } else if (ok) {
+                dist = exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d);
+            }
+            uint64_t mask = __ballot(cand && (len < k || top > dist));
             if (DBG) { t_dist += clock64() - tc; n_vis += j2 >= 0 ? 2 : 1; }
             if (mask == 0) continue;
             if (DBG) { tc = clock64(); n_ins += __popcll(mask); }

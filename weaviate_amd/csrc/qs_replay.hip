@@ -87,13 +87,17 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
         HIPCHK(hipGetLastError());
         return WV_OK;
     }
-    const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float);
+    // row filter from the bf16 planes (block-key indexes): gacc_r bounds the
+    // accumulation error of k_blk_replay's two-way per-lane sum of dpb products
+    const uint16_t* Xb = idx->qs_planes ? idx->Xb : nullptr;
+    const float gd = (float)gamma_n(idx->dpb + 8), gacc_r = (float)gamma_n(idx->dpb + 2);
+    const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float) + (size_t)idx->dpb * sizeof(float);
     if (rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
 #define WV_RP(M, V)                                                                                             \
     do {                                                                                                        \
         if (rlds > 64 * 1024) { HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); } \
-        if (idx->replay_dbg) k_blk_replay<M, V, 1><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list); \
-        else k_blk_replay<M, V><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list); \
+        if (idx->replay_dbg) k_blk_replay<M, V, 1><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r); \
+        else k_blk_replay<M, V><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r); \
     } while (0)
     switch (metric) {
     case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;

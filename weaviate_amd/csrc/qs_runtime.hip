@@ -35,7 +35,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     HIPCHK(idx->qsList.ensure((size_t)2 * qc * sizeof(int32_t)));
     if (!o_flags || phase) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
     if (phase && qc < nq) return set_err(WV_ERR_UNSUPPORTED, "two-phase shard search: batch exceeds one query chunk");
-    const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float);
+    const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float) + (size_t)idx->dpb * sizeof(float);
     if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
     // error-bound constants: reference-order fp32 (gamma_{dpb+8}) and the MFMA's
     // fp32 accumulation over NK chained 16-deep products (u' = 2^-22)
@@ -464,7 +464,7 @@ extern "C" int wv_index_replay_device(wv_index* idx, const float* d_queries, int
     const bool have_data = idx->dims != 0 && idx->npresent > 0;
     if (have_data && d != idx->dims)
         return set_err(WV_ERR_VECTOR_LENGTH, "%lld vs %d: vector lengths don't match", (long long)d, idx->dims);
-    const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float);
+    const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float) + (size_t)idx->dpb * sizeof(float);
     const bool keyed = have_data && idx->qs_keys_nq == nq && rlds <= 160 * 1024;
     if (keyed) {
         const float* Qn = idx->qn.as<float>();  // the prepared rows of that batch

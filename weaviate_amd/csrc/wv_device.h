@@ -171,6 +171,114 @@ __device__ __forceinline__ float exact_dist(const float* q, const float* x, int 
 }
 
 // ---------------------------------------------------------------------------
+// exact-order distance, 8 lanes per row (coalesced rows)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float lane_xor1(float v) {  // DPP quad_perm [1,0,3,2]
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_xor2(float v) {  // DPP quad_perm [2,3,0,1]
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_xor4(float v) {  // ds_swizzle bitmask mode, xor_mask 4
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (4 << 10) | 0x1F));
+}
+
+// True when exact_dist8 computes exact_dist<METRIC, VARIANT> for n elements:
+// the AVX2 order, and the AVX-512 order below 128 elements where both coincide.
+template <int METRIC, int VARIANT>
+__device__ __forceinline__ bool exact8_ok(int n) {
+    return METRIC != HAMMING && (VARIANT == AVX256 || n < 128);
+}
+
+// exact_dist8<METRIC, G>: exact_dist<METRIC, AVX256> of G rows per 8-lane
+// group at once.  Lane sub = lane & 7 owns float4 slot sub of every
+// 32-element chunk, i.e. acc[sub >> 1][4 (sub & 1) .. +3] of exact_raw, so a
+// load instruction reads whole 128-byte lines of 8 rows (the lane-per-row form
+// reads 16 bytes of 64 rows).  reduce_ymm4's tree pairs the slots by xor 2
+// (acc1 + acc0, acc3 + acc2), xor 4 (a23 + a01) and xor 1 (lo + hi); IEEE
+// addition is commutative, so both partners hold the identical sum.  The
+// 8-element tail feeds acc[0] (slots 0 and 1) and the scalar tail `sum` in
+// every lane, as in exact_raw.  All 64 lanes must be active, each group with
+// the same q and n; every lane returns its group's distances.
+template <int METRIC, int G>
+__device__ __forceinline__ void exact_dist8(const float* __restrict__ q, const float* const (&x)[G], int n,
+                                            int sub, float (&out)[G]) {
+    constexpr int M = METRIC == L2 ? L2 : DOT;
+    float4 acc[G];
+    float sum[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) { acc[g] = make_float4(0.f, 0.f, 0.f, 0.f); sum[g] = 0.f; }
+    int e = 0;
+    if (n >= 8) {
+        // one row per group: four chunks' loads in flight (16 VGPRs)
+#pragma unroll(G == 1 ? 4 : 1)
+        for (; n - e >= 32; e += 32) {
+            const float4 a = ld4(q + e + 4 * sub);
+            float4 b[G];
+#pragma unroll
+            for (int g = 0; g < G; g++) b[g] = ld4(x[g] + e + 4 * sub);
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                acc[g].x = elem_step<M>(acc[g].x, a.x, b[g].x);
+                acc[g].y = elem_step<M>(acc[g].y, a.y, b[g].y);
+                acc[g].z = elem_step<M>(acc[g].z, a.z, b[g].z);
+                acc[g].w = elem_step<M>(acc[g].w, a.w, b[g].w);
+            }
+        }
+        for (; n - e >= 8; e += 8) {
+            if (sub < 2) {
+                const float4 a = ld4(q + e + 4 * sub);
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    const float4 b = ld4(x[g] + e + 4 * sub);
+                    acc[g].x = elem_step<M>(acc[g].x, a.x, b.x);
+                    acc[g].y = elem_step<M>(acc[g].y, a.y, b.y);
+                    acc[g].z = elem_step<M>(acc[g].z, a.z, b.z);
+                    acc[g].w = elem_step<M>(acc[g].w, a.w, b.w);
+                }
+            }
+        }
+    }
+    for (; e < n; e++) {
+        const float a = q[e];
+#pragma unroll
+        for (int g = 0; g < G; g++) sum[g] = scalar_step<M>(sum[g], a, x[g][e]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        float r = sum[g];
+        if (n >= 8) {
+            float4 p = acc[g];
+            p.x = p.x + lane_xor2(p.x); p.y = p.y + lane_xor2(p.y);
+            p.z = p.z + lane_xor2(p.z); p.w = p.w + lane_xor2(p.w);
+            p.x = p.x + lane_xor4(p.x); p.y = p.y + lane_xor4(p.y);
+            p.z = p.z + lane_xor4(p.z); p.w = p.w + lane_xor4(p.w);
+            float h = (p.x + p.y) + (p.z + p.w);
+            h = h + lane_xor1(h);
+            r = r + h;
+        }
+        if (METRIC == DOT) r = -r;
+        if (METRIC == COSINE) { r = 1.f - r; r = r < 0.f ? 0.f : r; }
+        out[g] = r;
+    }
+}
+
+// 64 rows per wave with exact_dist8: xp[g] is the row of lane 8g + (lane >> 3);
+// returns the distance of row `lane` (the lane-per-row layout of the callers).
+template <int METRIC>
+__device__ __forceinline__ float exact8_rows64(const float* __restrict__ q, const float* const (&xp)[8], int n, int lane) {
+    float dv[8];
+    exact_dist8<METRIC, 8>(q, xp, n, lane & 7, dv);
+    float r = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+        const float t = __shfl(dv[g], (lane & 7) * 8);
+        r = (lane >> 3) == g ? t : r;
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
 // wave-wide bitonic sort over NS = 64*R (key,id) pairs; element e = r*64+lane.
 // Order: key ascending, then id ascending (placeholders: +inf, NO_ID).
 // ---------------------------------------------------------------------------
