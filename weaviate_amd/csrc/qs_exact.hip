@@ -11,7 +11,11 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
                       const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
                       int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
                       const float* capv) {
-#define WV_EXR(RV, M, V) k_blk_exact<RV, M, V><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv)
+#define WV_EXR(RV, M, V)                                                                                             \
+    do {                                                                                                             \
+        if (eb) k_blk_exact<RV, M, V, true><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv); \
+        else k_blk_exact<RV, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv); \
+    } while (0)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \
     case L2: if (v5) WV_EXR(RV, L2, AVX512); else WV_EXR(RV, L2, AVX256); break;   \

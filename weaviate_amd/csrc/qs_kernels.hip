@@ -876,10 +876,17 @@ struct WaveTopL {
         thr = cap = cap_;
         cnt = 0;
     }
+    // rows 0..R-2 are sorted: sort the pending row alone, reverse it (the R
+    // rows then form one bitonic sequence) and run only the final merge stage
+    // of the 64R-element network (the same sorted result as a full sort)
     __device__ __forceinline__ void merge(const float* bk, const uint32_t* bi, int lane) {
-        key[R - 1] = lane < cnt ? bk[lane] : __builtin_inff();
-        id[R - 1] = lane < cnt ? bi[lane] : NO_ID;
-        bitonic_sort<R>(key, id, lane);
+        float pk[1] = {lane < cnt ? bk[lane] : __builtin_inff()};
+        uint32_t pi[1] = {lane < cnt ? bi[lane] : NO_ID};
+        bitonic_sort<1>(pk, pi, lane);
+        key[R - 1] = __shfl(pk[0], 63 - lane);
+        id[R - 1] = (uint32_t)__shfl((int)pi[0], 63 - lane);
+#pragma unroll
+        for (int j = 32 * R; j > 0; j >>= 1) cmpx_step<R>(key, id, 64 * R, j, lane);
         thr = fminf(__shfl(key[R - 2], 63), cap);
         cnt = 0;
     }
@@ -1047,13 +1054,13 @@ __global__ __launch_bounds__(256) void k_blk_gthresh(const float* __restrict__ t
     if (lane == 0) ncand[q] = keep;
 }
 
-// k_blk_exact<R, METRIC, VARIANT>: one workgroup (4 waves) per query over its
+// k_blk_exact<R, METRIC, VARIANT, EB>: one workgroup (4 waves) per query over its
 // candidate blocks (each wave two blocks per pass: lanes 0-31 and 32-63, lane
-// = row); ebuf != null: the distances come from k_exact_bm.  Reference-order SingleDist of every valid row, top-(k+1) by
+// = row); EB: the distances come from k_exact_bm (ebuf).  Reference-order SingleDist of every valid row, top-(k+1) by
 // (distance, id) per wave, merged by wave 0; proof = the first min(k+1, n)
 // are strictly increasing (the reference heap then holds exactly the k
 // smallest and extractHeap returns them ascending).
-template <int R, int METRIC, int VARIANT>
+template <int R, int METRIC, int VARIANT, bool EB>
 __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
                                                    int64_t nrows, const float* __restrict__ Qn, int d,
                                                    const uint32_t* __restrict__ cand, const int32_t* __restrict__ ncand,
@@ -1094,7 +1101,7 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
             ok = row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
         }
         float e = __builtin_inff();
-        if (ebuf) {
+        if (EB) {  // its own instantiation: the distance code's registers stay out of the read-back form
             if (ok) e = ebuf[(int64_t)q * ldE + j * 32 + li];
         } else if (coop) {  // 8 lanes per row, rows 8g + (lane >> 3) of the pass
             const float* xp[8];
@@ -1395,7 +1402,7 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
                 bool need = ok;
                 if (ok && len >= k) {
                     float s0 = 0.f, s1 = 0.f;
-#pragma unroll 4
+#pragma unroll 8
                     for (int c = 0; c < dpb; c += 16) {
                         const uint4* xp = reinterpret_cast<const uint4*>(Xb + bf3_plane_index(row, c, dpb));
                         const uint4 v0 = xp[0], v1 = xp[1];
