@@ -432,6 +432,27 @@ def test_one_wave_replay_float_data(wv, oracle, metric, variant, d, k):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} d{d} q{qi}")
 
 
+@pytest.mark.parametrize("metric,variant,d,k", [("cosine", "avx256", 768, 10), ("l2-squared", "avx256", 130, 24),
+                                               ("dot", "avx512", 96, 10), ("cosine", "avx512", 200, 100)])
+def test_exact_row_filter_equals_unfiltered(wv, oracle, metric, variant, d, k):
+    """exact_filter 1 (k_blk_exact skips rows whose bf16-plane bound reaches
+    the cap) returns what exact_filter 0 (every candidate row exact) and the
+    oracle return, bit for bit."""
+    n = 30000
+    data = gen(oracle, 0, 99, n, d)
+    queries = gen(oracle, 0, 100, 200, d)
+    res = []
+    for filt in (0, 1):
+        idx, orc = build_pair(wv, oracle, metric, variant, data)
+        idx.set_option("exact_filter", filt)
+        res.append(idx.search_by_vector_batch(queries, k))
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    for qi in range(0, len(queries), 20):
+        ids, dists, counts = res[1]
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")
+
+
 @pytest.mark.parametrize("metric,kind,variant,n,d,k", [("l2-squared", 1, "avx256", 40000, 128, 100),   # C2-like ties
                                                       ("cosine", 0, "avx512", 30000, 200, 10),
                                                       ("dot", 0, "avx256", 20000, 500, 24),

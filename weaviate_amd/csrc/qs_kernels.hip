@@ -876,17 +876,11 @@ struct WaveTopL {
         thr = cap = cap_;
         cnt = 0;
     }
-    // rows 0..R-2 are sorted: sort the pending row alone, reverse it (the R
-    // rows then form one bitonic sequence) and run only the final merge stage
-    // of the 64R-element network (the same sorted result as a full sort)
+    // rows 0..R-2 are sorted: only the pending row is sorted, then merged
     __device__ __forceinline__ void merge(const float* bk, const uint32_t* bi, int lane) {
-        float pk[1] = {lane < cnt ? bk[lane] : __builtin_inff()};
-        uint32_t pi[1] = {lane < cnt ? bi[lane] : NO_ID};
-        bitonic_sort<1>(pk, pi, lane);
-        key[R - 1] = __shfl(pk[0], 63 - lane);
-        id[R - 1] = (uint32_t)__shfl((int)pi[0], 63 - lane);
-#pragma unroll
-        for (int j = 32 * R; j > 0; j >>= 1) cmpx_step<R>(key, id, 64 * R, j, lane);
+        key[R - 1] = lane < cnt ? bk[lane] : __builtin_inff();
+        id[R - 1] = lane < cnt ? bi[lane] : NO_ID;
+        bitonic_merge_last<R>(key, id, lane);
         thr = fminf(__shfl(key[R - 2], 63), cap);
         cnt = 0;
     }
@@ -1054,6 +1048,73 @@ __global__ __launch_bounds__(256) void k_blk_gthresh(const float* __restrict__ t
     if (lane == 0) ncand[q] = keep;
 }
 
+// ---------------------------------------------------------------------------
+// row filter helpers (k_blk_exact, k_blk_replay)
+// ---------------------------------------------------------------------------
+constexpr int QS_FILT_DPB = 1536;  // the widest block-key plane (k_qs_blockkey_w4)
+
+// S = sum_c bf16(q)_c * x_h,c of one stored row from the tiled bf16 plane
+// (lane per row: the plane interleaves 256 rows per 16-column chunk, so the
+// lanes' 32-byte reads are contiguous).  Two alternating fp32 accumulators:
+// the error is within gamma_{dpb+2} sum|terms| (gacc_r of the callers).
+__device__ __forceinline__ float plane_dot(const uint16_t* __restrict__ Xb, int64_t row, int dpb, const float* sqh) {
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll 8
+    for (int c = 0; c < dpb; c += 16) {
+        const uint4* xp = reinterpret_cast<const uint4*>(Xb + bf3_plane_index(row, c, dpb));
+        const uint4 v0 = xp[0], v1 = xp[1];
+        const float4* qp = reinterpret_cast<const float4*>(sqh + c);
+        const float4 a0 = qp[0], a1 = qp[1], a2 = qp[2], a3 = qp[3];
+        s0 = fmaf(__uint_as_float(v0.x << 16), a0.x, s0); s1 = fmaf(__uint_as_float(v0.x & 0xFFFF0000u), a0.y, s1);
+        s0 = fmaf(__uint_as_float(v0.y << 16), a0.z, s0); s1 = fmaf(__uint_as_float(v0.y & 0xFFFF0000u), a0.w, s1);
+        s0 = fmaf(__uint_as_float(v0.z << 16), a1.x, s0); s1 = fmaf(__uint_as_float(v0.z & 0xFFFF0000u), a1.y, s1);
+        s0 = fmaf(__uint_as_float(v0.w << 16), a1.z, s0); s1 = fmaf(__uint_as_float(v0.w & 0xFFFF0000u), a1.w, s1);
+        s0 = fmaf(__uint_as_float(v1.x << 16), a2.x, s0); s1 = fmaf(__uint_as_float(v1.x & 0xFFFF0000u), a2.y, s1);
+        s0 = fmaf(__uint_as_float(v1.y << 16), a2.z, s0); s1 = fmaf(__uint_as_float(v1.y & 0xFFFF0000u), a2.w, s1);
+        s0 = fmaf(__uint_as_float(v1.z << 16), a3.x, s0); s1 = fmaf(__uint_as_float(v1.z & 0xFFFF0000u), a3.y, s1);
+        s0 = fmaf(__uint_as_float(v1.w << 16), a3.z, s0); s1 = fmaf(__uint_as_float(v1.w & 0xFFFF0000u), a3.w, s1);
+    }
+    return s0 + s1;
+}
+
+// A_row of one stored row: the block key's formula with plane_dot's S
+template <int METRIC>
+__device__ __forceinline__ float plane_a(const uint16_t* __restrict__ Xb, const float* __restrict__ xn2, int64_t row,
+                                         int dpb, const float* sqh, float qn2) {
+    const float S = plane_dot(Xb, row, dpb, sqh);
+    const float kv = METRIC == L2 ? fmaf(-2.f, S, xn2[row]) : -S;
+    return qs_key_to_a(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, kv, qn2);
+}
+
+// Reference-order distances of the rows of the lanes with `need` (row = the
+// lane's stored row), 8 lanes per row (exact_dist8) in passes of 8 rows;
+// slot[0..63] is this wave's LDS scratch.  Every lane of the wave must call.
+template <int METRIC>
+__device__ __forceinline__ float exact8_compact(const float* __restrict__ qv, const float* __restrict__ X, int dpad,
+                                                int d, int64_t row, bool need, int lane, float* slot) {
+    const uint64_t nm = __ballot(need);
+    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0));
+    const int cnt = __popcll(nm);
+    float dist = 0.f;
+    if (cnt == 0) return dist;
+    if (need) slot[rank] = __int_as_float((int)row);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int p0 = 0; p0 < cnt; p0 += 8) {
+        const int gsel = p0 + (lane >> 3);
+        const int64_t rw = (int64_t)__float_as_int(slot[gsel < cnt ? gsel : 0]);  // spare groups repeat the list's first row
+        const float* xp1[1] = {X + rw * dpad};
+        float dv[1];
+        exact_dist8<METRIC, 1>(qv, xp1, d, lane & 7, dv);
+        const float dg = __shfl(dv[0], ((rank - p0) & 7) * 8);
+        if (need && rank >= p0 && rank < p0 + 8) dist = dg;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    return dist;
+}
+
 // k_blk_exact<R, METRIC, VARIANT, EB>: one workgroup (4 waves) per query over its
 // candidate blocks (each wave two blocks per pass: lanes 0-31 and 32-63, lane
 // = row); EB: the distances come from k_exact_bm (ebuf).  Reference-order SingleDist of every valid row, top-(k+1) by
@@ -1068,11 +1129,16 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
                                                    float* __restrict__ out_d, int32_t* __restrict__ out_n,
                                                    int32_t* __restrict__ flags, const int32_t* __restrict__ qlist,
                                                    const uint32_t* __restrict__ qcount,
-                                                   const float* __restrict__ ebuf = nullptr, int64_t ldE = 0,
-                                                   const float* __restrict__ cap = nullptr) {
+                                                   const float* __restrict__ ebuf, int64_t ldE,
+                                                   const float* __restrict__ cap, const float4* __restrict__ qinfo,
+                                                   const uint16_t* __restrict__ Xb, int dpb, const float* __restrict__ xn2,
+                                                   const uint32_t* __restrict__ qsmax, const uint32_t* __restrict__ maxn2,
+                                                   float gd, float gacc_r) {
     constexpr int L = 64 * (R - 1);
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
+    __shared__ float sslot[4][64];
+    __shared__ __attribute__((aligned(16))) float sqh[EB ? 4 : QS_FILT_DPB];
     __shared__ float lk[3][L];
     __shared__ uint32_t lid[3][L];
     __shared__ int snv[4];
@@ -1089,6 +1155,18 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     const float* qv = Qn + (int64_t)q * dpad;
     const int li = lane & 31, lh = lane >> 5;
     const bool coop = exact8_ok<METRIC, VARIANT>(d);
+    // row filter (capped exact pass, finite query): a row whose plane bound
+    // A_row - eps_r reaches the cap has an exact distance >= cap, which the
+    // list never keeps; only the others get the reference-order distance
+    const float4 qi = qinfo[q];
+    const bool filt = !EB && Xb != nullptr && cap != nullptr && qi.w == 0.f && dpb <= QS_FILT_DPB;
+    float eps_r = 0.f, capq = __builtin_inff();
+    if (filt) {
+        for (int c = threadIdx.x; c < dpb; c += 256) sqh[c] = (float)(__bf16)(c < d ? qv[c] : 0.f);
+        eps_r = qs_eps(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, qi, qsmax, maxn2, gd, gacc_r);
+        capq = cap[q];
+        __syncthreads();
+    }
     WaveTopL<R> t;
     t.init(cap ? cap[q] : __builtin_inff());  // only the k+1 smallest are used: nothing above cap
     int nvalid = 0;
@@ -1103,6 +1181,11 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         float e = __builtin_inff();
         if (EB) {  // its own instantiation: the distance code's registers stay out of the read-back form
             if (ok) e = ebuf[(int64_t)q * ldE + j * 32 + li];
+        } else if (filt) {
+            const bool need = ok && plane_a<METRIC>(Xb, xn2, row, dpb, sqh, qi.x) - eps_r < capq;
+            const float dl = coop ? exact8_compact<METRIC>(qv, X, dpad, d, row, need, lane, sslot[w])
+                                  : need ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
+            if (need) e = dl;
         } else if (coop) {  // 8 lanes per row, rows 8g + (lane >> 3) of the pass
             const float* xp[8];
 #pragma unroll
@@ -1400,46 +1483,9 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
             bool cand = ok;  // an exact distance was computed for this lane's row
             if (filt) {
                 bool need = ok;
-                if (ok && len >= k) {
-                    float s0 = 0.f, s1 = 0.f;
-#pragma unroll 8
-                    for (int c = 0; c < dpb; c += 16) {
-                        const uint4* xp = reinterpret_cast<const uint4*>(Xb + bf3_plane_index(row, c, dpb));
-                        const uint4 v0 = xp[0], v1 = xp[1];
-                        const float4* qp = reinterpret_cast<const float4*>(sqh + c);
-                        const float4 a0 = qp[0], a1 = qp[1], a2 = qp[2], a3 = qp[3];
-                        s0 = fmaf(__uint_as_float(v0.x << 16), a0.x, s0); s1 = fmaf(__uint_as_float(v0.x & 0xFFFF0000u), a0.y, s1);
-                        s0 = fmaf(__uint_as_float(v0.y << 16), a0.z, s0); s1 = fmaf(__uint_as_float(v0.y & 0xFFFF0000u), a0.w, s1);
-                        s0 = fmaf(__uint_as_float(v0.z << 16), a1.x, s0); s1 = fmaf(__uint_as_float(v0.z & 0xFFFF0000u), a1.y, s1);
-                        s0 = fmaf(__uint_as_float(v0.w << 16), a1.z, s0); s1 = fmaf(__uint_as_float(v0.w & 0xFFFF0000u), a1.w, s1);
-                        s0 = fmaf(__uint_as_float(v1.x << 16), a2.x, s0); s1 = fmaf(__uint_as_float(v1.x & 0xFFFF0000u), a2.y, s1);
-                        s0 = fmaf(__uint_as_float(v1.y << 16), a2.z, s0); s1 = fmaf(__uint_as_float(v1.y & 0xFFFF0000u), a2.w, s1);
-                        s0 = fmaf(__uint_as_float(v1.z << 16), a3.x, s0); s1 = fmaf(__uint_as_float(v1.z & 0xFFFF0000u), a3.y, s1);
-                        s0 = fmaf(__uint_as_float(v1.w << 16), a3.z, s0); s1 = fmaf(__uint_as_float(v1.w & 0xFFFF0000u), a3.w, s1);
-                    }
-                    const float S = s0 + s1;
-                    const float kv = METRIC == L2 ? fmaf(-2.f, S, xn2[row]) : -S;
-                    need = top > qs_key_to_a(metric, kv, qi.x) - eps_r;
-                }
-                if (coop) {  // the few rows that need it, 8 lanes per row (exact_dist8)
-                    const uint64_t nm = __ballot(need);
-                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0));
-                    const int cnt = __popcll(nm);
-                    if (need) s_d[rank] = __int_as_float((int)row);
-                    __syncthreads();
-                    for (int p0 = 0; p0 < cnt; p0 += 8) {
-                        const int gsel = p0 + (lane >> 3);
-                        const int64_t rw = (int64_t)__float_as_int(s_d[gsel < cnt ? gsel : 0]);  // spare groups repeat row 0 of the list
-                        const float* xp1[1] = {X + rw * dpad};
-                        float dv[1];
-                        exact_dist8<METRIC, 1>(qv, xp1, d, lane & 7, dv);
-                        const float dg = __shfl(dv[0], ((rank - p0) & 7) * 8);
-                        if (need && rank >= p0 && rank < p0 + 8) dist = dg;
-                    }
-                    __syncthreads();
-                } else if (need) {
-                    dist = exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d);
-                }
+                if (ok && len >= k) need = top > plane_a<METRIC>(Xb, xn2, row, dpb, sqh, qi.x) - eps_r;
+                if (coop) dist = exact8_compact<METRIC>(qv, X, dpad, d, row, need, lane, s_d);
+                else if (need) dist = exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d);
                 cand = need;
             } else if (coop) {  // 8 lanes per row, rows 8g + (lane >> 3) of the pair
                 const float* xp[8];
@@ -1796,7 +1842,7 @@ __device__ __forceinline__ float rp_offer(float (&sk)[RS], uint32_t (&sid)[RS], 
     if (!__any(v < thr)) return thr;
     sk[RS - 1] = v;
     sid[RS - 1] = 0;
-    bitonic_sort<RS>(sk, sid, lane);
+    bitonic_merge_last<RS>(sk, sid, lane);
     return rp_key_at<RS>(sk, k - 1);
 }
 

@@ -162,7 +162,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         const float* capv = (idx->exact_cap && phase == 0) ? idx->qsCap.as<float>() : nullptr;
         auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0) {
             launch_blk_exact(idx, s, RV, metric, v5, Qn, valid, (int)cn, k, kout, o_ids + c0 * kout, o_d + c0 * kout,
-                             o_n + c0, flags, list, cnt, eb, ldE, capv);
+                             o_n + c0, flags, list, cnt, eb, ldE, capv, qinfo);
         };
         if (phase != 2) sel(R, nullptr, nullptr, phase == 1 ? topA : nullptr);
         HIPCHK(hipGetLastError());

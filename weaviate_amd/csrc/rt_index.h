@@ -124,6 +124,7 @@ struct wv_index {
     // bf16 hi plane of X for the block-key path (qs_kernels.hip): [cap][dpb],
     // dpb = dims rounded up to 128, built when dpb <= QS_MAX_DPB
     int use_qs = 0, qs_planes = 0, dpb = 0;
+    int exact_filter = 0;           // k_blk_exact's bf16-plane row filter (option exact_filter)
     uint16_t* Xb = nullptr;
     uint32_t* qsmax = nullptr;      // device [4]: max |x - x_h|^2, max |x_h|^2 (float bits), non-finite flag
     uint32_t* qscount = nullptr;    // device [4]: [0] replayed queries (cumulative), [1] this batch's flagged,
@@ -232,7 +233,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
 void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
                       const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
                       int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
-                      const float* capv);
+                      const float* capv, const float4* qinfo);
 void launch_exact_bm(wv_index* idx, hipStream_t s, int metric, bool v5, const float* Qn, int64_t nb, size_t bm_lds,
                      int64_t ldE);
 // qs_replay.hip

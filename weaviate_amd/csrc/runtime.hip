@@ -607,6 +607,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "qs_force_flag") idx->qs_force_flag = value ? 1 : 0;
     else if (k == "exact_bm") idx->exact_bm = value ? 1 : 0;
     else if (k == "exact_cap") idx->exact_cap = value ? 1 : 0;
+    else if (k == "exact_filter") idx->exact_filter = value ? 1 : 0;  // 0: every candidate row gets its exact distance
     else if (k == "ef") idx->hnsw_ef = (int)value;  // hnsw UserConfig.EF (-1: dynamic)
     else if (k == "ef_min") idx->ef_min = (int)value;
     else if (k == "ef_max") idx->ef_max = (int)value;

@@ -328,6 +328,20 @@ __device__ __forceinline__ void bitonic_sort(float (&key)[R], uint32_t (&id)[R],
         for (int j = k >> 1; j > 0; j >>= 1) cmpx_step<R>(key, id, k, j, lane);
 }
 
+// Rows 0..R-2 already sorted, row R-1 arbitrary: sort row R-1 alone, reverse
+// it (the R rows then form one bitonic sequence) and run only the final merge
+// stage of the 64R network -- the same sorted list as bitonic_sort<R>.
+template <int R>
+__device__ __forceinline__ void bitonic_merge_last(float (&key)[R], uint32_t (&id)[R], int lane) {
+    float pk[1] = {key[R - 1]};
+    uint32_t pi[1] = {id[R - 1]};
+    bitonic_sort<1>(pk, pi, lane);
+    key[R - 1] = __shfl(pk[0], 63 - lane);
+    id[R - 1] = (uint32_t)__shfl((int)pi[0], 63 - lane);
+#pragma unroll
+    for (int j = 32 * R; j > 0; j >>= 1) cmpx_step<R>(key, id, 64 * R, j, lane);
+}
+
 // ---------------------------------------------------------------------------
 // synthetic data generator (identical to oracle/oracle.c or_gen_value)
 // ---------------------------------------------------------------------------
