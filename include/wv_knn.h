@@ -450,7 +450,7 @@ int wv_index_debug_blockkeys(wv_index *idx, int64_t q, float *A, float *eps, int
  * 6 = HBM-streaming GEMV, 3 = f32 MFMA select; other values are rejected),
  * "replay_par" (flagged-query replay form, default 2), "exact_bm" / "exact_cap"
  * / "exact_filter" (block-key exact pass forms; exact_filter 1 = bf16-plane row
- * bound in the capped pass, default 0), "replay_dbg" (1 = clock diagnostics of
+ * bound in the capped pass, default), "replay_dbg" (1 = clock diagnostics of
  * the one-wave replay, printed), "pq_cand" (1 = minima-only PQ search, 0 = the
  * full ADC matrix), "pq_adc3" (1 = queries-on-lanes ADC for 256 centroids,
  * 0 = k_pq_adc2), "bq_kernel" (1 = generic BQ kernels), "timing" (1 = record

@@ -124,7 +124,7 @@ struct wv_index {
     // bf16 hi plane of X for the block-key path (qs_kernels.hip): [cap][dpb],
     // dpb = dims rounded up to 128, built when dpb <= QS_MAX_DPB
     int use_qs = 0, qs_planes = 0, dpb = 0;
-    int exact_filter = 0;           // k_blk_exact's bf16-plane row filter (option exact_filter)
+    int exact_filter = 1;           // k_blk_exact's bf16-plane row filter (option exact_filter)
     uint16_t* Xb = nullptr;
     uint32_t* qsmax = nullptr;      // device [4]: max |x - x_h|^2, max |x_h|^2 (float bits), non-finite flag
     uint32_t* qscount = nullptr;    // device [4]: [0] replayed queries (cumulative), [1] this batch's flagged,
