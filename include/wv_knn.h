@@ -428,7 +428,15 @@ typedef struct wv_stats {
     double last_select_ms;   /* k_mfma_select time of the last batch (HIP events) */
     double last_total_ms;
     uint64_t last_group_queries; /* queries in the timed (first) group of the last quantized batch */
+    uint64_t last_route;     /* exact fp32 search route of the last batch: WV_ROUTE_* */
 } wv_stats;
+/* wv_stats.last_route: which key / select kernel the last exact batch ran */
+#define WV_ROUTE_NONE 0
+#define WV_ROUTE_QS_BF16 1   /* k_qs_blockkey (bf16 block keys, d <= 768) */
+#define WV_ROUTE_QS_W4 2     /* k_qs_blockkey_w4 (bf16 block keys, 768 < d <= 1536) */
+#define WV_ROUTE_QS_INT8 3   /* k_q8_blockkey (int8 block keys, 384 < d <= 1536) */
+#define WV_ROUTE_F32_SELECT 4 /* k_mfma_select3 (f32 MFMA select) */
+#define WV_ROUTE_GEMV 5      /* k_gemv_select (HBM-streaming GEMV, small batches) */
 int wv_index_stats(wv_index *idx, wv_stats *out);
 
 /* Diagnostic hook (tests): the last MFMA batch's candidates [nq][KP]:

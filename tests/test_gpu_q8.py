@@ -1,0 +1,119 @@
+"""GPU parity of the int8 block-key pass (q8_kernels.hip):
+k_q8_blockkey feeds the block-key selection / exact pass / replay for
+384 < d <= 1536.  Every query bit-exact against the oracle, the same results
+as the bf16 keys (option q8 = 0), and the int8 block keys within the proof's
+eps of the exact block minima."""
+import numpy as np
+import pytest
+
+from test_gpu_flat import VARIANTS, assert_same, build_pair, gen
+
+pytestmark = pytest.mark.gpu
+
+ROUTE_INT8, ROUTE_BF16, ROUTE_W4 = 3, 1, 2
+
+
+def check_block_keys(idx, oracle, kind, seed, n, d, metric, variant, queries, sample, data=None):
+    qs = queries[sample]
+    if metric == "cosine":
+        qs = np.stack([oracle.normalize(x) for x in qs])
+    if data is None:
+        D = oracle.gen_dists(kind, seed, n, d, oracle.METRIC[metric], VARIANTS[variant], qs, 8)
+    else:
+        D = np.stack([[oracle.single_dist(oracle.METRIC[metric], VARIANTS[variant], q, x) for x in data] for q in qs])
+    worst = 0.0
+    for i, q in enumerate(sample):
+        A, eps = idx.debug_blockkeys(int(q))
+        nb = (n // 32) * 32
+        bmin = D[i][:nb].reshape(-1, 32).min(axis=1).astype(np.float64)
+        err = np.abs(A[: bmin.size].astype(np.float64) - bmin)
+        worst = max(worst, float(err.max() / eps))
+        assert (err <= eps).all(), f"q{q}: int8 block-key error {err.max()} > eps {eps}"
+    return worst
+
+
+@pytest.mark.parametrize("metric,kind,variant,n,d,k", [
+    ("cosine", 0, "avx256", 30000, 768, 10),     # C3 shape: two blocks per ring slot
+    ("l2-squared", 0, "avx256", 20000, 768, 10),
+    ("dot", 0, "avx512", 20000, 640, 24),
+    ("cosine", 0, "avx256", 20000, 400, 10),     # dpb8 512: zero-padded columns
+    ("l2-squared", 1, "avx256", 20000, 512, 100),  # integer data: exact codes, ties -> replay
+    ("cosine", 0, "avx512", 16000, 1024, 10),    # one block per slot
+    ("l2-squared", 2, "avx256", 12000, 1100, 10),  # dpb8 1280
+    ("dot", 0, "avx256", 12000, 1536, 100),
+])
+def test_q8_keys_match_oracle_and_bf16(wv, oracle, metric, kind, variant, n, d, k):
+    data = gen(oracle, kind, 71, n, d)
+    queries = gen(oracle, kind, 72, 300, d)
+    idx, orc = build_pair(wv, oracle, metric, variant, data)
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] == ROUTE_INT8
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"q{qi}")
+    worst = check_block_keys(idx, oracle, kind, 71, n, d, metric, variant, queries, [0, 131, 299])
+    print(f"{metric} d={d}: int8 max |A_block - min E| / eps = {worst:.4f}")
+    idx.set_option("q8", 0)
+    ids2, dists2, counts2 = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] in (ROUTE_BF16, ROUTE_W4)
+    np.testing.assert_array_equal(counts, counts2)
+    np.testing.assert_array_equal(ids, ids2)
+    np.testing.assert_array_equal(dists.view(np.uint32), dists2.view(np.uint32))
+    idx.close()
+
+
+def test_q8_upsert_delete_allow_requantises_blocks(wv, oracle):
+    """Rows written into existing blocks (upserts with a 50x larger norm,
+    sparse ids) re-quantise the whole block (its scale grows); whole deleted
+    blocks key +inf; allow lists; every query equals the oracle."""
+    n, d, k = 9000, 768, 10
+    rng = np.random.default_rng(5)
+    data = gen(oracle, 0, 73, n, d)
+    ids = np.arange(n, dtype=np.uint64) * 3  # sparse: blocks hold every third id
+    idx = wv.FlatIndex(distance="l2-squared", variant="avx256")
+    idx.add_batch(ids, data)
+    orc = oracle.OracleFlat(oracle.METRIC["l2-squared"], VARIANTS["avx256"], d, int(ids.max()) + 1 + 3000)
+    orc.add_batch(ids, data)
+    up = rng.choice(n, 200, replace=False)
+    newv = (gen(oracle, 0, 74, 200, d) * np.float32(50.0)).astype(np.float32)
+    idx.add_batch(ids[up], newv)
+    orc.add_batch(ids[up], newv)
+    extra = np.arange(int(ids.max()) + 1, int(ids.max()) + 1 + 3000, dtype=np.uint64)[::7]
+    ev = gen(oracle, 0, 75, len(extra), d)
+    idx.add_batch(extra, ev)
+    orc.add_batch(extra, ev)
+    dele = ids[(ids >= 3 * 32 * 10) & (ids < 3 * 32 * 14)]  # whole 32-slot blocks
+    idx.delete(*[int(x) for x in dele])
+    orc.delete([int(x) for x in dele])
+    queries = gen(oracle, 0, 76, 120, d)
+    queries[:40] = data[up[:40]] * np.float32(50.0)  # near the upserted rows
+    got = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] == ROUTE_INT8
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], k), got[0][qi, :got[2][qi]], got[1][qi, :got[2][qi]], ctx=f"q{qi}")
+    allow = wv.AllowList(int(x) for x in ids[::5])
+    got = idx.search_by_vector_batch(queries, k, allow=allow)
+    for qi in range(0, len(queries), 7):
+        assert_same(orc.search(queries[qi], k, allow=set(int(x) for x in ids[::5])), got[0][qi, :got[2][qi]],
+                    got[1][qi, :got[2][qi]], ctx=f"allow q{qi}")
+    idx.close()
+
+
+@pytest.mark.parametrize("metric", ["cosine", "l2-squared"])
+def test_q8_heavy_tailed_rows_and_forced_replay(wv, oracle, metric):
+    """A few huge coordinates per row (int8 scales dominated by outliers: wide
+    bound, many candidate blocks, overflow into the second selection pass) and
+    every query forced through the keyed replay: still bit-exact."""
+    n, d, k = 20000, 512, 10
+    rng = np.random.default_rng(6)
+    data = gen(oracle, 0, 77, n, d)
+    spikes = rng.integers(0, d, size=(n, 2))
+    data[np.arange(n)[:, None], spikes] *= np.float32(40.0)
+    queries = gen(oracle, 0, 78, 64, d)
+    for force in (0, 1):
+        idx, orc = build_pair(wv, oracle, metric, "avx256", data)
+        idx.set_option("qs_force_flag", force)
+        ids, dists, counts = idx.search_by_vector_batch(queries, k)
+        assert idx.stats()["last_route"] == ROUTE_INT8
+        for qi in range(len(queries)):
+            assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"f{force} q{qi}")
+        idx.close()

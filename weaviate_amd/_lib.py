@@ -62,7 +62,12 @@ class WvStats(C.Structure):
         ("last_select_ms", C.c_double),
         ("last_total_ms", C.c_double),
         ("last_group_queries", C.c_uint64),
+        ("last_route", C.c_uint64),
     ]
+
+
+# wv_stats.last_route (include/wv_knn.h WV_ROUTE_*)
+ROUTES = {0: "none", 1: "qs_bf16", 2: "qs_w4", 3: "qs_int8", 4: "f32_select", 5: "gemv"}
 
 
 P = C.c_void_p

@@ -1,0 +1,461 @@
+// q8_kernels.hip -- int8 block keys for the exact fp32 flat search (DESIGN.md
+// §3.1f).  The same pipeline as the bf16 block-key path (qs_kernels.hip:
+// block keys -> k_blk_select -> k_blk_exact -> bounded replay), with the key
+// pass on v_mfma_i32_16x16x64_i8: twice the bf16 MFMA rate per clock, and the
+// integer products are exact, so the only approximation is the quantisation
+// itself, bounded per row at Add time.
+//
+//   corpus   x^ = sb * X8, X8 in [-127, 127], one scale sb per 32-row block
+//            (max |x| of the block / 127): the key epilogue stays one multiply
+//            per (query, block) for dot / cosine.  k_block_q8 rebuilds a whole
+//            block whenever one of its rows is written.
+//   queries  q^ = sq * Q8, one scale per query (k_query_q8).
+//   S        = fl(fl(sq * sb) * float(sum Q8 * X8)), the int32 sum exact.
+//   |q.x - S| <= |q^| R + |q - q^| H + |q - q^| R + 4u |q^| H
+//            (R = max |x - x^|, H = max |x^| over stored rows; the last term
+//            the three roundings of S), i.e. qs_eps with gacc = 4u: the
+//            selection, exact pass and replay of qs_kernels.hip apply as they
+//            are.
+//
+// Plane layout: the bf16 plane's tiling with two int8 columns per bf16
+// element (256-row tiles x 32-byte column chunks, q8_plane_byte), so the
+// LDS-DMA pieces, ring slots and fragment addresses of k_qs_blockkey's
+// one-block schedule carry over: a 64-column i8 MFMA chunk is a 32-column
+// bf16 chunk's bytes.
+#pragma once
+
+namespace wv {
+namespace {
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+constexpr int Q8_NONE = (int)0x80000000;  // "no valid row" in the integer max
+
+// byte offset of int8 column c of row `row` in a tiled int8 plane of dpb8 columns
+__host__ __device__ __forceinline__ int64_t q8_plane_byte(int64_t row, int c, int dpb8) {
+    return ((row >> 8) * (int64_t)(dpb8 >> 5) + (c >> 5)) * 8192 + ((row & 255) << 5) + (c & 31);
+}
+
+template <int OFF>
+__device__ __forceinline__ i32x4_t lds_ld16_o(unsigned base) {
+    i32x4_t v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(OFF));
+    return v;
+}
+
+// n copies of a 32-bit word (e.g. +inf block minima of an empty shard)
+__global__ void k_fill_u32(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+__device__ __forceinline__ int q8_code(float x, float inv) {
+    const float c = rintf(x * inv);
+    return (int)fminf(127.f, fmaxf(-127.f, c));
+}
+
+// ---------------------------------------------------------------------------
+// k_block_q8: one workgroup (4 waves) per 32-row block: sb = max |x| / 127 over
+// the block's 32 stored rows (present or not: a stale or zero row only costs
+// precision), X8 = rint(x / sb) clamped to +-127, and per row
+// |x - sb X8|^2, |sb X8|^2 into the index maxima qmax8[0], qmax8[1]
+// (atomicMax on float bits).  Blocks blist[i] or b0 + i.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_block_q8(const float* __restrict__ X, int dpad, int dims, int dpb8,
+                                                  const uint32_t* __restrict__ blist, int64_t b0,
+                                                  unsigned char* __restrict__ X8, float* __restrict__ sb8,
+                                                  uint32_t* __restrict__ qmax8) {
+    __shared__ float smax[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t blk = blist ? (int64_t)blist[blockIdx.x] : b0 + blockIdx.x;
+    const int64_t r0 = blk * 32;
+    float m = 0.f;
+    for (int r = 8 * w; r < 8 * w + 8; r++) {
+        const float* x = X + (r0 + r) * dpad;
+        for (int c = lane; c < dims; c += 64) m = fmaxf(m, fabsf(x[c]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) smax[w] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    const float sb = m / 127.f;
+    const float inv = m > 0.f ? 127.f / m : 0.f;
+    if (threadIdx.x == 0) sb8[blk] = sb;
+    for (int r = 8 * w; r < 8 * w + 8; r++) {
+        const int64_t row = r0 + r;
+        const float* x = X + row * dpad;
+        float sr = 0.f, sh = 0.f;
+        for (int c4 = 4 * lane; c4 < dpb8; c4 += 256) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int c = c4 + e;
+                const float v = c < dims ? x[c] : 0.f;
+                const int q = q8_code(v, inv);
+                const float h = sb * (float)q;       // x^ component (one rounding)
+                const float rv = fmaf(-sb, (float)q, v);  // x - x^ (one rounding)
+                sr = fmaf(rv, rv, sr);
+                sh = fmaf(h, h, sh);
+                word |= (uint32_t)(q & 0xFF) << (8 * e);
+            }
+            *reinterpret_cast<uint32_t*>(X8 + q8_plane_byte(row, c4, dpb8)) = word;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            sr += __shfl_xor(sr, o);
+            sh += __shfl_xor(sh, o);
+        }
+        if (lane == 0) {
+            atomicMax(&qmax8[0], __float_as_uint(sr));
+            atomicMax(&qmax8[1], __float_as_uint(sh));
+        }
+    }
+}
+
+// k_query_q8: wave per query row of Qn (rows [nq, nq_pad) are zero): sq =
+// max |q| / 127, Q8 into the tiled query plane, qscale[q] = sq, and
+// qinfo8[q] = (|q|^2, |q^|^2, |q - q^|^2, non-finite ? 1 : 0), |q|^2 and the
+// non-finite flag taken from k_query_split's qinfo16 (one |q|^2 per query on
+// every path).
+__global__ void k_query_q8(const float* __restrict__ Qn, int dpad, int dims, int dpb8, int64_t nq, int64_t nq_pad,
+                           const float4* __restrict__ qinfo16, unsigned char* __restrict__ Q8,
+                           float* __restrict__ qscale, float4* __restrict__ qinfo8) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (q >= nq_pad) return;
+    const float* x = Qn + q * dpad;
+    float m = 0.f;
+    bool bad = false;
+    if (q < nq)
+        for (int c = lane; c < dims; c += 64) {
+            const float v = x[c];
+            m = fmaxf(m, fabsf(v));
+            bad |= !__builtin_isfinite(v);
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    bad = __any(bad);
+    const float sq = m / 127.f;
+    const float inv = m > 0.f ? 127.f / m : 0.f;
+    float sh = 0.f, sr = 0.f;
+    for (int c4 = 4 * lane; c4 < dpb8; c4 += 256) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int c = c4 + e;
+            const float v = (q < nq && c < dims) ? x[c] : 0.f;
+            const int cq = bad ? 0 : q8_code(v, inv);
+            const float h = sq * (float)cq;
+            const float rv = fmaf(-sq, (float)cq, v);
+            sh = fmaf(h, h, sh);
+            sr = fmaf(rv, rv, sr);
+            word |= (uint32_t)(cq & 0xFF) << (8 * e);
+        }
+        *reinterpret_cast<uint32_t*>(Q8 + q8_plane_byte(q, c4, dpb8)) = word;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sh += __shfl_xor(sh, o);
+        sr += __shfl_xor(sr, o);
+    }
+    if (lane == 0) {
+        const float4 q16 = qinfo16[q];
+        qscale[q] = sq;
+        qinfo8[q] = make_float4(q16.x, sh, sr, (bad || q16.w != 0.f || !(sh < 1e30f)) ? 1.f : 0.f);
+    }
+}
+
+struct Q8Args {
+    const unsigned char* X8;   // corpus int8 plane, tiled (q8_plane_byte, dpb8 columns)
+    const float* sb;           // [cap/32] block scales
+    const float* xnorm2;       // [cap] |x|^2 of the stored fp32 rows (L2)
+    const uint32_t* valid;     // [cap/32] slots to scan (present & allowed)
+    const unsigned char* Q8;   // query int8 plane, tiled, nq_pad rows (multiple of 256)
+    const float* qscale;       // [nq_pad]
+    float* key;                // [nq_pad][ldk] block keys
+    int64_t ldk;
+    int64_t nslots;            // ring steps (RB 32-row blocks each) to scan
+    int slots_per_span;
+    int nspans;
+    int nqg;                   // query groups of 256
+};
+
+// ---------------------------------------------------------------------------
+// k_q8_blockkey<NC, RB, L2>: block keys of 256 queries (8 waves x 32) x one
+// span of the corpus, NC 64-column chunks per 32-row block, RB blocks per LDS
+// ring slot (3 slots, RB * 2NC KiB each, LDS-DMA filled two steps ahead).
+//   key (L2)      = min over the block's valid rows of fl(xnorm2 - 2 S)
+//   key (dot/cos) = -max over the block's valid rows of S
+// S = fl(fl(sq * sb) * float(sum_k Q8 X8)); a block with no valid row: +inf.
+// Per chunk: 2 A-fragment reads (row halves), 4 v_mfma_i32_16x16x64_i8 (2 row
+// halves x 2 query halves), one DMA piece of the group two steps ahead.  The
+// reduction over a block's rows runs beside the next block's MFMAs (RB = 2)
+// or after the slot; the cross-lane combine + key store of a slot's last
+// block is deferred into the next slot.  One barrier per slot.
+// ---------------------------------------------------------------------------
+template <int NC, int RB, bool ISL2>
+__global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
+    constexpr int NPB = 2 * NC;                     // 1 KiB pieces per 32-row block
+    constexpr int SLOT = RB * NPB * 1024;           // bytes per ring slot
+    constexpr int P = RB * NPB / 8;                 // pieces per wave per slot
+    static_assert((RB * NPB) % 8 == 0, "pieces per slot must split over 8 waves");
+    static_assert(RB == 1 || RB == 2, "RB must be 1 or 2");
+    constexpr int64_t TILE_B = (int64_t)NPB * 8192;  // bytes per 256-row tile of a plane
+    constexpr int NT = RB * NC;                     // chunks per slot
+    constexpr int P0 = P + 2 + (ISL2 ? 1 : 0);      // vector-memory ops per group, per wave
+    static_assert(P0 < NC, "the deferred key store must follow the slot's DMA pieces");
+    constexpr int X0 = 1;                           // chunk of the slot's extra LDS reads
+    constexpr int XE = 2 + (ISL2 ? 2 * RB : 0);     // extra reads: valid words, scales (+ norms)
+    constexpr int NBUF = 3;
+    extern __shared__ __attribute__((aligned(16))) unsigned char qsm[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int total = a.nqg * a.nspans;
+    const int b = blockIdx.x;
+    // XCD-aware order: the query groups of one span share an XCD (its L2)
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int span = logical / a.nqg, grp = logical % a.nqg;
+
+    // this wave's 32 queries as B fragments: Qf[2c + n] = chunk c, query half
+    // n: lane (j = lane & 15, kq = lane >> 4) holds query wave*32 + 16n + j,
+    // columns 64c + 16kq .. +15
+    i32x4_t Qf[2 * NC];
+    {
+        const int j = lane & 15, kq = lane >> 4;
+        const unsigned char* qp =
+            a.Q8 + (int64_t)grp * TILE_B + (kq >> 1) * 8192 + (wave * 32 + j) * 32 + 16 * (kq & 1);
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                Qf[2 * c + n] = *reinterpret_cast<const i32x4_t*>(qp + (2 * c) * 8192 + n * 16 * 32);
+    }
+    const int64_t q0 = (int64_t)grp * 256 + wave * 32;
+    const float sqA = a.qscale[q0 + (lane & 15)];
+    const float sqB = a.qscale[q0 + 16 + (lane & 15)];
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the query loads before the DMA ring
+
+    const int64_t s0 = (int64_t)span * a.slots_per_span;
+    int64_t s1 = s0 + a.slots_per_span;
+    if (s1 > a.nslots) s1 = a.nslots;
+    const int nsteps = s1 > s0 ? (int)(s1 - s0) : 0;
+
+    const uint32_t src_lane = (uint32_t)(16 * lane);
+    const unsigned ring = lds_addr(qsm);
+    // per-wave rings of 4 entries (step & 3): valid words [8][4][16 B], block
+    // scales [8][4][16 B], L2 norms [8][4][RB * 128 B]; every wave loads its own
+    // copy, so every wave issues the same vector-memory ops per step
+    const unsigned vring = ring + NBUF * SLOT + (unsigned)wave * 64u;
+    const unsigned sring = ring + NBUF * SLOT + 512u + (unsigned)wave * 64u;
+    const unsigned xnring = ring + NBUF * SLOT + 1024u + (unsigned)wave * (unsigned)(4 * RB * 128);
+    const int64_t tile0 = (s0 * RB * 32) >> 8;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.X8 + tile0 * TILE_B), (short)0, -1, 0x00020000);
+    int64_t igb = s0 * RB;
+    uint32_t ioff = (uint32_t)(((igb >> 3) - tile0) * TILE_B + (igb & 7) * 1024);
+    auto issue_piece = [&](int j, int t, int slot) {
+        if (j < P) {
+            const int p = wave + 8 * j;
+            const int rb = p / NPB, c = p % NPB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(size_t)(ring + (unsigned)(slot * SLOT + (rb * NPB + c) * 1024)),
+                                                     16, src_lane, ioff + (uint32_t)(rb * 1024 + c * 8192), 0, 0);
+        } else if (j == P) {
+            if (lane < RB)
+                __builtin_amdgcn_global_load_lds(a.valid + igb + lane, (lds_ptr_t)(size_t)(vring + (unsigned)((t & 3) * 16)), 4,
+                                                 0, 0);
+        } else if (j == P + 1) {
+            if (lane < RB)
+                __builtin_amdgcn_global_load_lds(a.sb + igb + lane, (lds_ptr_t)(size_t)(sring + (unsigned)((t & 3) * 16)), 4,
+                                                 0, 0);
+        } else {
+            if (lane < RB * 8)
+                __builtin_amdgcn_global_load_lds(a.xnorm2 + igb * 32 + 4 * lane,
+                                                 (lds_ptr_t)(size_t)(xnring + (unsigned)((t & 3) * RB * 128)), 16, 0, 0);
+        }
+        if (j == P0 - 1) {
+            igb += RB;
+            ioff += RB * 1024;
+            if ((igb & 7) == 0) ioff += (uint32_t)(TILE_B - 8192);
+        }
+    };
+    auto issue_group = [&](int t, int slot) {
+#pragma unroll
+        for (int j = 0; j < P0; j++) issue_piece(j, t, slot);
+    };
+
+    const int64_t qrow = q0 + (lane & 31);
+    float* krow = a.key + qrow * a.ldk;
+    // lane (i = lane&15, kq = lane>>4) reads row 16m+i, columns 64c+16kq..+15
+    // = piece 2c + (kq>>1), bytes 16(kq&1).. of the row (linear image)
+    const unsigned l16 = (unsigned)(((lane >> 5) & 1) * 1024 + (lane & 15) * 32 + 16 * ((lane >> 4) & 1));
+    i32x4_t B2[2][2];  // A fragments [chunk & 1][row half m]
+    if (nsteps > 0) {
+        issue_group(0, 0);
+        if (nsteps > 1) issue_group(1, 1);
+        qs_wait_vm(nsteps > 1 ? P0 : 0);  // group 0 landed, group 1 may stay in flight
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned sb0 = ring + l16;
+        B2[0][0] = lds_ld16_o<0>(sb0);
+        B2[0][1] = lds_ld16_o<512>(sb0);
+    }
+    // the pending block (a slot's last): per query half n the lane's partial
+    // key before the cross-lane combine
+    float mp0 = 0.f, mp1 = 0.f;
+    int64_t gbp = 0;
+    auto finish = [&](float p0, float p1, int64_t gb) {
+        // lanes g*16 + j (g = 0..3) hold partial keys of query 16n + j
+        float m0 = p0, m1 = p1;
+        const auto a0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m0), __float_as_uint(m0), false, false);
+        const auto a1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
+        m0 = ISL2 ? fminf(m0, __uint_as_float(a0[1])) : fmaxf(m0, __uint_as_float(a0[1]));
+        m1 = ISL2 ? fminf(m1, __uint_as_float(a1[1])) : fmaxf(m1, __uint_as_float(a1[1]));
+        const auto b0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m0), false, false);
+        const auto b1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
+        m0 = ISL2 ? fminf(m0, __uint_as_float(b0[1])) : fmaxf(m0, __uint_as_float(b0[1]));
+        m1 = ISL2 ? fminf(m1, __uint_as_float(b1[1])) : fmaxf(m1, __uint_as_float(b1[1]));
+        // lanes 0-15: queries j (n = 0) in m0, 16 + j in m1 -> lanes 16-31 take m1
+        const auto c01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m1), false, false);
+        const float m = __uint_as_float(c01[0]);
+        if (lane < 32) krow[gb] = ISL2 ? m : -m;
+    };
+    int cur = 0;
+    for (int t = 0; t < nsteps; t++) {
+        const int nxt = cur == NBUF - 1 ? 0 : cur + 1;
+        const int gslot = cur == 0 ? NBUF - 1 : cur - 1;  // slot of group t+2
+        const unsigned sbase = ring + (unsigned)(cur * SLOT) + l16;
+        const bool dma = t + 2 < nsteps;
+        const unsigned sm = (unsigned)(t & 3);
+        i32x4_t acc[RB][2][2];
+        uint2 vwv;
+        float2 sbv;
+        f32x4_t xa[RB], xb[RB];
+        // a block's reduction over its rows -> the lane's partial keys (p0, p1)
+        auto reduce = [&](auto rbc, float& p0, float& p1) {
+            constexpr int rb = decltype(rbc)::value;
+            const uint32_t vw = __builtin_amdgcn_readfirstlane(rb == 0 ? vwv.x : vwv.y);
+            const float sbf = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rb == 0 ? sbv.x : sbv.y)));
+            // acc[rb][m][n][r] is row 16m + 4g + r (g = lane>>4) of query 16n + (lane&15)
+            const uint32_t vl = vw >> (4 * ((lane >> 4) & 3));
+            const float s0f = sqA * sbf, s1f = sqB * sbf;
+            float mn[2];
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                if constexpr (ISL2) {
+                    const float cn = -2.f * (n ? s1f : s0f);
+                    float m = __builtin_inff();
+#pragma unroll
+                    for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const float v = fmaf(cn, (float)acc[rb][mm][n][r], mm ? xb[rb][r] : xa[rb][r]);
+                            m = fminf(m, ((vl >> (16 * mm + r)) & 1u) ? v : __builtin_inff());
+                        }
+                    mn[n] = m;
+                } else {
+                    int mi;
+                    if (vw == 0xFFFFFFFFu) {
+                        mi = max(max(max(acc[rb][0][n][0], acc[rb][0][n][1]), max(acc[rb][0][n][2], acc[rb][0][n][3])),
+                                 max(max(acc[rb][1][n][0], acc[rb][1][n][1]), max(acc[rb][1][n][2], acc[rb][1][n][3])));
+                    } else {
+                        mi = Q8_NONE;
+#pragma unroll
+                        for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                            for (int r = 0; r < 4; r++)
+                                mi = max(mi, ((vl >> (16 * mm + r)) & 1u) ? acc[rb][mm][n][r] : Q8_NONE);
+                    }
+                    // the scale is positive: the largest S is the largest product
+                    mn[n] = mi == Q8_NONE ? -__builtin_inff() : (n ? s1f : s0f) * (float)mi;
+                }
+            }
+            p0 = mn[0];
+            p1 = mn[1];
+        };
+        static_for<0, NT>([&](auto ttc) {
+            constexpr int tt = decltype(ttc)::value;
+            constexpr int rb = tt / NC, c = tt % NC;
+            if constexpr (tt + 1 < NT) {
+                constexpr int o1 = ((tt + 1) / NC * NPB + 2 * ((tt + 1) % NC)) * 1024;
+                B2[(tt + 1) & 1][0] = lds_ld16_o<o1>(sbase);
+                B2[(tt + 1) & 1][1] = lds_ld16_o<o1 + 512>(sbase);
+            }
+            if constexpr (tt == X0) {  // this slot's valid words, scales (+ L2 norms)
+                asm volatile("ds_read_b64 %0, %1" : "=v"(vwv) : "v"(vring + sm * 16u));
+                asm volatile("ds_read_b64 %0, %1" : "=v"(sbv) : "v"(sring + sm * 16u));
+                if constexpr (ISL2) {
+                    // rows 4g..4g+3 and 16+4g..+3 of block rb, g = lane>>4
+                    const unsigned xbase = xnring + sm * (unsigned)(RB * 128) + (unsigned)(16 * ((lane >> 4) & 3));
+                    xa[0] = lds_ld4f_o<0>(xbase);
+                    xb[0] = lds_ld4f_o<64>(xbase);
+                    if constexpr (RB == 2) {
+                        xa[RB - 1] = lds_ld4f_o<128>(xbase);
+                        xb[RB - 1] = lds_ld4f_o<192>(xbase);
+                    }
+                }
+            }
+            qs_wait_lgkm<(tt + 1 < NT ? 2 : 0) + (tt == X0 ? XE : 0)>();
+            asm volatile("" : "+v"(B2[tt & 1][0]), "+v"(B2[tt & 1][1]));
+            if constexpr (tt == X0 + 1) {
+                if constexpr (ISL2) {
+                    asm volatile("" : "+v"(vwv), "+v"(sbv), "+v"(xa[0]), "+v"(xb[0]));
+                    if constexpr (RB == 2) asm volatile("" : "+v"(xa[RB - 1]), "+v"(xb[RB - 1]));
+                } else {
+                    asm volatile("" : "+v"(vwv), "+v"(sbv));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < 2; m++)
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    if constexpr (c == 0)
+                        acc[rb][m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[tt & 1][m], Qf[2 * c + n],
+                                                                              i32x4_t{0, 0, 0, 0}, 0, 0, 0);
+                    else
+                        acc[rb][m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[tt & 1][m], Qf[2 * c + n],
+                                                                              acc[rb][m][n], 0, 0, 0);
+                }
+            // DMA of group t+2: one piece per chunk
+            if constexpr (tt < P0) {
+                if (dma) issue_piece(tt, t + 2, gslot);
+            }
+            // the previous slot's last block: cross-lane combine + key store
+            if constexpr (tt == P0) {
+                if (t > 0) finish(mp0, mp1, gbp);
+            }
+            // RB = 2: block 0 is reduced and stored beside block 1's MFMAs
+            if constexpr (RB == 2 && tt == NC + 1) {
+                float p0, p1;
+                reduce(std::integral_constant<int, 0>{}, p0, p1);
+                finish(p0, p1, (s0 + t) * RB);
+            }
+        });
+        reduce(std::integral_constant<int, RB - 1>{}, mp0, mp1);
+        gbp = (s0 + t) * RB + RB - 1;
+        // ---- end of the slot: the next group must have landed (every wave) ----
+        if (t + 1 < nsteps) {
+            // this wave's vector-memory ops after group t+1, in issue order: the
+            // stores of slot t-1, the pieces of group t+2, the stores of slot t
+            // (RB per slot; slot 0 has RB - 1)
+            if (t >= 2 && t + 2 < nsteps) {
+                qs_wait_vm_c<2 * RB + P0>();
+            } else {
+                const int y = (t == 0 ? RB - 1 : (t == 1 ? RB - 1 : RB) + RB) + (t + 2 < nsteps ? P0 : 0);
+                qs_wait_vm(y);
+            }
+            __builtin_amdgcn_s_barrier();  // slot t is free; slot t+1 has landed for every wave
+            __builtin_amdgcn_sched_barrier(0);
+            const unsigned sbn = ring + (unsigned)(nxt * SLOT) + l16;
+            B2[0][0] = lds_ld16_o<0>(sbn);
+            B2[0][1] = lds_ld16_o<512>(sbn);
+        }
+        cur = nxt;
+    }
+    if (nsteps > 0) finish(mp0, mp1, gbp);
+}
+
+}  // namespace
+}  // namespace wv

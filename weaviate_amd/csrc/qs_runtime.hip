@@ -15,8 +15,16 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                      float* topA, const float* gA, const float* gE, int W) {
     const int kout = mode == 1 ? k + 1 : k;
     const int NK = idx->dpb / 16;
-    const int RB = qs_rb(NK);
-    const int R = qs_R(k);
+    // int8 block keys (q8_kernels.hip): NC 64-column chunks per block, RB8 blocks per ring slot
+    const bool q8 = idx->q8_planes && idx->q8_opt;
+    const int NC8 = idx->dpb8 / 64;
+    const int RB8 = idx->dpb8 <= 768 ? 2 : 1;
+    const int RB = q8 ? RB8 : qs_rb(NK);
+    int R = qs_R(k);
+    if (q8) {  // the int8 bound is wider: one list size up (option q8_R)
+        if (idx->q8_R > 0) R = std::max(R, idx->q8_R);
+        else R = std::min(8, 2 * R);
+    }
     const int L = 64 * (R - 1);
     const int64_t nslots = std::max<int64_t>(1, (idx->hiwater + 32 * RB - 1) / (32 * RB));
     const int64_t nb = nslots * RB;  // 32-row blocks scanned = key row length
@@ -31,6 +39,11 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     HIPCHK(idx->qsCand.ensure((size_t)qc * std::max(L, 448) * sizeof(uint32_t)));  // 448: the overflow pass
     HIPCHK(idx->qsNc.ensure((size_t)qc * sizeof(int32_t)));
     HIPCHK(idx->qsEps.ensure((size_t)qc * sizeof(float)));
+    if (q8) {
+        HIPCHK(idx->q8Qb.ensure((size_t)qc * idx->dpb8));
+        HIPCHK(idx->q8Scale.ensure((size_t)qc * sizeof(float)));
+        HIPCHK(idx->q8Info.ensure((size_t)qc * sizeof(float4)));
+    }
     HIPCHK(idx->qsCap.ensure((size_t)qc * sizeof(float)));
     HIPCHK(idx->qsList.ensure((size_t)2 * qc * sizeof(int32_t)));
     if (!o_flags || phase) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
@@ -43,6 +56,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     const double hdep = NK + 16.0;
     const float gacc = (float)(hdep * u4 / (1.0 - hdep * u4));
     const float gd = (float)gamma_n(idx->dpb + 8);
+    // int8 keys: S = fl(fl(sq sb) float(sum)), at most three roundings of |q^ . x^|
+    const float gacc8 = 4.0001f * 5.9604645e-08f;
     const int metric = idx->metric == WV_METRIC_L2_SQUARED ? L2 : idx->metric == WV_METRIC_DOT ? DOT : COSINE;
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
     const float* Qn_all = idx->qn.as<float>();
@@ -57,9 +72,19 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         if (c0 == 0) { idx->qs_last_nq = cn == nq ? cn : 0; idx->qs_last_nb = nb; idx->qs_last_ldk = ldk; }
         const float* Qn = Qn_all + c0 * idx->dpad;
         float4* qinfo = idx->qsInfo.as<float4>();
-        if (phase != 2)
-        k_query_split<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dpb, cn, cn_pad,
-                                                                   idx->qsQb.as<uint16_t>(), qinfo);
+        if (phase != 2) {
+            k_query_split<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dpb, cn, cn_pad,
+                                                                       idx->qsQb.as<uint16_t>(), qinfo);
+            if (q8)
+                k_query_q8<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dims, idx->dpb8, cn, cn_pad,
+                                                                        qinfo, idx->q8Qb.as<unsigned char>(),
+                                                                        idx->q8Scale.as<float>(),
+                                                                        idx->q8Info.as<float4>());
+        }
+        // the selection's bound: int8 keys use their own query split and maxima
+        const float4* qinfo_sel = q8 ? idx->q8Info.as<float4>() : qinfo;
+        const uint32_t* qmax_sel = q8 ? idx->qmax8 : idx->qsmax;
+        const float gacc_sel = q8 ? gacc8 : gacc;
         // ---- block keys (the dominant kernel) ----
         QsArgs a;
         a.Xb = reinterpret_cast<const unsigned char*>(idx->Xb);
@@ -72,15 +97,16 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         a.dbg = idx->sel_dbg;
         // k_qs_blockkey_w4 for d > 768: 128-query workgroups, a 32-row block in two
         // column parts per ring step: dpb 1024 -> 4 slots of 32 KiB, 1536 -> 3 of 48 KiB
-        const bool w4 = idx->dpb > QS_W4_DPB;
+        const bool w4 = !q8 && idx->dpb > QS_W4_DPB;
         const int w4_nb = NK == 64 ? 4 : 3;
         a.nqg = (int)(cn_pad / (w4 ? 128 : QS_QPB));
         int64_t nspans = 256 / std::gcd(256, a.nqg);
         while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
         if (idx->spans_opt > 0) nspans = idx->spans_opt;
         {   // a span's plane bytes (+ one tile of slack) must stay below 4 GiB (32-bit buffer offsets)
-            const int64_t slot_b = (int64_t)RB * 32 * idx->dpb * 2;
-            const int64_t max_sps = ((1ll << 32) - 2 * 256ll * idx->dpb * 2) / slot_b;
+            const int64_t row_b = q8 ? (int64_t)idx->dpb8 : (int64_t)idx->dpb * 2;
+            const int64_t slot_b = (int64_t)RB * 32 * row_b;
+            const int64_t max_sps = ((1ll << 32) - 2 * 256ll * row_b) / slot_b;
             nspans = std::max<int64_t>(nspans, (nslots + max_sps - 1) / max_sps);
         }
         if (idx->spans_opt <= 0) {  // whole rounds of one workgroup per CU (10M x 1024: 5 spans = 320 groups -> 8)
@@ -92,7 +118,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         a.slots_per_span = (int)sps;
         a.nspans = (int)((nslots + sps - 1) / sps);
         const bool l2 = metric == L2;
-        const size_t lds = w4 ? (size_t)w4_nb * (NK / 4) * 2048 + 256 + (l2 ? (size_t)4 * 4 * 128 : 0)
+        const size_t lds = q8 ? (size_t)3 * RB * 2 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * RB * 128 : 0)
+                         : w4 ? (size_t)w4_nb * (NK / 4) * 2048 + 256 + (l2 ? (size_t)4 * 4 * 128 : 0)
                               : (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
         dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
         if (phase != 2) {
@@ -124,7 +151,37 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     } while (0)
 #define WV_QSWN(L2V)                                   \
     if (NK == 64) WV_QSW(64, L2V, 4); else WV_QSW(96, L2V, 3);
-        if (w4) {
+#define WV_Q8(NCV, RBV, L2V)                                                                                   \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, RBV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey<NCV, RBV, L2V><<<grid, 512, lds, s>>>(q8a);                                               \
+    } while (0)
+#define WV_Q8N(L2V)                                    \
+    switch (NC8) {                                     \
+    case 8: WV_Q8(8, 2, L2V); break;                   \
+    case 10: WV_Q8(10, 2, L2V); break;                 \
+    case 12: WV_Q8(12, 2, L2V); break;                 \
+    case 16: WV_Q8(16, 1, L2V); break;                 \
+    case 20: WV_Q8(20, 1, L2V); break;                 \
+    default: WV_Q8(24, 1, L2V); break;                 \
+    }
+        idx->stats.last_route = q8 ? WV_ROUTE_QS_INT8 : w4 ? WV_ROUTE_QS_W4 : WV_ROUTE_QS_BF16;
+        if (q8) {
+            Q8Args q8a;
+            q8a.X8 = idx->X8;
+            q8a.sb = idx->sb8;
+            q8a.xnorm2 = idx->xnorm2;
+            q8a.valid = valid;
+            q8a.Q8 = idx->q8Qb.as<unsigned char>();
+            q8a.qscale = idx->q8Scale.as<float>();
+            q8a.key = a.key;
+            q8a.ldk = ldk;
+            q8a.nslots = nslots;
+            q8a.slots_per_span = a.slots_per_span;
+            q8a.nspans = a.nspans;
+            q8a.nqg = a.nqg;
+            if (l2) { WV_Q8N(true); } else { WV_Q8N(false); }
+        } else if (w4) {
             if (l2) { WV_QSWN(true); } else { WV_QSWN(false); }
 #ifdef WV_QS_DBG  // timing experiments (k_qs_blockkey DBG bits), not in the product build
         } else if (idx->sel_dbg > 0 && !l2 && NK == 48) {
@@ -144,6 +201,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
 #undef WV_QS
 #undef WV_QSWN
 #undef WV_QSW
+#undef WV_Q8N
+#undef WV_Q8
         HIPCHK(hipGetLastError());
         if (time_it) { HIPCHK(hipEventRecord(idx->ev1, s)); idx->timed = 1; }
         idx->stats.mfma_launches++;
@@ -154,7 +213,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // select / exact pass RV over all queries (list == nullptr) or over the listed ones
         auto sel = [&](int RV, const int32_t* list, const uint32_t* cnt, float* tA) {
             const unsigned gw = (unsigned)((cn + 3) / 4);
-#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo, idx->qsmax, idx->d_maxn2, gd, gacc, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>())
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>())
             if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
 #undef WV_SELR
         };

@@ -835,9 +835,12 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         if (adc3) {
             dim3 g3((unsigned)((nslots + PQ3_ROWS - 1) / PQ3_ROWS), (unsigned)((nq + 63) / 64));
 #define WV_ADC3(DBGV) k_pq_adc3<DBGV><<<g3, 512, 0, s>>>(idx->pq_codes, pq_g16(m), m, valid, nslots, idx->lutg.as<float>(), (int)nq, wrapm, nblk, idx->rB.as<float>())
-            if (idx->pq_adc3 == 3) WV_ADC3(1);       // timing experiments only (wrong results)
+#ifdef WV_PQ_DBG  // timing experiments only (wrong results), never in the product build
+            if (idx->pq_adc3 == 3) WV_ADC3(1);
             else if (idx->pq_adc3 == 4) WV_ADC3(2);
-            else WV_ADC3(0);
+            else
+#endif
+            WV_ADC3(0);
 #undef WV_ADC3
         } else {
 #define WV_ADC2M(KCV)                                                                                        \
@@ -1076,7 +1079,10 @@ extern "C" int wv_index_quant_begin(wv_index* idx, const float* d_queries, int64
         if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
         idx->stats.last_group_queries = (uint64_t)nq;
     } else {
-        HIPCHK(hipMemsetAsync(idx->rB.p, 0x7f, (size_t)nq * (ld / EBLK) * sizeof(float), s));  // +huge: no rows
+        // no rows: every block minimum +inf (a finite fill would read as one row's distance)
+        const int64_t nbm = nq * (ld / EBLK);
+        k_fill_u32<<<(unsigned)((nbm + 255) / 256), 256, 0, s>>>(idx->rB.as<uint32_t>(), nbm, 0x7f800000u);
+        HIPCHK(hipGetLastError());
     }
     idx->qt_nq = nq;
     idx->qt_ld = ld;

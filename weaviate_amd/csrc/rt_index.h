@@ -35,6 +35,7 @@
 #include "rq_kernels.hip"
 #include "gemv_kernels.hip"
 #include "qs_kernels.hip"
+#include "q8_kernels.hip"
 #include "sq_kernels.hip"
 
 using namespace wv;
@@ -126,6 +127,15 @@ struct wv_index {
     int use_qs = 0, qs_planes = 0, dpb = 0;
     int exact_filter = 1;           // k_blk_exact's bf16-plane row filter (option exact_filter)
     uint16_t* Xb = nullptr;
+    // int8 block-key plane (q8_kernels.hip): [cap][dpb8] codes, one scale per
+    // 32-row block, built beside the bf16 plane when 384 < dims <= 1536
+    int q8_planes = 0, dpb8 = 0;
+    int q8_opt = 1;                 // option q8: block keys from the int8 plane (1) or the bf16 plane (0)
+    int q8_R = 0;                   // option q8_R: candidate lists for int8 keys (0: one level above qs_R)
+    unsigned char* X8 = nullptr;
+    float* sb8 = nullptr;
+    uint32_t* qmax8 = nullptr;      // device [4]: max |x - x^|^2, max |x^|^2 (float bits)
+    DBuf q8Qb, q8Scale, q8Info, q8Blk;
     uint32_t* qsmax = nullptr;      // device [4]: max |x - x_h|^2, max |x_h|^2 (float bits), non-finite flag
     uint32_t* qscount = nullptr;    // device [4]: [0] replayed queries (cumulative), [1] this batch's flagged,
                                     // [2] overflow second passes (cumulative), [3] this batch's
@@ -193,13 +203,15 @@ struct wv_index {
     int gemv_max = 8, gemv_wg = 1024, exact_multi = 1;  // batches up to this many queries take the GEMV select kernel (kver 6)
 };
 
-// The block keys, eps and prepared query rows of the last batch (qs_keys_nq)
-// and a pending sharded phase 1 (qs_phase_nq) describe one batch on one corpus
-// state: an Add, a Delete or another batch's query preparation ends them.
+// The block keys, eps and prepared query rows of the last batch (qs_keys_nq),
+// a pending sharded phase 1 (qs_phase_nq), a sharded hnsw flat batch (qt_nq)
+// and a sharded BQ batch (bq_nq) describe one batch on one corpus state: an
+// Add, a Delete or another batch's query preparation ends them.
 static void invalidate_batch(wv_index* idx) {
     idx->qs_keys_nq = 0;
     idx->qs_phase_nq = 0;
     idx->qt_nq = 0;
+    idx->bq_nq = 0;  // a sharded BQ batch's minima and query rows (wv_index_bq_begin)
 }
 
 // ---------------------------------------------------------------------------

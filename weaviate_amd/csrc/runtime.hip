@@ -63,6 +63,10 @@ static void set_dims(wv_index* idx, int64_t d) {
     idx->dpb = (int)round_up(d, 128);
     if (idx->dpb > QS_W4_DPB) idx->dpb = (int)round_up(d, 512);  // 512-column ring parts
     idx->qs_planes = (idx->use_qs && idx->dpb <= QS_MAX_DPB) ? 1 : 0;
+    // int8 plane: 128-column multiples up to 768 (two blocks per ring slot),
+    // 256-column multiples above (one block per slot), <= 48 KiB per slot
+    idx->dpb8 = (int)(d <= 768 ? round_up(d, 128) : round_up(d, 256));
+    idx->q8_planes = (idx->qs_planes && d > 384 && idx->dpb8 <= 1536) ? 1 : 0;
 }
 
 extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
@@ -106,6 +110,8 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     if (e == hipSuccess) e = hipMemset(idx->d_maxn2, 0, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&idx->qsmax, 4 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(idx->qsmax, 0, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&idx->qmax8, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(idx->qmax8, 0, 4 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&idx->qscount, 4 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(idx->qscount, 0, 4 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipEventCreate(&idx->ev0);
@@ -131,7 +137,8 @@ extern "C" void wv_index_destroy(wv_index* idx) {
                     &idx->cn, &idx->ident, &idx->lut, &idx->ascI, &idx->ascD, &idx->ascN, &idx->rqq, &idx->rqm,
                     &idx->rE2, &idx->rB2, &idx->gmA, &idx->gmI, &idx->qsQb, &idx->qsInfo, &idx->qsKey, &idx->qsCand,
                     &idx->qsNc, &idx->qsEps, &idx->qsFlags, &idx->qsList, &idx->qsScratch, &idx->rpBlk, &idx->rpLb,
-                    &idx->rpQ, &idx->rpE, &idx->rpVm, &idx->rpOff, &idx->rpTot, &idx->rpCtr, &idx->flCtr})
+                    &idx->rpQ, &idx->rpE, &idx->rpVm, &idx->rpOff, &idx->rpTot, &idx->rpCtr, &idx->flCtr,
+                    &idx->q8Qb, &idx->q8Scale, &idx->q8Info, &idx->q8Blk})
         b->release();
     if (idx->aux) hipStreamSynchronize(idx->aux);
     for (hipEvent_t e : {idx->evd[0], idx->evd[1], idx->evr[0], idx->evr[1]})
@@ -150,6 +157,9 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->pq_codes) hipFree(idx->pq_codes);
     if (idx->Xb) hipFree(idx->Xb);
     if (idx->qsmax) hipFree(idx->qsmax);
+    if (idx->X8) hipFree(idx->X8);
+    if (idx->sb8) hipFree(idx->sb8);
+    if (idx->qmax8) hipFree(idx->qmax8);
     if (idx->qscount) hipFree(idx->qscount);
     for (void* p : {(void*)idx->rq_src, (void*)idx->rq_sign, (void*)idx->rq_round, idx->rq_codes, (void*)idx->rq_meta})
         if (p) hipFree(p);
@@ -183,6 +193,8 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     uint32_t* pr = nullptr;
     uint64_t* cd = nullptr;
     uint16_t* xb = nullptr;
+    unsigned char* x8 = nullptr;
+    float* sb8 = nullptr;
     void* rqc = nullptr;
     float4* rqm = nullptr;
     uint32_t* pc = nullptr;
@@ -203,6 +215,10 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     WV_STEP("present", alloc((void**)&pr, (size_t)(nc / 32) * sizeof(uint32_t)));
     if (idx->compression == WV_COMPRESSION_BQ) WV_STEP("bq codes", alloc((void**)&cd, (size_t)words * nc * sizeof(uint64_t)));
     if (idx->qs_planes) WV_STEP("bf16 block-key plane", alloc((void**)&xb, qs_b));
+    if (idx->q8_planes) {
+        WV_STEP("int8 block-key plane", alloc((void**)&x8, (size_t)nc * idx->dpb8));
+        WV_STEP("int8 block scales", alloc((void**)&sb8, (size_t)(nc / 32) * sizeof(float)));
+    }
     if (idx->rq_ready) {
         WV_STEP("rq codes", alloc(&rqc, rq_cb));
         WV_STEP("rq meta", alloc((void**)&rqm, (size_t)nc * sizeof(float4)));
@@ -231,6 +247,14 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         WV_STEP("memset", hipMemsetAsync(xb, 0, qs_b, s));
         if (oc > 0 && idx->Xb)
             WV_STEP("copy", hipMemcpyAsync(xb, idx->Xb, (size_t)oc * idx->dpb * sizeof(uint16_t), hipMemcpyDeviceToDevice, s));
+    }
+    if (x8) {  // 256-row tiles: the old tiles are a prefix
+        WV_STEP("memset", hipMemsetAsync(x8, 0, (size_t)nc * idx->dpb8, s));
+        WV_STEP("memset", hipMemsetAsync(sb8, 0, (size_t)(nc / 32) * sizeof(float), s));
+        if (oc > 0 && idx->X8) {
+            WV_STEP("copy", hipMemcpyAsync(x8, idx->X8, (size_t)oc * idx->dpb8, hipMemcpyDeviceToDevice, s));
+            WV_STEP("copy", hipMemcpyAsync(sb8, idx->sb8, (size_t)(oc / 32) * sizeof(float), hipMemcpyDeviceToDevice, s));
+        }
     }
     if (rqc) {
         WV_STEP("memset", hipMemsetAsync(rqc, 0, rq_cb, s));
@@ -277,6 +301,8 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     swap_in(idx->present, pr);
     if (cd) { swap_in(idx->codes, cd); idx->words = words; }
     swap_in(idx->Xb, xb);
+    swap_in(idx->X8, x8);
+    swap_in(idx->sb8, sb8);
     if (rqc) {
         if (idx->rq_codes) hipFree(idx->rq_codes);
         idx->rq_codes = rqc;
@@ -385,6 +411,26 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
     }
 }
 
+// the int8 plane of every 32-row block holding one of the written slots
+// (host slot list): each block is re-quantised whole (its scale is the
+// block's max |x|), after the rows themselves were stored
+static int requant_blocks(wv_index* idx, const uint32_t* h_slots, int64_t n) {
+    if (!idx->q8_planes || n <= 0) return WV_OK;
+    std::vector<uint32_t> blk((size_t)n);
+    for (int64_t i = 0; i < n; i++) blk[(size_t)i] = h_slots[i] >> 5;
+    std::sort(blk.begin(), blk.end());
+    blk.erase(std::unique(blk.begin(), blk.end()), blk.end());
+    HIPCHK(idx->q8Blk.ensure(blk.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(idx->q8Blk.p, blk.data(), blk.size() * sizeof(uint32_t), hipMemcpyHostToDevice, idx->stream));
+    k_block_q8<<<(unsigned)blk.size(), 256, 0, idx->stream>>>(idx->X, idx->dpad, idx->dims, idx->dpb8,
+                                                              idx->q8Blk.as<uint32_t>(), 0, idx->X8, idx->sb8,
+                                                              idx->qmax8);
+    HIPCHK(hipGetLastError());
+    // the host list is read by the copy: keep it alive until the stream passes it
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    return WV_OK;
+}
+
 // host mirror of the device non-finite flag (rows with NaN/Inf route the exact
 // search to the all-rows path); called after a synchronised Add
 static int refresh_nonfinite(wv_index* idx) {
@@ -457,6 +503,8 @@ static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs
         HIPCHK(hipMemcpyAsync(idx->slots.p, hslots.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, idx->stream));
         launch_prepare(idx, idx->stage.as<float>(), (int64_t)m, idx->slots.as<uint32_t>(), as_stored);
         HIPCHK(hipGetLastError());
+        rc = requant_blocks(idx, hslots.data(), (int64_t)m);
+        if (rc) return rc;
         HIPCHK(hipStreamSynchronize(idx->stream));
         for (size_t j = 0; j < m; j++) {
             uint32_t s = hslots[j];
@@ -510,6 +558,8 @@ extern "C" int wv_index_add_range_device(wv_index* idx, uint64_t first_id, const
     HIPCHK(hipMemcpyAsync(idx->slots.p, hs.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, idx->stream));
     launch_prepare(idx, d_vecs, n, idx->slots.as<uint32_t>());
     HIPCHK(hipGetLastError());
+    rc = requant_blocks(idx, hs.data(), n);
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(idx->stream));
     for (int64_t i = 0; i < n; i++) {
         if (!idx->h_present[s0 + i]) { idx->h_present[s0 + i] = 1; idx->npresent++; }
@@ -579,8 +629,12 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "force_replay") idx->force_replay = (int)value;
     else if (k == "spans") idx->spans_opt = (int)value;
     else if (k == "replay_dbg") idx->replay_dbg = value != 0;  // diagnostics: k_blk_replay clock totals (printf)
-    else if (k == "pq_adc3") {  // 1: k_pq_adc3 (default), 0: k_pq_adc2; 3, 4: timing experiments (wrong results)
+    else if (k == "pq_adc3") {  // 1: k_pq_adc3 (default), 0: k_pq_adc2
+#ifdef WV_PQ_DBG  // 3, 4: timing experiments (wrong results), debug builds only
         if (value < 0 || value > 4) return set_err(WV_ERR_INVALID, "pq_adc3 must be 0..4");
+#else
+        if (value < 0 || value > 1) return set_err(WV_ERR_INVALID, "pq_adc3 must be 0 or 1");
+#endif
         idx->pq_adc3 = (int)value;
     }
     else if (k == "timing") idx->timing = (int)value;
@@ -628,6 +682,11 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
         idx->cache_opt = (int)value;
     }
     else if (k == "sel_dbg") idx->sel_dbg = (int)value;
+    else if (k == "q8") idx->q8_opt = value ? 1 : 0;  // int8 block keys (default 1) or bf16 (0)
+    else if (k == "q8_R") {
+        if (value != 0 && value != 2 && value != 4 && value != 8) return set_err(WV_ERR_INVALID, "q8_R must be 0, 2, 4 or 8");
+        idx->q8_R = (int)value;
+    }
     else if (k == "qgroup") idx->qgroup_opt = (int)value;
     else if (k == "sel_opt") idx->sel_opt = (int)value;
     else return set_err(WV_ERR_INVALID, "unknown option %s", key);
@@ -811,6 +870,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
                        int32_t* o_flags) {
     const int kout = mode == 1 ? k + 1 : k;
     idx->qs_keys_nq = 0;
+    idx->stats.last_route = WV_ROUTE_NONE;
     if (nq <= 0) return WV_OK;
     if (n_valid == 0 || idx->dims == 0) {
         HIPCHK(hipMemsetAsync(o_n, 0, (size_t)nq * sizeof(int32_t), s));
@@ -862,6 +922,7 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         int kver = idx->kernel_opt == 7 ? 0 : idx->kernel_opt;
         if (kver == 0) kver = nq <= idx->gemv_max ? 6 : 3;
         const bool gemv = kver == 6;
+        idx->stats.last_route = gemv ? WV_ROUTE_GEMV : WV_ROUTE_F32_SELECT;
         // GEMV: QG queries per workgroup staged in LDS (<= 64 KiB of query rows)
         // (the smallest of 1/2/4/8 covering nq: padded query columns cost FMAs and LDS reads)
         int gqg = nq <= 1 ? 1 : nq <= 2 ? 2 : nq <= 4 ? 4 : 8;
