@@ -52,6 +52,9 @@ FLAT = {
                name="10M x 768 fp32 cosine, k=10, exact flat search (BASELINE configs[2])"),
 }
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (spec, MI355X_MICROARCH.md)
+MFMA_I8_PEAK_TOPS = 5000.0      # MI355X dense int8 MFMA: 2x bf16 per clock (MI355X_MICROARCH.md, Matrix cores)
+# wv_stats.last_route (include/wv_knn.h WV_ROUTE_*) -> the dominant key kernel
+ROUTE_KERNEL = {1: "k_qs_blockkey", 2: "k_qs_blockkey_w4", 3: "k_q8_blockkey", 4: "k_mfma_select3", 5: "k_gemv_select"}
 # 32-bit integer VALU lane-ops/s: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  The
 # 32-lane/clk rate (78.6 T) is the f32 FMA rate; v_xor_b32 / v_bcnt_u32_b32 issue
 # at 4 cycles per wave64 (measured: k_bq_blockmin_lds sustains 33.6 T instr-lane-ops/s).
@@ -316,6 +319,42 @@ def measured_clock(workload: str, n_local: int, dims: int, batch: int, kernel: s
     return best
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def relaunch_cmd(argv, n: int, port: int):
+    """`python -m torch.distributed.run` over N local ranks running this same
+    bench.py with the same arguments (one process per GPU, rendezvous on
+    127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def maybe_relaunch(argv, gpus: int, env=None, run=None) -> int | None:
+    """--gpus N > 1 without a launcher (no WORLD_SIZE in the environment): start
+    the N-rank run as a child process -- before this process touches the GPU
+    (nothing here imports torch) -- relay its output and return its exit code.
+    None: no relaunch (a single GPU, or already one rank of a launcher)."""
+    env = os.environ if env is None else env
+    if gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    import subprocess
+    run = run or subprocess.run
+    cmd = relaunch_cmd(argv, gpus, free_port())
+    log("[bench] --gpus %d without a launcher: %s" % (gpus, " ".join(cmd)))
+    child_env = dict(env)
+    child_env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = run(cmd, env=child_env, stdout=subprocess.PIPE, text=True)
+    for line in (p.stdout or "").splitlines():
+        if line.startswith("{"):  # rank 0's JSON line
+            print(line, flush=True)
+    return p.returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", choices=["c3", "c1", "c2", "bq", "pq", "rq8", "rq1"], default="c3",
@@ -344,6 +383,9 @@ def main():
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per k_mfma_select launch from the rocprofv3 PMC pass")
     args = ap.parse_args()
+    rc = maybe_relaunch(sys.argv[1:], args.gpus)
+    if rc is not None:
+        sys.exit(rc)
     if args.cpu_threads is None:
         # every CPU this process may use: nproc, capped by a cgroup quota (more
         # threads than the quota only time-slice the same cores)
@@ -357,7 +399,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch one rank per GPU "
+                         "(bench.py starts torch.distributed.run itself when WORLD_SIZE is unset)")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     shard = world > 1 or args.sharded
@@ -415,6 +458,9 @@ def main():
     if pq:
         torch.cuda.synchronize()
         t_fit = time.perf_counter()
+        if shard and n_local < PQ_TRAIN:
+            # the single index trains on the first trainingLimit rows of the whole corpus: rank 0 must hold them
+            raise SystemExit(f"sharded PQ needs >= {PQ_TRAIN} rows on rank 0 (has {n_local})")
         if not shard or rank == 0:
             index.pq_fit(seed=SEED_CORPUS)  # rank 0 holds ids [0, n_local): the first trainingLimit rows
         if shard:  # one codebook for every shard (NewProductQuantizerWithEncoders on the others)
@@ -481,6 +527,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     replays = index.stats()["replayed_queries"] - replays0
+    route = int(index.stats().get("last_route", 0))
     if shard and not (bq or pq or rq_bits):
         replays = int(searcher.flagged)  # the cross-shard replay's queries (this rank's view = every rank's)
     sharded_check = None
@@ -507,8 +554,10 @@ def main():
     total_q = B * args.steps
     value = total_q / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    # the exact fp32 path's dominant kernel: the bf16 block-key pass (runtime.hip auto choice)
-    sel_kernel = "k_qs_blockkey"
+    # the exact fp32 path's dominant kernel: the block-key pass the runtime chose
+    # (int8 keys for 384 < d <= 1536, bf16 keys otherwise; wv_stats.last_route)
+    sel_kernel = ROUTE_KERNEL.get(route, "k_qs_blockkey")
+    int8_keys = sel_kernel == "k_q8_blockkey"
     total_avg = float(np.mean(tot_ms)) if tot_ms else 0.0
     # the dominant kernel of each workload: its PMC record (matched on kernel
     # name and configuration) is the only source of `traffic`
@@ -562,20 +611,25 @@ def main():
                 "hbm_GBps": n_local * words * 8 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
                 "traffic": args.traffic_bytes}
     else:
-        # roofline of the dominant kernel (k_qs_blockkey): one
-        # bf16 MFMA product per (query, row, dim): algorithmic flops per launch
-        # = 2 * B * n_local * d, over its measured average duration (HIP events
-        # on the stream it runs on), against the dense bf16 MFMA peak.
+        # roofline of the dominant kernel (k_q8_blockkey, DESIGN.md 3.1f, or
+        # k_qs_blockkey, 3.1d): one MFMA product per (query, row, dim):
+        # algorithmic ops per launch = 2 * B * n_local * d, over its measured
+        # average duration (HIP events on the stream it runs on), against the
+        # dense peak of the MFMA's input type (int8: 5 POPS, bf16: 2.5 PFLOPS).
         # the timed launch is the first query chunk of the batch (search_qs)
         f0 = int(index.stats().get("last_group_queries", 0)) or B
         flops = 2.0 * min(B, f0) * n_local * dims
         achieved = flops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
-        peak = MFMA_BF16_PEAK_TFLOPS
+        peak = MFMA_I8_PEAK_TOPS if int8_keys else MFMA_BF16_PEAK_TFLOPS
         roof = {"bound": "mfma", "kernel": sel_kernel, "achieved": achieved, "peak": peak,
-                "unit": "TFLOP/s", "frac": achieved / peak, "launch_ms": sel_avg,
-                "mfma": ("v_mfma_f32_16x16x32_bf16" if dims > 384 else "v_mfma_f32_32x32x16_bf16")
-                        + " (bf16 in, fp32 accumulate): block keys = per-32-row minima of the approximate "
-                          "distance; every returned distance is the reference-order fp32 value",
+                "unit": "TOPS (int8 MFMA)" if int8_keys else "TFLOP/s", "frac": achieved / peak, "launch_ms": sel_avg,
+                "mfma": ("v_mfma_i32_16x16x64_i8 (int8 in, exact int32 accumulate; per-block / per-query scales)"
+                         if int8_keys else
+                         ("v_mfma_f32_16x16x32_bf16" if dims > 384 else "v_mfma_f32_32x32x16_bf16")
+                         + " (bf16 in, fp32 accumulate)")
+                        + ": block keys = per-32-row minima of the approximate distance; every returned "
+                          "distance is the reference-order fp32 value",
+                "bf16_peak_equivalent_frac": achieved / MFMA_BF16_PEAK_TFLOPS,
                 "pipeline_ms": total_avg,
                 "f32_mfma_peak_equivalent_frac": achieved / MFMA_F32_PEAK_TFLOPS,
                 "traffic": args.traffic_bytes,
@@ -640,6 +694,7 @@ def main():
             "dtype": ("u8 codes (v_dot4) + f32 rescoring" if rq_bits == 8 else
                       "u64 codes x 5-bit query planes + f32 rescoring" if rq_bits == 1 else
                       "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else
+                      "f32 (exact result; int8 MFMA block-key filter)" if int8_keys else
                       "f32 (exact result; bf16 MFMA block-key filter)"),
             "data": ("synthetic (counter-based integer U{0..127} generator, seed 1 corpus / 2 queries)" if gen_kind == 1
                      else "synthetic (counter-based U[0,1) generator, seed 1 corpus / 2 queries)" if gen_kind == 2

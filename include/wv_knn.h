@@ -378,7 +378,7 @@ int wv_index_quant_begin(wv_index *idx, const float *d_queries, int64_t nq, int6
                          void *stream);
 /* the largest batch wv_index_quant_begin takes on this shard (larger batches run
  * the protocol per query chunk, the chunk agreed by all ranks) */
-int wv_index_quant_max_batch(wv_index *idx, int64_t *out);
+int wv_index_quant_max_batch(wv_index *idx, int32_t k, int32_t world, int64_t *out);
 int wv_index_quant_blockmin(wv_index *idx, float *d_out, void *stream);
 int wv_index_quant_replay(wv_index *idx, const uint64_t *d_in_ids, const float *d_in_dists, const int32_t *d_in_len,
                           int32_t extract, uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_len, void *stream);

@@ -117,3 +117,26 @@ def test_q8_heavy_tailed_rows_and_forced_replay(wv, oracle, metric):
         for qi in range(len(queries)):
             assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"f{force} q{qi}")
         idx.close()
+
+
+@pytest.mark.parametrize("metric,variant,d,k", [("cosine", "avx256", 768, 10), ("l2-squared", "avx512", 640, 24),
+                                               ("dot", "avx256", 1024, 100), ("cosine", "avx256", 1536, 10)])
+def test_q8_row_filter_equals_bf16_filter_and_unfiltered(wv, oracle, metric, variant, d, k):
+    """The exact pass's row bound from the int8 plane (q8_filter 1, default),
+    from the bf16 plane (q8_filter 0) and no row bound (exact_filter 0): the
+    same results bit for bit, equal to the oracle."""
+    n = 24000
+    data = gen(oracle, 0, 79, n, d)
+    queries = gen(oracle, 0, 80, 256, d)
+    res = []
+    for opts in ({}, {"q8_filter": 0}, {"exact_filter": 0}):
+        idx, orc = build_pair(wv, oracle, metric, variant, data, options=opts)
+        res.append(idx.search_by_vector_batch(queries, k))
+        assert idx.stats()["last_route"] == ROUTE_INT8
+        idx.close()
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    ids, dists, counts = res[0]
+    for qi in range(0, len(queries), 16):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")

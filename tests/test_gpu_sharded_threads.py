@@ -305,7 +305,7 @@ def test_sharded_quant_equals_single_index(wv, oracle, monkeypatch, comp, shards
         backs.append(GpuQuantShardBackend(idx, 0))
     if comp == "pq" and not rescore:  # rank r's distance group holds 37 + 10 r queries: chunks of 37 on every rank
         for r, b in enumerate(backs):
-            b.max_batch = (lambda v: (lambda: v))(37 + 10 * r)
+            b.max_batch = (lambda v: (lambda k, world: v))(37 + 10 * r)
     q = torch.from_numpy(queries).to("cuda")
     out, paths = run_quant_ranks(monkeypatch, backs, q, k, per)
     assert len(set(paths)) == 1, paths

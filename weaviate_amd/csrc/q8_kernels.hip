@@ -30,10 +30,7 @@ namespace {
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 constexpr int Q8_NONE = (int)0x80000000;  // "no valid row" in the integer max
 
-// byte offset of int8 column c of row `row` in a tiled int8 plane of dpb8 columns
-__host__ __device__ __forceinline__ int64_t q8_plane_byte(int64_t row, int c, int dpb8) {
-    return ((row >> 8) * (int64_t)(dpb8 >> 5) + (c >> 5)) * 8192 + ((row & 255) << 5) + (c & 31);
-}
+// (q8_plane_byte: qs_kernels.hip)
 
 template <int OFF>
 __device__ __forceinline__ i32x4_t lds_ld16_o(unsigned base) {

@@ -10,15 +10,18 @@
 void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
                       const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
                       int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
-                      const float* capv, const float4* qinfo) {
+                      const float* capv, const float4* qinfo, const Q8Filter* q8f) {
     // the capped pass filters rows by their bf16-plane bound (k_blk_exact);
     // gacc_r: plane_dot's two-way accumulation of dpb products
     const uint16_t* Xb = idx->qs_planes && idx->exact_filter ? idx->Xb : nullptr;
     const float gd = (float)gamma_n(idx->dpb + 8), gacc_r = (float)gamma_n(idx->dpb + 2);
+    // int8 keys: the row bound from the int8 plane (q8f), else the bf16 plane
+    Q8Filter f8{};
+    if (q8f && Xb) f8 = *q8f;
 #define WV_EXR(RV, M, V)                                                                                             \
     do {                                                                                                             \
-        if (eb) k_blk_exact<RV, M, V, true><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r); \
-        else k_blk_exact<RV, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r); \
+        if (eb) k_blk_exact<RV, M, V, true><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8); \
+        else k_blk_exact<RV, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8); \
     } while (0)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \

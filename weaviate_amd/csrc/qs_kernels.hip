@@ -26,6 +26,20 @@
 #include <type_traits>
 
 namespace wv {
+// the int8 plane of an index whose block keys came from it (k_blk_exact's row
+// filter then bounds rows from the int8 codes); X8 == nullptr: the bf16 plane.
+// External linkage: the exact pass's launcher (qs_exact.hip) takes it.
+struct Q8Filter {
+    const unsigned char* X8;
+    const float* sb8;
+    int dpb8;
+    const unsigned char* Q8;   // the batch's query codes (tiled plane)
+    const float* qscale;
+    const float4* qinfo8;
+    const uint32_t* qmax8;
+    float gacc8;
+};
+
 namespace {  // internal linkage: each runtime unit compiles the kernels it launches
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
@@ -1048,6 +1062,13 @@ __global__ __launch_bounds__(256) void k_blk_gthresh(const float* __restrict__ t
     if (lane == 0) ncand[q] = keep;
 }
 
+// byte offset of int8 column c of row `row` in a tiled int8 plane of dpb8
+// columns: 256-row tiles of 32-byte column chunks (the bf16 plane's tiling,
+// two int8 columns per bf16 element)
+__host__ __device__ __forceinline__ int64_t q8_plane_byte(int64_t row, int c, int dpb8) {
+    return ((row >> 8) * (int64_t)(dpb8 >> 5) + (c >> 5)) * 8192 + ((row & 255) << 5) + (c & 31);
+}
+
 // ---------------------------------------------------------------------------
 // row filter helpers (k_blk_exact, k_blk_replay)
 // ---------------------------------------------------------------------------
@@ -1083,6 +1104,44 @@ __device__ __forceinline__ float plane_a(const uint16_t* __restrict__ Xb, const 
                                          int dpb, const float* sqh, float qn2) {
     const float S = plane_dot(Xb, row, dpb, sqh);
     const float kv = METRIC == L2 ? fmaf(-2.f, S, xn2[row]) : -S;
+    return qs_key_to_a(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, kv, qn2);
+}
+
+// The int8-plane form (q8_kernels.hip layout: 256-row tiles of 32-byte
+// column chunks, lane per row reads contiguous 1 KiB per chunk): the exact
+// int32 dot of the row's codes with the query's (sq8: dpb8 / 4 packed words
+// in LDS), v_dot4_i32_i8.
+__device__ __forceinline__ int plane_dot_q8(const unsigned char* __restrict__ X8, int64_t row, int dpb8,
+                                            const uint32_t* sq8) {
+    int acc = 0;
+    const unsigned char* base = X8 + (row >> 8) * (int64_t)dpb8 * 256 + ((row & 255) << 5);
+#pragma unroll 4
+    for (int c = 0; c < dpb8; c += 32) {
+        const uint4* xp = reinterpret_cast<const uint4*>(base + (int64_t)(c >> 5) * 8192);
+        const uint4 v0 = xp[0], v1 = xp[1];
+        const uint4* qp = reinterpret_cast<const uint4*>(sq8 + (c >> 2));
+        const uint4 a0 = qp[0], a1 = qp[1];
+        acc = __builtin_amdgcn_sdot4((int)v0.x, (int)a0.x, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)v0.y, (int)a0.y, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)v0.z, (int)a0.z, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)v0.w, (int)a0.w, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)v1.x, (int)a1.x, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)v1.y, (int)a1.y, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)v1.z, (int)a1.z, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)v1.w, (int)a1.w, acc, false);
+    }
+    return acc;
+}
+
+// A_row from the int8 plane: k_q8_blockkey's key formula for one row
+// (S = fl(fl(sq sb) float(dot)); L2 fl(xnorm2 - 2 S) in one fma)
+template <int METRIC>
+__device__ __forceinline__ float plane_a_q8(const unsigned char* __restrict__ X8, const float* __restrict__ sb8,
+                                            const float* __restrict__ xn2, int64_t row, int dpb8, const uint32_t* sq8,
+                                            float sq, float qn2) {
+    const float s = sq * sb8[row >> 5];
+    const float Sf = (float)plane_dot_q8(X8, row, dpb8, sq8);
+    const float kv = METRIC == L2 ? fmaf(-2.f * s, Sf, xn2[row]) : -(s * Sf);
     return qs_key_to_a(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, kv, qn2);
 }
 
@@ -1133,12 +1192,13 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
                                                    const float* __restrict__ cap, const float4* __restrict__ qinfo,
                                                    const uint16_t* __restrict__ Xb, int dpb, const float* __restrict__ xn2,
                                                    const uint32_t* __restrict__ qsmax, const uint32_t* __restrict__ maxn2,
-                                                   float gd, float gacc_r) {
+                                                   float gd, float gacc_r, const Q8Filter q8f) {
     constexpr int L = 64 * (R - 1);
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
     __shared__ float sslot[4][64];
     __shared__ __attribute__((aligned(16))) float sqh[EB ? 4 : QS_FILT_DPB];
+    __shared__ __attribute__((aligned(16))) uint32_t sq8[EB ? 4 : QS_FILT_DPB / 4];
     __shared__ float lk[3][L];
     __shared__ uint32_t lid[3][L];
     __shared__ int snv[4];
@@ -1160,8 +1220,18 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     // list never keeps; only the others get the reference-order distance
     const float4 qi = qinfo[q];
     const bool filt = !EB && Xb != nullptr && cap != nullptr && qi.w == 0.f && dpb <= QS_FILT_DPB;
-    float eps_r = 0.f, capq = __builtin_inff();
-    if (filt) {
+    // int8-plane row bound (the keys were int8): half the plane bytes per row
+    const bool f8 = filt && q8f.X8 != nullptr && q8f.dpb8 <= QS_FILT_DPB;
+    float eps_r = 0.f, capq = __builtin_inff(), sqs = 0.f;
+    if (f8) {
+        for (int c4 = 4 * threadIdx.x; c4 < q8f.dpb8; c4 += 1024)
+            sq8[c4 >> 2] = *reinterpret_cast<const uint32_t*>(q8f.Q8 + q8_plane_byte(q, c4, q8f.dpb8));
+        eps_r = qs_eps(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, q8f.qinfo8[q], q8f.qmax8, maxn2, gd,
+                       q8f.gacc8);
+        sqs = q8f.qscale[q];
+        capq = cap[q];
+        __syncthreads();
+    } else if (filt) {
         for (int c = threadIdx.x; c < dpb; c += 256) sqh[c] = (float)(__bf16)(c < d ? qv[c] : 0.f);
         eps_r = qs_eps(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, qi, qsmax, maxn2, gd, gacc_r);
         capq = cap[q];
@@ -1182,7 +1252,8 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         if (EB) {  // its own instantiation: the distance code's registers stay out of the read-back form
             if (ok) e = ebuf[(int64_t)q * ldE + j * 32 + li];
         } else if (filt) {
-            const bool need = ok && plane_a<METRIC>(Xb, xn2, row, dpb, sqh, qi.x) - eps_r < capq;
+            const bool need = ok && (f8 ? plane_a_q8<METRIC>(q8f.X8, q8f.sb8, xn2, row, q8f.dpb8, sq8, sqs, qi.x)
+                                        : plane_a<METRIC>(Xb, xn2, row, dpb, sqh, qi.x)) - eps_r < capq;
             const float dl = coop ? exact8_compact<METRIC>(qv, X, dpad, d, row, need, lane, sslot[w])
                                   : need ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
             if (need) e = dl;

@@ -85,6 +85,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         const float4* qinfo_sel = q8 ? idx->q8Info.as<float4>() : qinfo;
         const uint32_t* qmax_sel = q8 ? idx->qmax8 : idx->qsmax;
         const float gacc_sel = q8 ? gacc8 : gacc;
+        Q8Filter q8f{idx->X8, idx->sb8, idx->dpb8, idx->q8Qb.as<unsigned char>(), idx->q8Scale.as<float>(),
+                     idx->q8Info.as<float4>(), idx->qmax8, gacc8};
         // ---- block keys (the dominant kernel) ----
         QsArgs a;
         a.Xb = reinterpret_cast<const unsigned char*>(idx->Xb);
@@ -221,7 +223,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         const float* capv = (idx->exact_cap && phase == 0) ? idx->qsCap.as<float>() : nullptr;
         auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0) {
             launch_blk_exact(idx, s, RV, metric, v5, Qn, valid, (int)cn, k, kout, o_ids + c0 * kout, o_d + c0 * kout,
-                             o_n + c0, flags, list, cnt, eb, ldE, capv, qinfo);
+                             o_n + c0, flags, list, cnt, eb, ldE, capv, qinfo, q8 && idx->q8_filter ? &q8f : nullptr);
         };
         if (phase != 2) sel(R, nullptr, nullptr, phase == 1 ? topA : nullptr);
         HIPCHK(hipGetLastError());

@@ -1039,12 +1039,24 @@ static int quant_params(const wv_index* idx, int k, int* limit, int* trim, int* 
     return set_err(WV_ERR_UNSUPPORTED, "quant sharding: trained PQ, SQ or RQ indexes only");
 }
 
-// the largest batch wv_index_quant_begin takes on this shard (one 16 GiB distance group)
-extern "C" int wv_index_quant_max_batch(wv_index* idx, int64_t* out) {
+// the largest batch wv_index_quant_begin takes on this shard for k at `world`
+// ranks: one 16 GiB distance group, and at most 2 GiB each for the PQ lookup
+// tables (nq m K floats) and the all-gathered replay records (world ranks x
+// nq x (3 cap + 1) words, cap = 2R + 64), so no rank fails an allocation
+// while the others wait in a collective
+extern "C" int wv_index_quant_max_batch(wv_index* idx, int32_t k, int32_t world, int64_t* out) {
     if (!idx || !out) return set_err(WV_ERR_INVALID, "nil argument");
     std::lock_guard<std::mutex> g(idx->mu);
     const int64_t ld = std::max<int64_t>(round_up(idx->hiwater, EBLK), EBLK);
-    *out = std::max<int64_t>(1, (16ll << 30) / (ld * 4));
+    int64_t mb = (16ll << 30) / (ld * 4);
+    int limit = k, trim = 0, rescore = 0, form = 0;
+    if (k > 0 && quant_params(idx, k, &limit, &trim, &rescore, &form) == WV_OK) {
+        const int64_t cap = 2ll * limit + 64;
+        mb = std::min<int64_t>(mb, (2ll << 30) / ((int64_t)std::max(world, 1) * (3 * cap + 1) * 4));
+        if (idx->compression == WV_COMPRESSION_PQ && idx->pq_m > 0 && idx->pq_ks > 0)
+            mb = std::min<int64_t>(mb, (2ll << 30) / ((int64_t)idx->pq_m * idx->pq_ks * 4));
+    }
+    *out = std::max<int64_t>(1, mb);
     return WV_OK;
 }
 

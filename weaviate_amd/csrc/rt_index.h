@@ -132,6 +132,7 @@ struct wv_index {
     int q8_planes = 0, dpb8 = 0;
     int q8_opt = 1;                 // option q8: block keys from the int8 plane (1) or the bf16 plane (0)
     int q8_R = 0;                   // option q8_R: candidate lists for int8 keys (0: one level above qs_R)
+    int q8_filter = 1;              // option q8_filter: the exact pass bounds rows from the int8 plane (1) or bf16 (0)
     unsigned char* X8 = nullptr;
     float* sb8 = nullptr;
     uint32_t* qmax8 = nullptr;      // device [4]: max |x - x^|^2, max |x^|^2 (float bits)
@@ -245,7 +246,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
 void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
                       const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
                       int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
-                      const float* capv, const float4* qinfo);
+                      const float* capv, const float4* qinfo, const Q8Filter* q8f);
 void launch_exact_bm(wv_index* idx, hipStream_t s, int metric, bool v5, const float* Qn, int64_t nb, size_t bm_lds,
                      int64_t ldE);
 // qs_replay.hip

@@ -683,6 +683,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     }
     else if (k == "sel_dbg") idx->sel_dbg = (int)value;
     else if (k == "q8") idx->q8_opt = value ? 1 : 0;  // int8 block keys (default 1) or bf16 (0)
+    else if (k == "q8_filter") idx->q8_filter = value ? 1 : 0;  // int8 keys: row bound from the int8 plane (1) or bf16 (0)
     else if (k == "q8_R") {
         if (value != 0 && value != 2 && value != 4 && value != 8) return set_err(WV_ERR_INVALID, "q8_R must be 0, 2, 4 or 8");
         idx->q8_R = (int)value;

@@ -362,10 +362,12 @@ class GpuQuantShardBackend(GpuShardBackend):
         self.R, self.nblk, self.rescore, self.form = int(out[0]), int(out[1]), bool(out[2]), int(out[3])
         return self.R
 
-    def max_batch(self) -> int:
+    def max_batch(self, k: int, world: int) -> int:
+        """Queries per quant_begin on this shard: its distance group, LUT and
+        the all-gathered replay records all fit (wv_index_quant_max_batch)."""
         import ctypes
         out = ctypes.c_int64()
-        self._check(self._l.wv_index_quant_max_batch(self.index._h, ctypes.addressof(out)))
+        self._check(self._l.wv_index_quant_max_batch(self.index._h, int(k), int(world), ctypes.addressof(out)))
         return int(out.value)
 
     def quant_bounds(self):
@@ -466,7 +468,7 @@ class ShardedQuantSearch:
         mb = getattr(self.b, "max_batch", None)
         chunk = nq
         if mb is not None:
-            t = torch.tensor([min(int(mb()), nq)], dtype=torch.int64, device=self.dev)
+            t = torch.tensor([min(int(mb(k, self.world)), nq)], dtype=torch.int64, device=self.dev)
             if self.world > 1:
                 dist.all_reduce(t, op=ReduceOp.MIN)
             chunk = max(1, int(t.item()))
