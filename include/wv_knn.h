@@ -437,6 +437,8 @@ typedef struct wv_stats {
 #define WV_ROUTE_QS_INT8 3   /* k_q8_blockkey (int8 block keys, 384 < d <= 1536) */
 #define WV_ROUTE_F32_SELECT 4 /* k_mfma_select3 (f32 MFMA select) */
 #define WV_ROUTE_GEMV 5      /* k_gemv_select (HBM-streaming GEMV, small batches) */
+#define WV_ROUTE_BQ_INT8 6   /* BQ block minima: k_q8_blockkey over +-1 code planes (integer MFMA) */
+#define WV_ROUTE_BQ_VALU 7   /* BQ block minima: k_bq_blockmin_lds / k_bq_blockmin (xor + popcount) */
 int wv_index_stats(wv_index *idx, wv_stats *out);
 
 /* Diagnostic hook (tests): the last MFMA batch's candidates [nq][KP]:
@@ -450,6 +452,11 @@ int wv_index_debug_candidates(wv_index *idx, float *A, float *E, uint32_t *I, fl
  * (A space, +inf for a block without a valid row) into A[*nb] and its error
  * bound eps(q).  Call with A == NULL to read *nb only. */
 int wv_index_debug_blockkeys(wv_index *idx, int64_t q, float *A, float *eps, int64_t *nb);
+
+/* Diagnostic hook (tests) of the BQ search: query q of the last BQ batch (one
+ * query group): the minimum hamming distance of every 256-row block
+ * (+inf without a valid row) into mins[*nblk].  mins == NULL: *nblk only. */
+int wv_index_debug_bqmin(wv_index *idx, int64_t q, float *mins, int64_t *nblk);
 
 /* tuning / testing knobs: "margin" (extra candidates of the f32 select
  * kernel, default 8), "force_replay" (1 = resolve every query by heap

@@ -140,3 +140,93 @@ def test_q8_row_filter_equals_bf16_filter_and_unfiltered(wv, oracle, metric, var
     ids, dists, counts = res[0]
     for qi in range(0, len(queries), 16):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")
+
+
+@pytest.mark.parametrize("metric,kind,d,k", [("cosine", 0, 768, 10), ("l2-squared", 1, 512, 100), ("dot", 0, 640, 10)])
+def test_q8_staggered_epilogue_same_keys(wv, oracle, metric, kind, d, k):
+    """q8_stag 1 (waves 4-7 reduce each block late) writes the same block keys
+    as the in-order schedule: identical results and block keys, both equal to
+    the oracle; corpus sizes that end mid-slot and mid-span."""
+    n = 20000 + 37
+    data = gen(oracle, kind, 81, n, d)
+    queries = gen(oracle, kind, 82, 300, d)
+    res, keys = [], []
+    for stag in (0, 1):
+        idx, orc = build_pair(wv, oracle, metric, "avx256", data, options={"q8_stag": stag})
+        res.append(idx.search_by_vector_batch(queries, k))
+        assert idx.stats()["last_route"] == ROUTE_INT8
+        keys.append([idx.debug_blockkeys(q)[0] for q in (0, 255, 299)])
+        idx.close()
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    for a, b in zip(keys[0], keys[1]):
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    ids, dists, counts = res[1]
+    for qi in range(0, len(queries), 10):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")
+
+
+# ---------------------------------------------------------------------------
+# BQ block minima on the integer matrix cores (k_q8_blockkey<..., BQ> over
+# +-1 code planes): hamming = (64 words - sum s_q s_x) / 2, exact
+# ---------------------------------------------------------------------------
+ROUTE_BQ_INT8, ROUTE_BQ_VALU = 6, 7
+
+
+@pytest.mark.parametrize("metric,kind,n,d,k,rescore", [
+    ("cosine", 0, 20000, 1536, 10, 200),   # C4 width: 24 words, one block per ring slot
+    ("l2-squared", 0, 9000, 1000, 10, 64),  # 16 words, zero-padded columns 1024..
+    ("dot", 0, 12000, 768, 5, 37),         # 12 words, two blocks per slot
+    ("cosine", 1, 6000, 450, 10, 50),      # 8 words; all-positive data: every code 0, ties everywhere
+    ("l2-squared", 2, 5000 + 77, 1100, 20, 20),  # 18 words, ragged corpus
+])
+def test_bq_int8_minima_equal_valu_and_oracle(wv, oracle, metric, kind, n, d, k, rescore):
+    from test_gpu_flat import build_bq_pair
+    data = gen(oracle, kind, 83, n, d)
+    queries = gen(oracle, kind, 84, 300, d)
+    idx, orc = build_bq_pair(wv, oracle, metric, "avx256", data, rescore)
+    got = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] == ROUTE_BQ_INT8
+    mins = [idx.debug_bqmin(q) for q in (0, 150, 299)]
+    idx.set_option("bq8", 0)
+    ref = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] == ROUTE_BQ_VALU
+    for q, m in zip((0, 150, 299), mins):
+        np.testing.assert_array_equal(m, idx.debug_bqmin(q), err_msg=f"block minima q{q}")
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    for q in range(0, len(queries), 12):
+        assert_same(orc.search(queries[q], k), got[0][q, :got[2][q]], got[1][q, :got[2][q]], f"bq {metric} q{q}")
+    idx.close()
+
+
+def test_bq_int8_deletes_allow_upserts(wv, oracle):
+    """Deleted rows, whole deleted 256-row blocks, upserts and allow lists: the
+    +-1 plane follows the codes, the minima equal the VALU kernel's."""
+    from test_gpu_flat import build_bq_pair
+    n, d, k = 9000, 768, 10
+    data = gen(oracle, 0, 85, n, d)
+    idx, orc = build_bq_pair(wv, oracle, "cosine", "avx512", data, 64)
+    dele = np.concatenate([np.arange(0, n, 7), np.arange(512, 1024)]).astype(np.uint64)
+    idx.delete(*dele)
+    orc.delete(dele)
+    up = gen(oracle, 0, 86, 300, d)
+    upids = np.arange(2000, 2300, dtype=np.uint64)
+    idx.add_batch(upids, up)
+    orc.add_batch(upids, up)
+    queries = gen(oracle, 0, 87, 64, d)
+    allow = np.arange(50, 7000, 3, dtype=np.uint64)
+    for al in (None, wv.AllowList(allow)):
+        got = idx.search_by_vector_batch(queries, k, allow=al)
+        assert idx.stats()["last_route"] == ROUTE_BQ_INT8
+        m0 = idx.debug_bqmin(5)
+        idx.set_option("bq8", 0)
+        ref = idx.search_by_vector_batch(queries, k, allow=al)
+        np.testing.assert_array_equal(m0, idx.debug_bqmin(5))
+        idx.set_option("bq8", 1)
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+        for q in range(0, len(queries), 8):
+            exp = orc.search(queries[q], k, allow=allow if al is not None else None)
+            assert_same(exp, got[0][q, :got[2][q]], got[1][q, :got[2][q]], f"q{q}")
+    idx.close()

@@ -67,7 +67,7 @@ class WvStats(C.Structure):
 
 
 # wv_stats.last_route (include/wv_knn.h WV_ROUTE_*)
-ROUTES = {0: "none", 1: "qs_bf16", 2: "qs_w4", 3: "qs_int8", 4: "f32_select", 5: "gemv"}
+ROUTES = {0: "none", 1: "qs_bf16", 2: "qs_w4", 3: "qs_int8", 4: "f32_select", 5: "gemv", 6: "bq_int8", 7: "bq_valu"}
 
 
 P = C.c_void_p
@@ -127,6 +127,7 @@ SIGNATURES = {
     "wv_index_quant_begin": (C.c_int, [P, P, i64, i64, i32, P, P]),
     "wv_index_quant_blockmin": (C.c_int, [P, P, P]),
     "wv_index_quant_max_batch": (C.c_int, [P, i32, i32, P]),
+    "wv_index_debug_bqmin": (C.c_int, [P, i64, P, P]),
     "wv_index_quant_replay": (C.c_int, [P, P, P, P, i32, P, P, P, P]),
     "wv_index_quant_replay_record": (C.c_int, [P, P, P, P, i32, P, P, P, P]),
     "wv_index_quant_finish": (C.c_int, [P, P, P, P, P, P, P, P, P, P]),

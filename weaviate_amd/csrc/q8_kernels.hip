@@ -175,6 +175,7 @@ struct Q8Args {
     int slots_per_span;
     int nspans;
     int nqg;                   // query groups of 256
+    int bq_bits;               // BQ: code bits 64 * words (hamming = (bq_bits - dot) / 2)
 };
 
 // ---------------------------------------------------------------------------
@@ -190,7 +191,17 @@ struct Q8Args {
 // or after the slot; the cross-lane combine + key store of a slot's last
 // block is deferred into the next slot.  One barrier per slot.
 // ---------------------------------------------------------------------------
-template <int NC, int RB, bool ISL2>
+// STAG (RB = 2): waves 4-7 -- each the SIMD partner of wave w - 4 -- run every
+// block's reduction P0 chunks into the next block instead of right after it
+// (MI355X_MICROARCH.md, two waves per SIMD, item 9: a stagger), so the two
+// waves of a SIMD do not issue their epilogue VALU at the same time.
+//
+// BQ (bq_kernels.hip's block minima on the matrix cores): X8 / Q8 are the
+// codes unpacked to +-1 (bit 0 -> +1, bit 1 -> -1; columns past the code bits
+// 0), so sum s_q s_x = bq_bits - 2 hamming exactly in int32; the kernel writes
+// the minimum hamming distance of every 256-row block (8 consecutive 32-row
+// blocks: the spans are whole 256-row blocks), +inf without a valid row.
+template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false>
 __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     constexpr int NPB = 2 * NC;                     // 1 KiB pieces per 32-row block
     constexpr int SLOT = RB * NPB * 1024;           // bytes per ring slot
@@ -201,6 +212,8 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     constexpr int NT = RB * NC;                     // chunks per slot
     constexpr int P0 = P + 2 + (ISL2 ? 1 : 0);      // vector-memory ops per group, per wave
     static_assert(P0 < NC, "the deferred key store must follow the slot's DMA pieces");
+    static_assert(!STAG || RB == 2, "the stagger defers a slot's second block");
+    static_assert(!BQ || (!ISL2 && !STAG), "BQ: integer maxima, in-order schedule");
     constexpr int X0 = 1;                           // chunk of the slot's extra LDS reads
     constexpr int XE = 2 + (ISL2 ? 2 * RB : 0);     // extra reads: valid words, scales (+ norms)
     constexpr int NBUF = 3;
@@ -230,8 +243,8 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
                 Qf[2 * c + n] = *reinterpret_cast<const i32x4_t*>(qp + (2 * c) * 8192 + n * 16 * 32);
     }
     const int64_t q0 = (int64_t)grp * 256 + wave * 32;
-    const float sqA = a.qscale[q0 + (lane & 15)];
-    const float sqB = a.qscale[q0 + 16 + (lane & 15)];
+    const float sqA = BQ ? 1.f : a.qscale[q0 + (lane & 15)];
+    const float sqB = BQ ? 1.f : a.qscale[q0 + 16 + (lane & 15)];
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the query loads before the DMA ring
 
     const int64_t s0 = (int64_t)span * a.slots_per_span;
@@ -316,8 +329,72 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         // lanes 0-15: queries j (n = 0) in m0, 16 + j in m1 -> lanes 16-31 take m1
         const auto c01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m1), false, false);
         const float m = __uint_as_float(c01[0]);
-        if (lane < 32) krow[gb] = ISL2 ? m : -m;
+        if constexpr (BQ) {
+            if (lane < 32) krow[gb] = m == -__builtin_inff() ? __builtin_inff() : 0.5f * ((float)a.bq_bits - m);
+        } else {
+            if (lane < 32) krow[gb] = ISL2 ? m : -m;
+        }
     };
+    // BQ: the running per-lane maxima over the current 256-row block, and
+    // whether the slot's last block completed one (its finish is deferred)
+    float run0 = -__builtin_inff(), run1 = -__builtin_inff();
+    bool pend = false;
+    // stores issued in slot t (the deferred finish + block 0's), for vmcnt
+    auto stores_in = [&](int t) -> int {
+        if constexpr (BQ) return (t > 0 && ((((s0 + t - 1) * RB + RB - 1) & 7) == 7)) ? 1 : 0;
+        else return (t > 0 ? 1 : 0) + RB - 1;
+    };
+    // a block's reduction over its rows (accumulators ac, valid word vw_, scale
+    // sb_, L2 norms xa_/xb_) -> the lane's partial keys (p0, p1)
+    auto reduce = [&](const i32x4_t (&ac)[2][2], uint32_t vw_, float sb_, const f32x4_t& xa_, const f32x4_t& xb_,
+                      float& p0, float& p1) {
+        const uint32_t vw = __builtin_amdgcn_readfirstlane(vw_);
+        const float sbf = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sb_)));
+        // ac[m][n][r] is row 16m + 4g + r (g = lane>>4) of query 16n + (lane&15)
+        const uint32_t vl = vw >> (4 * ((lane >> 4) & 3));
+        const float s0f = sqA * sbf, s1f = sqB * sbf;
+        float mn[2];
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            if constexpr (ISL2) {
+                const float cn = -2.f * (n ? s1f : s0f);
+                float m = __builtin_inff();
+#pragma unroll
+                for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float v = fmaf(cn, (float)ac[mm][n][r], mm ? xb_[r] : xa_[r]);
+                        m = fminf(m, ((vl >> (16 * mm + r)) & 1u) ? v : __builtin_inff());
+                    }
+                mn[n] = m;
+            } else {
+                int mi;
+                if (vw == 0xFFFFFFFFu) {
+                    mi = max(max(max(ac[0][n][0], ac[0][n][1]), max(ac[0][n][2], ac[0][n][3])),
+                             max(max(ac[1][n][0], ac[1][n][1]), max(ac[1][n][2], ac[1][n][3])));
+                } else {
+                    mi = Q8_NONE;
+#pragma unroll
+                    for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++)
+                            mi = max(mi, ((vl >> (16 * mm + r)) & 1u) ? ac[mm][n][r] : Q8_NONE);
+                }
+                // the scale is positive: the largest S is the largest product
+                if constexpr (BQ) mn[n] = mi == Q8_NONE ? -__builtin_inff() : (float)mi;
+                else mn[n] = mi == Q8_NONE ? -__builtin_inff() : (n ? s1f : s0f) * (float)mi;
+            }
+        }
+        p0 = mn[0];
+        p1 = mn[1];
+    };
+    i32x4_t acc[RB][2][2];
+    // STAG, waves 4-7: the previous slot's last block is reduced late, from its
+    // accumulators (kept: acc[1] is rewritten only from chunk NC on) and these
+    const bool late = STAG && wave >= 4;
+    uint32_t dvw = 0;
+    float dsb = 0.f;
+    f32x4_t dxa = {0.f, 0.f, 0.f, 0.f}, dxb = {0.f, 0.f, 0.f, 0.f};
     int cur = 0;
     for (int t = 0; t < nsteps; t++) {
         const int nxt = cur == NBUF - 1 ? 0 : cur + 1;
@@ -325,52 +402,13 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         const unsigned sbase = ring + (unsigned)(cur * SLOT) + l16;
         const bool dma = t + 2 < nsteps;
         const unsigned sm = (unsigned)(t & 3);
-        i32x4_t acc[RB][2][2];
         uint2 vwv;
         float2 sbv;
         f32x4_t xa[RB], xb[RB];
-        // a block's reduction over its rows -> the lane's partial keys (p0, p1)
-        auto reduce = [&](auto rbc, float& p0, float& p1) {
-            constexpr int rb = decltype(rbc)::value;
-            const uint32_t vw = __builtin_amdgcn_readfirstlane(rb == 0 ? vwv.x : vwv.y);
-            const float sbf = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rb == 0 ? sbv.x : sbv.y)));
-            // acc[rb][m][n][r] is row 16m + 4g + r (g = lane>>4) of query 16n + (lane&15)
-            const uint32_t vl = vw >> (4 * ((lane >> 4) & 3));
-            const float s0f = sqA * sbf, s1f = sqB * sbf;
-            float mn[2];
+        if constexpr (!ISL2) {
 #pragma unroll
-            for (int n = 0; n < 2; n++) {
-                if constexpr (ISL2) {
-                    const float cn = -2.f * (n ? s1f : s0f);
-                    float m = __builtin_inff();
-#pragma unroll
-                    for (int mm = 0; mm < 2; mm++)
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            const float v = fmaf(cn, (float)acc[rb][mm][n][r], mm ? xb[rb][r] : xa[rb][r]);
-                            m = fminf(m, ((vl >> (16 * mm + r)) & 1u) ? v : __builtin_inff());
-                        }
-                    mn[n] = m;
-                } else {
-                    int mi;
-                    if (vw == 0xFFFFFFFFu) {
-                        mi = max(max(max(acc[rb][0][n][0], acc[rb][0][n][1]), max(acc[rb][0][n][2], acc[rb][0][n][3])),
-                                 max(max(acc[rb][1][n][0], acc[rb][1][n][1]), max(acc[rb][1][n][2], acc[rb][1][n][3])));
-                    } else {
-                        mi = Q8_NONE;
-#pragma unroll
-                        for (int mm = 0; mm < 2; mm++)
-#pragma unroll
-                            for (int r = 0; r < 4; r++)
-                                mi = max(mi, ((vl >> (16 * mm + r)) & 1u) ? acc[rb][mm][n][r] : Q8_NONE);
-                    }
-                    // the scale is positive: the largest S is the largest product
-                    mn[n] = mi == Q8_NONE ? -__builtin_inff() : (n ? s1f : s0f) * (float)mi;
-                }
-            }
-            p0 = mn[0];
-            p1 = mn[1];
-        };
+            for (int r = 0; r < RB; r++) xa[r] = xb[r] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
         static_for<0, NT>([&](auto ttc) {
             constexpr int tt = decltype(ttc)::value;
             constexpr int rb = tt / NC, c = tt % NC;
@@ -421,26 +459,62 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             }
             // the previous slot's last block: cross-lane combine + key store
             if constexpr (tt == P0) {
-                if (t > 0) finish(mp0, mp1, gbp);
+                if (BQ ? pend : t > 0) {
+                    if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
+                    finish(mp0, mp1, gbp);
+                }
             }
             // RB = 2: block 0 is reduced and stored beside block 1's MFMAs
+            // (BQ: folded into the 256-row block's maxima, never its last)
             if constexpr (RB == 2 && tt == NC + 1) {
-                float p0, p1;
-                reduce(std::integral_constant<int, 0>{}, p0, p1);
-                finish(p0, p1, (s0 + t) * RB);
+                if (!late) {
+                    float p0, p1;
+                    reduce(acc[0], vwv.x, sbv.x, xa[0], xb[0], p0, p1);
+                    if constexpr (BQ) {
+                        run0 = fmaxf(run0, p0);
+                        run1 = fmaxf(run1, p1);
+                    } else {
+                        finish(p0, p1, (s0 + t) * RB);
+                    }
+                }
+            }
+            if constexpr (STAG && tt == NC + P0) {
+                if (late) {
+                    float p0, p1;
+                    reduce(acc[0], vwv.x, sbv.x, xa[0], xb[0], p0, p1);
+                    finish(p0, p1, (s0 + t) * RB);
+                }
             }
         });
-        reduce(std::integral_constant<int, RB - 1>{}, mp0, mp1);
+        if (late) {
+            dvw = vwv.y;
+            dsb = sbv.y;
+            dxa = xa[RB - 1];
+            dxb = xb[RB - 1];
+        } else {
+            reduce(acc[RB - 1], RB == 2 ? vwv.y : vwv.x, RB == 2 ? sbv.y : sbv.x, xa[RB - 1], xb[RB - 1], mp0, mp1);
+        }
         gbp = (s0 + t) * RB + RB - 1;
+        if constexpr (BQ) {
+            run0 = fmaxf(run0, mp0);
+            run1 = fmaxf(run1, mp1);
+            pend = (gbp & 7) == 7;
+            if (pend) {
+                mp0 = run0;
+                mp1 = run1;
+                run0 = run1 = -__builtin_inff();
+                gbp >>= 3;
+            }
+        }
         // ---- end of the slot: the next group must have landed (every wave) ----
         if (t + 1 < nsteps) {
             // this wave's vector-memory ops after group t+1, in issue order: the
             // stores of slot t-1, the pieces of group t+2, the stores of slot t
             // (RB per slot; slot 0 has RB - 1)
-            if (t >= 2 && t + 2 < nsteps) {
+            if (!BQ && t >= 2 && t + 2 < nsteps) {
                 qs_wait_vm_c<2 * RB + P0>();
             } else {
-                const int y = (t == 0 ? RB - 1 : (t == 1 ? RB - 1 : RB) + RB) + (t + 2 < nsteps ? P0 : 0);
+                const int y = (t >= 1 ? stores_in(t - 1) : 0) + stores_in(t) + (t + 2 < nsteps ? P0 : 0);
                 qs_wait_vm(y);
             }
             __builtin_amdgcn_s_barrier();  // slot t is free; slot t+1 has landed for every wave
@@ -451,7 +525,31 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         }
         cur = nxt;
     }
-    if (nsteps > 0) finish(mp0, mp1, gbp);
+    if (nsteps > 0 && (!BQ || pend)) {
+        if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
+        finish(mp0, mp1, gbp);
+    }
+}
+
+// BQ codes unpacked to +-1 int8 for k_q8_blockkey<..., BQ>: bit b of word w
+// (column 64 w + b) -> -1 if set, +1 if not; columns >= 64 * words -> 0.
+// Corpus rows (listed slots or [0, n)) from the word-major store codes[w * ccap
+// + slot]; thread per (row, 4 columns).
+__global__ void k_bq_unpack8(const uint64_t* __restrict__ codes, int64_t ccap, int words, int64_t n,
+                             const uint32_t* __restrict__ slots, int dpb8, unsigned char* __restrict__ X8) {
+    const int nw4 = dpb8 >> 2;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * nw4) return;
+    const int64_t r = i / nw4;
+    const int c4 = (int)(i % nw4) * 4;
+    const int64_t slot = slots ? (int64_t)slots[r] : r;
+    uint32_t word = 0;
+    if (c4 < 64 * words) {
+        const uint64_t bits = codes[(int64_t)(c4 >> 6) * ccap + slot] >> (c4 & 63);
+#pragma unroll
+        for (int e = 0; e < 4; e++) word |= (((bits >> e) & 1ull) ? 0xFFu : 0x01u) << (8 * e);
+    }
+    *reinterpret_cast<uint32_t*>(X8 + q8_plane_byte(slot, c4, dpb8)) = word;
 }
 
 }  // namespace

@@ -153,16 +153,18 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     } while (0)
 #define WV_QSWN(L2V)                                   \
     if (NK == 64) WV_QSW(64, L2V, 4); else WV_QSW(96, L2V, 3);
-#define WV_Q8(NCV, RBV, L2V)                                                                                   \
+#define WV_Q8S(NCV, RBV, L2V, STV)                                                                             \
     do {                                                                                                       \
-        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, RBV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-        k_q8_blockkey<NCV, RBV, L2V><<<grid, 512, lds, s>>>(q8a);                                               \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, RBV, L2V, STV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey<NCV, RBV, L2V, STV><<<grid, 512, lds, s>>>(q8a);                                          \
     } while (0)
+#define WV_Q8(NCV, RBV, L2V) WV_Q8S(NCV, RBV, L2V, false)
+#define WV_Q8T(NCV, L2V) do { if (idx->q8_stag) WV_Q8S(NCV, 2, L2V, true); else WV_Q8S(NCV, 2, L2V, false); } while (0)
 #define WV_Q8N(L2V)                                    \
     switch (NC8) {                                     \
-    case 8: WV_Q8(8, 2, L2V); break;                   \
-    case 10: WV_Q8(10, 2, L2V); break;                 \
-    case 12: WV_Q8(12, 2, L2V); break;                 \
+    case 8: WV_Q8T(8, L2V); break;                     \
+    case 10: WV_Q8T(10, L2V); break;                   \
+    case 12: WV_Q8T(12, L2V); break;                   \
     case 16: WV_Q8(16, 1, L2V); break;                 \
     case 20: WV_Q8(20, 1, L2V); break;                 \
     default: WV_Q8(24, 1, L2V); break;                 \
@@ -204,6 +206,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
 #undef WV_QSWN
 #undef WV_QSW
 #undef WV_Q8N
+#undef WV_Q8T
+#undef WV_Q8S
 #undef WV_Q8
         HIPCHK(hipGetLastError());
         if (time_it) { HIPCHK(hipEventRecord(idx->ev1, s)); idx->timed = 1; }

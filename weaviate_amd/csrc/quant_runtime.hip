@@ -47,9 +47,72 @@ static int bq_begin(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t n
     constexpr int QPB = 16;
     *G_out = std::max<int64_t>(QPB, std::min<int64_t>(round_up(nq, QPB), ((1ll << 30) / (nblk * 4)) / QPB * QPB));
     *R_out = R;
-    HIPCHK(idx->bqmin.ensure((size_t)(*G_out) * nblk * sizeof(float)));
+    // the integer-MFMA minima write whole 256-query groups
+    HIPCHK(idx->bqmin.ensure((size_t)round_up(*G_out, 256) * nblk * sizeof(float)));
     idx->bq_nq = nq;
     idx->bq_R = R;
+    return WV_OK;
+}
+
+// the block minima on the integer matrix cores: the +-1 planes of the codes
+// (k_bq_unpack8) through k_q8_blockkey<..., BQ>; hamming = (64 words - dot) / 2
+static bool bq8_route(const wv_index* idx) { return idx->bq8 != nullptr && idx->bq8_opt && idx->bq_kernel != 1; }
+
+static int bq_blockmin_i8(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t g0, int F, int64_t nblk,
+                          float* bm) {
+    const int dpb8 = idx->dpb8b;
+    const int NC = dpb8 / 64;
+    const int RB = dpb8 <= 768 ? 2 : 1;
+    const int64_t Fp = round_up(F, 256);
+    HIPCHK(idx->q8Qb.ensure((size_t)Fp * dpb8));
+    HIPCHK(hipMemsetAsync(idx->q8Qb.p, 0, (size_t)Fp * dpb8, s));
+    {
+        const int64_t nu = (int64_t)F * (dpb8 / 4);
+        k_bq_unpack8<<<(unsigned)((nu + 255) / 256), 256, 0, s>>>(idx->qcodes.as<uint64_t>() + g0, idx->bq_nq, idx->words,
+                                                                  F, nullptr, dpb8, idx->q8Qb.as<unsigned char>());
+    }
+    Q8Args a;
+    a.X8 = idx->bq8;
+    a.sb = reinterpret_cast<const float*>(valid);  // any readable [nblocks] array: BQ has no scales
+    a.xnorm2 = nullptr;
+    a.valid = valid;
+    a.Q8 = idx->q8Qb.as<unsigned char>();
+    a.qscale = nullptr;
+    a.key = bm;
+    a.ldk = nblk;
+    a.bq_bits = 64 * idx->words;
+    const int64_t steps_per_blk = 8 / RB;  // ring steps per 256-row block
+    a.nslots = nblk * steps_per_blk;
+    a.nqg = (int)(Fp / 256);
+    // spans of whole 256-row blocks, whole rounds of one workgroup per CU
+    int64_t nspans = 256 / std::gcd((int64_t)256, (int64_t)a.nqg);
+    while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
+    {   // a span's plane bytes below 4 GiB (32-bit buffer offsets)
+        const int64_t max_blk = ((1ll << 32) - 2 * 256ll * dpb8) / (256ll * dpb8);
+        nspans = std::max<int64_t>(nspans, (nblk + max_blk - 1) / max_blk);
+    }
+    nspans = std::max<int64_t>(1, std::min<int64_t>(nspans, nblk));
+    const int64_t bps = (nblk + nspans - 1) / nspans;  // 256-row blocks per span
+    a.slots_per_span = (int)(bps * steps_per_blk);
+    a.nspans = (int)((nblk + bps - 1) / bps);
+    const size_t lds = (size_t)3 * RB * 2 * NC * 1024 + 1024;
+    dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
+#define WV_BQ8(NCV, RBV)                                                                                        \
+    do {                                                                                                        \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, RBV, false, false, true>,                    \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                      \
+        k_q8_blockkey<NCV, RBV, false, false, true><<<grid, 512, lds, s>>>(a);                                  \
+    } while (0)
+    switch (NC) {
+    case 8: WV_BQ8(8, 2); break;
+    case 10: WV_BQ8(10, 2); break;
+    case 12: WV_BQ8(12, 2); break;
+    case 16: WV_BQ8(16, 1); break;
+    case 20: WV_BQ8(20, 1); break;
+    default: WV_BQ8(24, 1); break;
+    }
+#undef WV_BQ8
+    HIPCHK(hipGetLastError());
     return WV_OK;
 }
 
@@ -75,6 +138,14 @@ static int bq_blockmin(wv_index* idx, hipStream_t s, const uint32_t* valid, int6
     if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
     const uint64_t* qc = idx->qcodes.as<uint64_t>();
     float* bm = idx->bqmin.as<float>();
+    if (bq8_route(idx)) {
+        int rc = bq_blockmin_i8(idx, s, valid, g0, F, nblk, bm);
+        if (rc) return rc;
+        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
+        idx->stats.last_route = WV_ROUTE_BQ_INT8;
+        return WV_OK;
+    }
+    idx->stats.last_route = WV_ROUTE_BQ_VALU;
     {
         if (nw == 0) {
             dim3 grid((unsigned)nblk, (unsigned)((F + QPB - 1) / QPB));
@@ -192,6 +263,8 @@ int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
     HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
     HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
     HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
+    idx->bq_last_nq = G >= nq ? nq : 0;  // debug hook: a one-group batch's minima stay in bqmin
+    idx->bq_last_nblk = std::max<int64_t>((idx->hiwater + BQBLK - 1) / BQBLK, 1);
     for (int64_t g0 = 0; g0 < nq; g0 += G) {
         const int F = (int)std::min<int64_t>(G, nq - g0);
         rc = bq_blockmin(idx, s, valid, g0, F);
@@ -211,6 +284,20 @@ int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
         hipEventElapsedTime(&ms, idx->ev0, idx->ev1);
         idx->stats.last_select_ms = ms;
     }
+    return WV_OK;
+}
+
+extern "C" int wv_index_debug_bqmin(wv_index* idx, int64_t q, float* mins, int64_t* nblk) {
+    if (!idx || !nblk) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->compression != WV_COMPRESSION_BQ || idx->bq_last_nq <= 0 || q < 0 || q >= idx->bq_last_nq)
+        return set_err(WV_ERR_INVALID, "debug_bqmin: no such query in the last BQ batch's first group");
+    *nblk = idx->bq_last_nblk;
+    if (!mins) return WV_OK;
+    HIPCHK(hipStreamSynchronize(idx->stream));
+    HIPCHK(hipMemcpy(mins, idx->bqmin.as<float>() + q * idx->bq_last_nblk, (size_t)idx->bq_last_nblk * sizeof(float),
+                     hipMemcpyDeviceToHost));
     return WV_OK;
 }
 

@@ -67,6 +67,10 @@ static void set_dims(wv_index* idx, int64_t d) {
     // 256-column multiples above (one block per slot), <= 48 KiB per slot
     idx->dpb8 = (int)(d <= 768 ? round_up(d, 128) : round_up(d, 256));
     idx->q8_planes = (idx->qs_planes && d > 384 && idx->dpb8 <= 1536) ? 1 : 0;
+    if (idx->compression == WV_COMPRESSION_BQ) {  // +-1 code plane: 7..24 words (448..1536 bits)
+        const int w = (int)((d + 63) / 64), bits = 64 * w;
+        idx->dpb8b = (w >= 7 && w <= 24) ? (int)(bits <= 768 ? round_up(bits, 128) : round_up(bits, 256)) : 0;
+    }
 }
 
 extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
@@ -158,6 +162,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->Xb) hipFree(idx->Xb);
     if (idx->qsmax) hipFree(idx->qsmax);
     if (idx->X8) hipFree(idx->X8);
+    if (idx->bq8) hipFree(idx->bq8);
     if (idx->sb8) hipFree(idx->sb8);
     if (idx->qmax8) hipFree(idx->qmax8);
     if (idx->qscount) hipFree(idx->qscount);
@@ -195,6 +200,7 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     uint16_t* xb = nullptr;
     unsigned char* x8 = nullptr;
     float* sb8 = nullptr;
+    unsigned char* b8 = nullptr;
     void* rqc = nullptr;
     float4* rqm = nullptr;
     uint32_t* pc = nullptr;
@@ -214,6 +220,8 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     WV_STEP("xnorm2", alloc((void**)&xn, (size_t)nc * sizeof(float)));
     WV_STEP("present", alloc((void**)&pr, (size_t)(nc / 32) * sizeof(uint32_t)));
     if (idx->compression == WV_COMPRESSION_BQ) WV_STEP("bq codes", alloc((void**)&cd, (size_t)words * nc * sizeof(uint64_t)));
+    if (idx->compression == WV_COMPRESSION_BQ && idx->dpb8b > 0)
+        WV_STEP("bq +-1 plane", alloc((void**)&b8, (size_t)nc * idx->dpb8b));
     if (idx->qs_planes) WV_STEP("bf16 block-key plane", alloc((void**)&xb, qs_b));
     if (idx->q8_planes) {
         WV_STEP("int8 block-key plane", alloc((void**)&x8, (size_t)nc * idx->dpb8));
@@ -247,6 +255,11 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         WV_STEP("memset", hipMemsetAsync(xb, 0, qs_b, s));
         if (oc > 0 && idx->Xb)
             WV_STEP("copy", hipMemcpyAsync(xb, idx->Xb, (size_t)oc * idx->dpb * sizeof(uint16_t), hipMemcpyDeviceToDevice, s));
+    }
+    if (b8) {  // 256-row tiles: the old tiles are a prefix
+        WV_STEP("memset", hipMemsetAsync(b8, 0, (size_t)nc * idx->dpb8b, s));
+        if (oc > 0 && idx->bq8)
+            WV_STEP("copy", hipMemcpyAsync(b8, idx->bq8, (size_t)oc * idx->dpb8b, hipMemcpyDeviceToDevice, s));
     }
     if (x8) {  // 256-row tiles: the old tiles are a prefix
         WV_STEP("memset", hipMemsetAsync(x8, 0, (size_t)nc * idx->dpb8, s));
@@ -302,6 +315,7 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     if (cd) { swap_in(idx->codes, cd); idx->words = words; }
     swap_in(idx->Xb, xb);
     swap_in(idx->X8, x8);
+    swap_in(idx->bq8, b8);
     swap_in(idx->sb8, sb8);
     if (rqc) {
         if (idx->rq_codes) hipFree(idx->rq_codes);
@@ -408,6 +422,11 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
         const int64_t nt = n * idx->words;
         k_bq_encode_rows<<<(unsigned)((nt + 255) / 256), 256, 0, idx->stream>>>(idx->X, idx->dpad, n, idx->dims, d_slots,
                                                                                  idx->codes, idx->cap);
+        if (idx->bq8) {  // the +-1 plane of the same codes (integer-MFMA block minima)
+            const int64_t nu = n * (idx->dpb8b / 4);
+            k_bq_unpack8<<<(unsigned)((nu + 255) / 256), 256, 0, idx->stream>>>(idx->codes, idx->cap, idx->words, n,
+                                                                                d_slots, idx->dpb8b, idx->bq8);
+        }
     }
 }
 
@@ -683,7 +702,9 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     }
     else if (k == "sel_dbg") idx->sel_dbg = (int)value;
     else if (k == "q8") idx->q8_opt = value ? 1 : 0;  // int8 block keys (default 1) or bf16 (0)
-    else if (k == "q8_filter") idx->q8_filter = value ? 1 : 0;  // int8 keys: row bound from the int8 plane (1) or bf16 (0)
+    else if (k == "q8_filter") idx->q8_filter = value ? 1 : 0;
+    else if (k == "q8_stag") idx->q8_stag = value ? 1 : 0;  // staggered epilogues of the int8 key kernel
+    else if (k == "bq8") idx->bq8_opt = value ? 1 : 0;      // BQ block minima on the integer MFMA (1) or VALU (0)  // int8 keys: row bound from the int8 plane (1) or bf16 (0)
     else if (k == "q8_R") {
         if (value != 0 && value != 2 && value != 4 && value != 8) return set_err(WV_ERR_INVALID, "q8_R must be 0, 2, 4 or 8");
         idx->q8_R = (int)value;

@@ -185,6 +185,15 @@ class FlatIndex:
         check(self._l.wv_index_debug_blockkeys(self._h, int(q), _fptr(A), _fptr(eps), C.byref(nb)))
         return A, float(eps[0])
 
+    def debug_bqmin(self, q: int) -> np.ndarray:
+        """Diagnostic: the 256-row block minima of hamming distances of query q
+        of the last BQ batch (wv_index_debug_bqmin in include/wv_knn.h)."""
+        nb = C.c_int64(0)
+        check(self._l.wv_index_debug_bqmin(self._h, int(q), None, C.byref(nb)))
+        out = np.zeros(nb.value, np.float32)
+        check(self._l.wv_index_debug_bqmin(self._h, int(q), _fptr(out), C.byref(nb)))
+        return out
+
     # -- product quantizer (compressionhelpers.ProductQuantizer) -----------
     def pq_info(self) -> dict:
         out = (C.c_int32 * 4)()
