@@ -63,6 +63,7 @@ class WvStats(C.Structure):
         ("last_total_ms", C.c_double),
         ("last_group_queries", C.c_uint64),
         ("last_route", C.c_uint64),
+        ("last_scan_rows", C.c_uint64),
     ]
 
 

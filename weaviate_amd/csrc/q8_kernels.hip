@@ -39,6 +39,21 @@ __device__ __forceinline__ i32x4_t lds_ld16_o(unsigned base) {
     return v;
 }
 
+// valid bits of an allow list: slot = id - id_base, set when the slot is
+// below hiwater and present; cnt counts the bits newly set (duplicate ids once)
+__global__ void k_allow_bits(const uint64_t* __restrict__ ids, int64_t n, uint64_t id_base, int64_t hiwater,
+                             const uint32_t* __restrict__ present, uint32_t* __restrict__ bits,
+                             uint32_t* __restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t id = ids[i];
+    if (id < id_base || id - id_base >= (uint64_t)hiwater) return;
+    const uint64_t sl = id - id_base;
+    const uint32_t m = 1u << (sl & 31);
+    if (!(present[sl >> 5] & m)) return;
+    if (!(atomicOr(&bits[sl >> 5], m) & m)) atomicAdd(cnt, 1u);
+}
+
 // n copies of a 32-bit word (e.g. +inf block minima of an empty shard)
 __global__ void k_fill_u32(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -21,9 +21,10 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     const int RB8 = idx->dpb8 <= 768 ? 2 : 1;
     const int RB = q8 ? RB8 : qs_rb(NK);
     int R = qs_R(k);
-    if (q8) {  // the int8 bound is wider: one list size up (option q8_R)
+    if (q8) {  // the int8 bound is wider: 448-block lists (option q8_R; C3: ~110 candidate blocks
+               // per query, R = 4 sent a few percent to the overflow pass, profiles/r04_c3ab1_*)
         if (idx->q8_R > 0) R = std::max(R, idx->q8_R);
-        else R = std::min(8, 2 * R);
+        else R = 8;
     }
     const int L = 64 * (R - 1);
     const int64_t nslots = std::max<int64_t>(1, (idx->hiwater + 32 * RB - 1) / (32 * RB));

@@ -704,7 +704,8 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "q8") idx->q8_opt = value ? 1 : 0;  // int8 block keys (default 1) or bf16 (0)
     else if (k == "q8_filter") idx->q8_filter = value ? 1 : 0;
     else if (k == "q8_stag") idx->q8_stag = value ? 1 : 0;  // staggered epilogues of the int8 key kernel
-    else if (k == "bq8") idx->bq8_opt = value ? 1 : 0;      // BQ block minima on the integer MFMA (1) or VALU (0)  // int8 keys: row bound from the int8 plane (1) or bf16 (0)
+    else if (k == "bq8") idx->bq8_opt = value ? 1 : 0;      // BQ block minima on the integer MFMA (1) or VALU (0)
+    else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only  // int8 keys: row bound from the int8 plane (1) or bf16 (0)
     else if (k == "q8_R") {
         if (value != 0 && value != 2 && value != 4 && value != 8) return set_err(WV_ERR_INVALID, "q8_R must be 0, 2, 4 or 8");
         idx->q8_R = (int)value;
@@ -1102,27 +1103,87 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     return WV_OK;
 }
 
-// valid-slot bitmap for an allow list (present & allow); returns candidate count
+// valid-slot bitmap for an allow list (present & allow), built on the device
+// from the id list.  windowed: only the words of the allowed slot span
+// [lo, hi) are written (flat/index.go:590-608 seeks to allow.Min() and stops
+// past allow.Max()) and the caller scans only that span (ScanWindow); else the
+// whole bitmap up to hiwater.  Returns the candidate count (one host sync)
+// and the span.
 static int build_valid(wv_index* idx, hipStream_t s, const uint64_t* allow, int64_t n_allow, int32_t allow_mode,
-                       const uint32_t** valid_out, int64_t* n_valid) {
+                       const uint32_t** valid_out, int64_t* n_valid, int64_t* lo_out = nullptr,
+                       int64_t* hi_out = nullptr, bool windowed = false) {
+    if (lo_out) { *lo_out = 0; *hi_out = idx->hiwater; }
     if (allow_mode == 0) {
         *valid_out = idx->present;
         *n_valid = idx->npresent;
         return WV_OK;
     }
-    std::vector<uint32_t> bits((size_t)std::max<int64_t>(idx->cap / 32, 1), 0);
-    int64_t nv = 0;
+    int64_t lo = INT64_MAX, hi = -1;
     for (int64_t i = 0; i < n_allow; i++) {
         if (allow[i] < idx->id_base) continue;
-        uint64_t sl = allow[i] - idx->id_base;
-        if ((int64_t)sl >= idx->cap || !idx->h_present[sl]) continue;
-        if (!(bits[sl >> 5] & (1u << (sl & 31)))) { bits[sl >> 5] |= 1u << (sl & 31); nv++; }
+        const uint64_t sl = allow[i] - idx->id_base;
+        if ((int64_t)sl >= idx->hiwater) continue;
+        lo = std::min<int64_t>(lo, (int64_t)sl);
+        hi = std::max<int64_t>(hi, (int64_t)sl + 1);
     }
-    HIPCHK(idx->valid.ensure(bits.size() * sizeof(uint32_t)));
-    HIPCHK(hipMemcpyAsync(idx->valid.p, bits.data(), bits.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    *valid_out = idx->present;
+    *n_valid = 0;
+    if (hi <= lo) return WV_OK;
+    HIPCHK(idx->valid.ensure((size_t)std::max<int64_t>(idx->cap / 32, 1) * sizeof(uint32_t)));
+    HIPCHK(idx->allowIds.ensure((size_t)n_allow * sizeof(uint64_t) + 8));
+    HIPCHK(idx->allowCnt.ensure(sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(idx->allowIds.p, allow, (size_t)n_allow * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    // every word a kernel of the (windowed) scan reads: whole 256-row tiles
+    // from the window start (lo rounded down) to the span end rounded up
+    const int64_t w0 = windowed ? (lo / 256 * 256) >> 5 : 0;
+    const int64_t w1 = round_up(windowed ? hi : idx->hiwater, 256) >> 5;
+    HIPCHK(hipMemsetAsync(idx->valid.as<uint32_t>() + w0, 0, (size_t)(w1 - w0) * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(idx->allowCnt.p, 0, sizeof(uint32_t), s));
+    k_allow_bits<<<(unsigned)((n_allow + 255) / 256), 256, 0, s>>>(idx->allowIds.as<uint64_t>(), n_allow, idx->id_base,
+                                                                    idx->hiwater, idx->present,
+                                                                    idx->valid.as<uint32_t>(), idx->allowCnt.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    uint32_t nv = 0;
+    HIPCHK(hipMemcpyAsync(&nv, idx->allowCnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     *valid_out = idx->valid.as<uint32_t>();
     *n_valid = nv;
+    if (lo_out) { *lo_out = lo; *hi_out = hi; }
     return WV_OK;
+}
+
+// A search over the slot span [lo, hi) of the store only: the stored-row
+// arrays are offset to lo (a multiple of 256: whole tiles of the tiled planes)
+// and the index reads as one of hi - lo slots with id_base + lo, so every
+// kernel of the path scans only the span.  Exact fp32 and BQ indexes (their
+// layouts are row- or 256-row-tile-major); restored on scope exit.
+struct ScanWindow {
+    wv_index* idx;
+    int64_t lo;
+    float* X; float* xnorm2; uint32_t* present; uint16_t* Xb; unsigned char* X8; float* sb8;
+    uint64_t* codes; unsigned char* bq8; int64_t hiwater; uint64_t id_base;
+    ScanWindow(wv_index* i, int64_t lo_, int64_t hi_) : idx(i), lo(lo_) {
+        X = idx->X; xnorm2 = idx->xnorm2; present = idx->present; Xb = idx->Xb; X8 = idx->X8; sb8 = idx->sb8;
+        codes = idx->codes; bq8 = idx->bq8; hiwater = idx->hiwater; id_base = idx->id_base;
+        idx->hiwater = hi_ - lo;
+        if (lo == 0) return;
+        idx->X += lo * idx->dpad;
+        idx->xnorm2 += lo;
+        idx->present += lo / 32;
+        if (idx->Xb) idx->Xb += lo * idx->dpb;
+        if (idx->X8) { idx->X8 += lo * idx->dpb8; idx->sb8 += lo / 32; }
+        if (idx->codes) idx->codes += lo;  // word-major, stride cap
+        if (idx->bq8) idx->bq8 += lo * idx->dpb8b;
+        idx->id_base += (uint64_t)lo;
+    }
+    ~ScanWindow() {
+        idx->X = X; idx->xnorm2 = xnorm2; idx->present = present; idx->Xb = Xb; idx->X8 = X8; idx->sb8 = sb8;
+        idx->codes = codes; idx->bq8 = bq8; idx->hiwater = hiwater; idx->id_base = id_base;
+    }
+};
+
+static bool window_ok(const wv_index* idx) {
+    return idx->compression == WV_COMPRESSION_NONE || idx->compression == WV_COMPRESSION_BQ;
 }
 
 extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
@@ -1137,8 +1198,9 @@ extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queri
         return WV_OK;
     }
     const uint32_t* valid = nullptr;
-    int64_t n_valid = 0;
-    int rc = build_valid(idx, s, allow_ids, n_allow, allow_mode, &valid, &n_valid);
+    int64_t n_valid = 0, lo = 0, hi = 0;
+    const bool windowed = allow_mode == 1 && idx->scan_window && window_ok(idx);
+    int rc = build_valid(idx, s, allow_ids, n_allow, allow_mode, &valid, &n_valid, &lo, &hi, windowed);
     if (rc) return rc;
     if (n_valid == 0 || idx->dims == 0) {
         for (int64_t q = 0; q < nq; q++) out_counts[q] = 0;
@@ -1150,8 +1212,14 @@ extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queri
     HIPCHK(idx->oD.ensure((size_t)nq * kk * sizeof(float)));
     HIPCHK(idx->oN.ensure((size_t)nq * sizeof(int32_t)));
     HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
-    rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, valid, n_valid, idx->oIds.as<uint64_t>(),
-                     idx->oD.as<float>(), idx->oN.as<int32_t>(), nullptr);
+    {
+        // an allow list scans only its slot span (rounded down to a 256-row tile)
+        const int64_t lo_t = windowed ? lo / 256 * 256 : 0;
+        ScanWindow win(idx, lo_t, windowed ? hi : idx->hiwater);
+        idx->stats.last_scan_rows = (uint64_t)idx->hiwater;
+        rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, valid + lo_t / 32, n_valid,
+                         idx->oIds.as<uint64_t>(), idx->oD.as<float>(), idx->oN.as<int32_t>(), nullptr);
+    }
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
