@@ -564,7 +564,7 @@ def main():
     # the sharded PQ search (ShardedQuantSearch) computes full ADC rows with k_pq_adc2
     pq_kernel = "k_pq_adc3" if pq and not shard and not any(o.replace(" ", "") == "pq_adc3=0" for o in args.option) \
         else "k_pq_adc2"
-    dom_kernel = (pq_kernel if pq else "k_bq_blockmin_lds" if bq else
+    dom_kernel = (pq_kernel if pq else ("k_q8_blockkey_bq" if route == 6 else "k_bq_blockmin_lds") if bq else
                   ("k_rq8_dist" if rq_bits == 8 else "k_rq1_dist") if rq_bits else sel_kernel)
     if args.traffic_bytes is None:
         args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B, dom_kernel)
@@ -599,6 +599,19 @@ def main():
                 "peak": LDS_LOOKUP_PEAK_T, "unit": "T lookups/s", "frac": achieved / LDS_LOOKUP_PEAK_T,
                 "frac_of_b32_lookup_rate": achieved / LDS_LOOKUP_B32_T, "launch_ms": sel_avg,
                 "note": "launch_ms = first query group of the batch",
+                "traffic": args.traffic_bytes}
+    elif bq and route == 6:
+        # dominant kernel: the block minima on the integer matrix cores
+        # (k_q8_blockkey<..., BQ> over the +-1 code planes): one int8 product
+        # per (query, row, code bit), hamming = (bits - dot) / 2 exactly
+        words = (dims + 63) // 64
+        ops = 2.0 * B * n_local * 64 * words
+        achieved = ops / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0
+        roof = {"bound": "mfma", "kernel": "k_q8_blockkey (BQ +-1 planes)", "achieved": achieved,
+                "peak": MFMA_I8_PEAK_TOPS, "unit": "TOPS (int8 MFMA)", "frac": achieved / MFMA_I8_PEAK_TOPS,
+                "launch_ms": sel_avg,
+                "mfma": "v_mfma_i32_16x16x64_i8 over codes unpacked to +-1 int8: sum s_q s_x = bits - 2 hamming",
+                "valu_form_equivalent_Tops": 4.0 * B * n_local * words / (sel_avg * 1e-3) / 1e12 if sel_avg > 0 else 0.0,
                 "traffic": args.traffic_bytes}
     elif bq:
         # dominant kernel k_bq_blockmin: VALU-bound integer work, per (query,
@@ -693,6 +706,7 @@ def main():
             "vs_baseline": None,
             "dtype": ("u8 codes (v_dot4) + f32 rescoring" if rq_bits == 8 else
                       "u64 codes x 5-bit query planes + f32 rescoring" if rq_bits == 1 else
+                      "+-1 int8 codes (hamming on the integer MFMA) + f32 rescoring" if bq and route == 6 else
                       "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else
                       "f32 (exact result; int8 MFMA block-key filter)" if int8_keys else
                       "f32 (exact result; bf16 MFMA block-key filter)"),

@@ -230,3 +230,29 @@ def test_bq_int8_deletes_allow_upserts(wv, oracle):
             exp = orc.search(queries[q], k, allow=allow if al is not None else None)
             assert_same(exp, got[0][q, :got[2][q]], got[1][q, :got[2][q]], f"q{q}")
     idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,d,k", [("cosine", 0, 768, 10), ("l2-squared", 1, 512, 100), ("dot", 0, 640, 10),
+                                           ("cosine", 0, 1024, 10), ("l2-squared", 0, 1536, 24)])
+def test_q8_shape32_same_keys(wv, oracle, metric, kind, d, k):
+    """q8_shape 32 (v_mfma_i32_32x32x32_i8, one query per lane in the block
+    reduction) writes bit-identical block keys to the 16x16x64 kernel (the
+    per-row values and the scale are the same; maxima commute with the
+    monotone rounding), and the same results; corpus sizes end mid-slot."""
+    n = 16000 + 45
+    data = gen(oracle, kind, 92, n, d)
+    queries = gen(oracle, kind, 93, 300, d)
+    res, keys = [], []
+    for shape in (16, 32):
+        idx, orc = build_pair(wv, oracle, metric, "avx256", data, options={"q8_shape": shape})
+        res.append(idx.search_by_vector_batch(queries, k))
+        assert idx.stats()["last_route"] == ROUTE_INT8
+        keys.append([idx.debug_blockkeys(q)[0] for q in (0, 255, 299)])
+        idx.close()
+    for a, b in zip(keys[0], keys[1]):
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    ids, dists, counts = res[1]
+    for qi in range(0, len(queries), 10):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")

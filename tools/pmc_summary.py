@@ -10,7 +10,7 @@ for path in sorted(glob.glob(os.path.join(root, "*", "run_counter_collection.csv
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     for k, v in agg.items():
-        if not any(s in k for s in ("mfma_select", "gemv_select", "exact_rows", "bq_", "pq_", "hamming_scan", "qs_", "blk_", "rq")):
+        if not any(s in k for s in ("mfma_select", "gemv_select", "exact_rows", "bq_", "pq_", "hamming_scan", "qs_", "q8_", "blk_", "rq")):
             continue
         n = len(disp[k])
         ms = sum(disp[k].values()) / n

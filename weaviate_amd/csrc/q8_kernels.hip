@@ -28,6 +28,7 @@ namespace wv {
 namespace {
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x16_t __attribute__((ext_vector_type(16)));
 constexpr int Q8_NONE = (int)0x80000000;  // "no valid row" in the integer max
 
 // (q8_plane_byte: qs_kernels.hip)
@@ -52,6 +53,41 @@ __global__ void k_allow_bits(const uint64_t* __restrict__ ids, int64_t n, uint64
     const uint32_t m = 1u << (sl & 31);
     if (!(present[sl >> 5] & m)) return;
     if (!(atomicOr(&bits[sl >> 5], m) & m)) atomicAdd(cnt, 1u);
+}
+
+// gathered allow-list search: stored rows slots[i] -> row i of a sub-index
+// (fp32 row with its padding, |x|^2, and the bf16 plane row), thread per
+// (row, 16-byte piece); rows in [n, n_pad) are zeroed
+__global__ void k_gather_rows(const float* __restrict__ X, const float* __restrict__ xn2, int dpad,
+                              const uint16_t* __restrict__ Xb, int dpb, const uint32_t* __restrict__ slots, int64_t n,
+                              int64_t n_pad, float* __restrict__ Xo, float* __restrict__ xn2o, uint16_t* __restrict__ Xbo) {
+    const int per = dpad / 4 + (Xb ? dpb / 8 : 0) + 1;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pad * per) return;
+    const int64_t r = i / per;
+    const int p = (int)(i % per);
+    const bool live = r < n;
+    const int64_t sl = live ? (int64_t)slots[r] : 0;
+    if (p < dpad / 4) {
+        const float4 v = live ? reinterpret_cast<const float4*>(X + sl * dpad)[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+        reinterpret_cast<float4*>(Xo + r * dpad)[p] = v;
+    } else if (p < dpad / 4 + (Xb ? dpb / 8 : 0)) {
+        const int c = (p - dpad / 4) * 8;  // 8 bf16 columns: one 16-byte half of a 32-byte chunk row
+        const uint4 v = live ? *reinterpret_cast<const uint4*>(Xb + bf3_plane_index(sl, c, dpb)) : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(Xbo + bf3_plane_index(r, c, dpb)) = v;
+    } else {
+        xn2o[r] = live ? xn2[sl] : 0.f;
+    }
+}
+
+// ids[q][j] = id_base + slots[ids[q][j]] for j < counts[q] (sub-index positions -> doc ids)
+__global__ void k_remap_ids(uint64_t* __restrict__ ids, const int32_t* __restrict__ counts, int64_t nq, int k,
+                            const uint32_t* __restrict__ slots, uint64_t id_base) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq * k) return;
+    const int64_t q = i / k;
+    if ((int)(i % k) >= counts[q]) return;
+    ids[i] = id_base + slots[ids[i]];
 }
 
 // n copies of a 32-bit word (e.g. +inf block minima of an empty shard)
@@ -544,6 +580,204 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
         finish(mp0, mp1, gbp);
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_q8_blockkey32<NC, RB, L2>: the same int8 block keys on
+// v_mfma_i32_32x32x32_i8 (NC = dpb8 / 32 chunks of 32 columns per block, one
+// MFMA per chunk and wave: 32 rows x the wave's 32 queries).  The 32x32
+// accumulator holds 16 rows of ONE query per lane, so a block's reduction is
+// 15 lane-local maxima and one permlane32 swap (the 16x16x64 layout spreads a
+// query over four lane groups: two more swap levels and twice the selects).
+// The schedule is k_qs_blockkey's multi-block one (32x32x16 bf16 for d <= 384):
+// A fragments four chunks ahead, RB blocks per slot, the slot's DMA group three
+// steps ahead issued after its barrier, the half-swapped 1 KiB pieces that make
+// the 16-lane ds_read_b128 groups conflict-free.
+// ---------------------------------------------------------------------------
+template <int NC, int RB, bool ISL2>
+__global__ __launch_bounds__(512, 2) void k_q8_blockkey32(Q8Args a) {
+    constexpr int SLOT = RB * NC * 1024;           // bytes per ring slot
+    constexpr int P = RB * NC / 8;                 // 1 KiB DMA pieces per wave per slot
+    static_assert((RB * NC) % 8 == 0, "pieces per slot must split over 8 waves");
+    constexpr int64_t TILE_B = (int64_t)NC * 8192;  // bytes per 256-row tile of the plane
+    constexpr int NBUF = 3;
+    extern __shared__ __attribute__((aligned(16))) unsigned char qsm[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 31, lh = lane >> 5;
+    const int total = a.nqg * a.nspans;
+    const int b = blockIdx.x;
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int span = logical / a.nqg, grp = logical % a.nqg;
+
+    // B fragments: Qf[c] = lane (li, lh): query wave*32 + li, columns 32c + 16lh .. +15
+    i32x4_t Qf[NC];
+    {
+        const unsigned char* qp = a.Q8 + (int64_t)grp * TILE_B + (wave * 32 + li) * 32 + 16 * lh;
+#pragma unroll
+        for (int c = 0; c < NC; c++) Qf[c] = *reinterpret_cast<const i32x4_t*>(qp + c * 8192);
+    }
+    const int64_t qrow = (int64_t)grp * 256 + wave * 32 + li;
+    const float sq = a.qscale[qrow];
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the query loads before the DMA ring
+
+    const int64_t s0 = (int64_t)span * a.slots_per_span;
+    int64_t s1 = s0 + a.slots_per_span;
+    if (s1 > a.nslots) s1 = a.nslots;
+    const int nsteps = s1 > s0 ? (int)(s1 - s0) : 0;
+
+    // LDS-DMA: lane L writes bytes [16L, 16L+16) of a 1 KiB piece = row L>>1,
+    // physical half L&1 holding source half (L&1) ^ ((row>>3)&1)
+    const int prow = lane >> 1;
+    const uint32_t src_lane = (uint32_t)(prow * 32 + 16 * ((lane & 1) ^ ((prow >> 3) & 1)));
+    const unsigned ring = lds_addr(qsm);
+    // per-wave rings of 4 entries: valid words [8][4][16 B], scales [8][4][16 B],
+    // L2 norms [8][4][RB * 128 B]
+    const unsigned vring = ring + NBUF * SLOT + (unsigned)wave * 64u;
+    const unsigned sring = ring + NBUF * SLOT + 512u + (unsigned)wave * 64u;
+    const unsigned xnring = ring + NBUF * SLOT + 1024u + (unsigned)wave * (unsigned)(4 * RB * 128);
+    constexpr int P0 = P + 2 + (ISL2 ? 1 : 0);  // vector-memory ops per group, per wave
+    const int64_t tile0 = (s0 * RB * 32) >> 8;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.X8 + tile0 * TILE_B), (short)0, -1, 0x00020000);
+    int64_t igb = s0 * RB;
+    uint32_t ioff = (uint32_t)(((igb >> 3) - tile0) * TILE_B + (igb & 7) * 1024);
+    auto issue = [&](int t, int slot) {
+        const unsigned sbs = ring + (unsigned)(slot * SLOT);
+#pragma unroll
+        for (int i = 0; i < P; i++) {
+            const int p = wave + 8 * i;
+            const int rb = p / NC, c = p % NC;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(size_t)(sbs + (unsigned)((rb * NC + c) * 1024)), 16,
+                                                     src_lane, ioff + (uint32_t)(rb * 1024 + c * 8192), 0, 0);
+        }
+        if (lane < RB)
+            __builtin_amdgcn_global_load_lds(a.valid + igb + lane, (lds_ptr_t)(size_t)(vring + (unsigned)((t & 3) * 16)), 4, 0, 0);
+        if (lane < RB)
+            __builtin_amdgcn_global_load_lds(a.sb + igb + lane, (lds_ptr_t)(size_t)(sring + (unsigned)((t & 3) * 16)), 4, 0, 0);
+        if (ISL2 && lane < RB * 8)
+            __builtin_amdgcn_global_load_lds(a.xnorm2 + igb * 32 + 4 * lane,
+                                             (lds_ptr_t)(size_t)(xnring + (unsigned)((t & 3) * RB * 128)), 16, 0, 0);
+        igb += RB;
+        ioff += RB * 1024;
+        if ((igb & 7) == 0) ioff += (uint32_t)(TILE_B - 8192);
+    };
+
+    const unsigned lane_off = (unsigned)(li * 32 + 16 * (lh ^ ((li >> 3) & 1)));
+    float* krow = a.key + qrow * a.ldk;
+    i32x4_t A[4];
+    if (nsteps > 0) {
+        issue(0, 0);
+        if (nsteps > 1) issue(1, 1);
+        qs_wait_vm(nsteps > 1 ? P0 : 0);  // group 0 landed, group 1 may stay in flight
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (nsteps > 2) issue(2, 2);
+        const unsigned sb0 = ring + lane_off;
+        A[0] = lds_ld16_o<0>(sb0);
+        A[1] = lds_ld16_o<1024>(sb0);
+        A[2] = lds_ld16_o<2048>(sb0);
+        A[3] = lds_ld16_o<3072>(sb0);
+    }
+    int cur = 0;
+    for (int t = 0; t < nsteps; t++) {
+        const int nxt = cur == NBUF - 1 ? 0 : cur + 1;
+        const unsigned sbase = ring + (unsigned)(cur * SLOT) + lane_off;
+        const unsigned sbn = ring + (unsigned)(nxt * SLOT) + lane_off;
+        const unsigned sm = (unsigned)(t & 3);
+        static_for<0, RB>([&](auto rbc) {
+            constexpr int rb = decltype(rbc)::value;
+            // ---- the block's 32 rows x this wave's 32 queries: NC MFMAs, A fragments 4 ahead ----
+            i32x16_t acc;
+            static_for<0, NC>([&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                qs_wait_lgkm<(NC - 1 - c) < 3 ? (NC - 1 - c) : 3>();
+                asm volatile("" : "+v"(A[c & 3]));
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (c == 0)
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[c & 3], Qf[c], i32x16_t{}, 0, 0, 0);
+                else
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[c & 3], Qf[c], acc, 0, 0, 0);
+                if constexpr (c + 4 < NC) A[c & 3] = lds_ld16_o<(rb * NC + c + 4) * 1024>(sbase);
+            });
+            // ---- end of the slot: the next group must have landed (every wave) ----
+            if constexpr (rb == RB - 1) {
+                if (t + 1 < nsteps) {
+                    if (t >= 2 && t + 2 < nsteps) {
+                        qs_wait_vm_c<2 * RB + P0>();  // steady state
+                    } else {
+                        const int y = (RB - 1) + (t >= 1 ? RB : 0) + (t >= 2 ? 1 : 0) + (t + 2 < nsteps ? P0 : 0);
+                        qs_wait_vm(y);
+                    }
+                    __builtin_amdgcn_s_barrier();  // slot t is free: every wave's chain over it is done
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (t + 3 < nsteps) issue(t + 3, cur);
+                }
+            }
+            // ---- epilogue: the block's key for this lane's query ----
+            const int64_t gb = (s0 + t) * RB + rb;
+            uint32_t vwv;
+            float sbv;
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(vwv) : "v"(vring + sm * 16u), "i"(rb * 4));
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(sbv) : "v"(sring + sm * 16u), "i"(rb * 4));
+            // next block's first fragments (in flight during the epilogue)
+            const unsigned pb = rb + 1 < RB ? sbase : sbn;
+            constexpr int pr = rb + 1 < RB ? rb + 1 : 0;
+            float m;
+            if constexpr (ISL2) {
+                const unsigned xb = xnring + sm * (unsigned)(RB * 128) + (unsigned)(rb * 128 + 16 * lh);
+                f32x4_t x0 = lds_ld4f_o<0>(xb), x1 = lds_ld4f_o<32>(xb), x2 = lds_ld4f_o<64>(xb), x3 = lds_ld4f_o<96>(xb);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vwv), "+v"(sbv), "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+                A[0] = lds_ld16_o<(pr * NC + 0) * 1024>(pb);
+                A[1] = lds_ld16_o<(pr * NC + 1) * 1024>(pb);
+                A[2] = lds_ld16_o<(pr * NC + 2) * 1024>(pb);
+                A[3] = lds_ld16_o<(pr * NC + 3) * 1024>(pb);
+                const uint32_t vw = __builtin_amdgcn_readfirstlane(vwv);
+                const float c2 = -2.f * (sq * __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sbv))));
+                const uint32_t vl = vw >> (4 * lh);
+                const float xn[16] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3],
+                                      x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
+                m = __builtin_inff();
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    float v = fmaf(c2, (float)acc[r], xn[r]);
+                    if (vw != 0xFFFFFFFFu) v = ((vl >> ((r & 3) + 8 * (r >> 2))) & 1u) ? v : __builtin_inff();
+                    m = fminf(m, v);
+                }
+                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+                m = fminf(m, __uint_as_float(sw[1]));
+            } else {
+                A[0] = lds_ld16_o<(pr * NC + 0) * 1024>(pb);
+                A[1] = lds_ld16_o<(pr * NC + 1) * 1024>(pb);
+                A[2] = lds_ld16_o<(pr * NC + 2) * 1024>(pb);
+                A[3] = lds_ld16_o<(pr * NC + 3) * 1024>(pb);
+                asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(vwv), "+v"(sbv));
+                const uint32_t vw = __builtin_amdgcn_readfirstlane(vwv);
+                const float s = sq * __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sbv)));
+                const uint32_t vl = vw >> (4 * lh);
+                int mi;
+                if (vw == 0xFFFFFFFFu) {
+                    mi = acc[0];
+#pragma unroll
+                    for (int r = 1; r < 16; r++) mi = max(mi, acc[r]);
+                } else {
+                    mi = Q8_NONE;
+#pragma unroll
+                    for (int r = 0; r < 16; r++)
+                        mi = max(mi, ((vl >> ((r & 3) + 8 * (r >> 2))) & 1u) ? acc[r] : Q8_NONE);
+                }
+                // one query per lane: the halves' maxima combine across lh before the scale
+                const auto sw = __builtin_amdgcn_permlane32_swap((uint32_t)mi, (uint32_t)mi, false, false);
+                mi = max(mi, (int)sw[1]);
+                m = mi == Q8_NONE ? __builtin_inff() : -(s * (float)mi);
+            }
+            if (lh == 0) krow[gb] = m;
+        });
+        cur = nxt;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last (unused) prefetch
 }
 
 // BQ codes unpacked to +-1 int8 for k_q8_blockkey<..., BQ>: bit b of word w

@@ -185,7 +185,25 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             q8a.slots_per_span = a.slots_per_span;
             q8a.nspans = a.nspans;
             q8a.nqg = a.nqg;
-            if (l2) { WV_Q8N(true); } else { WV_Q8N(false); }
+            if (idx->q8_shape == 32) {
+#define WV_Q832(NCV, RBV, L2V)                                                                                \
+    do {                                                                                                      \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey32<NCV, RBV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey32<NCV, RBV, L2V><<<grid, 512, lds, s>>>(q8a);                                            \
+    } while (0)
+#define WV_Q832N(L2V)                                  \
+    switch (NC8) {                                     \
+    case 8: WV_Q832(16, 2, L2V); break;                \
+    case 10: WV_Q832(20, 2, L2V); break;               \
+    case 12: WV_Q832(24, 2, L2V); break;               \
+    case 16: WV_Q832(32, 1, L2V); break;               \
+    case 20: WV_Q832(40, 1, L2V); break;               \
+    default: WV_Q832(48, 1, L2V); break;               \
+    }
+                if (l2) { WV_Q832N(true); } else { WV_Q832N(false); }
+#undef WV_Q832N
+#undef WV_Q832
+            } else if (l2) { WV_Q8N(true); } else { WV_Q8N(false); }
         } else if (w4) {
             if (l2) { WV_QSWN(true); } else { WV_QSWN(false); }
 #ifdef WV_QS_DBG  // timing experiments (k_qs_blockkey DBG bits), not in the product build

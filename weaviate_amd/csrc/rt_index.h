@@ -120,6 +120,12 @@ struct wv_index {
     int bq8_opt = 1;
     int64_t bq_last_nq = 0, bq_last_nblk = 0;
     int scan_window = 1;         // option scan_window: an allow list scans only [allow.Min, allow.Max]
+    // gathered allow-list search: a sparse allow list's rows (ascending id) as
+    // a temporary sub-index searched by the same pipeline (option gather_max:
+    // the largest such list, 0 = off)
+    int64_t gather_max = 1 << 20;
+    wv_index* sub = nullptr;
+    DBuf subSlots;
     DBuf allowIds, allowCnt;     // the allow list on the device, its candidate count  // debug hook (wv_index_debug_bqmin): the last BQ batch's first group             // option bq8: block minima from the +-1 plane (1) or the VALU kernels (0)
     int64_t bq_nq = 0;           // BQ batch in flight (bq_begin): queries and R
     int bq_R = 0;
@@ -140,6 +146,7 @@ struct wv_index {
     int q8_planes = 0, dpb8 = 0;
     int q8_opt = 1;                 // option q8: block keys from the int8 plane (1) or the bf16 plane (0)
     int q8_R = 0;                   // option q8_R: candidate lists for int8 keys (0: R = 8, 448 blocks)
+    int q8_shape = 16;              // option q8_shape: 16 = v_mfma_i32_16x16x64_i8 kernel, 32 = 32x32x32
     int q8_stag = 0;                // option q8_stag: waves 4-7 reduce each block P0 chunks late (RB = 2)
     int q8_filter = 1;              // option q8_filter: the exact pass bounds rows from the int8 plane (1) or bf16 (0)
     unsigned char* X8 = nullptr;

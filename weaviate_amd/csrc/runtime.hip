@@ -132,6 +132,7 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
 
 extern "C" void wv_index_destroy(wv_index* idx) {
     if (!idx) return;
+    if (idx->sub) wv_index_destroy(idx->sub);
     batcher_free(idx->batcher);
     hipSetDevice(idx->device);
     if (idx->stream) hipStreamSynchronize(idx->stream);
@@ -704,8 +705,16 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "q8") idx->q8_opt = value ? 1 : 0;  // int8 block keys (default 1) or bf16 (0)
     else if (k == "q8_filter") idx->q8_filter = value ? 1 : 0;
     else if (k == "q8_stag") idx->q8_stag = value ? 1 : 0;  // staggered epilogues of the int8 key kernel
+    else if (k == "q8_shape") {  // int8 key kernel MFMA shape
+        if (value != 16 && value != 32) return set_err(WV_ERR_INVALID, "q8_shape must be 16 or 32");
+        idx->q8_shape = (int)value;
+    }
     else if (k == "bq8") idx->bq8_opt = value ? 1 : 0;      // BQ block minima on the integer MFMA (1) or VALU (0)
-    else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only  // int8 keys: row bound from the int8 plane (1) or bf16 (0)
+    else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only
+    else if (k == "gather_max") {  // sparse allow lists up to this many rows: gathered sub-index search
+        if (value < 0 || value > (1ll << 28)) return set_err(WV_ERR_INVALID, "gather_max out of range");
+        idx->gather_max = value;
+    }  // int8 keys: row bound from the int8 plane (1) or bf16 (0)
     else if (k == "q8_R") {
         if (value != 0 && value != 2 && value != 4 && value != 8) return set_err(WV_ERR_INVALID, "q8_R must be 0, 2, 4 or 8");
         idx->q8_R = (int)value;
@@ -1186,6 +1195,67 @@ static bool window_ok(const wv_index* idx) {
     return idx->compression == WV_COMPRESSION_NONE || idx->compression == WV_COMPRESSION_BQ;
 }
 
+// The allowed rows (slots ascending = the reference cursor's id order) as a
+// sub-index: fp32 rows, norms and bf16 plane rows gathered, the int8 plane
+// re-quantised per sub-index block; the parent's residual maxima bound the
+// gathered bf16 rows.  Same metric, variant and exact-path options.
+static int subindex_build(wv_index* idx, hipStream_t s, const std::vector<uint32_t>& slots) {
+    const int64_t n = (int64_t)slots.size();
+    if (!idx->sub) {
+        wv_config c{};
+        c.metric = idx->metric;
+        c.dims = idx->dims;
+        c.compression = WV_COMPRESSION_NONE;
+        c.rescore_limit = -1;
+        c.device = idx->device;
+        c.variant = idx->variant;
+        c.id_base = 0;
+        c.root_path = idx->root_path.c_str();
+        int rc = wv_index_create(&c, &idx->sub);
+        if (rc) return rc;
+    }
+    wv_index* sb = idx->sub;
+    sb->use_qs = idx->use_qs;
+    set_dims(sb, idx->dims);
+    sb->kernel_opt = idx->kernel_opt; sb->q8_opt = idx->q8_opt; sb->q8_R = idx->q8_R; sb->q8_filter = idx->q8_filter;
+    sb->q8_stag = idx->q8_stag; sb->q8_shape = idx->q8_shape; sb->exact_filter = idx->exact_filter; sb->exact_bm = idx->exact_bm;
+    sb->exact_cap = idx->exact_cap; sb->replay_par = idx->replay_par; sb->margin = idx->margin;
+    sb->gemv_max = idx->gemv_max; sb->gemv_wg = idx->gemv_wg; sb->exact_multi = idx->exact_multi;
+    sb->force_replay = idx->force_replay; sb->qs_force_flag = idx->qs_force_flag; sb->timing = idx->timing;
+    sb->hiwater = 0;
+    sb->npresent = 0;
+    int rc = ensure_capacity(sb, round_up(std::max<int64_t>(n, 1), 256));
+    if (rc) return rc;
+    HIPCHK(idx->subSlots.ensure((size_t)n * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(idx->subSlots.p, slots.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    const int64_t n_pad = round_up(n, 256);
+    {
+        const int64_t per = idx->dpad / 4 + (sb->qs_planes ? idx->dpb / 8 : 0) + 1;
+        const int64_t nt = n_pad * per;
+        k_gather_rows<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(idx->X, idx->xnorm2, idx->dpad,
+                                                                    sb->qs_planes ? idx->Xb : nullptr, idx->dpb,
+                                                                    idx->subSlots.as<uint32_t>(), n, n_pad, sb->X,
+                                                                    sb->xnorm2, sb->Xb);
+        HIPCHK(hipGetLastError());
+    }
+    std::vector<uint32_t> bits((size_t)(sb->cap / 32), 0);
+    for (int64_t i = 0; i < n; i++) bits[(size_t)(i >> 5)] |= 1u << (i & 31);
+    HIPCHK(hipMemcpyAsync(sb->present, bits.data(), bits.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(sb->d_maxn2, idx->d_maxn2, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(sb->qsmax, idx->qsmax, 4 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    if (sb->q8_planes) {
+        HIPCHK(hipMemsetAsync(sb->qmax8, 0, 4 * sizeof(uint32_t), s));
+        k_block_q8<<<(unsigned)(n_pad / 32), 256, 0, s>>>(sb->X, sb->dpad, sb->dims, sb->dpb8, nullptr, 0, sb->X8, sb->sb8,
+                                                          sb->qmax8);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(s));  // the host bitmap and slot list are read by the copies
+    sb->hiwater = n;
+    sb->npresent = n;
+    sb->has_nonfinite = idx->has_nonfinite;
+    return WV_OK;
+}
+
 extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
                                                const uint64_t* allow_ids, int64_t n_allow, int32_t allow_mode,
                                                uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
@@ -1199,6 +1269,52 @@ extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queri
     }
     const uint32_t* valid = nullptr;
     int64_t n_valid = 0, lo = 0, hi = 0;
+    if (allow_mode == 1 && idx->compression == WV_COMPRESSION_NONE && idx->qs_planes && n_allow <= idx->gather_max &&
+        idx->dims != 0 && d == idx->dims) {
+        // a sparse allow list: its rows as a sub-index (cost follows the list, not its span)
+        std::vector<uint32_t> slots;
+        slots.reserve((size_t)n_allow);
+        for (int64_t i = 0; i < n_allow; i++) {
+            if (allow_ids[i] < idx->id_base) continue;
+            const uint64_t sl = allow_ids[i] - idx->id_base;
+            if ((int64_t)sl < idx->hiwater && idx->h_present[sl]) slots.push_back((uint32_t)sl);
+        }
+        std::sort(slots.begin(), slots.end());
+        slots.erase(std::unique(slots.begin(), slots.end()), slots.end());
+        if (slots.empty()) {
+            for (int64_t q = 0; q < nq; q++) out_counts[q] = 0;
+            return WV_OK;
+        }
+        const int64_t span = (int64_t)slots.back() + 1 - (int64_t)slots.front() / 256 * 256;
+        if ((int64_t)slots.size() * 8 <= span) {
+            int rc = subindex_build(idx, s, slots);
+            if (rc) return rc;
+            const int kk = std::max(k, 1);
+            HIPCHK(idx->qraw.ensure((size_t)nq * d * sizeof(float)));
+            HIPCHK(idx->oIds.ensure((size_t)nq * kk * sizeof(uint64_t)));
+            HIPCHK(idx->oD.ensure((size_t)nq * kk * sizeof(float)));
+            HIPCHK(idx->oN.ensure((size_t)nq * sizeof(int32_t)));
+            HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
+            wv_index* sb = idx->sub;
+            rc = search_core(sb, s, idx->qraw.as<float>(), nq, d, k, 0, sb->present, sb->npresent,
+                             idx->oIds.as<uint64_t>(), idx->oD.as<float>(), idx->oN.as<int32_t>(), nullptr);
+            if (rc) return rc;
+            if (k > 0)
+                k_remap_ids<<<(unsigned)((nq * k + 255) / 256), 256, 0, s>>>(idx->oIds.as<uint64_t>(),
+                                                                             idx->oN.as<int32_t>(), nq, k,
+                                                                             idx->subSlots.as<uint32_t>(), idx->id_base);
+            HIPCHK(hipGetLastError());
+            idx->stats.last_route = sb->stats.last_route;
+            idx->stats.last_scan_rows = (uint64_t)sb->hiwater;
+            idx->stats.queries += (uint64_t)nq;
+            idx->stats.batches++;
+            HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(out_counts, idx->oN.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            return WV_OK;
+        }
+    }
     const bool windowed = allow_mode == 1 && idx->scan_window && window_ok(idx);
     int rc = build_valid(idx, s, allow_ids, n_allow, allow_mode, &valid, &n_valid, &lo, &hi, windowed);
     if (rc) return rc;
