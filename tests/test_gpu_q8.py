@@ -192,7 +192,9 @@ def test_bq_int8_minima_equal_valu_and_oracle(wv, oracle, metric, kind, n, d, k,
     ref = idx.search_by_vector_batch(queries, k)
     assert idx.stats()["last_route"] == ROUTE_BQ_VALU
     for q, m in zip((0, 150, 299), mins):
-        np.testing.assert_array_equal(m, idx.debug_bqmin(q), err_msg=f"block minima q{q}")
+        v = idx.debug_bqmin(q)
+        np.testing.assert_array_equal(m[: v.size], v, err_msg=f"block minima q{q}")
+        assert np.all(np.isinf(m[v.size:]))
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
     for q in range(0, len(queries), 12):
@@ -222,7 +224,8 @@ def test_bq_int8_deletes_allow_upserts(wv, oracle):
         m0 = idx.debug_bqmin(5)
         idx.set_option("bq8", 0)
         ref = idx.search_by_vector_batch(queries, k, allow=al)
-        np.testing.assert_array_equal(m0, idx.debug_bqmin(5))
+        v = idx.debug_bqmin(5)
+        np.testing.assert_array_equal(m0[: v.size], v)
         idx.set_option("bq8", 1)
         for a, b in zip(got, ref):
             np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))

@@ -128,7 +128,7 @@ SIGNATURES = {
     "wv_index_quant_begin": (C.c_int, [P, P, i64, i64, i32, P, P]),
     "wv_index_quant_blockmin": (C.c_int, [P, P, P]),
     "wv_index_quant_max_batch": (C.c_int, [P, i32, i32, P]),
-    "wv_index_debug_bqmin": (C.c_int, [P, i64, P, P]),
+    "wv_index_debug_bqmin": (C.c_int, [P, i64, P, P, P]),
     "wv_index_quant_replay": (C.c_int, [P, P, P, P, i32, P, P, P, P]),
     "wv_index_quant_replay_record": (C.c_int, [P, P, P, P, i32, P, P, P, P]),
     "wv_index_quant_finish": (C.c_int, [P, P, P, P, P, P, P, P, P, P]),

@@ -171,7 +171,12 @@ __global__ __launch_bounds__(256, 2) void k_bq_blockmin_lds(const uint64_t* __re
 // REC: record insertions (rec_* non-null); a separate instantiation keeps the
 // record's pointers out of the plain replay's scalar registers (the REC form
 // spilled 335 SGPRs: 26.6 ms vs 17.5 ms per C4 launch)
-template <int NW, bool REC>
+// BLK: rows per block minimum -- 256 (the VALU minima) or 32 (the integer-MFMA
+// minima, k_q8_blockkey<..., BQ>): with 32-row blocks a visited block is 32 rows
+// (lane = row, lanes 32-63 take the next visitable block speculatively: its
+// rows are offered only after the first block's, each against the heap top
+// of that moment, so the insertions are the in-order ones)
+template <int NW, bool REC, int BLK = BQBLK>
 __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ codes, int64_t ccap, int words,
                                                   const uint32_t* __restrict__ valid, int64_t nslots,
                                                   const uint64_t* __restrict__ qcodes, int64_t ldq,
@@ -200,6 +205,92 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
         if (REC) rec_n[li] = 0;
     }
     __syncthreads();
+    if constexpr (BLK == 32 && NW > 0) {
+        // 32-row blocks, software-pipelined: the codes of the next two visitable
+        // blocks (chosen under the top before the current insertions: a superset,
+        // a block that stops qualifying only offers rows ph_offer rejects) load
+        // while lane 0 inserts the current two blocks' rows.  Query words in
+        // registers; a block's valid word and codes load together.
+        uint64_t qw[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) qw[w] = w < words ? qc[(int64_t)w * ldq] : 0ull;
+        int64_t cb0 = 0;
+        float bmc = lane < nblk ? Bq[lane] : __builtin_inff();
+        float bmn = 64 + lane < nblk ? Bq[64 + lane] : __builtin_inff();
+        uint64_t cmask;
+        {
+            const int len = *s_len;
+            const float top = len > 0 ? hr[0].d : 0.f;
+            cmask = __ballot(lane < nblk && bmc != __builtin_inff() && (len < R || top > bmc));
+        }
+        auto next_blk = [&]() -> int64_t {
+            const int len = *s_len;
+            const float top = len > 0 ? hr[0].d : 0.f;
+            while (true) {
+                while (cmask) {
+                    const int j = __builtin_ctzll(cmask);
+                    cmask &= cmask - 1;
+                    if (len < R || top > __shfl(bmc, j)) return cb0 + j;
+                }
+                cb0 += 64;
+                if (cb0 >= nblk) return -1;
+                bmc = bmn;
+                bmn = cb0 + 64 + lane < nblk ? Bq[cb0 + 64 + lane] : __builtin_inff();
+                cmask = __ballot(cb0 + lane < nblk && bmc != __builtin_inff() && (len < R || top > bmc));
+            }
+        };
+        uint64_t x[NW];
+        uint32_t vword = 0;
+        auto load = [&](int64_t pa, int64_t pb) {
+            const int64_t blk = lane < 32 ? pa : pb;
+            const int64_t srow = blk * 32 + (lane & 31);
+            const bool in = blk >= 0 && srow < nslots;
+            vword = blk >= 0 ? valid[blk] : 0u;
+#pragma unroll
+            for (int w = 0; w < NW; w++) x[w] = (in && w < words) ? codes[(int64_t)w * ccap + srow] : 0ull;
+        };
+        int64_t pa = next_blk();
+        int64_t pb = pa >= 0 ? next_blk() : -1;
+        if (pa >= 0) load(pa, pb);
+        while (pa >= 0) {
+            const int64_t blk = lane < 32 ? pa : pb;
+            const int64_t srow = blk * 32 + (lane & 31);
+            const bool ok = blk >= 0 && srow < nslots && ((vword >> (lane & 31)) & 1u);
+            uint32_t h = 0;
+#pragma unroll
+            for (int w = 0; w < NW; w++) h += (uint32_t)__popcll(x[w] ^ qw[w]);
+            const float dist = (float)h;
+            const int64_t na = next_blk();
+            const int64_t nb = na >= 0 ? next_blk() : -1;
+            if (na >= 0) load(na, nb);  // in flight during the insertions below
+            const int len = *s_len;
+            const float top = len > 0 ? hr[0].d : 0.f;
+            uint64_t mask = __ballot(ok && (len < R || top > dist));
+            if (mask) {
+                s_d[lane] = dist;
+                __syncthreads();
+                if (lane == 0) {
+                    PHeap hp{hr, *s_len};
+                    while (mask) {  // block pa's rows (lanes 0-31), then pb's (32-63): id order
+                        const int jj = __builtin_ctzll(mask);
+                        mask &= mask - 1;
+                        const float dj = s_d[jj];
+                        const uint64_t sj = id_base + (uint64_t)((jj < 32 ? pa : pb) * 32 + (jj & 31));
+                        const bool ins = ph_offer(hp, R, sj, dj);
+                        if (REC && ins) {
+                            const int c = rec_n[li];
+                            if (c < cap) { rec_ids[(int64_t)li * cap + c] = sj; rec_d[(int64_t)li * cap + c] = dj; }
+                            rec_n[li] = c < cap ? c + 1 : cap + 1;
+                        }
+                    }
+                    *s_len = hp.len;
+                }
+                __syncthreads();
+            }
+            pa = na;
+            pb = nb;
+        }
+    } else
     for (int64_t b0 = 0; b0 < nblk; b0 += 64) {
         const float bm = (b0 + lane < nblk) ? Bq[b0 + lane] : __builtin_inff();
         int len = *s_len;

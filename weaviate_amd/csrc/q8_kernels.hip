@@ -250,8 +250,9 @@ struct Q8Args {
 // BQ (bq_kernels.hip's block minima on the matrix cores): X8 / Q8 are the
 // codes unpacked to +-1 (bit 0 -> +1, bit 1 -> -1; columns past the code bits
 // 0), so sum s_q s_x = bq_bits - 2 hamming exactly in int32; the kernel writes
-// the minimum hamming distance of every 256-row block (8 consecutive 32-row
-// blocks: the spans are whole 256-row blocks), +inf without a valid row.
+// the minimum hamming distance of every 32-row block (+inf without a valid
+// row) -- 8x finer than the VALU kernels' 256-row minima, so the replay
+// (k_bq_replay<.., 32>) recomputes 8x fewer rows per visited block.
 template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false>
 __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     constexpr int NPB = 2 * NC;                     // 1 KiB pieces per 32-row block
@@ -386,15 +387,8 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             if (lane < 32) krow[gb] = ISL2 ? m : -m;
         }
     };
-    // BQ: the running per-lane maxima over the current 256-row block, and
-    // whether the slot's last block completed one (its finish is deferred)
-    float run0 = -__builtin_inff(), run1 = -__builtin_inff();
-    bool pend = false;
     // stores issued in slot t (the deferred finish + block 0's), for vmcnt
-    auto stores_in = [&](int t) -> int {
-        if constexpr (BQ) return (t > 0 && ((((s0 + t - 1) * RB + RB - 1) & 7) == 7)) ? 1 : 0;
-        else return (t > 0 ? 1 : 0) + RB - 1;
-    };
+    auto stores_in = [&](int t) -> int { return (t > 0 ? 1 : 0) + RB - 1; };
     // a block's reduction over its rows (accumulators ac, valid word vw_, scale
     // sb_, L2 norms xa_/xb_) -> the lane's partial keys (p0, p1)
     auto reduce = [&](const i32x4_t (&ac)[2][2], uint32_t vw_, float sb_, const f32x4_t& xa_, const f32x4_t& xb_,
@@ -510,23 +504,17 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             }
             // the previous slot's last block: cross-lane combine + key store
             if constexpr (tt == P0) {
-                if (BQ ? pend : t > 0) {
+                if (t > 0) {
                     if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
                     finish(mp0, mp1, gbp);
                 }
             }
             // RB = 2: block 0 is reduced and stored beside block 1's MFMAs
-            // (BQ: folded into the 256-row block's maxima, never its last)
             if constexpr (RB == 2 && tt == NC + 1) {
                 if (!late) {
                     float p0, p1;
                     reduce(acc[0], vwv.x, sbv.x, xa[0], xb[0], p0, p1);
-                    if constexpr (BQ) {
-                        run0 = fmaxf(run0, p0);
-                        run1 = fmaxf(run1, p1);
-                    } else {
-                        finish(p0, p1, (s0 + t) * RB);
-                    }
+                    finish(p0, p1, (s0 + t) * RB);
                 }
             }
             if constexpr (STAG && tt == NC + P0) {
@@ -546,23 +534,12 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             reduce(acc[RB - 1], RB == 2 ? vwv.y : vwv.x, RB == 2 ? sbv.y : sbv.x, xa[RB - 1], xb[RB - 1], mp0, mp1);
         }
         gbp = (s0 + t) * RB + RB - 1;
-        if constexpr (BQ) {
-            run0 = fmaxf(run0, mp0);
-            run1 = fmaxf(run1, mp1);
-            pend = (gbp & 7) == 7;
-            if (pend) {
-                mp0 = run0;
-                mp1 = run1;
-                run0 = run1 = -__builtin_inff();
-                gbp >>= 3;
-            }
-        }
         // ---- end of the slot: the next group must have landed (every wave) ----
         if (t + 1 < nsteps) {
             // this wave's vector-memory ops after group t+1, in issue order: the
             // stores of slot t-1, the pieces of group t+2, the stores of slot t
             // (RB per slot; slot 0 has RB - 1)
-            if (!BQ && t >= 2 && t + 2 < nsteps) {
+            if (t >= 2 && t + 2 < nsteps) {
                 qs_wait_vm_c<2 * RB + P0>();
             } else {
                 const int y = (t >= 1 ? stores_in(t - 1) : 0) + stores_in(t) + (t + 2 < nsteps ? P0 : 0);
@@ -576,7 +553,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         }
         cur = nxt;
     }
-    if (nsteps > 0 && (!BQ || pend)) {
+    if (nsteps > 0) {
         if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
         finish(mp0, mp1, gbp);
     }

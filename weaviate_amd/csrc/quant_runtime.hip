@@ -4,6 +4,15 @@
 // (see rt_index.h for the unit split).
 #include "rt_index.h"
 
+static bool bq8_route(const wv_index* idx) { return idx->bq8 != nullptr && idx->bq8_opt && idx->bq_kernel != 1; }
+// rows per block minimum of the route: 32 on the integer MFMA (the block count
+// rounded to whole ring slots: two blocks per slot up to 768 bits), 256 otherwise
+static int64_t bq_blk(const wv_index* idx) { return bq8_route(idx) ? 32 : BQBLK; }
+static int64_t bq_nblk(const wv_index* idx) {
+    const int64_t nb = std::max<int64_t>((idx->hiwater + bq_blk(idx) - 1) / bq_blk(idx), 1);
+    return bq8_route(idx) && idx->dpb8b <= 768 ? round_up(nb, 2) : nb;
+}
+
 // searchByVectorQuantized (flat/index.go:460-532) for BQ indexes, every query
 // through the exact R-heap replay (bq_kernels.hip).  Outputs [nq][k].
 // Phase 1 of the BQ search: validation, query normalisation + codes, identity
@@ -35,8 +44,7 @@ static int bq_begin(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t n
     idx->stats.queries += (uint64_t)nq;
     idx->stats.batches++;
     idx->stats.replayed_queries += (uint64_t)nq;
-    const int64_t nslots = idx->hiwater;
-    const int64_t nblk = std::max<int64_t>((nslots + BQBLK - 1) / BQBLK, 1);
+    const int64_t nblk = bq_nblk(idx);
     // identity query list
     HIPCHK(idx->ident.ensure((size_t)nq * sizeof(int32_t)));
     {
@@ -45,7 +53,9 @@ static int bq_begin(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t n
         HIPCHK(hipMemcpyAsync(idx->ident.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
     }
     constexpr int QPB = 16;
-    *G_out = std::max<int64_t>(QPB, std::min<int64_t>(round_up(nq, QPB), ((1ll << 30) / (nblk * 4)) / QPB * QPB));
+    // one group of block minima up to 4 GiB (the 32-row minima of the integer
+    // route are 8x the 256-row ones: C4's 2048 x 195k blocks = 1.6 GB)
+    *G_out = std::max<int64_t>(QPB, std::min<int64_t>(round_up(nq, QPB), ((4ll << 30) / (nblk * 4)) / QPB * QPB));
     *R_out = R;
     // the integer-MFMA minima write whole 256-query groups
     HIPCHK(idx->bqmin.ensure((size_t)round_up(*G_out, 256) * nblk * sizeof(float)));
@@ -56,7 +66,6 @@ static int bq_begin(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t n
 
 // the block minima on the integer matrix cores: the +-1 planes of the codes
 // (k_bq_unpack8) through k_q8_blockkey<..., BQ>; hamming = (64 words - dot) / 2
-static bool bq8_route(const wv_index* idx) { return idx->bq8 != nullptr && idx->bq8_opt && idx->bq_kernel != 1; }
 
 static int bq_blockmin_i8(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t g0, int F, int64_t nblk,
                           float* bm) {
@@ -79,22 +88,22 @@ static int bq_blockmin_i8(wv_index* idx, hipStream_t s, const uint32_t* valid, i
     a.Q8 = idx->q8Qb.as<unsigned char>();
     a.qscale = nullptr;
     a.key = bm;
-    a.ldk = nblk;
+    a.ldk = nblk;  // 32-row blocks (a multiple of RB: bq_nblk)
     a.bq_bits = 64 * idx->words;
-    const int64_t steps_per_blk = 8 / RB;  // ring steps per 256-row block
-    a.nslots = nblk * steps_per_blk;
+    a.nslots = nblk / RB;
     a.nqg = (int)(Fp / 256);
-    // spans of whole 256-row blocks, whole rounds of one workgroup per CU
+    // whole rounds of one workgroup per CU
     int64_t nspans = 256 / std::gcd((int64_t)256, (int64_t)a.nqg);
     while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
     {   // a span's plane bytes below 4 GiB (32-bit buffer offsets)
-        const int64_t max_blk = ((1ll << 32) - 2 * 256ll * dpb8) / (256ll * dpb8);
-        nspans = std::max<int64_t>(nspans, (nblk + max_blk - 1) / max_blk);
+        const int64_t slot_b = (int64_t)RB * 32 * dpb8;
+        const int64_t max_sps = ((1ll << 32) - 2 * 256ll * dpb8) / slot_b;
+        nspans = std::max<int64_t>(nspans, (a.nslots + max_sps - 1) / max_sps);
     }
-    nspans = std::max<int64_t>(1, std::min<int64_t>(nspans, nblk));
-    const int64_t bps = (nblk + nspans - 1) / nspans;  // 256-row blocks per span
-    a.slots_per_span = (int)(bps * steps_per_blk);
-    a.nspans = (int)((nblk + bps - 1) / bps);
+    nspans = std::max<int64_t>(1, std::min<int64_t>(nspans, a.nslots));
+    const int64_t sps = (a.nslots + nspans - 1) / nspans;
+    a.slots_per_span = (int)sps;
+    a.nspans = (int)((a.nslots + sps - 1) / sps);
     const size_t lds = (size_t)3 * RB * 2 * NC * 1024 + 1024;
     dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
 #define WV_BQ8(NCV, RBV)                                                                                        \
@@ -130,7 +139,7 @@ static int bq_blockmin(wv_index* idx, hipStream_t s, const uint32_t* valid, int6
     constexpr int QPB = 16;
     const int64_t nq = idx->bq_nq;
     const int64_t nslots = idx->hiwater;
-    const int64_t nblk = std::max<int64_t>((nslots + BQBLK - 1) / BQBLK, 1);
+    const int64_t nblk = bq_nblk(idx);
     const int words = idx->words;
     const int nw = bq_nw(idx);
     const int32_t* qlist = idx->ident.as<int32_t>();
@@ -186,7 +195,8 @@ static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_
     const int64_t nq = idx->bq_nq;
     const int R = idx->bq_R;
     const int64_t nslots = idx->hiwater;
-    const int64_t nblk = std::max<int64_t>((nslots + BQBLK - 1) / BQBLK, 1);
+    const int64_t nblk = bq_nblk(idx);
+    const bool b32 = bq_blk(idx) == 32;
     const int words = idx->words;
     const int nw = bq_nw(idx);
     const int32_t* qlist = idx->ident.as<int32_t>();
@@ -194,15 +204,24 @@ static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_
     const float* bm = idx->bqmin.as<float>();
     const size_t lds_r = packed_replay_lds(R);
     if (lds_r > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "rescore limit %d too large for the replay heap", R);
-#define WV_RPR(NWV, RECV)                                                                                       \
+#define WV_RPB(NWV, RECV, BLKV)                                                                                 \
     do {                                                                                                        \
         if (lds_r > 64 * 1024)                                                                                  \
-            HIPCHK(hipFuncSetAttribute((const void*)k_bq_replay<NWV, RECV>,                                     \
+            HIPCHK(hipFuncSetAttribute((const void*)k_bq_replay<NWV, RECV, BLKV>,                               \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_r));                \
-        k_bq_replay<NWV, RECV><<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq, \
+        k_bq_replay<NWV, RECV, BLKV><<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq, \
                                                               qlist + g0, F, bm, nblk, R, idx->id_base, in_ids, \
                                                               in_d, in_len, pop, out_ids, out_d, out_n, rec_ids, \
                                                               rec_d, rec_n, cap);                               \
+    } while (0)
+#define WV_RPR(NWV, RECV)                                          \
+    do {                                                           \
+        if constexpr (NWV > 0) {                                   \
+            if (b32) WV_RPB(NWV, RECV, 32);                        \
+            else WV_RPB(NWV, RECV, BQBLK);                         \
+        } else {                                                   \
+            WV_RPB(NWV, RECV, BQBLK);                              \
+        }                                                          \
     } while (0)
 #define WV_RP(NWV) do { if (rec_n) WV_RPR(NWV, true); else WV_RPR(NWV, false); } while (0)
     switch (nw) {
@@ -216,6 +235,7 @@ static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_
     default: WV_RP(0); break;
     }
 #undef WV_RPR
+#undef WV_RPB
 #undef WV_RP
     HIPCHK(hipGetLastError());
     return WV_OK;
@@ -264,7 +284,8 @@ int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
     HIPCHK(idx->cn.ensure((size_t)nq * sizeof(int32_t)));
     HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
     idx->bq_last_nq = G >= nq ? nq : 0;  // debug hook: a one-group batch's minima stay in bqmin
-    idx->bq_last_nblk = std::max<int64_t>((idx->hiwater + BQBLK - 1) / BQBLK, 1);
+    idx->bq_last_nblk = bq_nblk(idx);
+    idx->bq_last_blk = bq_blk(idx);
     for (int64_t g0 = 0; g0 < nq; g0 += G) {
         const int F = (int)std::min<int64_t>(G, nq - g0);
         rc = bq_blockmin(idx, s, valid, g0, F);
@@ -287,8 +308,9 @@ int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
     return WV_OK;
 }
 
-extern "C" int wv_index_debug_bqmin(wv_index* idx, int64_t q, float* mins, int64_t* nblk) {
+extern "C" int wv_index_debug_bqmin(wv_index* idx, int64_t q, float* mins, int64_t* nblk, int64_t* blk_rows) {
     if (!idx || !nblk) return set_err(WV_ERR_INVALID, "nil argument");
+    if (blk_rows) *blk_rows = idx->bq_last_blk;
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
     if (idx->compression != WV_COMPRESSION_BQ || idx->bq_last_nq <= 0 || q < 0 || q >= idx->bq_last_nq)
@@ -349,7 +371,7 @@ extern "C" int wv_index_bq_bounds(wv_index* idx, float* d_out, void* stream) {
     HIPCHK(hipSetDevice(idx->device));
     if (idx->bq_nq <= 0) return set_err(WV_ERR_INVALID, "bq_bounds: no batch begun");
     hipStream_t s = (hipStream_t)stream;
-    const int64_t nblk = std::max<int64_t>((idx->hiwater + BQBLK - 1) / BQBLK, 1);
+    const int64_t nblk = bq_nblk(idx);
     const int nbins = idx->words * 64 + 1;
     const size_t lds = (size_t)nbins * sizeof(uint32_t);
     if (lds > 64 * 1024)

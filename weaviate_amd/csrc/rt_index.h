@@ -118,7 +118,7 @@ struct wv_index {
     unsigned char* bq8 = nullptr;
     int dpb8b = 0;
     int bq8_opt = 1;
-    int64_t bq_last_nq = 0, bq_last_nblk = 0;
+    int64_t bq_last_nq = 0, bq_last_nblk = 0, bq_last_blk = 256;
     int scan_window = 1;         // option scan_window: an allow list scans only [allow.Min, allow.Max]
     // gathered allow-list search: a sparse allow list's rows (ascending id) as
     // a temporary sub-index searched by the same pipeline (option gather_max:

@@ -185,13 +185,18 @@ class FlatIndex:
         check(self._l.wv_index_debug_blockkeys(self._h, int(q), _fptr(A), _fptr(eps), C.byref(nb)))
         return A, float(eps[0])
 
-    def debug_bqmin(self, q: int) -> np.ndarray:
-        """Diagnostic: the 256-row block minima of hamming distances of query q
-        of the last BQ batch (wv_index_debug_bqmin in include/wv_knn.h)."""
-        nb = C.c_int64(0)
-        check(self._l.wv_index_debug_bqmin(self._h, int(q), None, C.byref(nb)))
+    def debug_bqmin(self, q: int, rows: int = 256) -> np.ndarray:
+        """Diagnostic: the block minima of hamming distances of query q of the
+        last BQ batch (wv_index_debug_bqmin in include/wv_knn.h), reduced to
+        blocks of `rows` rows (a multiple of the route's block size)."""
+        nb, br = C.c_int64(0), C.c_int64(0)
+        check(self._l.wv_index_debug_bqmin(self._h, int(q), None, C.byref(nb), C.byref(br)))
         out = np.zeros(nb.value, np.float32)
-        check(self._l.wv_index_debug_bqmin(self._h, int(q), _fptr(out), C.byref(nb)))
+        check(self._l.wv_index_debug_bqmin(self._h, int(q), _fptr(out), C.byref(nb), C.byref(br)))
+        f = rows // br.value
+        if f > 1:
+            m = -(-out.size // f) * f
+            out = np.concatenate([out, np.full(m - out.size, np.inf, np.float32)]).reshape(-1, f).min(axis=1)
         return out
 
     # -- product quantizer (compressionhelpers.ProductQuantizer) -----------
