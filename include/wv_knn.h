@@ -429,6 +429,7 @@ typedef struct wv_stats {
     double last_total_ms;
     uint64_t last_group_queries; /* queries in the timed (first) group of the last quantized batch */
     uint64_t last_route;     /* exact fp32 search route of the last batch: WV_ROUTE_* */
+    uint64_t last_scan_rows; /* slots the last host-API batch scanned (an allow list: its slot span) */
 } wv_stats;
 /* wv_stats.last_route: which key / select kernel the last exact batch ran */
 #define WV_ROUTE_NONE 0
@@ -454,9 +455,10 @@ int wv_index_debug_candidates(wv_index *idx, float *A, float *E, uint32_t *I, fl
 int wv_index_debug_blockkeys(wv_index *idx, int64_t q, float *A, float *eps, int64_t *nb);
 
 /* Diagnostic hook (tests) of the BQ search: query q of the last BQ batch (one
- * query group): the minimum hamming distance of every 256-row block
- * (+inf without a valid row) into mins[*nblk].  mins == NULL: *nblk only. */
-int wv_index_debug_bqmin(wv_index *idx, int64_t q, float *mins, int64_t *nblk);
+ * query group): the minimum hamming distance of every block of *blk_rows rows
+ * (256 on the VALU route, 32 on the integer-MFMA route; +inf without a valid
+ * row) into mins[*nblk].  mins == NULL: the sizes only. */
+int wv_index_debug_bqmin(wv_index *idx, int64_t q, float *mins, int64_t *nblk, int64_t *blk_rows);
 
 /* tuning / testing knobs: "margin" (extra candidates of the f32 select
  * kernel, default 8), "force_replay" (1 = resolve every query by heap

@@ -143,16 +143,18 @@ def test_q8_row_filter_equals_bf16_filter_and_unfiltered(wv, oracle, metric, var
 
 
 @pytest.mark.parametrize("metric,kind,d,k", [("cosine", 0, 768, 10), ("l2-squared", 1, 512, 100), ("dot", 0, 640, 10)])
-def test_q8_staggered_epilogue_same_keys(wv, oracle, metric, kind, d, k):
-    """q8_stag 1 (waves 4-7 reduce each block late) writes the same block keys
-    as the in-order schedule: identical results and block keys, both equal to
-    the oracle; corpus sizes that end mid-slot and mid-span."""
+@pytest.mark.parametrize("variant_opt", [{"q8_stag": 1}, {"q8_pf": 2}])
+def test_q8_staggered_epilogue_same_keys(wv, oracle, metric, kind, d, k, variant_opt):
+    """q8_stag 1 (waves 4-7 reduce each block late) and q8_pf 2 (fragment reads
+    two chunks ahead) write the same block keys as the default schedule:
+    identical results and block keys, both equal to the oracle; corpus sizes
+    that end mid-slot and mid-span."""
     n = 20000 + 37
     data = gen(oracle, kind, 81, n, d)
     queries = gen(oracle, kind, 82, 300, d)
     res, keys = [], []
-    for stag in (0, 1):
-        idx, orc = build_pair(wv, oracle, metric, "avx256", data, options={"q8_stag": stag})
+    for opt in ({}, variant_opt):
+        idx, orc = build_pair(wv, oracle, metric, "avx256", data, options=opt)
         res.append(idx.search_by_vector_batch(queries, k))
         assert idx.stats()["last_route"] == ROUTE_INT8
         keys.append([idx.debug_blockkeys(q)[0] for q in (0, 255, 299)])

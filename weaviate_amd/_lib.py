@@ -172,11 +172,13 @@ def load() -> C.CDLL:
         import torch  # noqa: F401
     except Exception:
         pass
-    if not os.path.exists(LIB_PATH):
+    # WV_LIB_PATH: a timing-experiment build (tools/build_dbg.sh) in place of the product library
+    path = os.environ.get("WV_LIB_PATH", LIB_PATH)
+    if not os.path.exists(path):
         raise RuntimeError(
-            f"weaviate_amd: {LIB_PATH} not built; run `python -m weaviate_amd.build` "
+            f"weaviate_amd: {path} not built; run `python -m weaviate_amd.build` "
             "(the HIP library is required, there is no CPU fallback)")
-    lib = C.CDLL(LIB_PATH)
+    lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

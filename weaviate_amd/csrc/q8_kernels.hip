@@ -253,7 +253,10 @@ struct Q8Args {
 // the minimum hamming distance of every 32-row block (+inf without a valid
 // row) -- 8x finer than the VALU kernels' 256-row minima, so the replay
 // (k_bq_replay<.., 32>) recomputes 8x fewer rows per visited block.
-template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false>
+// PF: A-fragment reads PF chunks ahead of their MFMAs (PF + 1 register sets).
+// DBG (timing experiments in a -DWV_QS_DBG build only, wrong results): bit 0
+// drops the plane DMA, bit 1 the MFMAs, bit 2 the block reductions and stores.
+template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false, int PF = 1, int DBG = 0>
 __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     constexpr int NPB = 2 * NC;                     // 1 KiB pieces per 32-row block
     constexpr int SLOT = RB * NPB * 1024;           // bytes per ring slot
@@ -264,6 +267,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     constexpr int NT = RB * NC;                     // chunks per slot
     constexpr int P0 = P + 2 + (ISL2 ? 1 : 0);      // vector-memory ops per group, per wave
     static_assert(P0 < NC, "the deferred key store must follow the slot's DMA pieces");
+    static_assert(PF >= 1 && PF + 1 < NC, "prefetch distance");
     static_assert(!STAG || RB == 2, "the stagger defers a slot's second block");
     static_assert(!BQ || (!ISL2 && !STAG), "BQ: integer maxima, in-order schedule");
     constexpr int X0 = 1;                           // chunk of the slot's extra LDS reads
@@ -319,6 +323,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     uint32_t ioff = (uint32_t)(((igb >> 3) - tile0) * TILE_B + (igb & 7) * 1024);
     auto issue_piece = [&](int j, int t, int slot) {
         if (j < P) {
+            if constexpr (DBG & 1) return;
             const int p = wave + 8 * j;
             const int rb = p / NPB, c = p % NPB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(size_t)(ring + (unsigned)(slot * SLOT + (rb * NPB + c) * 1024)),
@@ -352,21 +357,32 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     // lane (i = lane&15, kq = lane>>4) reads row 16m+i, columns 64c+16kq..+15
     // = piece 2c + (kq>>1), bytes 16(kq&1).. of the row (linear image)
     const unsigned l16 = (unsigned)(((lane >> 5) & 1) * 1024 + (lane & 15) * 32 + 16 * ((lane >> 4) & 1));
-    i32x4_t B2[2][2];  // A fragments [chunk & 1][row half m]
+    constexpr int NB2 = PF + 1;
+    i32x4_t B2[NB2][2];  // A fragments [chunk % NB2][row half m]
+    // the first PF chunks of a slot, right after its barrier
+    auto head_reads = [&](unsigned sbh) {
+        static_for<0, PF>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if constexpr (j < NT) {
+                constexpr int o = (j / NC * NPB + 2 * (j % NC)) * 1024;
+                B2[j % NB2][0] = lds_ld16_o<o>(sbh);
+                B2[j % NB2][1] = lds_ld16_o<o + 512>(sbh);
+            }
+        });
+    };
     if (nsteps > 0) {
         issue_group(0, 0);
         if (nsteps > 1) issue_group(1, 1);
         qs_wait_vm(nsteps > 1 ? P0 : 0);  // group 0 landed, group 1 may stay in flight
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        const unsigned sb0 = ring + l16;
-        B2[0][0] = lds_ld16_o<0>(sb0);
-        B2[0][1] = lds_ld16_o<512>(sb0);
+        head_reads(ring + l16);
     }
     // the pending block (a slot's last): per query half n the lane's partial
     // key before the cross-lane combine
     float mp0 = 0.f, mp1 = 0.f;
     int64_t gbp = 0;
+    int dbg_sink = 0;  // DBG & 4: keeps the MFMAs live without the reductions; DBG & 8: the keys without stores
     auto finish = [&](float p0, float p1, int64_t gb) {
         // lanes g*16 + j (g = 0..3) hold partial keys of query 16n + j
         float m0 = p0, m1 = p1;
@@ -381,6 +397,10 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         // lanes 0-15: queries j (n = 0) in m0, 16 + j in m1 -> lanes 16-31 take m1
         const auto c01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m1), false, false);
         const float m = __uint_as_float(c01[0]);
+        if constexpr ((DBG & 8) != 0) {
+            dbg_sink ^= __float_as_int(m);
+            return;
+        }
         if constexpr (BQ) {
             if (lane < 32) krow[gb] = m == -__builtin_inff() ? __builtin_inff() : 0.5f * ((float)a.bq_bits - m);
         } else {
@@ -399,35 +419,53 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         const uint32_t vl = vw >> (4 * ((lane >> 4) & 3));
         const float s0f = sqA * sbf, s1f = sqB * sbf;
         float mn[2];
+        // the all-valid case (every block but a span's ragged tail, deletions and
+        // allow lists) is one uniform branch around both query halves, so the
+        // masked form's bit tests are not computed for it
+        if (vw == 0xFFFFFFFFu) {
 #pragma unroll
-        for (int n = 0; n < 2; n++) {
-            if constexpr (ISL2) {
-                const float cn = -2.f * (n ? s1f : s0f);
-                float m = __builtin_inff();
+            for (int n = 0; n < 2; n++) {
+                if constexpr (ISL2) {
+                    const float cn = -2.f * (n ? s1f : s0f);
+                    float m = __builtin_inff();
 #pragma unroll
-                for (int mm = 0; mm < 2; mm++)
+                    for (int mm = 0; mm < 2; mm++)
 #pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const float v = fmaf(cn, (float)ac[mm][n][r], mm ? xb_[r] : xa_[r]);
-                        m = fminf(m, ((vl >> (16 * mm + r)) & 1u) ? v : __builtin_inff());
-                    }
-                mn[n] = m;
-            } else {
-                int mi;
-                if (vw == 0xFFFFFFFFu) {
-                    mi = max(max(max(ac[0][n][0], ac[0][n][1]), max(ac[0][n][2], ac[0][n][3])),
-                             max(max(ac[1][n][0], ac[1][n][1]), max(ac[1][n][2], ac[1][n][3])));
+                        for (int r = 0; r < 4; r++)
+                            m = fminf(m, fmaf(cn, (float)ac[mm][n][r], mm ? xb_[r] : xa_[r]));
+                    mn[n] = m;
                 } else {
-                    mi = Q8_NONE;
+                    const int mi = max(max(max(ac[0][n][0], ac[0][n][1]), max(ac[0][n][2], ac[0][n][3])),
+                                       max(max(ac[1][n][0], ac[1][n][1]), max(ac[1][n][2], ac[1][n][3])));
+                    if constexpr (BQ) mn[n] = (float)mi;
+                    else mn[n] = (n ? s1f : s0f) * (float)mi;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                if constexpr (ISL2) {
+                    const float cn = -2.f * (n ? s1f : s0f);
+                    float m = __builtin_inff();
+#pragma unroll
+                    for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const float v = fmaf(cn, (float)ac[mm][n][r], mm ? xb_[r] : xa_[r]);
+                            m = fminf(m, ((vl >> (16 * mm + r)) & 1u) ? v : __builtin_inff());
+                        }
+                    mn[n] = m;
+                } else {
+                    int mi = Q8_NONE;
 #pragma unroll
                     for (int mm = 0; mm < 2; mm++)
 #pragma unroll
                         for (int r = 0; r < 4; r++)
                             mi = max(mi, ((vl >> (16 * mm + r)) & 1u) ? ac[mm][n][r] : Q8_NONE);
+                    // the scale is positive: the largest S is the largest product
+                    if constexpr (BQ) mn[n] = mi == Q8_NONE ? -__builtin_inff() : (float)mi;
+                    else mn[n] = mi == Q8_NONE ? -__builtin_inff() : (n ? s1f : s0f) * (float)mi;
                 }
-                // the scale is positive: the largest S is the largest product
-                if constexpr (BQ) mn[n] = mi == Q8_NONE ? -__builtin_inff() : (float)mi;
-                else mn[n] = mi == Q8_NONE ? -__builtin_inff() : (n ? s1f : s0f) * (float)mi;
             }
         }
         p0 = mn[0];
@@ -445,7 +483,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         const int nxt = cur == NBUF - 1 ? 0 : cur + 1;
         const int gslot = cur == 0 ? NBUF - 1 : cur - 1;  // slot of group t+2
         const unsigned sbase = ring + (unsigned)(cur * SLOT) + l16;
-        const bool dma = t + 2 < nsteps;
+        const int dma = __builtin_amdgcn_readfirstlane(t + 2 < nsteps ? 1 : 0);  // uniform: a scalar branch
         const unsigned sm = (unsigned)(t & 3);
         uint2 vwv;
         float2 sbv;
@@ -457,11 +495,6 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         static_for<0, NT>([&](auto ttc) {
             constexpr int tt = decltype(ttc)::value;
             constexpr int rb = tt / NC, c = tt % NC;
-            if constexpr (tt + 1 < NT) {
-                constexpr int o1 = ((tt + 1) / NC * NPB + 2 * ((tt + 1) % NC)) * 1024;
-                B2[(tt + 1) & 1][0] = lds_ld16_o<o1>(sbase);
-                B2[(tt + 1) & 1][1] = lds_ld16_o<o1 + 512>(sbase);
-            }
             if constexpr (tt == X0) {  // this slot's valid words, scales (+ L2 norms)
                 asm volatile("ds_read_b64 %0, %1" : "=v"(vwv) : "v"(vring + sm * 16u));
                 asm volatile("ds_read_b64 %0, %1" : "=v"(sbv) : "v"(sring + sm * 16u));
@@ -476,9 +509,17 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
                     }
                 }
             }
-            qs_wait_lgkm<(tt + 1 < NT ? 2 : 0) + (tt == X0 ? XE : 0)>();
-            asm volatile("" : "+v"(B2[tt & 1][0]), "+v"(B2[tt & 1][1]));
-            if constexpr (tt == X0 + 1) {
+            if constexpr (tt + PF < NT) {
+                constexpr int o1 = ((tt + PF) / NC * NPB + 2 * ((tt + PF) % NC)) * 1024;
+                B2[(tt + PF) % NB2][0] = lds_ld16_o<o1>(sbase);
+                B2[(tt + PF) % NB2][1] = lds_ld16_o<o1 + 512>(sbase);
+            }
+            // reads younger than chunk tt's: the chunks up to tt + PF, and the
+            // extras (issued at the start of step X0) while tt < X0 + PF
+            constexpr int ahead = (NT - 1 - tt) < PF ? (NT - 1 - tt) : PF;
+            qs_wait_lgkm<2 * ahead + ((tt >= X0 && tt < X0 + PF) ? XE : 0)>();
+            asm volatile("" : "+v"(B2[tt % NB2][0]), "+v"(B2[tt % NB2][1]));
+            if constexpr (tt == X0 + PF) {
                 if constexpr (ISL2) {
                     asm volatile("" : "+v"(vwv), "+v"(sbv), "+v"(xa[0]), "+v"(xb[0]));
                     if constexpr (RB == 2) asm volatile("" : "+v"(xa[RB - 1]), "+v"(xb[RB - 1]));
@@ -491,11 +532,12 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             for (int m = 0; m < 2; m++)
 #pragma unroll
                 for (int n = 0; n < 2; n++) {
+                    if constexpr (DBG & 2) { acc[rb][m][n] = B2[tt % NB2][m]; continue; }
                     if constexpr (c == 0)
-                        acc[rb][m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[tt & 1][m], Qf[2 * c + n],
+                        acc[rb][m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[tt % NB2][m], Qf[2 * c + n],
                                                                               i32x4_t{0, 0, 0, 0}, 0, 0, 0);
                     else
-                        acc[rb][m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[tt & 1][m], Qf[2 * c + n],
+                        acc[rb][m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[tt % NB2][m], Qf[2 * c + n],
                                                                               acc[rb][m][n], 0, 0, 0);
                 }
             // DMA of group t+2: one piece per chunk
@@ -503,14 +545,14 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
                 if (dma) issue_piece(tt, t + 2, gslot);
             }
             // the previous slot's last block: cross-lane combine + key store
-            if constexpr (tt == P0) {
+            if constexpr (tt == P0 && !(DBG & 4)) {
                 if (t > 0) {
                     if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
                     finish(mp0, mp1, gbp);
                 }
             }
             // RB = 2: block 0 is reduced and stored beside block 1's MFMAs
-            if constexpr (RB == 2 && tt == NC + 1) {
+            if constexpr (RB == 2 && tt == NC + 1 && !(DBG & 4)) {
                 if (!late) {
                     float p0, p1;
                     reduce(acc[0], vwv.x, sbv.x, xa[0], xb[0], p0, p1);
@@ -530,8 +572,12 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             dsb = sbv.y;
             dxa = xa[RB - 1];
             dxb = xb[RB - 1];
-        } else {
+        } else if constexpr (!(DBG & 4)) {
             reduce(acc[RB - 1], RB == 2 ? vwv.y : vwv.x, RB == 2 ? sbv.y : sbv.x, xa[RB - 1], xb[RB - 1], mp0, mp1);
+        } else {
+#pragma unroll
+            for (int r = 0; r < RB; r++)
+                dbg_sink ^= acc[r][0][0][0] ^ acc[r][0][1][0] ^ acc[r][1][0][0] ^ acc[r][1][1][0];
         }
         gbp = (s0 + t) * RB + RB - 1;
         // ---- end of the slot: the next group must have landed (every wave) ----
@@ -539,7 +585,9 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             // this wave's vector-memory ops after group t+1, in issue order: the
             // stores of slot t-1, the pieces of group t+2, the stores of slot t
             // (RB per slot; slot 0 has RB - 1)
-            if (t >= 2 && t + 2 < nsteps) {
+            if constexpr (DBG != 0) {
+                qs_wait_vm_c<0>();
+            } else if (t >= 2 && t + 2 < nsteps) {
                 qs_wait_vm_c<2 * RB + P0>();
             } else {
                 const int y = (t >= 1 ? stores_in(t - 1) : 0) + stores_in(t) + (t + 2 < nsteps ? P0 : 0);
@@ -547,15 +595,16 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             }
             __builtin_amdgcn_s_barrier();  // slot t is free; slot t+1 has landed for every wave
             __builtin_amdgcn_sched_barrier(0);
-            const unsigned sbn = ring + (unsigned)(nxt * SLOT) + l16;
-            B2[0][0] = lds_ld16_o<0>(sbn);
-            B2[0][1] = lds_ld16_o<512>(sbn);
+            head_reads(ring + (unsigned)(nxt * SLOT) + l16);
         }
         cur = nxt;
     }
-    if (nsteps > 0) {
+    if (nsteps > 0 && !(DBG & 4)) {
         if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
         finish(mp0, mp1, gbp);
+    }
+    if constexpr ((DBG & 12) != 0) {
+        if (a.ldk == -1234567) krow[0] = (float)dbg_sink;  // never true: the sink stays live
     }
 }
 

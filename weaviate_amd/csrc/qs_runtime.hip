@@ -154,13 +154,20 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     } while (0)
 #define WV_QSWN(L2V)                                   \
     if (NK == 64) WV_QSW(64, L2V, 4); else WV_QSW(96, L2V, 3);
-#define WV_Q8S(NCV, RBV, L2V, STV)                                                                             \
+#define WV_Q8S(NCV, RBV, L2V, STV, PFV)                                                                        \
     do {                                                                                                       \
-        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, RBV, L2V, STV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-        k_q8_blockkey<NCV, RBV, L2V, STV><<<grid, 512, lds, s>>>(q8a);                                          \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, RBV, L2V, STV, false, PFV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey<NCV, RBV, L2V, STV, false, PFV><<<grid, 512, lds, s>>>(q8a);                              \
     } while (0)
-#define WV_Q8(NCV, RBV, L2V) WV_Q8S(NCV, RBV, L2V, false)
-#define WV_Q8T(NCV, L2V) do { if (idx->q8_stag) WV_Q8S(NCV, 2, L2V, true); else WV_Q8S(NCV, 2, L2V, false); } while (0)
+#define WV_Q8(NCV, RBV, L2V) do { if (idx->q8_pf == 2) WV_Q8S(NCV, RBV, L2V, false, 2); else WV_Q8S(NCV, RBV, L2V, false, 1); } while (0)
+#ifdef WV_QS_DBG  // timing experiments (k_q8_blockkey DBG bits), not in the product build
+#define WV_Q8D(DV)                                                                                             \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<12, 2, false, false, false, 1, DV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey<12, 2, false, false, false, 1, DV><<<grid, 512, lds, s>>>(q8a);                           \
+    } while (0)
+#endif
+#define WV_Q8T(NCV, L2V) do { if (idx->q8_stag) WV_Q8S(NCV, 2, L2V, true, 1); else WV_Q8(NCV, 2, L2V); } while (0)
 #define WV_Q8N(L2V)                                    \
     switch (NC8) {                                     \
     case 8: WV_Q8T(8, L2V); break;                     \
@@ -185,6 +192,21 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             q8a.slots_per_span = a.slots_per_span;
             q8a.nspans = a.nspans;
             q8a.nqg = a.nqg;
+#ifdef WV_QS_DBG
+            if (idx->sel_dbg > 0 && !l2 && NC8 == 12) {
+                switch (idx->sel_dbg) {
+                case 1: WV_Q8D(1); break;
+                case 2: WV_Q8D(2); break;
+                case 3: WV_Q8D(3); break;
+                case 4: WV_Q8D(4); break;
+                case 5: WV_Q8D(5); break;
+                case 6: WV_Q8D(6); break;
+                case 8: WV_Q8D(8); break;
+                case 9: WV_Q8D(9); break;
+                default: WV_Q8D(7); break;
+                }
+            } else
+#endif
             if (idx->q8_shape == 32) {
 #define WV_Q832(NCV, RBV, L2V)                                                                                \
     do {                                                                                                      \
@@ -231,6 +253,12 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         HIPCHK(hipGetLastError());
         if (time_it) { HIPCHK(hipEventRecord(idx->ev1, s)); idx->timed = 1; }
         idx->stats.mfma_launches++;
+#ifdef WV_QS_DBG  // timing experiments: the keys are wrong, skip the rest of the pipeline
+        if (idx->sel_dbg > 0) {
+            HIPCHK(hipMemsetAsync(o_n + c0, 0, (size_t)cn * sizeof(int32_t), s));
+            continue;
+        }
+#endif
         }
         // ---- candidate blocks, exact rows, proof ----
         int32_t* flags = phase ? idx->qsFlags.as<int32_t>() : o_flags ? o_flags + c0 : idx->qsFlags.as<int32_t>();

@@ -147,7 +147,8 @@ struct wv_index {
     int q8_opt = 1;                 // option q8: block keys from the int8 plane (1) or the bf16 plane (0)
     int q8_R = 0;                   // option q8_R: candidate lists for int8 keys (0: R = 8, 448 blocks)
     int q8_shape = 16;              // option q8_shape: 16 = v_mfma_i32_16x16x64_i8 kernel, 32 = 32x32x32
-    int q8_stag = 0;                // option q8_stag: waves 4-7 reduce each block P0 chunks late (RB = 2)
+    int q8_stag = 0;
+    int q8_pf = 1;                  // option q8_pf: A-fragment reads 1 or 2 chunks ahead                // option q8_stag: waves 4-7 reduce each block P0 chunks late (RB = 2)
     int q8_filter = 1;              // option q8_filter: the exact pass bounds rows from the int8 plane (1) or bf16 (0)
     unsigned char* X8 = nullptr;
     float* sb8 = nullptr;

@@ -705,6 +705,10 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "q8") idx->q8_opt = value ? 1 : 0;  // int8 block keys (default 1) or bf16 (0)
     else if (k == "q8_filter") idx->q8_filter = value ? 1 : 0;
     else if (k == "q8_stag") idx->q8_stag = value ? 1 : 0;  // staggered epilogues of the int8 key kernel
+    else if (k == "q8_pf") {  // int8 key kernel: A-fragment prefetch distance
+        if (value != 1 && value != 2) return set_err(WV_ERR_INVALID, "q8_pf must be 1 or 2");
+        idx->q8_pf = (int)value;
+    }
     else if (k == "q8_shape") {  // int8 key kernel MFMA shape
         if (value != 16 && value != 32) return set_err(WV_ERR_INVALID, "q8_shape must be 16 or 32");
         idx->q8_shape = (int)value;
@@ -1218,7 +1222,7 @@ static int subindex_build(wv_index* idx, hipStream_t s, const std::vector<uint32
     sb->use_qs = idx->use_qs;
     set_dims(sb, idx->dims);
     sb->kernel_opt = idx->kernel_opt; sb->q8_opt = idx->q8_opt; sb->q8_R = idx->q8_R; sb->q8_filter = idx->q8_filter;
-    sb->q8_stag = idx->q8_stag; sb->q8_shape = idx->q8_shape; sb->exact_filter = idx->exact_filter; sb->exact_bm = idx->exact_bm;
+    sb->q8_stag = idx->q8_stag; sb->q8_shape = idx->q8_shape; sb->q8_pf = idx->q8_pf; sb->exact_filter = idx->exact_filter; sb->exact_bm = idx->exact_bm;
     sb->exact_cap = idx->exact_cap; sb->replay_par = idx->replay_par; sb->margin = idx->margin;
     sb->gemv_max = idx->gemv_max; sb->gemv_wg = idx->gemv_wg; sb->exact_multi = idx->exact_multi;
     sb->force_replay = idx->force_replay; sb->qs_force_flag = idx->qs_force_flag; sb->timing = idx->timing;
