@@ -254,8 +254,19 @@ struct Q8Args {
 // row) -- 8x finer than the VALU kernels' 256-row minima, so the replay
 // (k_bq_replay<.., 32>) recomputes 8x fewer rows per visited block.
 // PF: A-fragment reads PF chunks ahead of their MFMAs (PF + 1 register sets).
+// PAIR (RB = 2, in-order schedule): a slot's two blocks share one cross-lane
+// combine and one 64-lane key store.  Each block's reduction leaves, per lane,
+// the partial of its row group for both query halves -- raw int32 maxima for
+// dot/cos/BQ (the positive scale commutes with the maximum, so it is applied
+// once after the combine), fl(xnorm2 - 2S) minima for L2 -- and the combine is
+// a transpose-reduction: permlane32 swaps pair (A half 0, A half 1) and (B half
+// 0, B half 1), one permlane16 swap pairs the two results, three max/min ops
+// in all, ending with lane group G = lane >> 4 holding block A / B (G & 1) of
+// query half G >> 1.  The unpaired form takes five swaps and four ops per
+// block and stores from 32 lanes.
 // DBG (timing experiments in a -DWV_QS_DBG build only, wrong results): bit 0
-// drops the plane DMA, bit 1 the MFMAs, bit 2 the block reductions and stores.
+// drops the plane DMA, bit 1 the MFMAs, bit 2 the block reductions and stores,
+// bit 3 the key stores only.
 template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false, int PF = 1, int DBG = 0>
 __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     constexpr int NPB = 2 * NC;                     // 1 KiB pieces per 32-row block
@@ -301,6 +312,9 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     const int64_t q0 = (int64_t)grp * 256 + wave * 32;
     const float sqA = BQ ? 1.f : a.qscale[q0 + (lane & 15)];
     const float sqB = BQ ? 1.f : a.qscale[q0 + 16 + (lane & 15)];
+    constexpr bool PAIR = RB == 2 && !STAG;
+    // PAIR: the query of the lane's combined key (group G: half G >> 1)
+    const float sqO = (BQ || !PAIR) ? 1.f : a.qscale[q0 + (lane & 15) + 16 * (lane >> 5)];
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the query loads before the DMA ring
 
     const int64_t s0 = (int64_t)span * a.slots_per_span;
@@ -407,8 +421,39 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             if (lane < 32) krow[gb] = ISL2 ? m : -m;
         }
     };
+    // PAIR: the combine of a slot's two blocks (raw partials rA*, rB*, block
+    // scales sbA_, sbB_) and the 64-lane store of blocks gbA, gbA + 1
+    auto finish2 = [&](uint32_t rA0, uint32_t rA1, uint32_t rB0, uint32_t rB1, float sbA_, float sbB_, int64_t gbA) {
+        auto op = [](uint32_t x, uint32_t y) -> uint32_t {
+            if constexpr (ISL2) return __float_as_uint(fminf(__uint_as_float(x), __uint_as_float(y)));
+            else return (uint32_t)max((int)x, (int)y);
+        };
+        const auto sa = __builtin_amdgcn_permlane32_swap(rA0, rA1, false, false);
+        const auto sb2 = __builtin_amdgcn_permlane32_swap(rB0, rB1, false, false);
+        const uint32_t w = op(sa[0], sa[1]), u = op(sb2[0], sb2[1]);
+        const auto sw = __builtin_amdgcn_permlane16_swap(w, u, false, false);
+        const uint32_t r = op(sw[0], sw[1]);
+        float key;
+        if constexpr (ISL2) {
+            key = __uint_as_float(r);
+        } else {
+            const int mi = (int)r;
+            if constexpr (BQ) {
+                key = mi == Q8_NONE ? __builtin_inff() : 0.5f * ((float)a.bq_bits - (float)mi);
+            } else {
+                const float s = sqO * (((lane >> 4) & 1) ? sbB_ : sbA_);
+                key = mi == Q8_NONE ? __builtin_inff() : -(s * (float)mi);
+            }
+        }
+        if constexpr ((DBG & 8) != 0) {
+            dbg_sink ^= __float_as_int(key);
+            return;
+        }
+        a.key[(q0 + (lane & 15) + 16 * (lane >> 5)) * a.ldk + gbA + ((lane >> 4) & 1)] = key;
+    };
     // stores issued in slot t (the deferred finish + block 0's), for vmcnt
-    auto stores_in = [&](int t) -> int { return (t > 0 ? 1 : 0) + RB - 1; };
+    auto stores_in = [&](int t) -> int { return (t > 0 ? 1 : 0) + (PAIR ? 0 : RB - 1); };
+    constexpr int SPS = PAIR ? 1 : RB;  // key stores per slot
     // a block's reduction over its rows (accumulators ac, valid word vw_, scale
     // sb_, L2 norms xa_/xb_) -> the lane's partial keys (p0, p1)
     auto reduce = [&](const i32x4_t (&ac)[2][2], uint32_t vw_, float sb_, const f32x4_t& xa_, const f32x4_t& xb_,
@@ -471,6 +516,38 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         p0 = mn[0];
         p1 = mn[1];
     };
+    // PAIR: a block's raw per-lane partials (see finish2)
+    auto reduce_raw = [&](const i32x4_t (&ac)[2][2], uint32_t vw_, float sb_, const f32x4_t& xa_, const f32x4_t& xb_,
+                          uint32_t& r0, uint32_t& r1) {
+        const uint32_t vw = __builtin_amdgcn_readfirstlane(vw_);
+        const uint32_t vl = vw >> (4 * ((lane >> 4) & 3));
+        uint32_t rr[2];
+        if constexpr (ISL2) {
+            float p0, p1;
+            reduce(ac, vw_, sb_, xa_, xb_, p0, p1);
+            rr[0] = __float_as_uint(p0);
+            rr[1] = __float_as_uint(p1);
+        } else if (vw == 0xFFFFFFFFu) {
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                rr[n] = (uint32_t)max(max(max(ac[0][n][0], ac[0][n][1]), max(ac[0][n][2], ac[0][n][3])),
+                                      max(max(ac[1][n][0], ac[1][n][1]), max(ac[1][n][2], ac[1][n][3])));
+        } else {
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                int mi = Q8_NONE;
+#pragma unroll
+                for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) mi = max(mi, ((vl >> (16 * mm + r)) & 1u) ? ac[mm][n][r] : Q8_NONE);
+                rr[n] = (uint32_t)mi;
+            }
+        }
+        r0 = rr[0];
+        r1 = rr[1];
+    };
+    uint32_t pA0 = 0, pA1 = 0, pB0 = 0, pB1 = 0;  // PAIR: the pending slot's raw partials
+    float psA = 0.f, psB = 0.f;                    // and its block scales
     i32x4_t acc[RB][2][2];
     // STAG, waves 4-7: the previous slot's last block is reduced late, from its
     // accumulators (kept: acc[1] is rewritten only from chunk NC on) and these
@@ -547,12 +624,18 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             // the previous slot's last block: cross-lane combine + key store
             if constexpr (tt == P0 && !(DBG & 4)) {
                 if (t > 0) {
-                    if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
-                    finish(mp0, mp1, gbp);
+                    if constexpr (PAIR) {
+                        finish2(pA0, pA1, pB0, pB1, psA, psB, gbp);
+                    } else {
+                        if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
+                        finish(mp0, mp1, gbp);
+                    }
                 }
             }
+            // PAIR: block 0's partials beside block 1's MFMAs (stored with block 1)
+            if constexpr (PAIR && tt == NC + 1 && !(DBG & 4)) reduce_raw(acc[0], vwv.x, sbv.x, xa[0], xb[0], pA0, pA1);
             // RB = 2: block 0 is reduced and stored beside block 1's MFMAs
-            if constexpr (RB == 2 && tt == NC + 1 && !(DBG & 4)) {
+            if constexpr (RB == 2 && !PAIR && tt == NC + 1 && !(DBG & 4)) {
                 if (!late) {
                     float p0, p1;
                     reduce(acc[0], vwv.x, sbv.x, xa[0], xb[0], p0, p1);
@@ -572,6 +655,10 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             dsb = sbv.y;
             dxa = xa[RB - 1];
             dxb = xb[RB - 1];
+        } else if constexpr (PAIR && !(DBG & 4)) {
+            reduce_raw(acc[1], vwv.y, sbv.y, xa[1], xb[1], pB0, pB1);
+            psA = sbv.x;
+            psB = sbv.y;
         } else if constexpr (!(DBG & 4)) {
             reduce(acc[RB - 1], RB == 2 ? vwv.y : vwv.x, RB == 2 ? sbv.y : sbv.x, xa[RB - 1], xb[RB - 1], mp0, mp1);
         } else {
@@ -579,7 +666,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             for (int r = 0; r < RB; r++)
                 dbg_sink ^= acc[r][0][0][0] ^ acc[r][0][1][0] ^ acc[r][1][0][0] ^ acc[r][1][1][0];
         }
-        gbp = (s0 + t) * RB + RB - 1;
+        gbp = (s0 + t) * RB + (PAIR ? 0 : RB - 1);
         // ---- end of the slot: the next group must have landed (every wave) ----
         if (t + 1 < nsteps) {
             // this wave's vector-memory ops after group t+1, in issue order: the
@@ -588,7 +675,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             if constexpr (DBG != 0) {
                 qs_wait_vm_c<0>();
             } else if (t >= 2 && t + 2 < nsteps) {
-                qs_wait_vm_c<2 * RB + P0>();
+                qs_wait_vm_c<2 * SPS + P0>();
             } else {
                 const int y = (t >= 1 ? stores_in(t - 1) : 0) + stores_in(t) + (t + 2 < nsteps ? P0 : 0);
                 qs_wait_vm(y);
@@ -600,8 +687,12 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         cur = nxt;
     }
     if (nsteps > 0 && !(DBG & 4)) {
-        if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
-        finish(mp0, mp1, gbp);
+        if constexpr (PAIR) {
+            finish2(pA0, pA1, pB0, pB1, psA, psB, gbp);
+        } else {
+            if (late) reduce(acc[RB - 1], dvw, dsb, dxa, dxb, mp0, mp1);
+            finish(mp0, mp1, gbp);
+        }
     }
     if constexpr ((DBG & 12) != 0) {
         if (a.ldk == -1234567) krow[0] = (float)dbg_sink;  // never true: the sink stays live
