@@ -241,22 +241,36 @@ def test_removed_select_kernels_rejected(wv, oracle):
     ("cosine", 0, 30000, 768, 10, 1), ("cosine", 0, 30000, 768, 10, 8), ("l2-squared", 0, 20000, 100, 24, 3),
     ("dot", 2, 12000, 40, 5, 5), ("l2-squared", 1, 8000, 2500, 10, 6), ("cosine", 0, 5000, 1536, 32 - 8, 2)])
 def test_gemv_small_batches(wv, oracle, metric, kind, n, d, k, nq):
-    """Batches <= gemv_max take k_gemv_select (the HBM-streaming GEMV path) by default."""
+    """Small batches: the default route and the HBM-streaming GEMV (k_gemv_select).
+
+    Measured on C3 (profiles/r04_small_batch_c3.jsonl, tools/small_batch.py):
+    with block-key planes the padded int8 key pass beats the GEMV at every
+    B = 1..256 (B = 1: 3.39 vs 5.11 ms), so small batches keep the block-key
+    route wherever planes exist (d <= 1536) and take the GEMV only without them;
+    `kernel = 6` forces the GEMV.  Both routes are asserted and oracle-checked.
+    """
     data = gen(oracle, kind, 91, n, d)
     queries = gen(oracle, kind, 92, nq, d)
     idx, orc = build_pair(wv, oracle, metric, "avx256", data)
     idx.delete(*range(3, n, 17))
     orc.delete(list(range(3, n, 17)))
-    before = idx.stats()["replayed_queries"]
-    ids, dists, counts = idx.search_by_vector_batch(queries, k)
-    for qi in range(nq):
-        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
-    if kind == 0:  # continuous data: the fp32 error bound proves every query, no replay
-        assert idx.stats()["replayed_queries"] == before
-    allow = list(range(5, n, 3))
-    ids, dists, counts = idx.search_by_vector_batch(queries, k, allow=wv.AllowList(allow))
-    for qi in range(nq):
-        assert_same(orc.search(queries[qi], k, allow=allow), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"a{qi}")
+    planes = d <= 1536
+    for forced in (False, True):
+        idx.set_option("kernel", 6 if forced else 0)
+        expect = "gemv" if forced or not planes else ("qs_bf16", "qs_w4", "qs_int8")
+        before = idx.stats()["replayed_queries"]
+        ids, dists, counts = idx.search_by_vector_batch(queries, k)
+        route = wv._lib.ROUTES[idx.stats()["last_route"]]
+        assert route in (expect if isinstance(expect, tuple) else (expect,)), (forced, route)
+        for qi in range(nq):
+            assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
+        if kind == 0 and route == "gemv":  # continuous data: the fp32 error bound proves every query
+            assert idx.stats()["replayed_queries"] == before
+        allow = list(range(5, n, 3))
+        ids, dists, counts = idx.search_by_vector_batch(queries, k, allow=wv.AllowList(allow))
+        for qi in range(nq):
+            assert_same(orc.search(queries[qi], k, allow=allow), ids[qi, :counts[qi]], dists[qi, :counts[qi]],
+                        f"a{qi}")
     idx.close()
 
 
@@ -508,4 +522,71 @@ def test_block_keys_above_768_dims(wv, oracle, metric, kind, variant, n, d, k, o
         worst = max(worst, float(err.max() / eps))
         assert (err <= eps).all(), f"q{q}: block-key error {err.max()} > eps {eps}"
     print(f"d={d}: max |A_block - min E| / eps = {worst:.4f}")
+    idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,n,d,k,nq", [
+    ("l2-squared", 0, 20000, 128, 10, 100),   # C1-shaped: bf16 block keys
+    ("cosine", 0, 12000, 768, 10, 64),        # int8 block keys
+    ("l2-squared", 1, 9000, 128, 100, 50),    # integer ties: the heap replay inside the graph
+])
+def test_search_device_graph_replay(wv, oracle, metric, kind, n, d, k, nq):
+    """A repeated identical wv_index_search_device call on a caller stream is
+    captured into a hipGraph on its second occurrence and replayed after; the
+    replays must equal the uncaptured path, count their queries in the stats,
+    and stop applying once the corpus changes (Add / Delete / options)."""
+    torch = pytest.importorskip("torch")
+    from weaviate_amd import _lib
+    lib = _lib.load()
+    data = gen(oracle, kind, 95, n, d)
+    queries = gen(oracle, kind, 96, nq, d)
+    idx, _ = build_pair(wv, oracle, metric, "avx256", data)
+    orc = oracle.OracleFlat(oracle.METRIC[metric], VARIANTS["avx256"], d, n + 8)  # room for the added rows
+    orc.add_batch(np.arange(n, dtype=np.uint64), data)
+    qd = torch.from_numpy(queries).cuda()
+    oi = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    od = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    on = torch.empty(nq, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.Stream()
+
+    def run():
+        oi.fill_(-1)
+        od.fill_(-1)
+        on.fill_(-1)
+        torch.cuda.synchronize()
+        _lib.check(lib.wv_index_search_device(idx._h, qd.data_ptr(), nq, d, k, 0, oi.data_ptr(), od.data_ptr(),
+                                              on.data_ptr(), None, stream.cuda_stream))
+        stream.synchronize()
+        return oi.cpu().numpy().copy(), od.cpu().numpy().copy(), on.cpu().numpy().copy()
+
+    def check(res, tag):
+        ids, dists, counts = res
+        for qi in range(0, nq, max(1, nq // 16)):
+            assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]].astype(np.uint64),
+                        dists[qi, :counts[qi]], f"{tag} q{qi}")
+
+    idx.set_option("graph", 0)
+    ref = run()
+    check(ref, "plain")
+    idx.set_option("graph", 1)
+    q0 = idx.stats()["queries"]
+    for rep in range(4):  # 1: uncaptured, 2: captured, 3-4: replays
+        got = run()
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b, err_msg=f"rep {rep}")
+    assert idx.stats()["queries"] - q0 == 4 * nq
+    # the corpus changes: near-copies of the first queries become their nearest rows
+    extra = (queries[:8] + np.float32(1e-3)).astype(np.float32)
+    new_ids = np.arange(n, n + 8, dtype=np.uint64)
+    idx.add_batch(new_ids, extra)
+    orc.add_batch(new_ids, extra)
+    got = run()
+    check(got, "after add")
+    assert set(range(n, n + 8)) & set(got[0][:8].ravel().tolist())
+    idx.delete(*range(n, n + 8))
+    orc.delete(list(range(n, n + 8)))
+    for rep in range(3):
+        got = run()
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b, err_msg=f"after delete rep {rep}")
     idx.close()

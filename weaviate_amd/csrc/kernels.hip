@@ -929,11 +929,16 @@ __global__ __launch_bounds__(64) void k_distance_pairs(const float* __restrict__
 // formed in parallel, the float32 sum runs serially in element order (every
 // lane adds the same readlane'd square, so the sum is wave-uniform), then the
 // divisions are parallel.
+// rows [n, n_pad) of out are zeroed (the padded query group)
 __global__ __launch_bounds__(256) void k_normalize_rows(const float* __restrict__ in, int64_t n, int d,
-                                                        float* __restrict__ out, int ld) {
+                                                        float* __restrict__ out, int ld, int64_t n_pad = 0) {
     const int lane = threadIdx.x & 63;
     const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= n) return;
+    if (i >= n) {
+        if (i < n_pad)
+            for (int c = lane; c < ld; c += 64) out[i * ld + c] = 0.f;
+        return;
+    }
     const float* src = in + i * d;
     float* dst = out + i * ld;
     float nrm = 0.f;
@@ -977,12 +982,13 @@ __global__ void k_bq_encode(const float* __restrict__ in, int64_t n, int d, int 
 }
 
 // copy rows into a zero-padded [n][ld] buffer (queries for l2 / dot)
-__global__ void k_copy_pad_rows(const float* __restrict__ in, int64_t n, int d, float* __restrict__ out, int ld) {
+__global__ void k_copy_pad_rows(const float* __restrict__ in, int64_t n, int d, float* __restrict__ out, int ld,
+                                int64_t n_pad) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n * ld) return;
+    if (i >= n_pad * ld) return;
     int64_t r = i / ld;
     int c = (int)(i % ld);
-    out[i] = c < d ? in[r * d + c] : 0.f;
+    out[i] = (r < n && c < d) ? in[r * d + c] : 0.f;
 }
 
 // squared norm of each padded row (approximate path + error bound only)

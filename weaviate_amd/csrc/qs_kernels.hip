@@ -938,7 +938,14 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
                                                     int32_t* __restrict__ ncand, int32_t* __restrict__ flags,
                                                     float* __restrict__ eps_out, const int32_t* __restrict__ qlist,
                                                     const uint32_t* __restrict__ qcount, float* __restrict__ topA,
-                                                    float* __restrict__ cap_out = nullptr) {
+                                                    float* __restrict__ cap_out = nullptr,
+                                                    uint32_t* __restrict__ list_ctr = nullptr) {
+    // the batch's flag-list cursors (k_flag_list counters[1] of the final and
+    // the overflow lists), reset here instead of by two fills
+    if (list_ctr && blockIdx.x == 0 && threadIdx.x == 0) {
+        list_ctr[1] = 0u;
+        list_ctr[3] = 0u;
+    }
     constexpr int L = 64 * (R - 1);
     constexpr int U = 16;
     __shared__ float sbk[4][64];
@@ -1339,8 +1346,9 @@ __global__ __launch_bounds__(256) void k_inv_count(const uint32_t* __restrict__ 
     for (int j = lane; j < nc; j += 64) atomicAdd(&cnt[cand[(int64_t)q * L + j]], 1u);
 }
 
-// exclusive prefix of cnt[0..nb) -> off[0..nb], cnt reset to 0 (the scatter's
-// cursors); one workgroup of 1024 threads
+// exclusive prefix of cnt[0..nb) -> off[0..nb]; cnt stays (the scatter counts
+// it back down to 0, so the next batch starts from a zeroed array without a
+// fill); one workgroup of 1024 threads
 __global__ __launch_bounds__(1024) void k_inv_scan(uint32_t* __restrict__ cnt, int64_t nb, uint32_t* __restrict__ off) {
     __shared__ uint32_t part[1024];
     const int t = threadIdx.x;
@@ -1361,7 +1369,6 @@ __global__ __launch_bounds__(1024) void k_inv_scan(uint32_t* __restrict__ cnt, i
         const uint32_t c = cnt[b];
         off[b] = run;
         run += c;
-        cnt[b] = 0;
     }
     if (t == 1023) off[nb] = part[1023];
 }
@@ -1376,7 +1383,7 @@ __global__ __launch_bounds__(256) void k_inv_scatter(const uint32_t* __restrict_
     const int nc = ncand[q];
     for (int j = lane; j < nc; j += 64) {
         const uint32_t b = cand[(int64_t)q * L + j];
-        pairs[off[b] + atomicAdd(&cur[b], 1u)] = ((uint32_t)q << 9) | (uint32_t)j;
+        pairs[off[b] + atomicSub(&cur[b], 1u) - 1u] = ((uint32_t)q << 9) | (uint32_t)j;
     }
 }
 

@@ -264,9 +264,12 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         int32_t* flags = phase ? idx->qsFlags.as<int32_t>() : o_flags ? o_flags + c0 : idx->qsFlags.as<int32_t>();
         int32_t* olist = idx->qsList.as<int32_t>() + qc;  // second half: the overflow list
         // select / exact pass RV over all queries (list == nullptr) or over the listed ones
+        // phase 0: the first select resets the flag-list cursors (qscount[1], [3])
+        const bool ctr_reset = phase == 0;
         auto sel = [&](int RV, const int32_t* list, const uint32_t* cnt, float* tA) {
             const unsigned gw = (unsigned)((cn + 3) / 4);
-#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>())
+            uint32_t* lc = (ctr_reset && !list) ? idx->qscount : nullptr;
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc)
             if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
 #undef WV_SELR
         };
@@ -295,7 +298,10 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             HIPCHK(idx->bmOff.ensure((size_t)(nb + 1) * sizeof(uint32_t)));
             HIPCHK(idx->bmPairs.ensure((size_t)cn * L * sizeof(uint32_t)));
             HIPCHK(idx->bmE.ensure((size_t)cn * ldE * sizeof(float)));
-            HIPCHK(hipMemsetAsync(idx->bmCnt.p, 0, (size_t)nb * sizeof(uint32_t), s));
+            // bmCnt is all-zero between batches (k_inv_scatter counts it down);
+            // a new or never-completed buffer is zeroed once
+            if (idx->bmCnt_zp != idx->bmCnt.p) HIPCHK(hipMemsetAsync(idx->bmCnt.p, 0, idx->bmCnt.bytes, s));
+            idx->bmCnt_zp = nullptr;
             const unsigned gw = (unsigned)((cn + 3) / 4);
             k_inv_count<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
                                            idx->bmCnt.as<uint32_t>());
@@ -303,6 +309,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             k_inv_scatter<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
                                              idx->bmOff.as<uint32_t>(), idx->bmCnt.as<uint32_t>(),
                                              idx->bmPairs.as<uint32_t>());
+            HIPCHK(hipGetLastError());
+            idx->bmCnt_zp = idx->bmCnt.p;
             launch_exact_bm(idx, s, metric, v5, Qn, nb, bm_lds, ldE);
             HIPCHK(hipGetLastError());
             exa(R, nullptr, nullptr, idx->bmE.as<float>(), ldE);
@@ -311,7 +319,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         }
         HIPCHK(hipGetLastError());
         if (R < 8) {  // candidate lists that overflowed (flag 2): again with the 448-block lists
-            HIPCHK(hipMemsetAsync(idx->qscount + 3, 0, sizeof(uint32_t), s));
+            if (!ctr_reset) HIPCHK(hipMemsetAsync(idx->qscount + 3, 0, sizeof(uint32_t), s));
             k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, olist, idx->qscount + 2, 2);
             sel(8, olist, idx->qscount + 2, nullptr);
             exa(8, olist, idx->qscount + 2);
@@ -322,7 +330,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             HIPCHK(hipMemcpyAsync(o_flags + c0, flags, (size_t)cn * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         if (mode == 1) continue;
         // ---- flagged queries: the exact heap replay, bounded by the block keys ----
-        HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
+        if (!ctr_reset) HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
         k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount, 0);
         {
             int rc = launch_blk_replay(idx, s, a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, valid, Qn,

@@ -202,6 +202,30 @@ struct wv_index {
     DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
     DBuf rpBlk, rpLb, rpQ, rpE, rpVm, rpOff, rpTot, rpCtr;  // pooled replay (k_rp_*)
     DBuf bmCnt, bmOff, bmPairs, bmE;                          // block-major exact (k_inv_*, k_exact_bm)
+    void* bmCnt_zp = nullptr;                                 // bmCnt.p when it is known all-zero
+    // hipGraph replay of a repeated identical wv_index_search_device call
+    // (option graph): the captured launch sequence is valid while the corpus,
+    // its buffers and the options are unchanged (mut_gen) and the call's
+    // pointers and sizes are the same (GraphKey)
+    struct GraphKey {
+        const void* q = nullptr;
+        int64_t nq = 0, d = 0;
+        int32_t k = 0, mode = 0;
+        const void *ids = nullptr, *dd = nullptr, *cnt = nullptr, *flags = nullptr, *stream = nullptr;
+        uint64_t gen = 0;
+        bool operator==(const GraphKey& o) const {
+            return q == o.q && nq == o.nq && d == o.d && k == o.k && mode == o.mode && ids == o.ids && dd == o.dd &&
+                   cnt == o.cnt && flags == o.flags && stream == o.stream && gen == o.gen;
+        }
+    };
+    int graph_opt = 1;
+    uint64_t mut_gen = 1;
+    GraphKey g_key, g_seen;
+    bool g_failed = false;  // capture failed for g_seen: run it uncaptured
+    hipGraph_t g_graph = nullptr;
+    hipGraphExec_t g_exec = nullptr;
+    uint64_t g_dq = 0, g_db = 0, g_dm = 0;  // stats deltas of the captured call
+    int g_timed = 0, g_timed_total = 0;     // its timing-event state
     DBuf qsCap;                                               // per query: upper bound of the (k+1)-th exact distance
     int exact_cap = 1;                                        // k_blk_exact drops values above qsCap (phase 0)
     int replay_dbg = 0;                                       // k_blk_replay clock diagnostics (printf)
@@ -225,6 +249,8 @@ struct wv_index {
 // a pending sharded phase 1 (qs_phase_nq), a sharded hnsw flat batch (qt_nq)
 // and a sharded BQ batch (bq_nq) describe one batch on one corpus state: an
 // Add, a Delete or another batch's query preparation ends them.
+// the corpus, its buffers or the options changed: captured search graphs are stale
+static inline void note_mutation(wv_index* idx) { idx->mut_gen++; }
 static void invalidate_batch(wv_index* idx) {
     idx->qs_keys_nq = 0;
     idx->qs_phase_nq = 0;

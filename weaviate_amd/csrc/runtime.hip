@@ -136,6 +136,8 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     batcher_free(idx->batcher);
     hipSetDevice(idx->device);
     if (idx->stream) hipStreamSynchronize(idx->stream);
+    if (idx->g_exec) hipGraphExecDestroy(idx->g_exec);
+    if (idx->g_graph) hipGraphDestroy(idx->g_graph);
     for (DBuf* b : {&idx->stage, &idx->slots, &idx->qraw, &idx->qn, &idx->qn2, &idx->spanA, &idx->spanI, &idx->candA,
                     &idx->candI, &idx->candE, &idx->oIds, &idx->oD, &idx->oN, &idx->oF, &idx->valid, &idx->qlist,
                     &idx->hI, &idx->hD, &idx->hN, &idx->rE, &idx->rB, &idx->qcodes, &idx->bqmin, &idx->cslot,
@@ -182,6 +184,7 @@ extern "C" void wv_index_destroy(wv_index* idx) {
 // the old ones freed and the new ones committed.  On any failure the partial
 // new buffers are freed and the index is left exactly as it was.
 static int ensure_capacity(wv_index* idx, int64_t need) {
+    note_mutation(idx);
     if (need <= idx->cap) return WV_OK;
     int64_t nc = std::max<int64_t>(need, idx->cap * 2);
     nc = round_up(std::max<int64_t>(nc, 1024), BN3);
@@ -497,7 +500,7 @@ static int add_rows_locked(wv_index* idx, const uint64_t* ids, const float* vecs
         last[ids[i]] = i;
         maxslot = std::max<int64_t>(maxslot, (int64_t)s);
     }
-    invalidate_batch(idx);
+    invalidate_batch(idx); note_mutation(idx);
     rc = ensure_capacity(idx, maxslot + 1);
     if (rc) return rc;
     std::vector<int64_t> rows;
@@ -569,7 +572,7 @@ extern "C" int wv_index_add_range_device(wv_index* idx, uint64_t first_id, const
         if (rc) return rc;
     }
     const int64_t s0 = (int64_t)s0u;
-    invalidate_batch(idx);
+    invalidate_batch(idx); note_mutation(idx);
     rc = ensure_capacity(idx, s0 + n);
     if (rc) return rc;
     std::vector<uint32_t> hs((size_t)n);
@@ -594,7 +597,7 @@ extern "C" int wv_index_delete(wv_index* idx, const uint64_t* ids, int64_t n) {
     if (!idx) return set_err(WV_ERR_INVALID, "nil index");
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
-    invalidate_batch(idx);
+    invalidate_batch(idx); note_mutation(idx);
     bool dirty = false;
     for (int64_t i = 0; i < n; i++) {
         if (ids[i] < idx->id_base) continue;
@@ -640,6 +643,8 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     if (!idx || !key) return set_err(WV_ERR_INVALID, "nil argument");
     std::lock_guard<std::mutex> g(idx->mu);
     std::string k(key);
+    note_mutation(idx);
+    if (k == "graph") { idx->graph_opt = value ? 1 : 0; return WV_OK; }
     if (k == "batch_window_us") { if (value < 0 || value > 1000000) return set_err(WV_ERR_INVALID, "batch_window_us out of range"); idx->batch_window_us = value; return WV_OK; }
     if (k == "exact_multi") { idx->exact_multi = value ? 1 : 0; return WV_OK; }
     if (k == "gemv_wg") { if (value < 8 || value > 65536) return set_err(WV_ERR_INVALID, "gemv_wg out of range"); idx->gemv_wg = (int)value; return WV_OK; }
@@ -887,12 +892,12 @@ int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t n
     HIPCHK(idx->qn.ensure((size_t)nq_pad * idx->dpad * sizeof(float)));
     HIPCHK(idx->qn2.ensure((size_t)nq_pad * sizeof(float)));
     float* Qn = idx->qn.as<float>();
-    if (nq_pad > nq)
-        HIPCHK(hipMemsetAsync(Qn + nq * idx->dpad, 0, (size_t)(nq_pad - nq) * idx->dpad * sizeof(float), s));
+    // the padding rows [nq, nq_pad) are zeroed by the same launch
     if (idx->metric == WV_METRIC_COSINE_DOT)
-        k_normalize_rows<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
+        k_normalize_rows<<<(unsigned)((nq_pad + 3) / 4), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad, nq_pad);
     else
-        k_copy_pad_rows<<<(unsigned)((nq * idx->dpad + 255) / 256), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn, idx->dpad);
+        k_copy_pad_rows<<<(unsigned)((nq_pad * idx->dpad + 255) / 256), 256, 0, s>>>(d_qraw, nq, idx->dims, Qn,
+                                                                                   idx->dpad, nq_pad);
     k_row_norm2<<<(unsigned)((nq_pad + 3) / 4), 256, 0, s>>>(Qn, nq_pad, idx->dpad, idx->qn2.as<float>());
     HIPCHK(hipGetLastError());
     return WV_OK;
@@ -1419,6 +1424,58 @@ extern "C" int wv_index_search_device(wv_index* idx, const float* d_queries, int
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
     hipStream_t s = (hipStream_t)stream;  // NULL: the null stream (ordered with the caller's default-stream work)
+    // a repeated identical call on a caller stream replays the hipGraph captured
+    // on its second occurrence (uncompressed corpus; timing events become event-record nodes)
+    const bool graphable = idx->graph_opt && stream && idx->compression == WV_COMPRESSION_NONE &&
+                           !idx->rq_bits && nq > 0;
+    if (graphable) {
+        wv_index::GraphKey key;
+        key.q = d_queries; key.nq = nq; key.d = d; key.k = k; key.mode = mode; key.ids = d_ids; key.dd = d_dists;
+        key.cnt = d_counts; key.flags = mode == 1 ? d_flags : nullptr; key.stream = stream; key.gen = idx->mut_gen;
+        if (idx->g_exec && key == idx->g_key) {
+            HIPCHK(hipGraphLaunch(idx->g_exec, s));
+            idx->timed = idx->g_timed;
+            idx->timed_total = idx->g_timed_total;
+            idx->stats.queries += idx->g_dq;
+            idx->stats.batches += idx->g_db;
+            idx->stats.mfma_launches += idx->g_dm;
+            return WV_OK;
+        }
+        if (key == idx->g_seen && !idx->g_failed) {
+            if (idx->g_exec) { hipGraphExecDestroy(idx->g_exec); idx->g_exec = nullptr; }
+            if (idx->g_graph) { hipGraphDestroy(idx->g_graph); idx->g_graph = nullptr; }
+            const wv_stats st0 = idx->stats;
+            int rc = -1;
+            hipGraph_t gr = nullptr;
+            hipError_t ec = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+            if (ec == hipSuccess) {
+                rc = search_core(idx, s, d_queries, nq, d, k, mode, idx->present, idx->npresent, d_ids, d_dists,
+                                 d_counts, mode == 1 ? d_flags : nullptr);
+                ec = hipStreamEndCapture(s, &gr);
+            }
+            hipGraphExec_t ex = nullptr;
+            if (rc == 0 && ec == hipSuccess && gr && hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0) == hipSuccess) {
+                idx->g_graph = gr;
+                idx->g_exec = ex;
+                idx->g_key = key;
+                idx->g_dq = idx->stats.queries - st0.queries;
+                idx->g_db = idx->stats.batches - st0.batches;
+                idx->g_dm = idx->stats.mfma_launches - st0.mfma_launches;
+                idx->g_timed = idx->timed;
+                idx->g_timed_total = idx->timed_total;
+                HIPCHK(hipGraphLaunch(ex, s));
+                return WV_OK;
+            }
+            // not capturable (or failed): this call runs uncaptured below, and so do its repeats
+            if (gr) hipGraphDestroy(gr);
+            (void)hipGetLastError();
+            idx->stats = st0;
+            idx->g_failed = true;
+        } else if (!(key == idx->g_seen)) {
+            idx->g_seen = key;
+            idx->g_failed = false;
+        }
+    }
     int rc = search_core(idx, s, d_queries, nq, d, k, mode, idx->present, idx->npresent, d_ids, d_dists, d_counts,
                          mode == 1 ? d_flags : nullptr);
     if (rc) return rc;

@@ -208,6 +208,7 @@ extern "C" int wv_index_preload(wv_index* idx, uint64_t id, const float* vec, in
 extern "C" int wv_index_update_user_config(wv_index* idx, const wv_config* updated) {
     if (!idx || !updated) return set_err(WV_ERR_INVALID, "nil argument");
     std::lock_guard<std::mutex> g(idx->mu);
+    note_mutation(idx);
     const bool bq_rq = updated->compression == WV_COMPRESSION_BQ || updated->compression == WV_COMPRESSION_RQ8 ||
                        updated->compression == WV_COMPRESSION_RQ1;
     // (PQ / SQ here are the hnsw flatSearch restatement: limit / SQ.RescoreLimit follow the same field)
