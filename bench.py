@@ -557,7 +557,9 @@ def main():
     # the exact fp32 path's dominant kernel: the block-key pass the runtime chose
     # (int8 keys for 384 < d <= 1536, bf16 keys otherwise; wv_stats.last_route)
     sel_kernel = ROUTE_KERNEL.get(route, "k_qs_blockkey")
-    int8_keys = sel_kernel == "k_q8_blockkey"
+    if route == 3 and dims > 1536:  # int8-only planes: the two-column-part form
+        sel_kernel = "k_q8_blockkey_cp"
+    int8_keys = sel_kernel.startswith("k_q8_blockkey")
     total_avg = float(np.mean(tot_ms)) if tot_ms else 0.0
     # the dominant kernel of each workload: its PMC record (matched on kernel
     # name and configuration) is the only source of `traffic`

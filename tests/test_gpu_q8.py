@@ -261,3 +261,61 @@ def test_q8_shape32_same_keys(wv, oracle, metric, kind, d, k):
     ids, dists, counts = res[1]
     for qi in range(0, len(queries), 10):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")
+
+
+@pytest.mark.parametrize("metric,kind,variant,n,d,k", [
+    ("cosine", 0, "avx256", 12000, 2048, 10),     # dpb8 2048: two column parts of 16 chunks
+    ("l2-squared", 0, "avx512", 10000, 2048, 100),
+    ("dot", 0, "avx256", 9000, 2500, 10),          # dpb8 2560 (parts of 20), zero-padded columns
+    ("cosine", 0, "avx256", 8000, 3072, 10),       # dpb8 3072 (parts of 24)
+    ("l2-squared", 1, "avx256", 8000, 3072, 24),   # integer data: ties -> replay without a bf16 plane
+    ("cosine", 2, "avx512", 6000, 1600, 100),      # just above the bf16 planes' 1536
+])
+def test_q8_only_planes_above_1536_dims(wv, oracle, metric, kind, variant, n, d, k):
+    """1536 < d <= 3072: int8 block-key planes without a bf16 plane
+    (k_q8_blockkey_cp, 128-query groups, two column parts per block), the int8
+    row filter in the exact pass, the unfiltered bounded replay.  Every query
+    bit-exact against the oracle; block keys within eps; with deletes and an
+    allow list too."""
+    data = gen(oracle, kind, 171, n, d)
+    queries = gen(oracle, kind, 172, 300, d)
+    idx, orc = build_pair(wv, oracle, metric, variant, data)
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] == ROUTE_INT8
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"q{qi}")
+    worst = check_block_keys(idx, oracle, kind, 171, n, d, metric, variant, queries, [0, 131, 299])
+    print(f"{metric} d={d}: int8-only max |A_block - min E| / eps = {worst:.4f}")
+    dele = list(range(5, n, 11)) + list(range(64, 160))  # scattered rows and whole blocks
+    idx.delete(*dele)
+    orc.delete(dele)
+    allow = list(range(1, n, 3))
+    ids, dists, counts = idx.search_by_vector_batch(queries[:64], k)
+    ida, da, ca = idx.search_by_vector_batch(queries[:64], k, allow=wv.AllowList(allow))
+    assert idx.stats()["last_route"] == ROUTE_INT8
+    for qi in range(64):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"d{qi}")
+        assert_same(orc.search(queries[qi], k, allow=allow), ida[qi, :ca[qi]], da[qi, :ca[qi]], ctx=f"a{qi}")
+    idx.close()
+
+
+def test_q8_only_nonfinite_row_leaves_block_keys(wv, oracle):
+    """A stored NaN above 1536 dims (no bf16 plane to flag it) sends the index
+    to the all-rows path, which keeps the reference's NaN semantics."""
+    n, d, k = 3000, 2048, 10
+    data = gen(oracle, 0, 181, n, d)
+    queries = gen(oracle, 0, 182, 20, d)
+    idx, orc = build_pair(wv, oracle, "l2-squared", "avx256", data)
+    idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] == ROUTE_INT8
+    bad = data[7].copy()
+    bad[100] = np.nan
+    idx.add_batch(np.array([n], dtype=np.uint64), bad[None, :])
+    orc2 = oracle.OracleFlat(oracle.METRIC["l2-squared"], VARIANTS["avx256"], d, n + 1)
+    orc2.add_batch(np.arange(n, dtype=np.uint64), data)
+    orc2.add_batch(np.array([n], dtype=np.uint64), bad[None, :])
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] != ROUTE_INT8
+    for qi in range(len(queries)):
+        assert_same(orc2.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"n{qi}")
+    idx.close()

@@ -106,7 +106,9 @@ __device__ __forceinline__ int q8_code(float x, float inv) {
 // the block's 32 stored rows (present or not: a stale or zero row only costs
 // precision), X8 = rint(x / sb) clamped to +-127, and per row
 // |x - sb X8|^2, |sb X8|^2 into the index maxima qmax8[0], qmax8[1]
-// (atomicMax on float bits).  Blocks blist[i] or b0 + i.
+// (atomicMax on float bits); qmax8[2] = 1 once a block holds a non-finite
+// value (the int8-only planes above 1536 dims have no bf16 plane to flag it).
+// Blocks blist[i] or b0 + i.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_block_q8(const float* __restrict__ X, int dpad, int dims, int dpb8,
                                                   const uint32_t* __restrict__ blist, int64_t b0,
@@ -117,10 +119,16 @@ __global__ __launch_bounds__(256) void k_block_q8(const float* __restrict__ X, i
     const int64_t blk = blist ? (int64_t)blist[blockIdx.x] : b0 + blockIdx.x;
     const int64_t r0 = blk * 32;
     float m = 0.f;
+    bool bad = false;
     for (int r = 8 * w; r < 8 * w + 8; r++) {
         const float* x = X + (r0 + r) * dpad;
-        for (int c = lane; c < dims; c += 64) m = fmaxf(m, fabsf(x[c]));
+        for (int c = lane; c < dims; c += 64) {
+            const float v = x[c];
+            m = fmaxf(m, fabsf(v));
+            bad |= !__builtin_isfinite(v);
+        }
     }
+    if (__any(bad) && lane == 0) atomicOr(&qmax8[2], 1u);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if (lane == 0) smax[w] = m;
@@ -895,6 +903,229 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey32(Q8Args a) {
         cur = nxt;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last (unused) prefetch
+}
+
+// ---------------------------------------------------------------------------
+// k_q8_blockkey_cp<NCS, L2>: int8 block keys above 1536 dims (dpb8 = 2 NCS
+// 64-column chunks: 2048 / 2560 / 3072).  A wave's 32-query fragments would
+// need 4 NCS i32x4 (> 256 VGPRs), so a wave holds 16 queries (2 NCS i32x4, up
+// to 192 VGPRs; 128 queries per workgroup of 8 waves, two per SIMD) and a
+// 32-row block streams through the LDS ring in two column parts of NCS chunks
+// (3 slots of 2 NCS KiB, the next-but-one part's LDS-DMA group issued one
+// piece per chunk).  Per chunk: 2 A-fragment reads (row halves) and 2
+// v_mfma_i32_16x16x64_i8 (row halves x the wave's 16 queries); the block's
+// accumulators carry from part 0 into part 1, whose end reduces the block (the
+// valid word, scale and L2 norms ride with every part's DMA group, read in
+// part 1).  The cross-lane combine and key store of a block are deferred into
+// the next block's part 0.  Keys are k_q8_blockkey's, so select / exact /
+// replay apply unchanged.
+// ---------------------------------------------------------------------------
+template <int NCS, bool ISL2>
+__global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
+    constexpr int NC = 2 * NCS;                     // 64-column chunks per block
+    constexpr int NPB = 2 * NC;                     // 1 KiB pieces per block
+    constexpr int SPC = 2 * NCS;                    // pieces per step (one column part)
+    constexpr int SLOT = SPC * 1024;
+    constexpr int P = SPC / 8;                      // pieces per wave per step
+    static_assert(SPC % 8 == 0, "a part's pieces split over 8 waves");
+    constexpr int64_t TILE_B = (int64_t)NPB * 8192;  // bytes per 256-row tile of a plane
+    constexpr int P0 = P + 2 + (ISL2 ? 1 : 0);      // vector-memory ops per group, per wave
+    static_assert(P0 < NCS, "the deferred key store follows the step's DMA pieces");
+    constexpr int X0 = 1;                           // chunk of part 1's extra LDS reads
+    constexpr int XE = 2 + (ISL2 ? 2 : 0);
+    constexpr int NBUF = 3;
+    extern __shared__ __attribute__((aligned(16))) unsigned char qsm[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int total = a.nqg * a.nspans;
+    const int b = blockIdx.x;
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;  // a span's groups share an XCD
+    const int span = logical / a.nqg, grp = logical % a.nqg;
+
+    // the wave's 16 queries (group grp of 128 = half grp & 1 of a 256-row query tile)
+    i32x4_t Qf[NC];
+    const int64_t q0 = (int64_t)grp * 128 + wave * 16;
+    {
+        const int j = lane & 15, kq = lane >> 4;
+        const unsigned char* qp = a.Q8 + (int64_t)(grp >> 1) * TILE_B + (kq >> 1) * 8192 +
+                                  ((grp & 1) * 128 + wave * 16 + j) * 32 + 16 * (kq & 1);
+#pragma unroll
+        for (int c = 0; c < NC; c++) Qf[c] = *reinterpret_cast<const i32x4_t*>(qp + (2 * c) * 8192);
+    }
+    const float sq = a.qscale[q0 + (lane & 15)];
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the query loads retire before the DMA ring
+
+    const int64_t s0 = (int64_t)span * a.slots_per_span;  // blocks (one per two steps)
+    int64_t s1 = s0 + a.slots_per_span;
+    if (s1 > a.nslots) s1 = a.nslots;
+    const int nblk = s1 > s0 ? (int)(s1 - s0) : 0;
+    const int nsteps = 2 * nblk;
+
+    const uint32_t src_lane = (uint32_t)(16 * lane);
+    const unsigned ring = lds_addr(qsm);
+    const unsigned vring = ring + NBUF * SLOT + (unsigned)wave * 64u;
+    const unsigned sring = ring + NBUF * SLOT + 512u + (unsigned)wave * 64u;
+    const unsigned xnring = ring + NBUF * SLOT + 1024u + (unsigned)wave * 512u;
+    const int64_t tile0 = (s0 * 32) >> 8;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.X8 + tile0 * TILE_B), (short)0, -1, 0x00020000);
+    int64_t igb = s0;  // block of the next DMA group
+    uint32_t ioff = (uint32_t)(((igb >> 3) - tile0) * TILE_B + (igb & 7) * 1024);
+    // piece j of the group of step u (part PT), into ring slot `slot`
+    auto issue_piece = [&](auto ptc, int j, int u, int slot) {
+        constexpr int PT = decltype(ptc)::value;
+        if (j < P) {
+            const int pi = wave + 8 * j;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(size_t)(ring + (unsigned)(slot * SLOT + pi * 1024)),
+                                                     16, src_lane, ioff + (uint32_t)((PT * SPC + pi) * 8192), 0, 0);
+        } else if (j == P) {
+            if (lane < 1)
+                __builtin_amdgcn_global_load_lds(a.valid + igb, (lds_ptr_t)(size_t)(vring + (unsigned)((u & 3) * 16)), 4, 0,
+                                                 0);
+        } else if (j == P + 1) {
+            if (lane < 1)
+                __builtin_amdgcn_global_load_lds(a.sb + igb, (lds_ptr_t)(size_t)(sring + (unsigned)((u & 3) * 16)), 4, 0, 0);
+        } else {
+            if (lane < 8)
+                __builtin_amdgcn_global_load_lds(a.xnorm2 + igb * 32 + 4 * lane,
+                                                 (lds_ptr_t)(size_t)(xnring + (unsigned)((u & 3) * 128)), 16, 0, 0);
+        }
+        if (PT == 1 && j == P0 - 1) {  // the block's second part issued: on to the next block
+            igb += 1;
+            ioff += 1024;
+            if ((igb & 7) == 0) ioff += (uint32_t)(TILE_B - 8192);
+        }
+    };
+    // lane (i = lane&15, kq = lane>>4) reads row 16m + i, columns 64c + 16kq..+15
+    const unsigned l16 = (unsigned)(((lane >> 5) & 1) * 1024 + (lane & 15) * 32 + 16 * ((lane >> 4) & 1));
+    i32x4_t B2[2][2];  // A fragments [chunk & 1][row half m]
+    i32x4_t acc[2];    // [row half m]: element r is row 16m + 4g + r (g = lane >> 4) of query lane & 15
+    if (nsteps > 0) {
+        static_for<0, P0>([&](auto jc) { issue_piece(std::integral_constant<int, 0>{}, decltype(jc)::value, 0, 0); });
+        static_for<0, P0>([&](auto jc) { issue_piece(std::integral_constant<int, 1>{}, decltype(jc)::value, 1, 1); });
+        qs_wait_vm_c<P0>();  // group 0 landed, group 1 may stay in flight
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        B2[0][0] = lds_ld16_o<0>(ring + l16);
+        B2[0][1] = lds_ld16_o<512>(ring + l16);
+    }
+    // the pending block: the lane's partial (raw int max, or L2 float bits) and its scale
+    uint32_t pend = 0;
+    float psb = 0.f;
+    auto op = [](uint32_t x, uint32_t y) -> uint32_t {
+        if constexpr (ISL2) return __float_as_uint(fminf(__uint_as_float(x), __uint_as_float(y)));
+        else return (uint32_t)max((int)x, (int)y);
+    };
+    auto finish = [&](uint32_t r, float sbp, int64_t gb) {
+        const auto x32 = __builtin_amdgcn_permlane32_swap(r, r, false, false);
+        r = op(r, x32[1]);
+        const auto x16 = __builtin_amdgcn_permlane16_swap(r, r, false, false);
+        r = op(r, x16[1]);  // lanes 0-15: the block's key partial over all 32 rows, query lane
+        float key;
+        if constexpr (ISL2) {
+            key = __uint_as_float(r);
+        } else {
+            const int mi = (int)r;
+            key = mi == Q8_NONE ? __builtin_inff() : -((sq * sbp) * (float)mi);
+        }
+        if (lane < 16) a.key[(q0 + lane) * a.ldk + gb] = key;
+    };
+    int cur = 0;
+    for (int t = 0; t < nblk; t++) {
+        static_for<0, 2>([&](auto pc) {
+            constexpr int PT = decltype(pc)::value;
+            const int u = 2 * t + PT;
+            const int nxt = cur == NBUF - 1 ? 0 : cur + 1;
+            const int gslot = cur == 0 ? NBUF - 1 : cur - 1;  // slot of group u+2
+            const unsigned sbase = ring + (unsigned)(cur * SLOT) + l16;
+            const int dma = __builtin_amdgcn_readfirstlane(u + 2 < nsteps ? 1 : 0);
+            const unsigned sm = (unsigned)(u & 3);
+            uint32_t vw = 0;
+            float sbv = 0.f;
+            f32x4_t xa = {0.f, 0.f, 0.f, 0.f}, xb = {0.f, 0.f, 0.f, 0.f};
+            static_for<0, NCS>([&](auto ttc) {
+                constexpr int tt = decltype(ttc)::value;
+                if constexpr (PT == 1 && tt == X0) {  // the block's valid word, scale (+ L2 norms)
+                    asm volatile("ds_read_b32 %0, %1" : "=v"(vw) : "v"(vring + sm * 16u));
+                    asm volatile("ds_read_b32 %0, %1" : "=v"(sbv) : "v"(sring + sm * 16u));
+                    if constexpr (ISL2) {
+                        const unsigned xbase = xnring + sm * 128u + (unsigned)(16 * ((lane >> 4) & 3));
+                        xa = lds_ld4f_o<0>(xbase);
+                        xb = lds_ld4f_o<64>(xbase);
+                    }
+                }
+                if constexpr (tt + 1 < NCS) {
+                    constexpr int o1 = 2 * (tt + 1) * 1024;
+                    B2[(tt + 1) & 1][0] = lds_ld16_o<o1>(sbase);
+                    B2[(tt + 1) & 1][1] = lds_ld16_o<o1 + 512>(sbase);
+                }
+                constexpr int ahead = tt + 1 < NCS ? 1 : 0;
+                qs_wait_lgkm<2 * ahead + ((PT == 1 && tt == X0) ? XE : 0)>();
+                asm volatile("" : "+v"(B2[tt & 1][0]), "+v"(B2[tt & 1][1]));
+                if constexpr (PT == 1 && tt == X0 + 1) {  // the extras are older than chunk tt's reads
+                    if constexpr (ISL2) asm volatile("" : "+v"(vw), "+v"(sbv), "+v"(xa), "+v"(xb));
+                    else asm volatile("" : "+v"(vw), "+v"(sbv));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < 2; m++) {
+                    if constexpr (PT == 0 && tt == 0)
+                        acc[m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[0][m], Qf[0], i32x4_t{0, 0, 0, 0}, 0, 0, 0);
+                    else
+                        acc[m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[tt & 1][m], Qf[PT * NCS + tt], acc[m], 0, 0, 0);
+                }
+                if constexpr (tt < P0) {
+                    if (dma) issue_piece(pc, tt, u + 2, gslot);
+                }
+                if constexpr (PT == 0 && tt == P0) {
+                    if (t > 0) finish(pend, psb, s0 + t - 1);
+                }
+            });
+            if constexpr (PT == 1) {  // the block's reduction over its 32 rows
+                const uint32_t w = __builtin_amdgcn_readfirstlane(vw);
+                const float sbf = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sbv)));
+                const uint32_t vl = w >> (4 * ((lane >> 4) & 3));
+                if constexpr (ISL2) {
+                    const float cn = -2.f * (sq * sbf);
+                    float m = __builtin_inff();
+#pragma unroll
+                    for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const float v = fmaf(cn, (float)acc[mm][r], mm ? xb[r] : xa[r]);
+                            m = fminf(m, ((vl >> (16 * mm + r)) & 1u) ? v : __builtin_inff());
+                        }
+                    pend = __float_as_uint(m);
+                } else if (w == 0xFFFFFFFFu) {
+                    pend = (uint32_t)max(max(max(acc[0][0], acc[0][1]), max(acc[0][2], acc[0][3])),
+                                         max(max(acc[1][0], acc[1][1]), max(acc[1][2], acc[1][3])));
+                } else {
+                    int mi = Q8_NONE;
+#pragma unroll
+                    for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) mi = max(mi, ((vl >> (16 * mm + r)) & 1u) ? acc[mm][r] : Q8_NONE);
+                    pend = (uint32_t)mi;
+                }
+                psb = sbf;
+            }
+            // ---- end of the step: the next group must have landed (every wave) ----
+            if (u + 1 < nsteps) {
+                // this wave's vector-memory ops after group u+1, in issue order: the
+                // store of step u-1 or u (one per block, in part 0, from block 1 on),
+                // the pieces of group u+2
+                qs_wait_vm((t > 0 ? 1 : 0) + (dma ? P0 : 0));
+                __builtin_amdgcn_s_barrier();  // slot cur is free; slot nxt has landed for every wave
+                __builtin_amdgcn_sched_barrier(0);
+                B2[0][0] = lds_ld16_o<0>(ring + (unsigned)(nxt * SLOT) + l16);
+                B2[0][1] = lds_ld16_o<512>(ring + (unsigned)(nxt * SLOT) + l16);
+            }
+            cur = nxt;
+        });
+    }
+    if (nblk > 0) finish(pend, psb, s0 + nblk - 1);
 }
 
 // BQ codes unpacked to +-1 int8 for k_q8_blockkey<..., BQ>: bit b of word w

@@ -17,7 +17,7 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
     const float gd = (float)gamma_n(idx->dpb + 8), gacc_r = (float)gamma_n(idx->dpb + 2);
     // int8 keys: the row bound from the int8 plane (q8f), else the bf16 plane
     Q8Filter f8{};
-    if (q8f && Xb) f8 = *q8f;
+    if (q8f && idx->exact_filter && (Xb || idx->q8_only)) f8 = *q8f;
 #define WV_EXR(RV, M, V)                                                                                             \
     do {                                                                                                             \
         if (eb) k_blk_exact<RV, M, V, true><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8); \

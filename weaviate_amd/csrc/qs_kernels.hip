@@ -1080,6 +1080,7 @@ __host__ __device__ __forceinline__ int64_t q8_plane_byte(int64_t row, int c, in
 // row filter helpers (k_blk_exact, k_blk_replay)
 // ---------------------------------------------------------------------------
 constexpr int QS_FILT_DPB = 1536;  // the widest block-key plane (k_qs_blockkey_w4)
+constexpr int Q8_FILT_DPB = 3072;  // the widest int8 plane (k_q8_blockkey_cp)
 
 // S = sum_c bf16(q)_c * x_h,c of one stored row from the tiled bf16 plane
 // (lane per row: the plane interleaves 256 rows per 16-column chunk, so the
@@ -1205,7 +1206,7 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     __shared__ uint32_t sbi[4][64];
     __shared__ float sslot[4][64];
     __shared__ __attribute__((aligned(16))) float sqh[EB ? 4 : QS_FILT_DPB];
-    __shared__ __attribute__((aligned(16))) uint32_t sq8[EB ? 4 : QS_FILT_DPB / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t sq8[EB ? 4 : Q8_FILT_DPB / 4];
     __shared__ float lk[3][L];
     __shared__ uint32_t lid[3][L];
     __shared__ int snv[4];
@@ -1226,9 +1227,10 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     // A_row - eps_r reaches the cap has an exact distance >= cap, which the
     // list never keeps; only the others get the reference-order distance
     const float4 qi = qinfo[q];
-    const bool filt = !EB && Xb != nullptr && cap != nullptr && qi.w == 0.f && dpb <= QS_FILT_DPB;
-    // int8-plane row bound (the keys were int8): half the plane bytes per row
-    const bool f8 = filt && q8f.X8 != nullptr && q8f.dpb8 <= QS_FILT_DPB;
+    // int8-plane row bound (the keys were int8): half the plane bytes per row;
+    // above 1536 dims the only plane
+    const bool f8 = !EB && q8f.X8 != nullptr && cap != nullptr && qi.w == 0.f && q8f.dpb8 <= Q8_FILT_DPB;
+    const bool filt = f8 || (!EB && Xb != nullptr && cap != nullptr && qi.w == 0.f && dpb <= QS_FILT_DPB);
     float eps_r = 0.f, capq = __builtin_inff(), sqs = 0.f;
     if (f8) {
         for (int c4 = 4 * threadIdx.x; c4 < q8f.dpb8; c4 += 1024)

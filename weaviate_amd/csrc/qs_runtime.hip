@@ -16,7 +16,9 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     const int kout = mode == 1 ? k + 1 : k;
     const int NK = idx->dpb / 16;
     // int8 block keys (q8_kernels.hip): NC 64-column chunks per block, RB8 blocks per ring slot
-    const bool q8 = idx->q8_planes && idx->q8_opt;
+    // (above 1536 dims the int8 planes are the only ones: k_q8_blockkey_cp, 128-query groups)
+    const bool q8 = idx->q8_planes && (idx->q8_opt || idx->q8_only);
+    const bool q8cp = q8 && idx->q8_only;
     const int NC8 = idx->dpb8 / 64;
     const int RB8 = idx->dpb8 <= 768 ? 2 : 1;
     const int RB = q8 ? RB8 : qs_rb(NK);
@@ -102,7 +104,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // column parts per ring step: dpb 1024 -> 4 slots of 32 KiB, 1536 -> 3 of 48 KiB
         const bool w4 = !q8 && idx->dpb > QS_W4_DPB;
         const int w4_nb = NK == 64 ? 4 : 3;
-        a.nqg = (int)(cn_pad / (w4 ? 128 : QS_QPB));
+        a.nqg = (int)(cn_pad / ((w4 || q8cp) ? 128 : QS_QPB));
         int64_t nspans = 256 / std::gcd(256, a.nqg);
         while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
         if (idx->spans_opt > 0) nspans = idx->spans_opt;
@@ -121,7 +123,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         a.slots_per_span = (int)sps;
         a.nspans = (int)((nslots + sps - 1) / sps);
         const bool l2 = metric == L2;
-        const size_t lds = q8 ? (size_t)3 * RB * 2 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * RB * 128 : 0)
+        const size_t lds = q8cp ? (size_t)3 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * 128 : 0)
+                         : q8 ? (size_t)3 * RB * 2 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * RB * 128 : 0)
                          : w4 ? (size_t)w4_nb * (NK / 4) * 2048 + 256 + (l2 ? (size_t)4 * 4 * 128 : 0)
                               : (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
         dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
@@ -225,6 +228,21 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                 if (l2) { WV_Q832N(true); } else { WV_Q832N(false); }
 #undef WV_Q832N
 #undef WV_Q832
+            } else if (q8cp) {
+#define WV_Q8CP(NCSV, L2V)                                                                                     \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey_cp<NCSV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey_cp<NCSV, L2V><<<grid, 512, lds, s>>>(q8a);                                               \
+    } while (0)
+#define WV_Q8CPN(L2V)                                  \
+    switch (NC8) {                                     \
+    case 32: WV_Q8CP(16, L2V); break;                  \
+    case 40: WV_Q8CP(20, L2V); break;                  \
+    default: WV_Q8CP(24, L2V); break;                  \
+    }
+                if (l2) { WV_Q8CPN(true); } else { WV_Q8CPN(false); }
+#undef WV_Q8CPN
+#undef WV_Q8CP
             } else if (l2) { WV_Q8N(true); } else { WV_Q8N(false); }
         } else if (w4) {
             if (l2) { WV_QSWN(true); } else { WV_QSWN(false); }
@@ -412,7 +430,7 @@ extern "C" int wv_index_shard_phase1(wv_index* idx, const float* d_queries, int6
     hipStream_t s = (hipStream_t)stream;
     idx->qs_keys_nq = 0;
     idx->qs_phase_nq = 0;
-    const bool qs = idx->compression == WV_COMPRESSION_NONE && idx->qs_planes && !idx->has_nonfinite &&
+    const bool qs = idx->compression == WV_COMPRESSION_NONE && (idx->qs_planes || idx->q8_only) && !idx->has_nonfinite &&
                     (idx->kernel_opt == 0 || idx->kernel_opt == 7) && !idx->force_replay && qs_R(k) > 0 &&
                     idx->metric != WV_METRIC_HAMMING && idx->dims != 0 && idx->npresent > 0 && nq > 0;
     if (!qs) return set_err(WV_ERR_UNSUPPORTED, "two-phase shard search: not on the block-key path");

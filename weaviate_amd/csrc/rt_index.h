@@ -144,6 +144,7 @@ struct wv_index {
     // int8 block-key plane (q8_kernels.hip): [cap][dpb8] codes, one scale per
     // 32-row block, built beside the bf16 plane when 384 < dims <= 1536
     int q8_planes = 0, dpb8 = 0;
+    int q8_only = 0;                // 1536 < dims <= 3072: int8 planes without the bf16 plane
     int q8_opt = 1;                 // option q8: block keys from the int8 plane (1) or the bf16 plane (0)
     int q8_R = 0;                   // option q8_R: candidate lists for int8 keys (0: R = 8, 448 blocks)
     int q8_shape = 16;              // option q8_shape: 16 = v_mfma_i32_16x16x64_i8 kernel, 32 = 32x32x32
@@ -265,6 +266,7 @@ static void invalidate_batch(wv_index* idx) {
 // to 768 dims; k_qs_blockkey_w4 (one wave per SIMD, query fragments in the
 // 512-entry register file, dpb 1024 or 1536) up to 1536
 constexpr int QS_MAX_DPB = 1536;
+constexpr int Q8_MAX_DPB = 3072;  // int8-only block-key planes (k_q8_blockkey_cp)
 constexpr int QS_W4_DPB = 768;  // dpb above this: k_qs_blockkey_w4
 
 // ---------------------------------------------------------------------------

@@ -67,6 +67,13 @@ static void set_dims(wv_index* idx, int64_t d) {
     // 256-column multiples above (one block per slot), <= 48 KiB per slot
     idx->dpb8 = (int)(d <= 768 ? round_up(d, 128) : round_up(d, 256));
     idx->q8_planes = (idx->qs_planes && d > 384 && idx->dpb8 <= 1536) ? 1 : 0;
+    // above 1536 dims: int8 planes only (no bf16 plane), 512-column multiples up
+    // to 3072 -- two column parts of 16 / 20 / 24 chunks per block (k_q8_blockkey_cp)
+    idx->q8_only = (idx->use_qs && !idx->qs_planes && d > 1536 && round_up(d, 512) <= Q8_MAX_DPB) ? 1 : 0;
+    if (idx->q8_only) {
+        idx->dpb8 = (int)round_up(d, 512);
+        idx->q8_planes = 1;
+    }
     if (idx->compression == WV_COMPRESSION_BQ) {  // +-1 code plane: 7..24 words (448..1536 bits)
         const int w = (int)((d + 63) / 64), bits = 64 * w;
         idx->dpb8b = (w >= 7 && w <= 24) ? (int)(bits <= 768 ? round_up(bits, 128) : round_up(bits, 256)) : 0;
@@ -457,9 +464,10 @@ static int requant_blocks(wv_index* idx, const uint32_t* h_slots, int64_t n) {
 // host mirror of the device non-finite flag (rows with NaN/Inf route the exact
 // search to the all-rows path); called after a synchronised Add
 static int refresh_nonfinite(wv_index* idx) {
-    if (!idx->qs_planes || idx->has_nonfinite) return WV_OK;
+    if (!(idx->qs_planes || idx->q8_only) || idx->has_nonfinite) return WV_OK;
     uint32_t f = 0;
-    HIPCHK(hipMemcpy(&f, idx->qsmax + 2, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    // bf16 plane builder's flag, or k_block_q8's on the int8-only planes
+    HIPCHK(hipMemcpy(&f, idx->q8_only ? idx->qmax8 + 2 : idx->qsmax + 2, sizeof(uint32_t), hipMemcpyDeviceToHost));
     idx->has_nonfinite = f ? 1 : 0;
     return WV_OK;
 }
@@ -943,7 +951,8 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     if (rc) return rc;
     const float* Qn = idx->qn.as<float>();
     // block-key path (default): planes built, finite corpus, list sizes that fit
-    if (idx->qs_planes && !idx->has_nonfinite && (idx->kernel_opt == 0 || idx->kernel_opt == 7) && !idx->force_replay &&
+    if ((idx->qs_planes || idx->q8_only) && !idx->has_nonfinite && (idx->kernel_opt == 0 || idx->kernel_opt == 7) &&
+        !idx->force_replay &&
         qs_R(k) > 0 && idx->metric != WV_METRIC_HAMMING) {
         idx->stats.queries += (uint64_t)nq;
         idx->stats.batches++;
