@@ -1010,21 +1010,151 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
     }
 }
 
+// k_blk_select_f<R, RT>: k_blk_select's selection by filtering instead of a
+// sorted L-list.  The wave keeps only the 64 (RT - 1) smallest keys (enough for
+// M = the (k+1)-th; RT = qs_R(k)) and appends every block with A <= T_cur =
+// A(M_cur) + 2 eps to an LDS buffer of L + 64 entries.  M_cur (the merged
+// list's (k+1)-th) only falls, so T_cur bounds the final T from above: no
+// qualifying block is missed; a full buffer is compacted with the current
+// T_cur, and at the end with the final T.  The candidate list comes out in
+// scan order, not sorted (k_blk_exact takes any order; k_blk_gthresh
+// compacts).  flags[q] = 2 when more than L blocks qualify.  Same outputs
+// (ncand, eps, cap, topA, flags) and the same candidate set as k_blk_select.
+template <int R, int RT>
+__global__ __launch_bounds__(256) void k_blk_select_f(const float* __restrict__ key, int64_t ldk, int64_t nb, int nq,
+                                                      int k, int metric, const float4* __restrict__ qinfo,
+                                                      const uint32_t* __restrict__ qsmax,
+                                                      const uint32_t* __restrict__ maxn2, float gd, float gacc,
+                                                      uint32_t* __restrict__ cand, int32_t* __restrict__ ncand,
+                                                      int32_t* __restrict__ flags, float* __restrict__ eps_out,
+                                                      const int32_t* __restrict__ qlist,
+                                                      const uint32_t* __restrict__ qcount, float* __restrict__ topA,
+                                                      float* __restrict__ cap_out, uint32_t* __restrict__ list_ctr) {
+    if (list_ctr && blockIdx.x == 0 && threadIdx.x == 0) {
+        list_ctr[1] = 0u;
+        list_ctr[3] = 0u;
+    }
+    constexpr int L = 64 * (R - 1);
+    constexpr int CB = L + 64;
+    constexpr int U = 16;
+    __shared__ float sbk[4][64];
+    __shared__ uint32_t sbi[4][64];
+    __shared__ float cbk[4][CB];
+    __shared__ uint32_t cbi[4][CB];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    int q = blockIdx.x * 4 + w;
+    if (qlist) {
+        if ((uint32_t)q >= qcount[1]) return;
+        q = qlist[q];
+    }
+    if (q >= nq) return;
+    const float4 qi = qinfo[q];
+    const float eps = qs_eps(metric, qi, qsmax, maxn2, gd, gacc);
+    const float* kr = key + (int64_t)q * ldk;
+    WaveTopL<RT> t;
+    t.init();
+    float T = __builtin_inff();
+    int nc = 0;
+    bool over = false;
+    auto refresh = [&]() {
+        t.merge(sbk[w], sbi[w], lane);
+        const float mk = t.key_at(k);
+        T = mk == __builtin_inff() ? __builtin_inff() : qs_key_to_a(metric, mk, qi.x) + 2.0005f * eps;
+    };
+    auto compact = [&]() {
+        int n2 = 0;
+        for (int e0 = 0; e0 < nc; e0 += 64) {
+            const int e = e0 + lane;
+            const float v = e < nc ? cbk[w][e] : __builtin_inff();
+            const uint32_t id = e < nc ? cbi[w][e] : 0u;
+            const bool in = e < nc && qs_key_to_a(metric, v, qi.x) <= T;
+            const uint64_t m = __ballot(in);
+            // in place: the wave's reads of this chunk precede its writes, and a
+            // write goes to a position <= its read (LDS ops of a wave in order)
+            const int pos = n2 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (in) { cbk[w][pos] = v; cbi[w][pos] = id; }
+            n2 += __popcll(m);
+        }
+        nc = n2;
+    };
+    for (int64_t b0 = 0; b0 < nb; b0 += 64 * U) {
+        float v[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const int64_t bb = b0 + j * 64 + lane;
+            v[j] = bb < nb ? kr[bb] : __builtin_inff();
+        }
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < U; j++) any |= v[j] < t.thr;
+        if (__any(any)) {
+#pragma unroll
+            for (int j = 0; j < U; j++) t.offer(v[j], (uint32_t)(b0 + j * 64 + lane), sbk[w], sbi[w], lane);
+        }
+        if (over) continue;
+        bool anyc = false;  // one wave vote per chunk: most chunks append nothing
+#pragma unroll
+        for (int j = 0; j < U; j++) anyc |= v[j] < __builtin_inff() && qs_key_to_a(metric, v[j], qi.x) <= T;
+        if (!__any(anyc)) continue;
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            bool in = v[j] < __builtin_inff() && qs_key_to_a(metric, v[j], qi.x) <= T;
+            uint64_t m = __ballot(in);
+            if (m == 0) continue;
+            int n = __popcll(m);
+            if (nc + n > CB) {  // full: tighten T and drop what no longer qualifies
+                refresh();
+                compact();
+                in = in && qs_key_to_a(metric, v[j], qi.x) <= T;
+                m = __ballot(in);
+                n = __popcll(m);
+                if (nc + n > CB) { over = true; break; }
+            }
+            const int pos = nc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (in) { cbk[w][pos] = v[j]; cbi[w][pos] = (uint32_t)(b0 + j * 64 + lane); }
+            nc += n;
+        }
+    }
+    refresh();
+    const float mk = t.key_at(k);
+    const float M = qs_key_to_a(metric, mk, qi.x);
+    if (!over) compact();
+    const bool full = over || nc > L;
+    if (!full)
+        for (int e = lane; e < nc; e += 64) cand[(int64_t)q * L + e] = cbi[w][e];
+    if (lane == 0) {
+        ncand[q] = full ? L : nc;
+        eps_out[q] = eps;
+        if (cap_out)
+            cap_out[q] = mk == __builtin_inff() ? __builtin_inff() : qs_next_up(M + 1.001f * eps);
+        flags[q] = (full || qi.w != 0.f) ? 2 : 0;
+    }
+    if (topA) {  // sharded phase 1: this shard's k+1 smallest block-key A values
+#pragma unroll
+        for (int r = 0; r < RT - 1; r++) {
+            const int e = r * 64 + lane;
+            if (e <= k) topA[(int64_t)q * (k + 1) + e] = qs_key_to_a(metric, t.key[r], qi.x);
+        }
+    }
+}
+
 // k_blk_gthresh: sharded phase 2, wave per query.  M_g = the (k+1)-th smallest
 // of the W shards' k+1 smallest block-key A values (= the (k+1)-th smallest
 // key over the whole corpus), eps_max = the largest shard eps of the query.
 // The k+1 blocks under M_g each hold a row with E <= M_g + eps_max, so a
 // block of this shard with A > M_g + eps_max + eps cannot hold a global
-// top-(k+1) row; the candidate list (ascending by key) is cut to that prefix.
+// top-(k+1) row; the candidate list is compacted to the others (any order).
 // Queries with flag 2 (their own second pass) or more than 1024 gathered
 // values (W * (k+1) > 1024, e.g. k = 127 at 8 ranks) keep the local list:
-// still exact, only without the global cut.
+// still exact, only without the global cut.  cap (phase 1's local cap, valid
+// for the shard's own k+1 smallest) is lowered to the global one.
 __global__ __launch_bounds__(256) void k_blk_gthresh(const float* __restrict__ topA_all, const float* __restrict__ eps_all,
                                                      int W, int nq, int k, int metric, const float4* __restrict__ qinfo,
                                                      const float* __restrict__ key, int64_t ldk,
-                                                     const uint32_t* __restrict__ cand, int L,
+                                                     uint32_t* __restrict__ cand, int L,
                                                      int32_t* __restrict__ ncand, const float* __restrict__ eps_own,
-                                                     const int32_t* __restrict__ flags) {
+                                                     const int32_t* __restrict__ flags, float* __restrict__ cap) {
     __shared__ float sv[4][1024];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -1061,12 +1191,23 @@ __global__ __launch_bounds__(256) void k_blk_gthresh(const float* __restrict__ t
     const int nc = ncand[q];
     const float qn2 = qinfo[q].x;
     int keep = 0;
-    for (int e0 = 0; e0 < nc; e0 += 64) {
+    uint32_t* cq = cand + (int64_t)q * L;
+    for (int e0 = 0; e0 < nc; e0 += 64) {  // compaction in place (any list order)
         const int e = e0 + lane;
-        const bool in = e < nc && qs_key_to_a(metric, key[(int64_t)q * ldk + cand[(int64_t)q * L + e]], qn2) <= T;
-        keep += __popcll(__ballot(in));
+        const uint32_t b = e < nc ? cq[e] : 0u;
+        const bool in = e < nc && qs_key_to_a(metric, key[(int64_t)q * ldk + b], qn2) <= T;
+        const uint64_t m = __ballot(in);
+        const int pos = keep + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        if (in) cq[pos] = b;
+        keep += __popcll(m);
     }
-    if (lane == 0) ncand[q] = keep;
+    if (lane == 0) {
+        ncand[q] = keep;
+        // the k+1 blocks under M_g each hold a row with E <= M_g + eps_max: the
+        // global (k+1)-th smallest exact distance is below this cap, so the
+        // capped exact pass (k_blk_exact) may skip every row at or above it
+        if (cap) cap[q] = fminf(cap[q], qs_next_up(M + 1.001f * emax));
+    }
 }
 
 // byte offset of int8 column c of row `row` in a tiled int8 plane of dpb8
@@ -1299,6 +1440,15 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         for (int r = 0; r < R - 1; r++) t.offer(lk[w2][r * 64 + lane], lid[w2][r * 64 + lane], sbk[0], sbi[0], lane);
     t.merge(sbk[0], sbi[0], lane);
     nvalid = snv[0] + snv[1] + snv[2] + snv[3];
+    // with a finite cap the list holds exactly the rows below it (the others
+    // were skipped or rejected): a shard's cap in the sharded phase 2 may leave
+    // fewer than k+1 (the global top-(k+1) rows are all below it)
+    if (cap && cap[q] < __builtin_inff()) {
+        int nb = 0;
+#pragma unroll
+        for (int r = 0; r < R - 1; r++) nb += __popcll(__ballot(t.key[r] < __builtin_inff()));
+        nvalid = nb < nvalid ? nb : nvalid;
+    }
     const int m = (k + 1) < nvalid ? (k + 1) : nvalid;
     bool inc = true;
 #pragma unroll

@@ -287,12 +287,24 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         auto sel = [&](int RV, const int32_t* list, const uint32_t* cnt, float* tA) {
             const unsigned gw = (unsigned)((cn + 3) / 4);
             uint32_t* lc = (ctr_reset && !list) ? idx->qscount : nullptr;
+            const int RT = qs_R(k);  // the filtering select's sorted list: k+1 <= 64 (RT - 1)
+            if (idx->sel_filter) {
+#define WV_SELF(RV, RTV) k_blk_select_f<RV, RTV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc)
+                if (RV == 2) WV_SELF(2, 2);
+                else if (RV == 4) { if (RT == 2) WV_SELF(4, 2); else WV_SELF(4, 4); }
+                else if (RT == 2) WV_SELF(8, 2);
+                else if (RT == 4) WV_SELF(8, 4);
+                else WV_SELF(8, 8);
+#undef WV_SELF
+                return;
+            }
 #define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc)
             if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
 #undef WV_SELR
         };
-        // phase 2 cuts the lists with the global threshold: the local cap no longer bounds them
-        const float* capv = (idx->exact_cap && phase == 0) ? idx->qsCap.as<float>() : nullptr;
+        // per query an upper bound of the (k+1)-th smallest exact distance: the
+        // select's (phase 0), lowered to the global one by k_blk_gthresh (phase 2)
+        const float* capv = idx->exact_cap ? idx->qsCap.as<float>() : nullptr;
         auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0) {
             launch_blk_exact(idx, s, RV, metric, v5, Qn, valid, (int)cn, k, kout, o_ids + c0 * kout, o_d + c0 * kout,
                              o_n + c0, flags, list, cnt, eb, ldE, capv, qinfo, q8 && idx->q8_filter ? &q8f : nullptr);
@@ -303,7 +315,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         if (phase == 2)  // the global threshold cuts this shard's candidate lists
             k_blk_gthresh<<<(unsigned)((cn + 3) / 4), 256, 0, s>>>(gA, gE, W, (int)cn, k, metric, qinfo, a.key, ldk,
                                                                   idx->qsCand.as<uint32_t>(), L, idx->qsNc.as<int32_t>(),
-                                                                  idx->qsEps.as<float>(), flags);
+                                                                  idx->qsEps.as<float>(), flags,
+                                                                  idx->exact_cap ? idx->qsCap.as<float>() : nullptr);
         const size_t bm_lds = (size_t)32 * (idx->dpad + 4) * sizeof(float);
         // (bmE holds cn*L*32 floats: above a 4 GiB budget, or past the 2^23
         // queries k_inv_scatter's packed (q << 9 | j) can name, the

@@ -145,6 +145,7 @@ struct wv_index {
     // 32-row block, built beside the bf16 plane when 384 < dims <= 1536
     int q8_planes = 0, dpb8 = 0;
     int q8_only = 0;                // 1536 < dims <= 3072: int8 planes without the bf16 plane
+    int sel_filter = 1;             // option sel_filter: k_blk_select_f (1) or the sorted-list k_blk_select (0)
     int q8_opt = 1;                 // option q8: block keys from the int8 plane (1) or the bf16 plane (0)
     int q8_R = 0;                   // option q8_R: candidate lists for int8 keys (0: R = 8, 448 blocks)
     int q8_shape = 16;              // option q8_shape: 16 = v_mfma_i32_16x16x64_i8 kernel, 32 = 32x32x32

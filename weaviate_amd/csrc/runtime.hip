@@ -653,6 +653,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     std::string k(key);
     note_mutation(idx);
     if (k == "graph") { idx->graph_opt = value ? 1 : 0; return WV_OK; }
+    if (k == "sel_filter") { idx->sel_filter = value ? 1 : 0; return WV_OK; }
     if (k == "batch_window_us") { if (value < 0 || value > 1000000) return set_err(WV_ERR_INVALID, "batch_window_us out of range"); idx->batch_window_us = value; return WV_OK; }
     if (k == "exact_multi") { idx->exact_multi = value ? 1 : 0; return WV_OK; }
     if (k == "gemv_wg") { if (value < 8 || value > 65536) return set_err(WV_ERR_INVALID, "gemv_wg out of range"); idx->gemv_wg = (int)value; return WV_OK; }
