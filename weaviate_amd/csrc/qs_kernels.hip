@@ -1055,12 +1055,19 @@ __global__ __launch_bounds__(256) void k_blk_select_f(const float* __restrict__ 
     WaveTopL<RT> t;
     t.init();
     float T = __builtin_inff();
+    float Kt = __builtin_inff();  // key-space prefilter: A(v) <= T implies v <= Kt
     int nc = 0;
     bool over = false;
     auto refresh = [&]() {
         t.merge(sbk[w], sbi[w], lane);
         const float mk = t.key_at(k);
         T = mk == __builtin_inff() ? __builtin_inff() : qs_key_to_a(metric, mk, qi.x) + 2.0005f * eps;
+        // A = v (dot), fl(v + |q|^2) (L2), max(0, fl(1 + v)) (cosine): invert
+        // with a few ulps of slack (the exact A <= T test follows the prefilter)
+        if (!(T < __builtin_inff())) Kt = __builtin_inff();
+        else if (metric == DOT) Kt = T;
+        else if (metric == L2) Kt = (T - qi.x) + 4.8e-7f * fmaxf(fabsf(T), qi.x);
+        else Kt = T < 0.f ? -__builtin_inff() : (T - 1.f) + 4.8e-7f * fmaxf(1.f, fabsf(T));
     };
     auto compact = [&]() {
         int n2 = 0;
@@ -1095,11 +1102,12 @@ __global__ __launch_bounds__(256) void k_blk_select_f(const float* __restrict__ 
         if (over) continue;
         bool anyc = false;  // one wave vote per chunk: most chunks append nothing
 #pragma unroll
-        for (int j = 0; j < U; j++) anyc |= v[j] < __builtin_inff() && qs_key_to_a(metric, v[j], qi.x) <= T;
+        for (int j = 0; j < U; j++) anyc |= v[j] <= Kt;
         if (!__any(anyc)) continue;
 #pragma unroll
         for (int j = 0; j < U; j++) {
-            bool in = v[j] < __builtin_inff() && qs_key_to_a(metric, v[j], qi.x) <= T;
+            if (!__any(v[j] <= Kt)) continue;
+            bool in = v[j] <= Kt && v[j] < __builtin_inff() && qs_key_to_a(metric, v[j], qi.x) <= T;
             uint64_t m = __ballot(in);
             if (m == 0) continue;
             int n = __popcll(m);

@@ -287,14 +287,17 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         auto sel = [&](int RV, const int32_t* list, const uint32_t* cnt, float* tA) {
             const unsigned gw = (unsigned)((cn + 3) / 4);
             uint32_t* lc = (ctr_reset && !list) ? idx->qscount : nullptr;
-            const int RT = qs_R(k);  // the filtering select's sorted list: k+1 <= 64 (RT - 1)
-            if (idx->sel_filter) {
+            // the filtering select keeps a sorted list of 64 (RT - 1) >= k+1 entries
+            // instead of the output capacity's: it pays where RT < RV (int8 keys'
+            // 448-block lists at k < 64: C3 select 2.81 -> 2.14 ms, 1.25M-row
+            // shard 1.42 -> 0.59 ms); at RT == RV the sorted-list form is faster
+            // (C2: 0.61 vs 0.92 ms)
+            const int RT = qs_R(k);
+            if (idx->sel_filter && RT < RV) {
 #define WV_SELF(RV, RTV) k_blk_select_f<RV, RTV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc)
-                if (RV == 2) WV_SELF(2, 2);
-                else if (RV == 4) { if (RT == 2) WV_SELF(4, 2); else WV_SELF(4, 4); }
+                if (RV == 4) WV_SELF(4, 2);
                 else if (RT == 2) WV_SELF(8, 2);
-                else if (RT == 4) WV_SELF(8, 4);
-                else WV_SELF(8, 8);
+                else WV_SELF(8, 4);
 #undef WV_SELF
                 return;
             }
