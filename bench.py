@@ -139,6 +139,17 @@ def cpu_baseline(n_sample: int, nq: int, threads: int, spec=None):
     # the scan is linear in N: extrapolate to the full corpus
     qps_full = qps_sample * n_sample / spec["n"]
     kname = ("l2" if metric == orc.L2 else "dot") + ("_512" if variant == orc.AVX512 else "_256")
+    # the reference ships both SIMD variants: time the other one
+    # too where this host can run it (AVX-512 needs the host's support)
+    other = orc.AVX256 if variant == orc.AVX512 else orc.AVX512
+    other_line = None
+    if other == orc.AVX256 or orc.host_has_avx512():
+        t1 = time.perf_counter()
+        orc.cpu_baseline(metric, other, corpus, queries, k, threads, use_ref)
+        dt1 = time.perf_counter() - t1
+        other_line = {"variant": "avx512" if other == orc.AVX512 else "avx256",
+                      "kernel": ("l2" if metric == orc.L2 else "dot") + ("_512" if other == orc.AVX512 else "_256"),
+                      "value": nq / dt1 * n_sample / spec["n"], "seconds": round(dt1, 2)}
     return {
         "value": qps_full,
         "unit": "queries/s",
@@ -148,6 +159,7 @@ def cpu_baseline(n_sample: int, nq: int, threads: int, spec=None):
         "cgroup_cpus": info["cgroup_cpus"],
         "cpu_model": info["cpu_model"],
         "variant": info["variant"],
+        "other_variant": other_line,
         "sample": (f"{nq} queries x {n_sample} rows (first rows of the same corpus), {spec['metric']} k={k}, "
                    f"{'reference ' + kname + ' kernel (oracle/_ref)' if use_ref else 'oracle scalar restatement'} "
                    f"+ NewMax heap scan, {threads} threads, {dt:.1f} s"
