@@ -333,8 +333,10 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             HIPCHK(idx->bmPairs.ensure((size_t)cn * L * sizeof(uint32_t)));
             HIPCHK(idx->bmE.ensure((size_t)cn * ldE * sizeof(float)));
             // bmCnt is all-zero between batches (k_inv_scatter counts it down);
-            // a new or never-completed buffer is zeroed once
-            if (idx->bmCnt_zp != idx->bmCnt.p) HIPCHK(hipMemsetAsync(idx->bmCnt.p, 0, idx->bmCnt.bytes, s));
+            // a new, regrown (the allocator may hand back the same address) or
+            // never-completed buffer is zeroed once
+            if (idx->bmCnt_zp != idx->bmCnt.p || idx->bmCnt_zb != idx->bmCnt.bytes)
+                HIPCHK(hipMemsetAsync(idx->bmCnt.p, 0, idx->bmCnt.bytes, s));
             idx->bmCnt_zp = nullptr;
             const unsigned gw = (unsigned)((cn + 3) / 4);
             k_inv_count<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
@@ -345,6 +347,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                                              idx->bmPairs.as<uint32_t>());
             HIPCHK(hipGetLastError());
             idx->bmCnt_zp = idx->bmCnt.p;
+            idx->bmCnt_zb = idx->bmCnt.bytes;
             launch_exact_bm(idx, s, metric, v5, Qn, nb, bm_lds, ldE);
             HIPCHK(hipGetLastError());
             exa(R, nullptr, nullptr, idx->bmE.as<float>(), ldE);

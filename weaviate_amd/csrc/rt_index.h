@@ -204,7 +204,8 @@ struct wv_index {
     DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
     DBuf rpBlk, rpLb, rpQ, rpE, rpVm, rpOff, rpTot, rpCtr;  // pooled replay (k_rp_*)
     DBuf bmCnt, bmOff, bmPairs, bmE;                          // block-major exact (k_inv_*, k_exact_bm)
-    void* bmCnt_zp = nullptr;                                 // bmCnt.p when it is known all-zero
+    void* bmCnt_zp = nullptr;                                 // bmCnt.p / .bytes when it is known all-zero
+    size_t bmCnt_zb = 0;                                      // (a grown buffer may come back at the same address)
     // hipGraph replay of a repeated identical wv_index_search_device call
     // (option graph): the captured launch sequence is valid while the corpus,
     // its buffers and the options are unchanged (mut_gen) and the call's
