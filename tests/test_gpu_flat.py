@@ -591,3 +591,23 @@ def test_search_device_graph_replay(wv, oracle, metric, kind, n, d, k, nq):
         for a, b in zip(got, ref):
             np.testing.assert_array_equal(a, b, err_msg=f"after delete rep {rep}")
     idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,n,d,k", [
+    ("l2-squared", 0, 40000, 128, 500),    # bf16 keys, 960-block lists (no block-major pass)
+    ("cosine", 0, 40000, 768, 500),        # int8 keys
+    ("l2-squared", 1, 30000, 128, 900),    # integer data: ties -> the heap replay at k = 900
+    ("dot", 0, 20000, 2048, 600),          # int8-only planes
+])
+def test_large_k_stays_on_block_keys(wv, oracle, metric, kind, n, d, k):
+    """448 <= k < 960: the block-key path with 960-block candidate lists
+    (qs_R = 16) instead of the all-rows replay; every query against the oracle."""
+    data = gen(oracle, kind, 97, n, d)
+    queries = gen(oracle, kind, 98, 24, d)
+    idx, orc = build_pair(wv, oracle, metric, "avx256", data)
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    route = wv._lib.ROUTES[idx.stats()["last_route"]]
+    assert route in ("qs_bf16", "qs_w4", "qs_int8"), route
+    for qi in range(len(queries)):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
+    idx.close()

@@ -3,7 +3,9 @@
 // entry points (see rt_index.h for the unit split).
 #include "rt_index.h"
 
-int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : 0; }
+// candidate-list rows R (L = 64 (R - 1) blocks, a power-of-two bitonic width
+// 64 R): k + 1 <= 960 stays on the block-key path
+int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : k + 1 <= 960 ? 16 : 0; }
 
 // phase 0: the whole search.  Sharded two-phase form (mode 1, one query chunk):
 // phase 1 = block keys + local candidate selection, topA [nq][k+1] = this
@@ -26,7 +28,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     if (q8) {  // the int8 bound is wider: 448-block lists (option q8_R; C3: ~110 candidate blocks
                // per query, R = 4 sent a few percent to the overflow pass, profiles/r04_c3ab1_*)
         if (idx->q8_R > 0) R = std::max(R, idx->q8_R);
-        else R = 8;
+        else R = std::max(R, 8);
     }
     const int L = 64 * (R - 1);
     const int64_t nslots = std::max<int64_t>(1, (idx->hiwater + 32 * RB - 1) / (32 * RB));
@@ -302,7 +304,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                 return;
             }
 #define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc)
-            if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else WV_SELR(8);
+            if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else if (RV == 8) WV_SELR(8); else WV_SELR(16);
 #undef WV_SELR
         };
         // per query an upper bound of the (k+1)-th smallest exact distance: the
@@ -324,7 +326,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // (bmE holds cn*L*32 floats: above a 4 GiB budget, or past the 2^23
         // queries k_inv_scatter's packed (q << 9 | j) can name, the
         // candidate-major k_blk_exact computes the distances itself)
-        if (idx->exact_bm && bm_lds <= 64 * 1024 && nb < (1ll << 31) && cn < (1ll << 23) &&
+        if (idx->exact_bm && bm_lds <= 64 * 1024 && nb < (1ll << 31) && cn < (1ll << 23) && L <= 512 &&
             (int64_t)cn * L * 32 * 4 <= (4ll << 30)) {
             // block-major exact distances: invert the candidate lists per block
             const int64_t ldE = (int64_t)L * 32;
