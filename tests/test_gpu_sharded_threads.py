@@ -368,3 +368,63 @@ def test_c5_sharded_pq_full_size(wv, oracle, monkeypatch):
             np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), sd[i, :sn[i]].view(np.uint32))
     for b in backs:
         b.index.close()
+
+
+def test_bq_batch_refused_after_interleaved_add(wv, oracle):
+    """A sharded BQ batch (bq_begin's minima and query codes) ends with any
+    Add / Delete / other query preparation on the index: the later stages
+    (bounds, recorded replay, replay, rescore) are refused instead of reading
+    minima sized for the old corpus (invalidate_batch resets bq_nq)."""
+    from weaviate_amd import WeaviateError
+    from weaviate_amd.sharded import GpuBQShardBackend
+    n, d, k = 6000, 128, 10
+    data = oracle.gen_matrix(0, 57, 0, n + 500, d)
+    idx = wv.FlatIndex(distance="cosine", variant="avx256", bq=True, rescore_limit=40)
+    idx.add_batch(np.arange(n, dtype=np.uint64), data[:n])
+    b = GpuBQShardBackend(idx, 0)
+    q = torch.from_numpy(oracle.gen_matrix(0, 58, 0, 32, d)).to("cuda")
+    # (another search replaces the batch with its own, consistent minima)
+    for interleave in ("add", "delete"):
+        b.bq_begin(q, k)
+        b.bq_bounds()  # the batch is live
+        if interleave == "add":
+            idx.add_batch(np.arange(n, n + 500, dtype=np.uint64), data[n:])
+        else:
+            idx.delete(5)
+        with pytest.raises(WeaviateError):
+            b.bq_bounds()
+    idx.close()
+
+
+def test_sharded_rq_with_an_empty_shard(wv, oracle, monkeypatch):
+    """An empty rank (no rows in its id range) beside rq-8 shards: its block
+    minima are +inf (not a finite 0x7f-byte fill), so the bounds of
+    the later ranks stay those of real rows and every rank returns the single
+    index's result."""
+    from weaviate_amd.sharded import GpuQuantShardBackend
+    per, shards, d, k = 5000, 3, 64, 10
+    data = oracle.gen_matrix(0, 93, 0, per * (shards - 1), d)
+    queries = oracle.gen_matrix(0, 94, 0, 64, d)
+    kw = dict(distance="cosine", variant="avx256", rescore_limit=30, rq={"bits": 8})
+    single = wv.FlatIndex(**kw)
+    single.add_batch(np.arange(per * (shards - 1), dtype=np.uint64), data)
+    si, sd, sn = single.search_by_vector_batch(queries, k)
+    backs = []
+    for r in range(shards):
+        lo = r * per
+        idx = wv.FlatIndex(id_base=lo, dims=d, **kw)
+        if r < shards - 1:
+            idx.add_batch(np.arange(lo, lo + per, dtype=np.uint64), data[lo:lo + per])
+        backs.append(GpuQuantShardBackend(idx, 0))
+    q = torch.from_numpy(queries).to("cuda")
+    out, paths = run_quant_ranks(monkeypatch, backs, q, k, per)
+    for r in range(shards):
+        oi, od, on = (t.numpy() for t in out[r])
+        for i in range(len(queries)):
+            assert on[i] == sn[i], f"rank {r} q{i}"
+            np.testing.assert_array_equal(oi[i, :on[i]].astype(np.uint64), si[i, :sn[i]], err_msg=f"rank {r} q{i}")
+            np.testing.assert_array_equal(od[i, :on[i]].view(np.uint32), sd[i, :sn[i]].view(np.uint32),
+                                          err_msg=f"rank {r} q{i}")
+    for b in backs:
+        b.index.close()
+    single.close()

@@ -133,6 +133,15 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
         delete idx;
         return set_err(WV_ERR_HIP, "create: %s", hipGetErrorString(e));
     }
+    // rq with the dimension configured: the (seeded, dimension-only) rotation
+    // now rather than at the first Add, so an empty shard can answer a search
+    if (idx->rq_bits && idx->dims > 0) {
+        const int rc = rq_init(idx);
+        if (rc) {
+            wv_index_destroy(idx);
+            return rc;
+        }
+    }
     *out = idx;
     return WV_OK;
 }
