@@ -72,6 +72,7 @@ BQ_RESCORE = 200
 PQ_ROWS = 10_000_000
 PQ_DIMS = 960
 PQ_SEGMENTS = 240
+PQ_ADC_DEFAULT = "2"  # the index default of option pq_adc3 (rt_index.h): 2 = k_pq_adc4
 PQ_CENTROIDS = 256
 PQ_TRAIN = 100_000
 # 4-byte LUT lookups from LDS: the LDS array moves 256 B/clk/CU (ds_read_b64 /
@@ -576,7 +577,9 @@ def main():
     # the dominant kernel of each workload: its PMC record (matched on kernel
     # name and configuration) is the only source of `traffic`
     # the sharded PQ search (ShardedQuantSearch) computes full ADC rows with k_pq_adc2
-    pq_kernel = "k_pq_adc3" if pq and not shard and not any(o.replace(" ", "") == "pq_adc3=0" for o in args.option) \
+    pq_opt = [o.replace(" ", "") for o in args.option if o.replace(" ", "").startswith("pq_adc3=")]
+    pq_sel = pq_opt[-1].split("=")[1] if pq_opt else PQ_ADC_DEFAULT
+    pq_kernel = ("k_pq_adc2" if shard or pq_sel == "0" else "k_pq_adc4" if pq_sel == "2" else "k_pq_adc3") if pq \
         else "k_pq_adc2"
     dom_kernel = (pq_kernel if pq else ("k_q8_blockkey_bq" if route == 6 else "k_bq_blockmin_lds") if bq else
                   ("k_rq8_dist" if rq_bits == 8 else "k_rq1_dist") if rq_bits else sel_kernel)

@@ -131,7 +131,7 @@ def test_pq_errors(wv, oracle):
 # k_pq_adc3 (ks = 256 only: queries on the lanes, 1024-row chunks, 64-query groups): a row
 # count off the chunk size, m off the 16-segment group, two query groups (the second
 # partial), deleted rows and an allow list (invalid rows), integer data (ADC ties); the
-# same results as k_pq_adc2 and the oracle
+# same results as k_pq_adc2 and the oracle; k_pq_adc4 (pq_adc3 = 2, 16-byte LUT reads) too
 @pytest.mark.parametrize("metric,kind,rescore,k,rl,allow", [
     ("l2-squared", 0, False, 10, -1, False),
     ("cosine", 0, True, 10, 40, False),
@@ -162,11 +162,12 @@ def test_pq_adc3_matches_adc2_and_oracle(wv, oracle, metric, kind, rescore, k, r
         present &= mask
     queries = gen(oracle, kind, 172, nq, d)
     res = {}
-    for adc3 in (1, 0):
+    for adc3 in (1, 0, 2):
         idx.set_option("pq_adc3", adc3)
         res[adc3] = idx.search_by_vector_batch(queries, k, allow=al)
-    for a, b in zip(res[1], res[0]):
-        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    for alt in (0, 2):
+        for a, b in zip(res[1], res[alt]):
+            np.testing.assert_array_equal(np.asarray(a), np.asarray(b), err_msg=f"pq_adc3={alt}")
     ids, dists, counts = res[1]
     for qi in list(range(0, nq, 7)) + [63, 64, nq - 1]:
         qv = oracle.normalize(queries[qi]) if om == oracle.COSINE else queries[qi]

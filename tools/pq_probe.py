@@ -1,8 +1,9 @@
 """A/B of the PQ ADC kernels on the C5 shape (10M x 960, m=240, ks=256, B=256),
 interleaved in one process; ADC launch time (HIP events) and whole batch.
 Default configs: k_pq_adc3 (pq_adc3=1), k_pq_adc2 (pq_adc3=0), and the adc3
-timing experiments (pq_adc3=3: no LUT DMA, 4: no per-segment barrier; their
-results are wrong by construction and are not compared).  Results of the
+timing experiments (pq_adc3=3: no LUT DMA, 4: no per-segment barrier; 5:
+k_pq_adc4 without LUT DMA; debug library only, WV_LIB_PATH; their results are
+wrong by construction and are not compared).  pq_adc3=2 is k_pq_adc4.  Results of the
 other settings must be identical.  Usage: pq_probe.py [cfg ...]"""
 import os
 import sys
@@ -57,7 +58,7 @@ for cfg in cfgs:
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / 3
     got = (oi.clone(), od.clone(), on.clone())
-    timing_only = cfg in ("pq_adc3=3", "pq_adc3=4")
+    timing_only = cfg in ("pq_adc3=3", "pq_adc3=4", "pq_adc3=5")
     if ref is None and not timing_only:
         ref = got
     same = None if timing_only else all(torch.equal(a, b) for a, b in zip(ref, got))

@@ -870,5 +870,165 @@ __global__ __launch_bounds__(512, 1) void k_pq_adc3(const uint32_t* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_pq_adc4: k_pq_adc3 with 16-byte LUT reads.  Same workgroup (8 waves x 128
+// rows, 64 queries), same LDS image (two [code][64 queries] LUT slots + the
+// [16][1024] code bytes) and the same LUT DMA; lane (qd = lane & 15, r = lane
+// >> 4) keeps the sums of queries 4 qd .. 4 qd + 3 for the rows 128 w + 4 i + r,
+// i < 32 (128 VGPRs).  One ds_read_b128 reads four rows' LUT entries for all
+// 64 queries: its 16-lane groups ({0-3,12-15,20-27}, ...) hold 16 distinct
+// query quads, so their banks (4 qd .. 4 qd + 3) never collide whatever the
+// codes.  Per 256 lookups: one b128 read (4 LDS cycles), one v_perm (the
+// address: byte 0 = 16 qd, byte 1 = row r's code, byte 2 = slot) and two
+// v_pk_add_f32 — k_pq_adc3 spends two b64 reads, two v_perm and two pk_adds.
+// Each sum is the same segment-order fp32 sum: results are bit-identical.
+// ---------------------------------------------------------------------------
+typedef float pq_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ pq_f4 pq4_ld16(unsigned a) {
+    pq_f4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+
+// DBG (timing experiment only, wrong results): 1 = no LUT DMA in the loop
+template <int DBG>
+__global__ __launch_bounds__(512, 1) void k_pq_adc4(const uint32_t* __restrict__ codes, int g16, int m,
+                                                    const uint32_t* __restrict__ valid, int64_t nslots,
+                                                    const float* __restrict__ lutg, int nq, int metric,
+                                                    int64_t nblk_ld, float* __restrict__ bmin) {
+    __shared__ __attribute__((aligned(16))) unsigned char sm[PQ3_LDS];  // the kernel's only LDS: address 0
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int qd = lane & 15, r = lane >> 4;
+    const int64_t row0 = (int64_t)blockIdx.x * PQ3_ROWS;
+    const int G = blockIdx.y;
+    const unsigned smb = (unsigned)(size_t)((pq_lds_t)sm);
+    const unsigned cod = smb + 2 * PQ3_SLOT;
+    // byte 0 = 16 qd (lb), byte 1 = code byte r of the word, byte 2 = slot (lb), byte 3 = 0
+    const uint32_t sel = 0x0c020000u | ((4u + (uint32_t)r) << 8);
+    const uint32_t lb0 = smb + 16u * (uint32_t)qd;
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(lutg + (int64_t)G * m * 256 * 64), (short)0, -1, 0x00020000);
+    auto dma = [&](int sg) {  // LUT segment sg -> slot sg & 1: 8 KiB per wave
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const unsigned off = (unsigned)(i * 8192 + w * 1024);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (pq_lds_t)(size_t)(smb + (unsigned)((sg & 1) * PQ3_SLOT) + off),
+                                                     16, (uint32_t)(16 * lane), (uint32_t)sg * PQ3_SLOT + off, 0, 0);
+        }
+    };
+    auto load_codes = [&](int g, uint4& c0, uint4& c1) {
+        const uint4* cb = reinterpret_cast<const uint4*>(codes);
+        const int64_t rr = row0 + 2 * tid;
+        c0 = rr < nslots ? cb[((rr >> 8) * g16 + g) * 256 + (rr & 255)] : make_uint4(0u, 0u, 0u, 0u);
+        c1 = rr + 1 < nslots ? cb[(((rr + 1) >> 8) * g16 + g) * 256 + ((rr + 1) & 255)] : make_uint4(0u, 0u, 0u, 0u);
+    };
+    auto store_codes = [&](const uint4& c0, const uint4& c1) {
+        const uint32_t a[4] = {c0.x, c0.y, c0.z, c0.w}, b[4] = {c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t v = __builtin_amdgcn_perm(b[k >> 2], a[k >> 2], 0x0c0c0000u | (uint32_t)(k & 3) | ((uint32_t)(4 + (k & 3)) << 8));
+            *(__attribute__((address_space(3))) uint16_t*)(size_t)(cod + (unsigned)(k * PQ3_ROWS + 2 * tid)) = (uint16_t)v;
+        }
+    };
+    pq_f2 sa[32], sb[32];  // queries (4 qd, 4 qd + 1) and (4 qd + 2, 4 qd + 3) of row 4 i + r
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        sa[i] = pq_f2{0.f, 0.f};
+        sb[i] = pq_f2{0.f, 0.f};
+    }
+    uint4 nc0, nc1;
+    load_codes(0, nc0, nc1);
+    dma(0);
+    for (int s = 0; s < m; s++) {
+        if ((s & 15) == 0) {
+            __syncthreads();
+            store_codes(nc0, nc1);
+            if (s + 16 < m) load_codes((s >> 4) + 1, nc0, nc1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // slot s & 1 landed for every wave; slot (s + 1) & 1 is free
+        if (s + 1 < m && DBG != 1) dma(s + 1);
+        const unsigned crow = cod + (unsigned)((s & 15) * PQ3_ROWS + w * 128);
+        uint2 cw[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) cw[j] = pq3_ld8(crow + 8 * j);
+        pq3_wait_lgkm<0>();
+        const uint32_t lb = lb0 + (uint32_t)((s & 1) * PQ3_SLOT);
+        // 32 row quads in batches of 4: batch t + 1's reads in flight while t's are added
+        pq_f4 v[2][4];
+        auto issue = [&](int t, pq_f4 (&dst)[4]) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = 4 * t + u;  // rows 4 i .. 4 i + 3: dword i & 1 of cw[i >> 1]
+                const uint2 c = cw[i >> 1];
+                dst[u] = pq4_ld16(__builtin_amdgcn_perm((i & 1) ? c.y : c.x, lb, sel));
+            }
+        };
+        issue(0, v[0]);
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            if (t + 1 < 8) issue(t + 1, v[(t + 1) & 1]);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (t + 1 < 8) {
+                    switch (u) {
+                    case 0: asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(v[t & 1][0])); break;
+                    case 1: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(v[t & 1][1])); break;
+                    case 2: asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(v[t & 1][2])); break;
+                    default: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(v[t & 1][3])); break;
+                    }
+                } else {
+                    switch (u) {
+                    case 0: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(v[t & 1][0])); break;
+                    case 1: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(v[t & 1][1])); break;
+                    case 2: asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(v[t & 1][2])); break;
+                    default: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[t & 1][3])); break;
+                    }
+                }
+                const pq_f4 x = v[t & 1][u];
+                sa[4 * t + u] += pq_f2{x.x, x.y};
+                sb[4 * t + u] += pq_f2{x.z, x.w};
+            }
+        }
+    }
+    // per query: minimum over this wave's 128 rows (invalid rows +inf), across the
+    // four row lanes r, then the two waves of a 256-row block through LDS
+    const int64_t rw = row0 + (int64_t)w * 128;
+    uint32_t vw[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) vw[k] = rw + 32 * k < nslots ? valid[(rw >> 5) + k] : 0u;
+    float mq[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        const int rr = 4 * i + r;  // row within the wave's 128
+        const bool ok = rw + rr < nslots && ((vw[rr >> 5] >> (rr & 31)) & 1u);
+        if (ok) {
+            mq[0] = fminf(mq[0], pq_wrap(metric, sa[i].x));
+            mq[1] = fminf(mq[1], pq_wrap(metric, sa[i].y));
+            mq[2] = fminf(mq[2], pq_wrap(metric, sb[i].x));
+            mq[3] = fminf(mq[3], pq_wrap(metric, sb[i].y));
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        mq[c] = fminf(mq[c], __shfl_xor(mq[c], 16));
+        mq[c] = fminf(mq[c], __shfl_xor(mq[c], 32));
+    }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(sm);  // [8 waves][64 queries]
+    if (r == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) red[w * 64 + 4 * qd + c] = mq[c];
+    }
+    __syncthreads();
+    if (tid < 256) {  // block b = tid >> 6 (waves 2b, 2b + 1), query j = tid & 63
+        const int b = tid >> 6, j = tid & 63;
+        const int64_t q = (int64_t)G * 64 + j;
+        const int64_t blk = row0 / 256 + b;
+        if (q < nq && blk < nblk_ld) bmin[q * nblk_ld + blk] = fminf(red[(2 * b) * 64 + j], red[(2 * b + 1) * 64 + j]);
+    }
+}
+
 }  // namespace
 }  // namespace wv

@@ -233,7 +233,7 @@ struct wv_index {
     int exact_cap = 1;                                        // k_blk_exact drops values above qsCap (phase 0)
     int replay_dbg = 0;                                       // k_blk_replay clock diagnostics (printf)
     int pq_cand = 1;                                          // PQ search: block minima + candidate blocks (k_pq_cand)
-    int pq_adc3 = 1;                                          // minima by k_pq_adc3 (queries on the lanes), 0: k_pq_adc2
+    int pq_adc3 = 2;                                          // minima: 2 k_pq_adc4 (16-byte LUT reads), 1 k_pq_adc3, 0 k_pq_adc2
     DBuf lutg;                                                // the LUT regrouped for k_pq_adc3 [64-query group][s][c][64]
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
     DBuf flCtr;                      // device flag-list counters (replay_flags)

@@ -672,11 +672,11 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "force_replay") idx->force_replay = (int)value;
     else if (k == "spans") idx->spans_opt = (int)value;
     else if (k == "replay_dbg") idx->replay_dbg = value != 0;  // diagnostics: k_blk_replay clock totals (printf)
-    else if (k == "pq_adc3") {  // 1: k_pq_adc3 (default), 0: k_pq_adc2
-#ifdef WV_PQ_DBG  // 3, 4: timing experiments (wrong results), debug builds only
-        if (value < 0 || value > 4) return set_err(WV_ERR_INVALID, "pq_adc3 must be 0..4");
+    else if (k == "pq_adc3") {  // 2: k_pq_adc4 (16-byte LUT reads, default), 1: k_pq_adc3, 0: k_pq_adc2
+#ifdef WV_PQ_DBG  // 3, 4, 5: timing experiments (wrong results), debug builds only
+        if (value < 0 || value > 5) return set_err(WV_ERR_INVALID, "pq_adc3 must be 0..5");
 #else
-        if (value < 0 || value > 1) return set_err(WV_ERR_INVALID, "pq_adc3 must be 0 or 1");
+        if (value < 0 || value > 2) return set_err(WV_ERR_INVALID, "pq_adc3 must be 0, 1 or 2");
 #endif
         idx->pq_adc3 = (int)value;
     }
