@@ -944,20 +944,19 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
         if (adc3) {
             dim3 g3((unsigned)((nslots + PQ3_ROWS - 1) / PQ3_ROWS), (unsigned)((nq + 63) / 64));
 #define WV_ADC3(DBGV) k_pq_adc3<DBGV><<<g3, 512, 0, s>>>(idx->pq_codes, pq_g16(m), m, valid, nslots, idx->lutg.as<float>(), (int)nq, wrapm, nblk, idx->rB.as<float>())
-            if (idx->pq_adc3 == 2)
-                k_pq_adc4<0><<<g3, 512, 0, s>>>(idx->pq_codes, pq_g16(m), m, valid, nslots, idx->lutg.as<float>(),
-                                                (int)nq, wrapm, nblk, idx->rB.as<float>());
+#define WV_ADC4(DBGV) k_pq_adc4<DBGV><<<g3, 512, 0, s>>>(idx->pq_codes, pq_g16(m), m, valid, nslots, \
+                                   idx->lutg.as<float>(), (int)nq, wrapm, nblk, idx->rB.as<float>())
+            if (idx->pq_adc3 == 2) WV_ADC4(0);
             else
 #ifdef WV_PQ_DBG  // timing experiments only (wrong results), never in the product build
-            if (idx->pq_adc3 == 5)
-                k_pq_adc4<1><<<g3, 512, 0, s>>>(idx->pq_codes, pq_g16(m), m, valid, nslots, idx->lutg.as<float>(),
-                                                (int)nq, wrapm, nblk, idx->rB.as<float>());
+            if (idx->pq_adc3 == 5) WV_ADC4(1);
             else if (idx->pq_adc3 == 3) WV_ADC3(1);
             else if (idx->pq_adc3 == 4) WV_ADC3(2);
             else
 #endif
             WV_ADC3(0);
 #undef WV_ADC3
+#undef WV_ADC4
         } else {
 #define WV_ADC2M(KCV)                                                                                        \
     do {                                                                                                     \
