@@ -604,10 +604,11 @@ def main():
                 "hbm_write_GBps": f0 * ld * 4 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
                 "traffic": args.traffic_bytes}
     elif pq:
-        # dominant kernel k_pq_adc3 (k_pq_adc2 with --option pq_adc3=0): one
-        # LUT lookup (LDS gather) + fp32 add per (query, row, segment); adc3
-        # reads 64 queries' entries of one code per 32-lane ds_read_b64 group
-        # (conflict-free), so the LDS array rate for 4-byte lookups is the peak
+        # dominant kernel k_pq_adc4 (k_pq_adc3 / k_pq_adc2 with --option
+        # pq_adc3=1 / 0): one LUT lookup (LDS read) + fp32 add per (query, row,
+        # segment); adc4 reads 64 queries' entries of four rows' codes per
+        # ds_read_b128 (conflict-free), so the LDS array rate for 4-byte
+        # lookups is the peak
         ld = (n_local + 255) // 256 * 256
         f0 = int(index.stats().get("last_group_queries", 0)) or max(1, min(B, (2 << 30) // (ld * 4)))  # timed first group
         lookups = float(f0) * n_local * PQ_SEGMENTS
