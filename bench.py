@@ -447,11 +447,25 @@ def main():
 
     # ---- build the shard: generate + add in 1M-row chunks (device resident) ----
     t_build = time.perf_counter()
-    index = wv.FlatIndex(distance=metric_name, dims=dims, device=local_rank, variant="avx256", id_base=id0,
-                         bq=bq, rescore_limit=BQ_RESCORE if (bq or rq_bits) else -1,
-                         rq={"bits": rq_bits} if rq_bits else None,
-                         pq={"segments": PQ_SEGMENTS, "centroids": PQ_CENTROIDS, "trainingLimit": PQ_TRAIN,
-                             "rescore": False} if pq else None)
+    multi = None
+    if shard and flat is not None:
+        # the exact search over N GPUs: the library's multi-shard index (multi.hip)
+        # drives the protocol and owns an RCCL communicator; rank 0's unique id
+        # reaches every process over the launcher's process group
+        from weaviate_amd.multi import MultiFlatIndex, rccl_unique_id
+        uid = [rccl_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        multi = MultiFlatIndex(distance=metric_name, dims=dims, devices=[local_rank], world=world, rank0=rank,
+                               id_stride=(n_total + world - 1) // world, transport="rccl", unique_id=uid[0],
+                               variant="avx256")
+        index = multi.shards[0]
+    else:
+        index = wv.FlatIndex(distance=metric_name, dims=dims, device=local_rank, variant="avx256", id_base=id0,
+                             bq=bq, rescore_limit=BQ_RESCORE if (bq or rq_bits) else -1,
+                             rq={"bits": rq_bits} if rq_bits else None,
+                             pq={"segments": PQ_SEGMENTS, "centroids": PQ_CENTROIDS, "trainingLimit": PQ_TRAIN,
+                                 "rescore": False} if pq else None)
     for kv in args.option:
         key, val = kv.split("=", 1)
         index.set_option(key, int(val))
@@ -505,11 +519,11 @@ def main():
         def step():
             return searcher.search(queries, K_)
     elif shard:
-        from weaviate_amd.sharded import GpuShardBackend, ShardedFlatSearch
-        searcher = ShardedFlatSearch(GpuShardBackend(index, local_rank), dev)
-
         def step():
-            return searcher.search(queries, K_)
+            s = torch.cuda.current_stream(dev).cuda_stream
+            multi.search_device(queries.data_ptr(), B, dims, K_, out_ids.data_ptr(), out_d.data_ptr(),
+                                out_n.data_ptr(), s)
+            return out_ids, out_d, out_n
     else:
         def step():
             s = torch.cuda.current_stream(dev).cuda_stream
@@ -525,8 +539,7 @@ def main():
     torch.cuda.synchronize()
     sel_ms, tot_ms = [], []
     replays0 = index.stats()["replayed_queries"]
-    if shard and not (bq or pq or rq_bits):
-        searcher.flagged = 0
+    flagged0 = multi.stats()["flagged"] if multi is not None else 0
     t0 = time.perf_counter()
     res = None
     for _ in range(args.steps):
@@ -541,12 +554,12 @@ def main():
     elapsed = time.perf_counter() - t0
     replays = index.stats()["replayed_queries"] - replays0
     route = int(index.stats().get("last_route", 0))
-    if shard and not (bq or pq or rq_bits):
-        replays = int(searcher.flagged)  # the cross-shard replay's queries (this rank's view = every rank's)
+    if multi is not None:
+        replays = multi.stats()["flagged"] - flagged0  # the cross-shard replay's queries (every rank's view)
     sharded_check = None
     if args.sharded and world == 1 and (flat or pq or rq_bits):
         # the sharded protocol at one rank must equal the single-index search
-        si, sd, sn = step()[:3]
+        si, sd, sn = (t.clone() for t in step()[:3])
         s = torch.cuda.current_stream(dev).cuda_stream
         _lib.check(lib.wv_index_search_device(index._h, queries.data_ptr(), B, dims, K_, 0, out_ids.data_ptr(),
                                               out_d.data_ptr(), out_n.data_ptr(), None, s))
@@ -660,9 +673,7 @@ def main():
                          + " (bf16 in, fp32 accumulate)")
                         + ": block keys = per-32-row minima of the approximate distance; every returned "
                           "distance is the reference-order fp32 value",
-                "bf16_peak_equivalent_frac": achieved / MFMA_BF16_PEAK_TFLOPS,
                 "pipeline_ms": total_avg,
-                "f32_mfma_peak_equivalent_frac": achieved / MFMA_F32_PEAK_TFLOPS,
                 "traffic": args.traffic_bytes,
                 # DVFS: the chip holds a lower clock under this MFMA load; the PMC
                 # record gives the clock and the MFMA pipe's busy fraction
@@ -743,7 +754,9 @@ def main():
                                    else ", worker heap in one parallel hop (block-minimum bounds, recorded "
                                    "insertions, on-device merge)" + (", codebook trained on rank 0 and broadcast" if pq
                                                                      else ", all-gather rescoring") if (pq or rq_bits)
-                                   else ", RCCL all-gather merge") if world > 1 else ""),
+                                   else ", multi-shard index (multi.hip): library-owned RCCL communicator, "
+                                   "all-gathers of the block-key bounds and lists, on-device merge, parallel "
+                                   "cross-shard replay") if world > 1 else ""),
                 "replayed_queries": int(replays),
             },
             **({"sharded_equals_single": sharded_check} if sharded_check is not None else {}),
@@ -756,6 +769,8 @@ def main():
     if world > 1:
         dist.barrier()  # the other ranks wait for rank 0's host legs
     index.close()
+    if multi is not None:
+        multi.close()
     if shard:
         dist.destroy_process_group()
 

@@ -403,6 +403,66 @@ int wv_merge_shards(int32_t device, int32_t nshards, int64_t nq, int32_t k, cons
                     const float *d_dists, const int32_t *d_counts, const int32_t *d_flags, uint64_t *d_out_ids,
                     float *d_out_dists, int32_t *d_out_counts, int32_t *d_out_flags, void *stream);
 
+/* ---- the corpus sharded over GPUs, searched from one process ---------------
+ * Weaviate searches every shard of a node inside one Go process and merges the
+ * shard results there (adapters/repos/db/index.go:1928-2071, the merge
+ * sortby_distances.go:20-48).  wv_multi holds the shards of the ranks
+ * [rank0, rank0 + n_local) of a world of `world` ranks; rank r holds the doc
+ * ids [r * id_stride, (r+1) * id_stride) (the last rank: every id above), so
+ * one search over all ranks equals one flat index over the whole corpus bit
+ * for bit (ids, distances, tie order: the two-phase protocol of DESIGN.md §4,
+ * driven by the library, collectives on a transport it owns):
+ *   WV_TRANSPORT_RCCL   one RCCL communicator per local shard (librccl.so.1,
+ *                       bound at run time).  n_local == world: one process holds
+ *                       every GPU (unique_id may be NULL); otherwise one process
+ *                       per GPU group, all created with the 128-byte id that
+ *                       wv_rccl_unique_id gave rank 0 (the host passes it on);
+ *   WV_TRANSPORT_LOCAL  every rank is a shard of this process (devices may
+ *                       repeat): device copies, for tests and cost models.
+ * Exact (uncompressed) search only; allow lists are not taken. */
+#define WV_TRANSPORT_LOCAL 0
+#define WV_TRANSPORT_RCCL 1
+typedef struct wv_multi wv_multi;
+typedef struct wv_multi_config {
+    wv_config index;          /* every shard's config; .device / .id_base are set per shard */
+    int32_t world;            /* ranks in the world                                      */
+    int32_t rank0;            /* global rank of local shard 0                            */
+    int32_t n_local;          /* shards held by this process (ranks rank0 ..)            */
+    const int32_t *devices;   /* [n_local] HIP device of each local shard                */
+    uint64_t id_stride;       /* doc ids per rank                                        */
+    int32_t transport;        /* WV_TRANSPORT_*                                          */
+    const void *unique_id;    /* RCCL over processes: rank 0's wv_rccl_unique_id bytes   */
+} wv_multi_config;
+int wv_rccl_unique_id(void *out, int64_t cap); /* cap >= 128 */
+int wv_multi_create(const wv_multi_config *cfg, wv_multi **out);
+void wv_multi_destroy(wv_multi *m);
+/* local shard i's index (owned by m): bulk loads, options, stats */
+wv_index *wv_multi_shard(wv_multi *m, int32_t local);
+/* flat.AddBatch routed by id to the owning local shard (an id of another
+ * process's rank is an error) */
+int wv_multi_add_batch(wv_multi *m, const uint64_t *ids, const float *vecs, int64_t n, int64_t d);
+/* SearchByVector over all ranks: queries / outputs on local shard 0's device,
+ * ordered after and before `stream` (NULL: synchronous).  Every process of a
+ * multi-process world calls it with the same queries and gets the results. */
+int wv_multi_search_device(wv_multi *m, const float *d_queries, int64_t nq, int64_t d, int32_t k, uint64_t *d_ids,
+                           float *d_dists, int32_t *d_counts, void *stream);
+/* the same from host buffers (nq x k outputs, ascending, reference tie order) */
+int wv_multi_search_by_vector_batch(wv_multi *m, const float *queries, int64_t nq, int64_t d, int32_t k,
+                                    uint64_t *out_ids, float *out_dists, int32_t *out_counts);
+/* "sim" = 1: local shards run each stage one after another, timed alone
+ * (wv_multi_stage_ms); "rec_cap" (tests): capacity of the parallel replay's
+ * insertion records (0 = max(256, 16 k); a record that overflows sends its
+ * query down the serial chain); any other key is set on every shard */
+int wv_multi_set_option(wv_multi *m, const char *key, int64_t value);
+/* out[n]: searches, flagged queries, overflowed records, chain hops, last
+ * search's flagged and overflowed queries, world, rank0, n_local, transport */
+int wv_multi_stats(wv_multi *m, int64_t *out, int32_t n);
+/* option sim: per-shard stage times averaged over the searches since "sim"
+ * was last set, out[stage][n_local] for
+ * stages phase 1, phase 2, merge, replay, record merge, chain, collectives
+ * (the last one host-timed, in out[6][0]) */
+int wv_multi_stage_ms(wv_multi *m, double *out, int32_t n_local_cap);
+
 /* Provider.SingleDist batched over n pairs of d floats, exact reference order
  * (distancer/provider.go:14-24). Runs on device `device`. */
 int wv_distance_batch(int32_t device, int32_t metric, int32_t variant, const float *a, const float *b, int64_t n,

@@ -576,6 +576,19 @@ def test_search_device_graph_replay(wv, oracle, metric, kind, n, d, k, nq):
         for a, b in zip(got, ref):
             np.testing.assert_array_equal(a, b, err_msg=f"rep {rep}")
     assert idx.stats()["queries"] - q0 == 4 * nq
+    # a caller that reuses one query buffer (a cgo shim's pinned buffer): new
+    # contents at the same address replay the captured graph on the new queries
+    queries2 = gen(oracle, kind, 97, nq, d)
+    for rep in range(2):
+        qd.copy_(torch.from_numpy(queries2))
+        got2 = run()
+        for qi in range(0, nq, max(1, nq // 16)):
+            assert_same(orc.search(queries2[qi], k), got2[0][qi, :got2[2][qi]].astype(np.uint64),
+                        got2[1][qi, :got2[2][qi]], f"rewritten buffer rep {rep} q{qi}")
+        qd.copy_(torch.from_numpy(queries))
+        got = run()
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b, err_msg=f"restored buffer rep {rep}")
     # the corpus changes: near-copies of the first queries become their nearest rows
     extra = (queries[:8] + np.float32(1e-3)).astype(np.float32)
     new_ids = np.arange(n, n + 8, dtype=np.uint64)

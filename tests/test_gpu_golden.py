@@ -74,3 +74,29 @@ def test_flat_search_matches_reference_fixtures(wv, name, batched):
                 np.testing.assert_array_equal(bits(od), bits(dd[qi, :n]), err_msg=f"{name} k{k} q{qi}")
     finally:
         idx.close()
+
+
+@pytest.mark.parametrize("name", ["cos_768", "l2_int_512", "dot_1024"])
+def test_flat_search_matches_wide_reference_fixtures(wv, oracle, name):
+    """Reference-kernel-scored fixtures at 512 / 768 / 1024 dims: the search
+    runs on the int8 block-key route (k_q8_blockkey keys, int8 row filter,
+    reference-order exact pass) and must return every id, distance bit and
+    tie position of the fixture (tools/make_golden.py flat_search_wide)."""
+    from test_oracle import wide_corpus
+    g = np.load(os.path.join(GOLD, "flat_search_wide.npz"))
+    corpus, queries = wide_corpus(oracle, g, name), g[f"{name}_queries"]
+    metric = METRIC_NAME[int(g[f"{name}_metric"])]
+    idx = wv.FlatIndex(distance=metric, variant="avx256", dims=0)
+    idx.add_batch(np.arange(corpus.shape[0], dtype=np.uint64), corpus)
+    try:
+        for k in (1, 10, 33):
+            ids, dd, cnt = g[f"{name}_k{k}_ids"], g[f"{name}_k{k}_dists"], g[f"{name}_k{k}_counts"]
+            gi, gd, gc = idx.search_by_vector_batch(queries, k)
+            assert idx.stats()["last_route"] == 3  # WV_ROUTE_QS_INT8
+            for qi in range(len(queries)):
+                n = int(cnt[qi])
+                assert gc[qi] == n, (name, k, qi)
+                np.testing.assert_array_equal(gi[qi, :n], ids[qi, :n], err_msg=f"{name} k{k} q{qi}")
+                np.testing.assert_array_equal(bits(gd[qi, :n]), bits(dd[qi, :n]), err_msg=f"{name} k{k} q{qi}")
+    finally:
+        idx.close()

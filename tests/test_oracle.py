@@ -136,6 +136,39 @@ def test_oracle_flat_search_matches_golden(oracle):
                 np.testing.assert_array_equal(bits(od), bits(dd[qi, :n]))
 
 
+def wide_corpus(oracle, g, name):
+    """A flat_search_wide.npz corpus: regenerated from its generator parameters
+    (tools/make_golden.py flat_search_wide) and checked against its checksum."""
+    kind, seed, n, d = (int(x) for x in g[f"{name}_gen"])
+    corpus = oracle.gen_matrix(kind, seed, 0, n, d)
+    if int(g[f"{name}_dup7"]):
+        corpus[1::7] = corpus[0::7][: len(corpus[1::7])]
+    assert int(corpus.view(np.uint32).astype(np.uint64).sum()) == int(g[f"{name}_checksum"])
+    return corpus
+
+
+def test_oracle_flat_search_matches_wide_golden(oracle):
+    """The same at 512 / 768 / 1024 dims (rows the GPU searches on the int8
+    block-key route): restated kernels + heap == the reference's compiled
+    kernels + restated heap."""
+    g = np.load(os.path.join(GOLD, "flat_search_wide.npz"))
+    for name in ["cos_768", "l2_int_512", "dot_1024"]:
+        corpus, queries, metric = wide_corpus(oracle, g, name), g[f"{name}_queries"], int(g[f"{name}_metric"])
+        orc = oracle.OracleFlat(metric, oracle.AVX256, corpus.shape[1], corpus.shape[0])
+        orc.add_batch(np.arange(corpus.shape[0]), corpus)
+        for k in (1, 10, 33):
+            ids, dd, cnt = g[f"{name}_k{k}_ids"], g[f"{name}_k{k}_dists"], g[f"{name}_k{k}_counts"]
+            for qi in range(len(queries)):
+                rc, oi, od = orc.search(queries[qi], k)
+                assert rc == 0
+                n = int(cnt[qi])
+                np.testing.assert_array_equal(oi, ids[qi, :n], err_msg=f"{name} k{k} q{qi}")
+                np.testing.assert_array_equal(bits(od), bits(dd[qi, :n]))
+    # the integer case holds exact ties inside the top 33
+    d = g["l2_int_512_k33_dists"]
+    assert any(len(np.unique(r)) < len(r) for r in d)
+
+
 def test_tie_order_is_heap_order_not_sorted(oracle):
     """The reference result is NOT a (dist, id) sort under ties:
     make sure the fixtures exercise that."""

@@ -9,6 +9,8 @@ Runs in the CPU container only (needs /root/reference for oracle/_ref):
                        by the reference's compiled kernels and ranked by the
                        restated NewMax heap scan (oracle/baseline.c with
                        use_ref=1);
+  * flat_search_wide.npz -- the same at 512 / 768 / 1024 dims (the int8
+                       block-key route), corpora as generator parameters;
   * bq.npz          -- BinaryQuantizer.Encode known answers from
                        compressionhelpers/binary_quantization_test.go:102-146.
 
@@ -104,6 +106,47 @@ def flat_search():
     np.savez_compressed(os.path.join(OUT, "flat_search.npz"), **res)
 
 
+def flat_search_wide():
+    """Rows wide enough for the int8 block-key route (384 < d <= 1536): the
+    corpus is kept as its generator parameters (oracle.gen_matrix: the
+    counter-based generator the GPU tests share) plus a checksum of its bits,
+    the queries and the reference-kernel-scored results are stored."""
+    res = {}
+    for name, metric, kind, n, d, seed in [("cos_768", orc.COSINE, 0, 4000, 768, 11),
+                                           ("l2_int_512", orc.L2, 1, 3000, 512, 12),
+                                           ("dot_1024", orc.DOT, 0, 2000, 1024, 13)]:
+        corpus = orc.gen_matrix(kind, seed, 0, n, d)
+        queries = orc.gen_matrix(kind, seed + 100, 0, 12, d)
+        if name == "l2_int_512":  # near-duplicate rows: exact ties inside the candidate blocks
+            corpus[1::7] = corpus[0::7][: len(corpus[1::7])]
+        store = corpus.copy()
+        q = queries.copy()
+        if metric == orc.COSINE:
+            orc.lib().or_normalize_rows(orc.f(store), store.shape[0], d)
+            orc.lib().or_normalize_rows(orc.f(q), q.shape[0], d)
+        for k in (1, 10, 33):
+            ids, dd, cnt = orc.cpu_baseline(metric, orc.AVX256, store, q, k, 4, use_ref=True)
+            res[f"{name}_k{k}_ids"] = ids
+            res[f"{name}_k{k}_dists"] = dd
+            res[f"{name}_k{k}_counts"] = cnt
+        res[f"{name}_gen"] = np.array([kind, seed, n, d], np.int64)
+        res[f"{name}_dup7"] = np.array(1 if name == "l2_int_512" else 0)
+        res[f"{name}_checksum"] = np.array(int(corpus.view(np.uint32).astype(np.uint64).sum()), np.uint64)
+        res[f"{name}_queries"] = queries
+        res[f"{name}_metric"] = np.array(metric)
+    np.savez_compressed(os.path.join(OUT, "flat_search_wide.npz"), **res)
+
+
+def wide_corpus(g, name):
+    """The corpus of a flat_search_wide.npz case, regenerated and checked."""
+    kind, seed, n, d = (int(x) for x in g[f"{name}_gen"])
+    corpus = orc.gen_matrix(kind, seed, 0, n, d)
+    if int(g[f"{name}_dup7"]):
+        corpus[1::7] = corpus[0::7][: len(corpus[1::7])]
+    assert int(corpus.view(np.uint32).astype(np.uint64).sum()) == int(g[f"{name}_checksum"])
+    return corpus
+
+
 def bq():
     # binary_quantization_test.go:102-123 fixed values
     fixed_in = np.array([-1, 1, 0, np.nan, np.inf, -np.inf], np.float32)
@@ -115,6 +158,7 @@ if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     distances()
     flat_search()
+    flat_search_wide()
     bq()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -53,6 +53,19 @@ class WvConfig(C.Structure):
     ]
 
 
+class WvMultiConfig(C.Structure):
+    _fields_ = [
+        ("index", WvConfig),
+        ("world", C.c_int32),
+        ("rank0", C.c_int32),
+        ("n_local", C.c_int32),
+        ("devices", C.POINTER(C.c_int32)),
+        ("id_stride", C.c_uint64),
+        ("transport", C.c_int32),
+        ("unique_id", C.c_void_p),
+    ]
+
+
 class WvStats(C.Structure):
     _fields_ = [
         ("queries", C.c_uint64),
@@ -111,6 +124,16 @@ SIGNATURES = {
     "wv_heap_merge_records": (C.c_int, [i32, i32, i32, i32, i32, P, P, P, P, P, P, P, P, P, P, P]),
     "wv_index_replay": (C.c_int, [P, P, i64, i64, i32, pi32, i32, pu64, pf32, pi32, i32, pu64, pf32, pi32]),
     "wv_merge_shards": (C.c_int, [i32, i32, i64, i32, P, P, P, P, P, P, P, P, P]),
+    "wv_rccl_unique_id": (C.c_int, [P, i64]),
+    "wv_multi_create": (C.c_int, [C.POINTER(WvMultiConfig), C.POINTER(P)]),
+    "wv_multi_destroy": (None, [P]),
+    "wv_multi_shard": (P, [P, i32]),
+    "wv_multi_add_batch": (C.c_int, [P, pu64, pf32, i64, i64]),
+    "wv_multi_search_device": (C.c_int, [P, P, i64, i64, i32, P, P, P, P]),
+    "wv_multi_search_by_vector_batch": (C.c_int, [P, pf32, i64, i64, i32, pu64, pf32, pi32]),
+    "wv_multi_set_option": (C.c_int, [P, C.c_char_p, i64]),
+    "wv_multi_stats": (C.c_int, [P, C.POINTER(C.c_int64), i32]),
+    "wv_multi_stage_ms": (C.c_int, [P, C.POINTER(C.c_double), i32]),
     "wv_distance_batch": (C.c_int, [i32, i32, i32, pf32, pf32, i64, i64, pf32]),
     "wv_hamming_bitwise_batch": (C.c_int, [i32, pu64, pu64, i64, i64, pf32]),
     "wv_bq_encode_batch": (C.c_int, [i32, pf32, i64, i64, pu64]),

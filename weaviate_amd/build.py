@@ -13,9 +13,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libwvknn.so")
 # translation units compiled in parallel (see csrc/rt_index.h) and linked into one library
-UNITS = ["runtime.hip", "qs_runtime.hip", "qs_exact.hip", "qs_replay.hip", "quant_runtime.hip"]
+UNITS = ["runtime.hip", "qs_runtime.hip", "qs_exact.hip", "qs_replay.hip", "quant_runtime.hip", "multi.hip"]
 SOURCES = [os.path.join(HERE, "csrc", f) for f in (
-    "runtime.hip", "qs_runtime.hip", "qs_exact.hip", "qs_replay.hip", "quant_runtime.hip", "rt_index.h", "kernels.hip", "bq_kernels.hip",
+    "runtime.hip", "qs_runtime.hip", "qs_exact.hip", "qs_replay.hip", "quant_runtime.hip", "multi.hip", "rt_index.h", "kernels.hip", "bq_kernels.hip",
     "pq_kernels.hip", "kernels_bf3.hip", "rq_kernels.hip", "lsm_segment.hip", "batcher.hip", "gemv_kernels.hip",
     "qs_kernels.hip", "q8_kernels.hip", "sq_kernels.hip", "vector_index.hip", "wv_device.h")] + [os.path.join(REPO, "include", "wv_knn.h")]
 OBJDIR = os.path.join(HERE, "build")
@@ -38,17 +38,29 @@ def needs_rebuild() -> bool:
     return any(os.path.getmtime(s) > t for s in SOURCES if os.path.exists(s))
 
 
+def unit_stale(u: str, obj: str) -> bool:
+    """A unit's object is stale when the unit or a shared header (every source
+    that is not another unit) is newer."""
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    others = {os.path.join(HERE, "csrc", x) for x in UNITS if x != u}
+    return any(os.path.getmtime(s) > t for s in SOURCES if os.path.exists(s) and s not in others)
+
+
 def build_library(force: bool = False, verbose: bool = True) -> str:
     if force or needs_rebuild():
         os.makedirs(OBJDIR, exist_ok=True)
         procs, objs = [], []
         for u in UNITS:
             obj = os.path.join(OBJDIR, u.replace(".hip", ".o"))
+            objs.append(obj)
+            if not force and not unit_stale(u, obj):
+                continue
             cmd = [HIPCC, *FLAGS, "-I" + os.path.join(REPO, "include"), "-c", os.path.join(HERE, "csrc", u), "-o", obj]
             if verbose:
                 print("[weaviate_amd] " + " ".join(cmd), file=sys.stderr)
             procs.append((u, subprocess.Popen(cmd)))
-            objs.append(obj)
         failed = [u for u, p in procs if p.wait() != 0]
         if failed:
             raise subprocess.CalledProcessError(1, "hipcc " + " ".join(failed))

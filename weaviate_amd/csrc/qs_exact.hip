@@ -10,7 +10,7 @@
 void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
                       const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
                       int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
-                      const float* capv, const float4* qinfo, const Q8Filter* q8f) {
+                      const float* capv, const float4* qinfo, const Q8Filter* q8f, const uint32_t* fmask) {
     // the capped pass filters rows by their bf16-plane bound (k_blk_exact);
     // gacc_r: plane_dot's two-way accumulation of dpb products
     const uint16_t* Xb = idx->qs_planes && idx->exact_filter ? idx->Xb : nullptr;
@@ -20,8 +20,8 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
     if (q8f && idx->exact_filter && (Xb || idx->q8_only)) f8 = *q8f;
 #define WV_EXR(RV, M, V)                                                                                             \
     do {                                                                                                             \
-        if (eb) k_blk_exact<RV, M, V, true><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8); \
-        else k_blk_exact<RV, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8); \
+        if (eb) k_blk_exact<RV, M, V, true><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, nullptr); \
+        else k_blk_exact<RV, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, fmask); \
     } while (0)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \
@@ -31,7 +31,7 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
     }
     if (RV == 2) { WV_EXM(2); } else if (RV == 4) { WV_EXM(4); } else if (RV == 8) { WV_EXM(8); }
     else {  // k + 1 <= 960: 960-block lists, never block-major (9-bit list positions)
-#define WV_EX16(M, V) k_blk_exact<16, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8)
+#define WV_EX16(M, V) k_blk_exact<16, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, nullptr)
         switch (metric) {
         case L2: if (v5) WV_EX16(L2, AVX512); else WV_EX16(L2, AVX256); break;
         case DOT: if (v5) WV_EX16(DOT, AVX512); else WV_EX16(DOT, AVX256); break;
@@ -41,6 +41,21 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
     }
 #undef WV_EXM
 #undef WV_EXR
+}
+
+// k_q8_filt_bm<METRIC>: the int8 row filter block-major (survivor masks of
+// every listing, fmask [cn][L]); the capped exact pass reads them
+void launch_q8_filt_bm(wv_index* idx, hipStream_t s, int metric, const Q8Filter& f, const uint32_t* valid, int64_t nb,
+                       int L, const float* capv, const float4* qinfo, uint32_t* fmask) {
+    const float gd = (float)gamma_n(idx->dpb + 8);
+    const size_t lds = (size_t)(f.dpb8 >> 5) * 1024 + (size_t)8 * (f.dpb8 >> 5) * 32;
+#define WV_FB(M) k_q8_filt_bm<M><<<(unsigned)nb, 256, lds, s>>>(f, idx->xnorm2, valid, idx->hiwater, idx->bmOff.as<uint32_t>(), idx->bmPairs.as<uint32_t>(), L, capv, qinfo, idx->d_maxn2, gd, fmask)
+    switch (metric) {
+    case L2: WV_FB(L2); break;
+    case DOT: WV_FB(DOT); break;
+    default: WV_FB(COSINE); break;
+    }
+#undef WV_FB
 }
 
 // k_exact_bm<METRIC, VARIANT>: every listed (query, row) distance of each

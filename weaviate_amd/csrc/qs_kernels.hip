@@ -1349,7 +1349,8 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
                                                    const float* __restrict__ cap, const float4* __restrict__ qinfo,
                                                    const uint16_t* __restrict__ Xb, int dpb, const float* __restrict__ xn2,
                                                    const uint32_t* __restrict__ qsmax, const uint32_t* __restrict__ maxn2,
-                                                   float gd, float gacc_r, const Q8Filter q8f) {
+                                                   float gd, float gacc_r, const Q8Filter q8f,
+                                                   const uint32_t* __restrict__ fmask) {
     constexpr int L = 64 * (R - 1);
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
@@ -1381,7 +1382,11 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     const bool f8 = !EB && q8f.X8 != nullptr && cap != nullptr && qi.w == 0.f && q8f.dpb8 <= Q8_FILT_DPB;
     const bool filt = f8 || (!EB && Xb != nullptr && cap != nullptr && qi.w == 0.f && dpb <= QS_FILT_DPB);
     float eps_r = 0.f, capq = __builtin_inff(), sqs = 0.f;
-    if (f8) {
+    // the block-major int8 filter (k_q8_filt_bm) already decided each row
+    const bool fm = f8 && fmask != nullptr;
+    if (fm) {
+        capq = cap[q];
+    } else if (f8) {
         for (int c4 = 4 * threadIdx.x; c4 < q8f.dpb8; c4 += 1024)
             sq8[c4 >> 2] = *reinterpret_cast<const uint32_t*>(q8f.Q8 + q8_plane_byte(q, c4, q8f.dpb8));
         eps_r = qs_eps(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, q8f.qinfo8[q], q8f.qmax8, maxn2, gd,
@@ -1410,8 +1415,9 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         if (EB) {  // its own instantiation: the distance code's registers stay out of the read-back form
             if (ok) e = ebuf[(int64_t)q * ldE + j * 32 + li];
         } else if (filt) {
-            const bool need = ok && (f8 ? plane_a_q8<METRIC>(q8f.X8, q8f.sb8, xn2, row, q8f.dpb8, sq8, sqs, qi.x)
-                                        : plane_a<METRIC>(Xb, xn2, row, dpb, sqh, qi.x)) - eps_r < capq;
+            const bool need = fm ? ok && ((fmask[(int64_t)q * L + (j < nc ? j : 0)] >> li) & 1u)
+                                 : ok && (f8 ? plane_a_q8<METRIC>(q8f.X8, q8f.sb8, xn2, row, q8f.dpb8, sq8, sqs, qi.x)
+                                             : plane_a<METRIC>(Xb, xn2, row, dpb, sqh, qi.x)) - eps_r < capq;
             const float dl = coop ? exact8_compact<METRIC>(qv, X, dpad, d, row, need, lane, sslot[w])
                                   : need ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
             if (need) e = dl;
@@ -1508,29 +1514,61 @@ __global__ __launch_bounds__(256) void k_inv_count(const uint32_t* __restrict__ 
 
 // exclusive prefix of cnt[0..nb) -> off[0..nb]; cnt stays (the scatter counts
 // it back down to 0, so the next batch starts from a zeroed array without a
-// fill); one workgroup of 1024 threads
-__global__ __launch_bounds__(1024) void k_inv_scan(uint32_t* __restrict__ cnt, int64_t nb, uint32_t* __restrict__ off) {
-    __shared__ uint32_t part[1024];
-    const int t = threadIdx.x;
-    const int64_t per = (nb + 1023) / 1024;
-    const int64_t b0 = (int64_t)t * per, b1 = b0 + per < nb ? b0 + per : nb;
+// fill).  Two passes over chunks of 4096 counts: k_inv_part sums each chunk
+// (coalesced), k_inv_scan adds the sums of the chunks before its own and
+// scans the chunk (4 contiguous counts per thread + a workgroup scan).
+constexpr int INV_CHUNK = 4096;
+__global__ __launch_bounds__(1024) void k_inv_part(const uint32_t* __restrict__ cnt, int64_t nb,
+                                                   uint32_t* __restrict__ part) {
+    __shared__ uint32_t ws[16];
+    const int64_t base = (int64_t)blockIdx.x * INV_CHUNK;
     uint32_t s = 0;
-    for (int64_t b = b0; b < b1; b++) s += cnt[b];
-    part[t] = s;
+    for (int i = threadIdx.x; i < INV_CHUNK; i += 1024) s += base + i < nb ? cnt[base + i] : 0u;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
     __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < 16; w++) t += ws[w];
+        part[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_inv_scan(const uint32_t* __restrict__ cnt, int64_t nb,
+                                                   const uint32_t* __restrict__ part, uint32_t* __restrict__ off) {
+    __shared__ uint32_t sc[1024];
+    __shared__ uint32_t ws[16];
+    const int t = threadIdx.x;
+    // the chunks before this one
+    uint32_t pre = 0;
+    for (int c = t; c < (int)blockIdx.x; c += 1024) pre += part[c];
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+    if ((t & 63) == 0) ws[t >> 6] = pre;
+    const int64_t base = (int64_t)blockIdx.x * INV_CHUNK + 4 * t;
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        v[i] = base + i < nb ? cnt[base + i] : 0u;
+        s += v[i];
+    }
+    sc[t] = s;
+    __syncthreads();
+    uint32_t run = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) run += ws[w];
     for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t v = t >= o ? part[t - o] : 0u;
+        const uint32_t x = t >= o ? sc[t - o] : 0u;
         __syncthreads();
-        part[t] += v;
+        sc[t] += x;
         __syncthreads();
     }
-    uint32_t run = part[t] - s;
-    for (int64_t b = b0; b < b1; b++) {
-        const uint32_t c = cnt[b];
-        off[b] = run;
-        run += c;
+    run += sc[t] - s;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if (base + i < nb) off[base + i] = run;
+        run += v[i];
     }
-    if (t == 1023) off[nb] = part[1023];
+    if (base < nb && base + 4 >= nb) off[nb] = run;  // the thread holding the last count
 }
 
 __global__ __launch_bounds__(256) void k_inv_scatter(const uint32_t* __restrict__ cand, const int32_t* __restrict__ ncand,
@@ -1575,6 +1613,74 @@ __global__ __launch_bounds__(256) void k_exact_bm(const float* __restrict__ X, i
         const int64_t q = pr >> 9;
         const int j = (int)(pr & 511u);
         ebuf[q * ldE + j * 32 + li] = exact_dist<METRIC, VARIANT>(Qn + q * dpad, xr, d);
+    }
+}
+
+// Block-major int8 row filter of the capped exact pass (int8 block keys,
+// int8 rows of up to 1536 columns).  Candidate-major, every listing query
+// re-reads its candidate block's codes from HBM (C3: ~920k listings over
+// ~312k distinct blocks per 8192-query batch, 22.6 GB); here one workgroup per
+// listed 32-row block (the k_inv_* inversion) stages the block's codes in LDS
+// once and gives every listing (query, list position) the 32 rows' survivor
+// mask: bit r = row r is valid and A_row - eps_r < cap(q), with A_row the
+// same float arithmetic as plane_a_q8 (so the same rows survive).  LDS:
+// [chunk][32 rows][32 B] block codes, then per wave two listings' query codes.
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_q8_filt_bm(const Q8Filter f, const float* __restrict__ xn2,
+                                                    const uint32_t* __restrict__ valid, int64_t nrows,
+                                                    const uint32_t* __restrict__ off, const uint32_t* __restrict__ pairs,
+                                                    int L, const float* __restrict__ cap,
+                                                    const float4* __restrict__ qinfo,
+                                                    const uint32_t* __restrict__ maxn2, float gd,
+                                                    uint32_t* __restrict__ fmask) {
+    extern __shared__ uint4 fsm4[];
+    const int64_t b = blockIdx.x;
+    const uint32_t p0 = off[b], p1 = off[b + 1];
+    if (p0 == p1) return;
+    const int t = threadIdx.x;
+    const int nch = f.dpb8 >> 5;  // 32-byte column chunks
+    // the block's rows are 1 KiB contiguous per chunk in the tiled plane
+    const uint4* src = reinterpret_cast<const uint4*>(f.X8 + (b >> 3) * (int64_t)f.dpb8 * 256 + (b & 7) * 1024);
+    for (int i = t; i < nch * 64; i += 256) fsm4[i] = src[(int64_t)(i >> 6) * 512 + (i & 63)];
+    const int lane = t & 63, w = t >> 6, li = lane & 31, lh = lane >> 5;
+    uint4* qs = fsm4 + nch * 64 + (w * 2 + lh) * nch * 2;
+    const int64_t row = b * 32 + li;
+    const bool okr = row < nrows && ((valid[row >> 5] >> li) & 1u);
+    const float sbk = f.sb8[b];
+    const float x2 = METRIC == L2 ? xn2[row] : 0.f;
+    __syncthreads();
+    for (uint32_t pb = p0 + 2 * w; pb < p1; pb += 8) {
+        const uint32_t p = pb + lh;
+        const bool has = p < p1;
+        const uint32_t pr = pairs[has ? p : pb];
+        const int64_t q = pr >> 9;
+        const int j = (int)(pr & 511u);
+        for (int i = li; i < nch * 2; i += 32)
+            qs[i] = *reinterpret_cast<const uint4*>(f.Q8 + ((q >> 8) * nch + (i >> 1)) * 8192 + (q & 255) * 32 +
+                                                    (i & 1) * 16);
+        wave_sync_lds();
+        int acc = 0;
+        for (int c = 0; c < nch; c++) {
+            const uint4 v0 = fsm4[c * 64 + li * 2], v1 = fsm4[c * 64 + li * 2 + 1];
+            const uint4 a0 = qs[2 * c], a1 = qs[2 * c + 1];
+            acc = __builtin_amdgcn_sdot4((int)v0.x, (int)a0.x, acc, false);
+            acc = __builtin_amdgcn_sdot4((int)v0.y, (int)a0.y, acc, false);
+            acc = __builtin_amdgcn_sdot4((int)v0.z, (int)a0.z, acc, false);
+            acc = __builtin_amdgcn_sdot4((int)v0.w, (int)a0.w, acc, false);
+            acc = __builtin_amdgcn_sdot4((int)v1.x, (int)a1.x, acc, false);
+            acc = __builtin_amdgcn_sdot4((int)v1.y, (int)a1.y, acc, false);
+            acc = __builtin_amdgcn_sdot4((int)v1.z, (int)a1.z, acc, false);
+            acc = __builtin_amdgcn_sdot4((int)v1.w, (int)a1.w, acc, false);
+        }
+        const float eps_r = qs_eps(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, f.qinfo8[q], f.qmax8, maxn2,
+                                   gd, f.gacc8);
+        const float s = f.qscale[q] * sbk;
+        const float Sf = (float)acc;
+        const float kv = METRIC == L2 ? fmaf(-2.f * s, Sf, x2) : -(s * Sf);
+        const float A = qs_key_to_a(METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2, kv, qinfo[q].x);
+        const uint64_t m = __ballot(okr && A - eps_r < cap[q]);
+        if (has && li == 0) fmask[q * L + j] = (uint32_t)(m >> (32 * lh));
+        wave_sync_lds();  // the next listings' codes overwrite qs
     }
 }
 

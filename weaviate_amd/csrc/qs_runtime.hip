@@ -310,9 +310,11 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // per query an upper bound of the (k+1)-th smallest exact distance: the
         // select's (phase 0), lowered to the global one by k_blk_gthresh (phase 2)
         const float* capv = idx->exact_cap ? idx->qsCap.as<float>() : nullptr;
-        auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0) {
+        auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0,
+                       const uint32_t* fmask = nullptr) {
             launch_blk_exact(idx, s, RV, metric, v5, Qn, valid, (int)cn, k, kout, o_ids + c0 * kout, o_d + c0 * kout,
-                             o_n + c0, flags, list, cnt, eb, ldE, capv, qinfo, q8 && idx->q8_filter ? &q8f : nullptr);
+                             o_n + c0, flags, list, cnt, eb, ldE, capv, qinfo, q8 && idx->q8_filter ? &q8f : nullptr,
+                             fmask);
         };
         if (phase != 2) sel(R, nullptr, nullptr, phase == 1 ? topA : nullptr);
         HIPCHK(hipGetLastError());
@@ -326,14 +328,21 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // (bmE holds cn*L*32 floats: above a 4 GiB budget, or past the 2^23
         // queries k_inv_scatter's packed (q << 9 | j) can name, the
         // candidate-major k_blk_exact computes the distances itself)
-        if (idx->exact_bm && bm_lds <= 64 * 1024 && nb < (1ll << 31) && cn < (1ll << 23) && L <= 512 &&
-            (int64_t)cn * L * 32 * 4 <= (4ll << 30)) {
+        const bool bm_rows = idx->exact_bm && bm_lds <= 64 * 1024 && nb < (1ll << 31) && cn < (1ll << 23) && L <= 512 &&
+                             (int64_t)cn * L * 32 * 4 <= (4ll << 30);
+        // wider rows with int8 keys: the int8 row filter runs block-major
+        // (k_q8_filt_bm reads each listed block's codes once), the exact
+        // distances stay per query
+        const bool bm_filt = !bm_rows && q8 && idx->q8_bm && idx->q8_filter && idx->exact_filter && capv &&
+                             idx->dpb8 <= 1536 && nb < (1ll << 31) && cn < (1ll << 23) && L <= 512;
+        if (bm_rows || bm_filt) {
             // block-major exact distances: invert the candidate lists per block
             const int64_t ldE = (int64_t)L * 32;
             HIPCHK(idx->bmCnt.ensure((size_t)nb * sizeof(uint32_t)));
             HIPCHK(idx->bmOff.ensure((size_t)(nb + 1) * sizeof(uint32_t)));
             HIPCHK(idx->bmPairs.ensure((size_t)cn * L * sizeof(uint32_t)));
-            HIPCHK(idx->bmE.ensure((size_t)cn * ldE * sizeof(float)));
+            if (bm_rows) HIPCHK(idx->bmE.ensure((size_t)cn * ldE * sizeof(float)));
+            else HIPCHK(idx->fMask.ensure((size_t)cn * L * sizeof(uint32_t)));
             // bmCnt is all-zero between batches (k_inv_scatter counts it down);
             // a new, regrown (the allocator may hand back the same address) or
             // never-completed buffer is zeroed once
@@ -343,16 +352,26 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             const unsigned gw = (unsigned)((cn + 3) / 4);
             k_inv_count<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
                                            idx->bmCnt.as<uint32_t>());
-            k_inv_scan<<<1, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmOff.as<uint32_t>());
+            const unsigned nparts = (unsigned)((nb + INV_CHUNK - 1) / INV_CHUNK);
+            HIPCHK(idx->bmPart.ensure((size_t)nparts * sizeof(uint32_t)));
+            k_inv_part<<<nparts, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmPart.as<uint32_t>());
+            k_inv_scan<<<nparts, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmPart.as<uint32_t>(),
+                                               idx->bmOff.as<uint32_t>());
             k_inv_scatter<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
                                              idx->bmOff.as<uint32_t>(), idx->bmCnt.as<uint32_t>(),
                                              idx->bmPairs.as<uint32_t>());
             HIPCHK(hipGetLastError());
             idx->bmCnt_zp = idx->bmCnt.p;
             idx->bmCnt_zb = idx->bmCnt.bytes;
-            launch_exact_bm(idx, s, metric, v5, Qn, nb, bm_lds, ldE);
-            HIPCHK(hipGetLastError());
-            exa(R, nullptr, nullptr, idx->bmE.as<float>(), ldE);
+            if (bm_rows) {
+                launch_exact_bm(idx, s, metric, v5, Qn, nb, bm_lds, ldE);
+                HIPCHK(hipGetLastError());
+                exa(R, nullptr, nullptr, idx->bmE.as<float>(), ldE);
+            } else {
+                launch_q8_filt_bm(idx, s, metric, q8f, valid, nb, L, capv, qinfo, idx->fMask.as<uint32_t>());
+                HIPCHK(hipGetLastError());
+                exa(R, nullptr, nullptr, nullptr, 0, idx->fMask.as<uint32_t>());
+            }
         } else {
             exa(R, nullptr, nullptr);
         }

@@ -204,6 +204,9 @@ struct wv_index {
     DBuf qsQb, qsInfo, qsKey, qsCand, qsNc, qsEps, qsFlags, qsList, qsScratch;
     DBuf rpBlk, rpLb, rpQ, rpE, rpVm, rpOff, rpTot, rpCtr;  // pooled replay (k_rp_*)
     DBuf bmCnt, bmOff, bmPairs, bmE;                          // block-major exact (k_inv_*, k_exact_bm)
+    DBuf fMask;                                               // block-major int8 row filter: survivor masks [cn][L]
+    DBuf bmPart;                                              // chunk sums of the inversion's prefix scan
+    int q8_bm = 1;                                            // option q8_bm: the int8 row filter block-major (1) or per query (0)
     void* bmCnt_zp = nullptr;                                 // bmCnt.p / .bytes when it is known all-zero
     size_t bmCnt_zb = 0;                                      // (a grown buffer may come back at the same address)
     // hipGraph replay of a repeated identical wv_index_search_device call
@@ -293,7 +296,9 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
 void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
                       const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
                       int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
-                      const float* capv, const float4* qinfo, const Q8Filter* q8f);
+                      const float* capv, const float4* qinfo, const Q8Filter* q8f, const uint32_t* fmask = nullptr);
+void launch_q8_filt_bm(wv_index* idx, hipStream_t s, int metric, const Q8Filter& f, const uint32_t* valid, int64_t nb,
+                       int L, const float* capv, const float4* qinfo, uint32_t* fmask);
 void launch_exact_bm(wv_index* idx, hipStream_t s, int metric, bool v5, const float* Qn, int64_t nb, size_t bm_lds,
                      int64_t ldE);
 // qs_replay.hip
