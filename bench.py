@@ -440,7 +440,8 @@ def main():
     n_local = (n_total + world - 1) // world
     id0 = rank * n_local
     n_local = max(0, min(n_local, n_total - id0))
-    B = args.batch if args.batch is not None else (256 if pq else flat["batch"] if flat else 2048)
+    # pq: 2048 queries per step (the int8 key pass is MFMA-bound from ~1k queries; 256 keeps it HBM-bound)
+    B = args.batch if args.batch is not None else (2048 if pq else flat["batch"] if flat else 2048)
     # GIST-shaped U[0,1) for PQ, SIFT-shaped integers for c2, U[-1,1) otherwise
     gen_kind = 2 if pq else flat["kind"] if flat else 0
     metric_name = "l2-squared" if pq else flat["metric"] if flat else "cosine"
@@ -592,7 +593,8 @@ def main():
     # the sharded PQ search (ShardedQuantSearch) computes full ADC rows with k_pq_adc2
     pq_opt = [o.replace(" ", "") for o in args.option if o.replace(" ", "").startswith("pq_adc3=")]
     pq_sel = pq_opt[-1].split("=")[1] if pq_opt else PQ_ADC_DEFAULT
-    pq_kernel = ("k_pq_adc2" if shard or pq_sel == "0" else "k_pq_adc4" if pq_sel == "2" else "k_pq_adc3") if pq \
+    pq_kernel = ("k_q8_blockkey_pq" if route == 8 else
+                 "k_pq_adc2" if shard or pq_sel == "0" else "k_pq_adc4" if pq_sel == "2" else "k_pq_adc3") if pq \
         else "k_pq_adc2"
     dom_kernel = (pq_kernel if pq else ("k_q8_blockkey_bq" if route == 6 else "k_bq_blockmin_lds") if bq else
                   ("k_rq8_dist" if rq_bits == 8 else "k_rq1_dist") if rq_bits else sel_kernel)
@@ -616,6 +618,30 @@ def main():
                 "note": f"launch_ms = first query group ({f0} queries) of the batch",
                 "hbm_write_GBps": f0 * ld * 4 / (sel_avg * 1e-3) / 1e9 if sel_avg > 0 else 0.0,
                 "traffic": args.traffic_bytes}
+    elif pq and route == 8:
+        # dominant kernel: the block keys on the integer matrix cores over the
+        # centred int8 reconstruction plane (k_q8_blockkey):
+        # one int8 product per (query, row, dim) and the plane (n_local x dpb8
+        # bytes) streamed once per launch; the binding roofline is the larger
+        # fraction (HBM at small batches, MFMA at large)
+        dpb8 = (dims + 127) // 128 * 128 if dims <= 768 else (dims + 255) // 256 * 256
+        f0 = int(index.stats().get("last_group_queries", 0)) or B
+        t = sel_avg * 1e-3
+        ops = 2.0 * f0 * n_local * dims
+        plane = float(n_local) * dpb8
+        mfma_frac = ops / t / 1e12 / MFMA_I8_PEAK_TOPS if t > 0 else 0.0
+        hbm_frac = plane / t / 1e9 / HBM_PEAK_GBPS if t > 0 else 0.0
+        if hbm_frac >= mfma_frac:
+            roof = {"bound": "hbm", "kernel": pq_kernel, "achieved": plane / t / 1e9 if t > 0 else 0.0,
+                    "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": hbm_frac}
+        else:
+            roof = {"bound": "mfma", "kernel": pq_kernel, "achieved": ops / t / 1e12 if t > 0 else 0.0,
+                    "peak": MFMA_I8_PEAK_TOPS, "unit": "TOPS (int8 MFMA)", "frac": mfma_frac}
+        roof.update({"launch_ms": sel_avg, "mfma_frac": mfma_frac, "hbm_frac": hbm_frac,
+                     "algorithmic": f"2 x {f0} x {n_local} x {dims} int8 ops; {n_local} x {dpb8} plane bytes",
+                     "mfma": "v_mfma_i32_16x16x64_i8 over the centred reconstruction x~ - mu (l2 keys; exact ADC "
+                             "of the candidate rows from the LUT, reference segment order)",
+                     "traffic": args.traffic_bytes})
     elif pq:
         # dominant kernel k_pq_adc4 (k_pq_adc3 / k_pq_adc2 with --option
         # pq_adc3=1 / 0): one LUT lookup (LDS read) + fp32 add per (query, row,

@@ -500,6 +500,7 @@ typedef struct wv_stats {
 #define WV_ROUTE_GEMV 5      /* k_gemv_select (HBM-streaming GEMV, small batches) */
 #define WV_ROUTE_BQ_INT8 6   /* BQ block minima: k_q8_blockkey over +-1 code planes (integer MFMA) */
 #define WV_ROUTE_BQ_VALU 7   /* BQ block minima: k_bq_blockmin_lds / k_bq_blockmin (xor + popcount) */
+#define WV_ROUTE_PQ_INT8 8   /* PQ: k_q8_blockkey over the centred int8 reconstruction plane (l2-squared) */
 int wv_index_stats(wv_index *idx, wv_stats *out);
 
 /* Diagnostic hook (tests): the last MFMA batch's candidates [nq][KP]:

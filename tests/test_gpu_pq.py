@@ -175,3 +175,62 @@ def test_pq_adc3_matches_adc2_and_oracle(wv, oracle, metric, kind, rescore, k, r
         np.testing.assert_array_equal(ids[qi, :counts[qi]], oi, err_msg=f"q{qi}")
         np.testing.assert_array_equal(dists[qi, :counts[qi]].view(np.uint32), od.view(np.uint32), err_msg=f"q{qi}")
     idx.close()
+
+
+# PQ block keys on the integer matrix cores (option pq8, l2-squared, 384 < d <= 1536):
+# keys over the centred int8 reconstruction plane, candidate 32-row blocks, exact ADC of
+# their rows (k_pq_cand8); must equal the LUT-minima route (pq8 = 0) and the oracle bit
+# for bit -- with deleted rows, an allow list, integer data (ADC ties -> flagged ->
+# replay), rows added after the fit (a dirty block range rebuilt at the next search) and
+# a capacity growth (the plane reallocated)
+@pytest.mark.parametrize("kind,n,d,m,ks,rescore,k,rl,allow", [
+    (2, 9000, 960, 240, 256, False, 10, -1, False),   # the C5 shape (GIST-like U[0,1))
+    (2, 6000, 400, 100, 64, True, 10, 100, True),     # rescoring: worker heap 100
+    (1, 5000, 768, 192, 32, False, 20, -1, False),    # integer data: ADC ties
+    (0, 7000, 1024, 128, 256, False, 5, -1, True),    # ds = 8
+])
+def test_pq8_keys_match_lut_route_and_oracle(wv, oracle, kind, n, d, m, ks, rescore, k, rl, allow):
+    data = gen(oracle, kind, 181, n, d)
+    idx = wv.FlatIndex(distance="l2-squared", variant="avx256", rescore_limit=rl,
+                       pq={"segments": m, "centroids": ks, "rescore": rescore})
+    idx.add_batch(np.arange(n - 500, dtype=np.uint64), data[: n - 500])
+    idx.pq_fit(seed=19)
+    gone = list(range(3, n - 500, 89))
+    idx.delete(*gone)
+    queries = gen(oracle, kind, 182, 70, d)
+    idx.search_by_vector_batch(queries[:3], k)  # builds the plane
+    idx.add_batch(np.arange(n - 500, n, dtype=np.uint64), data[n - 500:])  # encoded on Add: dirty blocks
+    idx.add_batch(np.arange(40, 48, dtype=np.uint64), data[n - 8:])  # upserts inside built blocks
+    store = data.copy()
+    store[40:48] = data[n - 8:]
+    present = np.ones(n, np.uint8)
+    present[gone] = 0
+    al = None
+    if allow:
+        keep = [i for i in range(n) if i % 4 != 1]
+        al = wv.AllowList(keep)
+        mask = np.zeros(n, np.uint8)
+        mask[keep] = 1
+        present &= mask
+    res = {}
+    for opt in (1, 0):
+        idx.set_option("pq8", opt)
+        res[opt] = idx.search_by_vector_batch(queries, k, allow=al)
+        if opt == 1:
+            assert idx.stats()["last_route"] == 8  # WV_ROUTE_PQ_INT8
+    for a, b in zip(res[1], res[0]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    centers = idx.pq_centers()
+    codes = idx.pq_codes(n)
+    ids, dists, counts = res[1]
+    for qi in range(0, len(queries), 6):
+        oi, od = oracle.pq_flat_search(oracle.L2, 1, centers, codes, store, present, queries[qi], k, max(rl, k),
+                                       rescore)
+        np.testing.assert_array_equal(ids[qi, :counts[qi]], oi, err_msg=f"q{qi}")
+        np.testing.assert_array_equal(dists[qi, :counts[qi]].view(np.uint32), od.view(np.uint32), err_msg=f"q{qi}")
+    # growth: the plane follows the index capacity
+    idx.set_option("pq8", 1)
+    idx.reserve(4 * n)
+    for a, b in zip(idx.search_by_vector_batch(queries, k, allow=al), res[0]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    idx.close()

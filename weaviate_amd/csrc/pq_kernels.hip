@@ -1030,5 +1030,164 @@ __global__ __launch_bounds__(512, 1) void k_pq_adc4(const uint32_t* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// PQ block keys on the integer matrix cores.  For l2-squared
+// the ADC sum is ||q - x~||^2 up to fp32 rounding (LUT entries and their sum
+// are sums of non-negative terms: relative error <= gamma_{m + ds + 3}), x~ =
+// the row's decoded centroids.  The distance is translation invariant, so the
+// reconstruction is stored centred, x_c = fl(x~ - mu) with mu the per-dimension
+// mean of the codebook, as an int8 plane (k_block_q8: per-32-row-block
+// scales, residual maxima); the queries are centred the same way.  Centred
+// vectors are 2x shorter on U[0,1) data, which is what makes the int8 key's
+// Cauchy-Schwarz bound (|q^| R + |q - q^| H ..., qs_eps) narrow enough to cut
+// 10M rows to ~100 candidate blocks per query.
+// ---------------------------------------------------------------------------
+
+// rows [row0, row0 + n) decoded and centred into out[(r - row0) * dpad + c]
+// (fp32, zero padded), n2[r] = sum of squares (fp32), maxima[4] = max n2
+// (float bits); one wave per row
+__global__ __launch_bounds__(256) void k_pq_decode_center(const uint32_t* __restrict__ codes, int g16, int m, int ds,
+                                                          int K, const float* __restrict__ centers,
+                                                          const float* __restrict__ mu, int64_t row0, int64_t n,
+                                                          int dims, int dpad, float* __restrict__ out,
+                                                          float* __restrict__ n2, uint32_t* __restrict__ maxima) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const int64_t r = row0 + i;
+    const unsigned char* cb = reinterpret_cast<const unsigned char*>(codes);
+    float ss = 0.f;
+    for (int c = lane; c < dpad; c += 64) {
+        float v = 0.f;
+        if (c < dims) {
+            const int sg = c / ds, e = c - sg * ds;
+            const int code = cb[pq_code_word(r, sg, g16) * 4 + (sg & 3)];
+            v = centers[((int64_t)sg * K + code) * ds + e] - mu[c];
+        }
+        out[i * dpad + c] = v;
+        ss = fmaf(v, v, ss);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if (lane == 0) {
+        n2[r] = ss;
+        atomicMax(&maxima[4], __float_as_uint(ss));
+    }
+}
+
+// centred queries: Qc[q] = fl(Qn[q] - mu) (zero padding rows q >= nq and
+// columns c >= dims), qinfo[q] = (|q_c|^2, 0, 0, non-finite); wave per query
+__global__ __launch_bounds__(256) void k_pq_center_queries(const float* __restrict__ Qn, int dpad, int dims,
+                                                           const float* __restrict__ mu, int64_t nq, int64_t nq_pad,
+                                                           float* __restrict__ Qc, float4* __restrict__ qinfo) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq_pad) return;
+    float ss = 0.f;
+    bool bad = false;
+    for (int c = lane; c < dpad; c += 64) {
+        const float v = (q < nq && c < dims) ? Qn[q * dpad + c] - mu[c] : 0.f;
+        Qc[q * dpad + c] = v;
+        ss = fmaf(v, v, ss);
+        bad |= !__builtin_isfinite(v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    bad = __any(bad);
+    if (lane == 0) qinfo[q] = make_float4(ss, 0.f, 0.f, (bad || !(ss < 1e30f)) ? 1.f : 0.f);
+}
+
+// the exact ADC distance (the reference's segment-order fp32 sum) of every
+// valid row of query q's candidate 32-row blocks (k_blk_select(_f) lists:
+// cand[q][L], ncand[q]), the rows below cap[q] kept and sorted by (distance,
+// slot).  The R + 1 smallest distances are among them (the select's proof
+// with eps >= |A - ADC|); strictly increasing -> they are the worker heap's
+// content and its ascending extraction; else, or a list overflow (sel_flags),
+// more than PQC_CAP rows below the cap or a NaN, flag_out[q] = 1 (the full
+// replay resolves q).  Workgroup per query, 8 blocks x 32 rows per pass.
+template <int KC>
+__global__ __launch_bounds__(256) void k_pq_cand8(const uint32_t* __restrict__ codes, int g16, int m, int kk,
+                                                  const uint32_t* __restrict__ valid, int64_t nslots,
+                                                  const float* __restrict__ lut, const uint32_t* __restrict__ cand,
+                                                  int L, const int32_t* __restrict__ ncand,
+                                                  const int32_t* __restrict__ sel_flags, const float* __restrict__ cap,
+                                                  int R, int metric, uint64_t id_base, uint64_t* __restrict__ asc_ids,
+                                                  float* __restrict__ asc_d, int32_t* __restrict__ asc_n,
+                                                  int32_t* __restrict__ flag_out) {
+    __shared__ float sv[PQC_CAP];
+    __shared__ uint32_t ss[PQC_CAP];
+    __shared__ int s_cnt, s_bad;
+    const int k = KC > 0 ? KC : kk;
+    const int q = blockIdx.x;
+    const int t = threadIdx.x;
+    if (sel_flags[q] != 0) {
+        if (t == 0) flag_out[q] = 1;
+        return;
+    }
+    if (t == 0) { s_cnt = 0; s_bad = 0; }
+    __syncthreads();
+    const int nc = ncand[q];
+    const float capq = cap[q];
+    const float* Lq = lut + (int64_t)q * m * k;
+    const unsigned char* cb = reinterpret_cast<const unsigned char*>(codes);
+    for (int j0 = 0; j0 < nc; j0 += 8) {
+        const int j = j0 + (t >> 5);
+        if (j >= nc) break;
+        const int64_t row = (int64_t)cand[(int64_t)q * L + j] * 32 + (t & 31);
+        if (row >= nslots || !((valid[row >> 5] >> (row & 31)) & 1u)) continue;
+        float sum = 0.f;
+        for (int g = 0; g < g16; g++) {
+            const uint4 cw = *reinterpret_cast<const uint4*>(cb + ((((row >> 8) * g16 + g) << 8) + (row & 255)) * 16);
+            const uint32_t w4[4] = {cw.x, cw.y, cw.z, cw.w};
+            const int nv = m - 16 * g < 16 ? m - 16 * g : 16;
+            float lv[16];
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++)
+                lv[jj] = jj < nv ? Lq[(int64_t)(16 * g + jj) * k + ((w4[jj >> 2] >> (8 * (jj & 3))) & 0xFFu)] : 0.f;
+            for (int jj = 0; jj < nv; jj++) sum = sum + lv[jj];
+        }
+        const float e = pq_wrap(metric, sum);
+        if (e != e) s_bad = 1;
+        if (e < capq) {
+            const int pos = atomicAdd(&s_cnt, 1);
+            if (pos < PQC_CAP) { sv[pos] = e; ss[pos] = (uint32_t)row; }
+        }
+    }
+    __syncthreads();
+    const int n = s_cnt;
+    if (n > PQC_CAP || s_bad) {
+        if (t == 0) flag_out[q] = 1;
+        return;
+    }
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    for (int i = n + t; i < p2; i += 256) { sv[i] = __builtin_inff(); ss[i] = NO_ID; }
+    __syncthreads();
+    for (int k2 = 2; k2 <= p2; k2 <<= 1)
+        for (int jj = k2 >> 1; jj > 0; jj >>= 1) {
+            for (int i = t; i < p2; i += 256) {
+                const int ixj = i ^ jj;
+                if (ixj > i) {
+                    const float a = sv[i], c = sv[ixj];
+                    const uint32_t ia = ss[i], ic = ss[ixj];
+                    const bool gt = a > c || (a == c && ia > ic);
+                    if ((i & k2) == 0 ? gt : !gt) { sv[i] = c; sv[ixj] = a; ss[i] = ic; ss[ixj] = ia; }
+                }
+            }
+            __syncthreads();
+        }
+    const int mm = n < R + 1 ? n : R + 1;
+    if (t == 0) {
+        bool strict = true;
+        for (int i = 1; i < mm; i++) strict &= sv[i - 1] < sv[i];
+        flag_out[q] = strict ? 0 : 1;
+        asc_n[q] = n < R ? n : R;
+    }
+    for (int i = t; i < R && i < n; i += 256) {
+        asc_ids[(int64_t)q * R + i] = id_base + ss[i];
+        asc_d[(int64_t)q * R + i] = sv[i];
+    }
+}
+
 }  // namespace
 }  // namespace wv

@@ -221,6 +221,8 @@ __global__ void k_query_q8(const float* __restrict__ Qn, int dpad, int dims, int
     }
 }
 
+}  // namespace
+// external linkage: the key-pass launcher (qs_runtime.hip) serves other units
 struct Q8Args {
     const unsigned char* X8;   // corpus int8 plane, tiled (q8_plane_byte, dpb8 columns)
     const float* sb;           // [cap/32] block scales
@@ -236,6 +238,7 @@ struct Q8Args {
     int nqg;                   // query groups of 256
     int bq_bits;               // BQ: code bits 64 * words (hamming = (bq_bits - dot) / 2)
 };
+namespace {
 
 // ---------------------------------------------------------------------------
 // k_q8_blockkey<NC, RB, L2>: block keys of 256 queries (8 waves x 32) x one

@@ -7,6 +7,50 @@
 // 64 R): k + 1 <= 960 stays on the block-key path
 int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : k + 1 <= 960 ? 16 : 0; }
 
+// the int8 block-key pass (k_q8_blockkey, 512 <= dpb8 <= 1536) over a.nslots
+// ring slots for a.nqg 256-query groups, spans chosen as search_qs does
+// (XCD-aware groups, 4 GiB span planes, whole rounds of workgroups)
+int launch_q8_keys(wv_index* idx, hipStream_t s, Q8Args a, int dpb8, bool l2) {
+    const int NC8 = dpb8 / 64;
+    const int RB = dpb8 <= 768 ? 2 : 1;
+    int64_t nspans = 256 / std::gcd(256, a.nqg);
+    while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
+    if (idx->spans_opt > 0) nspans = idx->spans_opt;
+    const int64_t max_sps = ((1ll << 32) - 2 * 256ll * dpb8) / ((int64_t)RB * 32 * dpb8);
+    nspans = std::max<int64_t>(nspans, (a.nslots + max_sps - 1) / max_sps);
+    if (idx->spans_opt <= 0) {
+        const int64_t unit = 256 / std::gcd(256, a.nqg);
+        nspans = (nspans + unit - 1) / unit * unit;
+    }
+    nspans = std::max<int64_t>(1, std::min<int64_t>(nspans, a.nslots));
+    const int64_t sps = (a.nslots + nspans - 1) / nspans;
+    a.slots_per_span = (int)sps;
+    a.nspans = (int)((a.nslots + sps - 1) / sps);
+    const size_t lds = (size_t)3 * RB * 2 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
+    dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
+#define WV_Q8K(NCV, RBV, L2V)                                                                                  \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, RBV, L2V, false, false, 1>,                 \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                     \
+        k_q8_blockkey<NCV, RBV, L2V, false, false, 1><<<grid, 512, lds, s>>>(a);                                \
+    } while (0)
+#define WV_Q8KN(L2V)                                   \
+    switch (NC8) {                                     \
+    case 8: WV_Q8K(8, 2, L2V); break;                  \
+    case 10: WV_Q8K(10, 2, L2V); break;                \
+    case 12: WV_Q8K(12, 2, L2V); break;                \
+    case 16: WV_Q8K(16, 1, L2V); break;                \
+    case 20: WV_Q8K(20, 1, L2V); break;                \
+    case 24: WV_Q8K(24, 1, L2V); break;                \
+    default: return set_err(WV_ERR_UNSUPPORTED, "int8 keys: plane width %d", dpb8); \
+    }
+    if (l2) { WV_Q8KN(true); } else { WV_Q8KN(false); }
+#undef WV_Q8KN
+#undef WV_Q8K
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
 // phase 0: the whole search.  Sharded two-phase form (mode 1, one query chunk):
 // phase 1 = block keys + local candidate selection, topA [nq][k+1] = this
 // shard's k+1 smallest block-key A values (eps in idx->qsEps); phase 2 = the

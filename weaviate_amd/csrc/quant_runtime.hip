@@ -524,6 +524,8 @@ static int pq_alloc(wv_index* idx) {
 }
 
 static int pq_encode_all(wv_index* idx) {
+    idx->pq8_mu_dirty = 1;  // a new codebook: mu and every block of the reconstruction plane
+    pq8_mark(idx, 0, idx->hiwater);
     launch_pq_encode(idx, idx->hiwater, nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(idx->stream));
@@ -896,6 +898,173 @@ static int hnsw_prep(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
     return WV_OK;
 }
 
+// ---- PQ block keys on the integer matrix cores (pq_kernels.hip §3.6b) ----
+static int pq8_dpb8(int d) { return d <= 768 ? (int)round_up(d, 128) : (int)round_up(d, 256); }
+
+// l2-squared, 384 < d <= 1536 (the int8 key kernels' plane widths), a worker
+// heap the 448-block candidate lists hold, key rows within 16 GiB
+static bool pq8_route(const wv_index* idx, int R, int64_t nq) {
+    if (!idx->pq8_opt || idx->compression != WV_COMPRESSION_PQ || !idx->pq_trained || idx->pq8_bad ||
+        idx->metric != WV_METRIC_L2_SQUARED || idx->dims <= 384 || idx->dims > 1536 || R + 1 > 448 ||
+        idx->hiwater <= 0)
+        return false;
+    const int dpb8 = pq8_dpb8(idx->dims);
+    const int RB = dpb8 <= 768 ? 2 : 1;
+    const int64_t nb = (idx->hiwater + 32 * RB - 1) / (32 * RB) * RB;
+    return round_up(nq, QS_QPB) * nb * 4 <= (16ll << 30);
+}
+
+// the centred reconstruction plane up to date: (re)allocated with the index's
+// capacity, mu from the codebook, the dirty slot range re-decoded and
+// re-quantised in chunks of 2^18 rows
+static int pq8_sync(wv_index* idx, hipStream_t s) {
+    const int dims = idx->dims, dpad = idx->dpad, dpb8 = pq8_dpb8(dims);
+    bool full = false;
+    if (idx->pq8_cap != idx->cap || idx->pq8_dpb8 != dpb8 || !idx->pq8_X8) {
+        if (idx->pq8_X8) hipFree(idx->pq8_X8);
+        if (idx->pq8_sb) hipFree(idx->pq8_sb);
+        if (idx->pq8_n2) hipFree(idx->pq8_n2);
+        idx->pq8_X8 = nullptr; idx->pq8_sb = nullptr; idx->pq8_n2 = nullptr;
+        idx->pq8_cap = 0;
+        HIPCHK(hipMalloc(&idx->pq8_X8, (size_t)idx->cap * dpb8));
+        HIPCHK(hipMalloc(&idx->pq8_sb, (size_t)(idx->cap / 32) * sizeof(float)));
+        HIPCHK(hipMalloc(&idx->pq8_n2, (size_t)idx->cap * sizeof(float)));
+        HIPCHK(hipMemsetAsync(idx->pq8_X8, 0, (size_t)idx->cap * dpb8, s));
+        HIPCHK(hipMemsetAsync(idx->pq8_sb, 0, (size_t)(idx->cap / 32) * sizeof(float), s));
+        HIPCHK(hipMemsetAsync(idx->pq8_n2, 0, (size_t)idx->cap * sizeof(float), s));
+        idx->pq8_cap = idx->cap;
+        idx->pq8_dpb8 = dpb8;
+        full = true;
+    }
+    if (idx->pq8_mu_dirty) {  // mu = the per-dimension mean of the codebook
+        const int m = idx->pq_m, K = idx->pq_ks, ds = idx->pq_ds;
+        std::vector<float> cen((size_t)m * K * ds);
+        HIPCHK(hipMemcpy(cen.data(), idx->pq_centers, cen.size() * sizeof(float), hipMemcpyDeviceToHost));
+        std::vector<float> mu((size_t)dpad, 0.f);
+        for (int sg = 0; sg < m; sg++)
+            for (int e = 0; e < ds; e++) {
+                double acc = 0.0;
+                for (int c = 0; c < K; c++) acc += cen[((size_t)sg * K + c) * ds + e];
+                mu[(size_t)sg * ds + e] = (float)(acc / K);
+            }
+        HIPCHK(idx->pq8Mu.ensure((size_t)dpad * sizeof(float)));
+        HIPCHK(hipMemcpy(idx->pq8Mu.p, mu.data(), (size_t)dpad * sizeof(float), hipMemcpyHostToDevice));
+        idx->pq8_mu_dirty = 0;
+        full = true;
+    }
+    HIPCHK(idx->pq8Max.ensure(8 * sizeof(uint32_t)));
+    int64_t lo = idx->pq8_lo, hi = idx->pq8_hi;
+    if (full) {
+        HIPCHK(hipMemsetAsync(idx->pq8Max.p, 0, 8 * sizeof(uint32_t), s));
+        lo = 0;
+        hi = idx->hiwater;
+    }
+    hi = std::min<int64_t>(hi, idx->hiwater);
+    idx->pq8_lo = idx->pq8_hi = 0;
+    if (hi <= lo) return WV_OK;
+    const int64_t r0 = lo / 32 * 32, r1 = std::min<int64_t>(round_up(hi, 32), idx->cap);
+    const int64_t chunk = 1 << 18;
+    HIPCHK(idx->pq8Tmp.ensure((size_t)std::min<int64_t>(chunk, r1 - r0) * dpad * sizeof(float)));
+    float* tmp = idx->pq8Tmp.as<float>();
+    uint32_t* mx = idx->pq8Max.as<uint32_t>();
+    for (int64_t a = r0; a < r1; a += chunk) {
+        const int64_t n = std::min<int64_t>(chunk, r1 - a);
+        k_pq_decode_center<<<(unsigned)((n + 3) / 4), 256, 0, s>>>(idx->pq_codes, pq_g16(idx->pq_m), idx->pq_m,
+                                                                    idx->pq_ds, idx->pq_ks, idx->pq_centers,
+                                                                    idx->pq8Mu.as<float>(), a, n, dims, dpad, tmp,
+                                                                    idx->pq8_n2, mx);
+        // k_block_q8 addresses rows absolutely: shift the chunk buffer by its first row
+        k_block_q8<<<(unsigned)(n / 32), 256, 0, s>>>(tmp - a * dpad, dpad, dims, dpb8, nullptr, a / 32, idx->pq8_X8,
+                                                       idx->pq8_sb, mx);
+        HIPCHK(hipGetLastError());
+    }
+    uint32_t bad = 0;
+    HIPCHK(hipMemcpyAsync(&bad, mx + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    idx->pq8_bad = bad ? 1 : 0;  // a non-finite centroid: the LUT minima route from now on
+    return WV_OK;
+}
+
+// keys on the centred int8 planes -> candidate 32-row blocks (eps covers the
+// key's quantisation, the ADC's fp32 rounding and the centring) -> exact ADC
+// of their rows below the cap -> asc (ascI / ascD / ascN) or a flag in oF
+static int pq8_candidates(wv_index* idx, hipStream_t s, int64_t nq, int R, const uint32_t* valid) {
+    int rc = pq8_sync(idx, s);
+    if (rc) return rc;
+    if (idx->pq8_bad) return set_err(WV_ERR_UNSUPPORTED, "pq8: non-finite codebook");
+    const int dims = idx->dims, dpad = idx->dpad, dpb8 = idx->pq8_dpb8;
+    const int m = idx->pq_m, K = idx->pq_ks;
+    const int64_t nq_pad = round_up(nq, QS_QPB);
+    const int RB = dpb8 <= 768 ? 2 : 1;
+    const int64_t nslots = (idx->hiwater + 32 * RB - 1) / (32 * RB);
+    const int64_t nb = nslots * RB;
+    constexpr int RV = 8, L = 64 * (RV - 1);
+    HIPCHK(idx->pq8Qc.ensure((size_t)nq_pad * dpad * sizeof(float)));
+    HIPCHK(idx->qsInfo.ensure((size_t)nq_pad * sizeof(float4)));
+    HIPCHK(idx->q8Qb.ensure((size_t)nq_pad * dpb8));
+    HIPCHK(idx->q8Scale.ensure((size_t)nq_pad * sizeof(float)));
+    HIPCHK(idx->q8Info.ensure((size_t)nq_pad * sizeof(float4)));
+    HIPCHK(idx->qsKey.ensure((size_t)nq_pad * nb * sizeof(float)));
+    HIPCHK(idx->qsCand.ensure((size_t)nq * L * sizeof(uint32_t)));
+    HIPCHK(idx->qsNc.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->qsEps.ensure((size_t)nq * sizeof(float)));
+    HIPCHK(idx->qsCap.ensure((size_t)nq * sizeof(float)));
+    HIPCHK(idx->qsFlags.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->oF.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->qsList.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->flCtr.ensure(2 * sizeof(uint32_t)));
+    float4* qinfo = idx->qsInfo.as<float4>();
+    k_pq_center_queries<<<(unsigned)(nq_pad / 4), 256, 0, s>>>(idx->qn.as<float>(), dpad, dims, idx->pq8Mu.as<float>(),
+                                                               nq, nq_pad, idx->pq8Qc.as<float>(), qinfo);
+    k_query_q8<<<(unsigned)(nq_pad / 4), 256, 0, s>>>(idx->pq8Qc.as<float>(), dpad, dims, dpb8, nq, nq_pad, qinfo,
+                                                      idx->q8Qb.as<unsigned char>(), idx->q8Scale.as<float>(),
+                                                      idx->q8Info.as<float4>());
+    HIPCHK(hipGetLastError());
+    Q8Args a{};
+    a.X8 = idx->pq8_X8;
+    a.sb = idx->pq8_sb;
+    a.xnorm2 = idx->pq8_n2;
+    a.valid = valid;
+    a.Q8 = idx->q8Qb.as<unsigned char>();
+    a.qscale = idx->q8Scale.as<float>();
+    a.key = idx->qsKey.as<float>();
+    a.ldk = nb;
+    a.nslots = nslots;
+    a.nqg = (int)(nq_pad / QS_QPB);
+    if (idx->timing) HIPCHK(hipEventRecord(idx->ev0, s));
+    rc = launch_q8_keys(idx, s, a, dpb8, true);
+    if (rc) return rc;
+    if (idx->timing) HIPCHK(hipEventRecord(idx->ev1, s));
+    idx->stats.last_group_queries = (uint64_t)nq;
+    idx->stats.last_route = WV_ROUTE_PQ_INT8;
+    idx->stats.mfma_launches++;
+    // |A - ADC| <= eps: qs_eps's l2 form with g_d covering the plane norms'
+    // fp32 sums (dpb8 terms), the ADC's (m LUT sums of ds terms, all
+    // non-negative: relative error gamma_{m + ds + 3} <= (|q_c| + N)^2 terms)
+    // and 2u for the centring's two roundings
+    const uint32_t* mx = idx->pq8Max.as<uint32_t>();
+    const float gd = (float)(gamma_n(std::max(dpb8, m + idx->pq_ds) + 8) + 2.0 * 5.9604644775390625e-08);
+    const float gacc8 = 4.0001f * 5.9604645e-08f;
+    const int RT = qs_R(R);
+    const unsigned gw = (unsigned)((nq + 3) / 4);
+#define WV_PQSEL(RTV) k_blk_select_f<RV, RTV><<<gw, 256, 0, s>>>(a.key, nb, nb, (int)nq, R, L2, idx->q8Info.as<float4>(), mx, mx + 4, gd, gacc8, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), idx->qsEps.as<float>(), nullptr, nullptr, nullptr, idx->qsCap.as<float>(), nullptr)
+    if (RT == 2) WV_PQSEL(2);
+    else if (RT == 4) WV_PQSEL(4);
+    else
+        k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, nb, nb, (int)nq, R, L2, idx->q8Info.as<float4>(), mx, mx + 4, gd,
+                                            gacc8, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(),
+                                            idx->qsFlags.as<int32_t>(), idx->qsEps.as<float>(), nullptr, nullptr,
+                                            nullptr, idx->qsCap.as<float>(), nullptr);
+#undef WV_PQSEL
+    HIPCHK(hipGetLastError());
+#define WV_PQC8(KCV) k_pq_cand8<KCV><<<(unsigned)nq, 256, 0, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, idx->hiwater, idx->lut.as<float>(), idx->qsCand.as<uint32_t>(), L, idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), idx->qsCap.as<float>(), R, L2, idx->id_base, idx->ascI.as<uint64_t>(), idx->ascD.as<float>(), idx->ascN.as<int32_t>(), idx->oF.as<int32_t>())
+    if (K == 256) WV_PQC8(256);
+    else WV_PQC8(0);
+#undef WV_PQC8
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
 static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k, int limit,
                        int trim, int rescore, const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
     int comp = 0;
@@ -914,7 +1083,12 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     // the PQ candidate path flags), and whether its outputs go by query
     int64_t nrep = nq;
     int rep_by_query = 0;
-    if (comp == WV_COMPRESSION_PQ && idx->pq_cand && R + 1 <= 64) {
+    const bool pq8 = comp == WV_COMPRESSION_PQ && pq8_route(idx, R, nq);
+    if (pq8 || (comp == WV_COMPRESSION_PQ && idx->pq_cand && R + 1 <= 64)) {
+      if (pq8) {
+        rc = pq8_candidates(idx, s, nq, R, valid);
+        if (rc) return rc;
+      } else {
         // minima-only PQ search: block minima of every query (no B x N matrix),
         // candidate blocks, exact ADC of their rows, strict order -> asc
         const int m = idx->pq_m, K = idx->pq_ks;
@@ -981,12 +1155,14 @@ static int search_hnsw(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
             idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), idx->qsEps.as<float>(),
             nullptr, nullptr, nullptr, nullptr);
         HIPCHK(hipGetLastError());
-        int32_t* pflag = idx->oF.as<int32_t>();
+        int32_t* const pflag = idx->oF.as<int32_t>();
 #define WV_PQC(KCV) k_pq_cand<KCV><<<(unsigned)nq, 256, 0, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, nslots, idx->lut.as<float>(), idx->rB.as<float>(), nblk, idx->qsCand.as<uint32_t>(), 64, idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), R, wrapm, idx->id_base, idx->ascI.as<uint64_t>(), idx->ascD.as<float>(), idx->ascN.as<int32_t>(), pflag)
         if (K == 256) WV_PQC(256);
         else WV_PQC(0);
 #undef WV_PQC
         HIPCHK(hipGetLastError());
+      }
+        int32_t* pflag = idx->oF.as<int32_t>();
         HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
         k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(pflag, (int)nq, idx->qsList.as<int32_t>(),
                                                                   idx->flCtr.as<uint32_t>(), 0);

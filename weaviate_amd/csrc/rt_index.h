@@ -238,6 +238,18 @@ struct wv_index {
     int pq_cand = 1;                                          // PQ search: block minima + candidate blocks (k_pq_cand)
     int pq_adc3 = 2;                                          // minima: 2 k_pq_adc4 (16-byte LUT reads), 1 k_pq_adc3, 0 k_pq_adc2
     DBuf lutg;                                                // the LUT regrouped for k_pq_adc3 [64-query group][s][c][64]
+    // PQ block keys on the integer matrix cores (l2-squared, 384 < d <= 1536):
+    // the centred reconstruction x_c = x~ - mu as an int8 plane (k_block_q8
+    // layout and scales), its fp32 |x_c|^2 and maxima ([0] R^2, [1] H^2, [2]
+    // non-finite, [4] max |x_c|^2, float bits); rebuilt lazily over the dirty
+    // slot range [pq8_lo, pq8_hi) written since the last search
+    int pq8_opt = 1;                                          // option pq8
+    int64_t pq8_cap = 0, pq8_lo = 0, pq8_hi = 0;
+    int pq8_dpb8 = 0, pq8_mu_dirty = 1, pq8_bad = 0;
+    unsigned char* pq8_X8 = nullptr;
+    float* pq8_sb = nullptr;
+    float* pq8_n2 = nullptr;
+    DBuf pq8Max, pq8Mu, pq8Tmp, pq8Qc;
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
     DBuf flCtr;                      // device flag-list counters (replay_flags)
     int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
@@ -257,6 +269,14 @@ struct wv_index {
 // Add, a Delete or another batch's query preparation ends them.
 // the corpus, its buffers or the options changed: captured search graphs are stale
 static inline void note_mutation(wv_index* idx) { idx->mut_gen++; }
+// PQ codes of slots [lo, hi) were (re)written: the int8 reconstruction plane
+// of their blocks is stale
+static inline void pq8_mark(wv_index* idx, int64_t lo, int64_t hi) {
+    if (hi <= lo) return;
+    if (idx->pq8_hi <= idx->pq8_lo) { idx->pq8_lo = lo; idx->pq8_hi = hi; return; }
+    idx->pq8_lo = std::min(idx->pq8_lo, lo);
+    idx->pq8_hi = std::max(idx->pq8_hi, hi);
+}
 static void invalidate_batch(wv_index* idx) {
     idx->qs_keys_nq = 0;
     idx->qs_phase_nq = 0;
@@ -292,6 +312,7 @@ int qs_R(int k);
 int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid, uint64_t* o_ids,
               float* o_d, int32_t* o_n, int32_t* o_flags, int phase = 0, float* topA = nullptr,
               const float* gA = nullptr, const float* gE = nullptr, int W = 0);
+int launch_q8_keys(wv_index* idx, hipStream_t s, Q8Args a, int dpb8, bool l2);
 // qs_exact.hip
 void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
                       const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,

@@ -171,6 +171,9 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->sq_meta) hipFree(idx->sq_meta);
     idx->sqq.release();
     idx->sqm.release();
+    if (idx->pq8_X8) hipFree(idx->pq8_X8);
+    if (idx->pq8_sb) hipFree(idx->pq8_sb);
+    if (idx->pq8_n2) hipFree(idx->pq8_n2);
     if (idx->X) hipFree(idx->X);
     if (idx->xnorm2) hipFree(idx->xnorm2);
     if (idx->present) hipFree(idx->present);
@@ -347,6 +350,11 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     swap_in(idx->sq_meta, sqmt);
     idx->cap = nc;
     idx->h_present.resize((size_t)nc, 0);
+    if (idx->pq8_X8) {  // the PQ reconstruction plane is reallocated and rebuilt at the next search
+        hipFree(idx->pq8_X8); hipFree(idx->pq8_sb); hipFree(idx->pq8_n2);
+        idx->pq8_X8 = nullptr; idx->pq8_sb = nullptr; idx->pq8_n2 = nullptr;
+        idx->pq8_cap = 0;
+    }
     return WV_OK;
 }
 
@@ -454,6 +462,10 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
 // (host slot list): each block is re-quantised whole (its scale is the
 // block's max |x|), after the rows themselves were stored
 static int requant_blocks(wv_index* idx, const uint32_t* h_slots, int64_t n) {
+    if (idx->compression == WV_COMPRESSION_PQ && idx->pq_trained && n > 0) {
+        const auto mm = std::minmax_element(h_slots, h_slots + n);
+        pq8_mark(idx, (int64_t)*mm.first, (int64_t)*mm.second + 1);
+    }
     if (!idx->q8_planes || n <= 0) return WV_OK;
     std::vector<uint32_t> blk((size_t)n);
     for (int64_t i = 0; i < n; i++) blk[(size_t)i] = h_slots[i] >> 5;
@@ -704,6 +716,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "qs_force_flag") idx->qs_force_flag = value ? 1 : 0;
     else if (k == "exact_bm") idx->exact_bm = value ? 1 : 0;
     else if (k == "q8_bm") idx->q8_bm = value ? 1 : 0;
+    else if (k == "pq8") idx->pq8_opt = value ? 1 : 0;
     else if (k == "exact_cap") idx->exact_cap = value ? 1 : 0;
     else if (k == "exact_filter") idx->exact_filter = value ? 1 : 0;  // 0: every candidate row gets its exact distance
     else if (k == "ef") idx->hnsw_ef = (int)value;  // hnsw UserConfig.EF (-1: dynamic)
