@@ -54,7 +54,8 @@ FLAT = {
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (spec, MI355X_MICROARCH.md)
 MFMA_I8_PEAK_TOPS = 5000.0      # MI355X dense int8 MFMA: 2x bf16 per clock (MI355X_MICROARCH.md, Matrix cores)
 # wv_stats.last_route (include/wv_knn.h WV_ROUTE_*) -> the dominant key kernel
-ROUTE_KERNEL = {1: "k_qs_blockkey", 2: "k_qs_blockkey_w4", 3: "k_q8_blockkey", 4: "k_mfma_select3", 5: "k_gemv_select"}
+ROUTE_KERNEL = {1: "k_qs_blockkey", 2: "k_qs_blockkey_w4", 3: "k_q8_blockkey", 4: "k_mfma_select3", 5: "k_gemv_select",
+                9: "k_q8_gemv"}
 # 32-bit integer VALU lane-ops/s: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  The
 # 32-lane/clk rate (78.6 T) is the f32 FMA rate; v_xor_b32 / v_bcnt_u32_b32 issue
 # at 4 cycles per wave64 (measured: k_bq_blockmin_lds sustains 33.6 T instr-lane-ops/s).
@@ -586,7 +587,7 @@ def main():
     sel_kernel = ROUTE_KERNEL.get(route, "k_qs_blockkey")
     if route == 3 and dims > 1536:  # int8-only planes: the two-column-part form
         sel_kernel = "k_q8_blockkey_cp"
-    int8_keys = sel_kernel.startswith("k_q8_blockkey")
+    int8_keys = sel_kernel.startswith("k_q8_")
     total_avg = float(np.mean(tot_ms)) if tot_ms else 0.0
     # the dominant kernel of each workload: its PMC record (matched on kernel
     # name and configuration) is the only source of `traffic`

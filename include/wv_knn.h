@@ -422,6 +422,16 @@ int wv_merge_shards(int32_t device, int32_t nshards, int64_t nq, int32_t k, cons
  * Exact (uncompressed) search only; allow lists are not taken. */
 #define WV_TRANSPORT_LOCAL 0
 #define WV_TRANSPORT_RCCL 1
+/*   WV_TRANSPORT_HOST   one local shard per process; every collective staged
+ *                       through host memory and handed to the caller's
+ *                       functions (e.g. a gloo / MPI / TCP all-gather): a
+ *                       multi-process world without RCCL, or several processes
+ *                       sharing one GPU in tests.  allgather: send[bytes] from
+ *                       this rank -> recv[world][bytes]; broadcast: root's
+ *                       buf[bytes] -> buf on every rank; both return 0 on success. */
+#define WV_TRANSPORT_HOST 2
+typedef int (*wv_host_allgather_fn)(const void *send, void *recv, int64_t bytes, void *user);
+typedef int (*wv_host_broadcast_fn)(void *buf, int64_t bytes, int32_t root, void *user);
 typedef struct wv_multi wv_multi;
 typedef struct wv_multi_config {
     wv_config index;          /* every shard's config; .device / .id_base are set per shard */
@@ -432,6 +442,9 @@ typedef struct wv_multi_config {
     uint64_t id_stride;       /* doc ids per rank                                        */
     int32_t transport;        /* WV_TRANSPORT_*                                          */
     const void *unique_id;    /* RCCL over processes: rank 0's wv_rccl_unique_id bytes   */
+    wv_host_allgather_fn host_allgather; /* WV_TRANSPORT_HOST                           */
+    wv_host_broadcast_fn host_broadcast;
+    void *host_user;
 } wv_multi_config;
 int wv_rccl_unique_id(void *out, int64_t cap); /* cap >= 128 */
 int wv_multi_create(const wv_multi_config *cfg, wv_multi **out);
@@ -501,6 +514,7 @@ typedef struct wv_stats {
 #define WV_ROUTE_BQ_INT8 6   /* BQ block minima: k_q8_blockkey over +-1 code planes (integer MFMA) */
 #define WV_ROUTE_BQ_VALU 7   /* BQ block minima: k_bq_blockmin_lds / k_bq_blockmin (xor + popcount) */
 #define WV_ROUTE_PQ_INT8 8   /* PQ: k_q8_blockkey over the centred int8 reconstruction plane (l2-squared) */
+#define WV_ROUTE_Q8_GEMV 9   /* k_q8_gemv (int8 block keys of <= 32 queries streamed through registers) */
 int wv_index_stats(wv_index *idx, wv_stats *out);
 
 /* Diagnostic hook (tests): the last MFMA batch's candidates [nq][KP]:

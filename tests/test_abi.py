@@ -65,3 +65,34 @@ def test_validate_user_config_update_host_only(wv):
         v(dict(distance="dot"), dict(distance="dot", rq={"bits": 8}))
     with pytest.raises(wv.WeaviateError, match='rq.bits is immutable: attempted change from "8" to "1"'):
         v(dict(distance="dot", rq={"bits": 8}), dict(distance="dot", rq={"bits": 1}))
+
+
+def test_multi_config_validation_without_gpu():
+    """wv_multi_create refuses inconsistent worlds before touching a device:
+    the host language gets the error text, no GPU needed."""
+    import ctypes as C
+    from weaviate_amd import _lib
+    from weaviate_amd.flat import make_config
+    lib = _lib.load()
+    devs = (C.c_int32 * 2)(0, 0)
+
+    def create(world, rank0, n_local, transport, stride=100, uid=None, cfg=None):
+        mc = _lib.WvMultiConfig(cfg or make_config(distance="cosine", dims=8), world, rank0, n_local,
+                                C.cast(devs, C.POINTER(C.c_int32)), stride, transport, uid, None, None, None)
+        h = C.c_void_p()
+        rc = lib.wv_multi_create(C.byref(mc), C.byref(h))
+        return rc, (lib.wv_last_error() or b"").decode()
+
+    assert create(2, 0, 1, 0) == (_lib.WV_ERR_INVALID, "local transport: every rank must be a local shard")
+    rc, msg = create(2, 1, 1, 1)
+    assert rc == _lib.WV_ERR_INVALID and "unique id" in msg
+    rc, msg = create(2, 0, 1, 2)
+    assert rc == _lib.WV_ERR_INVALID and "callbacks" in msg
+    rc, msg = create(2, 2, 1, 0)
+    assert rc == _lib.WV_ERR_INVALID and "invalid multi config" in msg
+    rc, msg = create(2, 0, 2, 0, stride=0)
+    assert rc == _lib.WV_ERR_INVALID and "id_stride" in msg
+    rc, msg = create(1, 0, 1, 0, cfg=make_config(distance="cosine", dims=8, bq=True))
+    assert rc == _lib.WV_ERR_UNSUPPORTED and "exact" in msg
+    rc, msg = create(1, 0, 1, 7)
+    assert rc == _lib.WV_ERR_INVALID and "unknown transport" in msg

@@ -258,7 +258,7 @@ def test_gemv_small_batches(wv, oracle, metric, kind, n, d, k, nq):
     planes = d <= 3072  # bf16 / int8 planes up to 1536, int8-only planes up to 3072
     for forced in (False, True):
         idx.set_option("kernel", 6 if forced else 0)
-        expect = "gemv" if forced or not planes else ("qs_bf16", "qs_w4", "qs_int8")
+        expect = "gemv" if forced or not planes else ("qs_bf16", "qs_w4", "qs_int8", "q8_gemv")
         before = idx.stats()["replayed_queries"]
         ids, dists, counts = idx.search_by_vector_batch(queries, k)
         route = wv._lib.ROUTES[idx.stats()["last_route"]]

@@ -319,3 +319,46 @@ def test_q8_only_nonfinite_row_leaves_block_keys(wv, oracle):
     for qi in range(len(queries)):
         assert_same(orc2.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"n{qi}")
     idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,variant,n,d,k", [
+    ("cosine", 0, "avx256", 30000, 768, 10),
+    ("l2-squared", 0, "avx256", 20000, 400, 10),    # dpb8 512: zero-padded columns
+    ("dot", 0, "avx512", 12000, 1024, 24),
+    ("l2-squared", 1, "avx256", 20000, 512, 100),   # integer data: ties -> replay
+    ("cosine", 0, "avx256", 9000, 1536, 10),        # NC 24: one query group per wave
+])
+@pytest.mark.parametrize("nq", [1, 7, 16, 17, 32])
+def test_q8_gemv_small_batches_match_blockkey(wv, oracle, metric, kind, variant, n, d, k, nq):
+    """Batches of <= 32 queries take k_q8_gemv (the int8 plane streamed through
+    registers, no 256-query padding): the block keys must be bit-identical to
+    k_q8_blockkey's, the results equal to the oracle's, with deletions and an
+    allow list."""
+    data = gen(oracle, kind, 191, n, d)
+    queries = gen(oracle, kind, 192, nq, d)
+    idx, orc = build_pair(wv, oracle, metric, variant, data)
+    gone = list(range(11, n, 37))
+    idx.delete(*gone)
+    orc.delete(gone)
+    res, keys = {}, {}
+    for g in (1, 0):
+        idx.set_option("q8_gemv", g)
+        res[g] = idx.search_by_vector_batch(queries, k)
+        dpb8 = -(-d // 128) * 128 if d <= 768 else -(-d // 256) * 256
+        gemv = g and (nq <= 16 or dpb8 <= 1024)  # two query groups per wave need NC <= 16
+        assert idx.stats()["last_route"] == (9 if gemv else ROUTE_INT8)
+        keys[g] = [idx.debug_blockkeys(q)[0] for q in range(nq)]
+    for q in range(nq):
+        np.testing.assert_array_equal(keys[1][q].view(np.uint32), keys[0][q].view(np.uint32), err_msg=f"keys q{q}")
+    for a, b in zip(res[1], res[0]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    ids, dists, counts = res[1]
+    for qi in range(nq):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], ctx=f"q{qi}")
+    idx.set_option("q8_gemv", 1)
+    allow = list(range(3, n, 5))
+    ids, dists, counts = idx.search_by_vector_batch(queries, k, allow=wv.AllowList(allow))
+    for qi in range(nq):
+        assert_same(orc.search(queries[qi], k, allow=allow), ids[qi, :counts[qi]], dists[qi, :counts[qi]],
+                    ctx=f"a{qi}")
+    idx.close()

@@ -1,6 +1,7 @@
 """Small-batch route measurement on the C3 corpus (10M x 768 cosine, k = 10):
-per batch size, the padded block-key route (qs, the int8 key pass over
-256-query groups) vs the HBM-streaming GEMV select (kernel 6), device-resident
+per batch size, the register-streaming int8 key kernel (q8_gemv, <= 32
+queries), the padded block-key route (qs, the int8 key pass over 256-query
+groups) and the HBM-streaming fp32 GEMV select (kernel 6), device-resident
 queries, wall clock over repeated calls.  Prints one JSON line per (B, route)
 and a final line with the crossover the runtime's `gemv_max` default encodes."""
 import argparse
@@ -54,7 +55,9 @@ def run(B):
 best = {}
 for B in (int(b) for b in args.batches.split(",")):
     res = {}
-    for route, opts in (("qs", {"kernel": 0, "gemv_max": 0}), ("gemv", {"kernel": 6, "gemv_max": 4096})):
+    for route, opts in (("q8_gemv", {"kernel": 0, "gemv_max": 0, "q8_gemv": 1}),
+                        ("qs", {"kernel": 0, "gemv_max": 0, "q8_gemv": 0}),
+                        ("gemv", {"kernel": 6, "gemv_max": 4096})):
         for kk, vv in opts.items():
             idx.set_option(kk, vv)
         run(B)
@@ -68,7 +71,7 @@ for B in (int(b) for b in args.batches.split(",")):
         res[route] = (dt, oi[:B].cpu().clone(), od[:B].cpu().clone())
         print(json.dumps({"B": B, "route": route, "ran": _lib.ROUTES.get(st["last_route"], st["last_route"]),
                           "ms": round(dt * 1e3, 3), "qps": round(B / dt, 1)}), flush=True)
-    same = bool(torch.equal(res["qs"][1], res["gemv"][1]) and torch.equal(res["qs"][2], res["gemv"][2]))
+    same = all(bool(torch.equal(res["qs"][1], res[r][1]) and torch.equal(res["qs"][2], res[r][2])) for r in res)
     best[B] = min(res, key=lambda r: res[r][0])
     print(json.dumps({"B": B, "faster": best[B], "same_results": same}), flush=True)
 print(json.dumps({"faster_by_batch": best}), flush=True)

@@ -63,7 +63,15 @@ class WvMultiConfig(C.Structure):
         ("id_stride", C.c_uint64),
         ("transport", C.c_int32),
         ("unique_id", C.c_void_p),
+        ("host_allgather", C.c_void_p),
+        ("host_broadcast", C.c_void_p),
+        ("host_user", C.c_void_p),
     ]
+
+
+# WV_TRANSPORT_HOST callbacks (include/wv_knn.h)
+HOST_ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
+HOST_BROADCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p)
 
 
 class WvStats(C.Structure):
@@ -82,7 +90,7 @@ class WvStats(C.Structure):
 
 # wv_stats.last_route (include/wv_knn.h WV_ROUTE_*)
 ROUTES = {0: "none", 1: "qs_bf16", 2: "qs_w4", 3: "qs_int8", 4: "f32_select", 5: "gemv", 6: "bq_int8", 7: "bq_valu",
-          8: "pq_int8"}
+          8: "pq_int8", 9: "q8_gemv"}
 
 
 P = C.c_void_p

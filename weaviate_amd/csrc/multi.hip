@@ -232,6 +232,47 @@ struct RcclTransport : Transport {
     }
 };
 
+// one local shard; collectives staged through host memory to the caller's
+// functions (synchronous: the shard's stream is drained first)
+struct HostTransport : Transport {
+    int world = 1, rank = 0;
+    wv_host_allgather_fn ag = nullptr;
+    wv_host_broadcast_fn bc = nullptr;
+    void* user = nullptr;
+    std::vector<unsigned char> hs, hr;
+    int all_gather(int nf, const void* const* send, void* const* recv, const size_t* bytes) override {
+        HIPCHK(hipSetDevice(dev[0]));
+        for (int f = 0; f < nf; f++) {
+            hs.resize(std::max<size_t>(bytes[f], 1));
+            hr.resize(std::max<size_t>(bytes[f] * world, 1));
+            HIPCHK(hipMemcpyAsync(hs.data(), send[f], bytes[f], hipMemcpyDeviceToHost, s[0]));
+            HIPCHK(hipStreamSynchronize(s[0]));
+            if (ag(hs.data(), hr.data(), (int64_t)bytes[f], user) != 0)
+                return set_err(WV_ERR_HIP, "host transport: all-gather callback failed");
+            HIPCHK(hipMemcpyAsync(recv[f], hr.data(), bytes[f] * world, hipMemcpyHostToDevice, s[0]));
+            HIPCHK(hipStreamSynchronize(s[0]));
+        }
+        return WV_OK;
+    }
+    int broadcast(int nf, void* const* buf, const size_t* bytes, int root) override {
+        HIPCHK(hipSetDevice(dev[0]));
+        for (int f = 0; f < nf; f++) {
+            hs.resize(std::max<size_t>(bytes[f], 1));
+            if (rank == root) {
+                HIPCHK(hipMemcpyAsync(hs.data(), buf[f], bytes[f], hipMemcpyDeviceToHost, s[0]));
+                HIPCHK(hipStreamSynchronize(s[0]));
+            }
+            if (bc(hs.data(), (int64_t)bytes[f], root, user) != 0)
+                return set_err(WV_ERR_HIP, "host transport: broadcast callback failed");
+            if (rank != root) {
+                HIPCHK(hipMemcpyAsync(buf[f], hs.data(), bytes[f], hipMemcpyHostToDevice, s[0]));
+                HIPCHK(hipStreamSynchronize(s[0]));
+            }
+        }
+        return WV_OK;
+    }
+};
+
 // ---------------------------------------------------------------------------
 // small kernels of the protocol
 // ---------------------------------------------------------------------------
@@ -750,8 +791,11 @@ extern "C" int wv_multi_create(const wv_multi_config* cfg, wv_multi** out) {
     if (cfg->n_local > 64) return set_err(WV_ERR_INVALID, "at most 64 shards per process");
     if (cfg->index.compression != WV_COMPRESSION_NONE)
         return set_err(WV_ERR_UNSUPPORTED, "multi-shard index: exact (uncompressed) search only");
-    if (cfg->transport != WV_TRANSPORT_LOCAL && cfg->transport != WV_TRANSPORT_RCCL)
+    if (cfg->transport != WV_TRANSPORT_LOCAL && cfg->transport != WV_TRANSPORT_RCCL &&
+        cfg->transport != WV_TRANSPORT_HOST)
         return set_err(WV_ERR_INVALID, "unknown transport %d", cfg->transport);
+    if (cfg->transport == WV_TRANSPORT_HOST && (cfg->n_local != 1 || !cfg->host_allgather || !cfg->host_broadcast))
+        return set_err(WV_ERR_INVALID, "host transport: one local shard and both callbacks");
     if (cfg->transport == WV_TRANSPORT_LOCAL && cfg->n_local != cfg->world)
         return set_err(WV_ERR_INVALID, "local transport: every rank must be a local shard");
     if (cfg->transport == WV_TRANSPORT_RCCL && cfg->n_local != cfg->world && !cfg->unique_id)
@@ -794,6 +838,16 @@ extern "C" int wv_multi_create(const wv_multi_config* cfg, wv_multi** out) {
         auto t = std::make_unique<LocalTransport>();
         for (auto& R : m->r) { t->dev.push_back(R->dev); t->s.push_back(R->s); }
         rc = t->init();
+        tr = std::move(t);
+    } else if (cfg->transport == WV_TRANSPORT_HOST) {
+        auto t = std::make_unique<HostTransport>();
+        for (auto& R : m->r) { t->dev.push_back(R->dev); t->s.push_back(R->s); }
+        t->world = m->world;
+        t->rank = m->rank0;
+        t->ag = cfg->host_allgather;
+        t->bc = cfg->host_broadcast;
+        t->user = cfg->host_user;
+        rc = WV_OK;
         tr = std::move(t);
     } else {
         auto t = std::make_unique<RcclTransport>();

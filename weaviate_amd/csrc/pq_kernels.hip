@@ -1104,7 +1104,9 @@ __global__ __launch_bounds__(256) void k_pq_center_queries(const float* __restri
 // with eps >= |A - ADC|); strictly increasing -> they are the worker heap's
 // content and its ascending extraction; else, or a list overflow (sel_flags),
 // more than PQC_CAP rows below the cap or a NaN, flag_out[q] = 1 (the full
-// replay resolves q).  Workgroup per query, 8 blocks x 32 rows per pass.
+// replay resolves q).  Workgroup per query, 8 blocks x 32 rows per pass;
+// fmask (k_q8_filt_bm survivor masks [q][L]) skips rows whose int8 bound
+// already reaches the cap; qlist / qcount: the listed queries only.
 template <int KC>
 __global__ __launch_bounds__(256) void k_pq_cand8(const uint32_t* __restrict__ codes, int g16, int m, int kk,
                                                   const uint32_t* __restrict__ valid, int64_t nslots,
@@ -1113,12 +1115,17 @@ __global__ __launch_bounds__(256) void k_pq_cand8(const uint32_t* __restrict__ c
                                                   const int32_t* __restrict__ sel_flags, const float* __restrict__ cap,
                                                   int R, int metric, uint64_t id_base, uint64_t* __restrict__ asc_ids,
                                                   float* __restrict__ asc_d, int32_t* __restrict__ asc_n,
-                                                  int32_t* __restrict__ flag_out) {
+                                                  int32_t* __restrict__ flag_out, const uint32_t* __restrict__ fmask,
+                                                  const int32_t* __restrict__ qlist, const uint32_t* __restrict__ qcount) {
     __shared__ float sv[PQC_CAP];
     __shared__ uint32_t ss[PQC_CAP];
     __shared__ int s_cnt, s_bad;
     const int k = KC > 0 ? KC : kk;
-    const int q = blockIdx.x;
+    int q = blockIdx.x;
+    if (qlist) {  // a second pass over the listed queries (qcount[1] of them)
+        if ((uint32_t)q >= qcount[1]) return;
+        q = qlist[q];
+    }
     const int t = threadIdx.x;
     if (sel_flags[q] != 0) {
         if (t == 0) flag_out[q] = 1;
@@ -1135,6 +1142,9 @@ __global__ __launch_bounds__(256) void k_pq_cand8(const uint32_t* __restrict__ c
         if (j >= nc) break;
         const int64_t row = (int64_t)cand[(int64_t)q * L + j] * 32 + (t & 31);
         if (row >= nslots || !((valid[row >> 5] >> (row & 31)) & 1u)) continue;
+        // the block-major int8 row bound (k_q8_filt_bm): a row whose A_row - eps
+        // reaches the cap has an ADC >= cap, which the list never keeps
+        if (fmask && !((fmask[(int64_t)q * L + j] >> (t & 31)) & 1u)) continue;
         float sum = 0.f;
         for (int g = 0; g < g16; g++) {
             const uint4 cw = *reinterpret_cast<const uint4*>(cb + ((((row >> 8) * g16 + g) << 8) + (row & 255)) * 16);

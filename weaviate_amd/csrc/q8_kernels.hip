@@ -1152,5 +1152,94 @@ __global__ void k_bq_unpack8(const uint64_t* __restrict__ codes, int64_t ccap, i
     *reinterpret_cast<uint32_t*>(X8 + q8_plane_byte(slot, c4, dpb8)) = word;
 }
 
+// ---------------------------------------------------------------------------
+// k_q8_gemv<NC, QG, L2>: the block keys of a small batch (16 QG <= 32
+// queries) by streaming the int8 plane once through registers.  The 256-query
+// kernel pads a small batch to a full query group and keeps one workgroup per
+// CU (its LDS ring), which leaves the plane stream latency-bound (C3, B = 1:
+// 3.4 ms for 7.7 GB).  Here every wave owns whole 32-row blocks: per row half
+// m the A fragments come straight from the tiled plane (lane (i, kq): row
+// 16m + i, columns 64c + 16kq.., 16 contiguous bytes; 1 KiB per wave per
+// chunk), the queries' B fragments stay in VGPRs, no LDS, many waves per SIMD
+// in flight.  Products, scales and the key formula are k_q8_blockkey's (the
+// same v_mfma_i32_16x16x64_i8 integer sums, fl(sq sb), one fma for L2), so the
+// keys are bit-identical.
+// ---------------------------------------------------------------------------
+template <int NC, int QG, bool ISL2>
+__global__ __launch_bounds__(256) void k_q8_gemv(Q8Args a, int64_t nb) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int j = lane & 15, kq = lane >> 4;
+    const int64_t lofs = (int64_t)(kq >> 1) * 8192 + 16 * (kq & 1);
+    i32x4_t Qf[QG][NC];
+#pragma unroll
+    for (int g = 0; g < QG; g++)
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+            Qf[g][c] = *reinterpret_cast<const i32x4_t*>(a.Q8 + (int64_t)(2 * c) * 8192 + lofs + (16 * g + j) * 32);
+    float sq[QG];
+#pragma unroll
+    for (int g = 0; g < QG; g++) sq[g] = a.qscale[16 * g + j];
+    constexpr int64_t TILE_B = (int64_t)NC * 2 * 8192;
+    for (int64_t b = wave0; b < nb; b += nwaves) {
+        const int64_t r0 = b * 32;
+        const unsigned char* base = a.X8 + (r0 >> 8) * TILE_B + (r0 & 255) * 32 + lofs;
+        i32x4_t acc[2][QG];
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            i32x4_t A[NC];
+#pragma unroll
+            for (int c = 0; c < NC; c++)
+                A[c] = *reinterpret_cast<const i32x4_t*>(base + (int64_t)(2 * c) * 8192 + (16 * m + j) * 32);
+#pragma unroll
+            for (int g = 0; g < QG; g++) {
+                acc[m][g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], Qf[g][0], i32x4_t{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+                for (int c = 1; c < NC; c++) acc[m][g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[c], Qf[g][c], acc[m][g], 0, 0, 0);
+            }
+        }
+        // acc[m][g][r]: row 16m + 4 (lane >> 4) + r of query 16g + (lane & 15)
+        const uint32_t vw = a.valid[b];
+        const float sb = a.sb[b];
+        const int rg = 4 * (lane >> 4);
+        f32x4_t xn[2];
+        if constexpr (ISL2) {
+            xn[0] = *reinterpret_cast<const f32x4_t*>(a.xnorm2 + r0 + rg);
+            xn[1] = *reinterpret_cast<const f32x4_t*>(a.xnorm2 + r0 + 16 + rg);
+        }
+#pragma unroll
+        for (int g = 0; g < QG; g++) {
+            const float s = sq[g] * sb;
+            float key;
+            if constexpr (ISL2) {
+                const float cn = -2.f * s;
+                float mn = __builtin_inff();
+#pragma unroll
+                for (int m = 0; m < 2; m++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float v = fmaf(cn, (float)acc[m][g][r], xn[m][r]);
+                        mn = fminf(mn, ((vw >> (16 * m + rg + r)) & 1u) ? v : __builtin_inff());
+                    }
+                mn = fminf(mn, __shfl_xor(mn, 16));
+                mn = fminf(mn, __shfl_xor(mn, 32));
+                key = mn;
+            } else {
+                int mi = Q8_NONE;
+#pragma unroll
+                for (int m = 0; m < 2; m++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        mi = max(mi, ((vw >> (16 * m + rg + r)) & 1u) ? acc[m][g][r] : Q8_NONE);
+                mi = max(mi, __shfl_xor(mi, 16));
+                mi = max(mi, __shfl_xor(mi, 32));
+                key = mi == Q8_NONE ? __builtin_inff() : -(s * (float)mi);
+            }
+            if (lane < 16) a.key[(int64_t)(16 * g + lane) * a.ldk + b] = key;
+        }
+    }
+}
+
 }  // namespace
 }  // namespace wv

@@ -45,11 +45,11 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
 
 // k_q8_filt_bm<METRIC>: the int8 row filter block-major (survivor masks of
 // every listing, fmask [cn][L]); the capped exact pass reads them
-void launch_q8_filt_bm(wv_index* idx, hipStream_t s, int metric, const Q8Filter& f, const uint32_t* valid, int64_t nb,
-                       int L, const float* capv, const float4* qinfo, uint32_t* fmask) {
-    const float gd = (float)gamma_n(idx->dpb + 8);
+void launch_q8_filt_bm(wv_index* idx, hipStream_t s, int metric, const Q8Filter& f, const float* xn2,
+                       const uint32_t* valid, int64_t nb, int L, const float* capv, const float4* qinfo, float gd,
+                       uint32_t* fmask) {
     const size_t lds = (size_t)(f.dpb8 >> 5) * 1024 + (size_t)8 * (f.dpb8 >> 5) * 32;
-#define WV_FB(M) k_q8_filt_bm<M><<<(unsigned)nb, 256, lds, s>>>(f, idx->xnorm2, valid, idx->hiwater, idx->bmOff.as<uint32_t>(), idx->bmPairs.as<uint32_t>(), L, capv, qinfo, idx->d_maxn2, gd, fmask)
+#define WV_FB(M) k_q8_filt_bm<M><<<(unsigned)nb, 256, lds, s>>>(f, xn2, valid, idx->hiwater, idx->bmOff.as<uint32_t>(), idx->bmPairs.as<uint32_t>(), L, capv, qinfo, idx->d_maxn2, gd, fmask)
     switch (metric) {
     case L2: WV_FB(L2); break;
     case DOT: WV_FB(DOT); break;

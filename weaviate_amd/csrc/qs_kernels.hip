@@ -1147,6 +1147,129 @@ __global__ __launch_bounds__(256) void k_blk_select_f(const float* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Split selection for small batches (k_blk_select_f's outputs and candidate
+// set).  One wave per query streams ldk keys with a serial latency chain
+// (C3, B = 1: 312k keys, 0.73 ms -- a third of the batch); here a query's keys
+// are cut into P chunks, one wave each, in three short kernels:
+//   k_sel_part     the chunk's k+1 smallest keys (WaveTopL<RT>) -> part[q][p][k+1]
+//   k_sel_mid      one wave per query: M = A of the (k+1)-th smallest of the P
+//                  lists (= of all keys), eps, T = M + 2.0005 eps, the cap,
+//                  topA, flags (non-finite query: 2), ncand = 0
+//   k_sel_collect  every chunk again: blocks with A <= T appended through an
+//                  atomic cursor (any order: k_blk_exact and the inversion
+//                  take any order), more than L -> flag 2, ncand clamped to L
+// ---------------------------------------------------------------------------
+template <int RT>
+__global__ __launch_bounds__(64) void k_sel_part(const float* __restrict__ key, int64_t ldk, int64_t nb, int k, int P,
+                                                 float* __restrict__ part) {
+    __shared__ float sbk[64];
+    __shared__ uint32_t sbi[64];
+    constexpr int U = 16;
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int64_t q = blockIdx.y;
+    const int64_t per = (nb + P - 1) / P;
+    const int64_t b0 = (int64_t)p * per, b1 = b0 + per < nb ? b0 + per : nb;
+    const float* kr = key + q * ldk;
+    WaveTopL<RT> t;
+    t.init();
+    for (int64_t c0 = b0; c0 < b1; c0 += 64 * U) {
+        float v[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const int64_t bb = c0 + j * 64 + lane;
+            v[j] = bb < b1 ? kr[bb] : __builtin_inff();
+        }
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < U; j++) any |= v[j] < t.thr;
+        if (!__any(any)) continue;
+#pragma unroll
+        for (int j = 0; j < U; j++) t.offer(v[j], 0u, sbk, sbi, lane);
+    }
+    t.merge(sbk, sbi, lane);
+#pragma unroll
+    for (int r = 0; r < RT - 1; r++) {
+        const int e = r * 64 + lane;
+        if (e <= k) part[(q * P + p) * (k + 1) + e] = t.key[r];
+    }
+}
+
+template <int RT>
+__global__ __launch_bounds__(64) void k_sel_mid(const float* __restrict__ part, int P, int nq, int k, int metric,
+                                                const float4* __restrict__ qinfo, const uint32_t* __restrict__ qsmax,
+                                                const uint32_t* __restrict__ maxn2, float gd, float gacc,
+                                                int32_t* __restrict__ ncand, int32_t* __restrict__ flags,
+                                                float* __restrict__ eps_out, float* __restrict__ Tout,
+                                                float* __restrict__ topA, float* __restrict__ cap_out,
+                                                uint32_t* __restrict__ list_ctr) {
+    __shared__ float sbk[64];
+    __shared__ uint32_t sbi[64];
+    const int lane = threadIdx.x;
+    const int q = blockIdx.x;
+    if (list_ctr && q == 0 && lane == 0) {
+        list_ctr[1] = 0u;
+        list_ctr[3] = 0u;
+    }
+    const float4 qi = qinfo[q];
+    const float eps = qs_eps(metric, qi, qsmax, maxn2, gd, gacc);
+    const int n = P * (k + 1);
+    const float* pr = part + (int64_t)q * n;
+    WaveTopL<RT> t;
+    t.init();
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        t.offer(i < n ? pr[i] : __builtin_inff(), 0u, sbk, sbi, lane);
+    }
+    t.merge(sbk, sbi, lane);
+    const float mk = t.key_at(k);
+    const float M = qs_key_to_a(metric, mk, qi.x);
+    if (lane == 0) {
+        ncand[q] = 0;
+        eps_out[q] = eps;
+        Tout[q] = mk == __builtin_inff() ? __builtin_inff() : M + 2.0005f * eps;
+        if (cap_out) cap_out[q] = mk == __builtin_inff() ? __builtin_inff() : qs_next_up(M + 1.001f * eps);
+        flags[q] = qi.w != 0.f ? 2 : 0;
+    }
+    if (topA) {
+#pragma unroll
+        for (int r = 0; r < RT - 1; r++) {
+            const int e = r * 64 + lane;
+            if (e <= k) topA[(int64_t)q * (k + 1) + e] = qs_key_to_a(metric, t.key[r], qi.x);
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_sel_collect(const float* __restrict__ key, int64_t ldk, int64_t nb, int P,
+                                                    int metric, const float4* __restrict__ qinfo,
+                                                    const float* __restrict__ Tq, uint32_t* __restrict__ cand, int L,
+                                                    int32_t* __restrict__ ncand, int32_t* __restrict__ flags) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int64_t q = blockIdx.y;
+    const int64_t per = (nb + P - 1) / P;
+    const int64_t b0 = (int64_t)p * per, b1 = b0 + per < nb ? b0 + per : nb;
+    const float T = Tq[q];
+    const float qn2 = qinfo[q].x;
+    const float* kr = key + q * ldk;
+    for (int64_t bb = b0 + lane; bb - lane < b1; bb += 64) {
+        const float v = bb < b1 ? kr[bb] : __builtin_inff();
+        const bool in = v < __builtin_inff() && qs_key_to_a(metric, v, qn2) <= T;
+        const uint64_t m = __ballot(in);
+        if (m == 0) continue;
+        int base = 0;
+        if (lane == __builtin_ctzll(m)) base = atomicAdd(&ncand[q], __popcll(m));
+        base = __shfl(base, __builtin_ctzll(m));
+        const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        if (in && pos < L) cand[q * L + pos] = (uint32_t)bb;
+        if (in && pos >= L) flags[q] = 2;  // more than L qualify (select_f: nc > L)
+    }
+}
+
+__global__ void k_sel_clamp(int nq, int L, int32_t* __restrict__ ncand) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq && ncand[q] > L) ncand[q] = L;
+}
+
 // k_blk_gthresh: sharded phase 2, wave per query.  M_g = the (k+1)-th smallest
 // of the W shards' k+1 smallest block-key A values (= the (k+1)-th smallest
 // key over the whole corpus), eps_max = the largest shard eps of the query.

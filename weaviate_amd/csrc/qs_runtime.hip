@@ -7,6 +7,34 @@
 // 64 R): k + 1 <= 960 stays on the block-key path
 int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : k + 1 <= 960 ? 16 : 0; }
 
+// the candidate lists (cand [cn][L], ncand, unflagged queries) inverted per
+// 32-row block: bmOff [nb + 1] offsets of bmPairs (query << 9 | list position).
+// bmCnt is all-zero between batches (k_inv_scatter counts it down); a new,
+// regrown (the allocator may hand back the same address) or never-completed
+// buffer is zeroed once.
+int invert_lists(wv_index* idx, hipStream_t s, const uint32_t* cand, const int32_t* ncand, const int32_t* flags,
+                 int64_t cn, int L, int64_t nb) {
+    HIPCHK(idx->bmCnt.ensure((size_t)nb * sizeof(uint32_t)));
+    HIPCHK(idx->bmOff.ensure((size_t)(nb + 1) * sizeof(uint32_t)));
+    HIPCHK(idx->bmPairs.ensure((size_t)cn * L * sizeof(uint32_t)));
+    if (idx->bmCnt_zp != idx->bmCnt.p || idx->bmCnt_zb != idx->bmCnt.bytes)
+        HIPCHK(hipMemsetAsync(idx->bmCnt.p, 0, idx->bmCnt.bytes, s));
+    idx->bmCnt_zp = nullptr;
+    const unsigned gw = (unsigned)((cn + 3) / 4);
+    k_inv_count<<<gw, 256, 0, s>>>(cand, ncand, flags, (int)cn, L, idx->bmCnt.as<uint32_t>());
+    const unsigned nparts = (unsigned)((nb + INV_CHUNK - 1) / INV_CHUNK);
+    HIPCHK(idx->bmPart.ensure((size_t)nparts * sizeof(uint32_t)));
+    k_inv_part<<<nparts, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmPart.as<uint32_t>());
+    k_inv_scan<<<nparts, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmPart.as<uint32_t>(),
+                                       idx->bmOff.as<uint32_t>());
+    k_inv_scatter<<<gw, 256, 0, s>>>(cand, ncand, flags, (int)cn, L, idx->bmOff.as<uint32_t>(),
+                                     idx->bmCnt.as<uint32_t>(), idx->bmPairs.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    idx->bmCnt_zp = idx->bmCnt.p;
+    idx->bmCnt_zb = idx->bmCnt.bytes;
+    return WV_OK;
+}
+
 // the int8 block-key pass (k_q8_blockkey, 512 <= dpb8 <= 1536) over a.nslots
 // ring slots for a.nqg 256-query groups, spans chosen as search_qs does
 // (XCD-aware groups, 4 GiB span planes, whole rounds of workgroups)
@@ -256,7 +284,29 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                 }
             } else
 #endif
-            if (idx->q8_shape == 32) {
+            // small batches: the register-streaming kernel (one plane pass, no
+            // 256-query padding of the MFMA work), the same keys
+            const int qg = cn <= 16 ? 1 : 2;
+            const bool gemv = idx->q8_gemv && !q8cp && cn <= 32 && NC8 <= (qg == 1 ? 24 : 16) && nb < (1ll << 40);
+            if (gemv) {
+                idx->stats.last_route = WV_ROUTE_Q8_GEMV;
+                const unsigned gg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (nb + 3) / 4));
+#define WV_Q8G(NCV, QGV, L2V) k_q8_gemv<NCV, QGV, L2V><<<gg, 256, 0, s>>>(q8a, nb)
+#define WV_Q8GQ(NCV, L2V) do { if (qg == 1) WV_Q8G(NCV, 1, L2V); else WV_Q8G(NCV, 2, L2V); } while (0)
+#define WV_Q8GN(L2V)                                   \
+    switch (NC8) {                                     \
+    case 8: WV_Q8GQ(8, L2V); break;                    \
+    case 10: WV_Q8GQ(10, L2V); break;                  \
+    case 12: WV_Q8GQ(12, L2V); break;                  \
+    case 16: WV_Q8GQ(16, L2V); break;                  \
+    case 20: WV_Q8G(20, 1, L2V); break;                \
+    default: WV_Q8G(24, 1, L2V); break;                \
+    }
+                if (l2) { WV_Q8GN(true); } else { WV_Q8GN(false); }
+#undef WV_Q8GN
+#undef WV_Q8GQ
+#undef WV_Q8G
+            } else if (idx->q8_shape == 32) {
 #define WV_Q832(NCV, RBV, L2V)                                                                                \
     do {                                                                                                      \
         HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey32<NCV, RBV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
@@ -339,6 +389,29 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             // shard 1.42 -> 0.59 ms); at RT == RV the sorted-list form is faster
             // (C2: 0.61 vs 0.92 ms)
             const int RT = qs_R(k);
+            // small batches: the split selection (P waves per query)
+            if (!list && cn <= idx->sel_split_max && RT <= RV && RT <= 8) {
+                const int P = (int)std::max<int64_t>(1, std::min<int64_t>(256, (nb + 2047) / 2048));
+                const int LV = 64 * (RV - 1);
+                const size_t pb = (size_t)cn * P * (k + 1) * sizeof(float);
+                if (idx->qsScratch.ensure(pb + (size_t)cn * sizeof(float)) != hipSuccess) return;
+                float* part = idx->qsScratch.as<float>();
+                float* Tq = part + (size_t)cn * P * (k + 1);
+                dim3 gp((unsigned)P, (unsigned)cn);
+#define WV_SPLIT(RTV)                                                                                             \
+    do {                                                                                                          \
+        k_sel_part<RTV><<<gp, 64, 0, s>>>(a.key, ldk, nb, k, P, part);                                            \
+        k_sel_mid<RTV><<<(unsigned)cn, 64, 0, s>>>(part, P, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, \
+                                                   gd, gacc_sel, idx->qsNc.as<int32_t>(), flags,                  \
+                                                   idx->qsEps.as<float>(), Tq, tA, idx->qsCap.as<float>(), lc);    \
+    } while (0)
+                if (RT == 2) WV_SPLIT(2); else if (RT == 4) WV_SPLIT(4); else WV_SPLIT(8);
+#undef WV_SPLIT
+                k_sel_collect<<<gp, 64, 0, s>>>(a.key, ldk, nb, P, metric, qinfo_sel, Tq, idx->qsCand.as<uint32_t>(), LV,
+                                                idx->qsNc.as<int32_t>(), flags);
+                k_sel_clamp<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>((int)cn, LV, idx->qsNc.as<int32_t>());
+                return;
+            }
             if (idx->sel_filter && RT < RV) {
 #define WV_SELF(RV, RTV) k_blk_select_f<RV, RTV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc)
                 if (RV == 4) WV_SELF(4, 2);
@@ -387,32 +460,17 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             HIPCHK(idx->bmPairs.ensure((size_t)cn * L * sizeof(uint32_t)));
             if (bm_rows) HIPCHK(idx->bmE.ensure((size_t)cn * ldE * sizeof(float)));
             else HIPCHK(idx->fMask.ensure((size_t)cn * L * sizeof(uint32_t)));
-            // bmCnt is all-zero between batches (k_inv_scatter counts it down);
-            // a new, regrown (the allocator may hand back the same address) or
-            // never-completed buffer is zeroed once
-            if (idx->bmCnt_zp != idx->bmCnt.p || idx->bmCnt_zb != idx->bmCnt.bytes)
-                HIPCHK(hipMemsetAsync(idx->bmCnt.p, 0, idx->bmCnt.bytes, s));
-            idx->bmCnt_zp = nullptr;
-            const unsigned gw = (unsigned)((cn + 3) / 4);
-            k_inv_count<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
-                                           idx->bmCnt.as<uint32_t>());
-            const unsigned nparts = (unsigned)((nb + INV_CHUNK - 1) / INV_CHUNK);
-            HIPCHK(idx->bmPart.ensure((size_t)nparts * sizeof(uint32_t)));
-            k_inv_part<<<nparts, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmPart.as<uint32_t>());
-            k_inv_scan<<<nparts, 1024, 0, s>>>(idx->bmCnt.as<uint32_t>(), nb, idx->bmPart.as<uint32_t>(),
-                                               idx->bmOff.as<uint32_t>());
-            k_inv_scatter<<<gw, 256, 0, s>>>(idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, (int)cn, L,
-                                             idx->bmOff.as<uint32_t>(), idx->bmCnt.as<uint32_t>(),
-                                             idx->bmPairs.as<uint32_t>());
-            HIPCHK(hipGetLastError());
-            idx->bmCnt_zp = idx->bmCnt.p;
-            idx->bmCnt_zb = idx->bmCnt.bytes;
+            {
+                int rc = invert_lists(idx, s, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, cn, L, nb);
+                if (rc) return rc;
+            }
             if (bm_rows) {
                 launch_exact_bm(idx, s, metric, v5, Qn, nb, bm_lds, ldE);
                 HIPCHK(hipGetLastError());
                 exa(R, nullptr, nullptr, idx->bmE.as<float>(), ldE);
             } else {
-                launch_q8_filt_bm(idx, s, metric, q8f, valid, nb, L, capv, qinfo, idx->fMask.as<uint32_t>());
+                launch_q8_filt_bm(idx, s, metric, q8f, idx->xnorm2, valid, nb, L, capv, qinfo, (float)gamma_n(idx->dpb + 8),
+                                  idx->fMask.as<uint32_t>());
                 HIPCHK(hipGetLastError());
                 exa(R, nullptr, nullptr, nullptr, 0, idx->fMask.as<uint32_t>());
             }

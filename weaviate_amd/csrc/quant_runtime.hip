@@ -1057,11 +1057,44 @@ static int pq8_candidates(wv_index* idx, hipStream_t s, int64_t nq, int R, const
                                             nullptr, idx->qsCap.as<float>(), nullptr);
 #undef WV_PQSEL
     HIPCHK(hipGetLastError());
-#define WV_PQC8(KCV) k_pq_cand8<KCV><<<(unsigned)nq, 256, 0, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, idx->hiwater, idx->lut.as<float>(), idx->qsCand.as<uint32_t>(), L, idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), idx->qsCap.as<float>(), R, L2, idx->id_base, idx->ascI.as<uint64_t>(), idx->ascD.as<float>(), idx->ascN.as<int32_t>(), idx->oF.as<int32_t>())
-    if (K == 256) WV_PQC8(256);
-    else WV_PQC8(0);
-#undef WV_PQC8
+    // the int8 row bound, block-major: each listed block's codes read once
+    // (k_q8_filt_bm), survivor masks for the exact ADC below
+    uint32_t* fmask = nullptr;
+    if (idx->q8_bm) {
+        HIPCHK(idx->fMask.ensure((size_t)nq * L * sizeof(uint32_t)));
+        rc = invert_lists(idx, s, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), nq,
+                          L, nb);
+        if (rc) return rc;
+        Q8Filter f{idx->pq8_X8, idx->pq8_sb, dpb8, idx->q8Qb.as<unsigned char>(), idx->q8Scale.as<float>(),
+                   idx->q8Info.as<float4>(), mx, gacc8};
+        launch_q8_filt_bm(idx, s, L2, f, idx->pq8_n2, valid, nb, L, idx->qsCap.as<float>(), idx->q8Info.as<float4>(), gd,
+                          idx->fMask.as<uint32_t>());
+        HIPCHK(hipGetLastError());
+        fmask = idx->fMask.as<uint32_t>();
+    }
+#define WV_PQC8(KCV, CAND, LV, FM, QL, QC) k_pq_cand8<KCV><<<(unsigned)nq, 256, 0, s>>>(idx->pq_codes, pq_g16(m), m, K, valid, idx->hiwater, idx->lut.as<float>(), CAND, LV, idx->qsNc.as<int32_t>(), idx->qsFlags.as<int32_t>(), idx->qsCap.as<float>(), R, L2, idx->id_base, idx->ascI.as<uint64_t>(), idx->ascD.as<float>(), idx->ascN.as<int32_t>(), idx->oF.as<int32_t>(), FM, QL, QC)
+    if (K == 256) WV_PQC8(256, idx->qsCand.as<uint32_t>(), L, fmask, nullptr, nullptr);
+    else WV_PQC8(0, idx->qsCand.as<uint32_t>(), L, fmask, nullptr, nullptr);
     HIPCHK(hipGetLastError());
+    // queries whose 448-block lists overflowed (select flag 2): again with
+    // 960-block lists (the sorted select over the listed queries), exact ADC of
+    // every valid row of those blocks
+    if (R + 1 <= 960) {
+        constexpr int L16 = 64 * 15;
+        HIPCHK(idx->qsCand2.ensure((size_t)nq * L16 * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
+        k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(idx->qsFlags.as<int32_t>(), (int)nq,
+                                                                  idx->qsList.as<int32_t>(), idx->flCtr.as<uint32_t>(), 2);
+        k_blk_select<16><<<gw, 256, 0, s>>>(a.key, nb, nb, (int)nq, R, L2, idx->q8Info.as<float4>(), mx, mx + 4, gd,
+                                            gacc8, idx->qsCand2.as<uint32_t>(), idx->qsNc.as<int32_t>(),
+                                            idx->qsFlags.as<int32_t>(), idx->qsEps.as<float>(),
+                                            idx->qsList.as<int32_t>(), idx->flCtr.as<uint32_t>(), nullptr,
+                                            idx->qsCap.as<float>(), nullptr);
+        if (K == 256) WV_PQC8(256, idx->qsCand2.as<uint32_t>(), L16, nullptr, idx->qsList.as<int32_t>(), idx->flCtr.as<uint32_t>());
+        else WV_PQC8(0, idx->qsCand2.as<uint32_t>(), L16, nullptr, idx->qsList.as<int32_t>(), idx->flCtr.as<uint32_t>());
+        HIPCHK(hipGetLastError());
+    }
+#undef WV_PQC8
     return WV_OK;
 }
 

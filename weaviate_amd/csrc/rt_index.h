@@ -145,12 +145,14 @@ struct wv_index {
     // 32-row block, built beside the bf16 plane when 384 < dims <= 1536
     int q8_planes = 0, dpb8 = 0;
     int q8_only = 0;                // 1536 < dims <= 3072: int8 planes without the bf16 plane
+    int64_t sel_split_max = 512;    // option sel_split_max: batches up to this many queries use the split selection
     int sel_filter = 1;             // option sel_filter: k_blk_select_f (1) or the sorted-list k_blk_select (0)
     int q8_opt = 1;                 // option q8: block keys from the int8 plane (1) or the bf16 plane (0)
     int q8_R = 0;                   // option q8_R: candidate lists for int8 keys (0: R = 8, 448 blocks)
     int q8_shape = 16;              // option q8_shape: 16 = v_mfma_i32_16x16x64_i8 kernel, 32 = 32x32x32
     int q8_stag = 0;
     int q8_pf = 1;                  // option q8_pf: A-fragment reads 1 or 2 chunks ahead                // option q8_stag: waves 4-7 reduce each block P0 chunks late (RB = 2)
+    int q8_gemv = 1;                // option q8_gemv: batches of <= 32 queries stream the int8 plane through registers (k_q8_gemv)
     int q8_filter = 1;              // option q8_filter: the exact pass bounds rows from the int8 plane (1) or bf16 (0)
     unsigned char* X8 = nullptr;
     float* sb8 = nullptr;
@@ -249,7 +251,7 @@ struct wv_index {
     unsigned char* pq8_X8 = nullptr;
     float* pq8_sb = nullptr;
     float* pq8_n2 = nullptr;
-    DBuf pq8Max, pq8Mu, pq8Tmp, pq8Qc;
+    DBuf pq8Max, pq8Mu, pq8Tmp, pq8Qc, qsCand2;
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
     DBuf flCtr;                      // device flag-list counters (replay_flags)
     int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
@@ -313,13 +315,16 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
               float* o_d, int32_t* o_n, int32_t* o_flags, int phase = 0, float* topA = nullptr,
               const float* gA = nullptr, const float* gE = nullptr, int W = 0);
 int launch_q8_keys(wv_index* idx, hipStream_t s, Q8Args a, int dpb8, bool l2);
+int invert_lists(wv_index* idx, hipStream_t s, const uint32_t* cand, const int32_t* ncand, const int32_t* flags,
+                 int64_t cn, int L, int64_t nb);
 // qs_exact.hip
 void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5, const float* Qn,
                       const uint32_t* valid, int cn, int k, int kout, uint64_t* o_ids, float* o_d, int32_t* o_n,
                       int32_t* flags, const int32_t* list, const uint32_t* cnt, const float* eb, int64_t ldE,
                       const float* capv, const float4* qinfo, const Q8Filter* q8f, const uint32_t* fmask = nullptr);
-void launch_q8_filt_bm(wv_index* idx, hipStream_t s, int metric, const Q8Filter& f, const uint32_t* valid, int64_t nb,
-                       int L, const float* capv, const float4* qinfo, uint32_t* fmask);
+void launch_q8_filt_bm(wv_index* idx, hipStream_t s, int metric, const Q8Filter& f, const float* xn2,
+                       const uint32_t* valid, int64_t nb, int L, const float* capv, const float4* qinfo, float gd,
+                       uint32_t* fmask);
 void launch_exact_bm(wv_index* idx, hipStream_t s, int metric, bool v5, const float* Qn, int64_t nb, size_t bm_lds,
                      int64_t ldE);
 // qs_replay.hip

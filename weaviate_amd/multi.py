@@ -21,7 +21,7 @@ from . import _lib
 from ._lib import check
 from .flat import FlatIndex, make_config
 
-TRANSPORTS = {"local": 0, "rccl": 1}
+TRANSPORTS = {"local": 0, "rccl": 1, "host": 2}
 STAGES = ("phase1", "phase2", "merge", "replay", "merge_records", "chain", "collectives")
 
 
@@ -30,6 +30,39 @@ def rccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     check(_lib.load().wv_rccl_unique_id(buf, 128))
     return buf.raw
+
+
+def torch_host_callbacks(world: int, group=None):
+    """WV_TRANSPORT_HOST callbacks over torch.distributed (e.g. a gloo group):
+    the library hands host buffers, the collective runs on CPU tensors."""
+    import torch
+    import torch.distributed as dist
+
+    def view(p, n):
+        return torch.frombuffer((C.c_uint8 * n).from_address(p), dtype=torch.uint8)
+
+    def allgather(send_p, recv_p, nbytes, user):
+        try:
+            if nbytes > 0:
+                parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+                dist.all_gather(parts, view(send_p, nbytes).clone(), group=group)
+                out = torch.cat(parts)  # alive across the copy
+                C.memmove(recv_p, out.data_ptr(), world * nbytes)
+            return 0
+        except Exception:
+            return 1
+
+    def broadcast(buf_p, nbytes, root, user):
+        try:
+            if nbytes > 0:
+                t = view(buf_p, nbytes).clone()
+                dist.broadcast(t, src=int(root), group=group)
+                C.memmove(buf_p, t.data_ptr(), nbytes)
+            return 0
+        except Exception:
+            return 1
+
+    return _lib.HOST_ALLGATHER_FN(allgather), _lib.HOST_BROADCAST_FN(broadcast)
 
 
 class _ShardView(FlatIndex):
@@ -59,16 +92,23 @@ class MultiFlatIndex:
 
     def __init__(self, distance: str = "cosine", dims: int = 0, devices: Sequence[int] = (0,), world: int = 0,
                  rank0: int = 0, id_stride: int = 0, transport: str = "local", unique_id: Optional[bytes] = None,
-                 variant: str = "auto"):
+                 variant: str = "auto", host_callbacks=None):
+        """transport "host": host_callbacks = (allgather, broadcast) ctypes
+        callbacks (torch_host_callbacks(world) by default)."""
         self._l = _lib.load()
         devs = [int(x) for x in devices]
         world = int(world) or len(devs)
         self._devs = (C.c_int32 * len(devs))(*devs)
         self._uid = C.create_string_buffer(unique_id, 128) if unique_id is not None else None
+        self._cbs = None
+        if transport == "host":
+            self._cbs = host_callbacks or torch_host_callbacks(world)
         cfg_args = dict(distance=distance, dims=dims, variant=variant)
         self._cfg = _lib.WvMultiConfig(make_config(**cfg_args), world, int(rank0), len(devs),
                                        C.cast(self._devs, C.POINTER(C.c_int32)), int(id_stride),
-                                       TRANSPORTS[transport], C.cast(self._uid, C.c_void_p) if self._uid else None)
+                                       TRANSPORTS[transport], C.cast(self._uid, C.c_void_p) if self._uid else None,
+                                       C.cast(self._cbs[0], C.c_void_p) if self._cbs else None,
+                                       C.cast(self._cbs[1], C.c_void_p) if self._cbs else None, None)
         h = C.c_void_p()
         check(self._l.wv_multi_create(C.byref(self._cfg), C.byref(h)))
         self._h = h
