@@ -251,9 +251,10 @@ def verify_sample(workload: str, flat, gen_kind: int, n_total: int, dims: int, B
     (16 queries spread over the batch; 8 for PQ) against the oracle's exact
     scan of the regenerated corpus (oracle/scale.c; the reference heap
     semantics of flat/index.go:578-688), bit-exact ids and distances.
-    Returns {"verified": bool, "checked": n, ...} or None when the workload
-    has no oracle check here (rq: the 10M-row rotational oracle is too large
-    for the host leg)."""
+    rq-8 / rq-1: oracle/scale.c's or_rq_search_gen encodes every regenerated
+    row on the host (rq.c's rotation + encoder) and replays the R-heap per
+    sampled query.  Returns {"verified": bool, "checked": n, ...} or None when
+    the workload has no oracle check here."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc  # test infrastructure: the checker, outside the timed region
     ids, dists, counts = (t.cpu().numpy() for t in res)
@@ -273,6 +274,11 @@ def verify_sample(workload: str, flat, gen_kind: int, n_total: int, dims: int, B
     elif workload == "bq":
         qs = orc.gen_matrix(0, SEED_QUERY, 0, B, dims)[sample]
         oi, od, on = orc.bq_search_gen(0, SEED_CORPUS, n_total, dims, orc.COSINE, orc.AVX256, qs, k, bq_r, threads)
+        exp = [(oi[i, :on[i]], od[i, :on[i]]) for i in range(len(sample))]
+    elif workload in ("rq8", "rq1"):
+        qs = orc.gen_matrix(gen_kind, SEED_QUERY, 0, B, dims)[sample]
+        oi, od, on = orc.rq_search_gen(8 if workload == "rq8" else 1, gen_kind, SEED_CORPUS, n_total, dims, orc.COSINE,
+                                       orc.AVX256, qs, k, bq_r, threads)
         exp = [(oi[i, :on[i]], od[i, :on[i]]) for i in range(len(sample))]
     elif workload == "pq" and world == 1:
         from concurrent.futures import ThreadPoolExecutor
@@ -598,10 +604,32 @@ def main():
                  "k_pq_adc2" if shard or pq_sel == "0" else "k_pq_adc4" if pq_sel == "2" else "k_pq_adc3") if pq \
         else "k_pq_adc2"
     dom_kernel = (pq_kernel if pq else ("k_q8_blockkey_bq" if route == 6 else "k_bq_blockmin_lds") if bq else
-                  ("k_rq8_dist" if rq_bits == 8 else "k_rq1_dist") if rq_bits else sel_kernel)
+                  ("k_rq8_keys" if route == 10 else "k_rq8_dist" if rq_bits == 8 else "k_rq1_dist") if rq_bits
+                  else sel_kernel)
     if args.traffic_bytes is None:
         args.traffic_bytes = measured_traffic(args.workload, n_local, dims, B, dom_kernel)
-    if rq_bits:
+    if rq_bits and route == 10:
+        # dominant kernel: k_rq8_keys (rq8_mfma.hip), the
+        # exact rq-8 distance of every (query, row) on v_mfma_i32_16x16x64_i8
+        # (one int8 product per (query, row, code byte), D = dims rounded up to
+        # 64) plus the reference's float epilogue, reduced to 32-row minima in
+        # registers; the codes (n_local x D bytes) stream once per launch
+        D = (dims + 63) // 64 * 64
+        f0 = int(index.stats().get("last_group_queries", 0)) or B
+        t = sel_avg * 1e-3
+        ops = 2.0 * f0 * n_local * D
+        plane = float(n_local) * (D + 20)
+        mfma_frac = ops / t / 1e12 / MFMA_I8_PEAK_TOPS if t > 0 else 0.0
+        hbm_frac = plane / t / 1e9 / HBM_PEAK_GBPS if t > 0 else 0.0
+        roof = {"bound": "mfma", "kernel": "k_rq8_keys", "achieved": ops / t / 1e12 if t > 0 else 0.0,
+                "peak": MFMA_I8_PEAK_TOPS, "unit": "TOPS (int8 MFMA)", "frac": mfma_frac, "launch_ms": sel_avg,
+                "hbm_frac": hbm_frac,
+                "algorithmic": f"2 x {f0} x {n_local} x {D} int8 ops; {n_local} x {D + 20} code + meta bytes",
+                "mfma": "v_mfma_i32_16x16x64_i8 on (x - 128)(y - 128) + 128 (Sx + Sy) - 16384 D = dotByteImpl "
+                        "exactly; the reference's fp32 epilogue per (query, row), unfused",
+                "epilogue_valu_per_pair": "about 17 VALU ops per (query, row): the kernel is VALU-issue bound",
+                "traffic": args.traffic_bytes}
+    elif rq_bits:
         # dominant kernel k_rq8_dist / k_rq1_dist, timed on the first query
         # group of the batch (search_rq: groups of RQ_QPB multiples whose
         # distance rows fit 4 GiB).  rq-8: one v_dot4_u32_u8 per 4 code bytes
@@ -760,7 +788,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if bq else "strong",
             "vs_baseline": None,
-            "dtype": ("u8 codes (v_dot4) + f32 rescoring" if rq_bits == 8 else
+            "dtype": ("u8 codes (int8 MFMA, exact int32 dot) + f32 rescoring" if rq_bits == 8 and route == 10 else
+                      "u8 codes (v_dot4) + f32 rescoring" if rq_bits == 8 else
                       "u64 codes x 5-bit query planes + f32 rescoring" if rq_bits == 1 else
                       "+-1 int8 codes (hamming on the integer MFMA) + f32 rescoring" if bq and route == 6 else
                       "u64 hamming + f32 rescoring" if bq else "u8 codes + f32 LUT" if pq else

@@ -515,6 +515,7 @@ typedef struct wv_stats {
 #define WV_ROUTE_BQ_VALU 7   /* BQ block minima: k_bq_blockmin_lds / k_bq_blockmin (xor + popcount) */
 #define WV_ROUTE_PQ_INT8 8   /* PQ: k_q8_blockkey over the centred int8 reconstruction plane (l2-squared) */
 #define WV_ROUTE_Q8_GEMV 9   /* k_q8_gemv (int8 block keys of <= 32 queries streamed through registers) */
+#define WV_ROUTE_RQ8_INT8 10 /* flat rq-8: k_rq8_keys (exact rq-8 block minima on the integer MFMA) */
 int wv_index_stats(wv_index *idx, wv_stats *out);
 
 /* Diagnostic hook (tests): the last MFMA batch's candidates [nq][KP]:

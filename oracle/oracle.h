@@ -102,6 +102,8 @@ int or_gen_dists(int kind, uint64_t seed, long n, long d, int metric, int varian
 int or_heap_scan(const float *dists, long n, int k, uint64_t *out_ids, float *out_dists);
 int or_bq_search_gen(int kind, uint64_t seed, long n, long d, int metric, int variant, const float *queries, long nq,
                      int k, int rescore_limit, int nthreads, uint64_t *out_ids, float *out_d, int *out_n);
+int or_rq_search_gen(int bits, int kind, uint64_t seed, long n, long d, int metric, int variant, const float *queries,
+                     long nq, int k, int rescore_limit, int nthreads, uint64_t *out_ids, float *out_d, int *out_n);
 
 uint64_t or_gen_bits(uint64_t seed, uint64_t row, uint64_t col);
 float or_gen_value(int kind, uint64_t seed, uint64_t row, uint64_t col);

@@ -62,6 +62,9 @@ def lib() -> C.CDLL:
         o.or_bq_search_gen.restype = C.c_int
         o.or_bq_search_gen.argtypes = [C.c_int, C.c_uint64, C.c_long, C.c_long, C.c_int, C.c_int, pf, C.c_long,
                                        C.c_int, C.c_int, C.c_int, pu, pf, pi]
+        o.or_rq_search_gen.restype = C.c_int
+        o.or_rq_search_gen.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_long, C.c_long, C.c_int, C.c_int, pf,
+                                       C.c_long, C.c_int, C.c_int, C.c_int, pu, pf, pi]
         o.or_gen_value.restype = C.c_float
         o.or_gen_value.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64]
         o.bl_set_ref_kernels.argtypes = [C.c_void_p] * 4
@@ -538,6 +541,22 @@ def bq_search_gen(kind: int, seed: int, n: int, d: int, metric: int, variant: in
                                 ids.ctypes.data_as(pu), f(dd), cnt.ctypes.data_as(pi))
     if rc != 0:
         raise RuntimeError("bq_search_gen failed")
+    return ids, dd, cnt
+
+
+def rq_search_gen(bits: int, kind: int, seed: int, n: int, d: int, metric: int, variant: int, queries: np.ndarray,
+                  k: int, rescore_limit: int, nthreads: int = 16):
+    """flat rq-8 / rq-1 searchByVectorQuantized of raw queries over the
+    generated corpus (codes of every row built on the host, oracle/scale.c)."""
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    nq = q.shape[0]
+    ids = np.zeros((nq, k), np.uint64)
+    dd = np.zeros((nq, k), np.float32)
+    cnt = np.zeros(nq, np.int32)
+    rc = lib().or_rq_search_gen(bits, kind, seed, n, d, metric, variant, f(q), nq, k, rescore_limit, nthreads,
+                                ids.ctypes.data_as(pu), f(dd), cnt.ctypes.data_as(pi))
+    if rc != 0:
+        raise RuntimeError("rq_search_gen failed")
     return ids, dd, cnt
 
 

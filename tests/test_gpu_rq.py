@@ -140,3 +140,62 @@ def test_rq_errors(wv, oracle):
     with pytest.raises(wv.WeaviateError, match="vector lengths don't match"):
         idx.search_by_vector(np.zeros(99, np.float32), 3)
     idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,n,d,k,rescore,nq", [
+    ("cosine", 0, 40000, 768, 10, 200, 300),   # the bench's shape, smaller corpus
+    ("l2-squared", 0, 9000, 128, 10, 63, 70),   # R + 1 = 64: the 64-entry list is too short, RT 4
+    ("dot", 0, 7000, 320, 5, -1, 33),           # odd chunk count (D = 320, NC = 5)
+    ("l2-squared", 1, 12000, 64, 20, 100, 40),  # integer data: quantized ties -> replayed queries
+    ("cosine", 0, 3000, 1024, 3, 500, 20),      # D = 1024 (NC 16), R + 2 > 448: RT 16
+])
+def test_rq8_mfma_route_equals_replay_and_oracle(wv, oracle, metric, kind, n, d, k, rescore, nq):
+    """rq-8 on the integer MFMA (k_rq8_keys -> k_rq8_sel -> k_rq8_cand, flagged
+    queries replayed) against the distance-matrix route (rq_mfma 0) over every
+    query, and the oracle on a sample, bit for bit."""
+    data = gen(oracle, kind, 51, n, d)
+    queries = gen(oracle, kind, 52, nq, d)
+    queries[1] = data[17]  # a stored vector: distance ties with itself only
+    idx, orc = build(wv, oracle, 8, metric, "avx256", data, rescore)
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    st = idx.stats()
+    assert st["last_route"] == 10  # WV_ROUTE_RQ8_INT8
+    idx.set_option("rq_mfma", 0)
+    ids0, dists0, counts0 = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] != 10
+    np.testing.assert_array_equal(counts, counts0)
+    np.testing.assert_array_equal(ids, ids0)
+    bits_equal(dists, dists0, "mfma vs replay route")
+    for q in range(0, nq, max(1, nq // 6)):
+        rc, oi, od = orc.search(queries[q], k)
+        np.testing.assert_array_equal(ids[q, :counts[q]], oi, err_msg=f"q{q}")
+        bits_equal(dists[q, :counts[q]], od, f"q{q}")
+    idx.close()
+
+
+def test_rq8_mfma_route_ties_deletes_allow(wv, oracle):
+    """Identical rows tie on the quantized distance: those queries are flagged
+    and replayed; deletes and allow lists mask rows inside the key pass."""
+    n, d, k = 6000, 192, 10
+    data = gen(oracle, 0, 61, n, d)
+    data[2000:2300] = data[1999]
+    idx, orc = build(wv, oracle, 8, "l2-squared", "avx256", data, 50)
+    dele = np.arange(3, n, 11, dtype=np.uint64)
+    idx.delete(*dele)
+    orc.delete(dele)
+    queries = np.concatenate([gen(oracle, 0, 62, 40, d), data[1999:2000], data[4000:4001]])
+    before = idx.stats()["replayed_queries"]
+    ids, dists, counts = idx.search_by_vector_batch(queries, k)
+    assert idx.stats()["last_route"] == 10
+    assert idx.stats()["replayed_queries"] - before >= 1  # the duplicate-row query
+    for q in range(len(queries)):
+        rc, oi, od = orc.search(queries[q], k)
+        np.testing.assert_array_equal(ids[q, :counts[q]], oi, err_msg=f"q{q}")
+        bits_equal(dists[q, :counts[q]], od, f"q{q}")
+    allow = np.arange(100, 5000, 2, dtype=np.uint64)
+    for q in (0, 40, 41):
+        gi, gd = idx.search_by_vector(queries[q], k, allow=wv.AllowList(allow))
+        rc, oi, od = orc.search(queries[q], k, allow=allow)
+        np.testing.assert_array_equal(gi, oi, err_msg=f"allow q{q}")
+        bits_equal(gd, od, f"allow q{q}")
+    idx.close()

@@ -218,3 +218,21 @@ def test_bq_baseline_matches_oracle_bq(oracle):
             assert rc == 0
             np.testing.assert_array_equal(ids[q, :cnt[q]], oi)
             np.testing.assert_array_equal(dd[q, :cnt[q]].view(np.uint32), od.view(np.uint32))
+
+
+@pytest.mark.parametrize("bits", [8, 1])
+def test_rq_search_gen_matches_oracle_flat_rq(oracle, bits):
+    """The bench's full-size rq self-check (or_rq_search_gen: regenerated rows,
+    host codes) equals OracleFlatRQ on a stored copy of the same corpus."""
+    n, d, k, R = 2500, 136, 10, 40
+    data = oracle.gen_matrix(0, 5, 0, n, d)
+    qs = oracle.gen_matrix(0, 6, 0, 6, d)
+    for metric in (oracle.COSINE, oracle.L2, oracle.DOT):
+        ids, dd, cnt = oracle.rq_search_gen(bits, 0, 5, n, d, metric, oracle.AVX256, qs, k, R, 4)
+        o = oracle.OracleFlatRQ(bits, metric, oracle.AVX256, d, n, R)
+        o.add_batch(np.arange(n, dtype=np.uint64), data)
+        for i in range(len(qs)):
+            rc, oi, od = o.search(qs[i], k)
+            assert rc == 0 and cnt[i] == len(oi)
+            np.testing.assert_array_equal(ids[i, :cnt[i]], oi)
+            np.testing.assert_array_equal(dd[i, :cnt[i]].view(np.uint32), od.view(np.uint32))

@@ -90,7 +90,7 @@ class WvStats(C.Structure):
 
 # wv_stats.last_route (include/wv_knn.h WV_ROUTE_*)
 ROUTES = {0: "none", 1: "qs_bf16", 2: "qs_w4", 3: "qs_int8", 4: "f32_select", 5: "gemv", 6: "bq_int8", 7: "bq_valu",
-          8: "pq_int8", 9: "q8_gemv"}
+          8: "pq_int8", 9: "q8_gemv", 10: "rq8_int8"}
 
 
 P = C.c_void_p

@@ -761,8 +761,6 @@ static int ensure_aux(wv_index* idx) {
 }
 
 int rq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq);
-int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int F, int64_t ld, float* E,
-                   float* bmin);
 
 // SQ query codes: idx->qn (prepared, normalised for cosine) -> group-tiled sqq / sqm
 static int sq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq) {
@@ -1761,9 +1759,9 @@ int rq_init(wv_index* idx) {
     if (idx->cap > 0) {  // store already sized (reserve): allocate the codes for it
         const size_t cb = idx->rq_bits == 8 ? (size_t)idx->cap * D : (size_t)(D / 64) * idx->cap * sizeof(uint64_t);
         HIPCHK(hipMalloc(&idx->rq_codes, cb));
-        HIPCHK(hipMalloc(&idx->rq_meta, (size_t)idx->cap * sizeof(float4)));
+        HIPCHK(hipMalloc(&idx->rq_meta, (size_t)idx->cap * RQ_META_B));
         HIPCHK(hipMemset(idx->rq_codes, 0, cb));
-        HIPCHK(hipMemset(idx->rq_meta, 0, (size_t)idx->cap * sizeof(float4)));
+        HIPCHK(hipMemset(idx->rq_meta, 0, (size_t)idx->cap * RQ_META_B));
     }
     return WV_OK;
 }
@@ -1785,28 +1783,145 @@ int rq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq) {
 
 // quantized distances of queries [q0, q0 + F) (q0 % RQ_QPB == 0) -> E [F][ld], bmin
 int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int F, int64_t ld, float* E,
-                   float* bmin) {
+                   float* bmin, const void* qcodes, const float4* qmeta) {
     const int64_t nslots = idx->hiwater;
     const float fl2 = idx->metric == WV_METRIC_L2_SQUARED ? 1.f : 0.f;
     const float fcos = idx->metric == WV_METRIC_COSINE_DOT ? 1.f : 0.f;
+    if (!qcodes) qcodes = idx->rqq.p;
+    if (!qmeta) qmeta = idx->rqm.as<float4>();
     dim3 grid((unsigned)((F + RQ_QPB - 1) / RQ_QPB), (unsigned)(ld / 256));
     if (idx->rq_bits == 8)
         k_rq8_dist<<<grid, 256, 0, s>>>(reinterpret_cast<const uint4*>(idx->rq_codes), idx->rq_meta, idx->rq_D, valid,
-                                        nslots, idx->rqq.as<uint4>(), idx->rqm.as<float4>(), q0, F, fl2, fcos, ld, E,
+                                        nslots, reinterpret_cast<const uint4*>(qcodes), qmeta, q0, F, fl2, fcos, ld, E,
                                         bmin);
     else
         k_rq1_dist<<<grid, 256, 0, s>>>(reinterpret_cast<const uint64_t*>(idx->rq_codes), idx->cap, idx->rq_meta,
-                                        idx->rq_D / 64, valid, nslots, idx->rqq.as<uint64_t>(), idx->rqm.as<float4>(),
+                                        idx->rq_D / 64, valid, nslots, reinterpret_cast<const uint64_t*>(qcodes), qmeta,
                                         q0, F, fl2, fcos, ld, E, bmin);
     HIPCHK(hipGetLastError());
     return WV_OK;
 }
 
-// flat.searchByVectorQuantized (flat/index.go:460-532) for rq-8 / rq-1: exact
-// quantized distances + block minima (k_rq*_dist), the R-heap replayed in id
-// order (k_replay_scan, extracted ascending = reversed pop order), fp32
-// rescoring of the candidates (k_rescore_ids) and the k-heap fed in pop order
-// (k_bq_final with asc = 1).
+// rq-8 on the integer matrix cores (rq8_mfma.hip): the query fragments stay
+// in VGPRs up to D = 1024; the candidate lists hold R + 2 entries
+static bool rq8_route(const wv_index* idx, int R) {
+    return idx->rq_bits == 8 && idx->rq_mfma && idx->rq_D <= 1024 && qs_R(R + 1) != 0 && idx->hiwater > 0;
+}
+
+template <int NC>
+static void launch_rq8_keys(const RQ8Args& a, unsigned grid, hipStream_t s) {
+    constexpr size_t lds = 3 * ((size_t)32 * 64 * NC + 656);
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_rq8_keys<NC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    k_rq8_keys<NC><<<grid, 512, lds, s>>>(a);
+}
+
+// exact rq-8 block minima -> candidate blocks -> exact distances of their
+// rows: the ascending R-lists (ascI / ascD / ascN) of every query, oF[q] = 1
+// where a tie or a NaN leaves the heap's order to the replay
+static int rq8_candidates(wv_index* idx, hipStream_t s, int64_t nq, int R, const uint32_t* valid) {
+    const int D = idx->rq_D, NC = D / 64;
+    const int64_t nblk = (idx->hiwater + 31) / 32;
+    const int RT = qs_R(R + 1);
+    const int Lc = 64 * (RT - 1);
+    const int64_t nq_pad = round_up(nq, 256);
+    // query chunks: key rows of at most 4 GiB
+    int64_t QC = std::max<int64_t>(256, ((4ll << 30) / (nblk * 4)) / 256 * 256);
+    QC = std::min<int64_t>(QC, nq_pad);
+    HIPCHK(idx->rq8Qp.ensure((size_t)nq_pad * D));
+    HIPCHK(idx->rq8Qcs.ensure((size_t)nq_pad * sizeof(uint32_t)));
+    HIPCHK(idx->rq8Qm.ensure((size_t)nq_pad * sizeof(float4)));
+    HIPCHK(idx->qsKey.ensure((size_t)QC * nblk * sizeof(float)));
+    HIPCHK(idx->qsCand.ensure((size_t)nq * Lc * sizeof(uint32_t)));
+    HIPCHK(idx->qsNc.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->oF.ensure((size_t)nq * sizeof(int32_t)));
+    unsigned char* Qp = idx->rq8Qp.as<unsigned char>();
+    uint32_t* Qcs = idx->rq8Qcs.as<uint32_t>();
+    float4* Qm = idx->rq8Qm.as<float4>();
+    HIPCHK(hipMemsetAsync(Qm, 0, (size_t)nq_pad * sizeof(float4), s));
+    HIPCHK(hipMemcpyAsync(Qm, idx->rqm.p, (size_t)nq * sizeof(float4), hipMemcpyDeviceToDevice, s));
+    k_rq8_qprep<<<(unsigned)(nq_pad / 4), 256, 0, s>>>(idx->rqq.as<uint4>(), D, nq, nq_pad, Qp, Qcs);
+    HIPCHK(hipGetLastError());
+    const float fl2 = idx->metric == WV_METRIC_L2_SQUARED ? 1.f : 0.f;
+    const float fcos = idx->metric == WV_METRIC_COSINE_DOT ? 1.f : 0.f;
+    RQ8Args a{};
+    a.codes = reinterpret_cast<const unsigned char*>(idx->rq_codes);
+    a.meta = idx->rq_meta;
+    a.csum = rq_csum(idx);
+    a.valid = valid;
+    a.key = idx->qsKey.as<float>();
+    a.ldk = nblk;
+    a.nblk = nblk;
+    a.fl2 = fl2;
+    a.fcos = fcos;
+    for (int64_t c0 = 0; c0 < nq; c0 += QC) {
+        const int64_t cn = std::min<int64_t>(QC, nq - c0);
+        const int64_t cpad = round_up(cn, 256);
+        a.Qp = Qp + c0 * D;
+        a.qmeta = Qm + c0;
+        a.qcsum = Qcs + c0;
+        a.nqg = (int)(cpad / 256);
+        // spans: ~2048 workgroups (8 per CU), at least 16 blocks each
+        int64_t nspans = std::max<int64_t>(1, std::min<int64_t>(nblk / 16, (2048 + a.nqg - 1) / a.nqg));
+        const int64_t bps = (nblk + nspans - 1) / nspans;
+        nspans = (nblk + bps - 1) / bps;
+        a.blocks_per_span = (int)bps;
+        a.nspans = (int)nspans;
+        const unsigned grid = (unsigned)(a.nqg * nspans);
+        const bool time_it = idx->timing && c0 == 0;
+        if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
+        switch (NC) {
+        case 1: launch_rq8_keys<1>(a, grid, s); break;
+        case 2: launch_rq8_keys<2>(a, grid, s); break;
+        case 3: launch_rq8_keys<3>(a, grid, s); break;
+        case 4: launch_rq8_keys<4>(a, grid, s); break;
+        case 5: launch_rq8_keys<5>(a, grid, s); break;
+        case 6: launch_rq8_keys<6>(a, grid, s); break;
+        case 7: launch_rq8_keys<7>(a, grid, s); break;
+        case 8: launch_rq8_keys<8>(a, grid, s); break;
+        case 9: launch_rq8_keys<9>(a, grid, s); break;
+        case 10: launch_rq8_keys<10>(a, grid, s); break;
+        case 11: launch_rq8_keys<11>(a, grid, s); break;
+        case 12: launch_rq8_keys<12>(a, grid, s); break;
+        case 13: launch_rq8_keys<13>(a, grid, s); break;
+        case 14: launch_rq8_keys<14>(a, grid, s); break;
+        case 15: launch_rq8_keys<15>(a, grid, s); break;
+        default: launch_rq8_keys<16>(a, grid, s); break;
+        }
+        HIPCHK(hipGetLastError());
+        if (time_it) HIPCHK(hipEventRecord(idx->ev1, s));
+        const unsigned gw = (unsigned)((cn + 3) / 4);
+        uint32_t* cand = idx->qsCand.as<uint32_t>() + c0 * Lc;
+        int32_t* ncand = idx->qsNc.as<int32_t>() + c0;
+        int32_t* of = idx->oF.as<int32_t>() + c0;
+        const size_t lq = (size_t)4 * D;
+#define WV_RQ8(RTV)                                                                                                   \
+    do {                                                                                                              \
+        k_rq8_sel<RTV><<<gw, 256, 0, s>>>(a.key, nblk, nblk, (int)cn, R, cand, Lc, ncand, of);                        \
+        k_rq8_cand<RTV><<<gw, 256, lq, s>>>(reinterpret_cast<const uint4*>(idx->rq_codes), idx->rq_meta, valid,        \
+                                            idx->hiwater, a.Qp, a.qmeta, D, fl2, fcos, cand, Lc, ncand, (int)cn, R,    \
+                                            idx->id_base, idx->ascI.as<uint64_t>() + c0 * R,                           \
+                                            idx->ascD.as<float>() + c0 * R, idx->ascN.as<int32_t>() + c0, of);         \
+    } while (0)
+        if (RT == 2) WV_RQ8(2);
+        else if (RT == 4) WV_RQ8(4);
+        else if (RT == 8) WV_RQ8(8);
+        else WV_RQ8(16);
+#undef WV_RQ8
+        HIPCHK(hipGetLastError());
+    }
+    idx->stats.mfma_launches++;
+    idx->stats.last_route = WV_ROUTE_RQ8_INT8;
+    return WV_OK;
+}
+
+// flat.searchByVectorQuantized (flat/index.go:460-532) for rq-8 / rq-1: the
+// worker R-heap fed in id order (addResult == insertToHeap, :470-487),
+// extracted ascending (reversed pop order), fp32 rescoring of those
+// candidates (k_rescore_ids) and the k-heap fed in pop order (k_bq_final,
+// asc = 1).  rq-8 with rq8_route: the R-lists come from rq8_candidates and only
+// its flagged queries are replayed; otherwise every query: exact quantized
+// distances + block minima (k_rq*_dist) and the heap replayed in id order
+// (k_replay_scan).
 int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
                      const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n) {
     if (qd != idx->dims)  // SingleDist of the rescoring (distancer/errors.go:16)
@@ -1822,14 +1937,54 @@ int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
     if (rc) return rc;
     idx->stats.queries += (uint64_t)nq;
     idx->stats.batches++;
-    idx->stats.replayed_queries += (uint64_t)nq;
     HIPCHK(idx->ident.ensure((size_t)nq * sizeof(int32_t)));
     {
         std::vector<int32_t> id((size_t)nq);
         for (int64_t i = 0; i < nq; i++) id[i] = (int32_t)i;
         HIPCHK(hipMemcpyAsync(idx->ident.p, id.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
     }
+    HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
+    HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
+    HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
     const int32_t* qlist = idx->ident.as<int32_t>();
+    int64_t nrep = nq;
+    int rep_by_query = 0;
+    const void* qc = nullptr;
+    const float4* qm = nullptr;
+    const bool mfma = rq8_route(idx, R);
+    if (mfma) {
+        rc = rq8_candidates(idx, s, nq, R, valid);
+        if (rc) return rc;
+        HIPCHK(idx->qsList.ensure((size_t)nq * sizeof(int32_t)));
+        HIPCHK(idx->flCtr.ensure(2 * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
+        k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq,
+                                                                  idx->qsList.as<int32_t>(), idx->flCtr.as<uint32_t>(), 0);
+        HIPCHK(hipGetLastError());
+        uint32_t nf = 0;
+        HIPCHK(hipMemcpyAsync(&nf, idx->flCtr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        nrep = nf;
+        rep_by_query = 1;
+        qlist = idx->qsList.as<int32_t>();
+        if (nf > 0) {  // the flagged queries' codes, compacted into groups of RQ_QPB
+            const int nch = idx->rq_D / 16;
+            const int64_t nf32 = round_up((int64_t)nf, RQ_QPB);
+            HIPCHK(idx->rq8Fq.ensure((size_t)nf32 * idx->rq_D));
+            HIPCHK(idx->rq8Fm.ensure((size_t)nf32 * sizeof(float4)));
+            HIPCHK(hipMemsetAsync(idx->rq8Fq.p, 0, (size_t)nf32 * idx->rq_D, s));
+            HIPCHK(hipMemsetAsync(idx->rq8Fm.p, 0, (size_t)nf32 * sizeof(float4), s));
+            const int64_t nt = (int64_t)nf * nch;
+            k_rq8_gather_q<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(idx->rqq.as<uint4>(), idx->rqm.as<float4>(), nch,
+                                                                         qlist, (int)nf, idx->rq8Fq.as<uint4>(),
+                                                                         idx->rq8Fm.as<float4>());
+            HIPCHK(hipGetLastError());
+            qc = idx->rq8Fq.p;
+            qm = idx->rq8Fm.as<float4>();
+        }
+    }
+    idx->stats.replayed_queries += (uint64_t)nrep;
     const int64_t nslots = idx->hiwater;
     const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
     // query groups: multiples of RQ_QPB, two distance buffers of up to
@@ -1838,44 +1993,47 @@ int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
     // large as memory allows.  Group i's distances (whole GPU, stream s)
     // overlap group i-1's replay (stream aux); buffer i&1 is reused once
     // replay i-2 has finished with it.
-    size_t free_b = 0, total_b = 0;
-    HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    const int64_t have = (int64_t)(Eb0_bytes(idx) + free_b / 4);
-    const int64_t budget = std::max<int64_t>(std::min<int64_t>(16ll << 30, have), 1ll << 30);
-    int64_t G = (budget / (ld * 4)) / RQ_QPB * RQ_QPB;
-    G = std::max<int64_t>(RQ_QPB, std::min<int64_t>(G, round_up(nq, RQ_QPB)));
-    idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(G, nq);
-    rc = ensure_aux(idx);
-    if (rc) return rc;
-    DBuf* Eb[2] = {&idx->rE, &idx->rE2};
-    DBuf* Bb[2] = {&idx->rB, &idx->rB2};
-    for (int b = 0; b < 2; b++) {
-        HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
-        HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
-    }
-    HIPCHK(idx->ascI.ensure((size_t)nq * R * sizeof(uint64_t)));
-    HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
-    HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
-    HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
-    int64_t gi = 0;
-    for (int64_t g0 = 0; g0 < nq; g0 += G, gi++) {
-        const int F = (int)std::min<int64_t>(G, nq - g0);
-        const int b = (int)(gi & 1);
-        if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
-        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev0, s));
-        rc = rq_dist(idx, s, valid, g0, F, ld, Eb[b]->as<float>(), Bb[b]->as<float>());
+    if (nrep > 0) {
+        size_t free_b = 0, total_b = 0;
+        HIPCHK(hipMemGetInfo(&free_b, &total_b));
+        const int64_t have = (int64_t)(Eb0_bytes(idx) + free_b / 4);
+        const int64_t budget = std::max<int64_t>(std::min<int64_t>(16ll << 30, have), 1ll << 30);
+        int64_t G = (budget / (ld * 4)) / RQ_QPB * RQ_QPB;
+        G = std::max<int64_t>(RQ_QPB, std::min<int64_t>(G, round_up(nrep, RQ_QPB)));
+        if (!mfma) idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(G, nq);
+        rc = ensure_aux(idx);
         if (rc) return rc;
-        if (idx->timing && g0 == 0) HIPCHK(hipEventRecord(idx->ev1, s));
-        HIPCHK(hipEventRecord(idx->evd[b], s));
-        HIPCHK(hipStreamWaitEvent(idx->aux, idx->evd[b], 0));
-        HIPCHK(launch_replay_scan(R, (unsigned)F, idx->aux, Eb[b]->as<float>(), Bb[b]->as<float>(), valid, nslots, ld,
-                                  qlist + g0, F, R, idx->id_base, nullptr, nullptr, nullptr, 1, 0, R,
-                                  idx->ascI.as<uint64_t>() + g0 * R, idx->ascD.as<float>() + g0 * R,
-                                  idx->ascN.as<int32_t>() + g0, 0, 0, nullptr, nullptr, nullptr, 0));
-        HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
+        DBuf* Eb[2] = {&idx->rE, &idx->rE2};
+        DBuf* Bb[2] = {&idx->rB, &idx->rB2};
+        for (int b = 0; b < 2; b++) {
+            HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
+            HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+        }
+        int64_t gi = 0;
+        for (int64_t g0 = 0; g0 < nrep; g0 += G, gi++) {
+            const int F = (int)std::min<int64_t>(G, nrep - g0);
+            const int b = (int)(gi & 1);
+            if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
+            const bool time_it = idx->timing && g0 == 0 && !mfma;
+            if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
+            rc = rq_dist(idx, s, valid, g0, F, ld, Eb[b]->as<float>(), Bb[b]->as<float>(), qc, qm);
+            if (rc) return rc;
+            if (time_it) HIPCHK(hipEventRecord(idx->ev1, s));
+            HIPCHK(hipEventRecord(idx->evd[b], s));
+            HIPCHK(hipStreamWaitEvent(idx->aux, idx->evd[b], 0));
+            // rows by list position, or (flagged queries of the MFMA route) by query
+            const int64_t ao = rep_by_query ? 0 : g0;
+            HIPCHK(launch_replay_scan(R, (unsigned)F, idx->aux, Eb[b]->as<float>(), Bb[b]->as<float>(), valid, nslots, ld,
+                                      qlist + g0, F, R, idx->id_base, nullptr, nullptr, nullptr, 1, rep_by_query, R,
+                                      idx->ascI.as<uint64_t>() + ao * R, idx->ascD.as<float>() + ao * R,
+                                      idx->ascN.as<int32_t>() + ao, 0, 0, nullptr, nullptr, nullptr, 0));
+            HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
+        }
+        // join: the rescoring on s reads every group's heap
+        for (int b = 0; b < 2 && b < gi; b++) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
     }
-    // join: the rescoring on s reads every group's heap
-    for (int b = 0; b < 2 && b < gi; b++) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
+    if (mfma) idx->stats.last_group_queries = (uint64_t)nq;
+    qlist = idx->ident.as<int32_t>();
     idx->bq_nq = nq;
     idx->bq_R = R;
     rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
@@ -1938,6 +2096,7 @@ extern "C" int wv_index_rq_codes(wv_index* idx, void* out, int64_t n) {
             put_be32(c + 12, meta[s].w);
             for (int ch = 0; ch < nch; ch++)
                 memcpy(c + 16 + ch * 16, &tiled[((size_t)((s >> 8) * nch + ch) * 256 + (s & 255)) * 16], 16);
+            for (int j = 0; j < D; j++) c[16 + j] ^= 0x80;  // stored offset by 128
         }
     } else {
         std::vector<uint64_t> words((size_t)W * std::max<int64_t>(n, 1));

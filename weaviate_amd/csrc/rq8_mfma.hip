@@ -1,0 +1,452 @@
+// rq8_mfma.hip -- flat "rq-8" search on the integer matrix cores (DESIGN.md
+// §3.7b), without the B x N distance matrix.
+//
+// The reference's rq-8 distance (DistanceBetweenCompressedVectors,
+// compressionhelpers/rotational_quantization.go:294-306) is a float expression
+// of per-vector metadata and one exact integer, dotByteImpl(x, y) = sum x_i y_i
+// over the code bytes (:294).  The data codes are stored offset by 128
+// (x' = x - 128 as int8, k_rq_encode); with y' = y - 128 for the query,
+//     sum x y = sum x'y' + 128 (Sx + Sy) - 16384 D
+// exactly in int32 (|terms| < 2^31 for D <= 4096), so one
+// v_mfma_i32_16x16x64_i8 chain plus the two code sums is the reference's
+// integer bit for bit, and the epilogue is the reference's float expression
+// in its order, unfused (-ffp-contract=off).  Three kernels:
+//   k_rq8_keys  the exact rq-8 distance of every (query, row) of a 32-row
+//               block, reduced in registers to the block minimum (a NaN
+//               distance -> -inf: its block is always a candidate and the
+//               query is replayed)
+//   k_rq8_sel   wave per query: M = the (R+1)-th smallest block minimum;
+//               candidates = every block with minimum <= M -- they hold every
+//               row with distance < M and at least R+1 rows <= M
+//   k_rq8_cand  wave per query: exact distances of the candidates' rows
+//               (v_dot4_u32_u8, as k_rq8_dist), the R+1 smallest.  With no tie
+//               among them and no NaN, the reference heap's survivors
+//               (flat/index.go:470-487: the R smallest) and its pop order
+//               (descending) follow from the distances alone: the ascending
+//               list goes to ascI / ascD / ascN.  Otherwise the query is
+//               flagged and replayed exactly (k_rq8_dist + k_replay_scan).
+#pragma once
+
+namespace wv {
+
+// k_rq8_keys operands (external linkage: quant_runtime.hip launches it)
+struct RQ8Args {
+    const unsigned char* codes;  // data codes x' (256-row tiles of 16-byte chunks, rq_kernels.hip)
+    const float4* meta;          // [cap] {lower, step, step * codeSum, norm2}
+    const uint32_t* csum;        // [cap] code sums Sx
+    const uint32_t* valid;       // [cap / 32] slots to scan
+    const unsigned char* Qp;     // [nq_pad][D] query codes y' (int8), rows past nq zero
+    const float4* qmeta;         // [nq_pad]
+    const uint32_t* qcsum;       // [nq_pad] Sy
+    float* key;                  // [nq_pad][ldk] block minima
+    int64_t ldk;
+    int64_t nblk;                // 32-row blocks to scan
+    int blocks_per_span;
+    int nspans;
+    int nqg;                     // query groups of 256
+    float fl2, fcos;             // L2: 1, 0; cosine: 0, 1; dot: 0, 0 (rq_dist's)
+};
+
+namespace {
+
+// query codes of the group-tiled rq-8 layout -> Qp row q (y ^ 0x80 = y - 128
+// as int8) and the code sum; wave per query, rows [nq, nq_pad) zero
+__global__ __launch_bounds__(256) void k_rq8_qprep(const uint4* __restrict__ qcodes, int D, int64_t nq,
+                                                   int64_t nq_pad, unsigned char* __restrict__ Qp,
+                                                   uint32_t* __restrict__ qcsum) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq_pad) return;
+    const int nch = D >> 4;
+    uint32_t s = 0;
+    for (int c = lane; c < nch; c += 64) {
+        uint4 y = make_uint4(0u, 0u, 0u, 0u);
+        if (q < nq) y = qcodes[((q / RQ_QPB) * nch + c) * RQ_QPB + (q % RQ_QPB)];
+        s = __builtin_amdgcn_udot4(y.x, 0x01010101u, s, false);
+        s = __builtin_amdgcn_udot4(y.y, 0x01010101u, s, false);
+        s = __builtin_amdgcn_udot4(y.z, 0x01010101u, s, false);
+        s = __builtin_amdgcn_udot4(y.w, 0x01010101u, s, false);
+        const uint32_t X = q < nq ? 0x80808080u : 0u;
+        *reinterpret_cast<uint4*>(Qp + q * D + 16 * c) = make_uint4(y.x ^ X, y.y ^ X, y.z ^ X, y.w ^ X);
+    }
+    s = wave_sum_u32(s);
+    if (lane == 0) qcsum[q] = s;
+}
+
+__device__ __forceinline__ uint32_t rq8_lds_ld4(unsigned addr) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// k_rq8_keys<NC>: block minima of 256 queries (8 waves x 32, their codes in
+// VGPRs as B fragments) x one span of 32-row blocks, D = 64 NC.  A block's
+// codes (32 D bytes: 2 NC 1-KiB pieces, [16-byte chunk][row]), meta, code sums
+// and valid word land in an LDS ring of 3 slots by LDS-DMA two blocks ahead;
+// one barrier per block.  Per 64-column chunk: 2 A-fragment reads (row halves,
+// the next chunk's issued before this chunk's MFMAs), 4 MFMAs.  acc[m][n][r]
+// is row 16m + 4g + r (g = lane >> 4) of query 16n + (lane & 15); the C input
+// of the first chunk is 128 Sy, the epilogue adds 128 Sx - 16384 D.
+// ---------------------------------------------------------------------------
+template <int NC>
+__global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
+    constexpr int D = 64 * NC;
+    constexpr int NCH = 4 * NC;         // 16-byte chunks per row
+    constexpr int CB = 32 * D;          // code bytes per block
+    constexpr int MB = CB;              // meta: 32 x 16 B
+    constexpr int SB = CB + 512;        // code sums: 32 x 4 B
+    constexpr int VB = CB + 640;        // valid word
+    constexpr int SLOT = CB + 656;
+    constexpr int NP = 2 * NC + 3;      // wave-wide loads per block
+    constexpr int PW = (NP + 7) / 8;    // per wave (padded: every wave issues PW)
+    constexpr int NBUF = 3;
+    static_assert(SLOT % 16 == 0, "slot alignment");
+    static_assert((NC - 1) * 2048 + 256 < 65536, "ds_read offsets");
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int total = a.nqg * a.nspans;
+    const int b = blockIdx.x;
+    // XCD-aware order: the query groups of one span share an XCD (its L2)
+    const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
+    const int span = logical / a.nqg, grp = logical % a.nqg;
+    const int j = lane & 15, g = lane >> 4;
+    const int64_t q0 = (int64_t)grp * 256 + wave * 32;
+
+    // Qf[2c + n]: query q0 + 16n + j, columns 64c + 16g .. +15
+    i32x4_t Qf[2 * NC];
+    {
+        const unsigned char* qp = a.Qp + (q0 + j) * D + 16 * g;
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                Qf[2 * c + n] = *reinterpret_cast<const i32x4_t*>(qp + (int64_t)n * 16 * D + 64 * c);
+    }
+    float4 ym[2];
+    i32x4_t C0[2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        ym[n] = a.qmeta[q0 + 16 * n + j];
+        const int ky = (int)(128u * a.qcsum[q0 + 16 * n + j]);
+        C0[n] = i32x4_t{ky, ky, ky, ky};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the query loads retire before the DMA ring
+
+    const int64_t b0 = (int64_t)span * a.blocks_per_span;
+    int64_t b1 = b0 + a.blocks_per_span;
+    if (b1 > a.nblk) b1 = a.nblk;
+    const int nsteps = b1 > b0 ? (int)(b1 - b0) : 0;
+    const unsigned ring = lds_addr(rsm);
+    auto issue = [&](int t, int slot) {
+        const int64_t blk = b0 + t;
+        const int64_t T = blk >> 3;
+        const int r0 = (int)(blk & 7) * 32;
+        const unsigned sb = ring + (unsigned)(slot * SLOT);
+        static_for<0, PW>([&](auto jc) {
+            constexpr int jj = decltype(jc)::value;
+            int p = wave + 8 * jj;
+            if (p >= NP) p -= NP;  // padding: a copy of a piece another wave loads (same bytes, same place)
+            if (p < 2 * NC) {
+                const int c16 = 2 * p + (lane >> 5);
+                const unsigned char* gp = a.codes + ((T * NCH + c16) * 256 + r0 + (lane & 31)) * 16;
+                __builtin_amdgcn_global_load_lds(gp, (lds_ptr_t)(size_t)(sb + (unsigned)(p * 1024)), 16, 0, 0);
+            } else if (p == 2 * NC) {
+                if (lane < 32)
+                    __builtin_amdgcn_global_load_lds(a.meta + blk * 32 + lane, (lds_ptr_t)(size_t)(sb + MB), 16, 0, 0);
+            } else if (p == 2 * NC + 1) {
+                if (lane < 8)
+                    __builtin_amdgcn_global_load_lds(a.csum + blk * 32 + 4 * lane, (lds_ptr_t)(size_t)(sb + SB), 16, 0,
+                                                     0);
+            } else {
+                if (lane == 0)
+                    __builtin_amdgcn_global_load_lds(a.valid + blk, (lds_ptr_t)(size_t)(sb + VB), 4, 0, 0);
+            }
+        });
+    };
+    if (nsteps > 0) issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+
+    const unsigned l16 = (unsigned)(g * 512 + j * 16);
+    float* krow = a.key + (q0 + (lane & 31)) * a.ldk;
+    const float fD = (float)D;
+    const float s_ = 1.0f + a.fl2;
+    int cur = 0;
+    for (int t = 0; t < nsteps; t++) {
+        // loads and stores issued after block t's pieces: block t+1's (issued
+        // at t-1 or in the prologue) and the key stores of steps t-2, t-1
+        const int y = t == 0   ? (nsteps > 1 ? PW : 0)
+                      : t == 1 ? (nsteps > 2 ? PW : 0) + 1
+                               : (t + 1 < nsteps ? PW : 0) + 2;
+        qs_wait_vm(y);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 2 < nsteps) issue(t + 2, cur == 0 ? NBUF - 1 : cur - 1);
+        const unsigned sb = ring + (unsigned)(cur * SLOT);
+        const unsigned ab = sb + l16;
+        i32x4_t A[2][2];
+        i32x4_t acc[2][2];
+        A[0][0] = lds_ld16_o<0>(ab);
+        A[0][1] = lds_ld16_o<256>(ab);
+        static_for<0, NC>([&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            if constexpr (c + 1 < NC) {
+                A[(c + 1) & 1][0] = lds_ld16_o<(c + 1) * 2048>(ab);
+                A[(c + 1) & 1][1] = lds_ld16_o<(c + 1) * 2048 + 256>(ab);
+                qs_wait_lgkm<2>();
+            } else {
+                qs_wait_lgkm<0>();
+            }
+            asm volatile("" : "+v"(A[c & 1][0]), "+v"(A[c & 1][1]));
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < 2; m++)
+#pragma unroll
+                for (int n = 0; n < 2; n++)
+                    acc[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[c & 1][m], Qf[2 * c + n],
+                                                                      c == 0 ? C0[n] : acc[m][n], 0, 0, 0);
+        });
+        // the lane's rows 16m + 4g + r: meta, code sums; the block's valid word
+        i32x4_t mt[2][4], cs[2];
+        const unsigned mb = sb + MB + (unsigned)(g * 64);
+        mt[0][0] = lds_ld16_o<0>(mb);
+        mt[0][1] = lds_ld16_o<16>(mb);
+        mt[0][2] = lds_ld16_o<32>(mb);
+        mt[0][3] = lds_ld16_o<48>(mb);
+        mt[1][0] = lds_ld16_o<256>(mb);
+        mt[1][1] = lds_ld16_o<272>(mb);
+        mt[1][2] = lds_ld16_o<288>(mb);
+        mt[1][3] = lds_ld16_o<304>(mb);
+        const unsigned cb = sb + SB + (unsigned)(g * 16);
+        cs[0] = lds_ld16_o<0>(cb);
+        cs[1] = lds_ld16_o<64>(cb);
+        const uint32_t vw0 = rq8_lds_ld4(sb + VB);
+        qs_wait_lgkm<0>();
+        const uint32_t vw = __builtin_amdgcn_readfirstlane(vw0);
+        float p[2] = {__builtin_inff(), __builtin_inff()};
+        bool bad[2] = {false, false};
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float xl = __int_as_float(mt[m][r][0]);
+                const float xs = __int_as_float(mt[m][r][1]);
+                const float xz = __int_as_float(mt[m][r][2]);
+                const float xw = __int_as_float(mt[m][r][3]);
+                const float a1 = fD * xl;
+                const int kx = (int)(128u * (uint32_t)cs[m][r]) - 16384 * D;
+                const bool ok = (vw >> (16 * m + 4 * g + r)) & 1u;
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    const uint32_t dot = (uint32_t)(acc[m][n][r] + kx);
+                    // est = ((D lx ly + lx cy) + ly cx) + sx sy dot (the reference's order)
+                    float e1 = a1 * ym[n].x;
+                    const float e2 = xl * ym[n].z;
+                    const float e3 = ym[n].x * xz;
+                    float e4 = xs * ym[n].y;
+                    e4 = e4 * (float)dot;
+                    float est = e1 + e2;
+                    est = est + e3;
+                    est = est + e4;
+                    float tt = a.fl2 * (xw + ym[n].w);
+                    tt = tt + a.fcos;
+                    const float dist = tt - s_ * est;
+                    bad[n] = bad[n] || (ok && dist != dist);
+                    p[n] = fminf(p[n], ok ? dist : __builtin_inff());
+                }
+                __builtin_amdgcn_sched_barrier(0);  // one row at a time: bounds the live temporaries
+            }
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+            if (bad[n]) p[n] = -__builtin_inff();
+        // minimum over the 4 row groups: lanes j, j + 16, j + 32, j + 48
+        float m0 = p[0], m1 = p[1];
+        const auto a0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m0), __float_as_uint(m0), false, false);
+        const auto a1_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
+        m0 = fminf(m0, __uint_as_float(a0[1]));
+        m1 = fminf(m1, __uint_as_float(a1_[1]));
+        const auto b0_ = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m0), false, false);
+        const auto b1_ = __builtin_amdgcn_permlane16_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
+        m0 = fminf(m0, __uint_as_float(b0_[1]));
+        m1 = fminf(m1, __uint_as_float(b1_[1]));
+        // lanes 0-15: queries j (m0); lanes 16-31 take m1 (queries 16 + j)
+        const auto c01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m1), false, false);
+        if (lane < 32) krow[b0 + t] = __uint_as_float(c01[0]);
+        cur = cur == NBUF - 1 ? 0 : cur + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_rq8_sel<RT>: wave per query (4 per block).  The 64 (RT - 1) >= R + 2
+// smallest block minima (WaveTopL), M = the (R+1)-th; cand[q] = the blocks with
+// minimum <= M (a sorted prefix of the list).  oflag[q] = 1 when the list's
+// last entry is still <= M (ties at M may run past it): the query is replayed.
+// ---------------------------------------------------------------------------
+template <int RT>
+__global__ __launch_bounds__(256) void k_rq8_sel(const float* __restrict__ key, int64_t ldk, int64_t nb, int nq, int R,
+                                                 uint32_t* __restrict__ cand, int Lc, int32_t* __restrict__ ncand,
+                                                 int32_t* __restrict__ oflag) {
+    constexpr int U = 16;
+    __shared__ float sbk[4][64];
+    __shared__ uint32_t sbi[4][64];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int q = blockIdx.x * 4 + w;
+    if (q >= nq) return;
+    const float* kr = key + (int64_t)q * ldk;
+    WaveTopL<RT> t;
+    t.init();
+    for (int64_t c0 = 0; c0 < nb; c0 += 64 * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t bb = c0 + u * 64 + lane;
+            v[u] = bb < nb ? kr[bb] : __builtin_inff();
+        }
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < U; u++) any |= v[u] < t.thr;
+        if (!__any(any)) continue;
+#pragma unroll
+        for (int u = 0; u < U; u++) t.offer(v[u], (uint32_t)(c0 + u * 64 + lane), sbk[w], sbi[w], lane);
+    }
+    t.merge(sbk[w], sbi[w], lane);
+    const float M = t.key_at(R);
+    int cnt = 0;
+    bool last_in = false;
+#pragma unroll
+    for (int r = 0; r < RT - 1; r++) {
+        const bool in = t.key[r] <= M && t.key[r] < __builtin_inff();
+        const uint64_t bm = __ballot(in);
+        const int pos = cnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
+        if (in && pos < Lc) cand[(int64_t)q * Lc + pos] = t.id[r];
+        cnt += __popcll(bm);
+        if (r == RT - 2) last_in = (bm >> 63) & 1ull;
+    }
+    if (lane == 0) {
+        ncand[q] = cnt < Lc ? cnt : Lc;
+        oflag[q] = last_in ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_rq8_cand<RT>: wave per query (4 per block), skipped when k_rq8_sel flagged
+// it.  Lanes 0-31 / 32-63 take the rows of two candidate blocks at a time:
+// the exact rq-8 distance as k_rq8_dist computes it (v_dot4_u32_u8 over the
+// code bytes, the query's from LDS), offered to the wave's sorted
+// 64 (RT - 1) >= R + 1 list.  No tie among the R + 1 smallest and no NaN: the
+// R smallest ascending -> asc; else oflag[q] = 1.
+// ---------------------------------------------------------------------------
+template <int RT>
+__global__ __launch_bounds__(256) void k_rq8_cand(const uint4* __restrict__ codes, const float4* __restrict__ meta,
+                                                  const uint32_t* __restrict__ valid, int64_t nslots,
+                                                  const unsigned char* __restrict__ Qp, const float4* __restrict__ qmeta,
+                                                  int D, float fl2, float fcos, const uint32_t* __restrict__ cand, int Lc,
+                                                  const int32_t* __restrict__ ncand, int nq, int R, uint64_t id_base,
+                                                  uint64_t* __restrict__ ascI, float* __restrict__ ascD,
+                                                  int32_t* __restrict__ ascN, int32_t* __restrict__ oflag) {
+    extern __shared__ __attribute__((aligned(16))) uint4 cqs[];  // [4][D / 16] query codes (bytes y)
+    __shared__ float sbk[4][64];
+    __shared__ uint32_t sbi[4][64];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int q = blockIdx.x * 4 + w;
+    if (q >= nq) return;
+    if (oflag[q]) return;
+    const int nch = D >> 4;
+    uint4* qs = cqs + w * nch;
+    for (int c = lane; c < nch; c += 64) {
+        const uint4 y = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * D + 16 * c);
+        qs[c] = make_uint4(y.x ^ 0x80808080u, y.y ^ 0x80808080u, y.z ^ 0x80808080u, y.w ^ 0x80808080u);
+    }
+    wave_sync_lds();
+    const float4 ym = qmeta[q];
+    const float fD = (float)D;
+    const float s_ = 1.0f + fl2;
+    const int nc = ncand[q];
+    WaveTopL<RT> t;
+    t.init();
+    int nvalid = 0;
+    bool nan = false;
+    for (int i = 0; i < nc; i += 2) {
+        const int bi = i + (lane >> 5);
+        const bool has = bi < nc;
+        const uint32_t blk = has ? cand[(int64_t)q * Lc + bi] : 0u;
+        const int64_t slot = (int64_t)blk * 32 + (lane & 31);
+        const bool ok = has && slot < nslots && ((valid[blk] >> (lane & 31)) & 1u);
+        float dist = __builtin_inff();
+        if (ok) {
+            const uint4* xr = codes + ((slot >> 8) * nch) * 256 + (slot & 255);
+            uint32_t acc = 0;
+            for (int c = 0; c < nch; c++) {
+                uint4 x = xr[(int64_t)c * 256];
+                const uint4 y = qs[c];
+                acc = __builtin_amdgcn_udot4(x.x ^ 0x80808080u, y.x, acc, false);
+                acc = __builtin_amdgcn_udot4(x.y ^ 0x80808080u, y.y, acc, false);
+                acc = __builtin_amdgcn_udot4(x.z ^ 0x80808080u, y.z, acc, false);
+                acc = __builtin_amdgcn_udot4(x.w ^ 0x80808080u, y.w, acc, false);
+            }
+            const float4 xm = meta[slot];
+            float e1 = fD * xm.x;
+            e1 = e1 * ym.x;
+            const float e2 = xm.x * ym.z;
+            const float e3 = ym.x * xm.z;
+            float e4 = xm.y * ym.y;
+            e4 = e4 * (float)acc;
+            float est = e1 + e2;
+            est = est + e3;
+            est = est + e4;
+            float tt = fl2 * (xm.w + ym.w);
+            tt = tt + fcos;
+            dist = tt - s_ * est;
+            nan = nan || dist != dist;
+        }
+        nvalid += __popcll(__ballot(ok));
+        t.offer(dist, (uint32_t)slot, sbk[w], sbi[w], lane);
+    }
+    t.merge(sbk[w], sbi[w], lane);
+    const int nk = nvalid < R + 1 ? nvalid : R + 1;  // sorted entries that matter
+    bool tie = false;
+#pragma unroll
+    for (int r = 0; r < RT - 1; r++) {
+        const float nx0 = __shfl(t.key[r], (lane + 1) & 63);
+        const float nx1 = r + 1 < RT - 1 ? __shfl(t.key[r + 1 < RT - 1 ? r + 1 : r], 0) : __builtin_inff();
+        const float nx = lane < 63 ? nx0 : nx1;
+        const int e = r * 64 + lane;
+        tie = tie || (e + 1 < nk && t.key[r] == nx);
+    }
+    const bool flag = __any(tie) || __any(nan);
+    if (flag) {
+        if (lane == 0) oflag[q] = 1;
+        return;
+    }
+    const int nout = nvalid < R ? nvalid : R;
+#pragma unroll
+    for (int r = 0; r < RT - 1; r++) {
+        const int e = r * 64 + lane;
+        if (e < nout) {
+            ascI[(int64_t)q * R + e] = id_base + (uint64_t)t.id[r];
+            ascD[(int64_t)q * R + e] = t.key[r];
+        }
+    }
+    if (lane == 0) ascN[q] = nout;
+}
+
+// flagged queries' codes and meta (group-tiled rq-8 query layout) -> a
+// compact copy: entry f = query list[f]; thread per (entry, 16-byte chunk)
+__global__ void k_rq8_gather_q(const uint4* __restrict__ qcodes, const float4* __restrict__ qmeta, int nch,
+                               const int32_t* __restrict__ list, int nf, uint4* __restrict__ ocodes,
+                               float4* __restrict__ ometa) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)nf * nch) return;
+    const int f = (int)(i / nch), c = (int)(i % nch);
+    const int64_t q = list[f];
+    ocodes[((int64_t)(f / RQ_QPB) * nch + c) * RQ_QPB + f % RQ_QPB] = qcodes[((q / RQ_QPB) * nch + c) * RQ_QPB + q % RQ_QPB];
+    if (c == 0) ometa[f] = qmeta[q];
+}
+
+}  // namespace
+}  // namespace wv

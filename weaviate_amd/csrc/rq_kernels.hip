@@ -36,7 +36,8 @@ namespace {  // internal linkage: each runtime unit compiles the kernels it laun
 
 constexpr int RQ_QPB = 32;      // queries per distance block (scalar operands)
 constexpr int RQ_MAXD = 4096;   // rotation output dims supported (two LDS buffers)
-constexpr int RQ_ROUNDS = 3;    // rotationRounds (rotational_quantization.go:61, binary_...:27)
+constexpr int RQ_ROUNDS = 3;
+constexpr size_t RQ_META_B = sizeof(float4) + sizeof(uint32_t);  // per slot: meta, then (rq-8) the code sum    // rotationRounds (rotational_quantization.go:61, binary_...:27)
 
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
@@ -101,7 +102,8 @@ __global__ __launch_bounds__(256) void k_rq_encode(const float* __restrict__ row
                                                    const uint16_t* __restrict__ rot_src,
                                                    const float* __restrict__ rot_sign,
                                                    const float* __restrict__ rounding, void* __restrict__ codes,
-                                                   int64_t cap, float4* __restrict__ meta) {
+                                                   int64_t cap, float4* __restrict__ meta,
+                                                   uint32_t* __restrict__ csum_out) {
     extern __shared__ __attribute__((aligned(16))) float esm[];
     float* bufA = esm;
     float* bufB = esm + D;
@@ -149,7 +151,10 @@ __global__ __launch_bounds__(256) void k_rq_encode(const float* __restrict__ row
             }
             const int64_t o = QUERY ? ((r / RQ_QPB) * nch + c) * RQ_QPB + (r % RQ_QPB)
                                     : ((slot >> 8) * nch + c) * 256 + (slot & 255);
-            out[o] = make_uint4(w[0], w[1], w[2], w[3]);
+            // data codes are stored offset by 128 (byte x ^ 0x80 = int8 x - 128:
+            // the integer-MFMA operand of k_rq8_keys); query codes as they are
+            constexpr uint32_t X = QUERY ? 0u : 0x80808080u;
+            out[o] = make_uint4(w[0] ^ X, w[1] ^ X, w[2] ^ X, w[3] ^ X);
         }
         csum = wave_sum_u32(csum);
         if (lane == 0) redu[wv_] = csum;
@@ -163,6 +168,7 @@ __global__ __launch_bounds__(256) void k_rq_encode(const float* __restrict__ row
                 m = make_float4(lo, step, step * (float)cs, n2);
             }
             meta[slot] = m;
+            if (!QUERY && csum_out) csum_out[slot] = zero ? 0u : redu[0] + redu[1] + redu[2] + redu[3];
         }
     } else {
         const int W = D >> 6;
@@ -268,7 +274,11 @@ __global__ __launch_bounds__(256) void k_rq8_dist(const uint4* __restrict__ code
     const uint4* xr = codes + tile * nch * 256 + tid;
     const uint4* qg = qcodes + g * nch * RQ_QPB;
     for (int c = 0; c < nch; c++) {
-        const uint4 x = xr[(int64_t)c * 256];
+        uint4 x = xr[(int64_t)c * 256];
+        x.x ^= 0x80808080u;  // stored offset by 128 (k_rq_encode)
+        x.y ^= 0x80808080u;
+        x.z ^= 0x80808080u;
+        x.w ^= 0x80808080u;
         const uint4* qc = qg + c * RQ_QPB;
 #pragma unroll
         for (int q = 0; q < RQ_QPB; q++) {

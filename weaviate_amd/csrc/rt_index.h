@@ -36,6 +36,7 @@
 #include "gemv_kernels.hip"
 #include "qs_kernels.hip"
 #include "q8_kernels.hip"
+#include "rq8_mfma.hip"
 #include "sq_kernels.hip"
 
 using namespace wv;
@@ -181,7 +182,7 @@ struct wv_index {
     float* rq_sign = nullptr;     // [3][D]
     float* rq_round = nullptr;    // [D] (rq-1)
     void* rq_codes = nullptr;     // rq-8: tiled [cap][D] bytes; rq-1: [D/64][cap] u64
-    float4* rq_meta = nullptr;    // [cap]
+    float4* rq_meta = nullptr;    // [cap] meta, then (rq-8) [cap] uint32 code sums: rq_csum()
     // scalar quantizer (sq_kernels.hip): range a, b and the Go float32 constants
     int sq_ready = 0, sq_Dq = 0;
     float sq_a = 0.f, sq_b = 0.f, sq_a2 = 0.f, sq_ab = 0.f, sq_ib2 = 0.f;
@@ -252,6 +253,8 @@ struct wv_index {
     float* pq8_sb = nullptr;
     float* pq8_n2 = nullptr;
     DBuf pq8Max, pq8Mu, pq8Tmp, pq8Qc, qsCand2;
+    DBuf rq8Qp, rq8Qcs, rq8Qm, rq8Fq, rq8Fm;                  // rq-8 MFMA route: query planes, flagged queries
+    int rq_mfma = 1;                                          // option rq_mfma: rq-8 on the integer matrix cores
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
     DBuf flCtr;                      // device flag-list counters (replay_flags)
     int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
@@ -271,6 +274,8 @@ struct wv_index {
 // Add, a Delete or another batch's query preparation ends them.
 // the corpus, its buffers or the options changed: captured search graphs are stale
 static inline void note_mutation(wv_index* idx) { idx->mut_gen++; }
+// rq-8: the per-slot code sums stored behind the meta (rq_meta + cap)
+static inline uint32_t* rq_csum(wv_index* idx) { return reinterpret_cast<uint32_t*>(idx->rq_meta + idx->cap); }
 // PQ codes of slots [lo, hi) were (re)written: the int8 reconstruction plane
 // of their blocks is stale
 static inline void pq8_mark(wv_index* idx, int64_t lo, int64_t hi) {
@@ -308,7 +313,7 @@ int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float*
                uint64_t* rec_i = nullptr, float* rec_d = nullptr, int32_t* rec_n = nullptr, int rec_cap = 0);
 void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots);
 void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t ld, int64_t n, const uint32_t* d_slots,
-                      int query, void* codes, int64_t cap, float4* meta);
+                      int query, void* codes, int64_t cap, float4* meta, uint32_t* csum = nullptr);
 // qs_runtime.hip
 int qs_R(int k);
 int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid, uint64_t* o_ids,
@@ -346,4 +351,5 @@ int search_hnsw_flat(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t 
                      const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n);
 int rq_init(wv_index* idx);
 int rq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq);
-int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int F, int64_t ld, float* E, float* bmin);
+int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int F, int64_t ld, float* E, float* bmin,
+            const void* qcodes = nullptr, const float4* qmeta = nullptr);

@@ -252,7 +252,7 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     }
     if (idx->rq_ready) {
         WV_STEP("rq codes", alloc(&rqc, rq_cb));
-        WV_STEP("rq meta", alloc((void**)&rqm, (size_t)nc * sizeof(float4)));
+        WV_STEP("rq meta", alloc((void**)&rqm, (size_t)nc * RQ_META_B));
     }
     if (pq_w) WV_STEP("pq codes", alloc((void**)&pc, (size_t)pq_w * nc * sizeof(uint32_t)));
     if (idx->sq_ready) {
@@ -294,7 +294,7 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     }
     if (rqc) {
         WV_STEP("memset", hipMemsetAsync(rqc, 0, rq_cb, s));
-        WV_STEP("memset", hipMemsetAsync(rqm, 0, (size_t)nc * sizeof(float4), s));
+        WV_STEP("memset", hipMemsetAsync(rqm, 0, (size_t)nc * RQ_META_B, s));
         if (oc > 0 && idx->rq_codes) {
             if (idx->rq_bits == 8)  // tiles of 256 rows are contiguous: the old tiles are a prefix
                 WV_STEP("copy", hipMemcpyAsync(rqc, idx->rq_codes, (size_t)oc * idx->rq_D, hipMemcpyDeviceToDevice, s));
@@ -303,6 +303,9 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
                                                  (size_t)oc * sizeof(uint64_t), (size_t)oc * sizeof(uint64_t),
                                                  idx->rq_D / 64, hipMemcpyDeviceToDevice, s));
             WV_STEP("copy", hipMemcpyAsync(rqm, idx->rq_meta, (size_t)oc * sizeof(float4), hipMemcpyDeviceToDevice, s));
+            if (idx->rq_bits == 8)  // the code sums behind the meta
+                WV_STEP("copy", hipMemcpyAsync(reinterpret_cast<uint32_t*>(rqm + nc), rq_csum(idx),
+                                               (size_t)oc * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
         }
     }
     if (pc) {
@@ -406,11 +409,12 @@ void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots) {
 // rq-8 / rq-1 encode of n rows (rows[slot * ld], slot = slots[r] or r) into the
 // data layout (query = 0) or the group-tiled query layout (query = 1)
 void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t ld, int64_t n,
-                             const uint32_t* d_slots, int query, void* codes, int64_t cap, float4* meta) {
+                             const uint32_t* d_slots, int query, void* codes, int64_t cap, float4* meta,
+                             uint32_t* csum) {
     if (n <= 0) return;
     const size_t lds = 2 * (size_t)idx->rq_D * sizeof(float);
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
-#define WV_RQE(B, V, Q) k_rq_encode<B, V, Q><<<(unsigned)n, 256, lds, s>>>(rows, ld, n, idx->dims, d_slots, idx->rq_D, idx->rq_src, idx->rq_sign, idx->rq_round, codes, cap, meta)
+#define WV_RQE(B, V, Q) k_rq_encode<B, V, Q><<<(unsigned)n, 256, lds, s>>>(rows, ld, n, idx->dims, d_slots, idx->rq_D, idx->rq_src, idx->rq_sign, idx->rq_round, codes, cap, meta, csum)
     if (idx->rq_bits == 8) {
         if (query) { if (v5) WV_RQE(8, AVX512, 1); else WV_RQE(8, AVX256, 1); }
         else { if (v5) WV_RQE(8, AVX512, 0); else WV_RQE(8, AVX256, 0); }
@@ -445,7 +449,8 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
                                                                         idx->sq_Dq, idx->sq_a, idx->sq_b,
                                                                         idx->sq_codes, idx->sq_meta);
     if (idx->rq_ready)  // Preload: quantizer.EncodeBytes / EncodeUint64 of the stored row (flat/index.go:844-865)
-        launch_rq_encode(idx, idx->stream, idx->X, idx->dpad, n, d_slots, 0, idx->rq_codes, idx->cap, idx->rq_meta);
+        launch_rq_encode(idx, idx->stream, idx->X, idx->dpad, n, d_slots, 0, idx->rq_codes, idx->cap, idx->rq_meta,
+                         idx->rq_bits == 8 ? rq_csum(idx) : nullptr);
     if (idx->compression == WV_COMPRESSION_BQ) {  // Preload: quantizer.Encode of the stored row (flat/index.go:376)
         const int64_t nt = n * idx->words;
         k_bq_encode_rows<<<(unsigned)((nt + 255) / 256), 256, 0, idx->stream>>>(idx->X, idx->dpad, n, idx->dims, d_slots,
@@ -719,6 +724,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "pq8") idx->pq8_opt = value ? 1 : 0;
     else if (k == "q8_gemv") idx->q8_gemv = value ? 1 : 0;
     else if (k == "sel_split_max") idx->sel_split_max = value;
+    else if (k == "rq_mfma") idx->rq_mfma = value ? 1 : 0;
     else if (k == "exact_cap") idx->exact_cap = value ? 1 : 0;
     else if (k == "exact_filter") idx->exact_filter = value ? 1 : 0;  // 0: every candidate row gets its exact distance
     else if (k == "ef") idx->hnsw_ef = (int)value;  // hnsw UserConfig.EF (-1: dynamic)
