@@ -620,7 +620,7 @@ def test_large_k_stays_on_block_keys(wv, oracle, metric, kind, n, d, k):
     idx, orc = build_pair(wv, oracle, metric, "avx256", data)
     ids, dists, counts = idx.search_by_vector_batch(queries, k)
     route = wv._lib.ROUTES[idx.stats()["last_route"]]
-    assert route in ("qs_bf16", "qs_w4", "qs_int8"), route
+    assert route in ("qs_bf16", "qs_w4", "qs_int8", "q8_gemv"), route
     for qi in range(len(queries)):
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"q{qi}")
     idx.close()

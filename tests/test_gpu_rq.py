@@ -149,14 +149,16 @@ def test_rq_errors(wv, oracle):
     ("l2-squared", 1, 12000, 64, 20, 100, 40),  # integer data: quantized ties -> replayed queries
     ("cosine", 0, 3000, 1024, 3, 500, 20),      # D = 1024 (NC 16), R + 2 > 448: RT 16
 ])
-def test_rq8_mfma_route_equals_replay_and_oracle(wv, oracle, metric, kind, n, d, k, rescore, nq):
-    """rq-8 on the integer MFMA (k_rq8_keys -> k_rq8_sel -> k_rq8_cand, flagged
-    queries replayed) against the distance-matrix route (rq_mfma 0) over every
-    query, and the oracle on a sample, bit for bit."""
+@pytest.mark.parametrize("bits", [8, 1])
+def test_rq_mfma_route_equals_replay_and_oracle(wv, oracle, bits, metric, kind, n, d, k, rescore, nq):
+    """rq-8 / rq-1 on the integer MFMA (k_rq8_keys -> k_rq8_sel -> k_rq8_cand,
+    flagged queries replayed) against the distance-matrix route (rq_mfma 0)
+    over every query, and the oracle on a sample, bit for bit."""
     data = gen(oracle, kind, 51, n, d)
     queries = gen(oracle, kind, 52, nq, d)
     queries[1] = data[17]  # a stored vector: distance ties with itself only
-    idx, orc = build(wv, oracle, 8, metric, "avx256", data, rescore)
+    queries[2] = 0  # zero query (rq-1: RQMultiBitCode{}, dot 0)
+    idx, orc = build(wv, oracle, bits, metric, "avx256", data, rescore)
     ids, dists, counts = idx.search_by_vector_batch(queries, k)
     st = idx.stats()
     assert st["last_route"] == 10  # WV_ROUTE_RQ8_INT8
@@ -173,13 +175,14 @@ def test_rq8_mfma_route_equals_replay_and_oracle(wv, oracle, metric, kind, n, d,
     idx.close()
 
 
-def test_rq8_mfma_route_ties_deletes_allow(wv, oracle):
+@pytest.mark.parametrize("bits", [8, 1])
+def test_rq_mfma_route_ties_deletes_allow(wv, oracle, bits):
     """Identical rows tie on the quantized distance: those queries are flagged
     and replayed; deletes and allow lists mask rows inside the key pass."""
     n, d, k = 6000, 192, 10
     data = gen(oracle, 0, 61, n, d)
     data[2000:2300] = data[1999]
-    idx, orc = build(wv, oracle, 8, "l2-squared", "avx256", data, 50)
+    idx, orc = build(wv, oracle, bits, "l2-squared", "avx256", data, 50)
     dele = np.arange(3, n, 11, dtype=np.uint64)
     idx.delete(*dele)
     orc.delete(dele)

@@ -1762,6 +1762,10 @@ int rq_init(wv_index* idx) {
         HIPCHK(hipMalloc(&idx->rq_meta, (size_t)idx->cap * RQ_META_B));
         HIPCHK(hipMemset(idx->rq_codes, 0, cb));
         HIPCHK(hipMemset(idx->rq_meta, 0, (size_t)idx->cap * RQ_META_B));
+        if (idx->rq_bits == 1) {
+            HIPCHK(hipMalloc(&idx->rq1_pm, (size_t)idx->cap * D));
+            HIPCHK(hipMemset(idx->rq1_pm, 0, (size_t)idx->cap * D));
+        }
     }
     return WV_OK;
 }
@@ -1802,17 +1806,26 @@ int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int
     return WV_OK;
 }
 
-// rq-8 on the integer matrix cores (rq8_mfma.hip): the query fragments stay
-// in VGPRs up to D = 1024; the candidate lists hold R + 2 entries
+// rq-8 / rq-1 on the integer matrix cores (rq8_mfma.hip): the query
+// fragments stay in VGPRs up to D = 1024; the candidate lists hold R + 2
+// entries; rq-1 needs its +-1 plane
 static bool rq8_route(const wv_index* idx, int R) {
-    return idx->rq_bits == 8 && idx->rq_mfma && idx->rq_D <= 1024 && qs_R(R + 1) != 0 && idx->hiwater > 0;
+    return (idx->rq_bits == 8 || (idx->rq_bits == 1 && idx->rq1_pm)) && idx->rq_mfma && idx->rq_D <= 1024 &&
+           qs_R(R + 1) != 0 && idx->hiwater > 0;
 }
 
 template <int NC>
-static void launch_rq8_keys(const RQ8Args& a, unsigned grid, hipStream_t s) {
-    constexpr size_t lds = 3 * ((size_t)32 * 64 * NC + 656);
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_rq8_keys<NC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    k_rq8_keys<NC><<<grid, 512, lds, s>>>(a);
+static void launch_rq8_keys(const RQ8Args& a, unsigned grid, hipStream_t s, int bits) {
+    constexpr size_t lds = 4 * ((size_t)32 * 64 * NC + 656);  // NBUF slots (k_rq8_keys)
+    if (bits == 8) {
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute((const void*)k_rq8_keys<NC, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        k_rq8_keys<NC, 8><<<grid, 512, lds, s>>>(a);
+    } else {
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute((const void*)k_rq8_keys<NC, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        k_rq8_keys<NC, 1><<<grid, 512, lds, s>>>(a);
+    }
 }
 
 // exact rq-8 block minima -> candidate blocks -> exact distances of their
@@ -1839,12 +1852,18 @@ static int rq8_candidates(wv_index* idx, hipStream_t s, int64_t nq, int R, const
     float4* Qm = idx->rq8Qm.as<float4>();
     HIPCHK(hipMemsetAsync(Qm, 0, (size_t)nq_pad * sizeof(float4), s));
     HIPCHK(hipMemcpyAsync(Qm, idx->rqm.p, (size_t)nq * sizeof(float4), hipMemcpyDeviceToDevice, s));
-    k_rq8_qprep<<<(unsigned)(nq_pad / 4), 256, 0, s>>>(idx->rqq.as<uint4>(), D, nq, nq_pad, Qp, Qcs);
+    const int bits = idx->rq_bits;
+    if (bits == 8) {
+        k_rq8_qprep<<<(unsigned)(nq_pad / 4), 256, 0, s>>>(idx->rqq.as<uint4>(), D, nq, nq_pad, Qp, Qcs);
+    } else {
+        const int64_t nt = nq_pad * (D / 16);
+        k_rq1_qprep<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(idx->rqq.as<uint64_t>(), Qm, D, nq, nq_pad, Qp);
+    }
     HIPCHK(hipGetLastError());
     const float fl2 = idx->metric == WV_METRIC_L2_SQUARED ? 1.f : 0.f;
     const float fcos = idx->metric == WV_METRIC_COSINE_DOT ? 1.f : 0.f;
     RQ8Args a{};
-    a.codes = reinterpret_cast<const unsigned char*>(idx->rq_codes);
+    a.codes = bits == 8 ? reinterpret_cast<const unsigned char*>(idx->rq_codes) : idx->rq1_pm;
     a.meta = idx->rq_meta;
     a.csum = rq_csum(idx);
     a.valid = valid;
@@ -1853,6 +1872,9 @@ static int rq8_candidates(wv_index* idx, hipStream_t s, int64_t nq, int R, const
     a.nblk = nblk;
     a.fl2 = fl2;
     a.fcos = fcos;
+    a.dbg_serial = idx->rq_serial;
+    idx->rq_dbg_nq = std::min<int64_t>(QC, nq);
+    idx->rq_dbg_nb = nblk;
     for (int64_t c0 = 0; c0 < nq; c0 += QC) {
         const int64_t cn = std::min<int64_t>(QC, nq - c0);
         const int64_t cpad = round_up(cn, 256);
@@ -1870,22 +1892,22 @@ static int rq8_candidates(wv_index* idx, hipStream_t s, int64_t nq, int R, const
         const bool time_it = idx->timing && c0 == 0;
         if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
         switch (NC) {
-        case 1: launch_rq8_keys<1>(a, grid, s); break;
-        case 2: launch_rq8_keys<2>(a, grid, s); break;
-        case 3: launch_rq8_keys<3>(a, grid, s); break;
-        case 4: launch_rq8_keys<4>(a, grid, s); break;
-        case 5: launch_rq8_keys<5>(a, grid, s); break;
-        case 6: launch_rq8_keys<6>(a, grid, s); break;
-        case 7: launch_rq8_keys<7>(a, grid, s); break;
-        case 8: launch_rq8_keys<8>(a, grid, s); break;
-        case 9: launch_rq8_keys<9>(a, grid, s); break;
-        case 10: launch_rq8_keys<10>(a, grid, s); break;
-        case 11: launch_rq8_keys<11>(a, grid, s); break;
-        case 12: launch_rq8_keys<12>(a, grid, s); break;
-        case 13: launch_rq8_keys<13>(a, grid, s); break;
-        case 14: launch_rq8_keys<14>(a, grid, s); break;
-        case 15: launch_rq8_keys<15>(a, grid, s); break;
-        default: launch_rq8_keys<16>(a, grid, s); break;
+        case 1: launch_rq8_keys<1>(a, grid, s, bits); break;
+        case 2: launch_rq8_keys<2>(a, grid, s, bits); break;
+        case 3: launch_rq8_keys<3>(a, grid, s, bits); break;
+        case 4: launch_rq8_keys<4>(a, grid, s, bits); break;
+        case 5: launch_rq8_keys<5>(a, grid, s, bits); break;
+        case 6: launch_rq8_keys<6>(a, grid, s, bits); break;
+        case 7: launch_rq8_keys<7>(a, grid, s, bits); break;
+        case 8: launch_rq8_keys<8>(a, grid, s, bits); break;
+        case 9: launch_rq8_keys<9>(a, grid, s, bits); break;
+        case 10: launch_rq8_keys<10>(a, grid, s, bits); break;
+        case 11: launch_rq8_keys<11>(a, grid, s, bits); break;
+        case 12: launch_rq8_keys<12>(a, grid, s, bits); break;
+        case 13: launch_rq8_keys<13>(a, grid, s, bits); break;
+        case 14: launch_rq8_keys<14>(a, grid, s, bits); break;
+        case 15: launch_rq8_keys<15>(a, grid, s, bits); break;
+        default: launch_rq8_keys<16>(a, grid, s, bits); break;
         }
         HIPCHK(hipGetLastError());
         if (time_it) HIPCHK(hipEventRecord(idx->ev1, s));
@@ -1893,24 +1915,111 @@ static int rq8_candidates(wv_index* idx, hipStream_t s, int64_t nq, int R, const
         uint32_t* cand = idx->qsCand.as<uint32_t>() + c0 * Lc;
         int32_t* ncand = idx->qsNc.as<int32_t>() + c0;
         int32_t* of = idx->oF.as<int32_t>() + c0;
-        const size_t lq = (size_t)4 * D;
+        const size_t lq = (size_t)4 * (bits == 8 ? D : (5 * (D / 64) + 1) / 2 * 16);
+        const void* qsrc = bits == 8 ? (const void*)a.Qp : idx->rqq.p;
+#define WV_RQC(RTV, B)                                                                                                \
+    k_rq8_cand<RTV, B><<<gw, 256, lq, s>>>(idx->rq_codes, idx->cap, idx->rq_meta, valid, idx->hiwater, qsrc, c0,       \
+                                           a.qmeta, D, fl2, fcos, cand, Lc, ncand, (int)cn, R, idx->id_base,           \
+                                           idx->ascI.as<uint64_t>() + c0 * R, idx->ascD.as<float>() + c0 * R,         \
+                                           idx->ascN.as<int32_t>() + c0, of)
 #define WV_RQ8(RTV)                                                                                                   \
     do {                                                                                                              \
         k_rq8_sel<RTV><<<gw, 256, 0, s>>>(a.key, nblk, nblk, (int)cn, R, cand, Lc, ncand, of);                        \
-        k_rq8_cand<RTV><<<gw, 256, lq, s>>>(reinterpret_cast<const uint4*>(idx->rq_codes), idx->rq_meta, valid,        \
-                                            idx->hiwater, a.Qp, a.qmeta, D, fl2, fcos, cand, Lc, ncand, (int)cn, R,    \
-                                            idx->id_base, idx->ascI.as<uint64_t>() + c0 * R,                           \
-                                            idx->ascD.as<float>() + c0 * R, idx->ascN.as<int32_t>() + c0, of);         \
+        if (bits == 8) WV_RQC(RTV, 8);                                                                                 \
+        else WV_RQC(RTV, 1);                                                                                           \
     } while (0)
         if (RT == 2) WV_RQ8(2);
         else if (RT == 4) WV_RQ8(4);
         else if (RT == 8) WV_RQ8(8);
         else WV_RQ8(16);
 #undef WV_RQ8
+#undef WV_RQC
         HIPCHK(hipGetLastError());
     }
     idx->stats.mfma_launches++;
     idx->stats.last_route = WV_ROUTE_RQ8_INT8;
+    return WV_OK;
+}
+
+// the R-heap replay of searchByVectorQuantized for nrep queries: every query
+// (list == nullptr: asc rows by query index) or the listed ones (their codes
+// compacted into groups of RQ_QPB first, asc rows by query): exact quantized
+// distances + block minima (k_rq*_dist), the heap replayed in id order
+// (k_replay_scan).  Query groups: multiples of RQ_QPB, two distance buffers
+// of up to 16 GiB each (a quarter of the free HBM at most); group i's
+// distances (stream s) overlap group i-1's replay (stream aux).
+static int rq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int R, const int32_t* list, int64_t nrep) {
+    const void* qc = nullptr;
+    const float4* qm = nullptr;
+    if (list) {
+        const int64_t nf32 = round_up(nrep, RQ_QPB);
+        if (idx->rq_bits == 1) {
+            const int ne = 5 * (idx->rq_D / 64);
+            HIPCHK(idx->rq8Fq.ensure((size_t)nf32 * ne * sizeof(uint64_t)));
+            HIPCHK(idx->rq8Fm.ensure((size_t)nf32 * sizeof(float4)));
+            HIPCHK(hipMemsetAsync(idx->rq8Fq.p, 0, (size_t)nf32 * ne * sizeof(uint64_t), s));
+            HIPCHK(hipMemsetAsync(idx->rq8Fm.p, 0, (size_t)nf32 * sizeof(float4), s));
+            const int64_t nt = nrep * ne;
+            k_rq1_gather_q<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(idx->rqq.as<uint64_t>(), idx->rqm.as<float4>(), ne,
+                                                                         list, (int)nrep, idx->rq8Fq.as<uint64_t>(),
+                                                                         idx->rq8Fm.as<float4>());
+        } else {
+            const int nch = idx->rq_D / 16;
+            HIPCHK(idx->rq8Fq.ensure((size_t)nf32 * idx->rq_D));
+            HIPCHK(idx->rq8Fm.ensure((size_t)nf32 * sizeof(float4)));
+            HIPCHK(hipMemsetAsync(idx->rq8Fq.p, 0, (size_t)nf32 * idx->rq_D, s));
+            HIPCHK(hipMemsetAsync(idx->rq8Fm.p, 0, (size_t)nf32 * sizeof(float4), s));
+            const int64_t nt = nrep * nch;
+            k_rq8_gather_q<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(idx->rqq.as<uint4>(), idx->rqm.as<float4>(), nch,
+                                                                         list, (int)nrep, idx->rq8Fq.as<uint4>(),
+                                                                         idx->rq8Fm.as<float4>());
+        }
+        HIPCHK(hipGetLastError());
+        qc = idx->rq8Fq.p;
+        qm = idx->rq8Fm.as<float4>();
+    }
+    const int32_t* qlist = list ? list : idx->ident.as<int32_t>();
+    const int rep_by_query = list ? 1 : 0;
+    idx->stats.replayed_queries += (uint64_t)nrep;
+    const int64_t nslots = idx->hiwater;
+    const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const int64_t have = (int64_t)(Eb0_bytes(idx) + free_b / 4);
+    const int64_t budget = std::max<int64_t>(std::min<int64_t>(16ll << 30, have), 1ll << 30);
+    int64_t G = (budget / (ld * 4)) / RQ_QPB * RQ_QPB;
+    G = std::max<int64_t>(RQ_QPB, std::min<int64_t>(G, round_up(nrep, RQ_QPB)));
+    if (!list) idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(G, nrep);
+    int rc = ensure_aux(idx);
+    if (rc) return rc;
+    DBuf* Eb[2] = {&idx->rE, &idx->rE2};
+    DBuf* Bb[2] = {&idx->rB, &idx->rB2};
+    for (int b = 0; b < 2; b++) {
+        HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
+        HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
+    }
+    int64_t gi = 0;
+    for (int64_t g0 = 0; g0 < nrep; g0 += G, gi++) {
+        const int F = (int)std::min<int64_t>(G, nrep - g0);
+        const int b = (int)(gi & 1);
+        if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
+        const bool time_it = idx->timing && g0 == 0 && !list;
+        if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
+        rc = rq_dist(idx, s, valid, g0, F, ld, Eb[b]->as<float>(), Bb[b]->as<float>(), qc, qm);
+        if (rc) return rc;
+        if (time_it) HIPCHK(hipEventRecord(idx->ev1, s));
+        HIPCHK(hipEventRecord(idx->evd[b], s));
+        HIPCHK(hipStreamWaitEvent(idx->aux, idx->evd[b], 0));
+        // asc rows by list position (every query, in order) or by query
+        const int64_t ao = rep_by_query ? 0 : g0;
+        HIPCHK(launch_replay_scan(R, (unsigned)F, idx->aux, Eb[b]->as<float>(), Bb[b]->as<float>(), valid, nslots, ld,
+                                  qlist + g0, F, R, idx->id_base, nullptr, nullptr, nullptr, 1, rep_by_query, R,
+                                  idx->ascI.as<uint64_t>() + ao * R, idx->ascD.as<float>() + ao * R,
+                                  idx->ascN.as<int32_t>() + ao, 0, 0, nullptr, nullptr, nullptr, 0));
+        HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
+    }
+    // join: the rescoring on s reads every group's heap
+    for (int b = 0; b < 2 && b < gi; b++) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
     return WV_OK;
 }
 
@@ -1947,97 +2056,55 @@ int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
     HIPCHK(idx->ascD.ensure((size_t)nq * R * sizeof(float)));
     HIPCHK(idx->ascN.ensure((size_t)nq * sizeof(int32_t)));
     HIPCHK(idx->candE.ensure((size_t)nq * R * sizeof(float)));
-    const int32_t* qlist = idx->ident.as<int32_t>();
-    int64_t nrep = nq;
-    int rep_by_query = 0;
-    const void* qc = nullptr;
-    const float4* qm = nullptr;
     const bool mfma = rq8_route(idx, R);
-    if (mfma) {
-        rc = rq8_candidates(idx, s, nq, R, valid);
-        if (rc) return rc;
-        HIPCHK(idx->qsList.ensure((size_t)nq * sizeof(int32_t)));
-        HIPCHK(idx->flCtr.ensure(2 * sizeof(uint32_t)));
-        HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
-        k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq,
-                                                                  idx->qsList.as<int32_t>(), idx->flCtr.as<uint32_t>(), 0);
-        HIPCHK(hipGetLastError());
-        uint32_t nf = 0;
-        HIPCHK(hipMemcpyAsync(&nf, idx->flCtr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        nrep = nf;
-        rep_by_query = 1;
-        qlist = idx->qsList.as<int32_t>();
-        if (nf > 0) {  // the flagged queries' codes, compacted into groups of RQ_QPB
-            const int nch = idx->rq_D / 16;
-            const int64_t nf32 = round_up((int64_t)nf, RQ_QPB);
-            HIPCHK(idx->rq8Fq.ensure((size_t)nf32 * idx->rq_D));
-            HIPCHK(idx->rq8Fm.ensure((size_t)nf32 * sizeof(float4)));
-            HIPCHK(hipMemsetAsync(idx->rq8Fq.p, 0, (size_t)nf32 * idx->rq_D, s));
-            HIPCHK(hipMemsetAsync(idx->rq8Fm.p, 0, (size_t)nf32 * sizeof(float4), s));
-            const int64_t nt = (int64_t)nf * nch;
-            k_rq8_gather_q<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(idx->rqq.as<uint4>(), idx->rqm.as<float4>(), nch,
-                                                                         qlist, (int)nf, idx->rq8Fq.as<uint4>(),
-                                                                         idx->rq8Fm.as<float4>());
-            HIPCHK(hipGetLastError());
-            qc = idx->rq8Fq.p;
-            qm = idx->rq8Fm.as<float4>();
-        }
-    }
-    idx->stats.replayed_queries += (uint64_t)nrep;
-    const int64_t nslots = idx->hiwater;
-    const int64_t ld = std::max<int64_t>(round_up(nslots, EBLK), EBLK);
-    // query groups: multiples of RQ_QPB, two distance buffers of up to
-    // 16 GiB each (a quarter of the free HBM at most).  A replay wave's time
-    // does not shrink with the group (one wave per query), so groups are as
-    // large as memory allows.  Group i's distances (whole GPU, stream s)
-    // overlap group i-1's replay (stream aux); buffer i&1 is reused once
-    // replay i-2 has finished with it.
-    if (nrep > 0) {
-        size_t free_b = 0, total_b = 0;
-        HIPCHK(hipMemGetInfo(&free_b, &total_b));
-        const int64_t have = (int64_t)(Eb0_bytes(idx) + free_b / 4);
-        const int64_t budget = std::max<int64_t>(std::min<int64_t>(16ll << 30, have), 1ll << 30);
-        int64_t G = (budget / (ld * 4)) / RQ_QPB * RQ_QPB;
-        G = std::max<int64_t>(RQ_QPB, std::min<int64_t>(G, round_up(nrep, RQ_QPB)));
-        if (!mfma) idx->stats.last_group_queries = (uint64_t)std::min<int64_t>(G, nq);
-        rc = ensure_aux(idx);
-        if (rc) return rc;
-        DBuf* Eb[2] = {&idx->rE, &idx->rE2};
-        DBuf* Bb[2] = {&idx->rB, &idx->rB2};
-        for (int b = 0; b < 2; b++) {
-            HIPCHK(Eb[b]->ensure((size_t)G * ld * sizeof(float)));
-            HIPCHK(Bb[b]->ensure((size_t)G * (ld / EBLK) * sizeof(float)));
-        }
-        int64_t gi = 0;
-        for (int64_t g0 = 0; g0 < nrep; g0 += G, gi++) {
-            const int F = (int)std::min<int64_t>(G, nrep - g0);
-            const int b = (int)(gi & 1);
-            if (gi >= 2) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
-            const bool time_it = idx->timing && g0 == 0 && !mfma;
-            if (time_it) HIPCHK(hipEventRecord(idx->ev0, s));
-            rc = rq_dist(idx, s, valid, g0, F, ld, Eb[b]->as<float>(), Bb[b]->as<float>(), qc, qm);
-            if (rc) return rc;
-            if (time_it) HIPCHK(hipEventRecord(idx->ev1, s));
-            HIPCHK(hipEventRecord(idx->evd[b], s));
-            HIPCHK(hipStreamWaitEvent(idx->aux, idx->evd[b], 0));
-            // rows by list position, or (flagged queries of the MFMA route) by query
-            const int64_t ao = rep_by_query ? 0 : g0;
-            HIPCHK(launch_replay_scan(R, (unsigned)F, idx->aux, Eb[b]->as<float>(), Bb[b]->as<float>(), valid, nslots, ld,
-                                      qlist + g0, F, R, idx->id_base, nullptr, nullptr, nullptr, 1, rep_by_query, R,
-                                      idx->ascI.as<uint64_t>() + ao * R, idx->ascD.as<float>() + ao * R,
-                                      idx->ascN.as<int32_t>() + ao, 0, 0, nullptr, nullptr, nullptr, 0));
-            HIPCHK(hipEventRecord(idx->evr[b], idx->aux));
-        }
-        // join: the rescoring on s reads every group's heap
-        for (int b = 0; b < 2 && b < gi; b++) HIPCHK(hipStreamWaitEvent(s, idx->evr[b], 0));
-    }
-    if (mfma) idx->stats.last_group_queries = (uint64_t)nq;
-    qlist = idx->ident.as<int32_t>();
     idx->bq_nq = nq;
     idx->bq_R = R;
-    rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
-    if (rc) return rc;
+    if (!mfma) {
+        rc = rq_replay(idx, s, valid, R, nullptr, nq);
+        if (rc) return rc;
+        rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
+        if (rc) return rc;
+    } else {
+        rc = rq8_candidates(idx, s, nq, R, valid);
+        if (rc) return rc;
+        idx->stats.last_group_queries = (uint64_t)nq;
+        // oF: 1 = replay now, 2 = decided after the rescoring (k_rq_tiecheck)
+        HIPCHK(idx->qsList.ensure((size_t)2 * nq * sizeof(int32_t)));
+        HIPCHK(idx->flCtr.ensure(4 * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 4 * sizeof(uint32_t), s));
+        int32_t* list1 = idx->qsList.as<int32_t>();
+        int32_t* list2 = list1 + nq;
+        uint32_t* ctr = idx->flCtr.as<uint32_t>();
+        const unsigned gl = (unsigned)((nq + 255) / 256);
+        k_flag_list<<<gl, 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq, list1, ctr, 1);
+        k_flag_list<<<gl, 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq, list2, ctr + 2, 2);
+        HIPCHK(hipGetLastError());
+        uint32_t cnt[4] = {0, 0, 0, 0};
+        HIPCHK(hipMemcpyAsync(cnt, ctr, sizeof(cnt), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (cnt[1] > 0) {
+            rc = rq_replay(idx, s, valid, R, list1, cnt[1]);
+            if (rc) return rc;
+        }
+        rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
+        if (rc) return rc;
+        if (cnt[3] > 0) {  // ties among the quantized distances inside the R: ties among the rescored ones too?
+            k_rq_tiecheck<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(idx->candE.as<float>(), idx->ascN.as<int32_t>(),
+                                                                   (int)nq, R, idx->oF.as<int32_t>());
+            HIPCHK(hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), s));
+            k_flag_list<<<gl, 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq, list1, ctr, 3);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(cnt, ctr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (cnt[1] > 0) {
+                rc = rq_replay(idx, s, valid, R, list1, cnt[1]);
+                if (rc) return rc;
+                rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
+                if (rc) return rc;
+            }
+        }
+    }
+    const int32_t* qlist = idx->ident.as<int32_t>();
     const size_t lds_f = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
     if (lds_f > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_bq_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
@@ -2082,6 +2149,17 @@ extern "C" int wv_index_rq_codes(wv_index* idx, void* out, int64_t n) {
     const int D = idx->rq_D, W = D / 64;
     std::vector<float4> meta((size_t)std::max<int64_t>(n, 1));
     if (n) HIPCHK(hipMemcpy(meta.data(), idx->rq_meta, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
+    if (idx->rq_bits == 1 && idx->rq_serial == 16 && idx->rq1_pm) {  // debug: the +-1 plane, de-tiled [n][D]
+        const int64_t ntile = (n + 255) / 256;
+        std::vector<uint8_t> tiled((size_t)ntile * 256 * D);
+        if (n) HIPCHK(hipMemcpy(tiled.data(), idx->rq1_pm, tiled.size(), hipMemcpyDeviceToHost));
+        const int nch = D / 16;
+        for (int64_t s2 = 0; s2 < n; s2++)
+            for (int ch = 0; ch < nch; ch++)
+                memcpy((uint8_t*)out + (size_t)s2 * D + ch * 16,
+                       &tiled[((size_t)((s2 >> 8) * nch + ch) * 256 + (s2 & 255)) * 16], 16);
+        return WV_OK;
+    }
     if (idx->rq_bits == 8) {
         const int64_t ntile = (n + 255) / 256;
         std::vector<uint8_t> tiled((size_t)std::max<int64_t>(ntile * 256 * D, 1));

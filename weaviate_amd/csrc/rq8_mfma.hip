@@ -45,6 +45,7 @@ struct RQ8Args {
     int nspans;
     int nqg;                     // query groups of 256
     float fl2, fcos;             // L2: 1, 0; cosine: 0, 1; dot: 0, 0 (rq_dist's)
+    int dbg_serial;              // debug option rq_serial: one block in flight, drained before each barrier
 };
 
 namespace {
@@ -73,6 +74,35 @@ __global__ __launch_bounds__(256) void k_rq8_qprep(const uint4* __restrict__ qco
     if (lane == 0) qcsum[q] = s;
 }
 
+// rq-1 query planes (group-tiled, 5 per 64-bit word) -> Qp row q: per dim
+// w_i = sum_p 2^p (1 - 2 bit_pi) = 31 - 2 c_i (c_i the 5-bit code), or 0 for a
+// query encoded as zero (qmeta.z == 0: the reference's dot is 0 then); thread
+// per (query, 16 dims)
+__global__ void k_rq1_qprep(const uint64_t* __restrict__ planes, const float4* __restrict__ qmeta, int D,
+                            int64_t nq, int64_t nq_pad, unsigned char* __restrict__ Qp) {
+    const int nch = D >> 4, W = D >> 6;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq_pad * nch) return;
+    const int64_t q = i / nch;
+    const int c = (int)(i % nch);
+    uint32_t wd[4] = {0u, 0u, 0u, 0u};
+    if (q < nq && qmeta[q].z != 0.f) {
+        const int w = c >> 2, sh = 16 * (c & 3);
+        uint32_t pl[5];
+#pragma unroll
+        for (int p = 0; p < 5; p++)
+            pl[p] = (uint32_t)(planes[(((q / RQ_QPB) * W + w) * 5 + p) * RQ_QPB + (q % RQ_QPB)] >> sh) & 0xFFFFu;
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            int cc = 0;
+#pragma unroll
+            for (int p = 0; p < 5; p++) cc |= (int)((pl[p] >> b) & 1u) << p;
+            wd[b >> 2] |= (uint32_t)(unsigned char)(signed char)(31 - 2 * cc) << (8 * (b & 3));
+        }
+    }
+    *reinterpret_cast<uint4*>(Qp + q * D + 16 * c) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+}
+
 __device__ __forceinline__ uint32_t rq8_lds_ld4(unsigned addr) {
     uint32_t v;
     asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
@@ -89,7 +119,7 @@ __device__ __forceinline__ uint32_t rq8_lds_ld4(unsigned addr) {
 // is row 16m + 4g + r (g = lane >> 4) of query 16n + (lane & 15); the C input
 // of the first chunk is 128 Sy, the epilogue adds 128 Sx - 16384 D.
 // ---------------------------------------------------------------------------
-template <int NC>
+template <int NC, int BITS>
 __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
     constexpr int D = 64 * NC;
     constexpr int NCH = 4 * NC;         // 16-byte chunks per row
@@ -100,7 +130,7 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
     constexpr int SLOT = CB + 656;
     constexpr int NP = 2 * NC + 3;      // wave-wide loads per block
     constexpr int PW = (NP + 7) / 8;    // per wave (padded: every wave issues PW)
-    constexpr int NBUF = 3;
+    constexpr int NBUF = 4;  // a late wave reads block t-1's meta while block t+2 lands
     static_assert(SLOT % 16 == 0, "slot alignment");
     static_assert((NC - 1) * 2048 + 256 < 65536, "ds_read offsets");
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
@@ -115,6 +145,7 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
     const int span = logical / a.nqg, grp = logical % a.nqg;
     const int j = lane & 15, g = lane >> 4;
     const int64_t q0 = (int64_t)grp * 256 + wave * 32;
+    static_assert(BITS == 8 || BITS == 1, "rq-8 or rq-1");
 
     // Qf[2c + n]: query q0 + 16n + j, columns 64c + 16g .. +15
     i32x4_t Qf[2 * NC];
@@ -131,9 +162,15 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
 #pragma unroll
     for (int n = 0; n < 2; n++) {
         ym[n] = a.qmeta[q0 + 16 * n + j];
-        const int ky = (int)(128u * a.qcsum[q0 + 16 * n + j]);
+        const int ky = BITS == 8 ? (int)(128u * a.qcsum[q0 + 16 * n + j]) : 0;
         C0[n] = i32x4_t{ky, ky, ky, ky};
     }
+    // the fast epilogue: every product of the reference's expression stays far
+    // from overflow when both squared norms are <= 1e16 (|components| <= 1e8),
+    // so no NaN can arise, and 0 (n2x + n2y) + fcos == fcos for cosine / dot
+    constexpr float FINE = 1e16f;
+    const bool qfine = BITS == 8 ? (ym[0].w <= FINE && ym[1].w <= FINE) : (ym[0].y <= FINE && ym[1].y <= FINE);
+    const bool l2 = a.fl2 != 0.f;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the query loads retire before the DMA ring
 
     const int64_t b0 = (int64_t)span * a.blocks_per_span;
@@ -167,28 +204,24 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
             }
         });
     };
+    const int ahead = (a.dbg_serial & 1) ? 1 : 2;
     if (nsteps > 0) issue(0, 0);
-    if (nsteps > 1) issue(1, 1);
+    if (nsteps > 1 && ahead == 2) issue(1, 1);
 
     const unsigned l16 = (unsigned)(g * 512 + j * 16);
     float* krow = a.key + (q0 + (lane & 31)) * a.ldk;
     const float fD = (float)D;
     const float s_ = 1.0f + a.fl2;
-    int cur = 0;
-    for (int t = 0; t < nsteps; t++) {
-        // loads and stores issued after block t's pieces: block t+1's (issued
-        // at t-1 or in the prologue) and the key stores of steps t-2, t-1
-        const int y = t == 0   ? (nsteps > 1 ? PW : 0)
-                      : t == 1 ? (nsteps > 2 ? PW : 0) + 1
-                               : (t + 1 < nsteps ? PW : 0) + 2;
-        qs_wait_vm(y);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 2 < nsteps) issue(t + 2, cur == 0 ? NBUF - 1 : cur - 1);
-        const unsigned sb = ring + (unsigned)(cur * SLOT);
+    // Waves 4-7 (each the SIMD partner of wave w - 4) run block t-1's
+    // epilogue before block t's MFMAs instead of after them, so the two
+    // waves of a SIMD alternate MFMA and VALU phases (MI355X_MICROARCH.md, two
+    // waves per SIMD: a stagger) instead of issuing both at once.
+    const bool late = wave >= 4 && !(a.dbg_serial & 2);
+    i32x4_t acc[2][2];
+    float pend = 0.f;  // an early wave's key of the previous block, stored after the next barrier
+    auto mfma_block = [&](unsigned sb) {
         const unsigned ab = sb + l16;
         i32x4_t A[2][2];
-        i32x4_t acc[2][2];
         A[0][0] = lds_ld16_o<0>(ab);
         A[0][1] = lds_ld16_o<256>(ab);
         static_for<0, NC>([&](auto cc) {
@@ -209,6 +242,10 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
                     acc[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[c & 1][m], Qf[2 * c + n],
                                                                       c == 0 ? C0[n] : acc[m][n], 0, 0, 0);
         });
+    };
+    // a block's epilogue (its meta in slot sb, its sums in acc) -> the lane's
+    // key of it (lanes 0-31)
+    auto epilogue = [&](unsigned sb) -> float {
         // the lane's rows 16m + 4g + r: meta, code sums; the block's valid word
         i32x4_t mt[2][4], cs[2];
         const unsigned mb = sb + MB + (unsigned)(g * 64);
@@ -223,60 +260,122 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
         const unsigned cb = sb + SB + (unsigned)(g * 16);
         cs[0] = lds_ld16_o<0>(cb);
         cs[1] = lds_ld16_o<64>(cb);
-        const uint32_t vw0 = rq8_lds_ld4(sb + VB);
+        uint32_t vw0 = rq8_lds_ld4(sb + VB);
         qs_wait_lgkm<0>();
+        // the loaded registers are defined only after the wait: tie them to it,
+        // or the compiler may schedule their uses above it
+        asm volatile("" : "+v"(mt[0][0]), "+v"(mt[0][1]), "+v"(mt[0][2]), "+v"(mt[0][3]), "+v"(vw0));
+        asm volatile("" : "+v"(mt[1][0]), "+v"(mt[1][1]), "+v"(mt[1][2]), "+v"(mt[1][3]));
+        asm volatile("" : "+v"(cs[0]), "+v"(cs[1]));
         const uint32_t vw = __builtin_amdgcn_readfirstlane(vw0);
         float p[2] = {__builtin_inff(), __builtin_inff()};
         bool bad[2] = {false, false};
-#pragma unroll
+        // the fast forms: every row valid, every norm <= FINE (wave-uniform);
+        // l2: (1 (n2x + n2y) + 0) - 2 est, cosine / dot: (0 (..) + fcos) - 1 est
+        bool fine = qfine;
+    #pragma unroll
         for (int m = 0; m < 2; m++)
-#pragma unroll
+    #pragma unroll
+            for (int r = 0; r < 4; r++) fine = fine && __int_as_float(mt[m][r][BITS == 8 ? 3 : 1]) <= FINE;
+        const int mode = (vw == 0xFFFFFFFFu && __all(fine) && !(a.dbg_serial & 4)) ? (l2 ? 0 : 1) : 2;
+    #pragma unroll
+        for (int m = 0; m < 2; m++)
+    #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const float xl = __int_as_float(mt[m][r][0]);
-                const float xs = __int_as_float(mt[m][r][1]);
-                const float xz = __int_as_float(mt[m][r][2]);
-                const float xw = __int_as_float(mt[m][r][3]);
-                const float a1 = fD * xl;
-                const int kx = (int)(128u * (uint32_t)cs[m][r]) - 16384 * D;
                 const bool ok = (vw >> (16 * m + 4 * g + r)) & 1u;
-#pragma unroll
-                for (int n = 0; n < 2; n++) {
-                    const uint32_t dot = (uint32_t)(acc[m][n][r] + kx);
+                float est[2], xnorm;
+                if constexpr (BITS == 8) {
                     // est = ((D lx ly + lx cy) + ly cx) + sx sy dot (the reference's order)
-                    float e1 = a1 * ym[n].x;
-                    const float e2 = xl * ym[n].z;
-                    const float e3 = ym[n].x * xz;
-                    float e4 = xs * ym[n].y;
-                    e4 = e4 * (float)dot;
-                    float est = e1 + e2;
-                    est = est + e3;
-                    est = est + e4;
-                    float tt = a.fl2 * (xw + ym[n].w);
-                    tt = tt + a.fcos;
-                    const float dist = tt - s_ * est;
-                    bad[n] = bad[n] || (ok && dist != dist);
-                    p[n] = fminf(p[n], ok ? dist : __builtin_inff());
+                    const float xl = __int_as_float(mt[m][r][0]);
+                    const float xs = __int_as_float(mt[m][r][1]);
+                    const float xz = __int_as_float(mt[m][r][2]);
+                    xnorm = __int_as_float(mt[m][r][3]);
+                    const float a1 = fD * xl;
+                    const int kx = (int)(128u * (uint32_t)cs[m][r]) - 16384 * D;
+    #pragma unroll
+                    for (int n = 0; n < 2; n++) {
+                        const uint32_t dot = (uint32_t)(acc[m][n][r] + kx);
+                        float e1 = a1 * ym[n].x;
+                        const float e2 = xl * ym[n].z;
+                        const float e3 = ym[n].x * xz;
+                        float e4 = xs * ym[n].y;
+                        e4 = e4 * (float)dot;
+                        float e = e1 + e2;
+                        e = e + e3;
+                        est[n] = e + e4;
+                    }
+                } else {
+                    // rq-1 (BinaryRQDistancer.Distance, binary_rotational_quantization.go:364-385):
+                    // acc = sum s_x w_q = 31 qdim - sum_p 2^(p+1) popcount(x ^ plane_p) exactly
+                    const float xs = __int_as_float(mt[m][r][0]);
+                    xnorm = __int_as_float(mt[m][r][1]);
+    #pragma unroll
+                    for (int n = 0; n < 2; n++) {
+                        const float e = ym[n].x * xs;
+                        est[n] = e * (float)acc[m][n][r];
+                    }
+                }
+    #pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    const float yn = BITS == 8 ? ym[n].w : ym[n].y;
+                    if (mode == 0) {
+                        p[n] = fminf(p[n], (xnorm + yn) - 2.0f * est[n]);
+                    } else if (mode == 1) {
+                        p[n] = fminf(p[n], a.fcos - est[n]);
+                    } else {
+                        float tt = a.fl2 * (xnorm + yn);
+                        tt = tt + a.fcos;
+                        const float dist = tt - s_ * est[n];
+                        bad[n] = bad[n] || (ok && dist != dist);
+                        p[n] = fminf(p[n], ok ? dist : __builtin_inff());
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);  // one row at a time: bounds the live temporaries
             }
-#pragma unroll
+    #pragma unroll
         for (int n = 0; n < 2; n++)
             if (bad[n]) p[n] = -__builtin_inff();
         // minimum over the 4 row groups: lanes j, j + 16, j + 32, j + 48
+        // (ds_bpermute, which the compiler's hazard and wait tracking covers)
         float m0 = p[0], m1 = p[1];
-        const auto a0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m0), __float_as_uint(m0), false, false);
-        const auto a1_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
-        m0 = fminf(m0, __uint_as_float(a0[1]));
-        m1 = fminf(m1, __uint_as_float(a1_[1]));
-        const auto b0_ = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m0), false, false);
-        const auto b1_ = __builtin_amdgcn_permlane16_swap(__float_as_uint(m1), __float_as_uint(m1), false, false);
-        m0 = fminf(m0, __uint_as_float(b0_[1]));
-        m1 = fminf(m1, __uint_as_float(b1_[1]));
-        // lanes 0-15: queries j (m0); lanes 16-31 take m1 (queries 16 + j)
-        const auto c01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m0), __float_as_uint(m1), false, false);
-        if (lane < 32) krow[b0 + t] = __uint_as_float(c01[0]);
-        cur = cur == NBUF - 1 ? 0 : cur + 1;
+        m0 = fminf(m0, __shfl_xor(m0, 32));
+        m1 = fminf(m1, __shfl_xor(m1, 32));
+        m0 = fminf(m0, __shfl_xor(m0, 16));
+        m1 = fminf(m1, __shfl_xor(m1, 16));
+        // lanes 0-15: queries j (m0); lanes 16-31: queries 16 + j (m1)
+        return (lane & 16) ? m1 : m0;
+    };
+    for (int t = 0; t <= nsteps; t++) {
+        const int cur = t & (NBUF - 1);
+        if (t < nsteps) {
+            // block t's pieces landed: the loads issued after them are block
+            // t+1's (loads retire in order).  Key stores are not counted (one
+            // retiring before older loads would cut the wait short); one still
+            // in flight only lengthens it.
+            qs_wait_vm(t + 1 < nsteps && ahead == 2 ? PW : 0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (!late && t > 0 && lane < 32) krow[b0 + t - 1] = pend;
+            if (ahead == 2) {
+                if (t + 2 < nsteps) issue(t + 2, (t + 2) & (NBUF - 1));
+            } else if (t + 1 < nsteps) {
+                issue(t + 1, (t + 1) & (NBUF - 1));
+            }
+        }
+        if (!late) {
+            if (t < nsteps) {
+                mfma_block(ring + (unsigned)(cur * SLOT));
+                pend = epilogue(ring + (unsigned)(cur * SLOT));
+            }
+        } else {
+            if (t > 0) {
+                const float kv = epilogue(ring + (unsigned)(((t - 1) & (NBUF - 1)) * SLOT));
+                if (lane < 32) krow[b0 + t - 1] = kv;
+            }
+            if (t < nsteps) mfma_block(ring + (unsigned)(cur * SLOT));
+        }
     }
+    if (!late && nsteps > 0 && lane < 32) krow[b0 + nsteps - 1] = pend;
 }
 
 // ---------------------------------------------------------------------------
@@ -340,15 +439,20 @@ __global__ __launch_bounds__(256) void k_rq8_sel(const float* __restrict__ key, 
 // 64 (RT - 1) >= R + 1 list.  No tie among the R + 1 smallest and no NaN: the
 // R smallest ascending -> asc; else oflag[q] = 1.
 // ---------------------------------------------------------------------------
-template <int RT>
-__global__ __launch_bounds__(256) void k_rq8_cand(const uint4* __restrict__ codes, const float4* __restrict__ meta,
-                                                  const uint32_t* __restrict__ valid, int64_t nslots,
-                                                  const unsigned char* __restrict__ Qp, const float4* __restrict__ qmeta,
-                                                  int D, float fl2, float fcos, const uint32_t* __restrict__ cand, int Lc,
+// BITS = 1: rq-1's exact distance as k_rq1_dist computes it (xor + popcount of
+// the word-major bit codes against the 5 query planes, copied to LDS from
+// the group-tiled layout; query q of this launch is q_base + q there).
+template <int RT, int BITS>
+__global__ __launch_bounds__(256) void k_rq8_cand(const void* __restrict__ codes_, int64_t cap,
+                                                  const float4* __restrict__ meta, const uint32_t* __restrict__ valid,
+                                                  int64_t nslots, const void* __restrict__ qsrc, int64_t q_base,
+                                                  const float4* __restrict__ qmeta, int D, float fl2, float fcos,
+                                                  const uint32_t* __restrict__ cand, int Lc,
                                                   const int32_t* __restrict__ ncand, int nq, int R, uint64_t id_base,
                                                   uint64_t* __restrict__ ascI, float* __restrict__ ascD,
                                                   int32_t* __restrict__ ascN, int32_t* __restrict__ oflag) {
-    extern __shared__ __attribute__((aligned(16))) uint4 cqs[];  // [4][D / 16] query codes (bytes y)
+    // [4][D / 16] query code bytes (rq-8) or [4][5 W] planes (rq-1)
+    extern __shared__ __attribute__((aligned(16))) uint4 cqs[];
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
     const int lane = threadIdx.x & 63;
@@ -356,11 +460,20 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const uint4* __restrict__ code
     const int q = blockIdx.x * 4 + w;
     if (q >= nq) return;
     if (oflag[q]) return;
-    const int nch = D >> 4;
-    uint4* qs = cqs + w * nch;
-    for (int c = lane; c < nch; c += 64) {
-        const uint4 y = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * D + 16 * c);
-        qs[c] = make_uint4(y.x ^ 0x80808080u, y.y ^ 0x80808080u, y.z ^ 0x80808080u, y.w ^ 0x80808080u);
+    const int nch = D >> 4, W = D >> 6;
+    uint4* qs = cqs + w * (BITS == 8 ? nch : (5 * W + 1) / 2);
+    uint64_t* qpl = reinterpret_cast<uint64_t*>(qs);
+    if constexpr (BITS == 8) {
+        const unsigned char* Qp = reinterpret_cast<const unsigned char*>(qsrc);
+        for (int c = lane; c < nch; c += 64) {
+            const uint4 y = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * D + 16 * c);
+            qs[c] = make_uint4(y.x ^ 0x80808080u, y.y ^ 0x80808080u, y.z ^ 0x80808080u, y.w ^ 0x80808080u);
+        }
+    } else {
+        const uint64_t* planes = reinterpret_cast<const uint64_t*>(qsrc);
+        const int64_t gq = q_base + q;
+        for (int e = lane; e < 5 * W; e += 64)  // e = 5 w + p
+            qpl[e] = planes[((gq / RQ_QPB) * W * 5 + e) * RQ_QPB + gq % RQ_QPB];
     }
     wave_sync_lds();
     const float4 ym = qmeta[q];
@@ -378,7 +491,31 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const uint4* __restrict__ code
         const int64_t slot = (int64_t)blk * 32 + (lane & 31);
         const bool ok = has && slot < nslots && ((valid[blk] >> (lane & 31)) & 1u);
         float dist = __builtin_inff();
-        if (ok) {
+        if (BITS == 1 && ok) {
+            const uint64_t* codes = reinterpret_cast<const uint64_t*>(codes_);
+            uint32_t acc = 0;
+            for (int wd = 0; wd < W; wd++) {
+                const uint64_t x = codes[(int64_t)wd * cap + slot];
+                const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+#pragma unroll
+                for (int p = 0; p < 5; p++) {
+                    const uint64_t y = qpl[5 * wd + p];
+                    uint32_t h = __builtin_popcount(xl ^ (uint32_t)y);
+                    h += __builtin_popcount(xh ^ (uint32_t)(y >> 32));
+                    acc += h << (p + 1);
+                }
+            }
+            const int qdim = (int)ym.z;
+            const int dot = qdim > 0 ? 31 * qdim - (int)acc : 0;
+            const float4 xm = meta[slot];
+            float est = ym.x * xm.x;
+            est = est * (float)dot;
+            float tt = fl2 * (xm.y + ym.y);
+            tt = tt + fcos;
+            dist = tt - s_ * est;
+            nan = nan || dist != dist;
+        } else if (BITS == 8 && ok) {
+            const uint4* codes = reinterpret_cast<const uint4*>(codes_);
             const uint4* xr = codes + ((slot >> 8) * nch) * 256 + (slot & 255);
             uint32_t acc = 0;
             for (int c = 0; c < nch; c++) {
@@ -408,21 +545,28 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const uint4* __restrict__ code
         t.offer(dist, (uint32_t)slot, sbk[w], sbi[w], lane);
     }
     t.merge(sbk[w], sbi[w], lane);
+    // a tie at the boundary (the R-th and (R+1)-th smallest) leaves the heap's
+    // survivors to its insertion order: replayed (1).  A tie inside the R
+    // leaves only their pop order open, which matters to the k-heap of the
+    // rescored distances only if those tie as well: checked after the
+    // rescoring (2, k_rq_tiecheck).
     const int nk = nvalid < R + 1 ? nvalid : R + 1;  // sorted entries that matter
-    bool tie = false;
+    bool tie_b = false, tie_i = false;
 #pragma unroll
     for (int r = 0; r < RT - 1; r++) {
         const float nx0 = __shfl(t.key[r], (lane + 1) & 63);
         const float nx1 = r + 1 < RT - 1 ? __shfl(t.key[r + 1 < RT - 1 ? r + 1 : r], 0) : __builtin_inff();
         const float nx = lane < 63 ? nx0 : nx1;
         const int e = r * 64 + lane;
-        tie = tie || (e + 1 < nk && t.key[r] == nx);
+        const bool eq = e + 1 < nk && t.key[r] == nx;
+        tie_b = tie_b || (eq && e + 1 == R);
+        tie_i = tie_i || (eq && e + 1 < R);
     }
-    const bool flag = __any(tie) || __any(nan);
-    if (flag) {
+    if (__any(tie_b) || __any(nan)) {
         if (lane == 0) oflag[q] = 1;
         return;
     }
+    const bool tie_in = __any(tie_i);
     const int nout = nvalid < R ? nvalid : R;
 #pragma unroll
     for (int r = 0; r < RT - 1; r++) {
@@ -432,7 +576,32 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const uint4* __restrict__ code
             ascD[(int64_t)q * R + e] = t.key[r];
         }
     }
-    if (lane == 0) ascN[q] = nout;
+    if (lane == 0) {
+        ascN[q] = nout;
+        if (tie_in) oflag[q] = 2;
+    }
+}
+
+// queries k_rq8_cand left at 2 (equal quantized distances inside the R): a
+// tie among their rescored distances (or a NaN) makes the k-heap's result
+// depend on the pop order of the equal quantized ones -> 3 (replayed), else 0.
+// Wave per query; lists longer than 2048 are replayed without the check.
+__global__ __launch_bounds__(256) void k_rq_tiecheck(const float* __restrict__ candE, const int32_t* __restrict__ cnt,
+                                                     int nq, int R, int32_t* __restrict__ oflag) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq || oflag[q] != 2) return;
+    const int n = cnt[q];
+    const float* e = candE + (int64_t)q * R;
+    bool dup = n > 2048;
+    for (int i = lane; i < n && !dup; i += 64) {
+        const float v = e[i];
+        if (v != v) { dup = true; break; }
+        for (int j = i + 1; j < n; j++)
+            if (e[j] == v) { dup = true; break; }
+    }
+    const bool any = __any(dup);
+    if (lane == 0) oflag[q] = any ? 3 : 0;
 }
 
 // flagged queries' codes and meta (group-tiled rq-8 query layout) -> a
@@ -446,6 +615,19 @@ __global__ void k_rq8_gather_q(const uint4* __restrict__ qcodes, const float4* _
     const int64_t q = list[f];
     ocodes[((int64_t)(f / RQ_QPB) * nch + c) * RQ_QPB + f % RQ_QPB] = qcodes[((q / RQ_QPB) * nch + c) * RQ_QPB + q % RQ_QPB];
     if (c == 0) ometa[f] = qmeta[q];
+}
+
+// as k_rq8_gather_q for rq-1's planes: ne = 5 W u64 per query, group-tiled
+// ((g * ne + e) * RQ_QPB + q % RQ_QPB); thread per (entry, word)
+__global__ void k_rq1_gather_q(const uint64_t* __restrict__ planes, const float4* __restrict__ qmeta, int ne,
+                               const int32_t* __restrict__ list, int nf, uint64_t* __restrict__ oplanes,
+                               float4* __restrict__ ometa) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)nf * ne) return;
+    const int f = (int)(i / ne), e = (int)(i % ne);
+    const int64_t q = list[f];
+    oplanes[((int64_t)(f / RQ_QPB) * ne + e) * RQ_QPB + f % RQ_QPB] = planes[((q / RQ_QPB) * ne + e) * RQ_QPB + q % RQ_QPB];
+    if (e == 0) ometa[f] = qmeta[q];
 }
 
 }  // namespace

@@ -103,7 +103,8 @@ __global__ __launch_bounds__(256) void k_rq_encode(const float* __restrict__ row
                                                    const float* __restrict__ rot_sign,
                                                    const float* __restrict__ rounding, void* __restrict__ codes,
                                                    int64_t cap, float4* __restrict__ meta,
-                                                   uint32_t* __restrict__ csum_out) {
+                                                   uint32_t* __restrict__ csum_out,
+                                                   unsigned char* __restrict__ pm_out) {
     extern __shared__ __attribute__((aligned(16))) float esm[];
     float* bufA = esm;
     float* bufB = esm + D;
@@ -179,6 +180,23 @@ __global__ __launch_bounds__(256) void k_rq_encode(const float* __restrict__ row
                 for (int j = 0; j < 64; j++)
                     if (rx[w * 64 + j] > 0.f) bits |= 1ull << j;
                 out[(int64_t)w * cap + slot] = bits;
+            }
+            // the +-1 plane of the same bits (integer-MFMA operand of
+            // k_rq8_keys<.., 1>): byte 1 - 2 bit, tiled as the rq-8 codes
+            if (pm_out) {
+                const int nch = D >> 4;
+                for (int c = tid; c < nch; c += 256) {
+                    uint32_t wd[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++) {
+                        uint32_t word = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; b++) word |= (rx[c * 16 + jj * 4 + b] > 0.f ? 0xFFu : 0x01u) << (8 * b);
+                        wd[jj] = word;
+                    }
+                    reinterpret_cast<uint4*>(pm_out)[((slot >> 8) * nch + c) * 256 + (slot & 255)] =
+                        make_uint4(wd[0], wd[1], wd[2], wd[3]);
+                }
             }
             if (tid == 0) {  // sequential l1 / l2 (:165-176)
                 float l2 = 0.f, l1 = 0.f;

@@ -166,6 +166,7 @@ struct wv_index {
     uint64_t replayed_host = 0;     // replays counted on the host (legacy paths)
     int timed = 0;                  // ev0/ev1 bracket the last batch's dominant kernel
     int timed_total = 0;            // evt0/evt1 bracket the last batch's whole block-key pipeline
+    int64_t rq_dbg_nq = 0, rq_dbg_nb = 0;  // first chunk of the last rq MFMA batch (debug hook)
     int64_t qs_last_nq = 0, qs_last_nb = 0, qs_last_ldk = 0;  // first chunk of the last block-key batch (debug hook)
     // > 0: the block keys / eps / query planes of the last search (nq queries,
     // one chunk, no allow list) still describe the stored rows -- the
@@ -182,6 +183,7 @@ struct wv_index {
     float* rq_sign = nullptr;     // [3][D]
     float* rq_round = nullptr;    // [D] (rq-1)
     void* rq_codes = nullptr;     // rq-8: tiled [cap][D] bytes; rq-1: [D/64][cap] u64
+    unsigned char* rq1_pm = nullptr;  // rq-1: the +-1 plane of the codes, tiled [cap][D] bytes (k_rq8_keys<.., 1>)
     float4* rq_meta = nullptr;    // [cap] meta, then (rq-8) [cap] uint32 code sums: rq_csum()
     // scalar quantizer (sq_kernels.hip): range a, b and the Go float32 constants
     int sq_ready = 0, sq_Dq = 0;
@@ -254,7 +256,8 @@ struct wv_index {
     float* pq8_n2 = nullptr;
     DBuf pq8Max, pq8Mu, pq8Tmp, pq8Qc, qsCand2;
     DBuf rq8Qp, rq8Qcs, rq8Qm, rq8Fq, rq8Fm;                  // rq-8 MFMA route: query planes, flagged queries
-    int rq_mfma = 1;                                          // option rq_mfma: rq-8 on the integer matrix cores
+    int rq_mfma = 1;
+    int rq_serial = 0;                                        // option rq_serial (debug): k_rq8_keys without the DMA lookahead                                          // option rq_mfma: rq-8 on the integer matrix cores
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
     DBuf flCtr;                      // device flag-list counters (replay_flags)
     int64_t qs_phase_nq = 0;         // sharded phase 1 done for this batch size
@@ -313,7 +316,8 @@ int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float*
                uint64_t* rec_i = nullptr, float* rec_d = nullptr, int32_t* rec_n = nullptr, int rec_cap = 0);
 void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots);
 void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t ld, int64_t n, const uint32_t* d_slots,
-                      int query, void* codes, int64_t cap, float4* meta, uint32_t* csum = nullptr);
+                      int query, void* codes, int64_t cap, float4* meta, uint32_t* csum = nullptr,
+                      unsigned char* pm = nullptr);
 // qs_runtime.hip
 int qs_R(int k);
 int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid, uint64_t* o_ids,

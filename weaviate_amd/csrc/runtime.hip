@@ -188,7 +188,8 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->sb8) hipFree(idx->sb8);
     if (idx->qmax8) hipFree(idx->qmax8);
     if (idx->qscount) hipFree(idx->qscount);
-    for (void* p : {(void*)idx->rq_src, (void*)idx->rq_sign, (void*)idx->rq_round, idx->rq_codes, (void*)idx->rq_meta})
+    for (void* p : {(void*)idx->rq_src, (void*)idx->rq_sign, (void*)idx->rq_round, idx->rq_codes, (void*)idx->rq_meta,
+                    (void*)idx->rq1_pm})
         if (p) hipFree(p);
     if (idx->ev0) hipEventDestroy(idx->ev0);
     if (idx->ev1) hipEventDestroy(idx->ev1);
@@ -226,6 +227,7 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     unsigned char* b8 = nullptr;
     void* rqc = nullptr;
     float4* rqm = nullptr;
+    unsigned char* rpm = nullptr;
     uint32_t* pc = nullptr;
     uint4* sqc = nullptr;
     uint2* sqmt = nullptr;
@@ -253,6 +255,7 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     if (idx->rq_ready) {
         WV_STEP("rq codes", alloc(&rqc, rq_cb));
         WV_STEP("rq meta", alloc((void**)&rqm, (size_t)nc * RQ_META_B));
+        if (idx->rq_bits == 1) WV_STEP("rq-1 +-1 plane", alloc((void**)&rpm, (size_t)nc * idx->rq_D));
     }
     if (pq_w) WV_STEP("pq codes", alloc((void**)&pc, (size_t)pq_w * nc * sizeof(uint32_t)));
     if (idx->sq_ready) {
@@ -295,6 +298,11 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
     if (rqc) {
         WV_STEP("memset", hipMemsetAsync(rqc, 0, rq_cb, s));
         WV_STEP("memset", hipMemsetAsync(rqm, 0, (size_t)nc * RQ_META_B, s));
+        if (rpm) {  // 256-row tiles: the old tiles are a prefix
+            WV_STEP("memset", hipMemsetAsync(rpm, 0, (size_t)nc * idx->rq_D, s));
+            if (oc > 0 && idx->rq1_pm)
+                WV_STEP("copy", hipMemcpyAsync(rpm, idx->rq1_pm, (size_t)oc * idx->rq_D, hipMemcpyDeviceToDevice, s));
+        }
         if (oc > 0 && idx->rq_codes) {
             if (idx->rq_bits == 8)  // tiles of 256 rows are contiguous: the old tiles are a prefix
                 WV_STEP("copy", hipMemcpyAsync(rqc, idx->rq_codes, (size_t)oc * idx->rq_D, hipMemcpyDeviceToDevice, s));
@@ -347,6 +355,7 @@ static int ensure_capacity(wv_index* idx, int64_t need) {
         if (idx->rq_codes) hipFree(idx->rq_codes);
         idx->rq_codes = rqc;
         swap_in(idx->rq_meta, rqm);
+        swap_in(idx->rq1_pm, rpm);
     }
     swap_in(idx->pq_codes, pc);
     swap_in(idx->sq_codes, sqc);
@@ -410,11 +419,11 @@ void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots) {
 // data layout (query = 0) or the group-tiled query layout (query = 1)
 void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t ld, int64_t n,
                              const uint32_t* d_slots, int query, void* codes, int64_t cap, float4* meta,
-                             uint32_t* csum) {
+                             uint32_t* csum, unsigned char* pm) {
     if (n <= 0) return;
     const size_t lds = 2 * (size_t)idx->rq_D * sizeof(float);
     const bool v5 = idx->variant == WV_VARIANT_AVX512;
-#define WV_RQE(B, V, Q) k_rq_encode<B, V, Q><<<(unsigned)n, 256, lds, s>>>(rows, ld, n, idx->dims, d_slots, idx->rq_D, idx->rq_src, idx->rq_sign, idx->rq_round, codes, cap, meta, csum)
+#define WV_RQE(B, V, Q) k_rq_encode<B, V, Q><<<(unsigned)n, 256, lds, s>>>(rows, ld, n, idx->dims, d_slots, idx->rq_D, idx->rq_src, idx->rq_sign, idx->rq_round, codes, cap, meta, csum, pm)
     if (idx->rq_bits == 8) {
         if (query) { if (v5) WV_RQE(8, AVX512, 1); else WV_RQE(8, AVX256, 1); }
         else { if (v5) WV_RQE(8, AVX512, 0); else WV_RQE(8, AVX256, 0); }
@@ -450,7 +459,7 @@ static void launch_prepare(wv_index* idx, const float* d_in, int64_t n, const ui
                                                                         idx->sq_codes, idx->sq_meta);
     if (idx->rq_ready)  // Preload: quantizer.EncodeBytes / EncodeUint64 of the stored row (flat/index.go:844-865)
         launch_rq_encode(idx, idx->stream, idx->X, idx->dpad, n, d_slots, 0, idx->rq_codes, idx->cap, idx->rq_meta,
-                         idx->rq_bits == 8 ? rq_csum(idx) : nullptr);
+                         idx->rq_bits == 8 ? rq_csum(idx) : nullptr, idx->rq1_pm);
     if (idx->compression == WV_COMPRESSION_BQ) {  // Preload: quantizer.Encode of the stored row (flat/index.go:376)
         const int64_t nt = n * idx->words;
         k_bq_encode_rows<<<(unsigned)((nt + 255) / 256), 256, 0, idx->stream>>>(idx->X, idx->dpad, n, idx->dims, d_slots,
@@ -725,6 +734,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "q8_gemv") idx->q8_gemv = value ? 1 : 0;
     else if (k == "sel_split_max") idx->sel_split_max = value;
     else if (k == "rq_mfma") idx->rq_mfma = value ? 1 : 0;
+    else if (k == "rq_serial") idx->rq_serial = (int)value;
     else if (k == "exact_cap") idx->exact_cap = value ? 1 : 0;
     else if (k == "exact_filter") idx->exact_filter = value ? 1 : 0;  // 0: every candidate row gets its exact distance
     else if (k == "ef") idx->hnsw_ef = (int)value;  // hnsw UserConfig.EF (-1: dynamic)
@@ -802,6 +812,16 @@ extern "C" int wv_index_debug_blockkeys(wv_index* idx, int64_t q, float* A, floa
     if (!idx || !nb) return set_err(WV_ERR_INVALID, "nil argument");
     std::lock_guard<std::mutex> g(idx->mu);
     HIPCHK(hipSetDevice(idx->device));
+    if (idx->stats.last_route == WV_ROUTE_RQ8_INT8) {  // rq: the exact 32-row minima themselves, eps 0
+        if (q < 0 || q >= idx->rq_dbg_nq) return set_err(WV_ERR_INVALID, "debug_blockkeys: no such query");
+        *nb = idx->rq_dbg_nb;
+        if (!A) return WV_OK;
+        HIPCHK(hipStreamSynchronize(idx->stream));
+        HIPCHK(hipMemcpy(A, idx->qsKey.as<float>() + q * idx->rq_dbg_nb, (size_t)idx->rq_dbg_nb * sizeof(float),
+                         hipMemcpyDeviceToHost));
+        if (eps) *eps = 0.f;
+        return WV_OK;
+    }
     if (idx->qs_last_nq <= 0 || q < 0 || q >= idx->qs_last_nq)
         return set_err(WV_ERR_INVALID, "debug_blockkeys: no such query in the last block-key batch");
     *nb = idx->qs_last_nb;
