@@ -1,26 +1,16 @@
-"""Summaries of bench runs: `kstats.py BENCH.json KERNEL_STATS.csv [label]` prints
-the bench line's QPS / step / dominant kernel / roofline and the top kernels of
-the rocprofv3 kernel_stats.csv; `kstats.py CSV...` prints each CSV."""
+"""Top kernels of a rocprofv3 --stats kernel_stats.csv (or every one under a
+directory): total ms, calls, average us."""
 import csv
-import json
+import glob
+import os
 import sys
 
-
-def stats(path, top=14):
-    for x in list(csv.DictReader(open(path)))[:top]:
-        print(f"    {x['Name'][:66]:66s} {x['Calls']:>5s} avg_ms={float(x['AverageNs'])/1e6:9.4f} pct={float(x['Percentage']):6.2f}")
-
-
-args = sys.argv[1:]
-if args and args[0].endswith(".json"):
-    r = json.load(open(args[0]))
-    ro = r.get("roofline", {})
-    print("variant", args[2] if len(args) > 2 else "-", "qps", round(r["value"]), "ms", round(r["ms_per_step"], 2),
-          "key", ro.get("kernel"), round(ro.get("launch_ms", 0) or 0, 2), "frac", round(ro.get("frac", 0) or 0, 3),
-          "verified", r.get("verified"), "replayed", r["config"].get("replayed_queries"))
-    if len(args) > 1:
-        stats(args[1])
-else:
-    for p in args:
-        print("==", p)
-        stats(p, 1000)
+paths = []
+for a in sys.argv[1:] or ["gpurun_out"]:
+    paths += [a] if a.endswith(".csv") else glob.glob(os.path.join(a, "**", "*kernel_stats.csv"), recursive=True)
+for p in paths:
+    rows = sorted(csv.DictReader(open(p)), key=lambda r: -float(r["TotalDurationNs"]))
+    print(p)
+    for r in rows[:16]:
+        print(f'  {float(r["TotalDurationNs"]) / 1e6:9.2f} ms  n={int(r["Calls"]):>5}  avg={float(r["AverageNs"]) / 1e3:9.1f} us'
+              f'  {r["Name"][:100]}')

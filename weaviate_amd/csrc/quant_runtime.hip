@@ -1816,7 +1816,7 @@ static bool rq8_route(const wv_index* idx, int R) {
 
 template <int NC>
 static void launch_rq8_keys(const RQ8Args& a, unsigned grid, hipStream_t s, int bits) {
-    constexpr size_t lds = 4 * ((size_t)32 * 64 * NC + 656);  // NBUF slots (k_rq8_keys)
+    constexpr size_t lds = (size_t)rq8_nbuf(NC) * ((size_t)32 * 64 * NC + 656);  // the ring (k_rq8_keys)
     if (bits == 8) {
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute((const void*)k_rq8_keys<NC, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2023,6 +2023,35 @@ static int rq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int R,
     return WV_OK;
 }
 
+// the listed queries' R-heaps replayed from the MFMA route's exact 32-row
+// minima (k_rq8_replay), when the last rq8_candidates kept every query's keys
+// (one query chunk); else the distance-matrix replay (rq_replay)
+static int rq8_replay_list(wv_index* idx, hipStream_t s, const uint32_t* valid, int R, const int32_t* list,
+                           int64_t n, int64_t nq) {
+    if (idx->rq_dbg_nq != nq || idx->rq_serial == 8) return rq_replay(idx, s, valid, R, list, n);
+    idx->stats.replayed_queries += (uint64_t)n;
+    const int D = idx->rq_D;
+    const int64_t nblk = idx->rq_dbg_nb;
+    const float fl2 = idx->metric == WV_METRIC_L2_SQUARED ? 1.f : 0.f;
+    const float fcos = idx->metric == WV_METRIC_COSINE_DOT ? 1.f : 0.f;
+    const size_t lds = rq8_replay_lds(R, rq_query_lds_u4(idx->rq_bits, D));
+    const bool b8 = idx->rq_bits == 8;
+    const void* fn = b8 ? (const void*)k_rq8_replay<8> : (const void*)k_rq8_replay<1>;
+    if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const void* qsrc = b8 ? (const void*)idx->rq8Qp.p : idx->rqq.p;
+#define WV_RQR(B)                                                                                                  \
+    k_rq8_replay<B><<<(unsigned)n, 512, lds, s>>>(idx->qsKey.as<float>(), nblk, nblk, idx->rq_codes, idx->cap,      \
+                                                 idx->rq_meta, valid, idx->hiwater, qsrc, 0, idx->rq8Qm.as<float4>(), \
+                                                 D, fl2, fcos, list, (int)n, R, idx->id_base,                      \
+                                                 idx->ascI.as<uint64_t>(), idx->ascD.as<float>(),                  \
+                                                 idx->ascN.as<int32_t>())
+    if (b8) WV_RQR(8);
+    else WV_RQR(1);
+#undef WV_RQR
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
 // flat.searchByVectorQuantized (flat/index.go:460-532) for rq-8 / rq-1: the
 // worker R-heap fed in id order (addResult == insertToHeap, :470-487),
 // extracted ascending (reversed pop order), fp32 rescoring of those
@@ -2083,21 +2112,21 @@ int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
         HIPCHK(hipMemcpyAsync(cnt, ctr, sizeof(cnt), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (cnt[1] > 0) {
-            rc = rq_replay(idx, s, valid, R, list1, cnt[1]);
+            rc = rq8_replay_list(idx, s, valid, R, list1, cnt[1], nq);
             if (rc) return rc;
         }
         rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
         if (rc) return rc;
         if (cnt[3] > 0) {  // ties among the quantized distances inside the R: ties among the rescored ones too?
             k_rq_tiecheck<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(idx->candE.as<float>(), idx->ascN.as<int32_t>(),
-                                                                   (int)nq, R, idx->oF.as<int32_t>());
+                                                                   (int)nq, R, k, idx->oF.as<int32_t>());
             HIPCHK(hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), s));
             k_flag_list<<<gl, 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq, list1, ctr, 3);
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(cnt, ctr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             if (cnt[1] > 0) {
-                rc = rq_replay(idx, s, valid, R, list1, cnt[1]);
+                rc = rq8_replay_list(idx, s, valid, R, list1, cnt[1], nq);
                 if (rc) return rc;
                 rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
                 if (rc) return rc;
@@ -2157,7 +2186,7 @@ extern "C" int wv_index_rq_codes(wv_index* idx, void* out, int64_t n) {
         for (int64_t s2 = 0; s2 < n; s2++)
             for (int ch = 0; ch < nch; ch++)
                 memcpy((uint8_t*)out + (size_t)s2 * D + ch * 16,
-                       &tiled[((size_t)((s2 >> 8) * nch + ch) * 256 + (s2 & 255)) * 16], 16);
+                       &tiled[(size_t)rq_tile_u4(s2, ch, nch) * 16], 16);
         return WV_OK;
     }
     if (idx->rq_bits == 8) {
@@ -2173,7 +2202,7 @@ extern "C" int wv_index_rq_codes(wv_index* idx, void* out, int64_t n) {
             put_be32(c + 8, meta[s].z);
             put_be32(c + 12, meta[s].w);
             for (int ch = 0; ch < nch; ch++)
-                memcpy(c + 16 + ch * 16, &tiled[((size_t)((s >> 8) * nch + ch) * 256 + (s & 255)) * 16], 16);
+                memcpy(c + 16 + ch * 16, &tiled[(size_t)rq_tile_u4(s, ch, nch) * 16], 16);
             for (int j = 0; j < D; j++) c[16 + j] ^= 0x80;  // stored offset by 128
         }
     } else {

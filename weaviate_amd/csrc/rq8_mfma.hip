@@ -31,7 +31,7 @@ namespace wv {
 
 // k_rq8_keys operands (external linkage: quant_runtime.hip launches it)
 struct RQ8Args {
-    const unsigned char* codes;  // data codes x' (256-row tiles of 16-byte chunks, rq_kernels.hip)
+    const unsigned char* codes;  // data codes x' (32-row tiles of 16-byte chunks, rq_tile_u4)
     const float4* meta;          // [cap] {lower, step, step * codeSum, norm2}
     const uint32_t* csum;        // [cap] code sums Sx
     const uint32_t* valid;       // [cap / 32] slots to scan
@@ -109,11 +109,18 @@ __device__ __forceinline__ uint32_t rq8_lds_ld4(unsigned addr) {
     return v;
 }
 
+// ring slots of k_rq8_keys: as many as 150 KiB of LDS holds, 4..8
+__host__ __device__ constexpr int rq8_nbuf(int NC) {
+    return (150 * 1024) / (32 * 64 * NC + 656) > 8 ? 8 : (150 * 1024) / (32 * 64 * NC + 656) < 4 ? 4
+                                                                                              : (150 * 1024) / (32 * 64 * NC + 656);
+}
+
 // ---------------------------------------------------------------------------
 // k_rq8_keys<NC>: block minima of 256 queries (8 waves x 32, their codes in
 // VGPRs as B fragments) x one span of 32-row blocks, D = 64 NC.  A block's
 // codes (32 D bytes: 2 NC 1-KiB pieces, [16-byte chunk][row]), meta, code sums
-// and valid word land in an LDS ring of 3 slots by LDS-DMA two blocks ahead;
+// and valid word land in an LDS ring of rq8_nbuf(NC) slots by LDS-DMA
+// NBUF - 2 blocks ahead (as much in flight as 150 KiB of LDS holds);
 // one barrier per block.  Per 64-column chunk: 2 A-fragment reads (row halves,
 // the next chunk's issued before this chunk's MFMAs), 4 MFMAs.  acc[m][n][r]
 // is row 16m + 4g + r (g = lane >> 4) of query 16n + (lane & 15); the C input
@@ -130,7 +137,9 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
     constexpr int SLOT = CB + 656;
     constexpr int NP = 2 * NC + 3;      // wave-wide loads per block
     constexpr int PW = (NP + 7) / 8;    // per wave (padded: every wave issues PW)
-    constexpr int NBUF = 4;  // a late wave reads block t-1's meta while block t+2 lands
+    // a late wave reads block t-1's meta while block t + AHEAD lands
+    constexpr int NBUF = rq8_nbuf(NC);
+    constexpr int AHEAD = NBUF - 2;
     static_assert(SLOT % 16 == 0, "slot alignment");
     static_assert((NC - 1) * 2048 + 256 < 65536, "ds_read offsets");
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
@@ -180,17 +189,15 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
     const unsigned ring = lds_addr(rsm);
     auto issue = [&](int t, int slot) {
         const int64_t blk = b0 + t;
-        const int64_t T = blk >> 3;
-        const int r0 = (int)(blk & 7) * 32;
+        const unsigned char* gb = a.codes + blk * CB;  // the block's contiguous run (rq_tile_u4)
         const unsigned sb = ring + (unsigned)(slot * SLOT);
         static_for<0, PW>([&](auto jc) {
             constexpr int jj = decltype(jc)::value;
             int p = wave + 8 * jj;
             if (p >= NP) p -= NP;  // padding: a copy of a piece another wave loads (same bytes, same place)
             if (p < 2 * NC) {
-                const int c16 = 2 * p + (lane >> 5);
-                const unsigned char* gp = a.codes + ((T * NCH + c16) * 256 + r0 + (lane & 31)) * 16;
-                __builtin_amdgcn_global_load_lds(gp, (lds_ptr_t)(size_t)(sb + (unsigned)(p * 1024)), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(gb + p * 1024 + 16 * lane, (lds_ptr_t)(size_t)(sb + (unsigned)(p * 1024)),
+                                                 16, 0, 0);
             } else if (p == 2 * NC) {
                 if (lane < 32)
                     __builtin_amdgcn_global_load_lds(a.meta + blk * 32 + lane, (lds_ptr_t)(size_t)(sb + MB), 16, 0, 0);
@@ -204,9 +211,8 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
             }
         });
     };
-    const int ahead = (a.dbg_serial & 1) ? 1 : 2;
-    if (nsteps > 0) issue(0, 0);
-    if (nsteps > 1 && ahead == 2) issue(1, 1);
+    const int ahead = (a.dbg_serial & 1) ? 1 : AHEAD;
+    for (int t = 0; t < ahead && t < nsteps; t++) issue(t, t);
 
     const unsigned l16 = (unsigned)(g * 512 + j * 16);
     float* krow = a.key + (q0 + (lane & 31)) * a.ldk;
@@ -235,6 +241,11 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
             }
             asm volatile("" : "+v"(A[c & 1][0]), "+v"(A[c & 1][1]));
             __builtin_amdgcn_sched_barrier(0);
+            if (a.dbg_serial & 16) {  // timing experiment: no MFMAs (wrong keys)
+                acc[0][0] = A[c & 1][0];
+                acc[1][1] = A[c & 1][1];
+                return;
+            }
 #pragma unroll
             for (int m = 0; m < 2; m++)
 #pragma unroll
@@ -268,6 +279,7 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
         asm volatile("" : "+v"(mt[1][0]), "+v"(mt[1][1]), "+v"(mt[1][2]), "+v"(mt[1][3]));
         asm volatile("" : "+v"(cs[0]), "+v"(cs[1]));
         const uint32_t vw = __builtin_amdgcn_readfirstlane(vw0);
+        if (a.dbg_serial & 8) return __int_as_float(acc[0][0][0] ^ acc[1][1][3] ^ mt[0][0][0] ^ cs[1][0]);  // timing: no epilogue math
         float p[2] = {__builtin_inff(), __builtin_inff()};
         bool bad[2] = {false, false};
         // the fast forms: every row valid, every norm <= FINE (wave-uniform);
@@ -346,21 +358,23 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
         return (lane & 16) ? m1 : m0;
     };
     for (int t = 0; t <= nsteps; t++) {
-        const int cur = t & (NBUF - 1);
+        const int cur = t % NBUF;
         if (t < nsteps) {
-            // block t's pieces landed: the loads issued after them are block
-            // t+1's (loads retire in order).  Key stores are not counted (one
-            // retiring before older loads would cut the wait short); one still
-            // in flight only lengthens it.
-            qs_wait_vm(t + 1 < nsteps && ahead == 2 ? PW : 0);
+            // block t's pieces landed: vector-memory ops retire in issue order
+            // (loads, stores and LDS-DMA alike), so the wait leaves in flight
+            // exactly the ops issued after them: the pieces of the blocks up to
+            // t + ahead - 1 and the key stores of the steps since (an early
+            // wave stores before its step's pieces, a late wave after them).
+            // Counting the stores keeps the scattered key writes out of the
+            // critical path.
+            const int later = nsteps - 1 - t < ahead - 1 ? nsteps - 1 - t : ahead - 1;  // blocks issued after t
+            const int fs = t < ahead ? 1 : (late ? (t - ahead > 1 ? t - ahead : 1) : (t - ahead + 1 > 1 ? t - ahead + 1 : 1));
+            const int nst = t > fs ? t - fs : 0;  // the stores of steps fs .. t-1
+            qs_wait_vm(PW * later + nst);
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             if (!late && t > 0 && lane < 32) krow[b0 + t - 1] = pend;
-            if (ahead == 2) {
-                if (t + 2 < nsteps) issue(t + 2, (t + 2) & (NBUF - 1));
-            } else if (t + 1 < nsteps) {
-                issue(t + 1, (t + 1) & (NBUF - 1));
-            }
+            if (t + ahead < nsteps) issue(t + ahead, (t + ahead) % NBUF);
         }
         if (!late) {
             if (t < nsteps) {
@@ -369,7 +383,7 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
             }
         } else {
             if (t > 0) {
-                const float kv = epilogue(ring + (unsigned)(((t - 1) & (NBUF - 1)) * SLOT));
+                const float kv = epilogue(ring + (unsigned)(((t - 1) % NBUF) * SLOT));
                 if (lane < 32) krow[b0 + t - 1] = kv;
             }
             if (t < nsteps) mfma_block(ring + (unsigned)(cur * SLOT));
@@ -431,6 +445,92 @@ __global__ __launch_bounds__(256) void k_rq8_sel(const float* __restrict__ key, 
     }
 }
 
+// the exact rq-8 / rq-1 distance of stored row `slot` to one query, as
+// k_rq8_dist / k_rq1_dist compute it: rq-8 v_dot4_u32_u8 over the code bytes
+// (stored offset by 128) against the query's bytes (qs, LDS), rq-1 xor +
+// popcount of the word-major bits against the 5 query planes (qs as u64)
+template <int BITS>
+__device__ __forceinline__ float rq_row_dist(const void* __restrict__ codes_, int64_t cap,
+                                             const float4* __restrict__ meta, int64_t slot, const uint4* qs,
+                                             const float4& ym, int D, float fl2, float fcos) {
+    const float s_ = 1.0f + fl2;
+    if constexpr (BITS == 1) {
+        const uint64_t* codes = reinterpret_cast<const uint64_t*>(codes_);
+        const uint64_t* qpl = reinterpret_cast<const uint64_t*>(qs);
+        const int W = D >> 6;
+        uint32_t acc = 0;
+#pragma unroll 8
+        for (int wd = 0; wd < W; wd++) {
+            const uint64_t x = codes[(int64_t)wd * cap + slot];
+            const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+#pragma unroll
+            for (int p = 0; p < 5; p++) {
+                const uint64_t y = qpl[5 * wd + p];
+                uint32_t h = __builtin_popcount(xl ^ (uint32_t)y);
+                h += __builtin_popcount(xh ^ (uint32_t)(y >> 32));
+                acc += h << (p + 1);
+            }
+        }
+        const int qdim = (int)ym.z;
+        const int dot = qdim > 0 ? 31 * qdim - (int)acc : 0;
+        const float4 xm = meta[slot];
+        float est = ym.x * xm.x;
+        est = est * (float)dot;
+        float tt = fl2 * (xm.y + ym.y);
+        tt = tt + fcos;
+        return tt - s_ * est;
+    } else {
+        const int nch = D >> 4;
+        const uint4* xr = reinterpret_cast<const uint4*>(codes_) + rq_tile_u4(slot, 0, nch);
+        uint32_t acc = 0;
+        // 16 chunk loads in flight at a time (nch is a multiple of 4): the row's
+        // bytes are 16 scattered 16-byte pieces per group, latency-bound otherwise
+#pragma unroll 16
+        for (int c = 0; c < nch; c++) {
+            const uint4 x = xr[(int64_t)c * 32];
+            const uint4 y = qs[c];
+            acc = __builtin_amdgcn_udot4(x.x ^ 0x80808080u, y.x, acc, false);
+            acc = __builtin_amdgcn_udot4(x.y ^ 0x80808080u, y.y, acc, false);
+            acc = __builtin_amdgcn_udot4(x.z ^ 0x80808080u, y.z, acc, false);
+            acc = __builtin_amdgcn_udot4(x.w ^ 0x80808080u, y.w, acc, false);
+        }
+        const float4 xm = meta[slot];
+        float e1 = (float)D * xm.x;
+        e1 = e1 * ym.x;
+        const float e2 = xm.x * ym.z;
+        const float e3 = ym.x * xm.z;
+        float e4 = xm.y * ym.y;
+        e4 = e4 * (float)acc;
+        float est = e1 + e2;
+        est = est + e3;
+        est = est + e4;
+        float tt = fl2 * (xm.w + ym.w);
+        tt = tt + fcos;
+        return tt - s_ * est;
+    }
+}
+
+// a query's codes into LDS for rq_row_dist (wave-cooperative): rq-8 bytes
+// y (Qp holds y ^ 0x80), rq-1 the 5 W planes of query gq (group-tiled)
+template <int BITS>
+__device__ __forceinline__ void rq_query_to_lds(uint4* qs, const void* __restrict__ qsrc, int64_t q, int64_t gq, int D,
+                                                int lane) {
+    if constexpr (BITS == 8) {
+        const unsigned char* Qp = reinterpret_cast<const unsigned char*>(qsrc);
+        for (int c = lane; c < (D >> 4); c += 64) {
+            const uint4 y = *reinterpret_cast<const uint4*>(Qp + q * D + 16 * c);
+            qs[c] = make_uint4(y.x ^ 0x80808080u, y.y ^ 0x80808080u, y.z ^ 0x80808080u, y.w ^ 0x80808080u);
+        }
+    } else {
+        const uint64_t* planes = reinterpret_cast<const uint64_t*>(qsrc);
+        uint64_t* qpl = reinterpret_cast<uint64_t*>(qs);
+        const int W = D >> 6;
+        for (int e = lane; e < 5 * W; e += 64)  // e = 5 w + p
+            qpl[e] = planes[((gq / RQ_QPB) * W * 5 + e) * RQ_QPB + gq % RQ_QPB];
+    }
+}
+__host__ __device__ constexpr int rq_query_lds_u4(int bits, int D) { return bits == 8 ? D / 16 : (5 * (D / 64) + 1) / 2; }
+
 // ---------------------------------------------------------------------------
 // k_rq8_cand<RT>: wave per query (4 per block), skipped when k_rq8_sel flagged
 // it.  Lanes 0-31 / 32-63 take the rows of two candidate blocks at a time:
@@ -460,25 +560,10 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const void* __restrict__ codes
     const int q = blockIdx.x * 4 + w;
     if (q >= nq) return;
     if (oflag[q]) return;
-    const int nch = D >> 4, W = D >> 6;
-    uint4* qs = cqs + w * (BITS == 8 ? nch : (5 * W + 1) / 2);
-    uint64_t* qpl = reinterpret_cast<uint64_t*>(qs);
-    if constexpr (BITS == 8) {
-        const unsigned char* Qp = reinterpret_cast<const unsigned char*>(qsrc);
-        for (int c = lane; c < nch; c += 64) {
-            const uint4 y = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * D + 16 * c);
-            qs[c] = make_uint4(y.x ^ 0x80808080u, y.y ^ 0x80808080u, y.z ^ 0x80808080u, y.w ^ 0x80808080u);
-        }
-    } else {
-        const uint64_t* planes = reinterpret_cast<const uint64_t*>(qsrc);
-        const int64_t gq = q_base + q;
-        for (int e = lane; e < 5 * W; e += 64)  // e = 5 w + p
-            qpl[e] = planes[((gq / RQ_QPB) * W * 5 + e) * RQ_QPB + gq % RQ_QPB];
-    }
+    uint4* qs = cqs + w * rq_query_lds_u4(BITS, D);
+    rq_query_to_lds<BITS>(qs, qsrc, q, q_base + q, D, lane);
     wave_sync_lds();
     const float4 ym = qmeta[q];
-    const float fD = (float)D;
-    const float s_ = 1.0f + fl2;
     const int nc = ncand[q];
     WaveTopL<RT> t;
     t.init();
@@ -491,54 +576,8 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const void* __restrict__ codes
         const int64_t slot = (int64_t)blk * 32 + (lane & 31);
         const bool ok = has && slot < nslots && ((valid[blk] >> (lane & 31)) & 1u);
         float dist = __builtin_inff();
-        if (BITS == 1 && ok) {
-            const uint64_t* codes = reinterpret_cast<const uint64_t*>(codes_);
-            uint32_t acc = 0;
-            for (int wd = 0; wd < W; wd++) {
-                const uint64_t x = codes[(int64_t)wd * cap + slot];
-                const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-#pragma unroll
-                for (int p = 0; p < 5; p++) {
-                    const uint64_t y = qpl[5 * wd + p];
-                    uint32_t h = __builtin_popcount(xl ^ (uint32_t)y);
-                    h += __builtin_popcount(xh ^ (uint32_t)(y >> 32));
-                    acc += h << (p + 1);
-                }
-            }
-            const int qdim = (int)ym.z;
-            const int dot = qdim > 0 ? 31 * qdim - (int)acc : 0;
-            const float4 xm = meta[slot];
-            float est = ym.x * xm.x;
-            est = est * (float)dot;
-            float tt = fl2 * (xm.y + ym.y);
-            tt = tt + fcos;
-            dist = tt - s_ * est;
-            nan = nan || dist != dist;
-        } else if (BITS == 8 && ok) {
-            const uint4* codes = reinterpret_cast<const uint4*>(codes_);
-            const uint4* xr = codes + ((slot >> 8) * nch) * 256 + (slot & 255);
-            uint32_t acc = 0;
-            for (int c = 0; c < nch; c++) {
-                uint4 x = xr[(int64_t)c * 256];
-                const uint4 y = qs[c];
-                acc = __builtin_amdgcn_udot4(x.x ^ 0x80808080u, y.x, acc, false);
-                acc = __builtin_amdgcn_udot4(x.y ^ 0x80808080u, y.y, acc, false);
-                acc = __builtin_amdgcn_udot4(x.z ^ 0x80808080u, y.z, acc, false);
-                acc = __builtin_amdgcn_udot4(x.w ^ 0x80808080u, y.w, acc, false);
-            }
-            const float4 xm = meta[slot];
-            float e1 = fD * xm.x;
-            e1 = e1 * ym.x;
-            const float e2 = xm.x * ym.z;
-            const float e3 = ym.x * xm.z;
-            float e4 = xm.y * ym.y;
-            e4 = e4 * (float)acc;
-            float est = e1 + e2;
-            est = est + e3;
-            est = est + e4;
-            float tt = fl2 * (xm.w + ym.w);
-            tt = tt + fcos;
-            dist = tt - s_ * est;
+        if (ok) {
+            dist = rq_row_dist<BITS>(codes_, cap, meta, slot, qs, ym, D, fl2, fcos);
             nan = nan || dist != dist;
         }
         nvalid += __popcll(__ballot(ok));
@@ -582,12 +621,14 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const void* __restrict__ codes
     }
 }
 
-// queries k_rq8_cand left at 2 (equal quantized distances inside the R): a
-// tie among their rescored distances (or a NaN) makes the k-heap's result
-// depend on the pop order of the equal quantized ones -> 3 (replayed), else 0.
-// Wave per query; lists longer than 2048 are replayed without the check.
+// queries k_rq8_cand left at 2 (equal quantized distances inside the R): the
+// k-heap over the rescored distances (k_bq_final) depends on the feeding
+// (pop) order only through equal rescored distances among its survivors: a
+// value equal to another one and not above the k-th smallest (or a NaN) ->
+// 3 (replayed), else 0.  Wave per query; lists longer than 2048 are replayed
+// without the check.
 __global__ __launch_bounds__(256) void k_rq_tiecheck(const float* __restrict__ candE, const int32_t* __restrict__ cnt,
-                                                     int nq, int R, int32_t* __restrict__ oflag) {
+                                                     int nq, int R, int k, int32_t* __restrict__ oflag) {
     const int lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq || oflag[q] != 2) return;
@@ -597,11 +638,122 @@ __global__ __launch_bounds__(256) void k_rq_tiecheck(const float* __restrict__ c
     for (int i = lane; i < n && !dup; i += 64) {
         const float v = e[i];
         if (v != v) { dup = true; break; }
-        for (int j = i + 1; j < n; j++)
-            if (e[j] == v) { dup = true; break; }
+        int below = 0;
+        bool eq = false;
+        for (int j = 0; j < n; j++) {
+            const float u = e[j];
+            below += u < v ? 1 : 0;
+            eq = eq || (j != i && u == v);
+        }
+        if (eq && below < k) dup = true;  // v is among the k smallest (with its equals)
     }
     const bool any = __any(dup);
     if (lane == 0) oflag[q] = any ? 3 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// k_rq8_replay<BITS>: the reference R-heap (searchByVectorQuantized,
+// flat/index.go:470-487: insertToHeap in id order) of one listed query per
+// 512-thread workgroup, without a distance matrix.  Windows of 512 32-row
+// blocks in id order: a block is a candidate unless the heap is full and
+// !(top > its exact minimum from k_rq8_keys) -- no row of it could pass
+// `top.Dist > distance`, and the top never rises.  The candidates' rows get
+// their exact distances (rq_row_dist) 16 blocks at a time, 2 per wave; lane 0
+// then offers, in id order, the rows that pass against the top at that point
+// (ph_offer: k_replay_scan's packed heap; computing a row that then fails is
+// only wasted work).  Extracted ascending into asc row `q`.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr size_t rq8_replay_lds(int R, int qu4) {
+    return (size_t)R * 16 + 16 + (size_t)qu4 * 16 + 512 * 4 + 16 * 32 * 4 + 16 * 4 + 8 * 4;
+}
+template <int BITS>
+__global__ __launch_bounds__(512) void k_rq8_replay(const float* __restrict__ key, int64_t ldk, int64_t nblk,
+                                                    const void* __restrict__ codes, int64_t cap,
+                                                    const float4* __restrict__ meta, const uint32_t* __restrict__ valid,
+                                                    int64_t nslots, const void* __restrict__ qsrc, int64_t q_base,
+                                                    const float4* __restrict__ qmeta, int D, float fl2, float fcos,
+                                                    const int32_t* __restrict__ list, int nlist, int R,
+                                                    uint64_t id_base, uint64_t* __restrict__ ascI,
+                                                    float* __restrict__ ascD, int32_t* __restrict__ ascN) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+    HeapRec* hr = reinterpret_cast<HeapRec*>(rsm);
+    int* s_len = reinterpret_cast<int*>(hr + R);
+    uint4* qs = reinterpret_cast<uint4*>(rsm + (size_t)R * 16 + 16);
+    uint32_t* clist = reinterpret_cast<uint32_t*>(qs + rq_query_lds_u4(BITS, D));  // [512] window candidates
+    float* cd = reinterpret_cast<float*>(clist + 512);                              // [16][32] row distances
+    uint32_t* cm = reinterpret_cast<uint32_t*>(cd + 16 * 32);                        // [16] rows that pass
+    int* wcnt = reinterpret_cast<int*>(cm + 16);                                     // [8] per-wave counts
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = blockIdx.x;
+    if (li >= nlist) return;
+    const int q = list[li];
+    if (wave == 0) rq_query_to_lds<BITS>(qs, qsrc, q, q_base + q, D, lane);
+    if (tid == 0) *s_len = 0;
+    __syncthreads();
+    const float4 ym = qmeta[q];
+    const float* kq = key + (int64_t)q * ldk;
+    float kv = tid < nblk ? kq[tid] : __builtin_inff();
+    for (int64_t w0 = 0; w0 < nblk; w0 += 512) {
+        const float kcur = kv;
+        kv = w0 + 512 + tid < nblk ? kq[w0 + 512 + tid] : __builtin_inff();  // the next window, ahead
+        int len = *s_len;
+        float top = len > 0 ? hr[0].d : 0.f;
+        const bool cand = w0 + tid < nblk && (len < R || top > kcur);
+        const uint64_t mb = __ballot(cand);
+        if (lane == 0) wcnt[wave] = __popcll(mb);
+        __syncthreads();
+        int off = 0, nc = 0;
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            const int c = wcnt[w];
+            off += w < wave ? c : 0;
+            nc += c;
+        }
+        if (cand) clist[off + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0))] =
+            (uint32_t)(w0 + tid);
+        __syncthreads();
+        for (int c0 = 0; c0 < nc; c0 += 16) {
+            const int bi = c0 + 2 * wave + (lane >> 5);
+            const int64_t blk = bi < nc ? (int64_t)clist[bi] : 0;
+            const int64_t s = blk * 32 + (lane & 31);
+            const bool ok = bi < nc && s < nslots && ((valid[blk] >> (lane & 31)) & 1u);
+            const float dist = ok ? rq_row_dist<BITS>(codes, cap, meta, s, qs, ym, D, fl2, fcos) : 0.f;
+            len = *s_len;
+            top = len > 0 ? hr[0].d : 0.f;
+            const uint64_t pm = __ballot(ok && (len < R || top > dist));
+            cd[(2 * wave + (lane >> 5)) * 32 + (lane & 31)] = dist;
+            if (lane == 0) cm[2 * wave] = (uint32_t)pm;
+            if (lane == 32) cm[2 * wave + 1] = (uint32_t)(pm >> 32);
+            __syncthreads();
+            if (tid == 0) {
+                PHeap ph{hr, *s_len};
+                const int nb = nc - c0 < 16 ? nc - c0 : 16;
+                for (int b = 0; b < nb; b++) {
+                    uint32_t m = cm[b];
+                    const uint64_t base = id_base + (uint64_t)clist[c0 + b] * 32;
+                    while (m) {
+                        const int r = __builtin_ctz(m);
+                        m &= m - 1;
+                        ph_offer(ph, R, base + (uint64_t)r, cd[b * 32 + r]);
+                    }
+                }
+                *s_len = ph.len;
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {  // extractHeap: pop max-first, fill from the back
+        PHeap ph{hr, *s_len};
+        const int n = *s_len;
+        for (int i = n - 1; i >= 0; i--) {
+            uint64_t a;
+            float b;
+            ph_pop(ph, &a, &b);
+            ascI[(int64_t)q * R + i] = a;
+            ascD[(int64_t)q * R + i] = b;
+        }
+        ascN[q] = n;
+    }
 }
 
 // flagged queries' codes and meta (group-tiled rq-8 query layout) -> a

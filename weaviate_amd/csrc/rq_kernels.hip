@@ -20,9 +20,11 @@
 // reference's R-heap (flat/index.go:470-487) in id order.
 //
 // Layouts:
-//   rq-8 data codes: 256-row tiles of 16-byte chunks: chunk c of slot s is the
-//        uint4 at ((s/256) * (D/16) + c) * 256 + s%256 -> one wave load = 1 KiB
-//        contiguous; meta[s] = {lower, step, codeSum, norm2} (float4).
+//   rq-8 data codes: 32-row tiles of 16-byte chunks, stored offset by 128:
+//        chunk c of slot s is the uint4 at ((s/32) * (D/16) + c) * 32 + s%32
+//        (rq_tile_u4) -> 32 rows' chunk = 512 contiguous bytes, a 32-row block
+//        one contiguous run; meta[s] = {lower, step, codeSum, norm2} (float4),
+//        code sums after the meta (rq_csum).
 //   rq-1 data codes: word-major [W][cap] u64 (coalesced per word); meta[s] =
 //        {step, squaredNorm, 0, 0}.
 //   queries: group-tiled for uniform (scalar) loads in the distance kernels:
@@ -37,7 +39,14 @@ namespace {  // internal linkage: each runtime unit compiles the kernels it laun
 constexpr int RQ_QPB = 32;      // queries per distance block (scalar operands)
 constexpr int RQ_MAXD = 4096;   // rotation output dims supported (two LDS buffers)
 constexpr int RQ_ROUNDS = 3;
-constexpr size_t RQ_META_B = sizeof(float4) + sizeof(uint32_t);  // per slot: meta, then (rq-8) the code sum    // rotationRounds (rotational_quantization.go:61, binary_...:27)
+constexpr size_t RQ_META_B = sizeof(float4) + sizeof(uint32_t);  // per slot: meta, then (rq-8) the code sum
+// rq-8 codes (and the rq-1 +-1 plane): 32-row tiles of 16-byte chunks, the
+// uint4 index of chunk c of slot s -- a 32-row block is one contiguous
+// 32 D-byte run in [chunk][row] order (k_rq8_keys' LDS image, 1-KiB DMA
+// pieces), and 32 consecutive rows read one chunk as 512 contiguous bytes
+__host__ __device__ constexpr int64_t rq_tile_u4(int64_t s, int c, int nch) {
+    return ((s >> 5) * nch + c) * 32 + (s & 31);
+}    // rotationRounds (rotational_quantization.go:61, binary_...:27)
 
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
@@ -151,7 +160,7 @@ __global__ __launch_bounds__(256) void k_rq_encode(const float* __restrict__ row
                 w[j] = word;
             }
             const int64_t o = QUERY ? ((r / RQ_QPB) * nch + c) * RQ_QPB + (r % RQ_QPB)
-                                    : ((slot >> 8) * nch + c) * 256 + (slot & 255);
+                                    : rq_tile_u4(slot, c, nch);
             // data codes are stored offset by 128 (byte x ^ 0x80 = int8 x - 128:
             // the integer-MFMA operand of k_rq8_keys); query codes as they are
             constexpr uint32_t X = QUERY ? 0u : 0x80808080u;
@@ -194,7 +203,7 @@ __global__ __launch_bounds__(256) void k_rq_encode(const float* __restrict__ row
                         for (int b = 0; b < 4; b++) word |= (rx[c * 16 + jj * 4 + b] > 0.f ? 0xFFu : 0x01u) << (8 * b);
                         wd[jj] = word;
                     }
-                    reinterpret_cast<uint4*>(pm_out)[((slot >> 8) * nch + c) * 256 + (slot & 255)] =
+                    reinterpret_cast<uint4*>(pm_out)[rq_tile_u4(slot, c, nch)] =
                         make_uint4(wd[0], wd[1], wd[2], wd[3]);
                 }
             }
@@ -289,10 +298,10 @@ __global__ __launch_bounds__(256) void k_rq8_dist(const uint4* __restrict__ code
     uint32_t acc[RQ_QPB];
 #pragma unroll
     for (int q = 0; q < RQ_QPB; q++) acc[q] = 0;
-    const uint4* xr = codes + tile * nch * 256 + tid;
+    const uint4* xr = codes + rq_tile_u4(slot, 0, nch);
     const uint4* qg = qcodes + g * nch * RQ_QPB;
     for (int c = 0; c < nch; c++) {
-        uint4 x = xr[(int64_t)c * 256];
+        uint4 x = xr[(int64_t)c * 32];
         x.x ^= 0x80808080u;  // stored offset by 128 (k_rq_encode)
         x.y ^= 0x80808080u;
         x.z ^= 0x80808080u;
