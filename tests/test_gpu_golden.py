@@ -89,10 +89,14 @@ def test_flat_search_matches_wide_reference_fixtures(wv, oracle, name):
     idx = wv.FlatIndex(distance=metric, variant="avx256", dims=0)
     idx.add_batch(np.arange(corpus.shape[0], dtype=np.uint64), corpus)
     try:
-        for k in (1, 10, 33):
+        # both int8 key routes: the small-batch streaming kernel (k_q8_gemv,
+        # route 9, the default at this batch size) and k_q8_blockkey (route 3)
+        for gemv, routes in ((1, (9, 3)), (0, (3,))):
+          idx.set_option("q8_gemv", gemv)
+          for k in (1, 10, 33):
             ids, dd, cnt = g[f"{name}_k{k}_ids"], g[f"{name}_k{k}_dists"], g[f"{name}_k{k}_counts"]
             gi, gd, gc = idx.search_by_vector_batch(queries, k)
-            assert idx.stats()["last_route"] == 3  # WV_ROUTE_QS_INT8
+            assert idx.stats()["last_route"] in routes, (gemv, k)
             for qi in range(len(queries)):
                 n = int(cnt[qi])
                 assert gc[qi] == n, (name, k, qi)

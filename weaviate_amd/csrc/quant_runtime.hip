@@ -2097,40 +2097,40 @@ int search_rq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
         rc = rq8_candidates(idx, s, nq, R, valid);
         if (rc) return rc;
         idx->stats.last_group_queries = (uint64_t)nq;
-        // oF: 1 = replay now, 2 = decided after the rescoring (k_rq_tiecheck)
-        HIPCHK(idx->qsList.ensure((size_t)2 * nq * sizeof(int32_t)));
-        HIPCHK(idx->flCtr.ensure(4 * sizeof(uint32_t)));
-        HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 4 * sizeof(uint32_t), s));
-        int32_t* list1 = idx->qsList.as<int32_t>();
-        int32_t* list2 = list1 + nq;
-        uint32_t* ctr = idx->flCtr.as<uint32_t>();
-        const unsigned gl = (unsigned)((nq + 255) / 256);
-        k_flag_list<<<gl, 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq, list1, ctr, 1);
-        k_flag_list<<<gl, 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq, list2, ctr + 2, 2);
-        HIPCHK(hipGetLastError());
-        uint32_t cnt[4] = {0, 0, 0, 0};
-        HIPCHK(hipMemcpyAsync(cnt, ctr, sizeof(cnt), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        if (cnt[1] > 0) {
-            rc = rq8_replay_list(idx, s, valid, R, list1, cnt[1], nq);
-            if (rc) return rc;
-        }
+        // oF: 1 = replayed, 2 = decided by the rescored distances (k_rq_tiecheck:
+        // 3 replayed, else 0).  Every row is rescored first (replayed rows hold
+        // no candidates yet), then the replayed queries' rows once more.
         rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
         if (rc) return rc;
-        if (cnt[3] > 0) {  // ties among the quantized distances inside the R: ties among the rescored ones too?
-            k_rq_tiecheck<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(idx->candE.as<float>(), idx->ascN.as<int32_t>(),
-                                                                   (int)nq, R, k, idx->oF.as<int32_t>());
-            HIPCHK(hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), s));
-            k_flag_list<<<gl, 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq, list1, ctr, 3);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(cnt, ctr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            if (cnt[1] > 0) {
-                rc = rq8_replay_list(idx, s, valid, R, list1, cnt[1], nq);
-                if (rc) return rc;
-                rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), idx->candE.as<float>());
-                if (rc) return rc;
+        k_rq_tiecheck<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(idx->candE.as<float>(), idx->ascN.as<int32_t>(), (int)nq,
+                                                               R, k, idx->oF.as<int32_t>());
+        HIPCHK(idx->qsList.ensure((size_t)nq * sizeof(int32_t)));
+        HIPCHK(idx->flCtr.ensure(2 * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(idx->flCtr.p, 0, 2 * sizeof(uint32_t), s));
+        int32_t* list = idx->qsList.as<int32_t>();
+        k_flag_list<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(idx->oF.as<int32_t>(), (int)nq, list,
+                                                                  idx->flCtr.as<uint32_t>(), 0);
+        HIPCHK(hipGetLastError());
+        uint32_t cnt[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(cnt, idx->flCtr.p, sizeof(cnt), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (cnt[1] > 0) {
+            rc = rq8_replay_list(idx, s, valid, R, list, cnt[1], nq);
+            if (rc) return rc;
+            const int64_t np = (int64_t)cnt[1] * R;
+            const bool v5 = idx->variant == WV_VARIANT_AVX512;
+#define WV_RSL(M, V)                                                                                                 \
+    k_rescore_list<M, V><<<(unsigned)((np + 63) / 64), 64, 0, s>>>(idx->X, idx->dpad, idx->qn.as<float>(), idx->dims,  \
+                                                                   idx->ascI.as<uint64_t>(), idx->ascN.as<int32_t>(), \
+                                                                   list, (int)cnt[1], R, idx->id_base, idx->hiwater,  \
+                                                                   idx->candE.as<float>())
+            switch (idx->metric) {
+            case WV_METRIC_L2_SQUARED: if (v5) WV_RSL(L2, AVX512); else WV_RSL(L2, AVX256); break;
+            case WV_METRIC_DOT: if (v5) WV_RSL(DOT, AVX512); else WV_RSL(DOT, AVX256); break;
+            default: if (v5) WV_RSL(COSINE, AVX512); else WV_RSL(COSINE, AVX256); break;
             }
+#undef WV_RSL
+            HIPCHK(hipGetLastError());
         }
     }
     const int32_t* qlist = idx->ident.as<int32_t>();

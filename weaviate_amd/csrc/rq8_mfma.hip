@@ -559,7 +559,10 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const void* __restrict__ codes
     const int w = threadIdx.x >> 6;
     const int q = blockIdx.x * 4 + w;
     if (q >= nq) return;
-    if (oflag[q]) return;
+    if (oflag[q]) {  // k_rq8_sel's overflow: replayed; no rescoring of this row before that
+        if (lane == 0) ascN[q] = 0;
+        return;
+    }
     uint4* qs = cqs + w * rq_query_lds_u4(BITS, D);
     rq_query_to_lds<BITS>(qs, qsrc, q, q_base + q, D, lane);
     wave_sync_lds();
@@ -602,7 +605,10 @@ __global__ __launch_bounds__(256) void k_rq8_cand(const void* __restrict__ codes
         tie_i = tie_i || (eq && e + 1 < R);
     }
     if (__any(tie_b) || __any(nan)) {
-        if (lane == 0) oflag[q] = 1;
+        if (lane == 0) {
+            oflag[q] = 1;
+            ascN[q] = 0;
+        }
         return;
     }
     const bool tie_in = __any(tie_i);
@@ -754,6 +760,24 @@ __global__ __launch_bounds__(512) void k_rq8_replay(const float* __restrict__ ke
         }
         ascN[q] = n;
     }
+}
+
+// SingleDist of the replayed queries' candidates (k_rescore_ids with rows by
+// query: ids / counts / distances of query list[li] at row list[li])
+template <int METRIC, int VARIANT>
+__global__ __launch_bounds__(64) void k_rescore_list(const float* __restrict__ X, int dpad, const float* __restrict__ Q,
+                                                     int d, const uint64_t* __restrict__ ids,
+                                                     const int32_t* __restrict__ cnt, const int32_t* __restrict__ list,
+                                                     int nlist, int R, uint64_t id_base, int64_t nslots,
+                                                     float* __restrict__ outE) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (int64_t)nlist * R) return;
+    const int q = list[p / R], i = (int)(p % R);
+    if (i >= cnt[q]) return;
+    const int64_t e = (int64_t)q * R + i;
+    const uint64_t id = ids[e];
+    if (id < id_base || id - id_base >= (uint64_t)nslots) return;
+    outE[e] = exact_dist<METRIC, VARIANT>(Q + (int64_t)q * dpad, X + (int64_t)(id - id_base) * dpad, d);
 }
 
 // flagged queries' codes and meta (group-tiled rq-8 query layout) -> a
