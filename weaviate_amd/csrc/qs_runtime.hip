@@ -450,8 +450,11 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // wider rows with int8 keys: the int8 row filter runs block-major
         // (k_q8_filt_bm reads each listed block's codes once), the exact
         // distances stay per query
+        // (small batches keep the per-query filter: the inversion and the
+        // block-major launch cost more than the few listed blocks save there)
         const bool bm_filt = !bm_rows && q8 && idx->q8_bm && idx->q8_filter && idx->exact_filter && capv &&
-                             idx->dpb8 <= 1536 && nb < (1ll << 31) && cn < (1ll << 23) && L <= 512;
+                             idx->dpb8 <= 1536 && nb < (1ll << 31) && cn >= idx->q8_bm_min && cn < (1ll << 23) &&
+                             L <= 512;
         if (bm_rows || bm_filt) {
             // block-major exact distances: invert the candidate lists per block
             const int64_t ldE = (int64_t)L * 32;

@@ -257,6 +257,7 @@ struct wv_index {
     DBuf pq8Max, pq8Mu, pq8Tmp, pq8Qc, qsCand2;
     DBuf rq8Qp, rq8Qcs, rq8Qm, rq8Fq, rq8Fm;                  // rq-8 MFMA route: query planes, flagged queries
     int rq_mfma = 1;
+    int64_t q8_bm_min = 64;                                   // option q8_bm_min: smallest batch for the block-major int8 filter
     int rq_serial = 0;                                        // option rq_serial (debug): k_rq8_keys without the DMA lookahead                                          // option rq_mfma: rq-8 on the integer matrix cores
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima
     DBuf flCtr;                      // device flag-list counters (replay_flags)
