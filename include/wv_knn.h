@@ -147,14 +147,28 @@ int wv_index_search_by_vector_batch(wv_index *idx, const float *queries, int64_t
                                     const uint64_t *allow_ids, int64_t n_allow, int32_t allow_mode,
                                     uint64_t *out_ids, float *out_dists, int32_t *out_counts);
 
+/* flat.SearchByVector (flat/index.go:423-448) for nq queries, each under its
+ * own allow list: query q uses allow_ids[allow_offsets[q] .. allow_offsets[q+1])
+ * when allow_modes[q] == 1 (may be empty -> no results), no list when 0.
+ * allow_offsets has nq+1 entries.  Results equal nq one-query calls of
+ * wv_index_search_by_vector_batch (the concurrent filtered callers of
+ * shard_read.go:415-424 in one launch); options "pqa" (default 1: one shared
+ * block-key launch over the lists' union) and "pqa_budget_mb" (per-query
+ * bitmap memory per launch, default 4096). */
+int wv_index_search_by_vector_batch_multi_allow(wv_index *idx, const float *queries, int64_t nq, int64_t d,
+                                                int32_t k, const uint64_t *allow_ids, const int64_t *allow_offsets,
+                                                const int32_t *allow_modes, uint64_t *out_ids, float *out_dists,
+                                                int32_t *out_counts);
+
 /* flat.SearchByVector for ONE query (flat/index.go:423-448), the call a
  * goroutine makes (shard_read.go:415-424).  Thread-safe; concurrent callers on
  * one index are coalesced into batched launches (micro-batcher, batcher.hip):
  * a caller that finds no batch running leads the next one, waiting up to the
  * "batch_window_us" option (default 0) for company, at most "batch_max"
- * (default 4096) queries per launch; requests with an allow list, or another
- * d or k, run as their own group.  Results and errors equal those of a
- * one-query wv_index_search_by_vector_batch.  out_ids/out_dists capacity k. */
+ * (default 4096) queries per launch, grouped by (d, k); requests carrying
+ * their own allow lists share a launch through
+ * wv_index_search_by_vector_batch_multi_allow.  Results and errors equal those
+ * of a one-query wv_index_search_by_vector_batch.  out_ids/out_dists capacity k. */
 int wv_index_search_by_vector(wv_index *idx, const float *query, int64_t d, int32_t k, const uint64_t *allow_ids,
                               int64_t n_allow, int32_t allow_mode, uint64_t *out_ids, float *out_dists,
                               int32_t *out_count);

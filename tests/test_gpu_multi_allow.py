@@ -1,0 +1,125 @@
+"""GPU: per-query allow lists in one batch
+(wv_index_search_by_vector_batch_multi_allow).  Weaviate's concurrent callers
+each bring their own filter (shard_read.go:415-424 -> flat/index.go:423-448,
+helpers.AllowList per call); the batch must give every query exactly what a
+one-query search under its own list gives (and the oracle), with one
+block-key launch for the whole batch: keys over the lists' union, the exact
+pass and the replays over each query's own bitmap."""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _allow_lists(wv, n, nq, k, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(nq):
+        kind = i % 9
+        if kind == 0:
+            out.append(None)
+        elif kind == 1:  # sparse, some ids past the store
+            out.append(wv.AllowList(rng.integers(0, n + 500, 40)))
+        elif kind == 2:  # dense half
+            out.append(wv.AllowList(np.flatnonzero(rng.random(n) < 0.5)))
+        elif kind == 3:  # one contiguous span
+            a = int(rng.integers(0, n - 3000))
+            out.append(wv.AllowList(range(a, a + 3000)))
+        elif kind == 4:  # empty: no results (flat/index.go:590-594)
+            out.append(wv.AllowList())
+        elif kind == 5:
+            out.append(wv.AllowList(range(i % 7, n, 7)))
+        elif kind == 6:  # fewer rows than k
+            out.append(wv.AllowList(rng.integers(0, n, max(1, k // 2))))
+        elif kind == 7:  # a handful of neighbouring blocks
+            a = int(rng.integers(0, n - 200))
+            out.append(wv.AllowList(range(a, a + k + 3)))
+        else:  # every other block of 32 rows
+            out.append(wv.AllowList([j for j in range(n) if (j >> 5) % 2 == i % 2]))
+    return out
+
+
+@pytest.mark.parametrize("metric,n,d,k,nq", [
+    ("cosine", 20000, 128, 10, 54),
+    ("l2-squared", 30000, 96, 32, 45),
+    ("dot", 12000, 256, 5, 36),
+    ("cosine", 20000, 768, 10, 300),
+])
+def test_multi_allow_equals_one_query_calls(wv, oracle, metric, n, d, k, nq):
+    data = oracle.gen_matrix(0, 71, 0, n, d)
+    queries = oracle.gen_matrix(0, 72, 0, nq, d)
+    idx = wv.FlatIndex(distance=metric, variant="avx256")
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    deleted = list(range(5, n, 97))
+    idx.delete(*deleted)
+    allows = _allow_lists(wv, n, nq, k, seed=n + d)
+    b0 = idx.stats()["batches"]
+    ids, dists, counts = idx.search_by_vector_batch_multi_allow(queries, k, allows)
+    st = idx.stats()
+    assert st["batches"] - b0 == 1, "the batch must share one launch"
+    assert wv._lib.ROUTES[st["last_route"]].startswith(("qs_", "q8_")), st
+    for i in range(nq):
+        ei, ed, ec = idx.search_by_vector_batch(queries[i:i + 1], k, allow=allows[i])
+        assert counts[i] == ec[0], f"q{i}"
+        np.testing.assert_array_equal(ids[i, :counts[i]], ei[0, :ec[0]], err_msg=f"q{i}")
+        np.testing.assert_array_equal(dists[i, :counts[i]].view(np.uint32), ed[0, :ec[0]].view(np.uint32),
+                                      err_msg=f"q{i}")
+        if i % 9 == 4:
+            assert counts[i] == 0
+    # the oracle on a sample of every list kind
+    orc = oracle.OracleFlat(oracle.METRIC[metric], 1, d, n)
+    orc.add_batch(np.arange(n, dtype=np.uint64), data)
+    orc.delete(deleted)
+    for i in range(min(nq, 18)):
+        al = None if allows[i] is None else [int(x) for x in allows[i].ids]
+        rc, oi, od = orc.search(queries[i], k, al)
+        np.testing.assert_array_equal(ids[i, :counts[i]], oi, err_msg=f"q{i}")
+        np.testing.assert_array_equal(dists[i, :counts[i]].view(np.uint32), od.view(np.uint32), err_msg=f"q{i}")
+    idx.close()
+
+
+def test_multi_allow_fallback_routes_and_errors(wv, oracle):
+    """BQ has no shared-launch form: the batch is grouped by identical list and
+    still equals the one-query calls; bad arguments are rejected."""
+    n, d, k = 6000, 64, 8
+    data = oracle.gen_matrix(0, 73, 0, n, d)
+    queries = oracle.gen_matrix(0, 74, 0, 12, d)
+    idx = wv.FlatIndex(distance="l2-squared", variant="avx256", bq=True, rescore_limit=40)
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    common = wv.AllowList(range(0, n, 2))
+    allows = [None, common, wv.AllowList(range(100, 900)), common] * 3
+    ids, dists, counts = idx.search_by_vector_batch_multi_allow(queries, k, allows)
+    for i in range(len(queries)):
+        ei, ed, ec = idx.search_by_vector_batch(queries[i:i + 1], k, allow=allows[i])
+        assert counts[i] == ec[0]
+        np.testing.assert_array_equal(ids[i, :counts[i]], ei[0, :ec[0]])
+        np.testing.assert_array_equal(dists[i, :counts[i]].view(np.uint32), ed[0, :ec[0]].view(np.uint32))
+    with pytest.raises(wv.WeaviateError):
+        idx.search_by_vector_batch_multi_allow(queries, k, allows[:-1])
+    with pytest.raises(wv.WeaviateError, match="vector lengths don't match|same len"):
+        idx.search_by_vector_batch_multi_allow(np.ones((3, d + 1), np.float32), k, [None, common, None])
+    idx.close()
+
+
+def test_batcher_coalesces_distinct_allow_lists(wv, oracle):
+    """concurrent callers with their own allow lists share launches and each
+    gets its one-query result"""
+    n, d, k = 20000, 128, 10
+    data = oracle.gen_matrix(0, 75, 0, n, d)
+    queries = oracle.gen_matrix(0, 76, 0, 64, d)
+    idx = wv.FlatIndex(distance="cosine", variant="avx256")
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    idx.set_option("batch_window_us", 3000)
+    allows = _allow_lists(wv, n, len(queries), k, seed=5)
+    exp = [idx.search_by_vector_batch(queries[i:i + 1], k, allow=allows[i]) for i in range(len(queries))]
+    with ThreadPoolExecutor(32) as ex:
+        res = list(ex.map(lambda i: idx.search_by_vector(queries[i], k, allow=allows[i]), range(len(queries))))
+    for i, (ri, rd) in enumerate(res):
+        ei, ed, ec = exp[i]
+        np.testing.assert_array_equal(ri, ei[0, :ec[0]], err_msg=f"q{i}")
+        np.testing.assert_array_equal(rd.view(np.uint32), ed[0, :ec[0]].view(np.uint32), err_msg=f"q{i}")
+    st = idx.batcher_stats()
+    assert st["launches"] < st["calls"] and st["max_batch"] > 1, st
+    idx.close()

@@ -85,6 +85,20 @@ extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queri
     return WV_OK;
 }
 
+// per-query allow lists: the mock searches query by query (same contract)
+extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const float* queries, int64_t nq, int64_t d,
+                                                           int32_t k, const uint64_t* allow_ids,
+                                                           const int64_t* allow_offsets, const int32_t* allow_modes,
+                                                           uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    for (int64_t q = 0; q < nq; q++) {
+        const int rc = wv_index_search_by_vector_batch(idx, queries + q * d, 1, d, k, allow_ids + allow_offsets[q],
+                                                       allow_offsets[q + 1] - allow_offsets[q], allow_modes[q],
+                                                       out_ids + q * k, out_dists + q * k, out_counts + q);
+        if (rc) return rc;
+    }
+    return WV_OK;
+}
+
 #include "../weaviate_amd/csrc/batcher.hip"
 
 int main(int argc, char** argv) {
@@ -121,7 +135,7 @@ int main(int argc, char** argv) {
                 for (float& x : q) x = V(r);
                 std::vector<uint64_t> allow;
                 int32_t mode = 0;
-                if (kind == 6) {  // an allow list: its own batch group
+                if (kind == 6) {  // an allow list: batched through the per-query-list entry point
                     mode = 1;
                     for (int i = 0; i < 40; i++) allow.push_back(r() % (uint64_t)idx.n);
                 }

@@ -8,9 +8,10 @@
 // concurrent callers are coalesced: leader/follower, no background thread.
 // A caller enqueues its request; if no batch is running it becomes the
 // leader, optionally waits batch_window_us for company, takes every pending
-// request, groups them by (d, k) (one allow list = its own group, since the
-// batch entry point takes one allow list), runs each group through
-// wv_index_search_by_vector_batch and hands every follower its rows.  Requests
+// request, groups them by (d, k), runs each group through
+// wv_index_search_by_vector_batch (no request with an allow list) or
+// wv_index_search_by_vector_batch_multi_allow (each query its own list, one
+// block-key launch for the group) and hands every follower its rows.  Requests
 // that arrive while a batch runs form the next batch.  Results are identical
 // to individual calls: each query of a batch is searched independently.
 #include <chrono>
@@ -49,7 +50,7 @@ static wv_batcher* get_batcher(wv_index* idx) {
     return idx->batcher;
 }
 
-// Runs one group of requests sharing (d, k, allow) as one batch call.
+// Runs one group of requests sharing (d, k) as one batch call.
 static void run_group(wv_index* idx, std::vector<wv_batch_req*>& grp) {
     const int64_t n = (int64_t)grp.size();
     const int64_t d = grp[0]->d;
@@ -60,8 +61,25 @@ static void run_group(wv_index* idx, std::vector<wv_batch_req*>& grp) {
     std::vector<uint64_t> ids((size_t)(n * kk) + 1);
     std::vector<float> dists((size_t)(n * kk) + 1);
     std::vector<int32_t> cnt((size_t)n);
-    int rc = wv_index_search_by_vector_batch(idx, q.data(), n, d, k, grp[0]->allow_ids, grp[0]->n_allow,
+    bool lists = false;
+    for (wv_batch_req* r : grp) lists |= r->allow_mode != 0;
+    int rc;
+    if (!lists || n == 1) {
+        rc = wv_index_search_by_vector_batch(idx, q.data(), n, d, k, grp[0]->allow_ids, grp[0]->n_allow,
                                              grp[0]->allow_mode, ids.data(), dists.data(), cnt.data());
+    } else {
+        std::vector<uint64_t> aids;
+        std::vector<int64_t> off((size_t)n + 1, 0);
+        std::vector<int32_t> modes((size_t)n);
+        for (int64_t i = 0; i < n; i++) {
+            modes[(size_t)i] = grp[i]->allow_mode;
+            if (grp[i]->allow_mode != 0 && grp[i]->n_allow > 0)
+                aids.insert(aids.end(), grp[i]->allow_ids, grp[i]->allow_ids + grp[i]->n_allow);
+            off[(size_t)i + 1] = (int64_t)aids.size();
+        }
+        rc = wv_index_search_by_vector_batch_multi_allow(idx, q.data(), n, d, k, aids.data(), off.data(), modes.data(),
+                                                         ids.data(), dists.data(), cnt.data());
+    }
     std::string err = rc ? std::string(wv_last_error()) : std::string();
     for (int64_t i = 0; i < n; i++) {
         wv_batch_req* r = grp[i];
@@ -74,14 +92,12 @@ static void run_group(wv_index* idx, std::vector<wv_batch_req*>& grp) {
 }
 
 static void run_batch(wv_index* idx, std::vector<wv_batch_req*>& batch) {
-    // group by (d, k) for allow-free requests; allow-list requests alone
+    // group by (d, k); each request keeps its own allow list
     std::vector<std::vector<wv_batch_req*>> groups;
     for (wv_batch_req* r : batch) {
         bool placed = false;
-        if (r->allow_mode == 0) {
-            for (auto& g : groups)
-                if (g[0]->allow_mode == 0 && g[0]->d == r->d && g[0]->k == r->k) { g.push_back(r); placed = true; break; }
-        }
+        for (auto& g : groups)
+            if (g[0]->d == r->d && g[0]->k == r->k) { g.push_back(r); placed = true; break; }
         if (!placed) groups.push_back({r});
     }
     for (auto& g : groups) run_group(idx, g);

@@ -55,6 +55,47 @@ __global__ void k_allow_bits(const uint64_t* __restrict__ ids, int64_t n, uint64
     if (!(atomicOr(&bits[sl >> 5], m) & m)) atomicAdd(cnt, 1u);
 }
 
+// per-query allow bitmaps (wv_index_search_by_vector_batch_multi_allow): query
+// q's vq words at bits + q * vq.  Queries without a list (qlist) take the
+// present bitmap; a listed id sets its query's bit when the slot is present.
+__global__ void k_pqa_present(const uint32_t* __restrict__ present, int64_t vq, const int32_t* __restrict__ qlist,
+                              int64_t nl, uint32_t* __restrict__ bits) {
+    const int64_t n = nl * vq;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = i / vq, w = i - j * vq;
+        bits[(int64_t)qlist[j] * vq + w] = present[w];
+    }
+}
+
+// ids [off[0], off[nq]) of all lists as given; thread per id, its query by
+// binary search of the offsets (the last q with off[q] <= i)
+__global__ void k_pqa_bits(const uint64_t* __restrict__ ids, const int64_t* __restrict__ off,
+                           const int32_t* __restrict__ modes, int64_t nq, uint64_t id_base, int64_t hiwater,
+                           const uint32_t* __restrict__ present, int64_t vq, uint32_t* __restrict__ bits) {
+    const int64_t i = off[0] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= off[nq]) return;
+    int64_t lo = 0, hi = nq - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    if (modes[lo] == 0) return;
+    const uint64_t id = ids[i - off[0]];
+    if (id < id_base || id - id_base >= (uint64_t)hiwater) return;
+    const uint64_t sl = id - id_base;
+    const uint32_t m = 1u << (sl & 31);
+    if (present[sl >> 5] & m) atomicOr(&bits[lo * vq + (int64_t)(sl >> 5)], m);
+}
+
+// union of the nq bitmaps (the block keys' row set), thread per word
+__global__ void k_pqa_union(const uint32_t* __restrict__ bits, int64_t vq, int64_t nq, uint32_t* __restrict__ uni) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= vq) return;
+    uint32_t u = 0;
+    for (int64_t q = 0; q < nq; q++) u |= bits[q * vq + w];
+    uni[w] = u;
+}
+
 // gathered allow-list search: stored rows slots[i] -> row i of a sub-index
 // (fp32 row with its padding, |x|^2, and the bf16 plane row), thread per
 // (row, 16-byte piece); rows in [n, n_pad) are zeroed

@@ -20,8 +20,8 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
     if (q8f && idx->exact_filter && (Xb || idx->q8_only)) f8 = *q8f;
 #define WV_EXR(RV, M, V)                                                                                             \
     do {                                                                                                             \
-        if (eb) k_blk_exact<RV, M, V, true><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, nullptr); \
-        else k_blk_exact<RV, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, fmask); \
+        if (eb) k_blk_exact<RV, M, V, true><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, eb, ldE, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, nullptr, idx->cur_vq, idx->cur_tq, idx->qsEps.as<float>()); \
+        else k_blk_exact<RV, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, fmask, idx->cur_vq, idx->cur_tq, idx->qsEps.as<float>()); \
     } while (0)
 #define WV_EXM(RV)                                                          \
     switch (metric) {                                                       \
@@ -31,7 +31,7 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
     }
     if (RV == 2) { WV_EXM(2); } else if (RV == 4) { WV_EXM(4); } else if (RV == 8) { WV_EXM(8); }
     else {  // k + 1 <= 960: 960-block lists, never block-major (9-bit list positions)
-#define WV_EX16(M, V) k_blk_exact<16, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, nullptr)
+#define WV_EX16(M, V) k_blk_exact<16, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, nullptr, idx->cur_vq, idx->cur_tq, idx->qsEps.as<float>())
         switch (metric) {
         case L2: if (v5) WV_EX16(L2, AVX512); else WV_EX16(L2, AVX256); break;
         case DOT: if (v5) WV_EX16(DOT, AVX512); else WV_EX16(DOT, AVX256); break;

@@ -872,6 +872,9 @@ __device__ __forceinline__ float qs_next_up(float x) {
     return __uint_as_float(x > 0.f ? b + 1u : b - 1u);
 }
 
+// the next float below x (finite x): -qs_next_up(-x)
+__device__ __forceinline__ float qs_next_down(float x) { return -qs_next_up(-x); }
+
 // ---------------------------------------------------------------------------
 // wave-level streaming selection of the L = 64 (R-1) smallest (key, id) pairs:
 // list in rows 0..R-2 of the register arrays (sorted), row R-1 takes the LDS
@@ -939,7 +942,10 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
                                                     float* __restrict__ eps_out, const int32_t* __restrict__ qlist,
                                                     const uint32_t* __restrict__ qcount, float* __restrict__ topA,
                                                     float* __restrict__ cap_out = nullptr,
-                                                    uint32_t* __restrict__ list_ctr = nullptr) {
+                                                    uint32_t* __restrict__ list_ctr = nullptr,
+                                                    float* __restrict__ t_out = nullptr,
+                                                    const uint32_t* __restrict__ pv = nullptr, int64_t pvq = 0,
+                                                    const int32_t* __restrict__ mq = nullptr) {
     // the batch's flag-list cursors (k_flag_list counters[1] of the final and
     // the overflow lists), reset here instead of by two fills
     if (list_ctr && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -961,6 +967,9 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
     const float4 qi = qinfo[q];
     const float eps = qs_eps(metric, qi, qsmax, maxn2, gd, gacc);
     const float* kr = key + (int64_t)q * ldk;
+    // per-query allow bitmaps (pvq words each): a block without a row of the
+    // query's own (its bitmap word, one per 32-row block) is not a candidate
+    const uint32_t* vr = pvq ? pv + (int64_t)q * pvq : nullptr;
     WaveTopL<R> t;
     t.init();
     for (int64_t b0 = 0; b0 < nb; b0 += 64 * U) {
@@ -968,7 +977,7 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
 #pragma unroll
         for (int j = 0; j < U; j++) {
             const int64_t bb = b0 + j * 64 + lane;
-            v[j] = bb < nb ? kr[bb] : __builtin_inff();
+            v[j] = bb < nb && (!vr || vr[bb]) ? kr[bb] : __builtin_inff();
         }
         bool any = false;
 #pragma unroll
@@ -978,10 +987,18 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
         for (int j = 0; j < U; j++) t.offer(v[j], (uint32_t)(b0 + j * 64 + lane), sbk[w], sbi[w], lane);
     }
     t.merge(sbk[w], sbi[w], lane);
-    // M = A of the (k+1)-th smallest block key; T = M + 2 eps
-    const float mk = t.key_at(k);
+    // M = A of the (k+1)-th smallest block key; T = M + 2 eps.  mq (per-query
+    // allow lists): the mq[q]-th instead -- a block's key need not come from a
+    // row of the query's own, so sparser lists take a deeper threshold (any T
+    // keeps k_blk_exact's completeness proof; a deeper one passes it more often)
+    const int me = mq ? (mq[q] < k + 1 ? k : mq[q] > L ? L - 1 : mq[q] - 1) : k;
+    const float mk = t.key_at(me);
     const float M = qs_key_to_a(metric, mk, qi.x);
-    const float T = mk == __builtin_inff() ? __builtin_inff() : M + 2.0005f * eps;
+    float T = mk == __builtin_inff() ? __builtin_inff() : M + 2.0005f * eps;
+    if (mq) {  // a threshold the list can hold: below the (L+1)-th smallest A
+        const float kl = t.key_at(L);
+        if (kl < __builtin_inff()) T = fminf(T, qs_next_down(qs_key_to_a(metric, kl, qi.x)));
+    }
     int nc = 0;
 #pragma unroll
     for (int r = 0; r < R - 1; r++) {
@@ -995,11 +1012,15 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
         eps_out[q] = eps;
         // the k+1 smallest blocks each hold a row with E <= A + eps <= M + eps, so
         // the (k+1)-th smallest exact distance over the candidates is below cap
+        // (per-query lists: those blocks' rows need not be the query's; rows at
+        // or above T - eps cannot pass k_blk_exact's completeness test anyway)
         if (cap_out)
             cap_out[q] = mk == __builtin_inff() ? __builtin_inff()
-                                                 : qs_next_up(M + 1.001f * eps);
+                         : mq ? T - eps : qs_next_up(M + 1.001f * eps);
+        if (t_out) t_out[q] = T;  // per-query allow lists: k_blk_exact's completeness bound
         // the L-th entry also qualifies: blocks beyond the list may too
-        flags[q] = (nc >= L || qi.w != 0.f) ? 2 : 0;
+        // (mq: T is below every block past the list)
+        flags[q] = ((nc >= L && !mq) || qi.w != 0.f) ? 2 : 0;
     }
     if (topA) {  // sharded phase 1: this shard's k+1 smallest block-key A values
 #pragma unroll
@@ -1029,7 +1050,8 @@ __global__ __launch_bounds__(256) void k_blk_select_f(const float* __restrict__ 
                                                       int32_t* __restrict__ flags, float* __restrict__ eps_out,
                                                       const int32_t* __restrict__ qlist,
                                                       const uint32_t* __restrict__ qcount, float* __restrict__ topA,
-                                                      float* __restrict__ cap_out, uint32_t* __restrict__ list_ctr) {
+                                                      float* __restrict__ cap_out, uint32_t* __restrict__ list_ctr,
+                                                      float* __restrict__ t_out = nullptr) {
     if (list_ctr && blockIdx.x == 0 && threadIdx.x == 0) {
         list_ctr[1] = 0u;
         list_ctr[3] = 0u;
@@ -1136,6 +1158,7 @@ __global__ __launch_bounds__(256) void k_blk_select_f(const float* __restrict__ 
         eps_out[q] = eps;
         if (cap_out)
             cap_out[q] = mk == __builtin_inff() ? __builtin_inff() : qs_next_up(M + 1.001f * eps);
+        if (t_out) t_out[q] = T;
         flags[q] = (full || qi.w != 0.f) ? 2 : 0;
     }
     if (topA) {  // sharded phase 1: this shard's k+1 smallest block-key A values
@@ -1473,7 +1496,9 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
                                                    const uint16_t* __restrict__ Xb, int dpb, const float* __restrict__ xn2,
                                                    const uint32_t* __restrict__ qsmax, const uint32_t* __restrict__ maxn2,
                                                    float gd, float gacc_r, const Q8Filter q8f,
-                                                   const uint32_t* __restrict__ fmask) {
+                                                   const uint32_t* __restrict__ fmask, int64_t vq = 0,
+                                                   const float* __restrict__ tq = nullptr,
+                                                   const float* __restrict__ qeps = nullptr) {
     constexpr int L = 64 * (R - 1);
     __shared__ float sbk[4][64];
     __shared__ uint32_t sbi[4][64];
@@ -1491,6 +1516,7 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         q = qlist[q];
     }
     if (q >= nq) return;
+    const uint32_t* vrow = vq ? valid + (int64_t)q * vq : valid;  // per-query allow bitmaps (vq words each)
     if (flags[q]) return;  // overflowed selection: the replay resolves it
     const int nc = ncand[q];
     const float* qv = Qn + (int64_t)q * dpad;
@@ -1532,7 +1558,7 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         int64_t row = 0;
         if (j < nc) {
             row = (int64_t)cand[(int64_t)q * L + j] * 32 + li;
-            ok = row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+            ok = row < nrows && ((vrow[row >> 5] >> (row & 31)) & 1u);
         }
         float e = __builtin_inff();
         if (EB) {  // its own instantiation: the distance code's registers stay out of the read-back form
@@ -1597,6 +1623,14 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
         if (e >= 1 && e < m && !(t.key[r] > pv)) inc = false;
     }
     inc = __all(inc);
+    // per-query allow bitmaps (vq): the keys came from their union, so the
+    // k+1 blocks under M need not hold k+1 of this query's rows.  Rows of
+    // unlisted blocks are > T - eps (A > T there, E >= A - eps): the list is
+    // complete when it holds k+1 rows and its (k+1)-th is <= T - eps (the
+    // rounded difference one ulp down: below the exact one); else the replay
+    // decides.  T = inf: every block with a union row is listed.
+    if (vq && inc && tq[q] < __builtin_inff())
+        inc = nvalid >= k + 1 && t.key_at(k) <= qs_next_down(tq[q] - qeps[q]);
     if (!inc) {
         if (lane == 0) flags[q] = 1;
         return;
@@ -1855,7 +1889,7 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
                                                    const float* __restrict__ in_d, const int32_t* __restrict__ in_len,
                                                    int extract, int by_list, const uint16_t* __restrict__ Xb, int dpb,
                                                    const float* __restrict__ xn2, const uint32_t* __restrict__ qsmax,
-                                                   const uint32_t* __restrict__ maxn2, float gd, float gacc_r) {
+                                                   const uint32_t* __restrict__ maxn2, float gd, float gacc_r, int64_t vq = 0) {
     // dynamic LDS: [k] heap records (PHeap) | [64] f32 | len (16 B) | [RU * 64] keys | [dpb] bf16(q) as f32
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     HeapRec* hr = reinterpret_cast<HeapRec*>(rsm);
@@ -1865,6 +1899,7 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
     const int li_ = blockIdx.x;  // list position
     if (counters ? (uint32_t)li_ >= counters[1] : li_ >= nlist) return;
     const int q = qlist[li_];
+    const uint32_t* vrow = vq ? valid + (int64_t)q * vq : valid;  // per-query allow bitmaps (vq words each)
     const int metric = METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2;
     const float4 qi = qinfo[q];
     const bool noskip = qi.w != 0.f;
@@ -1919,7 +1954,7 @@ __global__ __launch_bounds__(64) void k_blk_replay(const float* __restrict__ key
         const int64_t bb = b0 + lane;
         float lb = __builtin_inff();
         bool has = false;
-        const uint32_t vwb = bb < nb && bb * 32 < nrows ? valid[bb] : 0u;  // the group's valid words (nb may pass the bitmap)
+        const uint32_t vwb = bb < nb && bb * 32 < nrows ? vrow[bb] : 0u;  // the group's valid words (nb may pass the bitmap)
         if (bb < nb) {
             const float kv = skey[(b0 - r0) + lane];
             has = noskip || kv < __builtin_inff();
@@ -2047,7 +2082,7 @@ __global__ __launch_bounds__(512) void k_blk_replay_par(const float* __restrict_
                                                         const uint64_t* __restrict__ in_ids,
                                                         const float* __restrict__ in_d,
                                                         const int32_t* __restrict__ in_len, int extract, int by_list,
-                                                        float* __restrict__ scratch) {
+                                                        float* __restrict__ scratch, int64_t vq = 0) {
     __shared__ uint64_t hid[64];
     __shared__ float hd[64];
     __shared__ float s_d[64];
@@ -2065,6 +2100,7 @@ __global__ __launch_bounds__(512) void k_blk_replay_par(const float* __restrict_
     const int li = lane & 31, lh = lane >> 5;
     for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
         const int q = qlist[li_];
+        const uint32_t* vrow = vq ? valid + (int64_t)q * vq : valid;  // per-query allow bitmaps (vq words each)
         const float4 qi = qinfo[q];
         const bool noskip = qi.w != 0.f;
         const float eps = eps_q[q];
@@ -2227,7 +2263,7 @@ __global__ __launch_bounds__(512) void k_blk_replay_par(const float* __restrict_
                     const int64_t b2 = __shfl(blk, j2 < 0 ? j1 : j2);
                     const bool okb = lh ? j2 >= 0 : true;
                     const int64_t row = (lh ? b2 : b1) * 32 + li;
-                    const bool ok = okb && row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+                    const bool ok = okb && row < nrows && ((vrow[row >> 5] >> (row & 31)) & 1u);
                     const float dist = ok ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
                     uint64_t mask = __ballot(ok && (len < k || top > dist));
                     if (mask == 0) continue;
@@ -2471,7 +2507,7 @@ __global__ __launch_bounds__(256) void k_rp_exact(const float* __restrict__ X, i
                                                   const int32_t* __restrict__ qlist, const uint32_t* __restrict__ pool_blk,
                                                   const int32_t* __restrict__ pool_q, const uint32_t* __restrict__ pool_ctr,
                                                   int64_t pool_cap, float* __restrict__ pool_E,
-                                                  uint32_t* __restrict__ pool_vm) {
+                                                  uint32_t* __restrict__ pool_vm, int64_t vq = 0) {
     const int lane = threadIdx.x & 63;
     const int li = lane & 31, lh = lane >> 5;
     int64_t used = (int64_t)pool_ctr[0];
@@ -2485,8 +2521,9 @@ __global__ __launch_bounds__(256) void k_rp_exact(const float* __restrict__ X, i
             const int lq = pool_q[e];
             if (lq >= 0) {
                 const int q = qlist[lq];
+                const uint32_t* vrow = vq ? valid + (int64_t)q * vq : valid;  // per-query allow bitmaps (vq words each)
                 const int64_t row = (int64_t)pool_blk[e] * 32 + li;
-                ok = row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+                ok = row < nrows && ((vrow[row >> 5] >> (row & 31)) & 1u);
                 if (ok) dist = exact_dist<METRIC, VARIANT>(Qn + (int64_t)q * dpad, X + row * dpad, d);
                 pool_E[e * 32 + li] = dist;
             }
@@ -2511,7 +2548,7 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
                                                 const float* __restrict__ pool_E, const uint32_t* __restrict__ pool_vm,
                                                 const int32_t* __restrict__ rp_off, const int32_t* __restrict__ rp_tot,
                                                 uint64_t* __restrict__ rec_ids, float* __restrict__ rec_d,
-                                                int32_t* __restrict__ rec_n, int rec_cap) {
+                                                int32_t* __restrict__ rec_n, int rec_cap, int64_t vq = 0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     uint64_t* hid = reinterpret_cast<uint64_t*>(rsm);
     float* hd = reinterpret_cast<float*>(hid + k);
@@ -2524,6 +2561,7 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
     const int li = lane & 31, lh = lane >> 5;
     for (int li_ = blockIdx.x; li_ < count; li_ += gridDim.x) {
         const int q = qlist[li_];
+        const uint32_t* vrow = vq ? valid + (int64_t)q * vq : valid;  // per-query allow bitmaps (vq words each)
         const float* qv = Qn + (int64_t)q * dpad;
         const int64_t orow = by_list ? li_ : q;
         int nrec = 0;  // recorded insertions (lane 0): the parallel cross-shard replay
@@ -2618,7 +2656,7 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
                     if (j1 < 0) break;
                     const int jj = lh ? j2 : j1;
                     const int64_t row = (b0 + jj) * 32 + li;
-                    const bool ok = jj >= 0 && row < nrows && ((valid[row >> 5] >> (row & 31)) & 1u);
+                    const bool ok = jj >= 0 && row < nrows && ((vrow[row >> 5] >> (row & 31)) & 1u);
                     const float dist = ok ? exact_dist<METRIC, VARIANT>(qv, X + row * dpad, d) : 0.f;
                     uint64_t mask = __ballot(ok && (len < k || top > dist));
                     if (mask == 0) continue;

@@ -24,7 +24,12 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
     // many flagged queries with large k (integer data, C2) replay faster in the
     // one-wave kernel, which visits only blocks under the true heap top
     const int RS = k < 64 ? 2 : k < 192 ? 4 : k < 448 ? 8 : 0;
-    if (blk_pooled(idx, k, nb)) {
+    // per-query allow bitmaps (cur_vq): the pooled and the 8-wave forms bound
+    // the heap top by block upper bounds A + eps, which hold for a block with a
+    // row of the keys' row set (the union) but not necessarily one of the
+    // query's own; the one-wave replay prunes by its true heap top only
+    const bool ub_ok = idx->cur_vq == 0;
+    if (ub_ok && blk_pooled(idx, k, nb)) {
         // pooled form: bounds + candidate pool (8 waves per query), exact
         // distances over the whole grid, one-wave heap per query
         const int64_t pool_cap = idx->rp_pool;
@@ -49,7 +54,7 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
 #undef WV_RPBS
 #undef WV_RPB
         HIPCHK(hipGetLastError());
-#define WV_RPE(M, V) k_rp_exact<M, V><<<1024, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, idx->rpBlk.as<uint32_t>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpE.as<float>(), idx->rpVm.as<uint32_t>())
+#define WV_RPE(M, V) k_rp_exact<M, V><<<1024, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, idx->rpBlk.as<uint32_t>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpE.as<float>(), idx->rpVm.as<uint32_t>(), idx->cur_vq)
         switch (metric) {
         case L2: if (v5) WV_RPE(L2, AVX512); else WV_RPE(L2, AVX256); break;
         case DOT: if (v5) WV_RPE(DOT, AVX512); else WV_RPE(DOT, AVX256); break;
@@ -62,7 +67,7 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
 #define WV_RPH(M, V)                                                                                            \
     do {                                                                                                        \
         if (hlds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k_rp_heap<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hlds)); \
-        k_rp_heap<M, V><<<(unsigned)g3, 64, hlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpE.as<float>(), idx->rpVm.as<uint32_t>(), idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>(), rec_i, rec_d, rec_n, rec_cap); \
+        k_rp_heap<M, V><<<(unsigned)g3, 64, hlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpE.as<float>(), idx->rpVm.as<uint32_t>(), idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>(), rec_i, rec_d, rec_n, rec_cap, idx->cur_vq); \
     } while (0)
         switch (metric) {
         case L2: if (v5) WV_RPH(L2, AVX512); else WV_RPH(L2, AVX256); break;
@@ -74,10 +79,10 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
         return WV_OK;
     }
     if (rec_i) return set_err(WV_ERR_UNSUPPORTED, "recorded replay needs the pooled block-key replay (k < 64)");
-    if (k < 64 && nch <= RP_MAXCH && idx->replay_par) {
+    if (ub_ok && k < 64 && nch <= RP_MAXCH && idx->replay_par) {
         const int64_t grid = std::min<int64_t>(max_list, 256);
         HIPCHK(idx->qsScratch.ensure((size_t)grid * nch * 64 * sizeof(float)));
-#define WV_RPP(M, V) k_blk_replay_par<M, V><<<(unsigned)grid, 512, 0, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, idx->qsScratch.as<float>())
+#define WV_RPP(M, V) k_blk_replay_par<M, V><<<(unsigned)grid, 512, 0, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, idx->qsScratch.as<float>(), idx->cur_vq)
         switch (metric) {
         case L2: if (v5) WV_RPP(L2, AVX512); else WV_RPP(L2, AVX256); break;
         case DOT: if (v5) WV_RPP(DOT, AVX512); else WV_RPP(DOT, AVX256); break;
@@ -96,8 +101,8 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
 #define WV_RP(M, V)                                                                                             \
     do {                                                                                                        \
         if (rlds > 64 * 1024) { HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); HIPCHK(hipFuncSetAttribute((const void*)k_blk_replay<M, V, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds)); } \
-        if (idx->replay_dbg) k_blk_replay<M, V, 1><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r); \
-        else k_blk_replay<M, V><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r); \
+        if (idx->replay_dbg) k_blk_replay<M, V, 1><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, idx->cur_vq); \
+        else k_blk_replay<M, V><<<(unsigned)max_list, 64, rlds, s>>>(key, ldk, nb, eps, qinfo, idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, counters, nlist, k, kout, idx->id_base, oi, od, on, in_i, in_d, in_n, extract, by_list, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, idx->cur_vq); \
     } while (0)
     switch (metric) {
     case L2: if (v5) WV_RP(L2, AVX512); else WV_RP(L2, AVX256); break;

@@ -102,6 +102,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         if (idx->q8_R > 0) R = std::max(R, idx->q8_R);
         else R = std::max(R, 8);
     }
+    if (idx->pqa_valid) R = std::max(R, idx->pqa_R);  // per-query lists: deeper thresholds (k_blk_select mq)
     const int L = 64 * (R - 1);
     const int64_t nslots = std::max<int64_t>(1, (idx->hiwater + 32 * RB - 1) / (32 * RB));
     const int64_t nb = nslots * RB;  // 32-row blocks scanned = key row length
@@ -125,6 +126,18 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     HIPCHK(idx->qsList.ensure((size_t)2 * qc * sizeof(int32_t)));
     if (!o_flags || phase) HIPCHK(idx->qsFlags.ensure((size_t)qc * sizeof(int32_t)));
     if (phase && qc < nq) return set_err(WV_ERR_UNSUPPORTED, "two-phase shard search: batch exceeds one query chunk");
+    // per-query allow bitmaps (wv_index_search_by_vector_batch_multi_allow):
+    // `valid` is their union (the block keys are lower bounds over it, so over
+    // each query's own rows too); the exact pass and the replays read query
+    // q's bitmap, and k_blk_exact proves completeness against the select's T
+    const bool pqa = idx->pqa_valid != nullptr;
+    if (pqa && (phase != 0 || mode != 0)) return set_err(WV_ERR_UNSUPPORTED, "per-query allow lists: top-k mode only");
+    struct PqaScope {
+        wv_index* i;
+        ~PqaScope() { i->cur_vq = 0; i->cur_tq = nullptr; }
+    } pqa_scope{idx};
+    if (pqa) HIPCHK(idx->qsT.ensure((size_t)qc * sizeof(float)));
+    float* t_sel = pqa ? idx->qsT.as<float>() : nullptr;
     const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float) + (size_t)idx->dpb * sizeof(float);
     if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
     // error-bound constants: reference-order fp32 (gamma_{dpb+8}) and the MFMA's
@@ -148,6 +161,10 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         const int64_t cn_pad = round_up(cn, QS_QPB);
         if (c0 == 0) { idx->qs_last_nq = cn == nq ? cn : 0; idx->qs_last_nb = nb; idx->qs_last_ldk = ldk; }
         const float* Qn = Qn_all + c0 * idx->dpad;
+        // the exact pass's and the replays' row bitmap(s)
+        const uint32_t* exv = pqa ? idx->pqa_valid + c0 * idx->pqa_vq : valid;
+        idx->cur_vq = pqa ? idx->pqa_vq : 0;
+        idx->cur_tq = t_sel;
         float4* qinfo = idx->qsInfo.as<float4>();
         if (phase != 2) {
             k_query_split<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dpb, cn, cn_pad,
@@ -390,7 +407,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             // (C2: 0.61 vs 0.92 ms)
             const int RT = qs_R(k);
             // small batches: the split selection (P waves per query)
-            if (!list && cn <= idx->sel_split_max && RT <= RV && RT <= 8) {
+            if (!list && !pqa && cn <= idx->sel_split_max && RT <= RV && RT <= 8) {
                 const int P = (int)std::max<int64_t>(1, std::min<int64_t>(256, (nb + 2047) / 2048));
                 const int LV = 64 * (RV - 1);
                 const size_t pb = (size_t)cn * P * (k + 1) * sizeof(float);
@@ -412,15 +429,15 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                 k_sel_clamp<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>((int)cn, LV, idx->qsNc.as<int32_t>());
                 return;
             }
-            if (idx->sel_filter && RT < RV) {
-#define WV_SELF(RV, RTV) k_blk_select_f<RV, RTV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc)
+            if (idx->sel_filter && RT < RV && !pqa) {
+#define WV_SELF(RV, RTV) k_blk_select_f<RV, RTV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc, t_sel)
                 if (RV == 4) WV_SELF(4, 2);
                 else if (RT == 2) WV_SELF(8, 2);
                 else WV_SELF(8, 4);
 #undef WV_SELF
                 return;
             }
-#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc)
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc, t_sel, pqa ? exv : nullptr, pqa ? idx->pqa_vq : 0, pqa ? idx->pqa_m + c0 : nullptr)
             if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else if (RV == 8) WV_SELR(8); else WV_SELR(16);
 #undef WV_SELR
         };
@@ -429,7 +446,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         const float* capv = idx->exact_cap ? idx->qsCap.as<float>() : nullptr;
         auto exa = [&](int RV, const int32_t* list, const uint32_t* cnt, const float* eb = nullptr, int64_t ldE = 0,
                        const uint32_t* fmask = nullptr) {
-            launch_blk_exact(idx, s, RV, metric, v5, Qn, valid, (int)cn, k, kout, o_ids + c0 * kout, o_d + c0 * kout,
+            launch_blk_exact(idx, s, RV, metric, v5, Qn, exv, (int)cn, k, kout, o_ids + c0 * kout, o_d + c0 * kout,
                              o_n + c0, flags, list, cnt, eb, ldE, capv, qinfo, q8 && idx->q8_filter ? &q8f : nullptr,
                              fmask);
         };
@@ -496,7 +513,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         if (!ctr_reset) HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
         k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount, 0);
         {
-            int rc = launch_blk_replay(idx, s, a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, valid, Qn,
+            int rc = launch_blk_replay(idx, s, a.key, ldk, nb, idx->qsEps.as<float>(), qinfo, exv, Qn,
                                        idx->qsList.as<int32_t>(), idx->qscount, 0, cn, k, kout, o_ids + c0 * kout,
                                        o_d + c0 * kout, o_n + c0, nullptr, nullptr, nullptr, 1, 0);
             if (rc) return rc;

@@ -257,6 +257,19 @@ struct wv_index {
     DBuf pq8Max, pq8Mu, pq8Tmp, pq8Qc, qsCand2;
     DBuf rq8Qp, rq8Qcs, rq8Qm, rq8Fq, rq8Fm;                  // rq-8 MFMA route: query planes, flagged queries
     int rq_mfma = 1;
+    // per-query allow lists (wv_index_search_by_vector_batch_allow): the exact
+    // pass and the replays of search_qs read query q's bitmap at
+    // pqa_valid + q * pqa_vq; cur_vq / cur_tq are set only while search_qs runs
+    // in that mode (the launchers pass them to the kernels)
+    const uint32_t* pqa_valid = nullptr;
+    const int32_t* pqa_m = nullptr;  // per query: the select's threshold depth (k_blk_select mq)
+    int pqa_R = 8;                   // the select / exact list size 64 (R - 1) for them
+    int pqa = 1;
+    int64_t pqa_budget_mb = 4096;
+    int64_t pqa_vq = 0;
+    int64_t cur_vq = 0;
+    const float* cur_tq = nullptr;
+    DBuf pqaBits, pqaUnion, pqaIds, pqaQ, pqaM, qsT;
     int64_t q8_bm_min = 64;                                   // option q8_bm_min: smallest batch for the block-major int8 filter
     int rq_serial = 0;                                        // option rq_serial (debug): k_rq8_keys without the DMA lookahead                                          // option rq_mfma: rq-8 on the integer matrix cores
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima

@@ -11,6 +11,7 @@
 // cap is a multiple of 128 (the MFMA tile) so tiles never read out of bounds.
 #include "rt_index.h"
 #include <cpuid.h>
+#include <map>
 
 // ---------------------------------------------------------------------------
 // errors
@@ -770,6 +771,8 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
         idx->q8_shape = (int)value;
     }
     else if (k == "bq8") idx->bq8_opt = value ? 1 : 0;      // BQ block minima on the integer MFMA (1) or VALU (0)
+    else if (k == "pqa") idx->pqa = value ? 1 : 0;  // per-query allow lists share one block-key launch
+    else if (k == "pqa_budget_mb") idx->pqa_budget_mb = std::max<int64_t>(value, 1);
     else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only
     else if (k == "gather_max") {  // sparse allow lists up to this many rows: gathered sub-index search
         if (value < 0 || value > (1ll << 28)) return set_err(WV_ERR_INVALID, "gather_max out of range");
@@ -964,6 +967,12 @@ int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t n
     return WV_OK;
 }
 
+// the block-key route (search_qs) serves this index and k
+static bool qs_route(const wv_index* idx, int k) {
+    return (idx->qs_planes || idx->q8_only) && !idx->has_nonfinite && (idx->kernel_opt == 0 || idx->kernel_opt == 7) &&
+           !idx->force_replay && qs_R(k) > 0 && idx->metric != WV_METRIC_HAMMING;
+}
+
 // Core batch search on device queries.  Outputs [nq][kout] device arrays.
 // mode 0: kout = k, flagged queries resolved by replay; mode 1: kout = k+1,
 // flags left for the caller.  n_valid = number of scan candidates.
@@ -1004,13 +1013,12 @@ static int search_core(wv_index* idx, hipStream_t s, const float* d_qraw, int64_
     if (rc) return rc;
     const float* Qn = idx->qn.as<float>();
     // block-key path (default): planes built, finite corpus, list sizes that fit
-    if ((idx->qs_planes || idx->q8_only) && !idx->has_nonfinite && (idx->kernel_opt == 0 || idx->kernel_opt == 7) &&
-        !idx->force_replay &&
-        qs_R(k) > 0 && idx->metric != WV_METRIC_HAMMING) {
+    if (qs_route(idx, k)) {
         idx->stats.queries += (uint64_t)nq;
         idx->stats.batches++;
         return search_qs(idx, s, nq, k, mode, valid, o_ids, o_d, o_n, o_flags);
     }
+    if (idx->pqa_valid) return set_err(WV_ERR_UNSUPPORTED, "per-query allow lists: block-key route only");
     const int KP = k + idx->margin;
     const bool mfma_ok = KP <= 32 && idx->metric != WV_METRIC_HAMMING && !idx->force_replay;
     idx->stats.queries += (uint64_t)nq;
@@ -1407,6 +1415,168 @@ extern "C" int wv_index_search_by_vector_batch(wv_index* idx, const float* queri
         rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, valid + lo_t / 32, n_valid,
                          idx->oIds.as<uint64_t>(), idx->oD.as<float>(), idx->oN.as<int32_t>(), nullptr);
     }
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_counts, idx->oN.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+// Per-query allow lists in one call: query q is searched under its own list
+// allow_ids[allow_offsets[q] .. allow_offsets[q+1]) when allow_modes[q] == 1,
+// unfiltered when 0 -- the results of wv_index_search_by_vector_batch called
+// per query (Weaviate's callers each bring their filter: shard_read.go:415-424
+// -> flat/index.go:423-448 with its own helpers.AllowList).  On the block-key
+// route the batch shares one launch: the keys run over the union of the
+// queries' rows, each query's exact pass and replay over its own bitmap
+// (search_qs).  Other routes: the queries grouped by identical list, one batch
+// call per group.
+static int multi_allow_grouped(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
+                               const uint64_t* allow_ids, const int64_t* off, const int32_t* modes, uint64_t* out_ids,
+                               float* out_dists, int32_t* out_counts) {
+    std::map<std::pair<int, std::string>, std::vector<int64_t>> groups;
+    for (int64_t q = 0; q < nq; q++) {
+        std::string key;
+        if (modes[q] == 1)
+            key.assign(reinterpret_cast<const char*>(allow_ids + off[q]), (size_t)(off[q + 1] - off[q]) * sizeof(uint64_t));
+        groups[{modes[q], key}].push_back(q);
+    }
+    const int64_t kk = std::max<int32_t>(k, 0), dd = std::max<int64_t>(d, 0);
+    std::vector<float> qb;
+    std::vector<uint64_t> ids;
+    std::vector<float> ds;
+    std::vector<int32_t> cnt;
+    for (auto& g : groups) {
+        const std::vector<int64_t>& qs = g.second;
+        const int64_t n = (int64_t)qs.size();
+        qb.resize((size_t)(n * dd) + 1);
+        ids.resize((size_t)(n * kk) + 1);
+        ds.resize((size_t)(n * kk) + 1);
+        cnt.resize((size_t)n);
+        for (int64_t i = 0; i < n; i++) memcpy(&qb[(size_t)(i * dd)], queries + qs[i] * dd, (size_t)dd * sizeof(float));
+        const int64_t q0 = qs[0];
+        int rc = wv_index_search_by_vector_batch(idx, qb.data(), n, d, k, modes[q0] ? allow_ids + off[q0] : nullptr,
+                                                 modes[q0] ? off[q0 + 1] - off[q0] : 0, modes[q0], ids.data(),
+                                                 ds.data(), cnt.data());
+        if (rc) return rc;
+        for (int64_t i = 0; i < n; i++) {
+            out_counts[qs[i]] = cnt[i];
+            memcpy(out_ids + qs[i] * kk, &ids[(size_t)(i * kk)], (size_t)cnt[i] * sizeof(uint64_t));
+            memcpy(out_dists + qs[i] * kk, &ds[(size_t)(i * kk)], (size_t)cnt[i] * sizeof(float));
+        }
+    }
+    return WV_OK;
+}
+
+extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const float* queries, int64_t nq, int64_t d,
+                                                           int32_t k, const uint64_t* allow_ids,
+                                                           const int64_t* allow_offsets, const int32_t* allow_modes,
+                                                           uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (nq < 0) return set_err(WV_ERR_INVALID, "negative batch");
+    if (nq == 0) return WV_OK;
+    if (!allow_offsets || !allow_modes || !out_counts || (d > 0 && !queries))
+        return set_err(WV_ERR_INVALID, "nil argument");
+    for (int64_t q = 0; q < nq; q++) {
+        if (allow_modes[q] != 0 && allow_modes[q] != 1) return set_err(WV_ERR_INVALID, "allow mode %d", allow_modes[q]);
+        if (allow_offsets[q] < 0 || allow_offsets[q + 1] < allow_offsets[q])
+            return set_err(WV_ERR_INVALID, "allow offsets not ascending at %lld", (long long)q);
+        if (allow_modes[q] == 1 && allow_offsets[q + 1] > allow_offsets[q] && !allow_ids)
+            return set_err(WV_ERR_INVALID, "nil allow ids");
+    }
+    std::unique_lock<std::mutex> g(idx->mu);
+    const int64_t vq = round_up(std::max<int64_t>(idx->hiwater, 1), 256) / 32;  // words per query bitmap
+    const int64_t qmax = std::max<int64_t>(1, (idx->pqa_budget_mb << 20) / (vq * (int64_t)sizeof(uint32_t)));
+    const bool fast = idx->pqa && nq > 1 && idx->compression == WV_COMPRESSION_NONE && !idx->rq_bits &&
+                      idx->dims != 0 && d == idx->dims && k > 0 && idx->npresent > 0 && qs_route(idx, k);
+    if (!fast) {
+        g.unlock();
+        return multi_allow_grouped(idx, queries, nq, d, k, allow_ids, allow_offsets, allow_modes, out_ids, out_dists,
+                                   out_counts);
+    }
+    if (nq > qmax) {  // bitmaps past the budget: consecutive sub-batches
+        g.unlock();
+        for (int64_t q0 = 0; q0 < nq; q0 += qmax) {
+            const int64_t n = std::min(qmax, nq - q0);
+            int rc = wv_index_search_by_vector_batch_multi_allow(idx, queries + q0 * d, n, d, k, allow_ids,
+                                                                 allow_offsets + q0, allow_modes + q0,
+                                                                 out_ids + q0 * k, out_dists + q0 * k, out_counts + q0);
+            if (rc) return rc;
+        }
+        return WV_OK;
+    }
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = idx->stream;
+    // the unlisted queries take the present bitmap; the ids of all lists go
+    // over as given (one copy), their queries found on the device
+    std::vector<int32_t> q0list;
+    for (int64_t q = 0; q < nq; q++)
+        if (allow_modes[q] == 0) q0list.push_back((int32_t)q);
+    const int64_t nids = allow_offsets[nq] - allow_offsets[0];
+    HIPCHK(idx->pqaBits.ensure((size_t)(nq * vq) * sizeof(uint32_t)));
+    HIPCHK(idx->pqaUnion.ensure((size_t)std::max<int64_t>(idx->cap / 32, vq) * sizeof(uint32_t)));
+    // pqaQ: [nq + 1] offsets (int64), [nq] modes, [n0] unlisted queries
+    HIPCHK(idx->pqaQ.ensure((size_t)(nq + 1) * sizeof(int64_t) + (size_t)(2 * nq + 2) * sizeof(int32_t)));
+    HIPCHK(idx->pqaIds.ensure((size_t)(nids + 1) * sizeof(uint64_t)));
+    // the select's threshold depth per query: a block key is the minimum over
+    // the union's rows, this query's own with probability ~ its share rho of
+    // the union, so ~ (k+1) / rho blocks hold its k+1 nearest; twice that
+    std::vector<int32_t> hm((size_t)nq);
+    {
+        int64_t tot = 0;
+        for (int64_t q = 0; q < nq; q++) tot += allow_modes[q] ? allow_offsets[q + 1] - allow_offsets[q] : idx->npresent;
+        const double U = (double)std::max<int64_t>(1, std::min<int64_t>(tot, idx->npresent));
+        for (int64_t q = 0; q < nq; q++) {
+            const double nqr = allow_modes[q] ? (double)std::max<int64_t>(1, allow_offsets[q + 1] - allow_offsets[q])
+                                              : U;
+            const double m = 2.0 * (k + 1) * std::max(1.0, U / nqr);
+            hm[(size_t)q] = allow_modes[q] == 0 ? k + 1 : (int32_t)std::min(960.0, std::ceil(m));
+        }
+    }
+    // 448-block lists, 960 when a query wants more (k_blk_exact<16>)
+    idx->pqa_R = *std::max_element(hm.begin(), hm.end()) > 448 ? 16 : 8;
+    HIPCHK(idx->pqaM.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(idx->pqaM.p, hm.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    int64_t* d_off = idx->pqaQ.as<int64_t>();
+    int32_t* d_modes = reinterpret_cast<int32_t*>(d_off + nq + 1);
+    int32_t* d_q0 = d_modes + nq + 1;
+    uint32_t* bits = idx->pqaBits.as<uint32_t>();
+    HIPCHK(hipMemsetAsync(bits, 0, (size_t)(nq * vq) * sizeof(uint32_t), s));
+    HIPCHK(hipMemcpyAsync(d_off, allow_offsets, (size_t)(nq + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_modes, allow_modes, (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (!q0list.empty()) {
+        HIPCHK(hipMemcpyAsync(d_q0, q0list.data(), q0list.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        const int64_t n = (int64_t)q0list.size() * vq;
+        k_pqa_present<<<(unsigned)std::min<int64_t>((n + 255) / 256, 4096), 256, 0, s>>>(
+            idx->present, vq, d_q0, (int64_t)q0list.size(), bits);
+        HIPCHK(hipGetLastError());
+    }
+    if (nids > 0) {
+        HIPCHK(hipMemcpyAsync(idx->pqaIds.p, allow_ids + allow_offsets[0], (size_t)nids * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, s));
+        k_pqa_bits<<<(unsigned)((nids + 255) / 256), 256, 0, s>>>(idx->pqaIds.as<uint64_t>(), d_off, d_modes, nq,
+                                                                  idx->id_base, idx->hiwater, idx->present, vq, bits);
+        HIPCHK(hipGetLastError());
+    }
+    uint32_t* uni = idx->pqaUnion.as<uint32_t>();
+    HIPCHK(hipMemsetAsync(uni, 0, (size_t)std::max<int64_t>(idx->cap / 32, vq) * sizeof(uint32_t), s));
+    k_pqa_union<<<(unsigned)((vq + 255) / 256), 256, 0, s>>>(bits, vq, nq, uni);
+    HIPCHK(hipGetLastError());
+    HIPCHK(idx->qraw.ensure((size_t)nq * d * sizeof(float)));
+    HIPCHK(idx->oIds.ensure((size_t)nq * k * sizeof(uint64_t)));
+    HIPCHK(idx->oD.ensure((size_t)nq * k * sizeof(float)));
+    HIPCHK(idx->oN.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
+    idx->stats.last_scan_rows = (uint64_t)idx->hiwater;
+    idx->pqa_valid = bits;
+    idx->pqa_vq = vq;
+    idx->pqa_m = idx->pqaM.as<int32_t>();
+    int rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, uni, idx->npresent, idx->oIds.as<uint64_t>(),
+                         idx->oD.as<float>(), idx->oN.as<int32_t>(), nullptr);
+    idx->pqa_valid = nullptr;
+    idx->pqa_vq = 0;
+    idx->pqa_m = nullptr;
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));

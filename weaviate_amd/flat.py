@@ -398,6 +398,33 @@ class FlatIndex:
                                                       _fptr(dists), _iptr(counts)))
         return ids, dists, counts
 
+    def search_by_vector_batch_multi_allow(self, queries, k: int, allows):
+        """SearchByVector for each row of `queries`, row i under its own allow
+        list allows[i] (None = unfiltered): one batched call
+        (wv_index_search_by_vector_batch_multi_allow), results equal to
+        per-row search_by_vector_batch calls.
+        Returns (ids[nq,k] uint64, dists[nq,k] float32, counts[nq] int32)."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq, d = q.shape
+        allows = list(allows)
+        if len(allows) != nq:
+            raise WeaviateError(_lib.WV_ERR_INVALID, f"{len(allows)} allow lists for {nq} queries")
+        kk = max(int(k), 1)
+        ids = np.zeros((nq, kk), dtype=np.uint64)
+        dists = np.zeros((nq, kk), dtype=np.float32)
+        counts = np.zeros(nq, dtype=np.int32)
+        modes = np.array([0 if a is None else 1 for a in allows], dtype=np.int32)
+        parts = [np.asarray(a.ids, dtype=np.uint64) for a in allows if a is not None]
+        aids = np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros(1, np.uint64), dtype=np.uint64)
+        off = np.zeros(nq + 1, dtype=np.int64)
+        off[1:] = np.cumsum([0 if a is None else a.ids.size for a in allows])
+        check(self._l.wv_index_search_by_vector_batch_multi_allow(
+            self._h, _fptr(q), nq, d, int(k), _uptr(aids), off.ctypes.data_as(C.c_void_p), _iptr(modes), _uptr(ids),
+            _fptr(dists), _iptr(counts)))
+        return ids, dists, counts
+
     def search_by_vector(self, vector, k: int, allow: Optional[AllowList] = None):
         """flat.SearchByVector: (ids, dists) ascending, len <= k.  One query per
         call, safe to call from many threads at once: concurrent calls are
