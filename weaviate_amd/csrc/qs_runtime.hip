@@ -114,7 +114,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     HIPCHK(idx->qsQb.ensure((size_t)qc * idx->dpb * sizeof(uint16_t)));
     HIPCHK(idx->qsInfo.ensure((size_t)qc * sizeof(float4)));
     HIPCHK(idx->qsKey.ensure((size_t)qc * ldk * sizeof(float)));
-    HIPCHK(idx->qsCand.ensure((size_t)qc * std::max(L, 448) * sizeof(uint32_t)));  // 448: the overflow pass
+    // 448: the overflow pass; 960: per-query lists' second pass
+    HIPCHK(idx->qsCand.ensure((size_t)qc * std::max(L, idx->pqa_valid ? 960 : 448) * sizeof(uint32_t)));
     HIPCHK(idx->qsNc.ensure((size_t)qc * sizeof(int32_t)));
     HIPCHK(idx->qsEps.ensure((size_t)qc * sizeof(float)));
     if (q8) {
@@ -503,6 +504,20 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, olist, idx->qscount + 2, 2);
             sel(8, olist, idx->qscount + 2, nullptr);
             exa(8, olist, idx->qscount + 2);
+            HIPCHK(hipGetLastError());
+        }
+        if (pqa && R < 16) {
+            // per-query lists whose proof failed (flag 1): once more with
+            // 960-block lists at the deepest threshold before the replay (the
+            // one-wave replay walks most blocks when the key bound is wide)
+            HIPCHK(idx->pqaM2.ensure((size_t)(c0 + cn) * sizeof(int32_t)));
+            k_fill_u32<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(idx->pqaM2.as<uint32_t>() + c0, cn, 960u);
+            k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, olist, idx->qscount + 2, 1);
+            const int32_t* keep = idx->pqa_m;
+            idx->pqa_m = idx->pqaM2.as<int32_t>();  // the select reads pqa_m + c0
+            sel(16, olist, idx->qscount + 2, nullptr);
+            idx->pqa_m = keep;
+            exa(16, olist, idx->qscount + 2);
             HIPCHK(hipGetLastError());
         }
         if (idx->qs_force_flag) HIPCHK(hipMemsetAsync(flags, 1, (size_t)cn * sizeof(int32_t), s));

@@ -266,10 +266,11 @@ struct wv_index {
     int pqa_R = 8;                   // the select / exact list size 64 (R - 1) for them
     int pqa = 1;
     int64_t pqa_budget_mb = 4096;
+    int64_t pqa_split_max = 64;
     int64_t pqa_vq = 0;
     int64_t cur_vq = 0;
     const float* cur_tq = nullptr;
-    DBuf pqaBits, pqaUnion, pqaIds, pqaQ, pqaM, qsT;
+    DBuf pqaBits, pqaUnion, pqaIds, pqaQ, pqaM, pqaM2, qsT;
     int64_t q8_bm_min = 64;                                   // option q8_bm_min: smallest batch for the block-major int8 filter
     int rq_serial = 0;                                        // option rq_serial (debug): k_rq8_keys without the DMA lookahead                                          // option rq_mfma: rq-8 on the integer matrix cores
     DBuf pqZero;                                              // zero norms / qinfo for k_blk_select over ADC minima

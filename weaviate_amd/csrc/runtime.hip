@@ -772,6 +772,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     }
     else if (k == "bq8") idx->bq8_opt = value ? 1 : 0;      // BQ block minima on the integer MFMA (1) or VALU (0)
     else if (k == "pqa") idx->pqa = value ? 1 : 0;  // per-query allow lists share one block-key launch
+    else if (k == "pqa_split_max") idx->pqa_split_max = std::max<int64_t>(value, 0);  // sparse lists searched alone
     else if (k == "pqa_budget_mb") idx->pqa_budget_mb = std::max<int64_t>(value, 1);
     else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only
     else if (k == "gather_max") {  // sparse allow lists up to this many rows: gathered sub-index search
@@ -1469,6 +1470,22 @@ static int multi_allow_grouped(wv_index* idx, const float* queries, int64_t nq, 
     return WV_OK;
 }
 
+// the select's threshold depth per query (k_blk_select mq): a block key is
+// the minimum over the union's rows, this query's own with probability ~ its
+// share rho of the union, so ~ (k+1) / rho blocks hold its k+1 nearest; twice
+// that (unclamped; unlisted queries: k+1)
+static void pqa_depths(const wv_index* idx, int64_t nq, int32_t k, const int64_t* off, const int32_t* modes,
+                       std::vector<double>& m) {
+    int64_t tot = 0;
+    for (int64_t q = 0; q < nq; q++) tot += modes[q] ? off[q + 1] - off[q] : idx->npresent;
+    const double U = (double)std::max<int64_t>(1, std::min<int64_t>(tot, idx->npresent));
+    m.assign((size_t)nq, (double)(k + 1));
+    for (int64_t q = 0; q < nq; q++)
+        if (modes[q]) m[(size_t)q] = 2.0 * (k + 1) * std::max(1.0, U / (double)std::max<int64_t>(1, off[q + 1] - off[q]));
+}
+
+static thread_local bool t_pqa_nosplit = false;
+
 extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const float* queries, int64_t nq, int64_t d,
                                                            int32_t k, const uint64_t* allow_ids,
                                                            const int64_t* allow_offsets, const int32_t* allow_modes,
@@ -1495,6 +1512,56 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
         return multi_allow_grouped(idx, queries, nq, d, k, allow_ids, allow_offsets, allow_modes, out_ids, out_dists,
                                    out_counts);
     }
+    std::vector<double> md;
+    pqa_depths(idx, nq, k, allow_offsets, allow_modes, md);
+    if (!t_pqa_nosplit) {
+        // lists too sparse for the union's keys (deeper than the 960-block
+        // lists) would end in the one-wave replay, a walk over every block
+        // key: a few of them go as their own searches instead (an allow list
+        // that sparse takes the gathered sub-index route)
+        std::vector<int64_t> sp, dn;
+        for (int64_t q = 0; q < nq; q++) (md[(size_t)q] > 960.0 ? sp : dn).push_back(q);
+        if (!sp.empty() && (int64_t)sp.size() <= idx->pqa_split_max && !dn.empty()) {
+            g.unlock();
+            const int64_t kk = std::max<int32_t>(k, 0);
+            for (int pass = 0; pass < 2; pass++) {
+                const std::vector<int64_t>& qs = pass ? dn : sp;
+                const int64_t n = (int64_t)qs.size();
+                std::vector<float> qb((size_t)(n * d) + 1);
+                std::vector<int64_t> off((size_t)n + 1, 0);
+                std::vector<int32_t> modes((size_t)n);
+                std::vector<uint64_t> aid;
+                for (int64_t i = 0; i < n; i++) {
+                    const int64_t q = qs[(size_t)i];
+                    memcpy(&qb[(size_t)(i * d)], queries + q * d, (size_t)d * sizeof(float));
+                    modes[(size_t)i] = allow_modes[q];
+                    if (allow_modes[q]) aid.insert(aid.end(), allow_ids + allow_offsets[q], allow_ids + allow_offsets[q + 1]);
+                    off[(size_t)i + 1] = (int64_t)aid.size();
+                }
+                std::vector<uint64_t> oi((size_t)(n * kk) + 1);
+                std::vector<float> od((size_t)(n * kk) + 1);
+                std::vector<int32_t> oc((size_t)n);
+                int rc;
+                if (pass == 0) {
+                    rc = multi_allow_grouped(idx, qb.data(), n, d, k, aid.data(), off.data(), modes.data(), oi.data(),
+                                             od.data(), oc.data());
+                } else {
+                    t_pqa_nosplit = true;
+                    rc = wv_index_search_by_vector_batch_multi_allow(idx, qb.data(), n, d, k, aid.data(), off.data(),
+                                                                     modes.data(), oi.data(), od.data(), oc.data());
+                    t_pqa_nosplit = false;
+                }
+                if (rc) return rc;
+                for (int64_t i = 0; i < n; i++) {
+                    const int64_t q = qs[(size_t)i];
+                    out_counts[q] = oc[(size_t)i];
+                    memcpy(out_ids + q * kk, &oi[(size_t)(i * kk)], (size_t)oc[(size_t)i] * sizeof(uint64_t));
+                    memcpy(out_dists + q * kk, &od[(size_t)(i * kk)], (size_t)oc[(size_t)i] * sizeof(float));
+                }
+            }
+            return WV_OK;
+        }
+    }
     if (nq > qmax) {  // bitmaps past the budget: consecutive sub-batches
         g.unlock();
         for (int64_t q0 = 0; q0 < nq; q0 += qmax) {
@@ -1519,21 +1586,8 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
     // pqaQ: [nq + 1] offsets (int64), [nq] modes, [n0] unlisted queries
     HIPCHK(idx->pqaQ.ensure((size_t)(nq + 1) * sizeof(int64_t) + (size_t)(2 * nq + 2) * sizeof(int32_t)));
     HIPCHK(idx->pqaIds.ensure((size_t)(nids + 1) * sizeof(uint64_t)));
-    // the select's threshold depth per query: a block key is the minimum over
-    // the union's rows, this query's own with probability ~ its share rho of
-    // the union, so ~ (k+1) / rho blocks hold its k+1 nearest; twice that
     std::vector<int32_t> hm((size_t)nq);
-    {
-        int64_t tot = 0;
-        for (int64_t q = 0; q < nq; q++) tot += allow_modes[q] ? allow_offsets[q + 1] - allow_offsets[q] : idx->npresent;
-        const double U = (double)std::max<int64_t>(1, std::min<int64_t>(tot, idx->npresent));
-        for (int64_t q = 0; q < nq; q++) {
-            const double nqr = allow_modes[q] ? (double)std::max<int64_t>(1, allow_offsets[q + 1] - allow_offsets[q])
-                                              : U;
-            const double m = 2.0 * (k + 1) * std::max(1.0, U / nqr);
-            hm[(size_t)q] = allow_modes[q] == 0 ? k + 1 : (int32_t)std::min(960.0, std::ceil(m));
-        }
-    }
+    for (int64_t q = 0; q < nq; q++) hm[(size_t)q] = (int32_t)std::min(960.0, std::ceil(md[(size_t)q]));
     // 448-block lists, 960 when a query wants more (k_blk_exact<16>)
     idx->pqa_R = *std::max_element(hm.begin(), hm.end()) > 448 ? 16 : 8;
     HIPCHK(idx->pqaM.ensure((size_t)nq * sizeof(int32_t)));
