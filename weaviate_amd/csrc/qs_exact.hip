@@ -30,14 +30,17 @@ void launch_blk_exact(wv_index* idx, hipStream_t s, int RV, int metric, bool v5,
     default: if (v5) WV_EXR(RV, COSINE, AVX512); else WV_EXR(RV, COSINE, AVX256); break; \
     }
     if (RV == 2) { WV_EXM(2); } else if (RV == 4) { WV_EXM(4); } else if (RV == 8) { WV_EXM(8); }
-    else {  // k + 1 <= 960: 960-block lists, never block-major (9-bit list positions)
-#define WV_EX16(M, V) k_blk_exact<16, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, nullptr, idx->cur_vq, idx->cur_tq, idx->qsEps.as<float>())
-        switch (metric) {
-        case L2: if (v5) WV_EX16(L2, AVX512); else WV_EX16(L2, AVX256); break;
-        case DOT: if (v5) WV_EX16(DOT, AVX512); else WV_EX16(DOT, AVX256); break;
-        default: if (v5) WV_EX16(COSINE, AVX512); else WV_EX16(COSINE, AVX256); break;
+    else {  // k + 1 <= 960 / 1984 / 4032: never block-major (9-bit list positions)
+#define WV_EXB(RB, M, V) k_blk_exact<RB, M, V, false><<<(unsigned)cn, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), cn, k, kout, idx->id_base, o_ids, o_d, o_n, flags, list, cnt, nullptr, 0, capv, qinfo, Xb, idx->dpb, idx->xnorm2, idx->qsmax, idx->d_maxn2, gd, gacc_r, f8, nullptr, idx->cur_vq, idx->cur_tq, idx->qsEps.as<float>())
+#define WV_EXBM(RB)                                                                     \
+        switch (metric) {                                                               \
+        case L2: if (v5) WV_EXB(RB, L2, AVX512); else WV_EXB(RB, L2, AVX256); break;    \
+        case DOT: if (v5) WV_EXB(RB, DOT, AVX512); else WV_EXB(RB, DOT, AVX256); break; \
+        default: if (v5) WV_EXB(RB, COSINE, AVX512); else WV_EXB(RB, COSINE, AVX256); break; \
         }
-#undef WV_EX16
+        if (RV == 16) { WV_EXBM(16); } else if (RV == 32) { WV_EXBM(32); } else { WV_EXBM(64); }
+#undef WV_EXBM
+#undef WV_EXB
     }
 #undef WV_EXM
 #undef WV_EXR

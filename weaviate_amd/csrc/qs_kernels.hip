@@ -995,8 +995,9 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
     const float mk = t.key_at(me);
     const float M = qs_key_to_a(metric, mk, qi.x);
     float T = mk == __builtin_inff() ? __builtin_inff() : M + 2.0005f * eps;
-    if (mq) {  // a threshold the list can hold: below the (L+1)-th smallest A
-        const float kl = t.key_at(L);
+    if (mq) {  // a threshold the list can hold: below the L-th smallest A (rows
+               // 0..R-2 hold exactly the L smallest keys; row R-1 is not kept exact)
+        const float kl = t.key_at(L - 1);
         if (kl < __builtin_inff()) T = fminf(T, qs_next_down(qs_key_to_a(metric, kl, qi.x)));
     }
     int nc = 0;

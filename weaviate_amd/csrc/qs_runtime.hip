@@ -6,6 +6,11 @@
 // candidate-list rows R (L = 64 (R - 1) blocks, a power-of-two bitonic width
 // 64 R): k + 1 <= 960 stays on the block-key path
 int qs_R(int k) { return k + 1 <= 64 ? 2 : k + 1 <= 192 ? 4 : k + 1 <= 448 ? 8 : k + 1 <= 960 ? 16 : 0; }
+// the single-index search goes further: 1984- and 4032-block lists (k + 1 <= 4032)
+int qs_R_flat(int k) {
+    const int r = qs_R(k);
+    return r ? r : k + 1 <= 1984 ? 32 : k + 1 <= 4032 ? 64 : 0;
+}
 
 // the candidate lists (cand [cn][L], ncand, unflagged queries) inverted per
 // 32-row block: bmOff [nb + 1] offsets of bmPairs (query << 9 | list position).
@@ -96,7 +101,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     const int NC8 = idx->dpb8 / 64;
     const int RB8 = idx->dpb8 <= 768 ? 2 : 1;
     const int RB = q8 ? RB8 : qs_rb(NK);
-    int R = qs_R(k);
+    int R = qs_R_flat(k);
     if (q8) {  // the int8 bound is wider: 448-block lists (option q8_R; C3: ~110 candidate blocks
                // per query, R = 4 sent a few percent to the overflow pass, profiles/r04_c3ab1_*)
         if (idx->q8_R > 0) R = std::max(R, idx->q8_R);
@@ -406,7 +411,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             // 448-block lists at k < 64: C3 select 2.81 -> 2.14 ms, 1.25M-row
             // shard 1.42 -> 0.59 ms); at RT == RV the sorted-list form is faster
             // (C2: 0.61 vs 0.92 ms)
-            const int RT = qs_R(k);
+            const int RT = qs_R_flat(k);
             // small batches: the split selection (P waves per query)
             if (!list && !pqa && cn <= idx->sel_split_max && RT <= RV && RT <= 8) {
                 const int P = (int)std::max<int64_t>(1, std::min<int64_t>(256, (nb + 2047) / 2048));
@@ -439,7 +444,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                 return;
             }
 #define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc, t_sel, pqa ? exv : nullptr, pqa ? idx->pqa_vq : 0, pqa ? idx->pqa_m + c0 : nullptr)
-            if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else if (RV == 8) WV_SELR(8); else WV_SELR(16);
+            if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else if (RV == 8) WV_SELR(8); else if (RV == 16) WV_SELR(16);
+            else if (RV == 32) WV_SELR(32); else WV_SELR(64);
 #undef WV_SELR
         };
         // per query an upper bound of the (k+1)-th smallest exact distance: the

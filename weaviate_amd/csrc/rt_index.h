@@ -335,6 +335,7 @@ void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t l
                       unsigned char* pm = nullptr);
 // qs_runtime.hip
 int qs_R(int k);
+int qs_R_flat(int k);
 int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid, uint64_t* o_ids,
               float* o_d, int32_t* o_n, int32_t* o_flags, int phase = 0, float* topA = nullptr,
               const float* gA = nullptr, const float* gE = nullptr, int W = 0);

@@ -971,7 +971,7 @@ int prepare_queries(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t n
 // the block-key route (search_qs) serves this index and k
 static bool qs_route(const wv_index* idx, int k) {
     return (idx->qs_planes || idx->q8_only) && !idx->has_nonfinite && (idx->kernel_opt == 0 || idx->kernel_opt == 7) &&
-           !idx->force_replay && qs_R(k) > 0 && idx->metric != WV_METRIC_HAMMING;
+           !idx->force_replay && qs_R_flat(k) > 0 && idx->metric != WV_METRIC_HAMMING;
 }
 
 // Core batch search on device queries.  Outputs [nq][kout] device arrays.
