@@ -18,6 +18,9 @@ for s0 in range(0, n, 1 << 20):
     idx.add_batch(np.arange(s0, e, dtype=np.uint64), data[s0:e])
 q = gen(2, B)
 idx.set_option("timing", 1)
+for kv in sys.argv[5:]:
+    key, val = kv.split("=")
+    idx.set_option(key, int(val))
 out = {}
 for k in [int(x) for x in sys.argv[4].split(",")]:
     idx.search_by_vector_batch(q, k)

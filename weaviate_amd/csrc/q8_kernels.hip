@@ -963,15 +963,21 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey32(Q8Args a) {
 // part 1).  The cross-lane combine and key store of a block are deferred into
 // the next block's part 0.  Keys are k_q8_blockkey's, so select / exact /
 // replay apply unchanged.
+// NP > 2 column parts (3072 < d <= 6144: NP x 16 chunks): the fragments of
+// 16 queries take up to 384 registers, so NW = 4 waves (one per SIMD, 64
+// queries per workgroup) own the unified VGPR/AGPR file; the block's
+// accumulators carry through all NP parts, the last one reduces the block and
+// carries the valid word, scale and norms; the key store of a block rides in
+// the next block's part 0 as before.
 // ---------------------------------------------------------------------------
-template <int NCS, bool ISL2>
-__global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
-    constexpr int NC = 2 * NCS;                     // 64-column chunks per block
+template <int NCS, bool ISL2, int NP = 2, int NW = 8>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 2 : 1) void k_q8_blockkey_cp(Q8Args a) {
+    constexpr int NC = NP * NCS;                    // 64-column chunks per block
     constexpr int NPB = 2 * NC;                     // 1 KiB pieces per block
     constexpr int SPC = 2 * NCS;                    // pieces per step (one column part)
     constexpr int SLOT = SPC * 1024;
-    constexpr int P = SPC / 8;                      // pieces per wave per step
-    static_assert(SPC % 8 == 0, "a part's pieces split over 8 waves");
+    constexpr int P = SPC / NW;                     // pieces per wave per step
+    static_assert(SPC % NW == 0, "a part's pieces split over the waves");
     constexpr int64_t TILE_B = (int64_t)NPB * 8192;  // bytes per 256-row tile of a plane
     constexpr int P0 = P + 2 + (ISL2 ? 1 : 0);      // vector-memory ops per group, per wave
     static_assert(P0 < NCS, "the deferred key store follows the step's DMA pieces");
@@ -988,13 +994,13 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
     const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;  // a span's groups share an XCD
     const int span = logical / a.nqg, grp = logical % a.nqg;
 
-    // the wave's 16 queries (group grp of 128 = half grp & 1 of a 256-row query tile)
+    // the wave's 16 queries (group grp of 16 NW rows of the 256-row query tiles)
     i32x4_t Qf[NC];
-    const int64_t q0 = (int64_t)grp * 128 + wave * 16;
+    const int64_t q0 = (int64_t)grp * (16 * NW) + wave * 16;
     {
         const int j = lane & 15, kq = lane >> 4;
-        const unsigned char* qp = a.Q8 + (int64_t)(grp >> 1) * TILE_B + (kq >> 1) * 8192 +
-                                  ((grp & 1) * 128 + wave * 16 + j) * 32 + 16 * (kq & 1);
+        const int64_t qr = q0 + j;
+        const unsigned char* qp = a.Q8 + (qr >> 8) * TILE_B + (kq >> 1) * 8192 + (qr & 255) * 32 + 16 * (kq & 1);
 #pragma unroll
         for (int c = 0; c < NC; c++) Qf[c] = *reinterpret_cast<const i32x4_t*>(qp + (2 * c) * 8192);
     }
@@ -1005,7 +1011,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
     int64_t s1 = s0 + a.slots_per_span;
     if (s1 > a.nslots) s1 = a.nslots;
     const int nblk = s1 > s0 ? (int)(s1 - s0) : 0;
-    const int nsteps = 2 * nblk;
+    const int nsteps = NP * nblk;
 
     const uint32_t src_lane = (uint32_t)(16 * lane);
     const unsigned ring = lds_addr(qsm);
@@ -1021,7 +1027,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
     auto issue_piece = [&](auto ptc, int j, int u, int slot) {
         constexpr int PT = decltype(ptc)::value;
         if (j < P) {
-            const int pi = wave + 8 * j;
+            const int pi = wave + NW * j;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(size_t)(ring + (unsigned)(slot * SLOT + pi * 1024)),
                                                      16, src_lane, ioff + (uint32_t)((PT * SPC + pi) * 8192), 0, 0);
         } else if (j == P) {
@@ -1036,7 +1042,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
                 __builtin_amdgcn_global_load_lds(a.xnorm2 + igb * 32 + 4 * lane,
                                                  (lds_ptr_t)(size_t)(xnring + (unsigned)((u & 3) * 128)), 16, 0, 0);
         }
-        if (PT == 1 && j == P0 - 1) {  // the block's second part issued: on to the next block
+        if (PT == NP - 1 && j == P0 - 1) {  // the block's last part issued: on to the next block
             igb += 1;
             ioff += 1024;
             if ((igb & 7) == 0) ioff += (uint32_t)(TILE_B - 8192);
@@ -1048,7 +1054,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
     i32x4_t acc[2];    // [row half m]: element r is row 16m + 4g + r (g = lane >> 4) of query lane & 15
     if (nsteps > 0) {
         static_for<0, P0>([&](auto jc) { issue_piece(std::integral_constant<int, 0>{}, decltype(jc)::value, 0, 0); });
-        static_for<0, P0>([&](auto jc) { issue_piece(std::integral_constant<int, 1>{}, decltype(jc)::value, 1, 1); });
+        static_for<0, P0>([&](auto jc) { issue_piece(std::integral_constant<int, 1 % NP>{}, decltype(jc)::value, 1, 1); });
         qs_wait_vm_c<P0>();  // group 0 landed, group 1 may stay in flight
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -1078,9 +1084,10 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
     };
     int cur = 0;
     for (int t = 0; t < nblk; t++) {
-        static_for<0, 2>([&](auto pc) {
+        static_for<0, NP>([&](auto pc) {
             constexpr int PT = decltype(pc)::value;
-            const int u = 2 * t + PT;
+            constexpr int PG = (PT + 2) % NP;  // the part of group u + 2
+            const int u = NP * t + PT;
             const int nxt = cur == NBUF - 1 ? 0 : cur + 1;
             const int gslot = cur == 0 ? NBUF - 1 : cur - 1;  // slot of group u+2
             const unsigned sbase = ring + (unsigned)(cur * SLOT) + l16;
@@ -1091,7 +1098,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
             f32x4_t xa = {0.f, 0.f, 0.f, 0.f}, xb = {0.f, 0.f, 0.f, 0.f};
             static_for<0, NCS>([&](auto ttc) {
                 constexpr int tt = decltype(ttc)::value;
-                if constexpr (PT == 1 && tt == X0) {  // the block's valid word, scale (+ L2 norms)
+                if constexpr (PT == NP - 1 && tt == X0) {  // the block's valid word, scale (+ L2 norms)
                     asm volatile("ds_read_b32 %0, %1" : "=v"(vw) : "v"(vring + sm * 16u));
                     asm volatile("ds_read_b32 %0, %1" : "=v"(sbv) : "v"(sring + sm * 16u));
                     if constexpr (ISL2) {
@@ -1106,9 +1113,9 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
                     B2[(tt + 1) & 1][1] = lds_ld16_o<o1 + 512>(sbase);
                 }
                 constexpr int ahead = tt + 1 < NCS ? 1 : 0;
-                qs_wait_lgkm<2 * ahead + ((PT == 1 && tt == X0) ? XE : 0)>();
+                qs_wait_lgkm<2 * ahead + ((PT == NP - 1 && tt == X0) ? XE : 0)>();
                 asm volatile("" : "+v"(B2[tt & 1][0]), "+v"(B2[tt & 1][1]));
-                if constexpr (PT == 1 && tt == X0 + 1) {  // the extras are older than chunk tt's reads
+                if constexpr (PT == NP - 1 && tt == X0 + 1) {  // the extras are older than chunk tt's reads
                     if constexpr (ISL2) asm volatile("" : "+v"(vw), "+v"(sbv), "+v"(xa), "+v"(xb));
                     else asm volatile("" : "+v"(vw), "+v"(sbv));
                 }
@@ -1121,13 +1128,13 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
                         acc[m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B2[tt & 1][m], Qf[PT * NCS + tt], acc[m], 0, 0, 0);
                 }
                 if constexpr (tt < P0) {
-                    if (dma) issue_piece(pc, tt, u + 2, gslot);
+                    if (dma) issue_piece(std::integral_constant<int, PG>{}, tt, u + 2, gslot);
                 }
                 if constexpr (PT == 0 && tt == P0) {
                     if (t > 0) finish(pend, psb, s0 + t - 1);
                 }
             });
-            if constexpr (PT == 1) {  // the block's reduction over its 32 rows
+            if constexpr (PT == NP - 1) {  // the block's reduction over its 32 rows
                 const uint32_t w = __builtin_amdgcn_readfirstlane(vw);
                 const float sbf = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sbv)));
                 const uint32_t vl = w >> (4 * ((lane >> 4) & 3));
@@ -1158,9 +1165,10 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey_cp(Q8Args a) {
             // ---- end of the step: the next group must have landed (every wave) ----
             if (u + 1 < nsteps) {
                 // this wave's vector-memory ops after group u+1, in issue order: the
-                // store of step u-1 or u (one per block, in part 0, from block 1 on),
-                // the pieces of group u+2
-                qs_wait_vm((t > 0 ? 1 : 0) + (dma ? P0 : 0));
+                // store of step u-1 or u (one per block, in part 0, from block 1 on:
+                // after group u+1 when step u or u-1 is a part 0), the pieces of
+                // group u+2
+                qs_wait_vm((t > 0 && (PT == 0 || PT == 1) ? 1 : 0) + (dma ? P0 : 0));
                 __builtin_amdgcn_s_barrier();  // slot cur is free; slot nxt has landed for every wave
                 __builtin_amdgcn_sched_barrier(0);
                 B2[0][0] = lds_ld16_o<0>(ring + (unsigned)(nxt * SLOT) + l16);

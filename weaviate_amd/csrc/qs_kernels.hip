@@ -995,11 +995,21 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
     const float mk = t.key_at(me);
     const float M = qs_key_to_a(metric, mk, qi.x);
     float T = mk == __builtin_inff() ? __builtin_inff() : M + 2.0005f * eps;
-    if (mq) {  // a threshold the list can hold: below the L-th smallest A (rows
-               // 0..R-2 hold exactly the L smallest keys; row R-1 is not kept exact)
+    // a threshold the list can hold: below the L-th smallest A (rows 0..R-2
+    // hold exactly the L smallest keys; row R-1 is not kept exact).  Always
+    // for per-query lists (mq); else (t_out) instead of the overflow flag when
+    // more than the list would qualify: k_blk_exact then proves the list
+    // complete against T (its (k+1)-th exact distance <= T - eps) or flags it
+    bool conv = false;
+    if (mq || t_out) {
         const float kl = t.key_at(L - 1);
-        if (kl < __builtin_inff()) T = fminf(T, qs_next_down(qs_key_to_a(metric, kl, qi.x)));
+        const float al = qs_key_to_a(metric, kl, qi.x);
+        if (kl < __builtin_inff() && (mq || al <= T)) {
+            conv = !mq && qs_next_down(al) < T;
+            T = fminf(T, qs_next_down(al));
+        }
     }
+    const bool proof = mq || conv;  // completeness against T in k_blk_exact
     int nc = 0;
 #pragma unroll
     for (int r = 0; r < R - 1; r++) {
@@ -1017,11 +1027,12 @@ __global__ __launch_bounds__(256) void k_blk_select(const float* __restrict__ ke
         // or above T - eps cannot pass k_blk_exact's completeness test anyway)
         if (cap_out)
             cap_out[q] = mk == __builtin_inff() ? __builtin_inff()
-                         : mq ? T - eps : qs_next_up(M + 1.001f * eps);
-        if (t_out) t_out[q] = T;  // per-query allow lists: k_blk_exact's completeness bound
+                         : proof ? T - eps : qs_next_up(M + 1.001f * eps);
+        // k_blk_exact's completeness bound (+inf: the 2-eps argument holds)
+        if (t_out) t_out[q] = proof ? T : __builtin_inff();
         // the L-th entry also qualifies: blocks beyond the list may too
-        // (mq: T is below every block past the list)
-        flags[q] = ((nc >= L && !mq) || qi.w != 0.f) ? 2 : 0;
+        // (proof: T is below every block past the list)
+        flags[q] = ((nc >= L && !proof) || qi.w != 0.f) ? 2 : 0;
     }
     if (topA) {  // sharded phase 1: this shard's k+1 smallest block-key A values
 #pragma unroll
@@ -1159,7 +1170,7 @@ __global__ __launch_bounds__(256) void k_blk_select_f(const float* __restrict__ 
         eps_out[q] = eps;
         if (cap_out)
             cap_out[q] = mk == __builtin_inff() ? __builtin_inff() : qs_next_up(M + 1.001f * eps);
-        if (t_out) t_out[q] = T;
+        if (t_out) t_out[q] = __builtin_inff();  // no lowered threshold: the 2-eps argument holds
         flags[q] = (full || qi.w != 0.f) ? 2 : 0;
     }
     if (topA) {  // sharded phase 1: this shard's k+1 smallest block-key A values
@@ -1630,7 +1641,9 @@ __global__ __launch_bounds__(256) void k_blk_exact(const float* __restrict__ X, 
     // complete when it holds k+1 rows and its (k+1)-th is <= T - eps (the
     // rounded difference one ulp down: below the exact one); else the replay
     // decides.  T = inf: every block with a union row is listed.
-    if (vq && inc && tq[q] < __builtin_inff())
+    // The same test for a list whose threshold was lowered below the L-th key
+    // (k_blk_select: more blocks than the list qualified).
+    if (tq && inc && tq[q] < __builtin_inff())
         inc = nvalid >= k + 1 && t.key_at(k) <= qs_next_down(tq[q] - qeps[q]);
     if (!inc) {
         if (lane == 0) flags[q] = 1;

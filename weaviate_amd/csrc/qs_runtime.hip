@@ -98,6 +98,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     // (above 1536 dims the int8 planes are the only ones: k_q8_blockkey_cp, 128-query groups)
     const bool q8 = idx->q8_planes && (idx->q8_opt || idx->q8_only);
     const bool q8cp = q8 && idx->q8_only;
+    const bool q8wide = q8cp && idx->dpb8 > Q8_MAX_DPB;  // NP = dpb8 / 1024 column parts, 64-query groups
     const int NC8 = idx->dpb8 / 64;
     const int RB8 = idx->dpb8 <= 768 ? 2 : 1;
     const int RB = q8 ? RB8 : qs_rb(NK);
@@ -142,8 +143,11 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         wv_index* i;
         ~PqaScope() { i->cur_vq = 0; i->cur_tq = nullptr; }
     } pqa_scope{idx};
-    if (pqa) HIPCHK(idx->qsT.ensure((size_t)qc * sizeof(float)));
-    float* t_sel = pqa ? idx->qsT.as<float>() : nullptr;
+    // the select's completeness bounds: per-query lists, and lists whose
+    // threshold the select lowered (phase 0 only: the sharded phases keep the
+    // 2-eps argument their global threshold relies on)
+    HIPCHK(idx->qsT.ensure((size_t)qc * sizeof(float)));
+    float* t_sel = (pqa || (phase == 0 && idx->sel_lower)) ? idx->qsT.as<float>() : nullptr;
     const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float) + (size_t)idx->dpb * sizeof(float);
     if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
     // error-bound constants: reference-order fp32 (gamma_{dpb+8}) and the MFMA's
@@ -201,7 +205,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // column parts per ring step: dpb 1024 -> 4 slots of 32 KiB, 1536 -> 3 of 48 KiB
         const bool w4 = !q8 && idx->dpb > QS_W4_DPB;
         const int w4_nb = NK == 64 ? 4 : 3;
-        a.nqg = (int)(cn_pad / ((w4 || q8cp) ? 128 : QS_QPB));
+        a.nqg = (int)(cn_pad / (q8wide ? 64 : (w4 || q8cp) ? 128 : QS_QPB));
         int64_t nspans = 256 / std::gcd(256, a.nqg);
         while ((int64_t)a.nqg * nspans < 256) nspans *= 2;
         if (idx->spans_opt > 0) nspans = idx->spans_opt;
@@ -220,7 +224,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         a.slots_per_span = (int)sps;
         a.nspans = (int)((nslots + sps - 1) / sps);
         const bool l2 = metric == L2;
-        const size_t lds = q8cp ? (size_t)3 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * 128 : 0)
+        const size_t lds = q8wide ? (size_t)3 * 32 * 1024 + 1024 + (l2 ? (size_t)4 * 512 : 0)
+                         : q8cp ? (size_t)3 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * 128 : 0)
                          : q8 ? (size_t)3 * RB * 2 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * RB * 128 : 0)
                          : w4 ? (size_t)w4_nb * (NK / 4) * 2048 + 256 + (l2 ? (size_t)4 * 4 * 128 : 0)
                               : (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
@@ -353,14 +358,23 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey_cp<NCSV, L2V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
         k_q8_blockkey_cp<NCSV, L2V><<<grid, 512, lds, s>>>(q8a);                                               \
     } while (0)
+#define WV_Q8CPW(NPV, L2V)                                                                                     \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey_cp<16, L2V, NPV, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey_cp<16, L2V, NPV, 4><<<grid, 256, lds, s>>>(q8a);                                         \
+    } while (0)
 #define WV_Q8CPN(L2V)                                  \
     switch (NC8) {                                     \
     case 32: WV_Q8CP(16, L2V); break;                  \
     case 40: WV_Q8CP(20, L2V); break;                  \
-    default: WV_Q8CP(24, L2V); break;                  \
+    case 48: WV_Q8CP(24, L2V); break;                  \
+    case 64: WV_Q8CPW(4, L2V); break;                  \
+    case 80: WV_Q8CPW(5, L2V); break;                  \
+    default: WV_Q8CPW(6, L2V); break;                  \
     }
                 if (l2) { WV_Q8CPN(true); } else { WV_Q8CPN(false); }
 #undef WV_Q8CPN
+#undef WV_Q8CPW
 #undef WV_Q8CP
             } else if (l2) { WV_Q8N(true); } else { WV_Q8N(false); }
         } else if (w4) {
@@ -433,6 +447,9 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                 k_sel_collect<<<gp, 64, 0, s>>>(a.key, ldk, nb, P, metric, qinfo_sel, Tq, idx->qsCand.as<uint32_t>(), LV,
                                                 idx->qsNc.as<int32_t>(), flags);
                 k_sel_clamp<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>((int)cn, LV, idx->qsNc.as<int32_t>());
+                if (t_sel)  // no lowered threshold (+inf): the 2-eps argument holds
+                    k_fill_u32<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(reinterpret_cast<uint32_t*>(t_sel), cn,
+                                                                            0x7f800000u);
                 return;
             }
             if (idx->sel_filter && RT < RV && !pqa) {

@@ -263,7 +263,8 @@ struct wv_index {
     // in that mode (the launchers pass them to the kernels)
     const uint32_t* pqa_valid = nullptr;
     const int32_t* pqa_m = nullptr;  // per query: the select's threshold depth (k_blk_select mq)
-    int pqa_R = 8;                   // the select / exact list size 64 (R - 1) for them
+    int pqa_R = 8;
+    int sel_lower = 0;  // k_blk_select lowers an overflowing threshold instead of flagging                   // the select / exact list size 64 (R - 1) for them
     int pqa = 1;
     int64_t pqa_budget_mb = 4096;
     int64_t pqa_split_max = 64;
@@ -316,7 +317,8 @@ static void invalidate_batch(wv_index* idx) {
 // to 768 dims; k_qs_blockkey_w4 (one wave per SIMD, query fragments in the
 // 512-entry register file, dpb 1024 or 1536) up to 1536
 constexpr int QS_MAX_DPB = 1536;
-constexpr int Q8_MAX_DPB = 3072;  // int8-only block-key planes (k_q8_blockkey_cp)
+constexpr int Q8_MAX_DPB = 3072;  // int8-only block-key planes (k_q8_blockkey_cp), two column parts
+constexpr int Q8_WIDE_DPB = 6144;  // ... NP = dpb8 / 1024 parts of 16 chunks above 3072
 constexpr int QS_W4_DPB = 768;  // dpb above this: k_qs_blockkey_w4
 
 // ---------------------------------------------------------------------------

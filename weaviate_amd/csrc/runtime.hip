@@ -69,10 +69,11 @@ static void set_dims(wv_index* idx, int64_t d) {
     idx->dpb8 = (int)(d <= 768 ? round_up(d, 128) : round_up(d, 256));
     idx->q8_planes = (idx->qs_planes && d > 384 && idx->dpb8 <= 1536) ? 1 : 0;
     // above 1536 dims: int8 planes only (no bf16 plane), 512-column multiples up
-    // to 3072 -- two column parts of 16 / 20 / 24 chunks per block (k_q8_blockkey_cp)
-    idx->q8_only = (idx->use_qs && !idx->qs_planes && d > 1536 && round_up(d, 512) <= Q8_MAX_DPB) ? 1 : 0;
+    // to 3072 -- two column parts of 16 / 20 / 24 chunks per block (k_q8_blockkey_cp);
+    // 1024-column multiples up to 6144 -- 4 / 5 / 6 parts of 16 chunks
+    idx->q8_only = (idx->use_qs && !idx->qs_planes && d > 1536 && round_up(d, 1024) <= Q8_WIDE_DPB) ? 1 : 0;
     if (idx->q8_only) {
-        idx->dpb8 = (int)round_up(d, 512);
+        idx->dpb8 = (int)(round_up(d, 512) <= Q8_MAX_DPB ? round_up(d, 512) : round_up(d, 1024));
         idx->q8_planes = 1;
     }
     if (idx->compression == WV_COMPRESSION_BQ) {  // +-1 code plane: 7..24 words (448..1536 bits)
@@ -771,7 +772,8 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
         idx->q8_shape = (int)value;
     }
     else if (k == "bq8") idx->bq8_opt = value ? 1 : 0;      // BQ block minima on the integer MFMA (1) or VALU (0)
-    else if (k == "pqa") idx->pqa = value ? 1 : 0;  // per-query allow lists share one block-key launch
+    else if (k == "pqa") idx->pqa = value ? 1 : 0;
+    else if (k == "sel_lower") idx->sel_lower = value ? 1 : 0;  // per-query allow lists share one block-key launch
     else if (k == "pqa_split_max") idx->pqa_split_max = std::max<int64_t>(value, 0);  // sparse lists searched alone
     else if (k == "pqa_budget_mb") idx->pqa_budget_mb = std::max<int64_t>(value, 1);
     else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only
