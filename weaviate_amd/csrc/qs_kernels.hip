@@ -111,6 +111,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_mul_f32 / v_pk_add_f32)
 template <int OFF>
 __device__ __forceinline__ f32x4_t lds_ld4f_o(unsigned base) {
     f32x4_t v;

@@ -290,6 +290,59 @@ __global__ __launch_bounds__(512, 2) void k_rq8_keys(RQ8Args a) {
     #pragma unroll
             for (int r = 0; r < 4; r++) fine = fine && __int_as_float(mt[m][r][BITS == 8 ? 3 : 1]) <= FINE;
         const int mode = (vw == 0xFFFFFFFFu && __all(fine) && !(a.dbg_serial & 4)) ? (l2 ? 0 : 1) : 2;
+        if (mode != 2 && !(a.dbg_serial & 32)) {
+            // the fast forms on packed fp32 (v_pk_mul_f32 / v_pk_add_f32: the
+            // two query halves n = 0, 1 of a row in one instruction, each
+            // element rounded as the scalar op would).  cosine / dot: fl(fcos -
+            // est) falls as est grows, so the block's minimum is fcos - (the
+            // maximum est) and the subtraction moves out of the row loop.
+            const f32x2_t yx = {ym[0].x, ym[1].x}, yz = {ym[0].z, ym[1].z};
+            const f32x2_t yyv = {BITS == 8 ? ym[0].y : ym[0].x, BITS == 8 ? ym[1].y : ym[1].x};
+            const f32x2_t ynv = {BITS == 8 ? ym[0].w : ym[0].y, BITS == 8 ? ym[1].w : ym[1].y};
+            f32x2_t best = {mode == 0 ? __builtin_inff() : -__builtin_inff(), mode == 0 ? __builtin_inff() : -__builtin_inff()};
+    #pragma unroll
+            for (int m = 0; m < 2; m++)
+    #pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    f32x2_t est;
+                    float xnorm;
+                    if constexpr (BITS == 8) {
+                        const float xl = __int_as_float(mt[m][r][0]);
+                        const float xs = __int_as_float(mt[m][r][1]);
+                        const float xz = __int_as_float(mt[m][r][2]);
+                        xnorm = __int_as_float(mt[m][r][3]);
+                        const float a1 = fD * xl;
+                        const int kx = (int)(128u * (uint32_t)cs[m][r]) - 16384 * D;
+                        const f32x2_t dotv = {(float)(uint32_t)(acc[m][0][r] + kx), (float)(uint32_t)(acc[m][1][r] + kx)};
+                        const f32x2_t e1 = f32x2_t{a1, a1} * yx;
+                        const f32x2_t e2 = f32x2_t{xl, xl} * yz;
+                        const f32x2_t e3 = yx * f32x2_t{xz, xz};
+                        f32x2_t e4 = f32x2_t{xs, xs} * yyv;
+                        e4 = e4 * dotv;
+                        est = ((e1 + e2) + e3) + e4;
+                    } else {
+                        const float xs = __int_as_float(mt[m][r][0]);
+                        xnorm = __int_as_float(mt[m][r][1]);
+                        const f32x2_t accv = {(float)acc[m][0][r], (float)acc[m][1][r]};
+                        est = (yyv * f32x2_t{xs, xs}) * accv;
+                    }
+                    if (mode == 0) {
+                        const f32x2_t v = (f32x2_t{xnorm, xnorm} + ynv) - f32x2_t{2.0f, 2.0f} * est;
+                        best[0] = fminf(best[0], v[0]);
+                        best[1] = fminf(best[1], v[1]);
+                    } else {
+                        best[0] = fmaxf(best[0], est[0]);
+                        best[1] = fmaxf(best[1], est[1]);
+                    }
+                }
+            if (mode == 1) {
+                p[0] = a.fcos - best[0];
+                p[1] = a.fcos - best[1];
+            } else {
+                p[0] = best[0];
+                p[1] = best[1];
+            }
+        } else
     #pragma unroll
         for (int m = 0; m < 2; m++)
     #pragma unroll
@@ -668,9 +721,15 @@ __global__ __launch_bounds__(256) void k_rq_tiecheck(const float* __restrict__ c
 // then offers, in id order, the rows that pass against the top at that point
 // (ph_offer: k_replay_scan's packed heap; computing a row that then fails is
 // only wasted work).  Extracted ascending into asc row `q`.
+// First every wave takes windows w = wave mod 8 and writes each window's
+// smallest block minimum to LDS (up to RQ_RP_WMAX windows); the scan then
+// passes a window whose minimum cannot beat a full heap's top without
+// touching its keys (the test is the per-block one applied to the window's
+// smallest key: no block of it would be a candidate).
 // ---------------------------------------------------------------------------
+constexpr int RQ_RP_WMAX = 4096;  // windows with an LDS minimum (2M blocks, 67M rows)
 __host__ __device__ constexpr size_t rq8_replay_lds(int R, int qu4) {
-    return (size_t)R * 16 + 16 + (size_t)qu4 * 16 + 512 * 4 + 16 * 32 * 4 + 16 * 4 + 8 * 4;
+    return (size_t)R * 16 + 16 + (size_t)qu4 * 16 + 512 * 4 + 16 * 32 * 4 + 16 * 4 + 8 * 4 + RQ_RP_WMAX * 4;
 }
 template <int BITS>
 __global__ __launch_bounds__(512) void k_rq8_replay(const float* __restrict__ key, int64_t ldk, int64_t nblk,
@@ -689,21 +748,35 @@ __global__ __launch_bounds__(512) void k_rq8_replay(const float* __restrict__ ke
     float* cd = reinterpret_cast<float*>(clist + 512);                              // [16][32] row distances
     uint32_t* cm = reinterpret_cast<uint32_t*>(cd + 16 * 32);                        // [16] rows that pass
     int* wcnt = reinterpret_cast<int*>(cm + 16);                                     // [8] per-wave counts
+    float* wmin = reinterpret_cast<float*>(wcnt + 8);                                // [RQ_RP_WMAX] window minima
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = blockIdx.x;
     if (li >= nlist) return;
     const int q = list[li];
     if (wave == 0) rq_query_to_lds<BITS>(qs, qsrc, q, q_base + q, D, lane);
     if (tid == 0) *s_len = 0;
-    __syncthreads();
     const float4 ym = qmeta[q];
     const float* kq = key + (int64_t)q * ldk;
-    float kv = tid < nblk ? kq[tid] : __builtin_inff();
+    const int64_t nwin = (nblk + 511) / 512;
+    const int64_t nwm = nwin < RQ_RP_WMAX ? nwin : RQ_RP_WMAX;
+    for (int64_t w = wave; w < nwm; w += 8) {
+        float m = __builtin_inff();
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int64_t bb = w * 512 + i * 64 + lane;
+            m = fminf(m, bb < nblk ? kq[bb] : __builtin_inff());
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+        if (lane == 0) wmin[w] = m;
+    }
+    __syncthreads();
     for (int64_t w0 = 0; w0 < nblk; w0 += 512) {
-        const float kcur = kv;
-        kv = w0 + 512 + tid < nblk ? kq[w0 + 512 + tid] : __builtin_inff();  // the next window, ahead
         int len = *s_len;
         float top = len > 0 ? hr[0].d : 0.f;
+        // (uniform: every thread reads the same heap state and window minimum)
+        if (w0 / 512 < nwm && len >= R && !(top > wmin[w0 / 512])) continue;
+        const float kcur = w0 + tid < nblk ? kq[w0 + tid] : __builtin_inff();
         const bool cand = w0 + tid < nblk && (len < R || top > kcur);
         const uint64_t mb = __ballot(cand);
         if (lane == 0) wcnt[wave] = __popcll(mb);
