@@ -240,14 +240,14 @@ def test_removed_select_kernels_rejected(wv, oracle):
 @pytest.mark.parametrize("metric,kind,n,d,k,nq", [
     ("cosine", 0, 30000, 768, 10, 1), ("cosine", 0, 30000, 768, 10, 8), ("l2-squared", 0, 20000, 100, 24, 3),
     ("dot", 2, 12000, 40, 5, 5), ("l2-squared", 1, 8000, 2500, 10, 6), ("cosine", 0, 5000, 1536, 32 - 8, 2),
-    ("cosine", 0, 3000, 3500, 10, 4)])  # above 3072: no planes, the GEMV by default
+    ("cosine", 0, 3000, 3500, 10, 4), ("cosine", 0, 3000, 6500, 10, 4)])  # above 6144: no planes, the GEMV by default
 def test_gemv_small_batches(wv, oracle, metric, kind, n, d, k, nq):
     """Small batches: the default route and the HBM-streaming GEMV (k_gemv_select).
 
     Measured on C3 (profiles/r04_small_batch_c3.jsonl, tools/small_batch.py):
     with block-key planes the padded int8 key pass beats the GEMV at every
     B = 1..256 (B = 1: 3.39 vs 5.11 ms), so small batches keep the block-key
-    route wherever planes exist (d <= 3072) and take the GEMV only without them;
+    route wherever planes exist (d <= 6144 since round 5) and take the GEMV only without them;
     `kernel = 6` forces the GEMV.  Both routes are asserted and oracle-checked.
     """
     data = gen(oracle, kind, 91, n, d)
@@ -255,7 +255,7 @@ def test_gemv_small_batches(wv, oracle, metric, kind, n, d, k, nq):
     idx, orc = build_pair(wv, oracle, metric, "avx256", data)
     idx.delete(*range(3, n, 17))
     orc.delete(list(range(3, n, 17)))
-    planes = d <= 3072  # bf16 / int8 planes up to 1536, int8-only planes up to 3072
+    planes = d <= 6144  # bf16 / int8 planes up to 1536, int8-only planes up to 6144
     for forced in (False, True):
         idx.set_option("kernel", 6 if forced else 0)
         expect = "gemv" if forced or not planes else ("qs_bf16", "qs_w4", "qs_int8", "q8_gemv")

@@ -198,9 +198,11 @@ def test_c5_pq_full_10m_x_960_bench_batch(wv, oracle):
     dummy = np.zeros(1, np.float32)
     queries = oracle.gen_matrix(2, 2, 0, 1024, d)
     res = {}
-    # the bench's batch and path, a larger batch, and the full-matrix multi-group form
-    for cand, nb in ((1, B), (1, 1024), (0, 1024)):
-        idx.set_option("pq_cand", cand)
+    # the bench's batch and path (the int8 route, cand 2 here), the VALU minima
+    # route at B and 1024, and the full-matrix multi-group form
+    for cand, nb in ((2, B), (1, B), (1, 1024), (0, 1024)):
+        idx.set_option("pq8", 1 if cand == 2 else 0)
+        idx.set_option("pq_cand", min(cand, 1))
         qd = torch.empty((nb, d), dtype=torch.float32, device="cuda")
         _lib.check(lib.wv_gen_device(0, 2, 2, 0, nb, d, qd.data_ptr(), None))
         oi_d = torch.empty((nb, k), dtype=torch.int64, device="cuda")
@@ -221,7 +223,7 @@ def test_c5_pq_full_10m_x_960_bench_batch(wv, oracle):
         for i, q in enumerate(sample):
             assert_rows(*res[cand, nb], q, exp[i][0], exp[i][1], f"c5 cand={cand} B={nb} (groups of {group})")
     # a query's result depends neither on the batch, the group it ran in nor the search form
-    for other in ((1, 1024), (0, 1024)):
+    for other in ((2, B), (1, 1024), (0, 1024)):
         for a, b in zip(res[1, B], res[other]):
             np.testing.assert_array_equal(np.asarray(a), np.asarray(b)[:B])
     for a, b in zip(res[1, 1024], res[0, 1024]):
