@@ -927,13 +927,15 @@ __global__ __launch_bounds__(64) void k_distance_pairs(const float* __restrict__
 // exact normalisation of arbitrary rows into a padded buffer (queries):
 // distancer.Normalize (normalize.go:16-32).  One wave per row: the squares are
 // formed in parallel, the float32 sum runs serially in element order (every
-// lane adds the same readlane'd square, so the sum is wave-uniform), then the
-// divisions are parallel.
+// lane adds the same squares, read back from LDS by broadcast 16 at a time,
+// so the sum is wave-uniform; a readlane per element cost 32 us per 768-d
+// row in the dependent SGPR chain), then the divisions are parallel.
 // rows [n, n_pad) of out are zeroed (the padded query group)
 __global__ __launch_bounds__(256) void k_normalize_rows(const float* __restrict__ in, int64_t n, int d,
                                                         float* __restrict__ out, int ld, int64_t n_pad = 0) {
-    const int lane = threadIdx.x & 63;
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    __shared__ float ssq[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 4 + w;
     if (i >= n) {
         if (i < n_pad)
             for (int c = lane; c < ld; c += 64) out[i * ld + c] = 0.f;
@@ -944,9 +946,25 @@ __global__ __launch_bounds__(256) void k_normalize_rows(const float* __restrict_
     float nrm = 0.f;
     for (int c0 = 0; c0 < d; c0 += 64) {
         const float v = c0 + lane < d ? src[c0 + lane] : 0.f;
-        const float sq = v * v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous chunk's reads are done
+        __builtin_amdgcn_wave_barrier();
+        ssq[w][lane] = v * v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int m = d - c0 < 64 ? d - c0 : 64;
-        for (int j = 0; j < m; j++) nrm = nrm + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), j));
+        if (m == 64) {
+#pragma unroll
+            for (int j0 = 0; j0 < 64; j0 += 16) {
+                float t[16];
+#pragma unroll
+                for (int j = 0; j < 16; j++) t[j] = ssq[w][j0 + j];
+#pragma unroll
+                for (int j = 0; j < 16; j++) nrm = nrm + t[j];
+            }
+        } else {
+            for (int j = 0; j < m; j++) nrm = nrm + ssq[w][j];
+        }
     }
     if (nrm == 0.f) {
         for (int c = lane; c < ld; c += 64) dst[c] = 0.f;

@@ -1196,6 +1196,20 @@ __global__ __launch_bounds__(256) void k_blk_select_f(const float* __restrict__ 
 //                  atomic cursor (any order: k_blk_exact and the inversion
 //                  take any order), more than L -> flag 2, ncand clamped to L
 // ---------------------------------------------------------------------------
+// a starting threshold for a wave's top-(k+1) list (k + 1 <= 64): `lm` = the
+// lane's smallest value (+inf: none); with at least k + 1 lanes holding a
+// value, their largest minimum bounds the (k+1)-th smallest from above (those
+// minima are k + 1 distinct elements), so anything above it is never kept.
+// Returns the offer threshold (values below it pass): next_up of that bound.
+__device__ __forceinline__ float wave_kp1_cap(float lm, int k) {
+    const bool has = lm < __builtin_inff();
+    const int nl = __popcll(__ballot(has));
+    float b = has ? lm : -__builtin_inff();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b = fmaxf(b, __shfl_xor(b, o));
+    return (k + 1 <= 64 && nl >= k + 1) ? qs_next_up(b) : __builtin_inff();
+}
+
 template <int RT>
 __global__ __launch_bounds__(64) void k_sel_part(const float* __restrict__ key, int64_t ldk, int64_t nb, int k, int P,
                                                  float* __restrict__ part) {
@@ -1208,7 +1222,18 @@ __global__ __launch_bounds__(64) void k_sel_part(const float* __restrict__ key, 
     const int64_t b0 = (int64_t)p * per, b1 = b0 + per < nb ? b0 + per : nb;
     const float* kr = key + q * ldk;
     WaveTopL<RT> t;
-    t.init();
+    {   // a pre-pass over the part (cache-resident on the second read): without
+        // a threshold every 64 keys offered forced a merge
+        float lm = __builtin_inff();
+        for (int64_t c0 = b0; c0 < b1; c0 += 64 * U) {
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int64_t bb = c0 + j * 64 + lane;
+                lm = fminf(lm, bb < b1 ? kr[bb] : __builtin_inff());
+            }
+        }
+        t.init(wave_kp1_cap(lm, k));
+    }
     for (int64_t c0 = b0; c0 < b1; c0 += 64 * U) {
         float v[U];
 #pragma unroll
@@ -1252,7 +1277,11 @@ __global__ __launch_bounds__(64) void k_sel_mid(const float* __restrict__ part, 
     const int n = P * (k + 1);
     const float* pr = part + (int64_t)q * n;
     WaveTopL<RT> t;
-    t.init();
+    {
+        float lm = __builtin_inff();
+        for (int i0 = 0; i0 < n; i0 += 64) lm = fminf(lm, i0 + lane < n ? pr[i0 + lane] : __builtin_inff());
+        t.init(wave_kp1_cap(lm, k));
+    }
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
         t.offer(i < n ? pr[i] : __builtin_inff(), 0u, sbk, sbi, lane);

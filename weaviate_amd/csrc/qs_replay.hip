@@ -29,7 +29,10 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
     // row of the keys' row set (the union) but not necessarily one of the
     // query's own; the one-wave replay prunes by its true heap top only
     const bool ub_ok = idx->cur_vq == 0;
-    if (ub_ok && blk_pooled(idx, k, nb)) {
+    // a few listed queries (small batches): the one-launch 8-wave form instead
+    // of the pooled form's three launches (most such calls list no query)
+    const bool few = max_list <= 16 && !rec_i && k < 64 && nch <= RP_MAXCH && idx->replay_par;
+    if (ub_ok && !few && blk_pooled(idx, k, nb)) {
         // pooled form: bounds + candidate pool (8 waves per query), exact
         // distances over the whole grid, one-wave heap per query
         const int64_t pool_cap = idx->rp_pool;
