@@ -3,7 +3,10 @@
 // buffers -- how the cgo shim's goroutines would call it) on the C3 corpus for
 // S seconds; prints one JSON line with QPS, launches, mean batch and latency.
 // Build: hipcc -O2 -std=c++17 tools/serve_bench.cpp -Iinclude -Lweaviate_amd -lwvknn -Wl,-rpath,'$ORIGIN/../weaviate_amd' -o tools/serve_bench
-// Run:   tools/serve_bench [n=10000000] [threads=256] [seconds=10] [window_us=0]
+// Run:   tools/serve_bench [n=10000000] [threads=256] [seconds=10] [window_us=0] [allow_pct=0]
+// allow_pct > 0: every thread searches under its own allow list (a random
+// allow_pct % of the ids, different per thread) -- filtered callers, batched
+// through wv_index_search_by_vector_batch_multi_allow.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,6 +35,7 @@ int main(int argc, char** argv) {
     const int T = argc > 2 ? atoi(argv[2]) : 256;
     const double secs = argc > 3 ? atof(argv[3]) : 10.0;
     const int64_t window = argc > 4 ? atoll(argv[4]) : 0;
+    const double allow_pct = argc > 5 ? atof(argv[5]) : 0.0;
     const int d = 768, k = 10, nq = 4096;
     wv_config cfg{};
     cfg.metric = WV_METRIC_COSINE_DOT;
@@ -70,6 +74,17 @@ int main(int argc, char** argv) {
     CK(wv_index_batcher_stats(idx, st0));
     std::atomic<int> fails{0};
     std::vector<std::vector<double>> lat(T);
+    std::vector<std::vector<uint64_t>> allow(T);
+    if (allow_pct > 0)
+        for (int t = 0; t < T; t++) {  // thread t's list: ids whose hash falls below allow_pct %
+            const uint64_t thr = (uint64_t)(allow_pct / 100.0 * 4294967296.0);
+            for (int64_t i = 0; i < n; i++) {
+                uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull + (uint64_t)(t + 1) * 0xBF58476D1CE4E5B9ull;
+                h ^= h >> 31;
+                h *= 0x94D049BB133111EBull;
+                if ((h >> 32) < thr) allow[t].push_back((uint64_t)i);
+            }
+        }
     auto stop = clk::now() + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(secs));
     auto t0 = clk::now();
     std::vector<std::thread> th;
@@ -80,7 +95,10 @@ int main(int argc, char** argv) {
             int32_t lc = 0;
             for (int i = t; clk::now() < stop; i += T) {
                 auto a = clk::now();
-                if (wv_index_search_by_vector(idx, &q[(size_t)(i % nq) * d], d, k, nullptr, 0, 0, li, ld, &lc)) fails++;
+                const std::vector<uint64_t>& al = allow[t];
+                if (wv_index_search_by_vector(idx, &q[(size_t)(i % nq) * d], d, k, al.empty() ? nullptr : al.data(),
+                                              (int64_t)al.size(), allow_pct > 0 ? 1 : 0, li, ld, &lc))
+                    fails++;
                 lat[t].push_back(std::chrono::duration<double, std::milli>(clk::now() - a).count());
             }
         });
@@ -92,10 +110,10 @@ int main(int argc, char** argv) {
     std::sort(all.begin(), all.end());
     auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, (size_t)(p * all.size()))]; };
     int64_t calls = st1[0] - st0[0], launches = st1[1] - st0[1];
-    printf("{\"workload\": \"%lld x %d cosine k=%d, single-query calls from %d C++ threads\", \"qps\": %.1f, "
+    printf("{\"workload\": \"%lld x %d cosine k=%d, single-query calls from %d C++ threads, allow lists %.2f %%\", \"qps\": %.1f, "
            "\"serial_qps\": %.1f, \"calls\": %lld, \"launches\": %lld, \"mean_batch\": %.1f, \"max_batch\": %lld, "
            "\"latency_ms\": {\"p50\": %.2f, \"p99\": %.2f}, \"window_us\": %lld, \"failures\": %d}\n",
-           (long long)n, d, k, T, calls / el, serial_qps, (long long)calls, (long long)launches,
+           (long long)n, d, k, T, allow_pct, calls / el, serial_qps, (long long)calls, (long long)launches,
            launches ? (double)calls / launches : 0.0, (long long)st1[2], pct(0.5), pct(0.99), (long long)window,
            fails.load());
     wv_index_destroy(idx);
