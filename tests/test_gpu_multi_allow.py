@@ -55,15 +55,19 @@ def test_multi_allow_equals_one_query_calls(wv, oracle, metric, n, d, k, nq):
     deleted = list(range(5, n, 97))
     idx.delete(*deleted)
     allows = _allow_lists(wv, n, nq, k, seed=n + d)
-    # every list in the shared launch (no sparse list searched alone)
+    # every list in the shared launch (no sparse list searched alone, the
+    # unresolved ones replayed inside it)
     idx.set_option("pqa_split_max", 0)
+    idx.set_option("pqa_alone", 0)
     b0 = idx.stats()["batches"]
     ids, dists, counts = idx.search_by_vector_batch_multi_allow(queries, k, allows)
     st = idx.stats()
     assert st["batches"] - b0 == 1, "the batch must share one launch"
     assert wv._lib.ROUTES[st["last_route"]].startswith(("qs_", "q8_")), st
-    # default: the sparsest lists alone, the rest shared -- the same rows
+    # default: the sparsest lists alone, the rest shared, the unresolved ones
+    # searched alone afterwards -- the same rows
     idx.set_option("pqa_split_max", 64)
+    idx.set_option("pqa_alone", 1)
     ids2, dists2, counts2 = idx.search_by_vector_batch_multi_allow(queries, k, allows)
     np.testing.assert_array_equal(counts2, counts)
     for i in range(nq):

@@ -547,6 +547,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         if (phase == 2 && o_flags)
             HIPCHK(hipMemcpyAsync(o_flags + c0, flags, (size_t)cn * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         if (mode == 1) continue;
+        if (pqa && o_flags) continue;  // per-query lists: the caller searches the unresolved queries alone
         // ---- flagged queries: the exact heap replay, bounded by the block keys ----
         if (!ctr_reset) HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
         k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount, 0);

@@ -268,6 +268,7 @@ struct wv_index {
     int pqa = 1;
     int64_t pqa_budget_mb = 4096;
     int64_t pqa_split_max = 64;
+    int pqa_alone = 1;
     int64_t pqa_vq = 0;
     int64_t cur_vq = 0;
     const float* cur_tq = nullptr;

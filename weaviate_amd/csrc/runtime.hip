@@ -774,6 +774,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "bq8") idx->bq8_opt = value ? 1 : 0;      // BQ block minima on the integer MFMA (1) or VALU (0)
     else if (k == "pqa") idx->pqa = value ? 1 : 0;
     else if (k == "sel_lower") idx->sel_lower = value ? 1 : 0;  // per-query allow lists share one block-key launch
+    else if (k == "pqa_alone") idx->pqa_alone = value ? 1 : 0;  // unresolved per-query lists searched alone
     else if (k == "pqa_split_max") idx->pqa_split_max = std::max<int64_t>(value, 0);  // sparse lists searched alone
     else if (k == "pqa_budget_mb") idx->pqa_budget_mb = std::max<int64_t>(value, 1);
     else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only
@@ -1491,6 +1492,54 @@ static thread_local bool t_pqa_nosplit = false;
 extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const float* queries, int64_t nq, int64_t d,
                                                            int32_t k, const uint64_t* allow_ids,
                                                            const int64_t* allow_offsets, const int32_t* allow_modes,
+                                                           uint64_t* out_ids, float* out_dists, int32_t* out_counts);
+
+// the queries qs of a multi-allow batch as their own batch -- grouped by list
+// (shared == false: one-query-list calls) or shared (the one-launch path, no
+// further split) -- results scattered back into the batch's outputs
+static int multi_allow_subset(wv_index* idx, const float* queries, int64_t d, int32_t k, const uint64_t* allow_ids,
+                              const int64_t* allow_offsets, const int32_t* allow_modes, const std::vector<int64_t>& qs,
+                              bool shared, uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    const int64_t kk = std::max<int32_t>(k, 0);
+    const int64_t n = (int64_t)qs.size();
+    std::vector<float> qb((size_t)(n * d) + 1);
+    std::vector<int64_t> off((size_t)n + 1, 0);
+    std::vector<int32_t> modes((size_t)n);
+    std::vector<uint64_t> aid;
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t q = qs[(size_t)i];
+        memcpy(&qb[(size_t)(i * d)], queries + q * d, (size_t)d * sizeof(float));
+        modes[(size_t)i] = allow_modes[q];
+        if (allow_modes[q]) aid.insert(aid.end(), allow_ids + allow_offsets[q], allow_ids + allow_offsets[q + 1]);
+        off[(size_t)i + 1] = (int64_t)aid.size();
+    }
+    aid.push_back(0);  // a valid pointer when every list is empty
+    std::vector<uint64_t> oi((size_t)(n * kk) + 1);
+    std::vector<float> od((size_t)(n * kk) + 1);
+    std::vector<int32_t> oc((size_t)n);
+    int rc;
+    if (!shared) {
+        rc = multi_allow_grouped(idx, qb.data(), n, d, k, aid.data(), off.data(), modes.data(), oi.data(), od.data(),
+                                 oc.data());
+    } else {
+        t_pqa_nosplit = true;
+        rc = wv_index_search_by_vector_batch_multi_allow(idx, qb.data(), n, d, k, aid.data(), off.data(), modes.data(),
+                                                         oi.data(), od.data(), oc.data());
+        t_pqa_nosplit = false;
+    }
+    if (rc) return rc;
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t q = qs[(size_t)i];
+        out_counts[q] = oc[(size_t)i];
+        memcpy(out_ids + q * kk, &oi[(size_t)(i * kk)], (size_t)oc[(size_t)i] * sizeof(uint64_t));
+        memcpy(out_dists + q * kk, &od[(size_t)(i * kk)], (size_t)oc[(size_t)i] * sizeof(float));
+    }
+    return WV_OK;
+}
+
+extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const float* queries, int64_t nq, int64_t d,
+                                                           int32_t k, const uint64_t* allow_ids,
+                                                           const int64_t* allow_offsets, const int32_t* allow_modes,
                                                            uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
     if (!idx) return set_err(WV_ERR_INVALID, "nil index");
     if (nq < 0) return set_err(WV_ERR_INVALID, "negative batch");
@@ -1525,43 +1574,11 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
         for (int64_t q = 0; q < nq; q++) (md[(size_t)q] > 960.0 ? sp : dn).push_back(q);
         if (!sp.empty() && (int64_t)sp.size() <= idx->pqa_split_max && !dn.empty()) {
             g.unlock();
-            const int64_t kk = std::max<int32_t>(k, 0);
-            for (int pass = 0; pass < 2; pass++) {
-                const std::vector<int64_t>& qs = pass ? dn : sp;
-                const int64_t n = (int64_t)qs.size();
-                std::vector<float> qb((size_t)(n * d) + 1);
-                std::vector<int64_t> off((size_t)n + 1, 0);
-                std::vector<int32_t> modes((size_t)n);
-                std::vector<uint64_t> aid;
-                for (int64_t i = 0; i < n; i++) {
-                    const int64_t q = qs[(size_t)i];
-                    memcpy(&qb[(size_t)(i * d)], queries + q * d, (size_t)d * sizeof(float));
-                    modes[(size_t)i] = allow_modes[q];
-                    if (allow_modes[q]) aid.insert(aid.end(), allow_ids + allow_offsets[q], allow_ids + allow_offsets[q + 1]);
-                    off[(size_t)i + 1] = (int64_t)aid.size();
-                }
-                std::vector<uint64_t> oi((size_t)(n * kk) + 1);
-                std::vector<float> od((size_t)(n * kk) + 1);
-                std::vector<int32_t> oc((size_t)n);
-                int rc;
-                if (pass == 0) {
-                    rc = multi_allow_grouped(idx, qb.data(), n, d, k, aid.data(), off.data(), modes.data(), oi.data(),
-                                             od.data(), oc.data());
-                } else {
-                    t_pqa_nosplit = true;
-                    rc = wv_index_search_by_vector_batch_multi_allow(idx, qb.data(), n, d, k, aid.data(), off.data(),
-                                                                     modes.data(), oi.data(), od.data(), oc.data());
-                    t_pqa_nosplit = false;
-                }
-                if (rc) return rc;
-                for (int64_t i = 0; i < n; i++) {
-                    const int64_t q = qs[(size_t)i];
-                    out_counts[q] = oc[(size_t)i];
-                    memcpy(out_ids + q * kk, &oi[(size_t)(i * kk)], (size_t)oc[(size_t)i] * sizeof(uint64_t));
-                    memcpy(out_dists + q * kk, &od[(size_t)(i * kk)], (size_t)oc[(size_t)i] * sizeof(float));
-                }
-            }
-            return WV_OK;
+            int rc = multi_allow_subset(idx, queries, d, k, allow_ids, allow_offsets, allow_modes, sp, false, out_ids,
+                                        out_dists, out_counts);
+            if (rc) return rc;
+            return multi_allow_subset(idx, queries, d, k, allow_ids, allow_offsets, allow_modes, dn, true, out_ids,
+                                      out_dists, out_counts);
         }
     }
     if (nq > qmax) {  // bitmaps past the budget: consecutive sub-batches
@@ -1628,17 +1645,32 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
     idx->pqa_valid = bits;
     idx->pqa_vq = vq;
     idx->pqa_m = idx->pqaM.as<int32_t>();
+    // the queries the shared launch leaves unresolved (flags) are searched
+    // alone afterwards (a sparse list's own gathered sub-index or window)
+    // instead of by the one-wave replay inside the launch, which walks every
+    // block key of the union for one query (35 ms at 1M rows, 2 % lists)
+    HIPCHK(idx->oF.ensure((size_t)nq * sizeof(int32_t)));
+    int32_t* dflags = idx->pqa_alone ? idx->oF.as<int32_t>() : nullptr;
     int rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, uni, idx->npresent, idx->oIds.as<uint64_t>(),
-                         idx->oD.as<float>(), idx->oN.as<int32_t>(), nullptr);
+                         idx->oD.as<float>(), idx->oN.as<int32_t>(), dflags);
     idx->pqa_valid = nullptr;
     idx->pqa_vq = 0;
     idx->pqa_m = nullptr;
     if (rc) return rc;
+    std::vector<int32_t> hf(dflags ? (size_t)nq : 0);
     HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(out_counts, idx->oN.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (dflags) HIPCHK(hipMemcpyAsync(hf.data(), dflags, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    return WV_OK;
+    std::vector<int64_t> left;
+    for (int64_t q = 0; q < (int64_t)hf.size(); q++)
+        if (hf[(size_t)q]) left.push_back(q);
+    if (left.empty()) return WV_OK;
+    idx->stats.replayed_queries += (uint64_t)left.size();
+    g.unlock();
+    return multi_allow_subset(idx, queries, d, k, allow_ids, allow_offsets, allow_modes, left, false, out_ids, out_dists,
+                              out_counts);
 }
 
 extern "C" int wv_index_hnsw_flat_search(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
