@@ -99,6 +99,9 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
     return WV_OK;
 }
 
+static void* batch_pinned_alloc(size_t bytes) { return malloc(bytes); }
+static void batch_pinned_free(void* p) { free(p); }
+
 #include "../weaviate_amd/csrc/batcher.hip"
 
 int main(int argc, char** argv) {

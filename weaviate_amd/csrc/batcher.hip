@@ -32,8 +32,18 @@ struct wv_batch_req {
     bool done = false;
 };
 
+// page-locked host memory for the leader's concatenated allow lists (defined
+// by the including unit: hipHostMalloc in the library, malloc in the TSan mock)
+static void* batch_pinned_alloc(size_t bytes);
+static void batch_pinned_free(void* p);
+
 struct wv_batcher {
     std::mutex m;
+    // the concatenated allow lists of a filtered group, reused across launches:
+    // page-locked (the copy to the device is one DMA) and warm (no page faults
+    // per launch); only the leader touches it
+    uint64_t* pin = nullptr;
+    size_t pin_cap = 0;
     std::condition_variable cv;         // followers: their batch is done / leader slot free
     std::condition_variable cv_window;  // the leader waiting out batch_window_us
     std::vector<wv_batch_req*> pending;
@@ -41,7 +51,10 @@ struct wv_batcher {
     int64_t calls = 0, launches = 0, max_batch_seen = 0;
 };
 
-static void batcher_free(wv_batcher* b) { delete b; }
+static void batcher_free(wv_batcher* b) {
+    if (b && b->pin) batch_pinned_free(b->pin);
+    delete b;
+}
 
 static wv_batcher* get_batcher(wv_index* idx) {
     static std::mutex create_mu;
@@ -51,7 +64,7 @@ static wv_batcher* get_batcher(wv_index* idx) {
 }
 
 // Runs one group of requests sharing (d, k) as one batch call.
-static void run_group(wv_index* idx, std::vector<wv_batch_req*>& grp) {
+static void run_group(wv_index* idx, wv_batcher* b, std::vector<wv_batch_req*>& grp) {
     const int64_t n = (int64_t)grp.size();
     const int64_t d = grp[0]->d;
     const int32_t k = grp[0]->k;
@@ -68,17 +81,28 @@ static void run_group(wv_index* idx, std::vector<wv_batch_req*>& grp) {
         rc = wv_index_search_by_vector_batch(idx, q.data(), n, d, k, grp[0]->allow_ids, grp[0]->n_allow,
                                              grp[0]->allow_mode, ids.data(), dists.data(), cnt.data());
     } else {
-        std::vector<uint64_t> aids;
         std::vector<int64_t> off((size_t)n + 1, 0);
         std::vector<int32_t> modes((size_t)n);
         for (int64_t i = 0; i < n; i++) {
             modes[(size_t)i] = grp[i]->allow_mode;
-            if (grp[i]->allow_mode != 0 && grp[i]->n_allow > 0)
-                aids.insert(aids.end(), grp[i]->allow_ids, grp[i]->allow_ids + grp[i]->n_allow);
-            off[(size_t)i + 1] = (int64_t)aids.size();
+            off[(size_t)i + 1] = off[(size_t)i] + (grp[i]->allow_mode != 0 ? std::max<int64_t>(grp[i]->n_allow, 0) : 0);
         }
-        rc = wv_index_search_by_vector_batch_multi_allow(idx, q.data(), n, d, k, aids.data(), off.data(), modes.data(),
-                                                         ids.data(), dists.data(), cnt.data());
+        const size_t need = (size_t)off[(size_t)n] + 1;
+        if (need > b->pin_cap) {
+            if (b->pin) batch_pinned_free(b->pin);
+            b->pin_cap = std::max(need, b->pin_cap * 2);
+            b->pin = static_cast<uint64_t*>(batch_pinned_alloc(b->pin_cap * sizeof(uint64_t)));
+            if (!b->pin) b->pin_cap = 0;
+        }
+        if (!b->pin) {
+            rc = set_err(WV_ERR_INVALID, "out of host memory for the batch's allow lists");
+        } else {
+            for (int64_t i = 0; i < n; i++)
+                if (off[(size_t)i + 1] > off[(size_t)i])
+                    memcpy(b->pin + off[(size_t)i], grp[i]->allow_ids, (size_t)grp[i]->n_allow * sizeof(uint64_t));
+            rc = wv_index_search_by_vector_batch_multi_allow(idx, q.data(), n, d, k, b->pin, off.data(), modes.data(),
+                                                             ids.data(), dists.data(), cnt.data());
+        }
     }
     std::string err = rc ? std::string(wv_last_error()) : std::string();
     for (int64_t i = 0; i < n; i++) {
@@ -91,7 +115,7 @@ static void run_group(wv_index* idx, std::vector<wv_batch_req*>& grp) {
     }
 }
 
-static void run_batch(wv_index* idx, std::vector<wv_batch_req*>& batch) {
+static void run_batch(wv_index* idx, wv_batcher* b, std::vector<wv_batch_req*>& batch) {
     // group by (d, k); each request keeps its own allow list
     std::vector<std::vector<wv_batch_req*>> groups;
     for (wv_batch_req* r : batch) {
@@ -100,7 +124,7 @@ static void run_batch(wv_index* idx, std::vector<wv_batch_req*>& batch) {
             if (g[0]->d == r->d && g[0]->k == r->k) { g.push_back(r); placed = true; break; }
         if (!placed) groups.push_back({r});
     }
-    for (auto& g : groups) run_group(idx, g);
+    for (auto& g : groups) run_group(idx, b, g);
 }
 
 extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int64_t d, int32_t k,
@@ -134,7 +158,7 @@ extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int6
             b->launches++;
             b->max_batch_seen = std::max<int64_t>(b->max_batch_seen, (int64_t)batch.size());
             lk.unlock();
-            run_batch(idx, batch);
+            run_batch(idx, b, batch);
             lk.lock();
             for (wv_batch_req* r : batch) r->done = true;
             b->busy = false;

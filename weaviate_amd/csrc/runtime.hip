@@ -1904,4 +1904,9 @@ extern "C" int wv_gen_device(int32_t device, int32_t kind, uint64_t seed, uint64
 #include "vector_index.hip"
 
 // micro-batcher of concurrent single-query SearchByVector calls
+static void* batch_pinned_alloc(size_t bytes) {
+    void* p = nullptr;
+    return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+static void batch_pinned_free(void* p) { (void)hipHostFree(p); }
 #include "batcher.hip"
