@@ -433,7 +433,10 @@ int wv_merge_shards(int32_t device, int32_t nshards, int64_t nq, int32_t k, cons
  *                       wv_rccl_unique_id gave rank 0 (the host passes it on);
  *   WV_TRANSPORT_LOCAL  every rank is a shard of this process (devices may
  *                       repeat): device copies, for tests and cost models.
- * Exact (uncompressed) search only; allow lists are not taken. */
+ * Every compression of the flat index: exact fp32 (two-phase block keys), BQ
+ * (the R-heap of flat/index.go:460-532 across the shards + rescoring), rq-8 /
+ * rq-1, trained PQ and SQ (the worker heap across the shards + rescoring:
+ * DESIGN.md §4b); allow lists through the _allow / _multi_allow calls. */
 #define WV_TRANSPORT_LOCAL 0
 #define WV_TRANSPORT_RCCL 1
 /*   WV_TRANSPORT_HOST   one local shard per process; every collective staged
@@ -476,10 +479,44 @@ int wv_multi_search_device(wv_multi *m, const float *d_queries, int64_t nq, int6
 /* the same from host buffers (nq x k outputs, ascending, reference tie order) */
 int wv_multi_search_by_vector_batch(wv_multi *m, const float *queries, int64_t nq, int64_t d, int32_t k,
                                     uint64_t *out_ids, float *out_dists, int32_t *out_counts);
+/* Filtered SearchByVector over every shard: each shard searches under its part
+ * of the allow list (shard_read.go:401-413 -> flat SearchByVector(..., allowList),
+ * :466; merged as index.go:2067-2071), equal to one flat index under the whole
+ * list.  allow_mode 0: no list; 1: allow_ids[0..n_allow) (host, doc ids; ids of
+ * other processes' ranks are ignored; empty -> no results, flat/index.go:590-594).
+ * Every search kind of the shards takes it: exact, BQ, rq-8 / rq-1, trained PQ,
+ * SQ.  The shards' handles must not be searched while a multi search runs. */
+int wv_multi_search_by_vector_batch_allow(wv_multi *m, const float *queries, int64_t nq, int64_t d, int32_t k,
+                                          const uint64_t *allow_ids, int64_t n_allow, int32_t allow_mode,
+                                          uint64_t *out_ids, float *out_dists, int32_t *out_counts);
+/* the same on device queries / outputs (local shard 0's device, `stream`) */
+int wv_multi_search_device_allow(wv_multi *m, const float *d_queries, int64_t nq, int64_t d, int32_t k,
+                                 const uint64_t *allow_ids, int64_t n_allow, int32_t allow_mode, uint64_t *d_ids,
+                                 float *d_dists, int32_t *d_counts, void *stream);
+/* every query under its own allow list (allow_offsets[nq+1], allow_modes[nq], as
+ * wv_index_search_by_vector_batch_multi_allow); results equal nq one-query
+ * filtered calls.  Queries with identical lists share one search. */
+int wv_multi_search_by_vector_batch_multi_allow(wv_multi *m, const float *queries, int64_t nq, int64_t d, int32_t k,
+                                                const uint64_t *allow_ids, const int64_t *allow_offsets,
+                                                const int32_t *allow_modes, uint64_t *out_ids, float *out_dists,
+                                                int32_t *out_counts);
+/* SearchByVectorDistance over every shard (flat/index.go:699-761 per shard,
+ * shard_read.go:439, merged by index.go:2067-2071); out_* capacity >= 100 */
+int wv_multi_search_by_vector_distance(wv_multi *m, const float *query, int64_t d, float target_distance,
+                                       int64_t max_limit, const uint64_t *allow_ids, int64_t n_allow,
+                                       int32_t allow_mode, uint64_t *out_ids, float *out_dists, int32_t *out_count);
+/* PQ shards: ProductQuantizer.Fit on the first trainingLimit present rows in
+ * doc-id order over all shards (one process: gathered from the shards in rank
+ * order; a world over processes: they must all lie on rank 0), the codebook
+ * installed on every shard; _set_centers installs a codebook trained elsewhere. */
+int wv_multi_pq_fit(wv_multi *m, uint64_t seed);
+int wv_multi_pq_set_centers(wv_multi *m, const float *centers, int64_t n_floats);
 /* "sim" = 1: local shards run each stage one after another, timed alone
  * (wv_multi_stage_ms); "rec_cap" (tests): capacity of the parallel replay's
- * insertion records (0 = max(256, 16 k); a record that overflows sends its
- * query down the serial chain); any other key is set on every shard */
+ * insertion records (0 = max(256, 16 k), BQ 2R, quantized 2R + 64; a record
+ * that overflows sends its query -- compressed: its chunk -- down the serial
+ * chain); "chain" = 1 (tests): compressed searches take the serial chain; any
+ * other key is set on every shard */
 int wv_multi_set_option(wv_multi *m, const char *key, int64_t value);
 /* out[n]: searches, flagged queries, overflowed records, chain hops, last
  * search's flagged and overflowed queries, world, rank0, n_local, transport */

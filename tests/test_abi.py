@@ -92,7 +92,9 @@ def test_multi_config_validation_without_gpu():
     assert rc == _lib.WV_ERR_INVALID and "invalid multi config" in msg
     rc, msg = create(2, 0, 2, 0, stride=0)
     assert rc == _lib.WV_ERR_INVALID and "id_stride" in msg
-    rc, msg = create(1, 0, 1, 0, cfg=make_config(distance="cosine", dims=8, bq=True))
-    assert rc == _lib.WV_ERR_UNSUPPORTED and "exact" in msg
+    bad = make_config(distance="cosine", dims=8, bq=True)
+    bad.compression = 9  # every WV_COMPRESSION_* is taken (BQ, PQ, rq-8 / rq-1, SQ); others are refused
+    rc, msg = create(1, 0, 1, 0, cfg=bad)
+    assert rc == _lib.WV_ERR_INVALID and "unknown compression" in msg
     rc, msg = create(1, 0, 1, 7)
     assert rc == _lib.WV_ERR_INVALID and "unknown transport" in msg

@@ -142,6 +142,13 @@ SIGNATURES = {
     "wv_multi_add_batch": (C.c_int, [P, pu64, pf32, i64, i64]),
     "wv_multi_search_device": (C.c_int, [P, P, i64, i64, i32, P, P, P, P]),
     "wv_multi_search_by_vector_batch": (C.c_int, [P, pf32, i64, i64, i32, pu64, pf32, pi32]),
+    "wv_multi_search_by_vector_batch_allow": (C.c_int, [P, pf32, i64, i64, i32, pu64, i64, i32, pu64, pf32, pi32]),
+    "wv_multi_search_device_allow": (C.c_int, [P, P, i64, i64, i32, pu64, i64, i32, P, P, P, P]),
+    "wv_multi_search_by_vector_batch_multi_allow": (C.c_int, [P, pf32, i64, i64, i32, pu64, P, pi32, pu64, pf32,
+                                                              pi32]),
+    "wv_multi_search_by_vector_distance": (C.c_int, [P, pf32, i64, f32, i64, pu64, i64, i32, pu64, pf32, pi32]),
+    "wv_multi_pq_fit": (C.c_int, [P, u64]),
+    "wv_multi_pq_set_centers": (C.c_int, [P, pf32, i64]),
     "wv_multi_set_option": (C.c_int, [P, C.c_char_p, i64]),
     "wv_multi_stats": (C.c_int, [P, C.POINTER(C.c_int64), i32]),
     "wv_multi_stage_ms": (C.c_int, [P, C.POINTER(C.c_double), i32]),

@@ -34,6 +34,7 @@
 
 #include <dlfcn.h>
 #include <chrono>
+#include <map>
 #include <memory>
 #include <rccl/rccl.h>  // types only: the library is bound at run time
 
@@ -334,6 +335,8 @@ __device__ float kth_smallest(const float* v, int n, int k, float* slot) {
 // ranks < r, k-th smallest block bound A + eps of their phase-1 keys) -- each
 // an upper bound of the real heap top at rank r's first row; the heap is k
 // copies of T_r (ids -1), empty when T_r is infinite
+// (the compressed R-heaps: ql, gc, gf NULL -- every query, every one of the k1
+// gathered block minima a bound of one distinct row)
 __global__ __launch_bounds__(256) void k_prefix_bound(int r, const int32_t* __restrict__ ql, int F, int k, int k1, int64_t nq,
                                                       const float* __restrict__ gd, const int32_t* __restrict__ gc,
                                                       const int32_t* __restrict__ gf, const float* __restrict__ gA,
@@ -343,12 +346,13 @@ __global__ __launch_bounds__(256) void k_prefix_bound(int r, const int32_t* __re
     __shared__ float slot;
     const int li = blockIdx.x;
     if (li >= F) return;
-    const int64_t q = ql[li];
+    const int64_t q = ql ? ql[li] : li;
     const int n = r * k1;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int rr = i / k1, j = i - rr * k1;
         const int64_t row = (int64_t)rr * nq + q;
-        pbv[i] = (j < gc[row] && gf[row] == 0) ? gd[row * k1 + j] : __builtin_inff();
+        const bool ok = (!gc || j < gc[row]) && (!gf || gf[row] == 0);
+        pbv[i] = ok ? gd[row * k1 + j] : __builtin_inff();
     }
     __syncthreads();
     float T = kth_smallest(pbv, n, k, &slot);
@@ -393,6 +397,71 @@ __global__ void k_scatter_rows(const int32_t* __restrict__ ql, int F, int k, con
     if (threadIdx.x == 0) on[q] = fn[li];
 }
 
+// order-preserving float <-> u32 keys (NaN above +inf, as torch.topk ranks it)
+__device__ inline uint32_t ord_key(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float ord_val(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k); }
+
+// per query the R smallest of its nblk block minima (sharded.py quant_bounds'
+// topk, unordered: only their R-th smallest is used), +inf padded.  One
+// workgroup per query: a 4-pass 8-bit radix select of the R-th smallest key,
+// then every value below it and as many copies of it as complete R.
+__global__ __launch_bounds__(256) void k_smallest_r(const float* __restrict__ bm, int64_t nblk, int R,
+                                                    float* __restrict__ out) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t s_prefix, s_need, s_cnt;
+    const int q = blockIdx.x;
+    const float* B = bm + (int64_t)q * nblk;
+    float* O = out + (int64_t)q * R;
+    if (nblk <= R) {
+        for (int i = threadIdx.x; i < R; i += blockDim.x) O[i] = i < nblk ? B[i] : __builtin_inff();
+        return;
+    }
+    if (threadIdx.x == 0) { s_prefix = 0; s_need = (uint32_t)R; s_cnt = 0; }
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+        const uint32_t prefix = s_prefix;
+        const uint32_t hi_mask = shift == 24 ? 0u : (0xffffffffu << (shift + 8));
+        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) {
+            const uint32_t key = ord_key(B[b]);
+            if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t c = 0, need = s_need;
+            for (int dgt = 0; dgt < 256; dgt++) {
+                if (c + hist[dgt] >= need) { s_prefix = prefix | ((uint32_t)dgt << shift); s_need = need - c; break; }
+                c += hist[dgt];
+            }
+        }
+        __syncthreads();
+    }
+    const uint32_t T = s_prefix;  // the R-th smallest key; s_need of its copies complete the R
+    const int below = R - (int)s_need;
+    for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) {
+        const float v = B[b];
+        if (ord_key(v) < T) O[atomicAdd(&s_cnt, 1u)] = v;
+    }
+    for (int i = below + threadIdx.x; i < R; i += blockDim.x) O[i] = ord_val(T);
+}
+
+// the merged R-heap extracted ascending -> its pop order (max first, flat/index.go:509-523)
+__global__ void k_rev_rows(const uint64_t* __restrict__ asc, const int32_t* __restrict__ n, int R,
+                           uint64_t* __restrict__ out) {
+    const int li = blockIdx.x;
+    const int m = n[li];
+    for (int j = threadIdx.x; j < R; j += blockDim.x)
+        out[(int64_t)li * R + j] = j < m ? asc[(int64_t)li * R + (m - 1 - j)] : ~0ull;
+}
+
+__global__ void k_iota32(int32_t* __restrict__ p, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = (int32_t)i;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -410,6 +479,12 @@ struct MRank {
     bool off = false;
     DBuf q, topA, eps, gA, gE, ids, dd, cnt, flg, gi, gd, gc, gf, oi, od, on, of, ql, nl, fki, fkd, fkn, ti, td, tn, ri, rd,
         rn, gri, grd, grn, sti, std_, fi, fd, fn, un, ul, nu, ci[2], cd[2], cn[2];
+    // compressed searches (BQ, PQ / SQ / RQ): bounds, candidates, rescoring
+    DBuf bm, bnd, gbnd, cand, E, gEall, iota, mb, gmb;
+    int64_t nblk = 0;
+    // a filtered search: the shard's own present bitmap while the allow bitmap stands in
+    uint32_t* saved_present = nullptr;
+    int64_t saved_npresent = 0;
 };
 
 struct wv_multi {
@@ -421,7 +496,8 @@ struct wv_multi {
     hipEvent_t e_call = nullptr;
     int32_t* pin = nullptr;  // pinned host words: flagged count, overflow count
     int sim = 0;
-    int rec_cap = 0;  // option rec_cap (tests): replay record capacity, 0 = max(256, 16 k)
+    int rec_cap = 0;  // option rec_cap (tests): replay record capacity, 0 = max(256, 16 k) (exact), 2R (BQ), 2R + 64 (quantized)
+    int force_chain = 0;  // option chain (tests): compressed searches take the serial chain
     double stage_ms[ST_N][64] = {};  // option sim: stage times summed over sim_n searches
     int64_t sim_n = 0;
     int64_t n_search = 0, n_flagged = 0, n_overflow = 0, n_chain = 0, last_flagged = 0, last_overflow = 0;
@@ -534,16 +610,12 @@ int chain_list(wv_multi* m, int64_t nq, int64_t d, int k, DBuf MRank::*listp, in
     });
 }
 
-int multi_search(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, uint64_t* o_i0, float* o_d0, int32_t* o_n0,
-                 hipStream_t cs) {
-    const int W = m->world, n = m->nl, k1 = k + 1;
-    if (m->sim) m->sim_n++;
-    m->last_flagged = m->last_overflow = 0;
-    // every shard's work follows the caller's stream; queries go to each device once
+// every shard's work follows the caller's stream; queries go to each device once
+int stage_queries(wv_multi* m, const float* q0, int64_t nq, int64_t d, hipStream_t cs) {
     MRank& H = *m->r[0];
     HIPCHK(hipSetDevice(H.dev));
     HIPCHK(hipEventRecord(m->e_call, cs));
-    for (int i = 0; i < n; i++) {
+    for (int i = 0; i < m->nl; i++) {
         MRank& R = *m->r[i];
         HIPCHK(hipSetDevice(R.dev));
         HIPCHK(hipStreamWaitEvent(R.s, m->e_call, 0));
@@ -554,6 +626,32 @@ int multi_search(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, uin
             HIPCHK(hipMemcpyPeerAsync(R.q.p, R.dev, q0, H.dev, qb, R.s));
             R.qp = R.q.as<float>();
         }
+    }
+    return WV_OK;
+}
+
+// the caller's stream waits for every shard
+int join_caller(wv_multi* m, hipStream_t cs) {
+    MRank& H = *m->r[0];
+    for (int i = 0; i < m->nl; i++) {
+        MRank& R = *m->r[i];
+        HIPCHK(hipSetDevice(R.dev));
+        HIPCHK(hipEventRecord(R.e_out, R.s));
+        HIPCHK(hipSetDevice(H.dev));
+        HIPCHK(hipStreamWaitEvent(cs, R.e_out, 0));
+    }
+    return WV_OK;
+}
+
+int multi_search(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, uint64_t* o_i0, float* o_d0, int32_t* o_n0,
+                 hipStream_t cs) {
+    const int W = m->world, n = m->nl, k1 = k + 1;
+    MRank& H = *m->r[0];
+    int rc = stage_queries(m, q0, nq, d, cs);
+    if (rc) return rc;
+    for (int i = 0; i < n; i++) {
+        MRank& R = *m->r[i];
+        HIPCHK(hipSetDevice(R.dev));
         HIPCHK(R.topA.ensure((size_t)nq * k1 * 4));
         HIPCHK(R.eps.ensure((size_t)nq * 4));
         HIPCHK(R.gA.ensure((size_t)W * nq * k1 * 4));
@@ -580,7 +678,7 @@ int multi_search(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, uin
     auto ON = [&](MRank& R, int i) { return i == 0 ? o_n0 : R.on.as<int32_t>(); };
 
     // 1. phase 1
-    int rc = run_stage(m, ST_PHASE1, [&](MRank& R, int) -> int {
+    rc = run_stage(m, ST_PHASE1, [&](MRank& R, int) -> int {
         R.off = false;
         int e = wv_index_shard_phase1(R.idx, R.qp, nq, d, k, R.topA.as<float>(), R.eps.as<float>(), R.s);
         if (e != WV_ERR_UNSUPPORTED) return e;
@@ -738,15 +836,470 @@ int multi_search(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, uin
             if (rc) return rc;
         }
     }
-    // the caller's stream waits for every shard
-    for (int i = 0; i < n; i++) {
+    return join_caller(m, cs);
+}
+
+// ---------------------------------------------------------------------------
+// compressed searches: the R-heap of flat.searchByVectorQuantized (BQ, rq-8 /
+// rq-1) or the worker heap of hnsw.flatSearch (trained PQ, SQ) across the
+// shards in id order (sharded.py ShardedBQSearch / ShardedQuantSearch, DESIGN
+// §4): every shard's compressed block minima in parallel; the R smallest
+// minima of each shard all-gathered; shard 0 replays from empty heaps, shard
+// r >= 1 from R copies of T_r recording its insertions; the records
+// all-gathered and applied on shard 0's states (wv_heap_merge_records) = the
+// serial chain's heaps (a record over its cap sends the chunk down that chain:
+// one broadcast per hop); then the candidates each shard owns are rescored,
+// the [world][nq][R] tiles all-gathered, and the rescoring heap runs on local
+// shard 0 (the caller's outputs).
+// ---------------------------------------------------------------------------
+enum { MK_EXACT, MK_BQ, MK_QUANT };
+
+int search_kind(const wv_index* i) {
+    if (i->compression == WV_COMPRESSION_BQ) return MK_BQ;
+    if (i->rq_bits || i->compression == WV_COMPRESSION_SQ || (i->compression == WV_COMPRESSION_PQ && i->pq_trained))
+        return MK_QUANT;
+    return MK_EXACT;  // uncompressed, or PQ before its codebook (the exact search, as one index runs it)
+}
+
+// the smallest of every rank's `v` (a batch size all ranks take): in-process
+// worlds directly, otherwise one all-gather of 8 bytes per rank
+int agree_min(wv_multi* m, const std::vector<int64_t>& local, int64_t* out) {
+    int64_t v = INT64_MAX;
+    for (int64_t x : local) v = std::min(v, x);
+    if (m->world == 1 || m->nl == m->world) { *out = v; return WV_OK; }
+    for (auto& Rp : m->r) {
+        MRank& R = *Rp;
+        HIPCHK(hipSetDevice(R.dev));
+        HIPCHK(R.mb.ensure(8));
+        HIPCHK(R.gmb.ensure((size_t)m->world * 8));
+        HIPCHK(hipMemcpyAsync(R.mb.p, &v, 8, hipMemcpyHostToDevice, R.s));
+    }
+    int rc = gather(m, {{&MRank::mb, &MRank::gmb}}, {(size_t)8});
+    if (rc) return rc;
+    MRank& H = *m->r[0];
+    std::vector<int64_t> all((size_t)m->world);
+    HIPCHK(hipSetDevice(H.dev));
+    HIPCHK(hipMemcpyAsync(all.data(), H.gmb.p, (size_t)m->world * 8, hipMemcpyDeviceToHost, H.s));
+    for (auto& Rp : m->r) { HIPCHK(hipSetDevice(Rp->dev)); HIPCHK(hipStreamSynchronize(Rp->s)); }
+    for (int64_t x : all) v = std::min(v, x);
+    *out = v;
+    return WV_OK;
+}
+
+int ensure_rank_iota(MRank& R, int64_t nq, hipStream_t s) {
+    if (R.iota.bytes >= (size_t)nq * 4) return WV_OK;
+    HIPCHK(R.iota.ensure((size_t)nq * 4));
+    k_iota32<<<(unsigned)((R.iota.bytes / 4 + 255) / 256), 256, 0, s>>>(R.iota.as<int32_t>(), (int64_t)(R.iota.bytes / 4));
+    HIPCHK(hipGetLastError());
+    return WV_OK;
+}
+
+// the parallel R-heap over the shards for one chunk of nc queries (each shard's
+// batch begun): bounds [nc][Rk] per shard (bounds_fn), replay states of shard 0
+// (replay_fn), recorded replays of shards r >= 1 (record_fn), the merge.  On
+// return *overflow = the chunk's queries whose record overflowed (0: fi / fd /
+// fn hold the merged heaps extracted ascending on every shard).
+template <class BoundsFn, class ReplayFn, class RecordFn>
+int rheap_parallel(wv_multi* m, int64_t nc, int Rk, int cap, BoundsFn bounds_fn, ReplayFn replay_fn, RecordFn record_fn,
+                   int* overflow) {
+    const int W = m->world;
+    int rc = run_stage(m, ST_PHASE2, [&](MRank& R, int) -> int {
+        HIPCHK(R.bnd.ensure((size_t)nc * Rk * 4));
+        HIPCHK(R.gbnd.ensure((size_t)W * nc * Rk * 4));
+        return bounds_fn(R);
+    });
+    if (rc) return rc;
+    rc = gather(m, {{&MRank::bnd, &MRank::gbnd}}, {(size_t)nc * Rk * 4});
+    if (rc) return rc;
+    rc = run_stage(m, ST_REPLAY, [&](MRank& R, int) -> int {
+        HIPCHK(R.ri.ensure((size_t)nc * cap * 8));
+        HIPCHK(R.rd.ensure((size_t)nc * cap * 4));
+        HIPCHK(R.rn.ensure((size_t)nc * 4));
+        HIPCHK(R.gri.ensure((size_t)W * nc * cap * 8));
+        HIPCHK(R.grd.ensure((size_t)W * nc * cap * 4));
+        HIPCHK(R.grn.ensure((size_t)W * nc * 4));
+        if (R.rank == 0) {
+            HIPCHK(R.ti.ensure((size_t)nc * Rk * 8));
+            HIPCHK(R.td.ensure((size_t)nc * Rk * 4));
+            HIPCHK(R.tn.ensure((size_t)nc * 4));
+            int e = replay_fn(R);
+            if (e) return e;
+            HIPCHK(hipSetDevice(R.dev));
+            k_state_to_rec<<<(unsigned)nc, 64, 0, R.s>>>(R.ti.as<uint64_t>(), R.td.as<float>(), R.tn.as<int32_t>(), (int)nc,
+                                                          Rk, cap, R.ri.as<uint64_t>(), R.rd.as<float>(), R.rn.as<int32_t>());
+            HIPCHK(hipGetLastError());
+            return WV_OK;
+        }
+        HIPCHK(R.fki.ensure((size_t)nc * Rk * 8));
+        HIPCHK(R.fkd.ensure((size_t)nc * Rk * 4));
+        HIPCHK(R.fkn.ensure((size_t)nc * 4));
+        const size_t lds = (size_t)R.rank * Rk * 4;
+        if (lds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "prefix bound: %d ranks x %d minima exceed LDS", R.rank, Rk);
+        HIPCHK(hipSetDevice(R.dev));
+        if (lds > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute((const void*)k_prefix_bound, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        k_prefix_bound<<<(unsigned)nc, 256, lds, R.s>>>(R.rank, nullptr, (int)nc, Rk, Rk, nc, R.gbnd.as<float>(), nullptr,
+                                                        nullptr, nullptr, nullptr, R.fki.as<uint64_t>(), R.fkd.as<float>(),
+                                                        R.fkn.as<int32_t>());
+        HIPCHK(hipGetLastError());
+        return record_fn(R);
+    });
+    if (rc) return rc;
+    rc = gather(m, {{&MRank::ri, &MRank::gri}, {&MRank::rd, &MRank::grd}, {&MRank::rn, &MRank::grn}},
+                {(size_t)nc * cap * 8, (size_t)nc * cap * 4, (size_t)nc * 4});
+    if (rc) return rc;
+    rc = run_stage(m, ST_MERGE_REC, [&](MRank& R, int i) -> int {
+        HIPCHK(R.sti.ensure((size_t)nc * Rk * 8));
+        HIPCHK(R.std_.ensure((size_t)nc * Rk * 4));
+        HIPCHK(R.fi.ensure((size_t)nc * Rk * 8));
+        HIPCHK(R.fd.ensure((size_t)nc * Rk * 4));
+        HIPCHK(R.fn.ensure((size_t)nc * 4));
+        HIPCHK(R.un.ensure((size_t)nc * 4));
+        HIPCHK(R.ul.ensure((size_t)nc * 4));
+        HIPCHK(R.nu.ensure(16));
+        HIPCHK(hipMemsetAsync(R.un.p, 0, (size_t)nc * 4, R.s));
+        HIPCHK(hipMemcpy2DAsync(R.sti.p, (size_t)Rk * 8, R.gri.p, (size_t)cap * 8, (size_t)Rk * 8, nc,
+                                hipMemcpyDeviceToDevice, R.s));
+        HIPCHK(hipMemcpy2DAsync(R.std_.p, (size_t)Rk * 4, R.grd.p, (size_t)cap * 4, (size_t)Rk * 4, nc,
+                                hipMemcpyDeviceToDevice, R.s));
+        int e = wv_heap_merge_records(R.dev, (int)nc, Rk, W, cap, R.sti.as<uint64_t>(), R.std_.as<float>(),
+                                      R.grn.as<int32_t>(), R.gri.as<uint64_t>(), R.grd.as<float>(), R.grn.as<int32_t>(),
+                                      R.fi.as<uint64_t>(), R.fd.as<float>(), R.fn.as<int32_t>(), R.un.as<int32_t>(), R.s);
+        if (e) return e;
+        HIPCHK(hipSetDevice(R.dev));
+        k_list_ascending<<<1, 1024, 0, R.s>>>(R.un.as<int32_t>(), nullptr, (int)nc, R.ul.as<int32_t>(), R.nu.as<int32_t>());
+        HIPCHK(hipGetLastError());
+        if (i == 0) HIPCHK(hipMemcpyAsync(m->pin + 1, R.nu.p, 4, hipMemcpyDeviceToHost, R.s));
+        return WV_OK;
+    });
+    if (rc) return rc;
+    MRank& H = *m->r[0];
+    HIPCHK(hipSetDevice(H.dev));
+    HIPCHK(hipStreamSynchronize(H.s));  // host sync: overflowed records (the same count on every rank)
+    *overflow = m->pin[1];
+    return WV_OK;
+}
+
+// the serial chain over the shards for one chunk (states [nc][Rk] by query): rank
+// h continues rank h-1's heaps (hop_fn(R, in_i, in_d, in_n, last, out...)), one
+// broadcast per hop; the last hop's output (pop order / extracted) ends in
+// ci / cd / cn[(W - 1) & 1] of every shard
+template <class HopFn>
+int rheap_chain(wv_multi* m, int64_t nc, int Rk, HopFn hop_fn) {
+    const int W = m->world, n = m->nl;
+    for (auto& Rp : m->r) {
+        MRank& R = *Rp;
+        HIPCHK(hipSetDevice(R.dev));
+        for (int b = 0; b < 2; b++) {
+            HIPCHK(R.ci[b].ensure((size_t)nc * Rk * 8));
+            HIPCHK(R.cd[b].ensure((size_t)nc * Rk * 4));
+            HIPCHK(R.cn[b].ensure((size_t)nc * 4));
+        }
+    }
+    for (int h = 0; h < W; h++) {
+        const int cur = h & 1, prev = cur ^ 1;
+        int rc = run_stage(m, ST_CHAIN, [&](MRank& R, int) -> int {
+            if (R.rank != h) return WV_OK;
+            m->n_chain++;
+            return hop_fn(R, h ? R.ci[prev].as<uint64_t>() : nullptr, h ? R.cd[prev].as<float>() : nullptr,
+                          h ? R.cn[prev].as<int32_t>() : nullptr, h == W - 1, R.ci[cur].as<uint64_t>(),
+                          R.cd[cur].as<float>(), R.cn[cur].as<int32_t>());
+        });
+        if (rc) return rc;
+        std::vector<void*> bufs;
+        for (int f = 0; f < 3; f++)
+            for (int i = 0; i < n; i++) {
+                MRank& R = *m->r[i];
+                bufs.push_back(f == 0 ? R.ci[cur].p : f == 1 ? R.cd[cur].p : R.cn[cur].p);
+            }
+        rc = bcast(m, bufs, {(size_t)nc * Rk * 8, (size_t)nc * Rk * 4, (size_t)nc * 4}, h);
+        if (rc) return rc;
+    }
+    return WV_OK;
+}
+
+// candidates [nc][Rk] (global ids) -> each shard's exact distances of the ids it
+// holds (rescore_fn), the tiles all-gathered into gEall [W][nc][Rk]
+template <class RescoreFn>
+int rescore_gather(wv_multi* m, int64_t nc, int Rk, RescoreFn rescore_fn) {
+    const int W = m->world;
+    int rc = run_stage(m, ST_MERGE, [&](MRank& R, int) -> int {
+        HIPCHK(R.E.ensure((size_t)nc * Rk * 4));
+        HIPCHK(R.gEall.ensure((size_t)W * nc * Rk * 4));
+        HIPCHK(hipMemsetAsync(R.E.p, 0, (size_t)nc * Rk * 4, R.s));
+        return rescore_fn(R);
+    });
+    if (rc) return rc;
+    if (W == 1) {
+        MRank& R = *m->r[0];
+        HIPCHK(hipSetDevice(R.dev));
+        HIPCHK(hipMemcpyAsync(R.gEall.p, R.E.p, (size_t)nc * Rk * 4, hipMemcpyDeviceToDevice, R.s));
+        return WV_OK;
+    }
+    return gather(m, {{&MRank::E, &MRank::gEall}}, {(size_t)nc * Rk * 4});
+}
+
+// BQ (flat/index.go:460-532) over the shards, chunks of the batch that one
+// block-minima group of every shard holds
+int multi_search_bq(wv_multi* m, int64_t nq, int64_t d, int k, uint64_t* o_i0, float* o_d0, int32_t* o_n0) {
+    const int W = m->world;
+    std::vector<int64_t> mb;
+    for (auto& R : m->r) mb.push_back(bq_max_batch(R->idx));
+    int64_t chunk = 0;
+    int rc = agree_min(m, mb, &chunk);
+    if (rc) return rc;
+    chunk = std::max<int64_t>(1, std::min(chunk, nq));
+    for (int64_t c0 = 0; c0 < nq; c0 += chunk) {
+        const int64_t nc = std::min(chunk, nq - c0);
+        rc = run_stage(m, ST_PHASE1, [&](MRank& R, int) -> int {
+            return wv_index_bq_begin(R.idx, R.qp + c0 * d, nc, d, k, R.s);
+        });
+        if (rc) return rc;
+        const int Rk = m->r[0]->idx->bq_R;  // searchTimeRescore: max(rescore limit, k), equal on every shard
+        bool chain = W == 1 || m->force_chain;
+        // the candidates in pop order on every shard: the parallel form's
+        // reversed merge (cand, fn) or the chain's last hop
+        auto candv = [&](MRank& R) -> DBuf& { return chain ? R.ci[(W - 1) & 1] : R.cand; };
+        auto cnv = [&](MRank& R) -> DBuf& { return chain ? R.cn[(W - 1) & 1] : R.fn; };
+        if (!chain) {
+            int ovf = 0;
+            const int cap = m->rec_cap > 0 ? std::max(m->rec_cap, Rk) : 2 * Rk;
+            rc = rheap_parallel(
+                m, nc, Rk, cap,
+                [&](MRank& R) { return wv_index_bq_bounds(R.idx, R.bnd.as<float>(), R.s); },
+                [&](MRank& R) {
+                    return wv_index_bq_replay(R.idx, nullptr, nullptr, nullptr, 0, R.ti.as<uint64_t>(), R.td.as<float>(),
+                                              R.tn.as<int32_t>(), R.s);
+                },
+                [&](MRank& R) {
+                    return wv_index_bq_replay_record(R.idx, R.fki.as<uint64_t>(), R.fkd.as<float>(), R.fkn.as<int32_t>(),
+                                                     cap, R.ri.as<uint64_t>(), R.rd.as<float>(), R.rn.as<int32_t>(),
+                                                     R.s);
+                },
+                &ovf);
+            if (rc) return rc;
+            m->last_overflow += ovf;
+            m->n_overflow += ovf;
+            if (ovf > 0) chain = true;
+            else {
+                rc = run_stage(m, ST_MERGE_REC, [&](MRank& R, int) -> int {
+                    HIPCHK(R.cand.ensure((size_t)nc * Rk * 8));
+                    k_rev_rows<<<(unsigned)nc, 64, 0, R.s>>>(R.fi.as<uint64_t>(), R.fn.as<int32_t>(), Rk,
+                                                             R.cand.as<uint64_t>());
+                    HIPCHK(hipGetLastError());
+                    return WV_OK;
+                });
+                if (rc) return rc;
+            }
+        }
+        if (chain) {
+            rc = rheap_chain(m, nc, Rk, [&](MRank& R, const uint64_t* ii, const float* id, const int32_t* in, bool last,
+                                            uint64_t* oi, float* od, int32_t* on) {
+                return wv_index_bq_replay(R.idx, ii, id, in, last ? 1 : 0, oi, od, on, R.s);
+            });
+            if (rc) return rc;
+        }
+        rc = rescore_gather(m, nc, Rk, [&](MRank& R) {
+            return wv_index_bq_rescore(R.idx, candv(R).as<uint64_t>(), cnv(R).as<int32_t>(), R.E.as<float>(), R.s);
+        });
+        if (rc) return rc;
+        MRank& H = *m->r[0];
+        HIPCHK(hipSetDevice(H.dev));
+        rc = ensure_rank_iota(H, nc, H.s);
+        if (rc) return rc;
+        const size_t lds_f = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
+        if (lds_f > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute((const void*)k_bq_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
+        k_bq_final<<<(unsigned)nc, 64, lds_f, H.s>>>(candv(H).as<uint64_t>(), H.gEall.as<float>(),
+                                                     cnv(H).as<int32_t>(), H.iota.as<int32_t>(), (int)nc, Rk, k, W,
+                                                     m->id_stride, o_i0 + c0 * k, o_d0 + c0 * k, o_n0 + c0, 0);
+        HIPCHK(hipGetLastError());
+    }
+    return WV_OK;
+}
+
+// trained PQ / SQ (hnsw/flat_search.go:28-141 + h.rescore) and flat rq-8 / rq-1
+// (flat/index.go:460-532) over the shards: the worker heap of limit R across the
+// shards, then the result heap / rescoring (wv_index_quant_*)
+int multi_search_quant(wv_multi* m, int64_t nq, int64_t d, int k, uint64_t* o_i0, float* o_d0, int32_t* o_n0) {
+    const int W = m->world;
+    std::vector<int64_t> mb;
+    for (auto& R : m->r) {
+        int64_t v = 1;
+        int rc = wv_index_quant_max_batch(R->idx, k, W, &v);
+        if (rc) return rc;
+        mb.push_back(v);
+    }
+    int64_t chunk = 0;
+    int rc = agree_min(m, mb, &chunk);
+    if (rc) return rc;
+    chunk = std::max<int64_t>(1, std::min(chunk, nq));
+    for (int64_t c0 = 0; c0 < nq; c0 += chunk) {
+        const int64_t nc = std::min(chunk, nq - c0);
+        int64_t info[64][4] = {};
+        rc = run_stage(m, ST_PHASE1, [&](MRank& R, int i) -> int {
+            int e = wv_index_quant_begin(R.idx, R.qp + c0 * d, nc, d, k, info[i], R.s);
+            R.nblk = info[i][1];
+            return e;
+        });
+        if (rc) return rc;
+        const int Rk = (int)info[0][0], rescore = (int)info[0][2], form = (int)info[0][3];
+        bool chain = W == 1 || m->force_chain;
+        // the merged worker heap extracted ascending: the parallel form's merge
+        // (fi, fd, fn) or the chain's last hop
+        auto aiv = [&](MRank& R) -> DBuf& { return chain ? R.ci[(W - 1) & 1] : R.fi; };
+        auto adv = [&](MRank& R) -> DBuf& { return chain ? R.cd[(W - 1) & 1] : R.fd; };
+        auto anv = [&](MRank& R) -> DBuf& { return chain ? R.cn[(W - 1) & 1] : R.fn; };
+        if (!chain) {
+            int ovf = 0;
+            const int cap = m->rec_cap > 0 ? std::max(m->rec_cap, Rk) : 2 * Rk + 64;
+            rc = rheap_parallel(
+                m, nc, Rk, cap,
+                [&](MRank& R) -> int {
+                    HIPCHK(R.bm.ensure((size_t)nc * R.nblk * 4));
+                    int e = wv_index_quant_blockmin(R.idx, R.bm.as<float>(), R.s);
+                    if (e) return e;
+                    HIPCHK(hipSetDevice(R.dev));
+                    k_smallest_r<<<(unsigned)nc, 256, 0, R.s>>>(R.bm.as<float>(), R.nblk, Rk, R.bnd.as<float>());
+                    HIPCHK(hipGetLastError());
+                    return WV_OK;
+                },
+                [&](MRank& R) {
+                    return wv_index_quant_replay(R.idx, nullptr, nullptr, nullptr, 0, R.ti.as<uint64_t>(),
+                                                 R.td.as<float>(), R.tn.as<int32_t>(), R.s);
+                },
+                [&](MRank& R) {
+                    return wv_index_quant_replay_record(R.idx, R.fki.as<uint64_t>(), R.fkd.as<float>(),
+                                                        R.fkn.as<int32_t>(), cap, R.ri.as<uint64_t>(), R.rd.as<float>(),
+                                                        R.rn.as<int32_t>(), R.s);
+                },
+                &ovf);
+            if (rc) return rc;
+            m->last_overflow += ovf;
+            m->n_overflow += ovf;
+            chain = ovf > 0;
+        }
+        if (chain) {
+            rc = rheap_chain(m, nc, Rk, [&](MRank& R, const uint64_t* ii, const float* id, const int32_t* in, bool last,
+                                            uint64_t* oi, float* od, int32_t* on) {
+                return wv_index_quant_replay(R.idx, ii, id, in, last ? 1 : 0, oi, od, on, R.s);
+            });
+            if (rc) return rc;
+        }
+        MRank& H = *m->r[0];
+        if (!rescore) {
+            HIPCHK(hipSetDevice(H.dev));
+            rc = wv_index_quant_finish(H.idx, aiv(H).as<uint64_t>(), adv(H).as<float>(), anv(H).as<int32_t>(),
+                                       o_i0 + c0 * k, o_d0 + c0 * k, o_n0 + c0, nullptr, nullptr, H.s);
+            if (rc) return rc;
+            continue;
+        }
+        rc = rescore_gather(m, nc, Rk, [&](MRank& R) -> int {
+            HIPCHK(R.cand.ensure((size_t)nc * Rk * 8));
+            HIPCHK(R.un.ensure((size_t)nc * 4));
+            int e = wv_index_quant_finish(R.idx, aiv(R).as<uint64_t>(), adv(R).as<float>(), anv(R).as<int32_t>(),
+                                          nullptr, nullptr, nullptr, R.cand.as<uint64_t>(), R.un.as<int32_t>(), R.s);
+            if (e) return e;
+            return wv_index_quant_rescore(R.idx, R.cand.as<uint64_t>(), R.un.as<int32_t>(), R.E.as<float>(), R.s);
+        });
+        if (rc) return rc;
+        HIPCHK(hipSetDevice(H.dev));
+        rc = ensure_rank_iota(H, nc, H.s);
+        if (rc) return rc;
+        if (form == 1) {  // searchByVectorQuantized's rescoring heap, candidates ascending
+            const size_t lds_f = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 16;
+            if (lds_f > 64 * 1024)
+                HIPCHK(hipFuncSetAttribute((const void*)k_bq_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
+            k_bq_final<<<(unsigned)nc, 64, lds_f, H.s>>>(H.cand.as<uint64_t>(), H.gEall.as<float>(), H.un.as<int32_t>(),
+                                                         H.iota.as<int32_t>(), (int)nc, Rk, k, W, m->id_stride,
+                                                         o_i0 + c0 * k, o_d0 + c0 * k, o_n0 + c0, 1);
+        } else {  // h.rescore
+            const size_t lds_q = (size_t)(k + 1) * (sizeof(uint64_t) + sizeof(float)) + 16;
+            if (lds_q > 64 * 1024)
+                HIPCHK(hipFuncSetAttribute((const void*)k_pq_rescore_final, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds_q));
+            k_pq_rescore_final<<<(unsigned)nc, 64, lds_q, H.s>>>(nullptr, H.gEall.as<float>(), H.un.as<int32_t>(),
+                                                                 H.iota.as<int32_t>(), (int)nc, Rk, k, 0, o_i0 + c0 * k,
+                                                                 o_d0 + c0 * k, o_n0 + c0, H.cand.as<uint64_t>(), W,
+                                                                 m->id_stride);
+        }
+        HIPCHK(hipGetLastError());
+    }
+    return WV_OK;
+}
+
+// every search of the multi-shard index: the protocol of the shards' kind
+int multi_dispatch(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, uint64_t* o_i0, float* o_d0, int32_t* o_n0,
+                   hipStream_t cs) {
+    const int kind = search_kind(m->r[0]->idx);
+    for (auto& R : m->r)
+        if (search_kind(R->idx) != kind)
+            return set_err(WV_ERR_INVALID, "multi-shard index: shards differ in compression state (train every shard's "
+                                           "quantizer: wv_multi_pq_fit / wv_multi_pq_set_centers)");
+    if (m->sim) m->sim_n++;
+    m->last_flagged = m->last_overflow = 0;
+    int rc;
+    if (kind == MK_EXACT) rc = multi_search(m, q0, nq, d, k, o_i0, o_d0, o_n0, cs);
+    else {
+        rc = stage_queries(m, q0, nq, d, cs);
+        if (!rc) rc = kind == MK_BQ ? multi_search_bq(m, nq, d, k, o_i0, o_d0, o_n0)
+                                    : multi_search_quant(m, nq, d, k, o_i0, o_d0, o_n0);
+        if (!rc) rc = join_caller(m, cs);
+    }
+    if (rc) return rc;
+    m->n_search++;
+    return WV_OK;
+}
+
+// A filtered search (the shard's allow list, shard_read.go:401-413 -> flat
+// SearchByVector(..., allowList), :466): while the scope stands, every local
+// shard reads present & allow (its part of the list) as its present bitmap, so
+// every stage of every protocol -- keys, exact rows, replays, BQ / quantized
+// minima -- scans only allowed rows.  Restored (and the batch state dropped)
+// when the scope ends.
+struct FilterScope {
+    wv_multi* m = nullptr;
+    ~FilterScope() { restore(); }
+    void restore() {
+        if (!m) return;
+        for (auto& Rp : m->r) {
+            MRank& R = *Rp;
+            if (!R.saved_present) continue;
+            hipSetDevice(R.dev);
+            hipStreamSynchronize(R.s);  // no kernel of the search still reads the allow bitmap
+            std::lock_guard<std::mutex> g(R.idx->mu);
+            R.idx->present = R.saved_present;
+            R.idx->npresent = R.saved_npresent;
+            R.saved_present = nullptr;
+            invalidate_batch(R.idx);
+            note_mutation(R.idx);
+        }
+        m = nullptr;
+    }
+};
+
+int filter_begin(wv_multi* m, FilterScope& fs, const uint64_t* allow, int64_t n_allow) {
+    std::vector<std::vector<uint64_t>> part((size_t)m->nl);
+    for (int64_t i = 0; i < n_allow; i++) {
+        const int r = owner_rank(m, allow[i]) - m->rank0;
+        if (r >= 0 && r < m->nl) part[(size_t)r].push_back(allow[i]);
+    }
+    fs.m = m;
+    for (int i = 0; i < m->nl; i++) {
         MRank& R = *m->r[i];
         HIPCHK(hipSetDevice(R.dev));
-        HIPCHK(hipEventRecord(R.e_out, R.s));
-        HIPCHK(hipSetDevice(H.dev));
-        HIPCHK(hipStreamWaitEvent(cs, R.e_out, 0));
+        std::lock_guard<std::mutex> g(R.idx->mu);
+        const uint32_t* valid = nullptr;
+        int64_t nv = 0;
+        int rc = shard_filter_bitmap(R.idx, R.s, part[(size_t)i].data(), (int64_t)part[(size_t)i].size(), &valid, &nv);
+        if (rc) return rc;
+        R.saved_present = R.idx->present;
+        R.saved_npresent = R.idx->npresent;
+        R.idx->present = const_cast<uint32_t*>(valid);
+        R.idx->npresent = nv;
+        invalidate_batch(R.idx);
+        note_mutation(R.idx);
     }
-    m->n_search++;
     return WV_OK;
 }
 
@@ -789,8 +1342,8 @@ extern "C" int wv_multi_create(const wv_multi_config* cfg, wv_multi** out) {
         return set_err(WV_ERR_INVALID, "invalid multi config: world %d, rank0 %d, n_local %d", cfg->world, cfg->rank0,
                        cfg->n_local);
     if (cfg->n_local > 64) return set_err(WV_ERR_INVALID, "at most 64 shards per process");
-    if (cfg->index.compression != WV_COMPRESSION_NONE)
-        return set_err(WV_ERR_UNSUPPORTED, "multi-shard index: exact (uncompressed) search only");
+    if (cfg->index.compression < WV_COMPRESSION_NONE || cfg->index.compression > WV_COMPRESSION_SQ)
+        return set_err(WV_ERR_INVALID, "unknown compression %d", cfg->index.compression);
     if (cfg->transport != WV_TRANSPORT_LOCAL && cfg->transport != WV_TRANSPORT_RCCL &&
         cfg->transport != WV_TRANSPORT_HOST)
         return set_err(WV_ERR_INVALID, "unknown transport %d", cfg->transport);
@@ -875,6 +1428,10 @@ extern "C" int wv_multi_set_option(wv_multi* m, const char* key, int64_t value) 
         memset(m->stage_ms, 0, sizeof(m->stage_ms));
         return WV_OK;
     }
+    if (std::string(key) == "chain") {
+        m->force_chain = value ? 1 : 0;
+        return WV_OK;
+    }
     if (std::string(key) == "rec_cap") {
         if (value < 0 || value > (1 << 20)) return set_err(WV_ERR_INVALID, "rec_cap out of range");
         m->rec_cap = (int)value;
@@ -900,6 +1457,12 @@ extern "C" int wv_multi_add_batch(wv_multi* m, const uint64_t* ids, const float*
                            (unsigned long long)ids[i], r + m->rank0);
         rows[r].push_back(i);
     }
+    // ValidateBeforeInsert on every receiving shard first: a failed call inserts nothing
+    for (int r = 0; r < m->nl; r++)
+        if (!rows[r].empty()) {
+            int rc = wv_index_validate_before_insert(m->r[r]->idx, d);
+            if (rc) return rc;
+        }
     std::vector<uint64_t> si;
     std::vector<float> sv;
     for (int r = 0; r < m->nl; r++) {
@@ -923,8 +1486,73 @@ extern "C" int wv_multi_search_device(wv_multi* m, const float* d_queries, int64
     if (nq < 0 || (nq > 0 && (!d_queries || !d_ids || !d_dists || !d_counts))) return set_err(WV_ERR_INVALID, "nil buffer");
     if (nq == 0) return WV_OK;
     std::lock_guard<std::mutex> g(m->mu);
-    int rc = multi_search(m, d_queries, nq, d, k, d_ids, d_dists, d_counts, (hipStream_t)stream);
+    int rc = multi_dispatch(m, d_queries, nq, d, k, d_ids, d_dists, d_counts, (hipStream_t)stream);
     if (rc) return rc;
+    if (!stream) {
+        HIPCHK(hipSetDevice(m->r[0]->dev));
+        HIPCHK(hipStreamSynchronize(nullptr));
+    }
+    return WV_OK;
+}
+
+namespace {
+int check_allow(const uint64_t* allow_ids, int64_t n_allow, int32_t allow_mode) {
+    if (allow_mode != 0 && allow_mode != 1) return set_err(WV_ERR_INVALID, "allow mode %d", allow_mode);
+    if (allow_mode == 1 && (n_allow < 0 || (n_allow > 0 && !allow_ids))) return set_err(WV_ERR_INVALID, "nil allow ids");
+    return WV_OK;
+}
+
+// one batch from host buffers (m->mu held); allow_mode 1: under the allow list
+int multi_host_batch(wv_multi* m, const float* queries, int64_t nq, int64_t d, int32_t k, const uint64_t* allow_ids,
+                     int64_t n_allow, int32_t allow_mode, uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    if (allow_mode == 1 && n_allow == 0) {  // flat/index.go:590-594: an empty allow list finds nothing
+        for (int64_t q = 0; q < nq; q++) out_counts[q] = 0;
+        return WV_OK;
+    }
+    MRank& H = *m->r[0];
+    HIPCHK(hipSetDevice(H.dev));
+    DBuf q, oi, od, on;
+    HIPCHK(q.ensure((size_t)nq * d * 4));
+    HIPCHK(oi.ensure((size_t)nq * k * 8));
+    HIPCHK(od.ensure((size_t)nq * k * 4));
+    HIPCHK(on.ensure((size_t)nq * 4));
+    HIPCHK(hipMemcpyAsync(q.p, queries, (size_t)nq * d * 4, hipMemcpyHostToDevice, H.s));
+    FilterScope fs;
+    int rc = allow_mode == 1 ? filter_begin(m, fs, allow_ids, n_allow) : WV_OK;
+    if (!rc) rc = multi_dispatch(m, q.as<float>(), nq, d, k, oi.as<uint64_t>(), od.as<float>(), on.as<int32_t>(), H.s);
+    if (rc) {
+        for (auto& R : m->r) { hipSetDevice(R->dev); hipStreamSynchronize(R->s); }
+        return rc;
+    }
+    HIPCHK(hipSetDevice(H.dev));
+    HIPCHK(hipMemcpyAsync(out_ids, oi.p, (size_t)nq * k * 8, hipMemcpyDeviceToHost, H.s));
+    HIPCHK(hipMemcpyAsync(out_dists, od.p, (size_t)nq * k * 4, hipMemcpyDeviceToHost, H.s));
+    HIPCHK(hipMemcpyAsync(out_counts, on.p, (size_t)nq * 4, hipMemcpyDeviceToHost, H.s));
+    HIPCHK(hipStreamSynchronize(H.s));
+    return WV_OK;
+}
+}  // namespace
+
+extern "C" int wv_multi_search_device_allow(wv_multi* m, const float* d_queries, int64_t nq, int64_t d, int32_t k,
+                                            const uint64_t* allow_ids, int64_t n_allow, int32_t allow_mode,
+                                            uint64_t* d_ids, float* d_dists, int32_t* d_counts, void* stream) {
+    if (!m) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    if (nq < 0 || (nq > 0 && (!d_queries || !d_ids || !d_dists || !d_counts))) return set_err(WV_ERR_INVALID, "nil buffer");
+    int rc = check_allow(allow_ids, n_allow, allow_mode);
+    if (rc) return rc;
+    if (nq == 0) return WV_OK;
+    std::lock_guard<std::mutex> g(m->mu);
+    hipStream_t cs = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(m->r[0]->dev));
+    if (allow_mode == 1 && n_allow == 0) {
+        HIPCHK(hipMemsetAsync(d_counts, 0, (size_t)nq * 4, cs));
+    } else {
+        FilterScope fs;
+        rc = allow_mode == 1 ? filter_begin(m, fs, allow_ids, n_allow) : WV_OK;
+        if (!rc) rc = multi_dispatch(m, d_queries, nq, d, k, d_ids, d_dists, d_counts, cs);
+        if (rc) return rc;
+    }
     if (!stream) {
         HIPCHK(hipSetDevice(m->r[0]->dev));
         HIPCHK(hipStreamSynchronize(nullptr));
@@ -934,26 +1562,225 @@ extern "C" int wv_multi_search_device(wv_multi* m, const float* d_queries, int64
 
 extern "C" int wv_multi_search_by_vector_batch(wv_multi* m, const float* queries, int64_t nq, int64_t d, int32_t k,
                                                uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    return wv_multi_search_by_vector_batch_allow(m, queries, nq, d, k, nullptr, 0, 0, out_ids, out_dists, out_counts);
+}
+
+extern "C" int wv_multi_search_by_vector_batch_allow(wv_multi* m, const float* queries, int64_t nq, int64_t d, int32_t k,
+                                                     const uint64_t* allow_ids, int64_t n_allow, int32_t allow_mode,
+                                                     uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
     if (!m) return set_err(WV_ERR_INVALID, "nil index");
     if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    int rc = check_allow(allow_ids, n_allow, allow_mode);
+    if (rc) return rc;
     if (nq <= 0) return WV_OK;
     if (!queries || !out_ids || !out_dists || !out_counts || d <= 0) return set_err(WV_ERR_INVALID, "nil buffer");
     std::lock_guard<std::mutex> g(m->mu);
+    return multi_host_batch(m, queries, nq, d, k, allow_ids, n_allow, allow_mode, out_ids, out_dists, out_counts);
+}
+
+extern "C" int wv_multi_search_by_vector_batch_multi_allow(wv_multi* m, const float* queries, int64_t nq, int64_t d,
+                                                           int32_t k, const uint64_t* allow_ids,
+                                                           const int64_t* allow_offsets, const int32_t* allow_modes,
+                                                           uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    if (!m) return set_err(WV_ERR_INVALID, "nil index");
+    if (k <= 0) return set_err(WV_ERR_INVALID, "k must be positive (reference heap Top() on empty queue)");
+    if (nq <= 0) return WV_OK;
+    if (!queries || !out_ids || !out_dists || !out_counts || !allow_offsets || !allow_modes || d <= 0)
+        return set_err(WV_ERR_INVALID, "nil buffer");
+    for (int64_t q = 0; q < nq; q++) {
+        if (allow_modes[q] != 0 && allow_modes[q] != 1) return set_err(WV_ERR_INVALID, "allow mode %d", allow_modes[q]);
+        if (allow_offsets[q] < 0 || allow_offsets[q + 1] < allow_offsets[q])
+            return set_err(WV_ERR_INVALID, "allow offsets not ascending at %lld", (long long)q);
+        if (allow_modes[q] == 1 && allow_offsets[q + 1] > allow_offsets[q] && !allow_ids)
+            return set_err(WV_ERR_INVALID, "nil allow ids");
+    }
+    std::lock_guard<std::mutex> g(m->mu);
+    // the queries grouped by identical list (every process groups the same
+    // queries and lists the same way: the map orders its keys), one filtered
+    // search over every shard per group
+    std::map<std::pair<int, std::string>, std::vector<int64_t>> groups;
+    for (int64_t q = 0; q < nq; q++) {
+        std::string key;
+        if (allow_modes[q] == 1)
+            key.assign(reinterpret_cast<const char*>(allow_ids + allow_offsets[q]),
+                       (size_t)(allow_offsets[q + 1] - allow_offsets[q]) * sizeof(uint64_t));
+        groups[{allow_modes[q], key}].push_back(q);
+    }
+    std::vector<float> qb;
+    std::vector<uint64_t> oi;
+    std::vector<float> od;
+    std::vector<int32_t> on;
+    for (auto& gq : groups) {
+        const std::vector<int64_t>& qs = gq.second;
+        const int64_t n = (int64_t)qs.size(), q0 = qs[0];
+        qb.resize((size_t)n * d);
+        oi.assign((size_t)n * k, 0);
+        od.assign((size_t)n * k, 0.f);
+        on.assign((size_t)n, 0);
+        for (int64_t i = 0; i < n; i++) memcpy(&qb[(size_t)i * d], queries + qs[(size_t)i] * d, (size_t)d * 4);
+        int rc = multi_host_batch(m, qb.data(), n, d, k, allow_modes[q0] ? allow_ids + allow_offsets[q0] : nullptr,
+                                  allow_offsets[q0 + 1] - allow_offsets[q0], allow_modes[q0], oi.data(), od.data(),
+                                  on.data());
+        if (rc) return rc;
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t q = qs[(size_t)i];
+            memcpy(out_ids + q * k, &oi[(size_t)i * k], (size_t)k * 8);
+            memcpy(out_dists + q * k, &od[(size_t)i * k], (size_t)k * 4);
+            out_counts[q] = on[(size_t)i];
+        }
+    }
+    return WV_OK;
+}
+
+// flat.SearchByVectorDistance (flat/index.go:699-761) over every shard: one
+// search with totalLimit = 100, then the results up to the target distance
+// (as wv_index_search_by_vector_distance); the per-shard calls of
+// shard_read.go:439 merged by distance (index.go:2067-2071) give the same rows
+extern "C" int wv_multi_search_by_vector_distance(wv_multi* m, const float* query, int64_t d, float target,
+                                                  int64_t max_limit, const uint64_t* allow_ids, int64_t n_allow,
+                                                  int32_t allow_mode, uint64_t* out_ids, float* out_dists,
+                                                  int32_t* out_count) {
+    (void)max_limit;
+    if (!m) return set_err(WV_ERR_INVALID, "nil index");
+    if (!query || !out_ids || !out_dists || !out_count || d <= 0) return set_err(WV_ERR_INVALID, "nil buffer");
+    int rc = check_allow(allow_ids, n_allow, allow_mode);
+    if (rc) return rc;
+    const int total_limit = 100;
+    std::vector<uint64_t> ids(total_limit);
+    std::vector<float> dd(total_limit);
+    int32_t n = 0;
+    {
+        std::lock_guard<std::mutex> g(m->mu);
+        rc = multi_host_batch(m, query, 1, d, total_limit, allow_ids, n_allow, allow_mode, ids.data(), dd.data(), &n);
+    }
+    if (rc) return rc;
+    int cnt = 0;
+    for (int i = 0; i < n && i < total_limit; i++) {
+        const double diff = std::fabs((double)dd[i] - (double)target);
+        if (dd[i] <= target || diff <= 1e-6) { out_ids[cnt] = ids[i]; out_dists[cnt] = dd[i]; cnt++; }
+        else break;
+    }
+    *out_count = cnt;
+    return WV_OK;
+}
+
+// ProductQuantizer.Fit for every shard (product_quantization.go:378-424): the
+// single index trains on its first trainingLimit present rows in id order; the
+// multi-shard index gathers those rows from the shards in rank order (one
+// process holding every rank) or finds them all on rank 0 (a world over
+// processes), trains there, and installs the codebook on every shard
+// (NewProductQuantizerWithEncoders, :193-203).
+extern "C" int wv_multi_pq_fit(wv_multi* m, uint64_t seed) {
+    if (!m) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(m->mu);
+    for (auto& R : m->r)
+        if (R->idx->compression != WV_COMPRESSION_PQ) return set_err(WV_ERR_INVALID, "pq_fit: index is not PQ-compressed");
     MRank& H = *m->r[0];
-    HIPCHK(hipSetDevice(H.dev));
-    DBuf q, oi, od, on;
-    HIPCHK(q.ensure((size_t)nq * d * 4));
-    HIPCHK(oi.ensure((size_t)nq * k * 8));
-    HIPCHK(od.ensure((size_t)nq * k * 4));
-    HIPCHK(on.ensure((size_t)nq * 4));
-    HIPCHK(hipMemcpyAsync(q.p, queries, (size_t)nq * d * 4, hipMemcpyHostToDevice, H.s));
-    int rc = multi_search(m, q.as<float>(), nq, d, k, oi.as<uint64_t>(), od.as<float>(), on.as<int32_t>(), H.s);
-    if (rc) { hipStreamSynchronize(H.s); return rc; }
-    HIPCHK(hipSetDevice(H.dev));
-    HIPCHK(hipMemcpyAsync(out_ids, oi.p, (size_t)nq * k * 8, hipMemcpyDeviceToHost, H.s));
-    HIPCHK(hipMemcpyAsync(out_dists, od.p, (size_t)nq * k * 4, hipMemcpyDeviceToHost, H.s));
-    HIPCHK(hipMemcpyAsync(out_counts, on.p, (size_t)nq * 4, hipMemcpyDeviceToHost, H.s));
-    HIPCHK(hipStreamSynchronize(H.s));
+    wv_index* hi = H.idx;
+    const int64_t L = hi->pq_training_limit > 0 ? hi->pq_training_limit : INT64_MAX;
+    const int64_t nfl = (int64_t)hi->pq_m * hi->pq_ks * (hi->dims > 0 && hi->pq_m > 0 ? hi->dims / hi->pq_m : 0);
+    int rc = WV_OK;
+    if (m->nl == m->world) {
+        // every rank here: the first L present rows of the shards in rank order
+        std::vector<std::pair<int, std::vector<uint32_t>>> take;
+        int64_t n = 0;
+        for (int i = 0; i < m->nl && n < L; i++) {
+            wv_index* x = m->r[i]->idx;
+            std::lock_guard<std::mutex> gi(x->mu);
+            std::vector<uint32_t> sl;
+            for (int64_t s = 0; s < x->hiwater && n < L; s++)
+                if (x->h_present[s]) { sl.push_back((uint32_t)s); n++; }
+            take.push_back({i, std::move(sl)});
+        }
+        if (hi->dims == 0) return set_err(WV_ERR_INVALID, "pq: dimensions not set yet");
+        for (auto& t : take)
+            if (m->r[t.first]->idx->dims != hi->dims && !t.second.empty())
+                return set_err(WV_ERR_INVALID, "pq_fit: shards differ in dimensions");
+        HIPCHK(hipSetDevice(H.dev));
+        DBuf T;
+        const int64_t ld = hi->dpad;
+        HIPCHK(T.ensure((size_t)std::max<int64_t>(n, 1) * ld * 4));
+        int64_t row = 0;
+        for (auto& t : take) {
+            MRank& R = *m->r[t.first];
+            const std::vector<uint32_t>& sl = t.second;
+            for (size_t a = 0; a < sl.size();) {  // runs of consecutive slots: one copy each
+                size_t b = a + 1;
+                while (b < sl.size() && sl[b] == sl[b - 1] + 1) b++;
+                const size_t bytes = (b - a) * (size_t)ld * 4;
+                const float* src = R.idx->X + (int64_t)sl[a] * ld;
+                if (R.dev == H.dev) HIPCHK(hipMemcpyAsync(T.as<float>() + row * ld, src, bytes, hipMemcpyDeviceToDevice, H.s));
+                else HIPCHK(hipMemcpyPeerAsync(T.as<float>() + row * ld, H.dev, src, R.dev, bytes, H.s));
+                row += (int64_t)(b - a);
+                a = b;
+            }
+        }
+        HIPCHK(hipStreamSynchronize(H.s));
+        std::lock_guard<std::mutex> gh(hi->mu);
+        rc = pq_fit_rows(hi, T.as<float>(), n, seed);
+        hipStreamSynchronize(hi->stream);
+        if (rc) return rc;
+    } else {
+        // a world over processes: the training rows must all lie on rank 0,
+        // which trains (every rank learns whether it could, so none waits alone)
+        std::vector<int64_t> st(1, 1);
+        std::string err;
+        if (H.rank == 0) {
+            {
+                std::lock_guard<std::mutex> gh(hi->mu);
+                if (hi->pq_training_limit <= 0 || hi->npresent < hi->pq_training_limit) st[0] = 0;
+            }
+            if (st[0] && wv_index_pq_fit(hi, seed) != WV_OK) {
+                err = wv_last_error();
+                st[0] = 0;
+            }
+        }
+        int64_t all_ok = 0;
+        rc = agree_min(m, st, &all_ok);
+        if (rc) return rc;
+        if (!all_ok)
+            return H.rank == 0 && !err.empty()
+                       ? set_err(WV_ERR_UNSUPPORTED, "pq_fit on rank 0: %s", err.c_str())
+                       : set_err(WV_ERR_UNSUPPORTED, "pq_fit: rank 0 could not train on the first trainingLimit rows "
+                                                     "(they span the processes' shards: fit one index and install "
+                                                     "its codebook with wv_multi_pq_set_centers)");
+    }
+    // the codebook from rank 0 to every shard
+    std::vector<float> hc((size_t)nfl);
+    for (auto& Rp : m->r) {
+        MRank& R = *Rp;
+        HIPCHK(hipSetDevice(R.dev));
+        HIPCHK(R.bm.ensure((size_t)nfl * 4));
+        if (R.rank == 0) {
+            rc = wv_index_pq_centers(R.idx, hc.data(), nfl);
+            if (rc) return rc;
+            HIPCHK(hipMemcpy(R.bm.p, hc.data(), (size_t)nfl * 4, hipMemcpyHostToDevice));
+        }
+    }
+    std::vector<void*> bufs;
+    for (auto& Rp : m->r) bufs.push_back(Rp->bm.p);
+    rc = bcast(m, bufs, {(size_t)nfl * 4}, 0);
+    if (rc) return rc;
+    for (auto& Rp : m->r) {
+        MRank& R = *Rp;
+        if (R.rank == 0) continue;
+        HIPCHK(hipSetDevice(R.dev));
+        HIPCHK(hipStreamSynchronize(R.s));
+        HIPCHK(hipMemcpy(hc.data(), R.bm.p, (size_t)nfl * 4, hipMemcpyDeviceToHost));
+        rc = wv_index_pq_set_centers(R.idx, hc.data(), nfl);
+        if (rc) return rc;
+    }
+    return WV_OK;
+}
+
+// NewProductQuantizerWithEncoders on every shard (a codebook trained elsewhere)
+extern "C" int wv_multi_pq_set_centers(wv_multi* m, const float* centers, int64_t n_floats) {
+    if (!m || !centers) return set_err(WV_ERR_INVALID, "nil argument");
+    std::lock_guard<std::mutex> g(m->mu);
+    for (auto& R : m->r) {
+        int rc = wv_index_pq_set_centers(R->idx, centers, n_floats);
+        if (rc) return rc;
+    }
     return WV_OK;
 }
 

@@ -533,48 +533,25 @@ static int pq_encode_all(wv_index* idx) {
     return WV_OK;
 }
 
-extern "C" int wv_index_pq_fit(wv_index* idx, uint64_t seed) {
-    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
-    std::lock_guard<std::mutex> g(idx->mu);
-    HIPCHK(hipSetDevice(idx->device));
-    if (idx->compression != WV_COMPRESSION_PQ) return set_err(WV_ERR_INVALID, "pq_fit: index is not PQ-compressed");
+// k-means of every segment over the n training rows T [n][dpad] (device, on
+// idx's device), then Encode of every stored row.  Caller holds idx->mu.
+int pq_fit_rows(wv_index* idx, const float* dT, int64_t n, uint64_t seed) {
     int rc = pq_validate(idx);
     if (rc) return rc;
     const int m = idx->pq_m, K = idx->pq_ks, ds = idx->pq_ds;
     hipStream_t s = idx->stream;
-    // training data: ProductQuantizer.Fit truncates to trainingLimit (:379-381)
-    std::vector<uint32_t> tslots;
-    for (int64_t sl = 0; sl < idx->hiwater; sl++)
-        if (idx->h_present[sl]) tslots.push_back((uint32_t)sl);
-    int64_t n = (int64_t)tslots.size();
-    if (idx->pq_training_limit > 0 && n > idx->pq_training_limit) n = idx->pq_training_limit;
     if (n < K) return set_err(WV_ERR_INVALID, "not enough data to fit k-means");  // kmeans.go:459-461
     rc = pq_alloc(idx);
     if (rc) return rc;
-    // T = the n training rows (gathered, dpad stride)
-    DBuf T, sub, asg, nbi, nbd, chg, act;
+    DBuf sub, asg, nbi, nbd, chg, act;
     const int64_t ldt = idx->dpad;
-    HIPCHK(T.ensure((size_t)n * ldt * sizeof(float)));
-    {
-        // contiguous copy when the first n present slots are 0..n-1, else a gather
-        bool contiguous = true;
-        for (int64_t i = 0; i < n; i++)
-            if (tslots[i] != (uint32_t)i) { contiguous = false; break; }
-        if (contiguous) {
-            HIPCHK(hipMemcpyAsync(T.p, idx->X, (size_t)n * ldt * sizeof(float), hipMemcpyDeviceToDevice, s));
-        } else {
-            for (int64_t i = 0; i < n; i++)
-                HIPCHK(hipMemcpyAsync(T.as<float>() + i * ldt, idx->X + (int64_t)tslots[i] * ldt, ldt * sizeof(float),
-                                      hipMemcpyDeviceToDevice, s));
-        }
-    }
     float* C = idx->pq_centers;
     const size_t lds_c = (size_t)K * ds * sizeof(float);
     if (K == 1) {  // computeCentroid (kmeans.go:447-452): every row in cluster 0
         HIPCHK(asg.ensure((size_t)m * n * sizeof(uint32_t)));
         HIPCHK(hipMemsetAsync(asg.p, 0, (size_t)m * n * sizeof(uint32_t), s));
         const size_t lds_u = (size_t)K * ds * sizeof(double) + KM_T * sizeof(uint32_t) + (size_t)KM_T * ds * sizeof(float);
-        k_km_update_centers<<<m, KM_T, lds_u, s>>>(T.as<float>(), ldt, n, K, ds, asg.as<uint32_t>(), nullptr, C);
+        k_km_update_centers<<<m, KM_T, lds_u, s>>>(dT, ldt, n, K, ds, asg.as<uint32_t>(), nullptr, C);
         HIPCHK(hipGetLastError());
         return pq_encode_all(idx);
     }
@@ -589,7 +566,7 @@ extern "C" int wv_index_pq_fit(wv_index* idx, uint64_t seed) {
     HIPCHK(hipMemcpyAsync(sub.p, hsub.data(), hsub.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
     {
         const int64_t tot = (int64_t)m * K * ds;
-        k_km_gather_centers<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(T.as<float>(), ldt, sub.as<int64_t>(), m, K, ds,
+        k_km_gather_centers<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(dT, ldt, sub.as<int64_t>(), m, K, ds,
                                                                           C);
     }
     HIPCHK(asg.ensure((size_t)m * n * sizeof(uint32_t)));
@@ -612,8 +589,8 @@ extern "C" int wv_index_pq_fit(wv_index* idx, uint64_t seed) {
     const size_t lds_u = (size_t)K * ds * sizeof(double) + KM_T * sizeof(uint32_t) + (size_t)KM_T * ds * sizeof(float);
     if (lds_u > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void*)k_km_update_centers, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_u));
-    k_km_assign_brute<<<rgrid, 256, lds_c, s>>>(T.as<float>(), ldt, n, K, ds, C, idx->variant, nullptr, asg.as<uint32_t>());
-    k_km_update_centers<<<m, KM_T, lds_u, s>>>(T.as<float>(), ldt, n, K, ds, asg.as<uint32_t>(), nullptr, C);
+    k_km_assign_brute<<<rgrid, 256, lds_c, s>>>(dT, ldt, n, K, ds, C, idx->variant, nullptr, asg.as<uint32_t>());
+    k_km_update_centers<<<m, KM_T, lds_u, s>>>(dT, ldt, n, K, ds, asg.as<uint32_t>(), nullptr, C);
     HIPCHK(hipGetLastError());
     int iterations = 1;  // initializeRandom counts as the first iteration (Metrics.update)
     std::vector<unsigned long long> hchg((size_t)m);
@@ -624,10 +601,10 @@ extern "C" int wv_index_pq_fit(wv_index* idx, uint64_t seed) {
         k_km_neighbors<<<dim3((unsigned)K, (unsigned)m), KM_T, 0, s>>>(C, K, ds, idx->variant, act.as<int32_t>(),
                                                                        nbi.as<uint32_t>(), nbd.as<float>());
         HIPCHK(hipMemsetAsync(chg.p, 0, (size_t)m * sizeof(unsigned long long), s));
-        k_km_assign_prune<<<rgrid, 256, lds_c, s>>>(T.as<float>(), ldt, n, K, ds, C, idx->variant, nbi.as<uint32_t>(),
+        k_km_assign_prune<<<rgrid, 256, lds_c, s>>>(dT, ldt, n, K, ds, C, idx->variant, nbi.as<uint32_t>(),
                                                     nbd.as<float>(), act.as<int32_t>(), asg.as<uint32_t>(),
                                                     chg.as<unsigned long long>());
-        k_km_update_centers<<<m, KM_T, lds_u, s>>>(T.as<float>(), ldt, n, K, ds, asg.as<uint32_t>(), act.as<int32_t>(),
+        k_km_update_centers<<<m, KM_T, lds_u, s>>>(dT, ldt, n, K, ds, asg.as<uint32_t>(), act.as<int32_t>(),
                                                    C);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(hchg.data(), chg.p, (size_t)m * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -641,8 +618,51 @@ extern "C" int wv_index_pq_fit(wv_index* idx, uint64_t seed) {
         HIPCHK(hipMemcpyAsync(act.p, active.data(), (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipStreamSynchronize(s));
-    T.release(); sub.release(); asg.release(); nbi.release(); nbd.release(); chg.release(); act.release();
+    sub.release(); asg.release(); nbi.release(); nbd.release(); chg.release(); act.release();
     return pq_encode_all(idx);
+}
+
+extern "C" int wv_index_pq_fit(wv_index* idx, uint64_t seed) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    std::lock_guard<std::mutex> g(idx->mu);
+    HIPCHK(hipSetDevice(idx->device));
+    if (idx->compression != WV_COMPRESSION_PQ) return set_err(WV_ERR_INVALID, "pq_fit: index is not PQ-compressed");
+    int rc = pq_validate(idx);
+    if (rc) return rc;
+    hipStream_t s = idx->stream;
+    // training data: ProductQuantizer.Fit truncates to trainingLimit (:379-381)
+    std::vector<uint32_t> tslots;
+    for (int64_t sl = 0; sl < idx->hiwater; sl++)
+        if (idx->h_present[sl]) tslots.push_back((uint32_t)sl);
+    int64_t n = (int64_t)tslots.size();
+    if (idx->pq_training_limit > 0 && n > idx->pq_training_limit) n = idx->pq_training_limit;
+    if (n < idx->pq_ks) return set_err(WV_ERR_INVALID, "not enough data to fit k-means");  // kmeans.go:459-461
+    // T = the n training rows (gathered, dpad stride)
+    DBuf T;
+    const int64_t ldt = idx->dpad;
+    HIPCHK(T.ensure((size_t)n * ldt * sizeof(float)));
+    {
+        // contiguous copy when the first n present slots are 0..n-1, else a gather
+        bool contiguous = true;
+        for (int64_t i = 0; i < n; i++)
+            if (tslots[i] != (uint32_t)i) { contiguous = false; break; }
+        if (contiguous) {
+            HIPCHK(hipMemcpyAsync(T.p, idx->X, (size_t)n * ldt * sizeof(float), hipMemcpyDeviceToDevice, s));
+        } else {
+            for (int64_t i = 0; i < n; i++)
+                HIPCHK(hipMemcpyAsync(T.as<float>() + i * ldt, idx->X + (int64_t)tslots[i] * ldt, ldt * sizeof(float),
+                                      hipMemcpyDeviceToDevice, s));
+        }
+    }
+    rc = pq_fit_rows(idx, T.as<float>(), n, seed);
+    HIPCHK(hipStreamSynchronize(s));
+    return rc;
+}
+
+// the largest batch wv_index_bq_begin takes on this shard (one block-minima group)
+int64_t bq_max_batch(const wv_index* idx) {
+    constexpr int QPB = 16;
+    return std::max<int64_t>(QPB, ((4ll << 30) / (bq_nblk(idx) * 4)) / QPB * QPB);
 }
 
 extern "C" int wv_index_pq_set_centers(wv_index* idx, const float* centers, int64_t n_floats) {

@@ -333,6 +333,8 @@ int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float*
                int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on, int by_query = 0,
                uint64_t* rec_i = nullptr, float* rec_d = nullptr, int32_t* rec_n = nullptr, int rec_cap = 0);
 void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots);
+int shard_filter_bitmap(wv_index* idx, hipStream_t s, const uint64_t* allow, int64_t n_allow, const uint32_t** valid,
+                        int64_t* n_valid);
 void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t ld, int64_t n, const uint32_t* d_slots,
                       int query, void* codes, int64_t cap, float4* meta, uint32_t* csum = nullptr,
                       unsigned char* pm = nullptr);
@@ -372,6 +374,8 @@ int search_pq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
               uint64_t* o_ids, float* o_d, int32_t* o_n);
 int search_hnsw_flat(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int64_t qd, int k,
                      const uint32_t* valid, uint64_t* o_ids, float* o_d, int32_t* o_n);
+int pq_fit_rows(wv_index* idx, const float* dT, int64_t n, uint64_t seed);
+int64_t bq_max_batch(const wv_index* idx);
 int rq_init(wv_index* idx);
 int rq_encode_queries(wv_index* idx, hipStream_t s, int64_t nq);
 int rq_dist(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t q0, int F, int64_t ld, float* E, float* bmin,

@@ -1244,6 +1244,33 @@ static int build_valid(wv_index* idx, hipStream_t s, const uint64_t* allow, int6
     return WV_OK;
 }
 
+// The allow-list bitmap of one shard of a filtered multi-shard search
+// (multi.hip): present & allow over the whole allocation (every word a kernel
+// may read, zero where no allowed row is), in idx->valid; *n_valid = its
+// population (one host sync).  The ids of other shards are skipped by range.
+int shard_filter_bitmap(wv_index* idx, hipStream_t s, const uint64_t* allow, int64_t n_allow, const uint32_t** valid,
+                        int64_t* n_valid) {
+    const int64_t words = std::max<int64_t>(idx->cap / 32, 1);
+    HIPCHK(idx->valid.ensure((size_t)words * sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(idx->valid.p, 0, (size_t)words * sizeof(uint32_t), s));
+    *valid = idx->valid.as<uint32_t>();
+    *n_valid = 0;
+    if (n_allow <= 0 || idx->hiwater == 0) return WV_OK;
+    HIPCHK(idx->allowIds.ensure((size_t)n_allow * sizeof(uint64_t) + 8));
+    HIPCHK(idx->allowCnt.ensure(sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(idx->allowIds.p, allow, (size_t)n_allow * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(idx->allowCnt.p, 0, sizeof(uint32_t), s));
+    k_allow_bits<<<(unsigned)((n_allow + 255) / 256), 256, 0, s>>>(idx->allowIds.as<uint64_t>(), n_allow, idx->id_base,
+                                                                    idx->hiwater, idx->present,
+                                                                    idx->valid.as<uint32_t>(), idx->allowCnt.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    uint32_t nv = 0;
+    HIPCHK(hipMemcpyAsync(&nv, idx->allowCnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *n_valid = nv;
+    return WV_OK;
+}
+
 // A search over the slot span [lo, hi) of the store only: the stored-row
 // arrays are offset to lo (a multiple of 256: whole tiles of the tiled planes)
 // and the index reads as one of hi - lo slots with id_base + lo, so every

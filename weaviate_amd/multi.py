@@ -19,7 +19,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check
-from .flat import FlatIndex, make_config
+from .flat import AllowList, FlatIndex, _allow_args, _fptr, _iptr, _uptr, make_config
 
 TRANSPORTS = {"local": 0, "rccl": 1, "host": 2}
 STAGES = ("phase1", "phase2", "merge", "replay", "merge_records", "chain", "collectives")
@@ -76,8 +76,11 @@ class _ShardView(FlatIndex):
         self._root = cfg_args.get("root_path", b"")
         self._cfg_args = dict(cfg_args, device=device, id_base=id_base)
         self.metric = owner.metric
-        self.bq = self.pq = self.rq = self.sq = False
-        self.rescore_limit = -1
+        self.bq = bool(cfg_args.get("bq"))
+        self.pq = cfg_args.get("pq") is not None
+        self.rq = cfg_args.get("rq") is not None
+        self.sq = bool(cfg_args.get("sq"))
+        self.rescore_limit = int(cfg_args.get("rescore_limit", -1))
         self.device = device
         self.id_base = id_base
 
@@ -92,9 +95,11 @@ class MultiFlatIndex:
 
     def __init__(self, distance: str = "cosine", dims: int = 0, devices: Sequence[int] = (0,), world: int = 0,
                  rank0: int = 0, id_stride: int = 0, transport: str = "local", unique_id: Optional[bytes] = None,
-                 variant: str = "auto", host_callbacks=None):
+                 variant: str = "auto", host_callbacks=None, bq: bool = False, rescore_limit: int = -1,
+                 pq: Optional[dict] = None, rq: Optional[dict] = None, sq: bool = False):
         """transport "host": host_callbacks = (allgather, broadcast) ctypes
-        callbacks (torch_host_callbacks(world) by default)."""
+        callbacks (torch_host_callbacks(world) by default).  bq / rescore_limit
+        / pq / rq / sq: every shard's compression, as FlatIndex takes them."""
         self._l = _lib.load()
         devs = [int(x) for x in devices]
         world = int(world) or len(devs)
@@ -103,7 +108,8 @@ class MultiFlatIndex:
         self._cbs = None
         if transport == "host":
             self._cbs = host_callbacks or torch_host_callbacks(world)
-        cfg_args = dict(distance=distance, dims=dims, variant=variant)
+        cfg_args = dict(distance=distance, dims=dims, variant=variant, bq=bq, rescore_limit=rescore_limit, pq=pq, rq=rq,
+                        sq=sq)
         self._cfg = _lib.WvMultiConfig(make_config(**cfg_args), world, int(rank0), len(devs),
                                        C.cast(self._devs, C.POINTER(C.c_int32)), int(id_stride),
                                        TRANSPORTS[transport], C.cast(self._uid, C.c_void_p) if self._uid else None,
@@ -149,9 +155,9 @@ class MultiFlatIndex:
         check(self._l.wv_multi_add_batch(self._h, ids.ctypes.data_as(C.POINTER(C.c_uint64)),
                                          v.ctypes.data_as(C.POINTER(C.c_float)), ids.size, v.shape[1]))
 
-    def search_by_vector_batch(self, queries: np.ndarray, k: int):
-        """SearchByVector over every rank -> (ids [nq, k] uint64, dists [nq, k]
-        float32, counts [nq])."""
+    def search_by_vector_batch(self, queries: np.ndarray, k: int, allow: Optional[AllowList] = None):
+        """SearchByVector over every rank (under `allow`, each shard its part of
+        the list) -> (ids [nq, k] uint64, dists [nq, k] float32, counts [nq])."""
         q = np.ascontiguousarray(queries, dtype=np.float32)
         if q.ndim == 1:
             q = q[None, :]
@@ -159,16 +165,64 @@ class MultiFlatIndex:
         ids = np.zeros((nq, k), dtype=np.uint64)
         dd = np.zeros((nq, k), dtype=np.float32)
         cnt = np.zeros(nq, dtype=np.int32)
-        check(self._l.wv_multi_search_by_vector_batch(self._h, q.ctypes.data_as(C.POINTER(C.c_float)), nq, d, int(k),
-                                                      ids.ctypes.data_as(C.POINTER(C.c_uint64)),
-                                                      dd.ctypes.data_as(C.POINTER(C.c_float)),
-                                                      cnt.ctypes.data_as(C.POINTER(C.c_int32))))
+        ap, na, mode, _keep = _allow_args(allow)
+        check(self._l.wv_multi_search_by_vector_batch_allow(self._h, _fptr(q), nq, d, int(k), ap, na, mode, _uptr(ids),
+                                                            _fptr(dd), _iptr(cnt)))
         return ids, dd, cnt
 
+    def search_by_vector_batch_multi_allow(self, queries: np.ndarray, k: int, allows):
+        """Row i under its own allow list allows[i] (None = unfiltered)."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq, d = q.shape
+        allows = list(allows)
+        if len(allows) != nq:
+            raise _lib.WeaviateError(_lib.WV_ERR_INVALID, f"{len(allows)} allow lists for {nq} queries")
+        ids = np.zeros((nq, k), dtype=np.uint64)
+        dd = np.zeros((nq, k), dtype=np.float32)
+        cnt = np.zeros(nq, dtype=np.int32)
+        modes = np.array([0 if a is None else 1 for a in allows], dtype=np.int32)
+        parts = [np.asarray(a.ids, dtype=np.uint64) for a in allows if a is not None]
+        aids = np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros(1, np.uint64), dtype=np.uint64)
+        off = np.zeros(nq + 1, dtype=np.int64)
+        off[1:] = np.cumsum([0 if a is None else a.ids.size for a in allows])
+        check(self._l.wv_multi_search_by_vector_batch_multi_allow(
+            self._h, _fptr(q), nq, d, int(k), _uptr(aids), off.ctypes.data_as(C.c_void_p), _iptr(modes), _uptr(ids),
+            _fptr(dd), _iptr(cnt)))
+        return ids, dd, cnt
+
+    def search_by_vector_distance(self, vector, target_distance: float, max_limit: int,
+                                  allow: Optional[AllowList] = None):
+        """SearchByVectorDistance over every rank (flat/index.go:699-761)."""
+        v = np.ascontiguousarray(vector, dtype=np.float32).ravel()
+        ids = np.zeros(100, dtype=np.uint64)
+        dists = np.zeros(100, dtype=np.float32)
+        n = np.zeros(1, dtype=np.int32)
+        ap, na, mode, _keep = _allow_args(allow)
+        check(self._l.wv_multi_search_by_vector_distance(self._h, _fptr(v), v.size, float(target_distance),
+                                                         int(max_limit), ap, na, mode, _uptr(ids), _fptr(dists),
+                                                         _iptr(n)))
+        return ids[: n[0]].copy(), dists[: n[0]].copy()
+
+    def pq_fit(self, seed: int = 0) -> None:
+        """ProductQuantizer.Fit over the shards' first trainingLimit rows in id
+        order; the codebook installed on every shard."""
+        check(self._l.wv_multi_pq_fit(self._h, int(seed)))
+
+    def pq_set_centers(self, centers: np.ndarray) -> None:
+        c = np.ascontiguousarray(centers, dtype=np.float32).ravel()
+        check(self._l.wv_multi_pq_set_centers(self._h, _fptr(c), c.size))
+
     def search_device(self, q_ptr: int, nq: int, d: int, k: int, ids_ptr: int, dists_ptr: int, counts_ptr: int,
-                      stream: Optional[int] = None) -> None:
+                      stream: Optional[int] = None, allow: Optional[AllowList] = None) -> None:
         """Device buffers on local shard 0's GPU, ordered on `stream`."""
-        check(self._l.wv_multi_search_device(self._h, q_ptr, nq, d, int(k), ids_ptr, dists_ptr, counts_ptr, stream))
+        if allow is None:
+            check(self._l.wv_multi_search_device(self._h, q_ptr, nq, d, int(k), ids_ptr, dists_ptr, counts_ptr, stream))
+            return
+        ap, na, mode, _keep = _allow_args(allow)
+        check(self._l.wv_multi_search_device_allow(self._h, q_ptr, nq, d, int(k), ap, na, mode, ids_ptr, dists_ptr,
+                                                   counts_ptr, stream))
 
     def stats(self) -> dict:
         out = (C.c_int64 * 10)()
