@@ -8,7 +8,7 @@ corpus on one GPU).  One step = one batch of B = 8192 queries through the
 full SearchByVector pipeline (query normalisation, bf16 block-key MFMA pass,
 candidate-block selection, exact-order distances of the candidate rows,
 exactness proof, bounded heap replay of any flagged query; for N>1 the
-two-phase sharded search of weaviate_amd/sharded.py: RCCL all-gathers of the
+two-phase sharded search of the multi-shard index (multi.hip): RCCL all-gathers of the
 block-key bounds and of the packed lists, the on-device merge and the
 parallel cross-shard replay).  Inputs are synthetic (counter-based generator,
 identical on CPU and GPU) and resident in HBM before timing starts.
@@ -386,7 +386,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None)
-    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--rows", "--n", dest="n", type=int, default=None,
+                    help="corpus rows (--rows under torch.distributed.run: its parser claims --n as a prefix)")
     ap.add_argument("--dims", type=int, default=None,
                     help="exact flat workloads: override the row width (e.g. 1024 / 1536, the block-key w4 kernel)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -395,8 +396,8 @@ def main():
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the self-check of sampled result rows against the oracle (outside the timed region)")
     ap.add_argument("--sharded", action="store_true",
-                    help="run the multi-GPU protocol (ShardedFlatSearch / ShardedBQSearch over RCCL) even at "
-                         "WORLD_SIZE 1 (launch under torch.distributed.run): a one-GPU check of the N>1 path")
+                    help="run the multi-GPU path (the multi-shard index over RCCL, multi.hip) even at WORLD_SIZE 1 "
+                         "(launch under torch.distributed.run): a one-GPU check of the N>1 path")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-queries", type=int, default=None)
     ap.add_argument("--cpu-threads", type=int, default=None, help="default: nproc (all CPUs this process may use)")
@@ -456,24 +457,19 @@ def main():
     # ---- build the shard: generate + add in 1M-row chunks (device resident) ----
     t_build = time.perf_counter()
     multi = None
-    if shard and flat is not None:
-        # the exact search over N GPUs: the library's multi-shard index (multi.hip)
-        # drives the protocol and owns an RCCL communicator; rank 0's unique id
-        # reaches every process over the launcher's process group
-        from weaviate_amd.multi import MultiFlatIndex, rccl_unique_id
-        uid = [rccl_unique_id() if rank == 0 else None]
-        if world > 1:
-            dist.broadcast_object_list(uid, src=0)
-        multi = MultiFlatIndex(distance=metric_name, dims=dims, devices=[local_rank], world=world, rank0=rank,
-                               id_stride=(n_total + world - 1) // world, transport="rccl", unique_id=uid[0],
-                               variant="avx256")
+    comp = dict(bq=bq, rescore_limit=BQ_RESCORE if (bq or rq_bits) else -1, rq={"bits": rq_bits} if rq_bits else None,
+                pq={"segments": PQ_SEGMENTS, "centroids": PQ_CENTROIDS, "trainingLimit": PQ_TRAIN,
+                    "rescore": False} if pq else None)
+    if shard:
+        # the search over N GPUs: the library's multi-shard index (multi.hip)
+        # drives the protocol of the workload's kind (exact two-phase block keys,
+        # BQ R-heap, PQ / rq worker heap) and owns an RCCL communicator; rank 0's
+        # unique id reaches every process over the launcher's process group
+        from weaviate_amd.sharded import open_multi
+        multi = open_multi(n_total, local_rank, distance=metric_name, dims=dims, variant="avx256", **comp)
         index = multi.shards[0]
     else:
-        index = wv.FlatIndex(distance=metric_name, dims=dims, device=local_rank, variant="avx256", id_base=id0,
-                             bq=bq, rescore_limit=BQ_RESCORE if (bq or rq_bits) else -1,
-                             rq={"bits": rq_bits} if rq_bits else None,
-                             pq={"segments": PQ_SEGMENTS, "centroids": PQ_CENTROIDS, "trainingLimit": PQ_TRAIN,
-                                 "rescore": False} if pq else None)
+        index = wv.FlatIndex(distance=metric_name, dims=dims, device=local_rank, variant="avx256", id_base=id0, **comp)
     for kv in args.option:
         key, val = kv.split("=", 1)
         index.set_option(key, int(val))
@@ -496,14 +492,10 @@ def main():
         if shard and n_local < PQ_TRAIN:
             # the single index trains on the first trainingLimit rows of the whole corpus: rank 0 must hold them
             raise SystemExit(f"sharded PQ needs >= {PQ_TRAIN} rows on rank 0 (has {n_local})")
-        if not shard or rank == 0:
-            index.pq_fit(seed=SEED_CORPUS)  # rank 0 holds ids [0, n_local): the first trainingLimit rows
-        if shard:  # one codebook for every shard (NewProductQuantizerWithEncoders on the others)
-            cen = torch.from_numpy(index.pq_centers()).to(dev) if rank == 0 else \
-                torch.empty((PQ_SEGMENTS, PQ_CENTROIDS, PQ_DIMS // PQ_SEGMENTS), dtype=torch.float32, device=dev)
-            dist.broadcast(cen, src=0)
-            if rank != 0:
-                index.pq_set_centers(cen.cpu().numpy())
+        if shard:  # rank 0 holds ids [0, n_local): it trains, the codebook goes to every shard over RCCL
+            multi.pq_fit(seed=SEED_CORPUS)
+        else:
+            index.pq_fit(seed=SEED_CORPUS)
         torch.cuda.synchronize()
         fit_s = time.perf_counter() - t_fit
         log(f"[rank {rank}] pq fit ({PQ_SEGMENTS} x k-means k={PQ_CENTROIDS} on {PQ_TRAIN} rows) + encode "
@@ -514,19 +506,7 @@ def main():
     out_d = torch.empty((B, K_), dtype=torch.float32, device=dev)
     out_n = torch.empty(B, dtype=torch.int32, device=dev)
 
-    if shard and (pq or rq_bits):
-        from weaviate_amd.sharded import GpuQuantShardBackend, ShardedQuantSearch
-        searcher = ShardedQuantSearch(GpuQuantShardBackend(index, local_rank), dev, (n_total + world - 1) // world)
-
-        def step():
-            return searcher.search(queries, K_)
-    elif shard and bq:
-        from weaviate_amd.sharded import GpuBQShardBackend, ShardedBQSearch
-        searcher = ShardedBQSearch(GpuBQShardBackend(index, local_rank), dev, (n_total + world - 1) // world)
-
-        def step():
-            return searcher.search(queries, K_)
-    elif shard:
+    if shard:
         def step():
             s = torch.cuda.current_stream(dev).cuda_stream
             multi.search_device(queries.data_ptr(), B, dims, K_, out_ids.data_ptr(), out_d.data_ptr(),
@@ -565,7 +545,7 @@ def main():
     if multi is not None:
         replays = multi.stats()["flagged"] - flagged0  # the cross-shard replay's queries (every rank's view)
     sharded_check = None
-    if args.sharded and world == 1 and (flat or pq or rq_bits):
+    if args.sharded and world == 1:
         # the sharded protocol at one rank must equal the single-index search
         si, sd, sn = (t.clone() for t in step()[:3])
         s = torch.cuda.current_stream(dev).cuda_stream
@@ -597,7 +577,7 @@ def main():
     total_avg = float(np.mean(tot_ms)) if tot_ms else 0.0
     # the dominant kernel of each workload: its PMC record (matched on kernel
     # name and configuration) is the only source of `traffic`
-    # the sharded PQ search (ShardedQuantSearch) computes full ADC rows with k_pq_adc2
+    # the sharded PQ search (the multi-shard worker heap, wv_index_quant_*) computes full ADC rows with k_pq_adc2
     pq_opt = [o.replace(" ", "") for o in args.option if o.replace(" ", "").startswith("pq_adc3=")]
     pq_sel = pq_opt[-1].split("=")[1] if pq_opt else PQ_ADC_DEFAULT
     pq_kernel = ("k_q8_blockkey_pq" if route == 8 else

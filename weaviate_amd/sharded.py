@@ -20,15 +20,39 @@ the rank scans in rank order.  Exactness:
    broadcast per hop, states indexed by query, the flagged list built on the
    device: no host synchronisation), the last rank applies extractHeap.
 
-The collective layer is torch.distributed (backend "nccl" = RCCL on ROCm,
-"gloo" on CPU for tests); the per-rank kernels sit behind a small backend
-interface so the protocol can be exercised on CPU.
+The GPU product path is the library's multi-shard index (multi.hip, the
+wv_multi_* C ABI): it runs these protocols -- exact two-phase, BQ R-heap,
+PQ / SQ / rq worker heap, allow lists -- in C++ with its own RCCL
+communicator, so a cgo host reaches them without Python.  open_multi() below
+is the thin torch.distributed client of it (one process per GPU, rank 0's
+RCCL id broadcast over the launcher's group).  The protocol classes that
+follow (ShardedFlatSearch, ShardedBQSearch, ShardedQuantSearch) are the same
+protocols over torch.distributed with the per-rank kernels behind a small
+backend interface, kept as the CPU-testable statement of the protocols
+(gloo, oracle-backed backends: tests/test_sharded*_gloo.py).
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 from torch.distributed import ReduceOp
+
+
+def open_multi(n_total: int, local_rank: int, **index_kw):
+    """The corpus of n_total doc ids over the ranks of the default process
+    group (contiguous id ranges of ceil(n_total / world)), this process's rank
+    as one shard of a wv_multi index on GPU `local_rank` with a library-owned
+    RCCL communicator (weaviate_amd.multi.MultiFlatIndex).  index_kw: the
+    shards' FlatIndex configuration (distance, dims, bq, rescore_limit, pq, rq,
+    sq, variant)."""
+    from .multi import MultiFlatIndex, rccl_unique_id
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    uid = [rccl_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    return MultiFlatIndex(devices=[local_rank], world=world, rank0=rank, id_stride=(n_total + world - 1) // world,
+                          transport="rccl", unique_id=uid[0], **index_kw)
 
 
 def prefix_bound(r: int, ql: torch.Tensor, k: int, gd, gc, gf, bounds=None) -> torch.Tensor:
