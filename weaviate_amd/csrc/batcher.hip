@@ -8,10 +8,10 @@
 // concurrent callers are coalesced: leader/follower, no background thread.
 // A caller enqueues its request; if no batch is running it becomes the
 // leader, optionally waits batch_window_us for company, takes every pending
-// request, groups them by (d, k), runs each group through
-// wv_index_search_by_vector_batch (no request with an allow list) or
+// request, groups them by (d, k), runs each group's unfiltered requests
+// through wv_index_search_by_vector_batch and its filtered ones through
 // wv_index_search_by_vector_batch_multi_allow (each query its own list, one
-// block-key launch for the group) and hands every follower its rows.  Requests
+// block-key launch) and hands every follower its rows.  Requests
 // that arrive while a batch runs form the next batch.  Results are identical
 // to individual calls: each query of a batch is searched independently.
 #include <chrono>
@@ -63,8 +63,11 @@ static wv_batcher* get_batcher(wv_index* idx) {
     return idx->batcher;
 }
 
-// Runs one group of requests sharing (d, k) as one batch call.
-static void run_group(wv_index* idx, wv_batcher* b, std::vector<wv_batch_req*>& grp) {
+// One launch for requests sharing (d, k): no list among them ->
+// wv_index_search_by_vector_batch; lists -> wv_index_search_by_vector_batch_multi_allow
+// (each query its own list).  On success every request gets its rows; on
+// failure nothing is written and the error is returned.
+static int launch_requests(wv_index* idx, wv_batcher* b, const std::vector<wv_batch_req*>& grp) {
     const int64_t n = (int64_t)grp.size();
     const int64_t d = grp[0]->d;
     const int32_t k = grp[0]->k;
@@ -85,7 +88,7 @@ static void run_group(wv_index* idx, wv_batcher* b, std::vector<wv_batch_req*>& 
         std::vector<int32_t> modes((size_t)n);
         for (int64_t i = 0; i < n; i++) {
             modes[(size_t)i] = grp[i]->allow_mode;
-            off[(size_t)i + 1] = off[(size_t)i] + (grp[i]->allow_mode != 0 ? std::max<int64_t>(grp[i]->n_allow, 0) : 0);
+            off[(size_t)i + 1] = off[(size_t)i] + (grp[i]->allow_mode != 0 ? grp[i]->n_allow : 0);
         }
         const size_t need = (size_t)off[(size_t)n] + 1;
         if (need > b->pin_cap) {
@@ -104,14 +107,41 @@ static void run_group(wv_index* idx, wv_batcher* b, std::vector<wv_batch_req*>& 
                                                              ids.data(), dists.data(), cnt.data());
         }
     }
-    std::string err = rc ? std::string(wv_last_error()) : std::string();
+    if (rc) return rc;
     for (int64_t i = 0; i < n; i++) {
         wv_batch_req* r = grp[i];
-        r->rc = rc;
-        if (rc) { r->err = err; continue; }
+        r->rc = WV_OK;
         *r->out_count = cnt[i];
         memcpy(r->out_ids, &ids[(size_t)(i * kk)], (size_t)cnt[i] * sizeof(uint64_t));
         memcpy(r->out_dists, &dists[(size_t)(i * kk)], (size_t)cnt[i] * sizeof(float));
+    }
+    return WV_OK;
+}
+
+// Runs one group of requests sharing (d, k): the requests without an allow
+// list in one plain launch (they never pay for the per-query bitmaps of the
+// filtered form), the filtered ones in one multi-allow launch.  A launch that
+// fails is retried request by request, so every caller gets exactly the
+// result or error of its own one-query call.
+static void run_group(wv_index* idx, wv_batcher* b, std::vector<wv_batch_req*>& grp) {
+    std::vector<wv_batch_req*> part[2];
+    for (wv_batch_req* r : grp) part[r->allow_mode != 0 ? 1 : 0].push_back(r);
+    for (auto& sub : part) {
+        if (sub.empty()) continue;
+        int rc = launch_requests(idx, b, sub);
+        if (rc == WV_OK) continue;
+        if (sub.size() == 1) {
+            sub[0]->rc = rc;
+            sub[0]->err = wv_last_error();
+            continue;
+        }
+        for (wv_batch_req* r : sub) {
+            const int rc1 = launch_requests(idx, b, {r});
+            if (rc1) {
+                r->rc = rc1;
+                r->err = wv_last_error();
+            }
+        }
     }
 }
 
@@ -132,6 +162,10 @@ extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int6
                                          uint64_t* out_ids, float* out_dists, int32_t* out_count) {
     if (!idx || !out_count) return set_err(WV_ERR_INVALID, "nil argument");
     if (d > 0 && !query) return set_err(WV_ERR_INVALID, "nil query");
+    // a malformed list fails this caller alone, before it can share a launch;
+    // any non-zero mode is a list, as in a one-query batch call
+    allow_mode = allow_mode != 0 ? 1 : 0;
+    if (allow_mode == 1 && (n_allow < 0 || (n_allow > 0 && !allow_ids))) return set_err(WV_ERR_INVALID, "nil allow ids");
     wv_batcher* b = get_batcher(idx);
     wv_batch_req req{query, d, k, allow_ids, n_allow, allow_mode, out_ids, out_dists, out_count};
     std::unique_lock<std::mutex> lk(b->m);

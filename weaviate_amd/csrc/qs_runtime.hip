@@ -417,6 +417,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // select / exact pass RV over all queries (list == nullptr) or over the listed ones
         // phase 0: the first select resets the flag-list cursors (qscount[1], [3])
         const bool ctr_reset = phase == 0;
+        // sel_rc: a failed scratch allocation (checked after every sel call)
+        int sel_rc = WV_OK;
         auto sel = [&](int RV, const int32_t* list, const uint32_t* cnt, float* tA) {
             const unsigned gw = (unsigned)((cn + 3) / 4);
             uint32_t* lc = (ctr_reset && !list) ? idx->qscount : nullptr;
@@ -431,7 +433,10 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                 const int P = (int)std::max<int64_t>(1, std::min<int64_t>(256, (nb + 2047) / 2048));
                 const int LV = 64 * (RV - 1);
                 const size_t pb = (size_t)cn * P * (k + 1) * sizeof(float);
-                if (idx->qsScratch.ensure(pb + (size_t)cn * sizeof(float)) != hipSuccess) return;
+                if (idx->qsScratch.ensure(pb + (size_t)cn * sizeof(float)) != hipSuccess) {
+                    sel_rc = set_err(WV_ERR_HIP, "split selection: %zu bytes of scratch", pb + (size_t)cn * sizeof(float));
+                    return;
+                }
                 float* part = idx->qsScratch.as<float>();
                 float* Tq = part + (size_t)cn * P * (k + 1);
                 dim3 gp((unsigned)P, (unsigned)cn);
@@ -475,6 +480,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                              fmask);
         };
         if (phase != 2) sel(R, nullptr, nullptr, phase == 1 ? topA : nullptr);
+        if (sel_rc) return sel_rc;
         HIPCHK(hipGetLastError());
         if (phase == 1) continue;
         if (phase == 2)  // the global threshold cuts this shard's candidate lists
@@ -526,6 +532,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             if (!ctr_reset) HIPCHK(hipMemsetAsync(idx->qscount + 3, 0, sizeof(uint32_t), s));
             k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, olist, idx->qscount + 2, 2);
             sel(8, olist, idx->qscount + 2, nullptr);
+            if (sel_rc) return sel_rc;
             exa(8, olist, idx->qscount + 2);
             HIPCHK(hipGetLastError());
         }
@@ -539,6 +546,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             const int32_t* keep = idx->pqa_m;
             idx->pqa_m = idx->pqaM2.as<int32_t>();  // the select reads pqa_m + c0
             sel(16, olist, idx->qscount + 2, nullptr);
+            if (sel_rc) return sel_rc;
             idx->pqa_m = keep;
             exa(16, olist, idx->qscount + 2);
             HIPCHK(hipGetLastError());
