@@ -168,6 +168,46 @@ def test_q8_staggered_epilogue_same_keys(wv, oracle, metric, kind, d, k, variant
         assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")
 
 
+@pytest.mark.parametrize("metric,kind,d,k", [("cosine", 0, 768, 10), ("l2-squared", 1, 512, 100), ("dot", 0, 640, 10)])
+@pytest.mark.parametrize("nq", [40, 64, 100, 300])
+def test_q8_live_padding_waves_same_keys(wv, oracle, metric, kind, d, k, nq):
+    """q8_live (default 1): in a batch that is not a multiple of 256 queries the
+    waves holding only padding queries skip their MFMAs; every real query's
+    keys and results equal the full schedule's (q8_live 0) and the oracle."""
+    n = 20000 + 37
+    data = gen(oracle, kind, 83, n, d)
+    queries = gen(oracle, kind, 84, nq, d)
+    res, keys = [], []
+    probe = sorted({0, 31, 32, nq - 1})
+    for opt in ({"q8_live": 0, "q8_gemv": 0}, {"q8_live": 1, "q8_gemv": 0}):
+        idx, orc = build_pair(wv, oracle, metric, "avx256", data, options=opt)
+        res.append(idx.search_by_vector_batch(queries, k))
+        assert idx.stats()["last_route"] == ROUTE_INT8
+        keys.append([idx.debug_blockkeys(q)[0] for q in probe])
+        idx.close()
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    for a, b in zip(keys[0], keys[1]):
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    ids, dists, counts = res[1]
+    for qi in range(0, nq, 7):
+        assert_same(orc.search(queries[qi], k), ids[qi, :counts[qi]], dists[qi, :counts[qi]], f"{metric} q{qi}")
+
+
+def test_q8_prio_same_keys(wv, oracle):
+    """q8_prio 1 (waves 4-7 at s_setprio 1) changes the issue order only."""
+    n, d, k = 20000 + 37, 768, 10
+    data = gen(oracle, 0, 85, n, d)
+    queries = gen(oracle, 0, 86, 512, d)
+    res = []
+    for opt in ({"q8_prio": 0}, {"q8_prio": 1}):
+        idx, orc = build_pair(wv, oracle, "cosine", "avx256", data, options=opt)
+        res.append(idx.search_by_vector_batch(queries, k) + (idx.debug_blockkeys(300)[0],))
+        idx.close()
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+
+
 # ---------------------------------------------------------------------------
 # BQ block minima on the integer matrix cores (k_q8_blockkey<..., BQ> over
 # +-1 code planes): hamming = (64 words - sum s_q s_x) / 2, exact

@@ -278,6 +278,8 @@ struct Q8Args {
     int nspans;
     int nqg;                   // query groups of 256
     int bq_bits;               // BQ: code bits 64 * words (hamming = (bq_bits - dot) / 2)
+    int64_t nq_live = 1ll << 62;  // k_q8_blockkey<.., LIVE>: the launch's real queries (the rest is padding)
+    int prio = 0;                 // k_q8_blockkey: 1 = waves 4-7 at s_setprio 1 for the whole loop
 };
 namespace {
 
@@ -319,7 +321,14 @@ namespace {
 // DBG (timing experiments in a -DWV_QS_DBG build only, wrong results): bit 0
 // drops the plane DMA, bit 1 the MFMAs, bit 2 the block reductions and stores,
 // bit 3 the key stores only.
-template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false, int PF = 1, int DBG = 0>
+// LIVE (PAIR schedule; a batch that is not a multiple of 256 queries): a wave
+// whose 32 queries all lie at or past a.nq_live -- the padding of the last
+// query group -- reads no fragments and issues no MFMA or reduction; it still
+// issues its share of every slot's DMA and its key stores (+inf), so each
+// wave's vector-memory counts, which the ring's vmcnt waits rely on, are those
+// of the full schedule.  A batch of 64 queries runs the MFMAs of 2 waves
+// instead of 8 (the HBM stream of the plane is then the bound).
+template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false, int PF = 1, int DBG = 0, bool LIVE = false>
 __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     constexpr int NPB = 2 * NC;                     // 1 KiB pieces per 32-row block
     constexpr int SLOT = RB * NPB * 1024;           // bytes per ring slot
@@ -333,6 +342,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     static_assert(PF >= 1 && PF + 1 < NC, "prefetch distance");
     static_assert(!STAG || RB == 2, "the stagger defers a slot's second block");
     static_assert(!BQ || (!ISL2 && !STAG), "BQ: integer maxima, in-order schedule");
+    static_assert(!LIVE || (RB == 2 && !STAG && !BQ && DBG == 0), "LIVE: the paired in-order schedule");
     constexpr int X0 = 1;                           // chunk of the slot's extra LDS reads
     constexpr int XE = 2 + (ISL2 ? 2 * RB : 0);     // extra reads: valid words, scales (+ norms)
     constexpr int NBUF = 3;
@@ -346,12 +356,14 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     // XCD-aware order: the query groups of one span share an XCD (its L2)
     const int logical = (total % 8 == 0) ? (b % 8) * (total / 8) + (b / 8) : b;
     const int span = logical / a.nqg, grp = logical % a.nqg;
+    // uniform: grp from blockIdx, wave readfirstlane'd
+    const bool act = !LIVE || (int64_t)grp * 256 + wave * 32 < a.nq_live;
 
     // this wave's 32 queries as B fragments: Qf[2c + n] = chunk c, query half
     // n: lane (j = lane & 15, kq = lane >> 4) holds query wave*32 + 16n + j,
     // columns 64c + 16kq .. +15
     i32x4_t Qf[2 * NC];
-    {
+    if (act) {
         const int j = lane & 15, kq = lane >> 4;
         const unsigned char* qp =
             a.Q8 + (int64_t)grp * TILE_B + (kq >> 1) * 8192 + (wave * 32 + j) * 32 + 16 * (kq & 1);
@@ -442,7 +454,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         qs_wait_vm(nsteps > 1 ? P0 : 0);  // group 0 landed, group 1 may stay in flight
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        head_reads(ring + l16);
+        if (act) head_reads(ring + l16);
     }
     // the pending block (a slot's last): per query half n the lane's partial
     // key before the cross-lane combine
@@ -598,7 +610,10 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         r0 = rr[0];
         r1 = rr[1];
     };
-    uint32_t pA0 = 0, pA1 = 0, pB0 = 0, pB1 = 0;  // PAIR: the pending slot's raw partials
+    // PAIR: the pending slot's raw partials ("no valid row" until a block is
+    // reduced: a LIVE wave without queries stores +inf keys)
+    constexpr uint32_t PNONE = ISL2 ? 0x7f800000u : (uint32_t)Q8_NONE;
+    uint32_t pA0 = PNONE, pA1 = PNONE, pB0 = PNONE, pB1 = PNONE;
     float psA = 0.f, psB = 0.f;                    // and its block scales
     i32x4_t acc[RB][2][2];
     // STAG, waves 4-7: the previous slot's last block is reduced late, from its
@@ -607,6 +622,14 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     uint32_t dvw = 0;
     float dsb = 0.f;
     f32x4_t dxa = {0.f, 0.f, 0.f, 0.f}, dxb = {0.f, 0.f, 0.f, 0.f};
+    // static priority for the younger half of the SIMD pairs (MI355X_MICROARCH.md,
+    // two waves per SIMD, item 4): one s_setprio before the loop, none inside
+    if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
+    // the slot loop; LIVE: a second copy for a wave without queries (ACT false:
+    // no fragment reads, MFMAs or reductions; the same DMA, key stores and
+    // barriers), so neither copy branches around its MFMAs
+    auto slot_loop = [&](auto actc) {
+    constexpr bool ACT = decltype(actc)::value;
     int cur = 0;
     for (int t = 0; t < nsteps; t++) {
         const int nxt = cur == NBUF - 1 ? 0 : cur + 1;
@@ -624,7 +647,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         static_for<0, NT>([&](auto ttc) {
             constexpr int tt = decltype(ttc)::value;
             constexpr int rb = tt / NC, c = tt % NC;
-            if constexpr (tt == X0) {  // this slot's valid words, scales (+ L2 norms)
+            if constexpr (tt == X0 && ACT) {  // this slot's valid words, scales (+ L2 norms)
                 asm volatile("ds_read_b64 %0, %1" : "=v"(vwv) : "v"(vring + sm * 16u));
                 asm volatile("ds_read_b64 %0, %1" : "=v"(sbv) : "v"(sring + sm * 16u));
                 if constexpr (ISL2) {
@@ -638,7 +661,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
                     }
                 }
             }
-            if constexpr (tt + PF < NT) {
+            if constexpr (tt + PF < NT && ACT) {
                 constexpr int o1 = ((tt + PF) / NC * NPB + 2 * ((tt + PF) % NC)) * 1024;
                 B2[(tt + PF) % NB2][0] = lds_ld16_o<o1>(sbase);
                 B2[(tt + PF) % NB2][1] = lds_ld16_o<o1 + 512>(sbase);
@@ -657,6 +680,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ACT)
 #pragma unroll
             for (int m = 0; m < 2; m++)
 #pragma unroll
@@ -685,7 +709,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
                 }
             }
             // PAIR: block 0's partials beside block 1's MFMAs (stored with block 1)
-            if constexpr (PAIR && tt == NC + 1 && !(DBG & 4)) reduce_raw(acc[0], vwv.x, sbv.x, xa[0], xb[0], pA0, pA1);
+            if constexpr (PAIR && tt == NC + 1 && !(DBG & 4) && ACT) reduce_raw(acc[0], vwv.x, sbv.x, xa[0], xb[0], pA0, pA1);
             // RB = 2: block 0 is reduced and stored beside block 1's MFMAs
             if constexpr (RB == 2 && !PAIR && tt == NC + 1 && !(DBG & 4)) {
                 if (!late) {
@@ -708,9 +732,11 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             dxa = xa[RB - 1];
             dxb = xb[RB - 1];
         } else if constexpr (PAIR && !(DBG & 4)) {
-            reduce_raw(acc[1], vwv.y, sbv.y, xa[1], xb[1], pB0, pB1);
-            psA = sbv.x;
-            psB = sbv.y;
+            if constexpr (ACT) {
+                reduce_raw(acc[1], vwv.y, sbv.y, xa[1], xb[1], pB0, pB1);
+                psA = sbv.x;
+                psB = sbv.y;
+            }
         } else if constexpr (!(DBG & 4)) {
             reduce(acc[RB - 1], RB == 2 ? vwv.y : vwv.x, RB == 2 ? sbv.y : sbv.x, xa[RB - 1], xb[RB - 1], mp0, mp1);
         } else {
@@ -734,9 +760,16 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             }
             __builtin_amdgcn_s_barrier();  // slot t is free; slot t+1 has landed for every wave
             __builtin_amdgcn_sched_barrier(0);
-            head_reads(ring + (unsigned)(nxt * SLOT) + l16);
+            if constexpr (ACT) head_reads(ring + (unsigned)(nxt * SLOT) + l16);
         }
         cur = nxt;
+    }
+    };
+    if constexpr (LIVE) {
+        if (act) slot_loop(std::true_type{});
+        else slot_loop(std::false_type{});
+    } else {
+        slot_loop(std::true_type{});
     }
     if (nsteps > 0 && !(DBG & 4)) {
         if constexpr (PAIR) {

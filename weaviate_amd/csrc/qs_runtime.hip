@@ -272,7 +272,15 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         k_q8_blockkey<12, 2, false, false, false, 1, DV><<<grid, 512, lds, s>>>(q8a);                           \
     } while (0)
 #endif
-#define WV_Q8T(NCV, L2V) do { if (idx->q8_stag) WV_Q8S(NCV, 2, L2V, true, 1); else WV_Q8(NCV, 2, L2V); } while (0)
+#define WV_Q8L(NCV, L2V)                                                                                       \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, 2, L2V, false, false, 1, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey<NCV, 2, L2V, false, false, 1, 0, true><<<grid, 512, lds, s>>>(q8a);                     \
+    } while (0)
+        // a partial last query group (batches that are not a multiple of 256):
+        // the padding's waves skip their MFMAs (LIVE)
+        const bool q8live = idx->q8_live && cn % QS_QPB != 0;
+#define WV_Q8T(NCV, L2V) do { if (idx->q8_stag) WV_Q8S(NCV, 2, L2V, true, 1); else if (q8live) WV_Q8L(NCV, L2V); else WV_Q8(NCV, 2, L2V); } while (0)
 #define WV_Q8N(L2V)                                    \
     switch (NC8) {                                     \
     case 8: WV_Q8T(8, L2V); break;                     \
@@ -297,6 +305,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             q8a.slots_per_span = a.slots_per_span;
             q8a.nspans = a.nspans;
             q8a.nqg = a.nqg;
+            q8a.nq_live = cn;
+            q8a.prio = idx->q8_prio;
 #ifdef WV_QS_DBG
             if (idx->sel_dbg > 0 && !l2 && NC8 == 12) {
                 switch (idx->sel_dbg) {
@@ -399,6 +409,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
 #undef WV_QSW
 #undef WV_Q8N
 #undef WV_Q8T
+#undef WV_Q8L
 #undef WV_Q8S
 #undef WV_Q8
         HIPCHK(hipGetLastError());

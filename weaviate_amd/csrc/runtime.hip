@@ -734,6 +734,8 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "q8_bm") idx->q8_bm = value ? 1 : 0;
     else if (k == "pq8") idx->pq8_opt = value ? 1 : 0;
     else if (k == "q8_gemv") idx->q8_gemv = value ? 1 : 0;
+    else if (k == "q8_live") idx->q8_live = value ? 1 : 0;
+    else if (k == "q8_prio") idx->q8_prio = value ? 1 : 0;
     else if (k == "sel_split_max") idx->sel_split_max = value;
     else if (k == "rq_mfma") idx->rq_mfma = value ? 1 : 0;
     else if (k == "q8_bm_min") idx->q8_bm_min = value;
@@ -1328,7 +1330,7 @@ static int subindex_build(wv_index* idx, hipStream_t s, const std::vector<uint32
     sb->use_qs = idx->use_qs;
     set_dims(sb, idx->dims);
     sb->kernel_opt = idx->kernel_opt; sb->q8_opt = idx->q8_opt; sb->q8_R = idx->q8_R; sb->q8_filter = idx->q8_filter;
-    sb->q8_stag = idx->q8_stag; sb->q8_shape = idx->q8_shape; sb->q8_pf = idx->q8_pf; sb->exact_filter = idx->exact_filter; sb->exact_bm = idx->exact_bm; sb->q8_bm = idx->q8_bm; sb->q8_gemv = idx->q8_gemv; sb->sel_split_max = idx->sel_split_max; sb->q8_bm_min = idx->q8_bm_min;
+    sb->q8_stag = idx->q8_stag; sb->q8_shape = idx->q8_shape; sb->q8_pf = idx->q8_pf; sb->exact_filter = idx->exact_filter; sb->exact_bm = idx->exact_bm; sb->q8_bm = idx->q8_bm; sb->q8_gemv = idx->q8_gemv; sb->q8_live = idx->q8_live; sb->q8_prio = idx->q8_prio; sb->sel_split_max = idx->sel_split_max; sb->q8_bm_min = idx->q8_bm_min;
     sb->exact_cap = idx->exact_cap; sb->replay_par = idx->replay_par; sb->margin = idx->margin;
     sb->gemv_max = idx->gemv_max; sb->gemv_wg = idx->gemv_wg; sb->exact_multi = idx->exact_multi;
     sb->force_replay = idx->force_replay; sb->qs_force_flag = idx->qs_force_flag; sb->timing = idx->timing;
