@@ -519,7 +519,8 @@ int wv_multi_pq_set_centers(wv_multi *m, const float *centers, int64_t n_floats)
  * other key is set on every shard */
 int wv_multi_set_option(wv_multi *m, const char *key, int64_t value);
 /* out[n]: searches, flagged queries, overflowed records, chain hops, last
- * search's flagged and overflowed queries, world, rank0, n_local, transport */
+ * search's flagged and overflowed queries, world, rank0, n_local, transport,
+ * last search's host time in the call and of it blocked in its host syncs (us) */
 int wv_multi_stats(wv_multi *m, int64_t *out, int32_t n);
 /* option sim: per-shard stage times averaged over the searches since "sim"
  * was last set, out[stage][n_local] for

@@ -23,6 +23,7 @@ ap.add_argument("--batch", type=int, default=8192)
 ap.add_argument("--k", type=int, default=10)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--no-single", action="store_true")
+ap.add_argument("--rev", action="store_true", help="time the shards in reverse order (option sim_rev)")
 args = ap.parse_args()
 
 import numpy as np  # noqa: E402
@@ -51,6 +52,7 @@ oi = torch.empty((B, k), dtype=torch.int64, device=dev)
 od = torch.empty((B, k), dtype=torch.float32, device=dev)
 on = torch.empty(B, dtype=torch.int32, device=dev)
 torch.cuda.synchronize()
+m.set_option("sim_rev", 1 if args.rev else 0)
 m.set_option("sim", 1)
 m.search_device(q.data_ptr(), B, d, k, oi.data_ptr(), od.data_ptr(), on.data_ptr(), None)  # warm-up
 m.set_option("sim", 1)  # restart the averaging: back-to-back searches, as the GPUs of a real run see them
@@ -58,6 +60,24 @@ for rep in range(args.reps):
     m.search_device(q.data_ptr(), B, d, k, oi.data_ptr(), od.data_ptr(), on.data_ptr(), None)
 rows = [m.stage_ms()]
 st = m.stats()
+# without sim: one host thread issues every shard's stages back to back on its
+# streams; its time in the call minus the time blocked in the protocol's host
+# syncs is the issue cost a host thread pays per step for all shards
+m.set_option("sim", 0)
+s_ = torch.cuda.Stream(dev)
+host_issue_ms, host_wait_ms = {}, {}
+for ht in (1, 0):  # a host thread per shard (default), one thread for all shards
+    m.set_option("host_threads", ht)
+    host = []
+    for rep in range(args.reps):
+        with torch.cuda.stream(s_):
+            m.search_device(q.data_ptr(), B, d, k, oi.data_ptr(), od.data_ptr(), on.data_ptr(), s_.cuda_stream)
+        hs = m.stats()
+        host.append((hs["host_us"], hs["host_wait_us"]))
+        s_.synchronize()
+    host_issue_ms[ht] = float(np.median([(a - b) / 1e3 for a, b in host]))
+    host_wait_ms[ht] = float(np.median([b / 1e3 for a, b in host]))
+m.set_option("host_threads", 1)
 # the collectives' bytes per rank: keys + eps, the lists, the records
 k1 = k + 1
 gbytes = [B * k1 * 4 + B * 4, B * k1 * 16 + B * 8]
@@ -71,7 +91,9 @@ compute = sum(stage_max.values())
 xfer_est = sum(25e-3 + (W - 1) * b / 100e9 * 1e3 for b in gbytes)
 out = dict(world=W, n=n, d=d, batch=B, k=k, flagged=F, stage_max_ms=stage_max, per_shard_ms=per_shard,
            compute_ms=compute, allgather_bytes_per_rank=gbytes, allgather_est_ms=xfer_est,
-           predicted_step_ms=compute + xfer_est)
+           predicted_step_ms=compute + xfer_est, timed_order="reverse" if args.rev else "forward",
+           host_issue_ms={"thread_per_shard": host_issue_ms[1], "one_thread": host_issue_ms[0]},
+           host_wait_ms={"thread_per_shard": host_wait_ms[1], "one_thread": host_wait_ms[0]})
 same = None
 if not args.no_single:
     res = (oi.clone(), od.clone(), on.clone())

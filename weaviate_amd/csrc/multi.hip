@@ -34,7 +34,10 @@
 
 #include <dlfcn.h>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <map>
+#include <thread>
 #include <memory>
 #include <rccl/rccl.h>  // types only: the library is bound at run time
 
@@ -465,6 +468,62 @@ __global__ void k_iota32(int32_t* __restrict__ p, int64_t n) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// host threads: one per local shard beyond the first, so the stages of the
+// shards of one process are issued in parallel (a shard's stage is a few
+// dozen launches, ~0.4 ms of host time: issued one shard after another, the
+// last of 8 GPUs would start its stage ~3 ms after the first)
+// ---------------------------------------------------------------------------
+struct StagePool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done;
+    std::function<void(int)> task;
+    uint64_t gen = 0;
+    int pending = 0;
+    bool stop = false;
+    explicit StagePool(int n) {
+        for (int i = 1; i < n; i++)
+            th.emplace_back([this, i] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(int)> t;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        t = task;
+                    }
+                    t(i);
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (--pending == 0) done.notify_one();
+                }
+            });
+    }
+    ~StagePool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+    // fn(i) for every shard: 1.. on the pool's threads, 0 on the caller's
+    void run(int n, const std::function<void(int)>& fn) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            task = fn;
+            pending = n - 1;
+            gen++;
+        }
+        cv.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return pending == 0; });
+    }
+};
+
+// ---------------------------------------------------------------------------
 // the multi-shard index
 // ---------------------------------------------------------------------------
 enum { ST_PHASE1, ST_PHASE2, ST_MERGE, ST_REPLAY, ST_MERGE_REC, ST_CHAIN, ST_XFER, ST_N };
@@ -493,9 +552,13 @@ struct wv_multi {
     uint64_t id_stride = 0;
     std::vector<std::unique_ptr<MRank>> r;
     std::unique_ptr<Transport> tr;
+    std::unique_ptr<StagePool> pool;  // option host_threads (default 1 with several local shards)
     hipEvent_t e_call = nullptr;
     int32_t* pin = nullptr;  // pinned host words: flagged count, overflow count
     int sim = 0;
+    int sim_rev = 0;  // option sim_rev: option sim times the shards in reverse order (is a slow first shard the shard or its slot?)
+    // host time of the last search: spent issuing work vs blocked in the host syncs (us)
+    double host_total_us = 0, host_wait_us = 0;
     int rec_cap = 0;  // option rec_cap (tests): replay record capacity, 0 = max(256, 16 k) (exact), 2R (BQ), 2R + 64 (quantized)
     int force_chain = 0;  // option chain (tests): compressed searches take the serial chain
     double stage_ms[ST_N][64] = {};  // option sim: stage times summed over sim_n searches
@@ -510,11 +573,35 @@ int owner_rank(const wv_multi* m, uint64_t id) {
     return (int)std::min<uint64_t>(r, (uint64_t)(m->world - 1));
 }
 
+// a host sync of the protocol, its blocked time accounted (wv_multi_stats)
+hipError_t host_sync(wv_multi* m, hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t e = hipStreamSynchronize(s);
+    m->host_wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    return e;
+}
+
 // issue one stage on every local shard; with option sim every shard's part is
 // timed alone (HIP events, then a sync before the next shard)
 template <class Fn>
 int run_stage(wv_multi* m, int st, Fn fn) {
-    for (int i = 0; i < m->nl; i++) {
+    if (m->pool && !m->sim) {
+        // every shard's part on its own host thread; a failure's text moves to
+        // the caller's thread (wv_last_error is per thread)
+        std::vector<int> rc((size_t)m->nl, WV_OK);
+        std::vector<std::string> err((size_t)m->nl);
+        m->pool->run(m->nl, [&](int i) {
+            MRank& R = *m->r[i];
+            hipError_t e = hipSetDevice(R.dev);
+            rc[(size_t)i] = e == hipSuccess ? fn(R, i) : set_err(WV_ERR_HIP, "hipSetDevice: %s", hipGetErrorString(e));
+            if (rc[(size_t)i]) err[(size_t)i] = wv_last_error();
+        });
+        for (int i = 0; i < m->nl; i++)
+            if (rc[(size_t)i]) return set_err(rc[(size_t)i], "%s", err[(size_t)i].c_str());
+        return WV_OK;
+    }
+    for (int i0 = 0; i0 < m->nl; i0++) {
+        const int i = m->sim && m->sim_rev ? m->nl - 1 - i0 : i0;
         MRank& R = *m->r[i];
         HIPCHK(hipSetDevice(R.dev));
         if (m->sim) HIPCHK(hipEventRecord(R.t0, R.s));
@@ -717,7 +804,7 @@ int multi_search(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, uin
     });
     if (rc) return rc;
     HIPCHK(hipSetDevice(H.dev));
-    HIPCHK(hipStreamSynchronize(H.s));  // host sync 1: the list length (equal on every rank)
+    HIPCHK(host_sync(m, H.s));  // host sync 1: the list length (equal on every rank)
     const int F = m->pin[0];
     m->last_flagged = F;
     m->n_flagged += F;
@@ -791,7 +878,7 @@ int multi_search(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, uin
         });
         if (rc) return rc;
         HIPCHK(hipSetDevice(H.dev));
-        HIPCHK(hipStreamSynchronize(H.s));  // host sync 2: overflowed records (the same on every rank)
+        HIPCHK(host_sync(m, H.s));  // host sync 2: overflowed records (the same on every rank)
         const int U = m->pin[1];
         m->last_overflow = U;
         m->n_overflow += U;
@@ -975,7 +1062,7 @@ int rheap_parallel(wv_multi* m, int64_t nc, int Rk, int cap, BoundsFn bounds_fn,
     if (rc) return rc;
     MRank& H = *m->r[0];
     HIPCHK(hipSetDevice(H.dev));
-    HIPCHK(hipStreamSynchronize(H.s));  // host sync: overflowed records (the same count on every rank)
+    HIPCHK(host_sync(m, H.s));  // host sync: overflowed records (the same count on every rank)
     *overflow = m->pin[1];
     return WV_OK;
 }
@@ -1238,6 +1325,8 @@ int multi_dispatch(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, u
                                            "quantizer: wv_multi_pq_fit / wv_multi_pq_set_centers)");
     if (m->sim) m->sim_n++;
     m->last_flagged = m->last_overflow = 0;
+    m->host_wait_us = 0;
+    const auto t_call = std::chrono::steady_clock::now();
     int rc;
     if (kind == MK_EXACT) rc = multi_search(m, q0, nq, d, k, o_i0, o_d0, o_n0, cs);
     else {
@@ -1247,6 +1336,7 @@ int multi_dispatch(wv_multi* m, const float* q0, int64_t nq, int64_t d, int k, u
         if (!rc) rc = join_caller(m, cs);
     }
     if (rc) return rc;
+    m->host_total_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call).count();
     m->n_search++;
     return WV_OK;
 }
@@ -1321,6 +1411,7 @@ extern "C" void wv_multi_destroy(wv_multi* m) {
         hipSetDevice(R->dev);
         if (R->s) hipStreamSynchronize(R->s);
     }
+    m->pool.reset();
     m->tr.reset();
     for (auto& R : m->r) {
         hipSetDevice(R->dev);
@@ -1410,6 +1501,7 @@ extern "C" int wv_multi_create(const wv_multi_config* cfg, wv_multi** out) {
     }
     m->tr = std::move(tr);
     if (rc) return fail(rc);
+    if (m->nl > 1) m->pool = std::make_unique<StagePool>(m->nl);
     *out = m;
     return WV_OK;
 }
@@ -1426,6 +1518,15 @@ extern "C" int wv_multi_set_option(wv_multi* m, const char* key, int64_t value) 
         m->sim = value ? 1 : 0;
         m->sim_n = 0;
         memset(m->stage_ms, 0, sizeof(m->stage_ms));
+        return WV_OK;
+    }
+    if (std::string(key) == "host_threads") {  // 0: one host thread issues every shard's stages
+        if (!value) m->pool.reset();
+        else if (!m->pool && m->nl > 1) m->pool = std::make_unique<StagePool>(m->nl);
+        return WV_OK;
+    }
+    if (std::string(key) == "sim_rev") {
+        m->sim_rev = value ? 1 : 0;
         return WV_OK;
     }
     if (std::string(key) == "chain") {
@@ -1788,7 +1889,7 @@ extern "C" int wv_multi_stats(wv_multi* m, int64_t* out, int32_t n) {
     if (!m || !out) return set_err(WV_ERR_INVALID, "nil argument");
     std::lock_guard<std::mutex> g(m->mu);
     const int64_t v[] = {m->n_search, m->n_flagged, m->n_overflow, m->n_chain, m->last_flagged, m->last_overflow,
-                         m->world, m->rank0, m->nl, m->kind};
+                         m->world, m->rank0, m->nl, m->kind, (int64_t)m->host_total_us, (int64_t)m->host_wait_us};
     for (int i = 0; i < n && i < (int)(sizeof(v) / sizeof(v[0])); i++) out[i] = v[i];
     return WV_OK;
 }

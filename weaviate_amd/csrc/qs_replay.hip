@@ -29,9 +29,12 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
     // row of the keys' row set (the union) but not necessarily one of the
     // query's own; the one-wave replay prunes by its true heap top only
     const bool ub_ok = idx->cur_vq == 0;
-    // a few listed queries (small batches): the one-launch 8-wave form instead
-    // of the pooled form's three launches (most such calls list no query)
-    const bool few = max_list <= 16 && !rec_i && k < 64 && nch <= RP_MAXCH && idx->replay_par;
+    // a few listed queries of a small batch, counted on the device (most such
+    // calls list no query): the one-launch 8-wave form instead of the pooled
+    // form's three launches.  A host list (counters NULL: the cross-shard
+    // replay's flagged queries, every one of which replays) takes the pooled
+    // form: 9 flagged C3 queries on a 1.25M-row shard 2.8 -> 0.5 ms
+    const bool few = counters && max_list <= 16 && !rec_i && k < 64 && nch <= RP_MAXCH && idx->replay_par;
     if (ub_ok && !few && blk_pooled(idx, k, nb)) {
         // pooled form: bounds + candidate pool (8 waves per query), exact
         // distances over the whole grid, one-wave heap per query

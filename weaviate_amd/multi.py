@@ -225,10 +225,10 @@ class MultiFlatIndex:
                                                    counts_ptr, stream))
 
     def stats(self) -> dict:
-        out = (C.c_int64 * 10)()
-        check(self._l.wv_multi_stats(self._h, out, 10))
+        out = (C.c_int64 * 12)()
+        check(self._l.wv_multi_stats(self._h, out, 12))
         keys = ("searches", "flagged", "overflowed", "chain_hops", "last_flagged", "last_overflowed", "world",
-                "rank0", "n_local", "transport")
+                "rank0", "n_local", "transport", "host_us", "host_wait_us")
         return dict(zip(keys, [int(x) for x in out]))
 
     def stage_ms(self) -> dict:
