@@ -136,3 +136,29 @@ def test_batcher_coalesces_distinct_allow_lists(wv, oracle):
     st = idx.batcher_stats()
     assert st["launches"] < st["calls"] and st["max_batch"] > 1, st
     idx.close()
+
+
+@pytest.mark.parametrize("opts,k,nq", [({"pqa_budget_mb": 1}, 10, 200),     # bitmap budget: sub-batches (offsets q0 * k)
+                                       ({"sel_lower": 1}, 10, 64),           # the select's lowered thresholds
+                                       ({}, 1000, 24),                       # k > 959: 1984-block lists, R = 32
+                                       ({"pqa_split_max": 0, "pqa_alone": 0}, 300, 40)])
+def test_multi_allow_option_paths_equal_one_query_calls(wv, oracle, opts, k, nq):
+    """The multi-allow paths ADVICE r5 listed as untested: the per-query bitmap
+    budget's sub-batch recursion, sel_lower = 1, large k with per-query
+    bitmaps; each against the one-query calls."""
+    n, d = 30000, 128
+    data = oracle.gen_matrix(1, 73, 0, n, d)  # integer data: ties, replays
+    queries = oracle.gen_matrix(1, 74, 0, nq, d)
+    idx = wv.FlatIndex(distance="l2-squared", variant="avx256")
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    for kk, vv in opts.items():
+        idx.set_option(kk, vv)
+    allows = _allow_lists(wv, n, nq, min(k, 64), seed=7 + k)
+    ids, dists, counts = idx.search_by_vector_batch_multi_allow(queries, k, allows)
+    for i in range(nq):
+        ei, ed, ec = idx.search_by_vector_batch(queries[i:i + 1], k, allow=allows[i])
+        assert counts[i] == ec[0], f"q{i}"
+        np.testing.assert_array_equal(ids[i, :counts[i]], ei[0, :ec[0]], err_msg=f"q{i}")
+        np.testing.assert_array_equal(dists[i, :counts[i]].view(np.uint32), ed[0, :ec[0]].view(np.uint32),
+                                      err_msg=f"q{i}")
+    idx.close()

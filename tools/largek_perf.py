@@ -1,6 +1,6 @@
 """block-key route time vs k (device time from the index's own events)"""
 import sys, json, time, numpy as np
-sys.path.insert(0, "/root/repo")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import weaviate_amd as wv
 from weaviate_amd import _lib
 import torch

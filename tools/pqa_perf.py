@@ -1,6 +1,6 @@
 """per-query allow lists: one shared launch vs one call per list (host-inclusive)"""
 import sys, time, json, numpy as np
-sys.path.insert(0, "/root/repo")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import weaviate_amd as wv
 wv.load()
 import torch
