@@ -3,10 +3,11 @@
 // buffers -- how the cgo shim's goroutines would call it) on the C3 corpus for
 // S seconds; prints one JSON line with QPS, launches, mean batch and latency.
 // Build: hipcc -O2 -std=c++17 tools/serve_bench.cpp -Iinclude -Lweaviate_amd -lwvknn -Wl,-rpath,'$ORIGIN/../weaviate_amd' -o tools/serve_bench
-// Run:   tools/serve_bench [n=10000000] [threads=256] [seconds=10] [window_us=0] [allow_pct=0]
-// allow_pct > 0: every thread searches under its own allow list (a random
-// allow_pct % of the ids, different per thread) -- filtered callers, batched
-// through wv_index_search_by_vector_batch_multi_allow.
+// Run:   tools/serve_bench [n=10000000] [threads=256] [seconds=10] [window_us=0] [allow_pct=0] [filtered_pct=100]
+// allow_pct > 0: filtered_pct % of the threads search under their own allow
+// list (a random allow_pct % of the ids, different per thread) -- filtered
+// callers, batched through wv_index_search_by_vector_batch_multi_allow; the
+// other threads search unfiltered (their own launch of the same batch).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,6 +37,7 @@ int main(int argc, char** argv) {
     const double secs = argc > 3 ? atof(argv[3]) : 10.0;
     const int64_t window = argc > 4 ? atoll(argv[4]) : 0;
     const double allow_pct = argc > 5 ? atof(argv[5]) : 0.0;
+    const double filtered_pct = argc > 6 ? atof(argv[6]) : 100.0;
     const int d = 768, k = 10, nq = 4096;
     wv_config cfg{};
     cfg.metric = WV_METRIC_COSINE_DOT;
@@ -75,8 +77,11 @@ int main(int argc, char** argv) {
     std::atomic<int> fails{0};
     std::vector<std::vector<double>> lat(T);
     std::vector<std::vector<uint64_t>> allow(T);
+    int nfilt = 0;
     if (allow_pct > 0)
         for (int t = 0; t < T; t++) {  // thread t's list: ids whose hash falls below allow_pct %
+            if (t >= (int)(T * filtered_pct / 100.0 + 0.5)) continue;  // an unfiltered caller
+            nfilt++;
             const uint64_t thr = (uint64_t)(allow_pct / 100.0 * 4294967296.0);
             for (int64_t i = 0; i < n; i++) {
                 uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull + (uint64_t)(t + 1) * 0xBF58476D1CE4E5B9ull;
@@ -96,8 +101,9 @@ int main(int argc, char** argv) {
             for (int i = t; clk::now() < stop; i += T) {
                 auto a = clk::now();
                 const std::vector<uint64_t>& al = allow[t];
-                if (wv_index_search_by_vector(idx, &q[(size_t)(i % nq) * d], d, k, al.empty() ? nullptr : al.data(),
-                                              (int64_t)al.size(), allow_pct > 0 ? 1 : 0, li, ld, &lc))
+                const bool filtered = allow_pct > 0 && t < nfilt;
+                if (wv_index_search_by_vector(idx, &q[(size_t)(i % nq) * d], d, k, filtered ? al.data() : nullptr,
+                                              (int64_t)al.size(), filtered ? 1 : 0, li, ld, &lc))
                     fails++;
                 lat[t].push_back(std::chrono::duration<double, std::milli>(clk::now() - a).count());
             }
@@ -110,10 +116,10 @@ int main(int argc, char** argv) {
     std::sort(all.begin(), all.end());
     auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, (size_t)(p * all.size()))]; };
     int64_t calls = st1[0] - st0[0], launches = st1[1] - st0[1];
-    printf("{\"workload\": \"%lld x %d cosine k=%d, single-query calls from %d C++ threads, allow lists %.2f %%\", \"qps\": %.1f, "
+    printf("{\"workload\": \"%lld x %d cosine k=%d, single-query calls from %d C++ threads, %d of them with allow lists of %.2f %%\", \"qps\": %.1f, "
            "\"serial_qps\": %.1f, \"calls\": %lld, \"launches\": %lld, \"mean_batch\": %.1f, \"max_batch\": %lld, "
            "\"latency_ms\": {\"p50\": %.2f, \"p99\": %.2f}, \"window_us\": %lld, \"failures\": %d}\n",
-           (long long)n, d, k, T, allow_pct, calls / el, serial_qps, (long long)calls, (long long)launches,
+           (long long)n, d, k, T, nfilt, allow_pct, calls / el, serial_qps, (long long)calls, (long long)launches,
            launches ? (double)calls / launches : 0.0, (long long)st1[2], pct(0.5), pct(0.99), (long long)window,
            fails.load());
     wv_index_destroy(idx);
