@@ -162,3 +162,41 @@ def test_multi_allow_option_paths_equal_one_query_calls(wv, oracle, opts, k, nq)
         np.testing.assert_array_equal(dists[i, :counts[i]].view(np.uint32), ed[0, :ec[0]].view(np.uint32),
                                       err_msg=f"q{i}")
     idx.close()
+
+
+@pytest.mark.parametrize("id_base,opts,k,nq", [(0, {}, 10, 54),
+                                               (1000013, {}, 10, 45),                       # unaligned shard base
+                                               (64, {"pqa_split_max": 0, "pqa_alone": 0}, 32, 40),
+                                               (0, {"pqa_budget_mb": 1}, 10, 120),           # sub-batches: via lists
+                                               (0, {}, 300, 30)])
+def test_multi_allow_bitmap_form_equals_id_lists(wv, oracle, id_base, opts, k, nq):
+    """wv_index_search_by_vector_batch_multi_allow_bitmap: the same lists as
+    dense doc-id bitmaps give the id-list call's rows (and the oracle's), on an
+    index whose doc ids start at id_base (a shard): the bitmap words are read
+    from id_base on with the bit shift id_base % 32."""
+    n, d = 20000, 128
+    data = oracle.gen_matrix(1, 81, 0, n, d)  # integer data: ties
+    queries = oracle.gen_matrix(1, 82, 0, nq, d)
+    idx = wv.FlatIndex(distance="l2-squared", variant="avx256", id_base=id_base)
+    idx.add_batch(np.arange(id_base, id_base + n, dtype=np.uint64), data)
+    idx.delete(*range(id_base + 3, id_base + n, 101))
+    for kk, vv in opts.items():
+        idx.set_option(kk, vv)
+    base = _allow_lists(wv, n, nq, min(k, 64), seed=11 + k)
+    allows = [None if a is None else wv.AllowList(a.ids.astype(np.uint64) + np.uint64(id_base)) for a in base]
+    ids, dists, counts = idx.search_by_vector_batch_multi_allow(queries, k, allows)
+    bi, bd, bc = idx.search_by_vector_batch_multi_allow(queries, k, allows, bitmap=True)
+    np.testing.assert_array_equal(bc, counts)
+    for i in range(nq):
+        np.testing.assert_array_equal(bi[i, :counts[i]], ids[i, :counts[i]], err_msg=f"q{i}")
+        np.testing.assert_array_equal(bd[i, :counts[i]].view(np.uint32), dists[i, :counts[i]].view(np.uint32),
+                                      err_msg=f"q{i}")
+    orc = oracle.OracleFlat(oracle.METRIC["l2-squared"], 1, d, n)
+    orc.add_batch(np.arange(n, dtype=np.uint64), data)
+    orc.delete(list(range(3, n, 101)))
+    for i in range(min(nq, 12)):
+        al = None if base[i] is None else [int(x) for x in base[i].ids]
+        rc, oi, od = orc.search(queries[i], k, al)
+        np.testing.assert_array_equal(bi[i, :bc[i]], oi.astype(np.uint64) + np.uint64(id_base), err_msg=f"q{i}")
+        np.testing.assert_array_equal(bd[i, :bc[i]].view(np.uint32), od.view(np.uint32), err_msg=f"q{i}")
+    idx.close()

@@ -125,6 +125,8 @@ SIGNATURES = {
     "wv_index_search_by_vector_batch": (C.c_int, [P, pf32, i64, i64, i32, pu64, i64, i32, pu64, pf32, pi32]),
     "wv_index_search_by_vector_batch_multi_allow": (C.c_int, [P, pf32, i64, i64, i32, pu64, P, pi32, pu64, pf32,
                                                               pi32]),
+    "wv_index_search_by_vector_batch_multi_allow_bitmap": (C.c_int, [P, pf32, i64, i64, i32, P, i64, pi32, pu64,
+                                                                     pf32, pi32]),
     "wv_index_search_by_vector_distance": (C.c_int, [P, pf32, i64, f32, i64, pu64, i64, i32, pu64, pf32, pi32]),
     "wv_index_search_device": (C.c_int, [P, P, i64, i64, i32, i32, P, P, P, P, P]),
     "wv_index_replay_device": (C.c_int, [P, P, i64, i64, i32, P, i32, P, P, P, i32, P, P, P, P]),

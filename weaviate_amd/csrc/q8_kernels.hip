@@ -87,6 +87,27 @@ __global__ void k_pqa_bits(const uint64_t* __restrict__ ids, const int64_t* __re
     if (present[sl >> 5] & m) atomicOr(&bits[lo * vq + (int64_t)(sl >> 5)], m);
 }
 
+// per-query bitmaps from the caller's doc-id bitmaps (the bitmap form of the
+// multi-allow call): raw holds each query's words from doc id (id_base & ~31)
+// on (sw words per query, avail of them copied), so slot word w is the funnel
+// shift of raw words w, w + 1 by id_base & 31; ANDed with present.  Unlisted
+// queries (mode 0) take the present bitmap.  Thread per (query, word).
+__global__ void k_pqa_from_bits(const uint32_t* __restrict__ raw, int64_t sw, int64_t avail,
+                                const int32_t* __restrict__ modes, int64_t nq, int sh,
+                                const uint32_t* __restrict__ present, int64_t vq, uint32_t* __restrict__ bits) {
+    const int64_t n = nq * vq;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = i / vq, w = i - q * vq;
+        uint32_t v = present[w];
+        if (modes[q]) {
+            const uint32_t* r = raw + q * sw;
+            const uint32_t lo = w < avail ? r[w] : 0u, hi = w + 1 < avail ? r[w + 1] : 0u;
+            v &= sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+        }
+        bits[i] = v;
+    }
+}
+
 // union of the nq bitmaps (the block keys' row set), thread per word
 __global__ void k_pqa_union(const uint32_t* __restrict__ bits, int64_t vq, int64_t nq, uint32_t* __restrict__ uni) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -2386,15 +2386,47 @@ __device__ __forceinline__ float rp_key_at(const float (&key)[RS], int e) {
 // is below thr; returns the new k-th smallest
 template <int RS>
 __device__ __forceinline__ float rp_offer(float (&sk)[RS], uint32_t (&sid)[RS], float v, float thr, int k, int lane) {
-    if (!__any(v < thr)) return thr;
+    uint64_t bm = __ballot(v < thr);
+    if (!bm) return thr;
+    if (__popcll(bm) <= 8) {
+        // a few values under the threshold (the common case after the first
+        // chunks): insert them one by one into rows 0..RS-2 (element e = 64 r +
+        // lane, ascending; the last one drops out), new[e] = old[e] < x ? old[e]
+        // : max(x, old[e - 1]) -- a few shuffles each instead of a 64-value sort
+        // (the list's ids stay 0: k_rp_bounds keeps values only)
+        while (bm) {
+            const int l = __builtin_ctzll(bm);
+            bm &= bm - 1;
+            const float x = __shfl(v, l);
+            if (!(x < thr)) continue;
+            float prev_last = -__builtin_inff();
+#pragma unroll
+            for (int r = 0; r < RS - 1; r++) {
+                const float o = sk[r];
+                const float up = __shfl_up(o, 1);
+                const float last = __shfl(o, 63);
+                const float pe = lane == 0 ? prev_last : up;
+                sk[r] = o < x ? o : fmaxf(x, pe);
+                prev_last = last;
+            }
+            thr = rp_key_at<RS>(sk, k - 1);
+        }
+        return thr;
+    }
     sk[RS - 1] = v;
     sid[RS - 1] = 0;
     bitonic_merge_last<RS>(sk, sid, lane);
     return rp_key_at<RS>(sk, k - 1);
 }
 
+// k_rp_bounds: 16 waves per listed query, two chunks per wave and step (64
+// loads in flight per lane): a lone flagged query of a 10M-row corpus (306
+// chunks) is latency-bound in one workgroup
+// (8 waves for RS = 4 / 8: their sorted lists need the registers)
+constexpr int rp_bounds_nw(int RS) { return RS == 2 ? 16 : 8; }
+
 template <int RS, int METRIC>
-__global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key, int64_t ldk, int64_t nb,
+__global__ __launch_bounds__(64 * rp_bounds_nw(RS)) void k_rp_bounds(const float* __restrict__ key, int64_t ldk, int64_t nb,
                                                    const float* __restrict__ eps_q, const float4* __restrict__ qinfo,
                                                    const int32_t* __restrict__ qlist, const uint32_t* __restrict__ counters,
                                                    int nlist, int k, const float* __restrict__ in_d,
@@ -2407,6 +2439,7 @@ __global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key
     __shared__ int scc[RP_MAXCH];
     __shared__ float sg0[16];
     __shared__ int s_total, s_off;
+    constexpr int NW = rp_bounds_nw(RS);
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int metric = METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2;
@@ -2426,18 +2459,23 @@ __global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key
             continue;
         }
         // 1. per chunk, per lane: the smallest row upper bound A + eps of 16 blocks
-        for (int c = w; c < nch; c += RP_NW) {
-            float kv[16];
+        for (int c = w; c < nch; c += 2 * NW) {
+            float kv[2][16];
 #pragma unroll
-            for (int u = 0; u < 16; u++) {
-                const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
-                kv[u] = bb < nb ? kr[bb] : __builtin_inff();
+            for (int h = 0; h < 2; h++) {  // one base address per chunk, immediate offsets
+                const float* kc = kr + (int64_t)(c + h * NW) * RP_CH;
+                const int64_t rem = nb - (int64_t)(c + h * NW) * RP_CH;
+#pragma unroll
+                for (int u = 0; u < 16; u++) kv[h][u] = u * 64 + lane < rem ? kc[u * 64 + lane] : __builtin_inff();
             }
-            float m = __builtin_inff();
 #pragma unroll
-            for (int u = 0; u < 16; u++)
-                if (kv[u] < __builtin_inff()) m = fminf(m, qs_key_to_a(metric, kv[u], qi.x) + eps);
-            sc[(int64_t)c * 64 + lane] = m;
+            for (int h = 0; h < 2; h++) {
+                float m = __builtin_inff();
+#pragma unroll
+                for (int u = 0; u < 16; u++)
+                    if (kv[h][u] < __builtin_inff()) m = fminf(m, qs_key_to_a(metric, kv[h][u], qi.x) + eps);
+                if (c + h * NW < nch) sc[(int64_t)(c + h * NW) * 64 + lane] = m;
+            }
         }
         __syncthreads();
         // 2. wave 0: suc[c] = k-th smallest of the handed-over heap and of the
@@ -2453,16 +2491,22 @@ __global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key
             }
             bitonic_sort<RS>(sk, sid, lane);
             float thr = rp_key_at<RS>(sk, k - 1);
-            for (int c0 = 0; c0 < nch; c0 += 16) {
-                float v[16];
+            float v[16];  // the next 16 chunks' lane minima are read while these merge
 #pragma unroll
-                for (int u = 0; u < 16; u++) v[u] = c0 + u < nch ? sc[(int64_t)(c0 + u) * 64 + lane] : __builtin_inff();
+            for (int u = 0; u < 16; u++) v[u] = u < nch ? sc[(int64_t)u * 64 + lane] : __builtin_inff();
+            for (int c0 = 0; c0 < nch; c0 += 16) {
+                float vn[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++)
+                    vn[u] = c0 + 16 + u < nch ? sc[(int64_t)(c0 + 16 + u) * 64 + lane] : __builtin_inff();
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     if (c0 + u >= nch) break;
                     if (lane == 0) suc[c0 + u] = thr;
                     thr = rp_offer<RS>(sk, sid, v[u], thr, k, lane);
                 }
+#pragma unroll
+                for (int u = 0; u < 16; u++) v[u] = vn[u];
             }
             // chunk 0 per 64-block group: also bounded by the k-th smallest A + eps
             // of its own earlier groups (the chunk-level bound is weakest there)
@@ -2486,31 +2530,43 @@ __global__ __launch_bounds__(512) void k_rp_bounds(const float* __restrict__ key
         for (int pass = 0; pass < 2; pass++) {
             const int off = pass ? s_off : 0;
             if (pass == 0 || off >= 0) {
-                for (int c = w; c < nch; c += RP_NW) {
-                    float kv[16];
+                for (int c2 = w; c2 < nch; c2 += 2 * NW) {
+                    float ka[16], kb[16];  // both chunks' keys in flight, one body (ballot SGPRs)
+                    {
+                        const float* kc = kr + (int64_t)c2 * RP_CH;
+                        const int64_t rem = nb - (int64_t)c2 * RP_CH;
 #pragma unroll
-                    for (int u = 0; u < 16; u++) {
-                        const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
-                        kv[u] = bb < nb ? kr[bb] : __builtin_inff();
+                        for (int u = 0; u < 16; u++) ka[u] = u * 64 + lane < rem ? kc[u * 64 + lane] : __builtin_inff();
+                        const int64_t remb = rem - (int64_t)NW * RP_CH;
+#pragma unroll
+                        for (int u = 0; u < 16; u++)
+                            kb[u] = u * 64 + lane < remb ? kc[(int64_t)NW * RP_CH + u * 64 + lane] : __builtin_inff();
                     }
-                    const float U = suc[c];
-                    int pos = pass ? off + scc[c] : 0;
+#pragma unroll 1
+                    for (int h = 0; h < 2; h++) {
+                        const int c = c2 + h * NW;
+                        if (c >= nch) break;
+                        const float U = suc[c];
+                        int pos = pass ? off + scc[c] : 0;
 #pragma unroll
-                    for (int u = 0; u < 16; u++) {
-                        const int64_t bb = (int64_t)c * RP_CH + u * 64 + lane;
-                        const float lb = qs_key_to_a(metric, kv[u], qi.x) - eps;
-                        const bool in = kv[u] < __builtin_inff() && lb < (c == 0 ? sg0[u] : U);
-                        const uint64_t m = __ballot(in);
-                        if (pass && in) {
-                            const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                            pool_blk[o] = (uint32_t)bb;
-                            pool_lb[o] = lb;
-                            pool_q[o] = li_;
+                        for (int u = 0; u < 16; u++) {
+                            const uint32_t bb = (uint32_t)(c * RP_CH + u * 64 + lane);
+                            const float lb = qs_key_to_a(metric, ka[u], qi.x) - eps;
+                            const bool in = ka[u] < __builtin_inff() && lb < (c == 0 ? sg0[u] : U);
+                            const uint64_t m = __ballot(in);
+                            if (pass && in) {
+                                const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                                pool_blk[o] = (uint32_t)bb;
+                                pool_lb[o] = lb;
+                                pool_q[o] = li_;
+                            }
+                            pos += __popcll(m);
                         }
-                        pos += __popcll(m);
+#pragma unroll
+                        for (int u = 0; u < 16; u++) ka[u] = kb[u];
+                        if (!pass && lane == 0) scc[c] = pos;
                     }
-                    if (!pass && lane == 0) scc[c] = pos;
                 }
             }
             __syncthreads();
@@ -2630,43 +2686,68 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
         const int off = rp_off[li_];
         if (off >= 0) {
             const int tot = rp_tot[li_];
+            // a window of RPW pooled blocks = 512 rows, row e = lane + 64 u of
+            // block e >> 5 held in registers; the next window's rows are read
+            // while this one is tested.  The heap top only falls, so a row at or
+            // above the top at the window's start (heap full) is never inserted
+            // there: a window without such a row is skipped whole, otherwise
+            // lane 0 runs insertToHeap over its candidate rows in id order.
+            uint32_t* sBlk = reinterpret_cast<uint32_t*>(s_d);  // [RPW] block ids of the window
+            float cur[RPW / 2], nxt[RPW / 2];
+            auto load_win = [&](int w0, float (&v)[RPW / 2]) {
+                const int nwin = tot - w0 < RPW ? tot - w0 : RPW;
+#pragma unroll
+                for (int u = 0; u < RPW / 2; u++) {
+                    const int e = lane + 64 * u;
+                    v[u] = (e >> 5) < nwin ? pool_E[(int64_t)(off + w0) * 32 + e] : 0.f;
+                }
+            };
+            if (tot > 0) load_win(0, cur);
             for (int w0 = 0; w0 < tot; w0 += RPW) {
                 const int nwin = tot - w0 < RPW ? tot - w0 : RPW;
-                // the window's distances (independent of the heap state): one load round
-#pragma unroll
-                for (int j = 0; j < RPW / 2; j++) {
-                    const int e = 2 * j + lh;
-                    if (e < nwin) sE[e * 32 + li] = pool_E[(int64_t)(off + w0 + e) * 32 + li];
-                }
+                const bool more = w0 + RPW < tot;
+                if (more) load_win(w0 + RPW, nxt);
                 const uint32_t blk = lane < nwin ? pool_blk[off + w0 + lane] : 0u;
-                const float lb = lane < nwin ? pool_lb[off + w0 + lane] : __builtin_inff();
                 const uint32_t vm = lane < nwin ? pool_vm[off + w0 + lane] : 0u;
-                wave_sync_lds();
-                for (int j = 0; j < nwin; j++) {
-                    const int len = *s_len;
-                    const float top = len > 0 ? hd[0] : 0.f;
-                    const float lbj = __shfl(lb, j);
-                    if (!(len < k || top > lbj)) continue;
-                    const uint32_t vmj = (uint32_t)__shfl((int)vm, j);
-                    const float dist = lane < 32 ? sE[j * 32 + lane] : 0.f;
-                    const bool ok = lane < 32 && ((vmj >> lane) & 1u);
-                    uint64_t mask = __ballot(ok && (len < k || top > dist));
-                    if (mask == 0) continue;
-                    const uint32_t bj = (uint32_t)__shfl((int)blk, j);
+                const int len = *s_len;
+                const bool open = len < k;
+                const float top = len > 0 ? hd[0] : 0.f;
+                uint32_t cb = 0;
+#pragma unroll
+                for (int u = 0; u < RPW / 2; u++) {
+                    const int b = 2 * u + lh;
+                    const uint32_t vmb = (uint32_t)__shfl((int)vm, b);
+                    const bool ok = b < nwin && ((vmb >> li) & 1u);
+                    if (ok && (open || top > cur[u])) cb |= 1u << u;
+                }
+                if (__any(cb != 0)) {
+#pragma unroll
+                    for (int u = 0; u < RPW / 2; u++) sE[lane + 64 * u] = cur[u];
+                    if (lane < RPW) sBlk[lane] = blk;
+                    uint64_t cm[RPW / 2];
+#pragma unroll
+                    for (int u = 0; u < RPW / 2; u++) cm[u] = __ballot((cb >> u) & 1u);
+                    wave_sync_lds();
                     if (lane == 0) {
                         ReplayHeap h{hid, hd, len};
-                        while (mask) {
-                            const int l = __builtin_ctzll(mask);
-                            mask &= mask - 1;
-                            const float dj = sE[j * 32 + l];
-                            const uint64_t idj = id_base + (uint64_t)bj * 32 + (uint64_t)l;
-                            ins(h, idj, dj);
+#pragma unroll
+                        for (int u = 0; u < RPW / 2; u++) {
+                            uint64_t mask = cm[u];
+                            while (mask) {
+                                const int e = 64 * u + __builtin_ctzll(mask);
+                                mask &= mask - 1;
+                                const uint64_t idj = id_base + (uint64_t)sBlk[e >> 5] * 32 + (uint64_t)(e & 31);
+                                ins(h, idj, sE[e]);
+                            }
                         }
                         *s_len = h.len;
                     }
-                    wave_sync_lds();
+                    wave_sync_lds();  // heap state for the next window; sE / sBlk are rewritten there
                 }
-                wave_sync_lds();  // the window buffer is rewritten next
+                if (more) {
+#pragma unroll
+                    for (int u = 0; u < RPW / 2; u++) cur[u] = nxt[u];
+                }
             }
         } else {
             // every block (non-finite values or pool exhausted), distances on the fly

@@ -50,7 +50,7 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
         HIPCHK(idx->rpTot.ensure((size_t)max_list * sizeof(int32_t)));
         HIPCHK(idx->rpCtr.ensure(sizeof(uint32_t)));
         HIPCHK(hipMemsetAsync(idx->rpCtr.p, 0, sizeof(uint32_t), s));
-#define WV_RPB(RSV, M) k_rp_bounds<RSV, M><<<(unsigned)g1, 512, 0, s>>>(key, ldk, nb, eps, qinfo, list, counters, nlist, k, in_d, in_n, idx->qsScratch.as<float>(), idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>(), by_list)
+#define WV_RPB(RSV, M) k_rp_bounds<RSV, M><<<(unsigned)g1, 64 * rp_bounds_nw(RSV), 0, s>>>(key, ldk, nb, eps, qinfo, list, counters, nlist, k, in_d, in_n, idx->qsScratch.as<float>(), idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpOff.as<int32_t>(), idx->rpTot.as<int32_t>(), by_list)
 #define WV_RPBS(M) do { if (RS == 2) WV_RPB(2, M); else if (RS == 4) WV_RPB(4, M); else WV_RPB(8, M); } while (0)
         switch (metric) {
         case L2: WV_RPBS(L2); break;

@@ -1516,6 +1516,51 @@ static void pqa_depths(const wv_index* idx, int64_t nq, int32_t k, const int64_t
         if (modes[q]) m[(size_t)q] = 2.0 * (k + 1) * std::max(1.0, U / (double)std::max<int64_t>(1, off[q + 1] - off[q]));
 }
 
+// the shared block-key launch of a multi-allow batch once the per-query
+// bitmaps (bits, vq words each, ANDed with present) are on the device: union,
+// search_core, results to the host; left = the queries the launch flagged
+// (searched alone by the caller).  Called with idx->mu held.
+static int pqa_run(wv_index* idx, hipStream_t s, const float* queries, int64_t nq, int64_t d, int32_t k, int64_t vq,
+                   uint32_t* bits, uint64_t* out_ids, float* out_dists, int32_t* out_counts,
+                   std::vector<int64_t>& left) {
+    uint32_t* uni = idx->pqaUnion.as<uint32_t>();
+    HIPCHK(hipMemsetAsync(uni, 0, (size_t)std::max<int64_t>(idx->cap / 32, vq) * sizeof(uint32_t), s));
+    k_pqa_union<<<(unsigned)((vq + 255) / 256), 256, 0, s>>>(bits, vq, nq, uni);
+    HIPCHK(hipGetLastError());
+    HIPCHK(idx->qraw.ensure((size_t)nq * d * sizeof(float)));
+    HIPCHK(idx->oIds.ensure((size_t)nq * k * sizeof(uint64_t)));
+    HIPCHK(idx->oD.ensure((size_t)nq * k * sizeof(float)));
+    HIPCHK(idx->oN.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
+    idx->stats.last_scan_rows = (uint64_t)idx->hiwater;
+    idx->pqa_valid = bits;
+    idx->pqa_vq = vq;
+    idx->pqa_m = idx->pqaM.as<int32_t>();
+    // the queries the shared launch leaves unresolved (flags) are searched
+    // alone afterwards (a sparse list's own gathered sub-index or window)
+    // instead of by the one-wave replay inside the launch, which walks every
+    // block key of the union for one query (35 ms at 1M rows, 2 % lists)
+    HIPCHK(idx->oF.ensure((size_t)nq * sizeof(int32_t)));
+    int32_t* dflags = idx->pqa_alone ? idx->oF.as<int32_t>() : nullptr;
+    int rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, uni, idx->npresent, idx->oIds.as<uint64_t>(),
+                         idx->oD.as<float>(), idx->oN.as<int32_t>(), dflags);
+    idx->pqa_valid = nullptr;
+    idx->pqa_vq = 0;
+    idx->pqa_m = nullptr;
+    if (rc) return rc;
+    std::vector<int32_t> hf(dflags ? (size_t)nq : 0);
+    HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_counts, idx->oN.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (dflags) HIPCHK(hipMemcpyAsync(hf.data(), dflags, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int64_t q = 0; q < (int64_t)hf.size(); q++)
+        if (hf[(size_t)q]) left.push_back(q);
+    idx->stats.replayed_queries += (uint64_t)left.size();
+    return WV_OK;
+}
+
+
 static thread_local bool t_pqa_nosplit = false;
 
 extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const float* queries, int64_t nq, int64_t d,
@@ -1661,45 +1706,107 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
                                                                   idx->id_base, idx->hiwater, idx->present, vq, bits);
         HIPCHK(hipGetLastError());
     }
-    uint32_t* uni = idx->pqaUnion.as<uint32_t>();
-    HIPCHK(hipMemsetAsync(uni, 0, (size_t)std::max<int64_t>(idx->cap / 32, vq) * sizeof(uint32_t), s));
-    k_pqa_union<<<(unsigned)((vq + 255) / 256), 256, 0, s>>>(bits, vq, nq, uni);
-    HIPCHK(hipGetLastError());
-    HIPCHK(idx->qraw.ensure((size_t)nq * d * sizeof(float)));
-    HIPCHK(idx->oIds.ensure((size_t)nq * k * sizeof(uint64_t)));
-    HIPCHK(idx->oD.ensure((size_t)nq * k * sizeof(float)));
-    HIPCHK(idx->oN.ensure((size_t)nq * sizeof(int32_t)));
-    HIPCHK(hipMemcpyAsync(idx->qraw.p, queries, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, s));
-    idx->stats.last_scan_rows = (uint64_t)idx->hiwater;
-    idx->pqa_valid = bits;
-    idx->pqa_vq = vq;
-    idx->pqa_m = idx->pqaM.as<int32_t>();
-    // the queries the shared launch leaves unresolved (flags) are searched
-    // alone afterwards (a sparse list's own gathered sub-index or window)
-    // instead of by the one-wave replay inside the launch, which walks every
-    // block key of the union for one query (35 ms at 1M rows, 2 % lists)
-    HIPCHK(idx->oF.ensure((size_t)nq * sizeof(int32_t)));
-    int32_t* dflags = idx->pqa_alone ? idx->oF.as<int32_t>() : nullptr;
-    int rc = search_core(idx, s, idx->qraw.as<float>(), nq, d, k, 0, uni, idx->npresent, idx->oIds.as<uint64_t>(),
-                         idx->oD.as<float>(), idx->oN.as<int32_t>(), dflags);
-    idx->pqa_valid = nullptr;
-    idx->pqa_vq = 0;
-    idx->pqa_m = nullptr;
-    if (rc) return rc;
-    std::vector<int32_t> hf(dflags ? (size_t)nq : 0);
-    HIPCHK(hipMemcpyAsync(out_ids, idx->oIds.p, (size_t)nq * k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(out_dists, idx->oD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(out_counts, idx->oN.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    if (dflags) HIPCHK(hipMemcpyAsync(hf.data(), dflags, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
     std::vector<int64_t> left;
-    for (int64_t q = 0; q < (int64_t)hf.size(); q++)
-        if (hf[(size_t)q]) left.push_back(q);
-    if (left.empty()) return WV_OK;
-    idx->stats.replayed_queries += (uint64_t)left.size();
+    int rc = pqa_run(idx, s, queries, nq, d, k, vq, bits, out_ids, out_dists, out_counts, left);
+    if (rc || left.empty()) return rc;
     g.unlock();
     return multi_allow_subset(idx, queries, d, k, allow_ids, allow_offsets, allow_modes, left, false, out_ids, out_dists,
                               out_counts);
+}
+
+// bitmap allow lists -> id lists (absolute doc ids), for the paths that take lists
+static void bits_to_lists(const uint32_t* bits, int64_t words, const int32_t* modes, int64_t nq,
+                          std::vector<uint64_t>& ids, std::vector<int64_t>& off) {
+    ids.clear();
+    off.assign((size_t)nq + 1, 0);
+    for (int64_t q = 0; q < nq; q++) {
+        if (modes[q])
+            for (int64_t w = 0; w < words; w++)
+                for (uint32_t v = bits[q * words + w]; v; v &= v - 1)
+                    ids.push_back((uint64_t)(w * 32 + __builtin_ctz(v)));
+        off[(size_t)q + 1] = (int64_t)ids.size();
+    }
+    ids.push_back(0);
+}
+
+extern "C" int wv_index_search_by_vector_batch_multi_allow_bitmap(wv_index* idx, const float* queries, int64_t nq,
+                                                                  int64_t d, int32_t k, const uint32_t* allow_bits,
+                                                                  int64_t words, const int32_t* allow_modes,
+                                                                  uint64_t* out_ids, float* out_dists,
+                                                                  int32_t* out_counts) {
+    if (!idx) return set_err(WV_ERR_INVALID, "nil index");
+    if (nq < 0) return set_err(WV_ERR_INVALID, "negative batch");
+    if (nq == 0) return WV_OK;
+    if (words < 0) return set_err(WV_ERR_INVALID, "negative bitmap words");
+    if (!allow_modes || !out_counts || (d > 0 && !queries)) return set_err(WV_ERR_INVALID, "nil argument");
+    bool listed = false;
+    for (int64_t q = 0; q < nq; q++) {
+        if (allow_modes[q] != 0 && allow_modes[q] != 1) return set_err(WV_ERR_INVALID, "allow mode %d", allow_modes[q]);
+        listed |= allow_modes[q] == 1;
+    }
+    if (listed && words > 0 && !allow_bits) return set_err(WV_ERR_INVALID, "nil allow bitmap");
+    // list sizes (the select depths) from the bitmaps
+    std::vector<int64_t> off((size_t)nq + 1, 0);
+    for (int64_t q = 0; q < nq; q++) {
+        int64_t c = 0;
+        if (allow_modes[q])
+            for (int64_t w = 0; w < words; w++) c += __builtin_popcount(allow_bits[q * words + w]);
+        off[(size_t)q + 1] = off[(size_t)q] + c;
+    }
+    auto by_lists = [&](std::unique_lock<std::mutex>& g, const std::vector<int64_t>* qs) -> int {
+        g.unlock();
+        std::vector<uint64_t> ids;
+        std::vector<int64_t> lo;
+        bits_to_lists(allow_bits, words, allow_modes, nq, ids, lo);
+        if (!qs)
+            return wv_index_search_by_vector_batch_multi_allow(idx, queries, nq, d, k, ids.data(), lo.data(),
+                                                               allow_modes, out_ids, out_dists, out_counts);
+        return multi_allow_subset(idx, queries, d, k, ids.data(), lo.data(), allow_modes, *qs, false, out_ids, out_dists,
+                                  out_counts);
+    };
+    std::unique_lock<std::mutex> g(idx->mu);
+    const int64_t vq = round_up(std::max<int64_t>(idx->hiwater, 1), 256) / 32;
+    const int64_t sw = vq + 1;  // raw words per query: the slot window plus the shift's spill word
+    const int64_t qmax = std::max<int64_t>(1, (idx->pqa_budget_mb << 20) / (vq * (int64_t)sizeof(uint32_t) * 2));
+    const bool fast = idx->pqa && nq > 1 && idx->compression == WV_COMPRESSION_NONE && !idx->rq_bits &&
+                      idx->dims != 0 && d == idx->dims && k > 0 && idx->npresent > 0 && qs_route(idx, k) && nq <= qmax;
+    std::vector<double> md;
+    if (fast) pqa_depths(idx, nq, k, off.data(), allow_modes, md);
+    bool split = false;
+    if (fast) {  // the id-list call's split of too-sparse lists (see there)
+        int64_t nsp = 0;
+        for (int64_t q = 0; q < nq; q++) nsp += md[(size_t)q] > 960.0;
+        split = nsp > 0 && nsp <= idx->pqa_split_max && nsp < nq;
+    }
+    if (!fast || split) return by_lists(g, nullptr);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = idx->stream;
+    std::vector<int32_t> hm((size_t)nq);
+    for (int64_t q = 0; q < nq; q++) hm[(size_t)q] = (int32_t)std::min(960.0, std::ceil(md[(size_t)q]));
+    idx->pqa_R = *std::max_element(hm.begin(), hm.end()) > 448 ? 16 : 8;
+    HIPCHK(idx->pqaM.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(idx->pqaM.p, hm.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIPCHK(idx->pqaBits.ensure((size_t)(nq * vq) * sizeof(uint32_t)));
+    HIPCHK(idx->pqaUnion.ensure((size_t)std::max<int64_t>(idx->cap / 32, vq) * sizeof(uint32_t)));
+    HIPCHK(idx->pqaQ.ensure((size_t)(nq + 1) * sizeof(int32_t)));
+    // the callers' words from doc id id_base & ~31 on: one strided copy (pqaIds holds them here)
+    const int64_t b0 = (int64_t)(idx->id_base >> 5);
+    const int64_t avail = std::max<int64_t>(0, std::min<int64_t>(sw, words - b0));
+    HIPCHK(idx->pqaIds.ensure((size_t)(nq * sw) * sizeof(uint32_t) + 8));
+    uint32_t* raw = reinterpret_cast<uint32_t*>(idx->pqaIds.p);
+    if (avail > 0)
+        HIPCHK(hipMemcpy2DAsync(raw, (size_t)sw * sizeof(uint32_t), allow_bits + b0, (size_t)words * sizeof(uint32_t),
+                                (size_t)avail * sizeof(uint32_t), (size_t)nq, hipMemcpyHostToDevice, s));
+    int32_t* d_modes = idx->pqaQ.as<int32_t>();
+    HIPCHK(hipMemcpyAsync(d_modes, allow_modes, (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    uint32_t* bits = idx->pqaBits.as<uint32_t>();
+    k_pqa_from_bits<<<(unsigned)std::min<int64_t>((nq * vq + 255) / 256, 8192), 256, 0, s>>>(
+        raw, sw, avail, d_modes, nq, (int)(idx->id_base & 31), idx->present, vq, bits);
+    HIPCHK(hipGetLastError());
+    std::vector<int64_t> left;
+    int rc = pqa_run(idx, s, queries, nq, d, k, vq, bits, out_ids, out_dists, out_counts, left);
+    if (rc || left.empty()) return rc;
+    return by_lists(g, &left);
 }
 
 extern "C" int wv_index_hnsw_flat_search(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,

@@ -398,11 +398,12 @@ class FlatIndex:
                                                       _fptr(dists), _iptr(counts)))
         return ids, dists, counts
 
-    def search_by_vector_batch_multi_allow(self, queries, k: int, allows):
+    def search_by_vector_batch_multi_allow(self, queries, k: int, allows, bitmap: bool = False):
         """SearchByVector for each row of `queries`, row i under its own allow
         list allows[i] (None = unfiltered): one batched call
-        (wv_index_search_by_vector_batch_multi_allow), results equal to
-        per-row search_by_vector_batch calls.
+        (wv_index_search_by_vector_batch_multi_allow, or with bitmap=True the
+        lists as dense doc-id bitmaps, ..._multi_allow_bitmap), results equal
+        to per-row search_by_vector_batch calls.
         Returns (ids[nq,k] uint64, dists[nq,k] float32, counts[nq] int32)."""
         q = np.ascontiguousarray(queries, dtype=np.float32)
         if q.ndim == 1:
@@ -416,6 +417,18 @@ class FlatIndex:
         dists = np.zeros((nq, kk), dtype=np.float32)
         counts = np.zeros(nq, dtype=np.int32)
         modes = np.array([0 if a is None else 1 for a in allows], dtype=np.int32)
+        if bitmap:
+            top = max([int(a.ids.max()) + 1 for a in allows if a is not None and a.ids.size] + [1])
+            words = (top + 31) // 32
+            bits = np.zeros((nq, words), dtype=np.uint32)
+            for i, a in enumerate(allows):
+                if a is not None and a.ids.size:
+                    v = np.asarray(a.ids, dtype=np.uint64)
+                    np.bitwise_or.at(bits[i], (v >> 5).astype(np.int64), (np.uint32(1) << (v & 31).astype(np.uint32)))
+            check(self._l.wv_index_search_by_vector_batch_multi_allow_bitmap(
+                self._h, _fptr(q), nq, d, int(k), bits.ctypes.data_as(C.c_void_p), words, _iptr(modes), _uptr(ids),
+                _fptr(dists), _iptr(counts)))
+            return ids, dists, counts
         parts = [np.asarray(a.ids, dtype=np.uint64) for a in allows if a is not None]
         aids = np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros(1, np.uint64), dtype=np.uint64)
         off = np.zeros(nq + 1, dtype=np.int64)
