@@ -101,6 +101,31 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
 
 static void* batch_pinned_alloc(size_t bytes) { return malloc(bytes); }
 static void batch_pinned_free(void* p) { free(p); }
+static uint32_t* batch_row_alloc(int64_t words, const uint32_t** dev) {
+    uint32_t* p = static_cast<uint32_t*>(malloc((size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t)));
+    *dev = p;
+    return p;
+}
+static void batch_row_free(uint32_t* p) { free(p); }
+static uint64_t batch_id_base(const wv_index*) { return 0; }
+
+#include "../weaviate_amd/csrc/batch_row.h"
+// the slot-bitmap batch: rows back to id lists, then query by query
+static int batch_search_slot_bitmaps(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
+                                     const wv_batch_row* rows, uint64_t* out_ids, float* out_dists,
+                                     int32_t* out_counts) {
+    for (int64_t q = 0; q < nq; q++) {
+        std::vector<uint64_t> ids;
+        for (int64_t w = 0; w < rows[q].words; w++)
+            for (uint32_t v = rows[q].host[w]; v; v &= v - 1) ids.push_back((uint64_t)(w * 32 + __builtin_ctz(v)));
+        ids.push_back(0);
+        const int rc = wv_index_search_by_vector_batch(idx, queries + q * d, 1, d, k, ids.data(),
+                                                       (int64_t)ids.size() - 1, 1, out_ids + q * k, out_dists + q * k,
+                                                       out_counts + q);
+        if (rc) return rc;
+    }
+    return WV_OK;
+}
 
 #include "../weaviate_amd/csrc/batcher.hip"
 
@@ -138,9 +163,13 @@ int main(int argc, char** argv) {
                 for (float& x : q) x = V(r);
                 std::vector<uint64_t> allow;
                 int32_t mode = 0;
-                if (kind == 6) {  // an allow list: batched through the per-query-list entry point
+                if (kind == 6) {  // a dense allow list: its slot bitmap built by this caller
                     mode = 1;
                     for (int i = 0; i < 40; i++) allow.push_back(r() % (uint64_t)idx.n);
+                } else if (kind == 5) {  // a sparse one (ids kept; a bitmap batch gets the leader's row)
+                    mode = 1;
+                    for (int i = 0; i < 3; i++) allow.push_back(r() % (uint64_t)idx.n);
+                    if (c % 5 == 0) allow.push_back(1ull << 40);  // an id past any slot
                 }
                 std::vector<uint64_t> ids((size_t)k);
                 std::vector<float> dd((size_t)k);

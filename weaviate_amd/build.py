@@ -17,7 +17,7 @@ UNITS = ["runtime.hip", "qs_runtime.hip", "qs_exact.hip", "qs_replay.hip", "quan
 SOURCES = [os.path.join(HERE, "csrc", f) for f in (
     "runtime.hip", "qs_runtime.hip", "qs_exact.hip", "qs_replay.hip", "quant_runtime.hip", "multi.hip", "rt_index.h", "kernels.hip", "bq_kernels.hip",
     "pq_kernels.hip", "kernels_bf3.hip", "rq_kernels.hip", "lsm_segment.hip", "batcher.hip", "gemv_kernels.hip",
-    "qs_kernels.hip", "q8_kernels.hip", "sq_kernels.hip", "vector_index.hip", "wv_device.h", "rq8_mfma.hip")] + [os.path.join(REPO, "include", "wv_knn.h")]
+    "qs_kernels.hip", "q8_kernels.hip", "sq_kernels.hip", "vector_index.hip", "wv_device.h", "rq8_mfma.hip", "batch_row.h")] + [os.path.join(REPO, "include", "wv_knn.h")]
 OBJDIR = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [

@@ -17,6 +17,8 @@
 #include <chrono>
 #include <condition_variable>
 
+#include "batch_row.h"
+
 struct wv_batch_req {
     const float* q;
     int64_t d;
@@ -30,12 +32,19 @@ struct wv_batch_req {
     int rc = WV_OK;
     std::string err;
     bool done = false;
+    wv_batch_row row{};   // the list as a slot bitmap (row.host != nullptr), built by the caller
+    int64_t row_cap = 0;
 };
 
 // page-locked host memory for the leader's concatenated allow lists (defined
 // by the including unit: hipHostMalloc in the library, malloc in the TSan mock)
 static void* batch_pinned_alloc(size_t bytes);
 static void batch_pinned_free(void* p);
+// page-locked rows kernels read in place (*dev), the allow bitmaps; and the
+// batch search over them (batch_search_slot_bitmaps, defined by the includer)
+static uint32_t* batch_row_alloc(int64_t words, const uint32_t** dev);
+static void batch_row_free(uint32_t* p);
+static uint64_t batch_id_base(const wv_index* idx);
 
 struct wv_batcher {
     std::mutex m;
@@ -49,11 +58,64 @@ struct wv_batcher {
     std::vector<wv_batch_req*> pending;
     bool busy = false, in_window = false;
     int64_t calls = 0, launches = 0, max_batch_seen = 0;
+    // free bitmap rows (page-locked, reused: allocating page-locked memory per
+    // call would cost more than the list)
+    struct Row { uint32_t* h; const uint32_t* d; int64_t cap; };
+    std::vector<Row> rows_free;
 };
 
 static void batcher_free(wv_batcher* b) {
     if (b && b->pin) batch_pinned_free(b->pin);
+    if (b)
+        for (auto& r : b->rows_free) batch_row_free(r.h);
     delete b;
+}
+
+// A list as a slot bitmap when that is the smaller form (8-byte ids against
+// one bit per slot up to the largest listed slot: lists above ~1/64 of the
+// span), in a pooled page-locked row.  False: keep the id list.
+static bool build_row(wv_batcher* b, uint64_t id_base, const uint64_t* ids, int64_t n, wv_batch_row* row,
+                      int64_t* cap, bool force = false) {
+    if (n <= 0) return false;
+    constexpr uint64_t kSlots = 1ull << 36;  // beyond any index's capacity: such ids are never present
+    uint64_t top = 0;
+    bool any = false;
+    for (int64_t i = 0; i < n; i++)
+        if (ids[i] >= id_base && ids[i] - id_base < kSlots) { top = std::max<uint64_t>(top, ids[i] - id_base); any = true; }
+    const int64_t words = (int64_t)(top >> 5) + 1;
+    if (!force && (!any || 2 * n <= words)) return false;
+    wv_batcher::Row r{nullptr, nullptr, 0};
+    {
+        std::lock_guard<std::mutex> g(b->m);
+        for (size_t i = 0; i < b->rows_free.size(); i++)
+            if (b->rows_free[i].cap >= words) {
+                r = b->rows_free[i];
+                b->rows_free.erase(b->rows_free.begin() + (std::ptrdiff_t)i);
+                break;
+            }
+    }
+    if (!r.h) {
+        r.cap = (words + 1023) / 1024 * 1024;
+        r.h = batch_row_alloc(r.cap, &r.d);
+        if (!r.h) return false;
+    }
+    memset(r.h, 0, (size_t)words * sizeof(uint32_t));
+    for (int64_t i = 0; i < n; i++)
+        if (ids[i] >= id_base && ids[i] - id_base < kSlots) {
+            const uint64_t sl = ids[i] - id_base;
+            r.h[sl >> 5] |= 1u << (sl & 31);
+        }
+    *row = wv_batch_row{r.d, r.h, words, n};
+    *cap = r.cap;
+    return true;
+}
+
+static void release_row(wv_batcher* b, wv_batch_row* row, int64_t cap) {
+    if (!row->host) return;
+    std::lock_guard<std::mutex> g(b->m);
+    if (b->rows_free.size() < 1024) b->rows_free.push_back({const_cast<uint32_t*>(row->host), row->dev, cap});
+    else batch_row_free(const_cast<uint32_t*>(row->host));
+    row->host = nullptr;
 }
 
 static wv_batcher* get_batcher(wv_index* idx) {
@@ -83,6 +145,29 @@ static int launch_requests(wv_index* idx, wv_batcher* b, const std::vector<wv_ba
     if (!lists || n == 1) {
         rc = wv_index_search_by_vector_batch(idx, q.data(), n, d, k, grp[0]->allow_ids, grp[0]->n_allow,
                                              grp[0]->allow_mode, ids.data(), dists.data(), cnt.data());
+    } else if (std::any_of(grp.begin(), grp.end(), [](wv_batch_req* r) { return r->row.host != nullptr; })) {
+        // the lists as slot bitmaps read in place by the device: the callers
+        // built theirs; the leader builds the (sparse) rest
+        std::vector<wv_batch_row> rows((size_t)n);
+        std::vector<std::pair<wv_batch_row, int64_t>> mine;
+        rc = WV_OK;
+        for (int64_t i = 0; i < n && !rc; i++) {
+            wv_batch_req* r = grp[i];
+            if (r->row.host) { rows[(size_t)i] = r->row; continue; }
+            wv_batch_row row{nullptr, nullptr, 0, r->n_allow};
+            int64_t cap = 0;
+            if (r->n_allow > 0) {  // a sparse list: a row of its own all the same
+                if (!build_row(b, batch_id_base(idx), r->allow_ids, r->n_allow, &row, &cap, true)) {
+                    rc = set_err(WV_ERR_INVALID, "out of host memory for the batch's allow bitmaps");
+                    break;
+                }
+                mine.push_back({row, cap});
+            }
+            rows[(size_t)i] = row;
+        }
+        if (!rc)
+            rc = batch_search_slot_bitmaps(idx, q.data(), n, d, k, rows.data(), ids.data(), dists.data(), cnt.data());
+        for (auto& m : mine) release_row(b, &m.first, m.second);
     } else {
         std::vector<int64_t> off((size_t)n + 1, 0);
         std::vector<int32_t> modes((size_t)n);
@@ -168,6 +253,9 @@ extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int6
     if (allow_mode == 1 && (n_allow < 0 || (n_allow > 0 && !allow_ids))) return set_err(WV_ERR_INVALID, "nil allow ids");
     wv_batcher* b = get_batcher(idx);
     wv_batch_req req{query, d, k, allow_ids, n_allow, allow_mode, out_ids, out_dists, out_count};
+    // a dense list: its slot bitmap, built here (in parallel with the other
+    // callers) instead of by the leader
+    if (allow_mode == 1 && n_allow > 0) build_row(b, batch_id_base(idx), allow_ids, n_allow, &req.row, &req.row_cap);
     std::unique_lock<std::mutex> lk(b->m);
     b->calls++;
     b->pending.push_back(&req);
@@ -201,6 +289,8 @@ extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int6
             b->cv.wait(lk);
         }
     }
+    lk.unlock();
+    release_row(b, &req.row, req.row_cap);
     if (req.rc) return set_err(req.rc, "%s", req.err.c_str());
     return WV_OK;
 }

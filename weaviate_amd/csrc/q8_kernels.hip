@@ -23,6 +23,7 @@
 // one-block schedule carry over: a 64-column i8 MFMA chunk is a 32-column
 // bf16 chunk's bytes.
 #pragma once
+#include "batch_row.h"
 
 namespace wv {
 namespace {
@@ -104,6 +105,20 @@ __global__ void k_pqa_from_bits(const uint32_t* __restrict__ raw, int64_t sw, in
             const uint32_t lo = w < avail ? r[w] : 0u, hi = w + 1 < avail ? r[w + 1] : 0u;
             v &= sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
         }
+        bits[i] = v;
+    }
+}
+
+// per-query bitmaps from the micro-batcher's slot-bitmap rows (batch_row.h),
+// read in place from page-locked host memory; ANDed with present.  Thread per
+// (query, word).
+__global__ void k_pqa_from_rows(const wv_batch_row* __restrict__ rows, const int32_t* __restrict__ modes, int64_t nq,
+                                const uint32_t* __restrict__ present, int64_t vq, uint32_t* __restrict__ bits) {
+    const int64_t n = nq * vq;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = i / vq, w = i - q * vq;
+        uint32_t v = present[w];
+        if (modes[q]) v &= w < rows[q].words ? rows[q].dev[w] : 0u;
         bits[i] = v;
     }
 }

@@ -2368,7 +2368,7 @@ __global__ __launch_bounds__(512) void k_blk_replay_par(const float* __restrict_
 // A query whose candidates do not fit the pool, or with non-finite values,
 // replays every block with on-the-fly distances in k_rp_heap.
 // ---------------------------------------------------------------------------
-constexpr int RPW = 16;  // k_rp_heap window (blocks)
+constexpr int RPW = 64;  // k_rp_heap window (blocks)
 
 // element e of a wave-sorted list of RS rows (broadcast)
 template <int RS>
@@ -2558,7 +2558,7 @@ __global__ __launch_bounds__(64 * rp_bounds_nw(RS)) void k_rp_bounds(const float
                                 const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
                                 pool_blk[o] = (uint32_t)bb;
-                                pool_lb[o] = lb;
+                                pool_lb[o] = c == 0 ? sg0[u] : U;  // the heap top's bound at this block
                                 pool_q[o] = li_;
                             }
                             pos += __popcll(m);
@@ -2600,11 +2600,15 @@ __global__ __launch_bounds__(64 * rp_bounds_nw(RS)) void k_rp_bounds(const float
     }
 }
 
-// exact distances of the pooled blocks' rows: pool_E[e][32], valid masks pool_vm[e]
+// exact distances of the pooled blocks' rows: pool_E[e][32], and in pool_vm[e]
+// the rows that can enter the heap: valid and E < pool_ub[e], the bound of the
+// heap top at that block (k_rp_bounds; +inf: the heap may still be short, every
+// valid row)
 template <int METRIC, int VARIANT>
 __global__ __launch_bounds__(256) void k_rp_exact(const float* __restrict__ X, int dpad, const uint32_t* __restrict__ valid,
                                                   int64_t nrows, const float* __restrict__ Qn, int d,
                                                   const int32_t* __restrict__ qlist, const uint32_t* __restrict__ pool_blk,
+                                                  const float* __restrict__ pool_ub,
                                                   const int32_t* __restrict__ pool_q, const uint32_t* __restrict__ pool_ctr,
                                                   int64_t pool_cap, float* __restrict__ pool_E,
                                                   uint32_t* __restrict__ pool_vm, int64_t vq = 0) {
@@ -2626,6 +2630,8 @@ __global__ __launch_bounds__(256) void k_rp_exact(const float* __restrict__ X, i
                 ok = row < nrows && ((vrow[row >> 5] >> (row & 31)) & 1u);
                 if (ok) dist = exact_dist<METRIC, VARIANT>(Qn + (int64_t)q * dpad, X + row * dpad, d);
                 pool_E[e * 32 + li] = dist;
+                const float ub = pool_ub[e];
+                ok = ok && (dist < ub || !(ub < __builtin_inff()));
             }
         }
         const uint64_t m = __ballot(ok);
@@ -2654,7 +2660,8 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
     float* hd = reinterpret_cast<float*>(hid + k);
     float* s_d = hd + k;                 // [64]
     float* sE = s_d + 64;                // [RPW][32]
-    int* s_len = reinterpret_cast<int*>(sE + RPW * 32);
+    uint64_t* sM = reinterpret_cast<uint64_t*>(((uintptr_t)(sE + RPW * 32) + 7) & ~(uintptr_t)7);  // [RPW / 2]
+    int* s_len = reinterpret_cast<int*>(sM + RPW / 2);
     const int lane = threadIdx.x;
     const int metric = METRIC == COSINE ? COSINE : METRIC == DOT ? DOT : L2;
     const int count = counters ? (int)counters[1] : nlist;
@@ -2686,12 +2693,13 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
         const int off = rp_off[li_];
         if (off >= 0) {
             const int tot = rp_tot[li_];
-            // a window of RPW pooled blocks = 512 rows, row e = lane + 64 u of
-            // block e >> 5 held in registers; the next window's rows are read
-            // while this one is tested.  The heap top only falls, so a row at or
-            // above the top at the window's start (heap full) is never inserted
-            // there: a window without such a row is skipped whole, otherwise
-            // lane 0 runs insertToHeap over its candidate rows in id order.
+            // a window of RPW = 64 pooled blocks = 2048 rows, row e = lane + 64 u
+            // of block e >> 5 held in registers; the next window's rows are read
+            // while this one is tested.  pool_vm holds only the rows under the
+            // bound of the heap top at their block (k_rp_exact), and the top only
+            // falls: a window with no such row under the top at its start (heap
+            // full) is skipped whole, otherwise lane 0 runs insertToHeap over its
+            // candidate rows in id order.
             uint32_t* sBlk = reinterpret_cast<uint32_t*>(s_d);  // [RPW] block ids of the window
             float cur[RPW / 2], nxt[RPW / 2];
             auto load_win = [&](int w0, float (&v)[RPW / 2]) {
@@ -2709,40 +2717,41 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
                 if (more) load_win(w0 + RPW, nxt);
                 const uint32_t blk = lane < nwin ? pool_blk[off + w0 + lane] : 0u;
                 const uint32_t vm = lane < nwin ? pool_vm[off + w0 + lane] : 0u;
-                const int len = *s_len;
-                const bool open = len < k;
-                const float top = len > 0 ? hd[0] : 0.f;
-                uint32_t cb = 0;
+                if (__any(vm != 0u)) {
+                    const int len = *s_len;
+                    const bool open = len < k;
+                    const float top = len > 0 ? hd[0] : 0.f;
+                    uint32_t cb = 0;
 #pragma unroll
-                for (int u = 0; u < RPW / 2; u++) {
-                    const int b = 2 * u + lh;
-                    const uint32_t vmb = (uint32_t)__shfl((int)vm, b);
-                    const bool ok = b < nwin && ((vmb >> li) & 1u);
-                    if (ok && (open || top > cur[u])) cb |= 1u << u;
-                }
-                if (__any(cb != 0)) {
+                    for (int u = 0; u < RPW / 2; u++) {
+                        const uint32_t vmb = (uint32_t)__shfl((int)vm, 2 * u + lh);
+                        if (((vmb >> li) & 1u) && (open || top > cur[u])) cb |= 1u << u;
+                    }
+                    if (__any(cb != 0)) {
 #pragma unroll
-                    for (int u = 0; u < RPW / 2; u++) sE[lane + 64 * u] = cur[u];
-                    if (lane < RPW) sBlk[lane] = blk;
-                    uint64_t cm[RPW / 2];
-#pragma unroll
-                    for (int u = 0; u < RPW / 2; u++) cm[u] = __ballot((cb >> u) & 1u);
-                    wave_sync_lds();
-                    if (lane == 0) {
-                        ReplayHeap h{hid, hd, len};
+                        for (int u = 0; u < RPW / 2; u++) sE[lane + 64 * u] = cur[u];
+                        sBlk[lane] = blk;
 #pragma unroll
                         for (int u = 0; u < RPW / 2; u++) {
-                            uint64_t mask = cm[u];
-                            while (mask) {
-                                const int e = 64 * u + __builtin_ctzll(mask);
-                                mask &= mask - 1;
-                                const uint64_t idj = id_base + (uint64_t)sBlk[e >> 5] * 32 + (uint64_t)(e & 31);
-                                ins(h, idj, sE[e]);
-                            }
+                            const uint64_t m = __ballot((cb >> u) & 1u);
+                            if (lane == 0) sM[u] = m;
                         }
-                        *s_len = h.len;
+                        wave_sync_lds();
+                        if (lane == 0) {
+                            ReplayHeap h{hid, hd, len};
+                            for (int u = 0; u < RPW / 2; u++) {
+                                uint64_t mask = sM[u];
+                                while (mask) {
+                                    const int e = 64 * u + __builtin_ctzll(mask);
+                                    mask &= mask - 1;
+                                    const uint64_t idj = id_base + (uint64_t)sBlk[e >> 5] * 32 + (uint64_t)(e & 31);
+                                    ins(h, idj, sE[e]);
+                                }
+                            }
+                            *s_len = h.len;
+                        }
+                        wave_sync_lds();  // heap state for the next window; sE / sBlk / sM are rewritten there
                     }
-                    wave_sync_lds();  // heap state for the next window; sE / sBlk are rewritten there
                 }
                 if (more) {
 #pragma unroll

@@ -60,7 +60,7 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
 #undef WV_RPBS
 #undef WV_RPB
         HIPCHK(hipGetLastError());
-#define WV_RPE(M, V) k_rp_exact<M, V><<<1024, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, idx->rpBlk.as<uint32_t>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpE.as<float>(), idx->rpVm.as<uint32_t>(), idx->cur_vq)
+#define WV_RPE(M, V) k_rp_exact<M, V><<<1024, 256, 0, s>>>(idx->X, idx->dpad, valid, idx->hiwater, Qn, idx->dims, list, idx->rpBlk.as<uint32_t>(), idx->rpLb.as<float>(), idx->rpQ.as<int32_t>(), idx->rpCtr.as<uint32_t>(), pool_cap, idx->rpE.as<float>(), idx->rpVm.as<uint32_t>(), idx->cur_vq)
         switch (metric) {
         case L2: if (v5) WV_RPE(L2, AVX512); else WV_RPE(L2, AVX256); break;
         case DOT: if (v5) WV_RPE(DOT, AVX512); else WV_RPE(DOT, AVX256); break;
@@ -68,7 +68,7 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
         }
 #undef WV_RPE
         HIPCHK(hipGetLastError());
-        const size_t hlds = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 64 * sizeof(float) + RPW * 32 * sizeof(float) + 16;
+        const size_t hlds = (size_t)k * (sizeof(uint64_t) + sizeof(float)) + 64 * sizeof(float) + RPW * 32 * sizeof(float) + 8 + (RPW / 2) * sizeof(uint64_t) + 16;
         const int64_t g3 = std::min<int64_t>(max_list, 2048);
 #define WV_RPH(M, V)                                                                                            \
     do {                                                                                                        \

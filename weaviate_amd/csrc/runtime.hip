@@ -11,6 +11,7 @@
 // cap is a multiple of 128 (the MFMA tile) so tiles never read out of bounds.
 #include "rt_index.h"
 #include <cpuid.h>
+#include <functional>
 #include <map>
 
 // ---------------------------------------------------------------------------
@@ -1716,17 +1717,78 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
 
 // bitmap allow lists -> id lists (absolute doc ids), for the paths that take lists
 static void bits_to_lists(const uint32_t* bits, int64_t words, const int32_t* modes, int64_t nq,
-                          std::vector<uint64_t>& ids, std::vector<int64_t>& off) {
+                          std::vector<uint64_t>& ids, std::vector<int64_t>& off, const std::vector<char>* want) {
     ids.clear();
     off.assign((size_t)nq + 1, 0);
     for (int64_t q = 0; q < nq; q++) {
-        if (modes[q])
+        if (modes[q] && (!want || (*want)[(size_t)q]))
             for (int64_t w = 0; w < words; w++)
                 for (uint32_t v = bits[q * words + w]; v; v &= v - 1)
                     ids.push_back((uint64_t)(w * 32 + __builtin_ctz(v)));
         off[(size_t)q + 1] = (int64_t)ids.size();
     }
     ids.push_back(0);
+}
+
+// The shared multi-allow launch from per-query bitmaps, whatever their host
+// form: off = the lists' size prefix sums (the select depths), fill writes the
+// per-query device bitmaps (vq words each, ANDed with present), lists gives
+// the same lists as ids (the paths that take id lists: a batch the shared
+// launch does not serve, a split of too-sparse lists, the flagged queries).
+// Called with g holding idx->mu; returns with it released or held.
+typedef std::function<int(hipStream_t, int64_t, uint32_t*, const int32_t*)> PqaFill;
+typedef std::function<void(std::vector<uint64_t>&, std::vector<int64_t>&, const std::vector<char>*)> PqaLists;
+static int pqa_bitmap_core(wv_index* idx, std::unique_lock<std::mutex>& g, const float* queries, int64_t nq, int64_t d,
+                           int32_t k, const int32_t* allow_modes, const std::vector<int64_t>& off, const PqaFill& fill,
+                           const PqaLists& lists, uint64_t* out_ids, float* out_dists, int32_t* out_counts) {
+    auto by_lists = [&](const std::vector<int64_t>* qs) -> int {
+        g.unlock();
+        std::vector<uint64_t> ids;
+        std::vector<int64_t> lo;
+        std::vector<char> want;  // the flagged queries' lists only
+        if (qs) {
+            want.assign((size_t)nq, 0);
+            for (int64_t q : *qs) want[(size_t)q] = 1;
+        }
+        lists(ids, lo, qs ? &want : nullptr);
+        if (!qs)
+            return wv_index_search_by_vector_batch_multi_allow(idx, queries, nq, d, k, ids.data(), lo.data(),
+                                                               allow_modes, out_ids, out_dists, out_counts);
+        return multi_allow_subset(idx, queries, d, k, ids.data(), lo.data(), allow_modes, *qs, false, out_ids, out_dists,
+                                  out_counts);
+    };
+    const int64_t vq = round_up(std::max<int64_t>(idx->hiwater, 1), 256) / 32;
+    const int64_t qmax = std::max<int64_t>(1, (idx->pqa_budget_mb << 20) / (vq * (int64_t)sizeof(uint32_t) * 2));
+    const bool fast = idx->pqa && nq > 1 && idx->compression == WV_COMPRESSION_NONE && !idx->rq_bits &&
+                      idx->dims != 0 && d == idx->dims && k > 0 && idx->npresent > 0 && qs_route(idx, k) && nq <= qmax;
+    std::vector<double> md;
+    if (fast) pqa_depths(idx, nq, k, off.data(), allow_modes, md);
+    bool split = false;
+    if (fast) {  // the id-list call's split of too-sparse lists (see there)
+        int64_t nsp = 0;
+        for (int64_t q = 0; q < nq; q++) nsp += md[(size_t)q] > 960.0;
+        split = nsp > 0 && nsp <= idx->pqa_split_max && nsp < nq;
+    }
+    if (!fast || split) return by_lists(nullptr);
+    HIPCHK(hipSetDevice(idx->device));
+    hipStream_t s = idx->stream;
+    std::vector<int32_t> hm((size_t)nq);
+    for (int64_t q = 0; q < nq; q++) hm[(size_t)q] = (int32_t)std::min(960.0, std::ceil(md[(size_t)q]));
+    idx->pqa_R = *std::max_element(hm.begin(), hm.end()) > 448 ? 16 : 8;
+    HIPCHK(idx->pqaM.ensure((size_t)nq * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(idx->pqaM.p, hm.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIPCHK(idx->pqaBits.ensure((size_t)(nq * vq) * sizeof(uint32_t)));
+    HIPCHK(idx->pqaUnion.ensure((size_t)std::max<int64_t>(idx->cap / 32, vq) * sizeof(uint32_t)));
+    HIPCHK(idx->pqaQ.ensure((size_t)(nq + 1) * sizeof(int32_t)));
+    int32_t* d_modes = idx->pqaQ.as<int32_t>();
+    HIPCHK(hipMemcpyAsync(d_modes, allow_modes, (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    uint32_t* bits = idx->pqaBits.as<uint32_t>();
+    int rc = fill(s, vq, bits, d_modes);
+    if (rc) return rc;
+    std::vector<int64_t> left;
+    rc = pqa_run(idx, s, queries, nq, d, k, vq, bits, out_ids, out_dists, out_counts, left);
+    if (rc || left.empty()) return rc;
+    return by_lists(&left);
 }
 
 extern "C" int wv_index_search_by_vector_batch_multi_allow_bitmap(wv_index* idx, const float* queries, int64_t nq,
@@ -1753,60 +1815,60 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow_bitmap(wv_index* idx,
             for (int64_t w = 0; w < words; w++) c += __builtin_popcount(allow_bits[q * words + w]);
         off[(size_t)q + 1] = off[(size_t)q] + c;
     }
-    auto by_lists = [&](std::unique_lock<std::mutex>& g, const std::vector<int64_t>* qs) -> int {
-        g.unlock();
-        std::vector<uint64_t> ids;
-        std::vector<int64_t> lo;
-        bits_to_lists(allow_bits, words, allow_modes, nq, ids, lo);
-        if (!qs)
-            return wv_index_search_by_vector_batch_multi_allow(idx, queries, nq, d, k, ids.data(), lo.data(),
-                                                               allow_modes, out_ids, out_dists, out_counts);
-        return multi_allow_subset(idx, queries, d, k, ids.data(), lo.data(), allow_modes, *qs, false, out_ids, out_dists,
-                                  out_counts);
-    };
     std::unique_lock<std::mutex> g(idx->mu);
-    const int64_t vq = round_up(std::max<int64_t>(idx->hiwater, 1), 256) / 32;
-    const int64_t sw = vq + 1;  // raw words per query: the slot window plus the shift's spill word
-    const int64_t qmax = std::max<int64_t>(1, (idx->pqa_budget_mb << 20) / (vq * (int64_t)sizeof(uint32_t) * 2));
-    const bool fast = idx->pqa && nq > 1 && idx->compression == WV_COMPRESSION_NONE && !idx->rq_bits &&
-                      idx->dims != 0 && d == idx->dims && k > 0 && idx->npresent > 0 && qs_route(idx, k) && nq <= qmax;
-    std::vector<double> md;
-    if (fast) pqa_depths(idx, nq, k, off.data(), allow_modes, md);
-    bool split = false;
-    if (fast) {  // the id-list call's split of too-sparse lists (see there)
-        int64_t nsp = 0;
-        for (int64_t q = 0; q < nq; q++) nsp += md[(size_t)q] > 960.0;
-        split = nsp > 0 && nsp <= idx->pqa_split_max && nsp < nq;
-    }
-    if (!fast || split) return by_lists(g, nullptr);
-    HIPCHK(hipSetDevice(idx->device));
-    hipStream_t s = idx->stream;
-    std::vector<int32_t> hm((size_t)nq);
-    for (int64_t q = 0; q < nq; q++) hm[(size_t)q] = (int32_t)std::min(960.0, std::ceil(md[(size_t)q]));
-    idx->pqa_R = *std::max_element(hm.begin(), hm.end()) > 448 ? 16 : 8;
-    HIPCHK(idx->pqaM.ensure((size_t)nq * sizeof(int32_t)));
-    HIPCHK(hipMemcpyAsync(idx->pqaM.p, hm.data(), (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    HIPCHK(idx->pqaBits.ensure((size_t)(nq * vq) * sizeof(uint32_t)));
-    HIPCHK(idx->pqaUnion.ensure((size_t)std::max<int64_t>(idx->cap / 32, vq) * sizeof(uint32_t)));
-    HIPCHK(idx->pqaQ.ensure((size_t)(nq + 1) * sizeof(int32_t)));
-    // the callers' words from doc id id_base & ~31 on: one strided copy (pqaIds holds them here)
-    const int64_t b0 = (int64_t)(idx->id_base >> 5);
-    const int64_t avail = std::max<int64_t>(0, std::min<int64_t>(sw, words - b0));
-    HIPCHK(idx->pqaIds.ensure((size_t)(nq * sw) * sizeof(uint32_t) + 8));
-    uint32_t* raw = reinterpret_cast<uint32_t*>(idx->pqaIds.p);
-    if (avail > 0)
-        HIPCHK(hipMemcpy2DAsync(raw, (size_t)sw * sizeof(uint32_t), allow_bits + b0, (size_t)words * sizeof(uint32_t),
-                                (size_t)avail * sizeof(uint32_t), (size_t)nq, hipMemcpyHostToDevice, s));
-    int32_t* d_modes = idx->pqaQ.as<int32_t>();
-    HIPCHK(hipMemcpyAsync(d_modes, allow_modes, (size_t)nq * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    uint32_t* bits = idx->pqaBits.as<uint32_t>();
-    k_pqa_from_bits<<<(unsigned)std::min<int64_t>((nq * vq + 255) / 256, 8192), 256, 0, s>>>(
-        raw, sw, avail, d_modes, nq, (int)(idx->id_base & 31), idx->present, vq, bits);
-    HIPCHK(hipGetLastError());
-    std::vector<int64_t> left;
-    int rc = pqa_run(idx, s, queries, nq, d, k, vq, bits, out_ids, out_dists, out_counts, left);
-    if (rc || left.empty()) return rc;
-    return by_lists(g, &left);
+    // the callers' words from doc id id_base & ~31 on, one strided copy (pqaIds
+    // holds them), then the shift by id_base & 31 on the device
+    PqaFill fill = [&](hipStream_t s, int64_t vq, uint32_t* bits, const int32_t* d_modes) -> int {
+        const int64_t sw = vq + 1;  // the slot window plus the shift's spill word
+        const int64_t b0 = (int64_t)(idx->id_base >> 5);
+        const int64_t avail = std::max<int64_t>(0, std::min<int64_t>(sw, words - b0));
+        HIPCHK(idx->pqaIds.ensure((size_t)(nq * sw) * sizeof(uint32_t) + 8));
+        uint32_t* raw = reinterpret_cast<uint32_t*>(idx->pqaIds.p);
+        if (avail > 0)
+            HIPCHK(hipMemcpy2DAsync(raw, (size_t)sw * sizeof(uint32_t), allow_bits + b0, (size_t)words * sizeof(uint32_t),
+                                    (size_t)avail * sizeof(uint32_t), (size_t)nq, hipMemcpyHostToDevice, s));
+        k_pqa_from_bits<<<(unsigned)std::min<int64_t>((nq * vq + 255) / 256, 8192), 256, 0, s>>>(
+            raw, sw, avail, d_modes, nq, (int)(idx->id_base & 31), idx->present, vq, bits);
+        HIPCHK(hipGetLastError());
+        return WV_OK;
+    };
+    PqaLists lists = [&](std::vector<uint64_t>& ids, std::vector<int64_t>& lo, const std::vector<char>* want) {
+        bits_to_lists(allow_bits, words, allow_modes, nq, ids, lo, want);
+    };
+    return pqa_bitmap_core(idx, g, queries, nq, d, k, allow_modes, off, fill, lists, out_ids, out_dists, out_counts);
+}
+
+// The micro-batcher's filtered requests as slot bitmaps (batcher.hip): row q
+// = rows[q].words words of bits over slots (doc id - id_base), page-locked
+// host memory the kernel reads in place (rows[q].dev), list size rows[q].n.
+static int batch_search_slot_bitmaps(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
+                                     const wv_batch_row* rows, uint64_t* out_ids, float* out_dists,
+                                     int32_t* out_counts) {
+    std::vector<int32_t> modes((size_t)nq, 1);
+    std::vector<int64_t> off((size_t)nq + 1, 0);
+    for (int64_t q = 0; q < nq; q++) off[(size_t)q + 1] = off[(size_t)q] + std::max<int64_t>(rows[q].n, 0);
+    std::unique_lock<std::mutex> g(idx->mu);
+    PqaFill fill = [&](hipStream_t s, int64_t vq, uint32_t* bits, const int32_t* d_modes) -> int {
+        HIPCHK(idx->pqaIds.ensure((size_t)nq * sizeof(wv_batch_row)));
+        HIPCHK(hipMemcpyAsync(idx->pqaIds.p, rows, (size_t)nq * sizeof(wv_batch_row), hipMemcpyHostToDevice, s));
+        k_pqa_from_rows<<<(unsigned)std::min<int64_t>((nq * vq + 255) / 256, 8192), 256, 0, s>>>(
+            reinterpret_cast<const wv_batch_row*>(idx->pqaIds.p), d_modes, nq, idx->present, vq, bits);
+        HIPCHK(hipGetLastError());
+        return WV_OK;
+    };
+    PqaLists lists = [&](std::vector<uint64_t>& ids, std::vector<int64_t>& lo, const std::vector<char>* want) {
+        ids.clear();
+        lo.assign((size_t)nq + 1, 0);
+        for (int64_t q = 0; q < nq; q++) {
+            if (!want || (*want)[(size_t)q])
+                for (int64_t w = 0; w < rows[q].words; w++)
+                    for (uint32_t v = rows[q].host[w]; v; v &= v - 1)
+                        ids.push_back(idx->id_base + (uint64_t)(w * 32 + __builtin_ctz(v)));
+            lo[(size_t)q + 1] = (int64_t)ids.size();
+        }
+        ids.push_back(0);
+    };
+    return pqa_bitmap_core(idx, g, queries, nq, d, k, modes.data(), off, fill, lists, out_ids, out_dists, out_counts);
 }
 
 extern "C" int wv_index_hnsw_flat_search(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
@@ -2045,4 +2107,16 @@ static void* batch_pinned_alloc(size_t bytes) {
     return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;
 }
 static void batch_pinned_free(void* p) { (void)hipHostFree(p); }
+// page-locked rows the device reads in place (the batcher's allow bitmaps)
+static uint32_t* batch_row_alloc(int64_t words, const uint32_t** dev) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, (size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
+        return nullptr;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) { (void)hipHostFree(p); return nullptr; }
+    *dev = static_cast<const uint32_t*>(dp);
+    return static_cast<uint32_t*>(p);
+}
+static void batch_row_free(uint32_t* p) { (void)hipHostFree(p); }
+static uint64_t batch_id_base(const wv_index* idx) { return idx->id_base; }  // fixed at create
 #include "batcher.hip"
