@@ -200,3 +200,46 @@ def test_multi_allow_bitmap_form_equals_id_lists(wv, oracle, id_base, opts, k, n
         np.testing.assert_array_equal(bi[i, :bc[i]], oi.astype(np.uint64) + np.uint64(id_base), err_msg=f"q{i}")
         np.testing.assert_array_equal(bd[i, :bc[i]].view(np.uint32), od.view(np.uint32), err_msg=f"q{i}")
     idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,d,k,nq", [("cosine", 0, 768, 10, 300),
+                                               ("dot", 1, 512, 10, 100),     # integer data: ties, replays
+                                               ("cosine", 1, 640, 32, 64),
+                                               ("dot", 0, 768, 1, 40)])
+def test_multi_allow_per_query_keys_equal_union_keys(wv, oracle, metric, kind, d, k, nq):
+    """Per-query masked int8 keys (k_q8_blockkey<.., MASK>, option pqa_keys = 1,
+    the default for dot / cosine at 384 < d <= 768) against the union's keys
+    with per-query thresholds (pqa_keys = 0), the one-query calls and the
+    oracle: ids, distance bits and tie order."""
+    n = 24000
+    data = oracle.gen_matrix(kind, 91, 0, n, d)
+    queries = oracle.gen_matrix(kind, 92, 0, nq, d)
+    idx = wv.FlatIndex(distance=metric, variant="avx256")
+    idx.add_batch(np.arange(n, dtype=np.uint64), data)
+    idx.delete(*range(9, n, 89))
+    allows = _allow_lists(wv, n, nq, k, seed=d + k)
+    ids, dists, counts = idx.search_by_vector_batch_multi_allow(queries, k, allows)
+    assert wv._lib.ROUTES[idx.stats()["last_route"]] == "qs_int8", idx.stats()
+    bi, bd, bc = idx.search_by_vector_batch_multi_allow(queries, k, allows, bitmap=True)
+    idx.set_option("pqa_keys", 0)
+    ui, ud, uc = idx.search_by_vector_batch_multi_allow(queries, k, allows)
+    for other in ((bi, bd, bc), (ui, ud, uc)):
+        np.testing.assert_array_equal(other[2], counts)
+        for i in range(nq):
+            np.testing.assert_array_equal(other[0][i, :counts[i]], ids[i, :counts[i]], err_msg=f"q{i}")
+            np.testing.assert_array_equal(other[1][i, :counts[i]].view(np.uint32), dists[i, :counts[i]].view(np.uint32),
+                                          err_msg=f"q{i}")
+    for i in range(0, nq, max(1, nq // 24)):
+        ei, ed, ec = idx.search_by_vector_batch(queries[i:i + 1], k, allow=allows[i])
+        assert counts[i] == ec[0], f"q{i}"
+        np.testing.assert_array_equal(ids[i, :counts[i]], ei[0, :ec[0]], err_msg=f"q{i}")
+        np.testing.assert_array_equal(dists[i, :counts[i]].view(np.uint32), ed[0, :ec[0]].view(np.uint32))
+    orc = oracle.OracleFlat(oracle.METRIC[metric], 1, d, n)
+    orc.add_batch(np.arange(n, dtype=np.uint64), data)
+    orc.delete(list(range(9, n, 89)))
+    for i in range(min(nq, 12)):
+        al = None if allows[i] is None else [int(x) for x in allows[i].ids]
+        rc, oi, od = orc.search(queries[i], k, al)
+        np.testing.assert_array_equal(ids[i, :counts[i]], oi, err_msg=f"q{i}")
+        np.testing.assert_array_equal(dists[i, :counts[i]].view(np.uint32), od.view(np.uint32), err_msg=f"q{i}")
+    idx.close()

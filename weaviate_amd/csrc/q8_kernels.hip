@@ -316,6 +316,11 @@ struct Q8Args {
     int bq_bits;               // BQ: code bits 64 * words (hamming = (bq_bits - dot) / 2)
     int64_t nq_live = 1ll << 62;  // k_q8_blockkey<.., LIVE>: the launch's real queries (the rest is padding)
     int prio = 0;                 // k_q8_blockkey: 1 = waves 4-7 at s_setprio 1 for the whole loop
+    // k_q8_blockkey<.., MASK>: per-query row bitmaps (query q's word for block b
+    // at qmask[q * qmask_ld + b]; queries past qmask_n read row qmask_n - 1)
+    const uint32_t* qmask = nullptr;
+    int64_t qmask_ld = 0;
+    int64_t qmask_n = 1;
 };
 namespace {
 
@@ -357,6 +362,13 @@ namespace {
 // DBG (timing experiments in a -DWV_QS_DBG build only, wrong results): bit 0
 // drops the plane DMA, bit 1 the MFMAs, bit 2 the block reductions and stores,
 // bit 3 the key stores only.
+// MASK (PAIR, dot / cosine): per-query allow bitmaps (the multi-allow batch):
+// a block's key for query q is the maximum over the rows of q's own list only
+// (a.qmask word of q and the block ANDed with the valid word), so each query's
+// keys bound its own rows -- the plain select and proof then apply per query.
+// One more LDS-DMA op per wave and group: the 64 mask words of the wave's 32
+// queries x the slot's 2 blocks, laid out [block][query j][half n] so a lane
+// reads its two queries' words of a block with one ds_read_b64.
 // LIVE (PAIR schedule; a batch that is not a multiple of 256 queries): a wave
 // whose 32 queries all lie at or past a.nq_live -- the padding of the last
 // query group -- reads no fragments and issues no MFMA or reduction; it still
@@ -364,7 +376,8 @@ namespace {
 // wave's vector-memory counts, which the ring's vmcnt waits rely on, are those
 // of the full schedule.  A batch of 64 queries runs the MFMAs of 2 waves
 // instead of 8 (the HBM stream of the plane is then the bound).
-template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false, int PF = 1, int DBG = 0, bool LIVE = false>
+template <int NC, int RB, bool ISL2, bool STAG = false, bool BQ = false, int PF = 1, int DBG = 0, bool LIVE = false,
+          bool MASK = false>
 __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     constexpr int NPB = 2 * NC;                     // 1 KiB pieces per 32-row block
     constexpr int SLOT = RB * NPB * 1024;           // bytes per ring slot
@@ -373,14 +386,15 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     static_assert(RB == 1 || RB == 2, "RB must be 1 or 2");
     constexpr int64_t TILE_B = (int64_t)NPB * 8192;  // bytes per 256-row tile of a plane
     constexpr int NT = RB * NC;                     // chunks per slot
-    constexpr int P0 = P + 2 + (ISL2 ? 1 : 0);      // vector-memory ops per group, per wave
+    constexpr int P0 = P + 2 + (ISL2 ? 1 : 0) + (MASK ? 1 : 0);  // vector-memory ops per group, per wave
     static_assert(P0 < NC, "the deferred key store must follow the slot's DMA pieces");
     static_assert(PF >= 1 && PF + 1 < NC, "prefetch distance");
     static_assert(!STAG || RB == 2, "the stagger defers a slot's second block");
     static_assert(!BQ || (!ISL2 && !STAG), "BQ: integer maxima, in-order schedule");
     static_assert(!LIVE || (RB == 2 && !STAG && !BQ && DBG == 0), "LIVE: the paired in-order schedule");
+    static_assert(!MASK || (RB == 2 && !STAG && !BQ && !ISL2 && DBG == 0), "MASK: paired dot / cosine keys");
     constexpr int X0 = 1;                           // chunk of the slot's extra LDS reads
-    constexpr int XE = 2 + (ISL2 ? 2 * RB : 0);     // extra reads: valid words, scales (+ norms)
+    constexpr int XE = 2 + (ISL2 ? 2 * RB : 0) + (MASK ? 2 : 0);  // extra reads: valid words, scales (+ norms / masks)
     constexpr int NBUF = 3;
     extern __shared__ __attribute__((aligned(16))) unsigned char qsm[];
 
@@ -399,6 +413,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     // n: lane (j = lane & 15, kq = lane >> 4) holds query wave*32 + 16n + j,
     // columns 64c + 16kq .. +15
     i32x4_t Qf[2 * NC];
+    const int64_t q0 = (int64_t)grp * 256 + wave * 32;
     if (act) {
         const int j = lane & 15, kq = lane >> 4;
         const unsigned char* qp =
@@ -409,7 +424,6 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             for (int n = 0; n < 2; n++)
                 Qf[2 * c + n] = *reinterpret_cast<const i32x4_t*>(qp + (2 * c) * 8192 + n * 16 * 32);
     }
-    const int64_t q0 = (int64_t)grp * 256 + wave * 32;
     const float sqA = BQ ? 1.f : a.qscale[q0 + (lane & 15)];
     const float sqB = BQ ? 1.f : a.qscale[q0 + 16 + (lane & 15)];
     constexpr bool PAIR = RB == 2 && !STAG;
@@ -430,6 +444,8 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     const unsigned vring = ring + NBUF * SLOT + (unsigned)wave * 64u;
     const unsigned sring = ring + NBUF * SLOT + 512u + (unsigned)wave * 64u;
     const unsigned xnring = ring + NBUF * SLOT + 1024u + (unsigned)wave * (unsigned)(4 * RB * 128);
+    // MASK: [8 waves][4 steps][64 words] per-query mask words (after the valid / scale rings)
+    const unsigned mring = ring + NBUF * SLOT + 1024u + (unsigned)wave * 1024u;
     const int64_t tile0 = (s0 * RB * 32) >> 8;
     const __amdgpu_buffer_rsrc_t xrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.X8 + tile0 * TILE_B), (short)0, -1, 0x00020000);
@@ -450,6 +466,13 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             if (lane < RB)
                 __builtin_amdgcn_global_load_lds(a.sb + igb + lane, (lds_ptr_t)(size_t)(sring + (unsigned)((t & 3) * 16)), 4,
                                                  0, 0);
+        } else if constexpr (MASK) {
+            // lane (block rb, query j, half n) -> LDS word rb * 32 + 2 j + n
+            const int rbm = lane >> 5, jq = (lane >> 1) & 15, hn = lane & 1;
+            int64_t qq = q0 + 16 * hn + jq;
+            if (qq >= a.qmask_n) qq = a.qmask_n - 1;
+            __builtin_amdgcn_global_load_lds(a.qmask + qq * a.qmask_ld + igb + rbm,
+                                             (lds_ptr_t)(size_t)(mring + (unsigned)((t & 3) * 256)), 4, 0, 0);
         } else {
             if (lane < RB * 8)
                 __builtin_amdgcn_global_load_lds(a.xnorm2 + igb * 32 + 4 * lane,
@@ -618,11 +641,22 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
     };
     // PAIR: a block's raw per-lane partials (see finish2)
     auto reduce_raw = [&](const i32x4_t (&ac)[2][2], uint32_t vw_, float sb_, const f32x4_t& xa_, const f32x4_t& xb_,
-                          uint32_t& r0, uint32_t& r1) {
+                          uint32_t& r0, uint32_t& r1, uint2 mw = uint2{0u, 0u}) {
         const uint32_t vw = __builtin_amdgcn_readfirstlane(vw_);
         const uint32_t vl = vw >> (4 * ((lane >> 4) & 3));
         uint32_t rr[2];
-        if constexpr (ISL2) {
+        if constexpr (MASK) {  // each query half its own rows (per-lane bits)
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                const uint32_t vq_ = ((n ? mw.y : mw.x) & vw) >> (4 * ((lane >> 4) & 3));
+                int mi = Q8_NONE;
+#pragma unroll
+                for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) mi = max(mi, ((vq_ >> (16 * mm + r)) & 1u) ? ac[mm][n][r] : Q8_NONE);
+                rr[n] = (uint32_t)mi;
+            }
+        } else if constexpr (ISL2) {
             float p0, p1;
             reduce(ac, vw_, sb_, xa_, xb_, p0, p1);
             rr[0] = __float_as_uint(p0);
@@ -675,6 +709,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
         const unsigned sm = (unsigned)(t & 3);
         uint2 vwv;
         float2 sbv;
+        uint2 mw0 = uint2{0u, 0u}, mw1 = uint2{0u, 0u};  // MASK: this lane's two queries' words of blocks 0, 1
         f32x4_t xa[RB], xb[RB];
         if constexpr (!ISL2) {
 #pragma unroll
@@ -686,6 +721,11 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             if constexpr (tt == X0 && ACT) {  // this slot's valid words, scales (+ L2 norms)
                 asm volatile("ds_read_b64 %0, %1" : "=v"(vwv) : "v"(vring + sm * 16u));
                 asm volatile("ds_read_b64 %0, %1" : "=v"(sbv) : "v"(sring + sm * 16u));
+                if constexpr (MASK) {
+                    const unsigned mb = mring + sm * 256u + (unsigned)((lane & 15) * 8);
+                    asm volatile("ds_read_b64 %0, %1" : "=v"(mw0) : "v"(mb));
+                    asm volatile("ds_read_b64 %0, %1 offset:128" : "=v"(mw1) : "v"(mb));
+                }
                 if constexpr (ISL2) {
                     // rows 4g..4g+3 and 16+4g..+3 of block rb, g = lane>>4
                     const unsigned xbase = xnring + sm * (unsigned)(RB * 128) + (unsigned)(16 * ((lane >> 4) & 3));
@@ -713,6 +753,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
                     if constexpr (RB == 2) asm volatile("" : "+v"(xa[RB - 1]), "+v"(xb[RB - 1]));
                 } else {
                     asm volatile("" : "+v"(vwv), "+v"(sbv));
+                    if constexpr (MASK) asm volatile("" : "+v"(mw0), "+v"(mw1));
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -745,7 +786,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
                 }
             }
             // PAIR: block 0's partials beside block 1's MFMAs (stored with block 1)
-            if constexpr (PAIR && tt == NC + 1 && !(DBG & 4) && ACT) reduce_raw(acc[0], vwv.x, sbv.x, xa[0], xb[0], pA0, pA1);
+            if constexpr (PAIR && tt == NC + 1 && !(DBG & 4) && ACT) reduce_raw(acc[0], vwv.x, sbv.x, xa[0], xb[0], pA0, pA1, mw0);
             // RB = 2: block 0 is reduced and stored beside block 1's MFMAs
             if constexpr (RB == 2 && !PAIR && tt == NC + 1 && !(DBG & 4)) {
                 if (!late) {
@@ -769,7 +810,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_blockkey(Q8Args a) {
             dxb = xb[RB - 1];
         } else if constexpr (PAIR && !(DBG & 4)) {
             if constexpr (ACT) {
-                reduce_raw(acc[1], vwv.y, sbv.y, xa[1], xb[1], pB0, pB1);
+                reduce_raw(acc[1], vwv.y, sbv.y, xa[1], xb[1], pB0, pB1, mw1);
                 psA = sbv.x;
                 psB = sbv.y;
             }

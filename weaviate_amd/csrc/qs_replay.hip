@@ -28,7 +28,7 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
     // the heap top by block upper bounds A + eps, which hold for a block with a
     // row of the keys' row set (the union) but not necessarily one of the
     // query's own; the one-wave replay prunes by its true heap top only
-    const bool ub_ok = idx->cur_vq == 0;
+    const bool ub_ok = idx->cur_vq == 0 || idx->cur_pqk;  // per-query keys bound the query's own rows
     // a few listed queries of a small batch, counted on the device (most such
     // calls list no query): the one-launch 8-wave form instead of the pooled
     // form's three launches.  A host list (counters NULL: the cross-shard

@@ -89,6 +89,14 @@ int launch_q8_keys(wv_index* idx, hipStream_t s, Q8Args a, int dpb8, bool l2) {
 // shard's k+1 smallest block-key A values (eps in idx->qsEps); phase 2 = the
 // global threshold from every shard's topA / eps (gA [W][nq][k+1], gE [W][nq],
 // k_blk_gthresh), exact distances, overflow pass.
+// per-query masked keys serve this index's multi-allow batches (the paired
+// int8 dot / cosine key kernel; see search_qs)
+bool pqa_keys_route(const wv_index* idx) {
+    const bool q8 = idx->q8_planes && (idx->q8_opt || idx->q8_only);
+    return idx->pqa_keys && q8 && !idx->q8_only && idx->dpb8 <= 768 && idx->metric != WV_METRIC_L2_SQUARED &&
+           !idx->q8_stag && idx->q8_shape != 32 && idx->sel_dbg <= 0;
+}
+
 int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const uint32_t* valid,
                      uint64_t* o_ids, float* o_d, int32_t* o_n, int32_t* o_flags, int phase,
                      float* topA, const float* gA, const float* gE, int W) {
@@ -102,13 +110,21 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     const int NC8 = idx->dpb8 / 64;
     const int RB8 = idx->dpb8 <= 768 ? 2 : 1;
     const int RB = q8 ? RB8 : qs_rb(NK);
+    const bool pqa = idx->pqa_valid != nullptr;
+    // per-query keys (option pqa_keys, int8 paired dot / cosine keys): the key
+    // pass masks each query's rows with its own bitmap (k_q8_blockkey<..,
+    // MASK>), so every key bounds the query's own rows and the plain select,
+    // 2-eps proof and bounded replay apply; otherwise (pqs) the union's keys with
+    // the per-query deeper thresholds below
+    const bool pqk = pqa && pqa_keys_route(idx);
+    const bool pqs = pqa && !pqk;
     int R = qs_R_flat(k);
     if (q8) {  // the int8 bound is wider: 448-block lists (option q8_R; C3: ~110 candidate blocks
                // per query, R = 4 sent a few percent to the overflow pass, profiles/r04_c3ab1_*)
         if (idx->q8_R > 0) R = std::max(R, idx->q8_R);
         else R = std::max(R, 8);
     }
-    if (idx->pqa_valid) R = std::max(R, idx->pqa_R);  // per-query lists: deeper thresholds (k_blk_select mq)
+    if (pqs) R = std::max(R, idx->pqa_R);  // per-query lists on the union's keys: deeper thresholds (k_blk_select mq)
     const int L = 64 * (R - 1);
     const int64_t nslots = std::max<int64_t>(1, (idx->hiwater + 32 * RB - 1) / (32 * RB));
     const int64_t nb = nslots * RB;  // 32-row blocks scanned = key row length
@@ -137,17 +153,16 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
     // `valid` is their union (the block keys are lower bounds over it, so over
     // each query's own rows too); the exact pass and the replays read query
     // q's bitmap, and k_blk_exact proves completeness against the select's T
-    const bool pqa = idx->pqa_valid != nullptr;
     if (pqa && (phase != 0 || mode != 0)) return set_err(WV_ERR_UNSUPPORTED, "per-query allow lists: top-k mode only");
     struct PqaScope {
         wv_index* i;
-        ~PqaScope() { i->cur_vq = 0; i->cur_tq = nullptr; }
+        ~PqaScope() { i->cur_vq = 0; i->cur_tq = nullptr; i->cur_pqk = false; }
     } pqa_scope{idx};
     // the select's completeness bounds: per-query lists, and lists whose
     // threshold the select lowered (phase 0 only: the sharded phases keep the
     // 2-eps argument their global threshold relies on)
     HIPCHK(idx->qsT.ensure((size_t)qc * sizeof(float)));
-    float* t_sel = (pqa || (phase == 0 && idx->sel_lower)) ? idx->qsT.as<float>() : nullptr;
+    float* t_sel = (pqs || (phase == 0 && idx->sel_lower)) ? idx->qsT.as<float>() : nullptr;
     const size_t rlds = packed_replay_lds(k) + 16 * 64 * sizeof(float) + (size_t)idx->dpb * sizeof(float);
     if (mode == 0 && rlds > 160 * 1024) return set_err(WV_ERR_UNSUPPORTED, "k %d too large for the replay heap", k);
     // error-bound constants: reference-order fp32 (gamma_{dpb+8}) and the MFMA's
@@ -175,6 +190,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         const uint32_t* exv = pqa ? idx->pqa_valid + c0 * idx->pqa_vq : valid;
         idx->cur_vq = pqa ? idx->pqa_vq : 0;
         idx->cur_tq = t_sel;
+        idx->cur_pqk = pqk;
         float4* qinfo = idx->qsInfo.as<float4>();
         if (phase != 2) {
             k_query_split<<<(unsigned)((cn_pad + 3) / 4), 256, 0, s>>>(Qn, idx->dpad, idx->dpb, cn, cn_pad,
@@ -226,7 +242,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         const bool l2 = metric == L2;
         const size_t lds = q8wide ? (size_t)3 * 32 * 1024 + 1024 + (l2 ? (size_t)4 * 512 : 0)
                          : q8cp ? (size_t)3 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * 128 : 0)
-                         : q8 ? (size_t)3 * RB * 2 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * RB * 128 : 0)
+                         : q8 ? (size_t)3 * RB * 2 * NC8 * 1024 + 1024 + (l2 ? (size_t)8 * 4 * RB * 128 : 0) +
+                                    (pqk ? (size_t)8 * 1024 : 0)
                          : w4 ? (size_t)w4_nb * (NK / 4) * 2048 + 256 + (l2 ? (size_t)4 * 4 * 128 : 0)
                               : (size_t)QS_NBUF * RB * NK * 1024 + 512 + (l2 ? (size_t)8 * 4 * RB * 128 : 0);
         dim3 grid((unsigned)((int64_t)a.nqg * a.nspans));
@@ -280,7 +297,19 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         // a partial last query group (batches that are not a multiple of 256):
         // the padding's waves skip their MFMAs (LIVE)
         const bool q8live = idx->q8_live && cn % QS_QPB != 0;
-#define WV_Q8T(NCV, L2V) do { if (idx->q8_stag) WV_Q8S(NCV, 2, L2V, true, 1); else if (q8live) WV_Q8L(NCV, L2V); else WV_Q8(NCV, 2, L2V); } while (0)
+// per-query keys (pqk: never L2, stag or the 32-wide shape)
+#define WV_Q8M(NCV, LIVEV)                                                                                     \
+    do {                                                                                                       \
+        HIPCHK(hipFuncSetAttribute((const void*)k_q8_blockkey<NCV, 2, false, false, false, 1, 0, LIVEV, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+        k_q8_blockkey<NCV, 2, false, false, false, 1, 0, LIVEV, true><<<grid, 512, lds, s>>>(q8a);           \
+    } while (0)
+#define WV_Q8T(NCV, L2V)                                                                                       \
+    do {                                                                                                       \
+        if constexpr (!L2V) {                                                                                  \
+            if (pqk) { if (q8live) WV_Q8M(NCV, true); else WV_Q8M(NCV, false); break; }                       \
+        }                                                                                                      \
+        if (idx->q8_stag) WV_Q8S(NCV, 2, L2V, true, 1); else if (q8live) WV_Q8L(NCV, L2V); else WV_Q8(NCV, 2, L2V); \
+    } while (0)
 #define WV_Q8N(L2V)                                    \
     switch (NC8) {                                     \
     case 8: WV_Q8T(8, L2V); break;                     \
@@ -307,6 +336,11 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             q8a.nqg = a.nqg;
             q8a.nq_live = cn;
             q8a.prio = idx->q8_prio;
+            if (pqk) {  // query q of this chunk: its bitmap row (the exact pass's too)
+                q8a.qmask = exv;
+                q8a.qmask_ld = idx->pqa_vq;
+                q8a.qmask_n = cn;
+            }
 #ifdef WV_QS_DBG
             if (idx->sel_dbg > 0 && !l2 && NC8 == 12) {
                 switch (idx->sel_dbg) {
@@ -325,7 +359,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             // small batches: the register-streaming kernel (one plane pass, no
             // 256-query padding of the MFMA work), the same keys
             const int qg = cn <= 16 ? 1 : 2;
-            const bool gemv = idx->q8_gemv && !q8cp && cn <= 32 && NC8 <= (qg == 1 ? 24 : 16) && nb < (1ll << 40);
+            const bool gemv = idx->q8_gemv && !q8cp && !pqk && cn <= 32 && NC8 <= (qg == 1 ? 24 : 16) && nb < (1ll << 40);
             if (gemv) {
                 idx->stats.last_route = WV_ROUTE_Q8_GEMV;
                 const unsigned gg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (nb + 3) / 4));
@@ -409,6 +443,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
 #undef WV_QSW
 #undef WV_Q8N
 #undef WV_Q8T
+#undef WV_Q8M
 #undef WV_Q8L
 #undef WV_Q8S
 #undef WV_Q8
@@ -440,7 +475,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             // (C2: 0.61 vs 0.92 ms)
             const int RT = qs_R_flat(k);
             // small batches: the split selection (P waves per query)
-            if (!list && !pqa && cn <= idx->sel_split_max && RT <= RV && RT <= 8) {
+            if (!list && !pqs && cn <= idx->sel_split_max && RT <= RV && RT <= 8) {
                 const int P = (int)std::max<int64_t>(1, std::min<int64_t>(256, (nb + 2047) / 2048));
                 const int LV = 64 * (RV - 1);
                 const size_t pb = (size_t)cn * P * (k + 1) * sizeof(float);
@@ -468,7 +503,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                                                                             0x7f800000u);
                 return;
             }
-            if (idx->sel_filter && RT < RV && !pqa) {
+            if (idx->sel_filter && RT < RV && !pqs) {
 #define WV_SELF(RV, RTV) k_blk_select_f<RV, RTV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc, t_sel)
                 if (RV == 4) WV_SELF(4, 2);
                 else if (RT == 2) WV_SELF(8, 2);
@@ -476,7 +511,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
 #undef WV_SELF
                 return;
             }
-#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc, t_sel, pqa ? exv : nullptr, pqa ? idx->pqa_vq : 0, pqa ? idx->pqa_m + c0 : nullptr)
+#define WV_SELR(RV) k_blk_select<RV><<<gw, 256, 0, s>>>(a.key, ldk, nb, (int)cn, k, metric, qinfo_sel, qmax_sel, idx->d_maxn2, gd, gacc_sel, idx->qsCand.as<uint32_t>(), idx->qsNc.as<int32_t>(), flags, idx->qsEps.as<float>(), list, cnt, tA, idx->qsCap.as<float>(), lc, t_sel, pqs ? exv : nullptr, pqs ? idx->pqa_vq : 0, pqs ? idx->pqa_m + c0 : nullptr)
             if (RV == 2) WV_SELR(2); else if (RV == 4) WV_SELR(4); else if (RV == 8) WV_SELR(8); else if (RV == 16) WV_SELR(16);
             else if (RV == 32) WV_SELR(32); else WV_SELR(64);
 #undef WV_SELR
@@ -547,7 +582,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
             exa(8, olist, idx->qscount + 2);
             HIPCHK(hipGetLastError());
         }
-        if (pqa && R < 16) {
+        if (pqs && R < 16) {
             // per-query lists whose proof failed (flag 1): once more with
             // 960-block lists at the deepest threshold before the replay (the
             // one-wave replay walks most blocks when the key bound is wide)
@@ -566,7 +601,7 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
         if (phase == 2 && o_flags)
             HIPCHK(hipMemcpyAsync(o_flags + c0, flags, (size_t)cn * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         if (mode == 1) continue;
-        if (pqa && o_flags) continue;  // per-query lists: the caller searches the unresolved queries alone
+        if (pqs && o_flags) continue;  // per-query lists on the union's keys: the caller searches the unresolved queries alone
         // ---- flagged queries: the exact heap replay, bounded by the block keys ----
         if (!ctr_reset) HIPCHK(hipMemsetAsync(idx->qscount + 1, 0, sizeof(uint32_t), s));
         k_flag_list<<<(unsigned)((cn + 255) / 256), 256, 0, s>>>(flags, (int)cn, idx->qsList.as<int32_t>(), idx->qscount, 0);
@@ -576,6 +611,8 @@ int search_qs(wv_index* idx, hipStream_t s, int64_t nq, int k, int mode, const u
                                        o_d + c0 * kout, o_n + c0, nullptr, nullptr, nullptr, 1, 0);
             if (rc) return rc;
         }
+        // per-query keys: the flagged queries are resolved here, none is left for the caller
+        if (pqk && o_flags) HIPCHK(hipMemsetAsync(o_flags + c0, 0, (size_t)cn * sizeof(int32_t), s));
     }
     if (idx->timing) {
         HIPCHK(hipEventRecord(idx->evt1, s));

@@ -271,9 +271,11 @@ struct wv_index {
     int64_t pqa_budget_mb = 4096;
     int64_t pqa_split_max = 64;
     int pqa_alone = 1;
+    int pqa_keys = 1;       // option pqa_keys: per-query masked int8 keys (k_q8_blockkey<.., MASK>)
     int64_t pqa_vq = 0;
     int64_t cur_vq = 0;
     const float* cur_tq = nullptr;
+    bool cur_pqk = false;   // search_qs: this batch's keys are per-query (the replays' upper bounds hold)
     DBuf pqaBits, pqaUnion, pqaIds, pqaQ, pqaM, pqaM2, qsT;
     int64_t q8_bm_min = 64;                                   // option q8_bm_min: smallest batch for the block-major int8 filter
     int rq_serial = 0;                                        // option rq_serial (debug): k_rq8_keys without the DMA lookahead                                          // option rq_mfma: rq-8 on the integer matrix cores
@@ -335,6 +337,7 @@ int run_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, const float*
                int out_by_query, int kout, uint64_t* oi, float* od, int32_t* on, int by_query = 0,
                uint64_t* rec_i = nullptr, float* rec_d = nullptr, int32_t* rec_n = nullptr, int rec_cap = 0);
 void launch_pq_encode(wv_index* idx, int64_t n, const uint32_t* d_slots);
+bool pqa_keys_route(const wv_index* idx);  // qs_runtime.hip: per-query masked keys for multi-allow batches
 int shard_filter_bitmap(wv_index* idx, hipStream_t s, const uint64_t* allow, int64_t n_allow, const uint32_t** valid,
                         int64_t* n_valid);
 void launch_rq_encode(wv_index* idx, hipStream_t s, const float* rows, int64_t ld, int64_t n, const uint32_t* d_slots,

@@ -778,6 +778,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "pqa") idx->pqa = value ? 1 : 0;
     else if (k == "sel_lower") idx->sel_lower = value ? 1 : 0;  // per-query allow lists share one block-key launch
     else if (k == "pqa_alone") idx->pqa_alone = value ? 1 : 0;  // unresolved per-query lists searched alone
+    else if (k == "pqa_keys") idx->pqa_keys = value ? 1 : 0;    // per-query masked int8 keys
     else if (k == "pqa_split_max") idx->pqa_split_max = std::max<int64_t>(value, 0);  // sparse lists searched alone
     else if (k == "pqa_budget_mb") idx->pqa_budget_mb = std::max<int64_t>(value, 1);
     else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only
@@ -1640,7 +1641,7 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
     }
     std::vector<double> md;
     pqa_depths(idx, nq, k, allow_offsets, allow_modes, md);
-    if (!t_pqa_nosplit) {
+    if (!t_pqa_nosplit && !pqa_keys_route(idx)) {  // (per-query keys serve sparse lists in the launch)
         // lists too sparse for the union's keys (deeper than the 960-block
         // lists) would end in the one-wave replay, a walk over every block
         // key: a few of them go as their own searches instead (an allow list
@@ -1764,7 +1765,7 @@ static int pqa_bitmap_core(wv_index* idx, std::unique_lock<std::mutex>& g, const
     std::vector<double> md;
     if (fast) pqa_depths(idx, nq, k, off.data(), allow_modes, md);
     bool split = false;
-    if (fast) {  // the id-list call's split of too-sparse lists (see there)
+    if (fast && !pqa_keys_route(idx)) {  // the id-list call's split of too-sparse lists (see there)
         int64_t nsp = 0;
         for (int64_t q = 0; q < nq; q++) nsp += md[(size_t)q] > 960.0;
         split = nsp > 0 && nsp <= idx->pqa_split_max && nsp < nq;
