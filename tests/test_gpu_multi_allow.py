@@ -127,12 +127,18 @@ def test_batcher_coalesces_distinct_allow_lists(wv, oracle):
     idx.set_option("batch_window_us", 3000)
     allows = _allow_lists(wv, n, len(queries), k, seed=5)
     exp = [idx.search_by_vector_batch(queries[i:i + 1], k, allow=allows[i]) for i in range(len(queries))]
-    with ThreadPoolExecutor(32) as ex:
-        res = list(ex.map(lambda i: idx.search_by_vector(queries[i], k, allow=allows[i]), range(len(queries))))
-    for i, (ri, rd) in enumerate(res):
-        ei, ed, ec = exp[i]
-        np.testing.assert_array_equal(ri, ei[0, :ec[0]], err_msg=f"q{i}")
-        np.testing.assert_array_equal(rd.view(np.uint32), ed[0, :ec[0]].view(np.uint32), err_msg=f"q{i}")
+    # three rounds in different orders: the callers' pooled bitmap rows are
+    # reused by other callers (stale rows would give another caller's list)
+    rng = np.random.default_rng(3)
+    for rnd in range(3):
+        order = rng.permutation(len(queries)) if rnd else np.arange(len(queries))
+        with ThreadPoolExecutor(32) as ex:
+            res = dict(zip(order, ex.map(lambda i: idx.search_by_vector(queries[i], k, allow=allows[i]), order)))
+        for i in range(len(queries)):
+            ri, rd = res[i]
+            ei, ed, ec = exp[i]
+            np.testing.assert_array_equal(ri, ei[0, :ec[0]], err_msg=f"round {rnd} q{i}")
+            np.testing.assert_array_equal(rd.view(np.uint32), ed[0, :ec[0]].view(np.uint32), err_msg=f"round {rnd} q{i}")
     st = idx.batcher_stats()
     assert st["launches"] < st["calls"] and st["max_batch"] > 1, st
     idx.close()

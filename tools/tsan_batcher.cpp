@@ -36,7 +36,7 @@ static int set_err(int code, const char* fmt, ...) {
 extern "C" const char* wv_last_error(void) { return g_err.c_str(); }
 
 struct wv_batcher;
-static void batcher_free(wv_batcher* b);
+static void batcher_free(wv_index* idx, wv_batcher* b);
 
 // the fields batcher.hip reads, as runtime.hip declares them
 struct wv_index {
@@ -101,13 +101,16 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
 
 static void* batch_pinned_alloc(size_t bytes) { return malloc(bytes); }
 static void batch_pinned_free(void* p) { free(p); }
-static uint32_t* batch_row_alloc(int64_t words, const uint32_t** dev) {
-    uint32_t* p = static_cast<uint32_t*>(malloc((size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t)));
-    *dev = p;
-    return p;
+static uint32_t* batch_row_alloc(wv_index*, int64_t words) {
+    return static_cast<uint32_t*>(malloc((size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t)));
 }
-static void batch_row_free(uint32_t* p) { free(p); }
+static void batch_row_free(wv_index*, uint32_t* p) { free(p); }
+static int batch_row_upload(wv_index*, uint32_t* dev, const uint32_t* host, int64_t words) {
+    memcpy(dev, host, (size_t)words * sizeof(uint32_t));
+    return WV_OK;
+}
 static uint64_t batch_id_base(const wv_index*) { return 0; }
+static bool batch_rows_on(const wv_index*) { return true; }
 
 #include "../weaviate_amd/csrc/batch_row.h"
 // the slot-bitmap batch: rows back to id lists, then query by query
@@ -166,6 +169,15 @@ int main(int argc, char** argv) {
                 if (kind == 6) {  // a dense allow list: its slot bitmap built by this caller
                     mode = 1;
                     for (int i = 0; i < 40; i++) allow.push_back(r() % (uint64_t)idx.n);
+                } else if (kind == 4) {  // dense lists shared by many callers (every other block) or a span
+                    mode = 1;
+                    if (c % 2) {
+                        for (int64_t j = 0; j < idx.n; j++)
+                            if ((j >> 5) % 2 == t % 2) allow.push_back((uint64_t)j);
+                    } else {
+                        const uint64_t a0 = r() % (uint64_t)(idx.n - 100);
+                        for (uint64_t j = a0; j < a0 + 100; j++) allow.push_back(j);
+                    }
                 } else if (kind == 5) {  // a sparse one (ids kept; a bitmap batch gets the leader's row)
                     mode = 1;
                     for (int i = 0; i < 3; i++) allow.push_back(r() % (uint64_t)idx.n);
@@ -202,6 +214,6 @@ int main(int argc, char** argv) {
     wv_index_batcher_stats(&idx, st);
     printf("tsan_batcher: %d threads x %d calls, %lld batches (max %lld), %lld dimension errors, %lld mismatches\n",
            threads, calls, (long long)st[1], (long long)st[2], (long long)errs.load(), (long long)bad.load());
-    batcher_free(idx.batcher);
+    batcher_free(&idx, idx.batcher);
     return bad.load() == 0 && st[0] == (int64_t)threads * calls ? 0 : 1;
 }

@@ -84,10 +84,12 @@ static inline int64_t pq_mwp(int m) { return (int64_t)((m + 15) / 16) * 4; }
 static inline int pq_g16(int m) { return (m + 15) / 16; }
 
 struct wv_batcher;
-static void batcher_free(wv_batcher* b);
+static void batcher_free(wv_index* idx, wv_batcher* b);
 
 struct wv_index {
     std::mutex mu;
+    std::mutex row_mu;                 // creates row_stream (the batcher's callers copy their allow bitmaps on it)
+    hipStream_t row_stream = nullptr;
     int metric = WV_METRIC_COSINE_DOT;
     int variant = WV_VARIANT_AVX256;
     int compression = WV_COMPRESSION_NONE;
@@ -101,6 +103,7 @@ struct wv_index {
     int exact_bm = 1;           // block-major exact distances (rows <= 508 floats): 1 on, 0 off
     int device = 0;
     uint64_t id_base = 0;
+    uint64_t id_base0 = 0;  // id_base as created (a ScanWindow shifts id_base under mu; the batcher's callers read this)
     std::string root_path;
 
     int dims = 0, dpad = 0;
@@ -272,6 +275,7 @@ struct wv_index {
     int64_t pqa_split_max = 64;
     int pqa_alone = 1;
     int pqa_keys = 1;       // option pqa_keys: per-query masked int8 keys (k_q8_blockkey<.., MASK>)
+    std::atomic<int> batch_rows{1};  // option batch_rows: the batcher's dense lists as slot bitmaps (read by callers)
     int64_t pqa_vq = 0;
     int64_t cur_vq = 0;
     const float* cur_tq = nullptr;

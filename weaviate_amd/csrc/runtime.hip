@@ -105,6 +105,7 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
     idx->rescore_limit = cfg->rescore_limit;
     idx->device = cfg->device;
     idx->id_base = cfg->id_base;
+    idx->id_base0 = cfg->id_base;
     idx->root_path = cfg->root_path ? cfg->root_path : "";
     // block-key path for the exact fp32 search (qs_kernels.hip); the bf16x3
     // select kernels (kernels_bf3.hip) need option bf3_planes before the first Add
@@ -152,8 +153,9 @@ extern "C" int wv_index_create(const wv_config* cfg, wv_index** out) {
 extern "C" void wv_index_destroy(wv_index* idx) {
     if (!idx) return;
     if (idx->sub) wv_index_destroy(idx->sub);
-    batcher_free(idx->batcher);
     hipSetDevice(idx->device);
+    batcher_free(idx, idx->batcher);
+    if (idx->row_stream) hipStreamDestroy(idx->row_stream);
     if (idx->stream) hipStreamSynchronize(idx->stream);
     if (idx->g_exec) hipGraphExecDestroy(idx->g_exec);
     if (idx->g_graph) hipGraphDestroy(idx->g_graph);
@@ -779,6 +781,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "sel_lower") idx->sel_lower = value ? 1 : 0;  // per-query allow lists share one block-key launch
     else if (k == "pqa_alone") idx->pqa_alone = value ? 1 : 0;  // unresolved per-query lists searched alone
     else if (k == "pqa_keys") idx->pqa_keys = value ? 1 : 0;    // per-query masked int8 keys
+    else if (k == "batch_rows") idx->batch_rows = value ? 1 : 0;  // batcher: dense lists as slot bitmaps
     else if (k == "pqa_split_max") idx->pqa_split_max = std::max<int64_t>(value, 0);  // sparse lists searched alone
     else if (k == "pqa_budget_mb") idx->pqa_budget_mb = std::max<int64_t>(value, 1);
     else if (k == "scan_window") idx->scan_window = value ? 1 : 0;  // allow lists scan their slot span only
@@ -1840,14 +1843,15 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow_bitmap(wv_index* idx,
 }
 
 // The micro-batcher's filtered requests as slot bitmaps (batcher.hip): row q
-// = rows[q].words words of bits over slots (doc id - id_base), page-locked
-// host memory the kernel reads in place (rows[q].dev), list size rows[q].n.
+// = rows[q].words words of bits over slots (doc id - id_base) in device memory
+// (rows[q].dev; the same bits on the host at rows[q].host), list size rows[q].n.
 static int batch_search_slot_bitmaps(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
                                      const wv_batch_row* rows, uint64_t* out_ids, float* out_dists,
                                      int32_t* out_counts) {
     std::vector<int32_t> modes((size_t)nq, 1);
     std::vector<int64_t> off((size_t)nq + 1, 0);
     for (int64_t q = 0; q < nq; q++) off[(size_t)q + 1] = off[(size_t)q] + std::max<int64_t>(rows[q].n, 0);
+
     std::unique_lock<std::mutex> g(idx->mu);
     PqaFill fill = [&](hipStream_t s, int64_t vq, uint32_t* bits, const int32_t* d_modes) -> int {
         HIPCHK(idx->pqaIds.ensure((size_t)nq * sizeof(wv_batch_row)));
@@ -2108,16 +2112,31 @@ static void* batch_pinned_alloc(size_t bytes) {
     return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;
 }
 static void batch_pinned_free(void* p) { (void)hipHostFree(p); }
-// page-locked rows the device reads in place (the batcher's allow bitmaps)
-static uint32_t* batch_row_alloc(int64_t words, const uint32_t** dev) {
+// device rows for the batcher's allow bitmaps, each filled by its caller's
+// thread on a stream of its own (non-blocking: it does not wait for the
+// search running on idx->stream)
+static uint32_t* batch_row_alloc(wv_index* idx, int64_t words) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, (size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
-        return nullptr;
-    void* dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) { (void)hipHostFree(p); return nullptr; }
-    *dev = static_cast<const uint32_t*>(dp);
-    return static_cast<uint32_t*>(p);
+    if (hipSetDevice(idx->device) != hipSuccess) return nullptr;
+    return hipMalloc(&p, (size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t)) == hipSuccess
+               ? static_cast<uint32_t*>(p) : nullptr;
 }
-static void batch_row_free(uint32_t* p) { (void)hipHostFree(p); }
-static uint64_t batch_id_base(const wv_index* idx) { return idx->id_base; }  // fixed at create
+static void batch_row_free(wv_index* idx, uint32_t* p) {
+    (void)hipSetDevice(idx->device);
+    (void)hipFree(p);
+}
+static int batch_row_upload(wv_index* idx, uint32_t* dev, const uint32_t* host, int64_t words) {
+    HIPCHK(hipSetDevice(idx->device));
+    {
+        std::lock_guard<std::mutex> g(idx->row_mu);
+        if (!idx->row_stream) HIPCHK(hipStreamCreateWithFlags(&idx->row_stream, hipStreamNonBlocking));
+    }
+    HIPCHK(hipMemcpyAsync(dev, host, (size_t)words * sizeof(uint32_t), hipMemcpyHostToDevice, idx->row_stream));
+    HIPCHK(hipStreamSynchronize(idx->row_stream));
+    return WV_OK;
+}
+// the create-time base: id_base itself is shifted by a ScanWindow while a
+// windowed search holds mu, and the callers read this without mu
+static uint64_t batch_id_base(const wv_index* idx) { return idx->id_base0; }
+static bool batch_rows_on(const wv_index* idx) { return idx->batch_rows.load(std::memory_order_relaxed) != 0; }
 #include "batcher.hip"
