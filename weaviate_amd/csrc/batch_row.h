@@ -1,8 +1,7 @@
 // One filtered caller's allow list as a slot bitmap (the micro-batcher,
 // batcher.hip -> k_pqa_from_rows): bit i of word i >> 5 = slot i = doc id
-// id_base + i.  dev: the device row the caller copied it to; host: the same
-// bits on the host (the id-list fallbacks); n: the list's length (its select
-// depth).
+// id_base + i.  host: the caller's page-locked row; dev: the same memory
+// mapped for kernels (read in place); n: the list's length (its select depth).
 #pragma once
 #include <cstdint>
 

@@ -32,21 +32,19 @@ struct wv_batch_req {
     int rc = WV_OK;
     std::string err;
     bool done = false;
-    wv_batch_row row{};   // the list as a slot bitmap (row.dev != nullptr), built by the caller
+    wv_batch_row row{};   // the list as a slot bitmap in a page-locked row (row.host), built by the caller
     int64_t row_cap = 0;
-    std::vector<uint32_t> bits;  // row.host: the bitmap on the host (the id-list fallbacks read it)
 };
 
 // page-locked host memory for the leader's concatenated allow lists (defined
 // by the including unit: hipHostMalloc in the library, malloc in the TSan mock)
 static void* batch_pinned_alloc(size_t bytes);
 static void batch_pinned_free(void* p);
-// device rows for the allow bitmaps (allocated once, pooled), filled by the
-// caller's own copy; and the batch search over them
-// (batch_search_slot_bitmaps, defined by the includer)
-static uint32_t* batch_row_alloc(wv_index* idx, int64_t words);
+// page-locked, device-mapped host rows for the allow bitmaps (allocated once,
+// pooled), filled by the caller's thread and read in place by the leader's
+// search (batch_search_slot_bitmaps, defined by the includer)
+static uint32_t* batch_row_alloc(wv_index* idx, int64_t words, const uint32_t** dev);
 static void batch_row_free(wv_index* idx, uint32_t* p);
-static int batch_row_upload(wv_index* idx, uint32_t* dev, const uint32_t* host, int64_t words);
 static uint64_t batch_id_base(const wv_index* idx);
 static bool batch_rows_on(const wv_index* idx);  // option batch_rows
 
@@ -62,25 +60,26 @@ struct wv_batcher {
     std::vector<wv_batch_req*> pending;
     bool busy = false, in_window = false;
     int64_t calls = 0, launches = 0, max_batch_seen = 0;
-    // free device bitmap rows (reused: an allocation per call would cost more
-    // than the list)
-    struct Row { uint32_t* d; int64_t cap; };
+    // free page-locked bitmap rows (reused: an allocation per call would cost
+    // more than the list)
+    struct Row { uint32_t* h; const uint32_t* d; int64_t cap; };
     std::vector<Row> rows_free;
 };
 
 static void batcher_free(wv_index* idx, wv_batcher* b) {
     if (b && b->pin) batch_pinned_free(b->pin);
     if (b)
-        for (auto& r : b->rows_free) batch_row_free(idx, r.d);
+        for (auto& r : b->rows_free) batch_row_free(idx, r.h);
     delete b;
 }
 
 // A list as a slot bitmap when that is the smaller form (8-byte ids against
 // one bit per slot up to the largest listed slot: lists above ~1/64 of the
-// span): built on the host in bits, copied by this thread into a pooled
-// device row.  False: keep the id list (or, forced, out of memory).
-static bool build_row(wv_index* idx, wv_batcher* b, const uint64_t* ids, int64_t n, std::vector<uint32_t>& bits,
-                      wv_batch_row* row, int64_t* cap, bool force = false) {
+// span): built in cacheable memory, then one sequential copy into a pooled
+// page-locked row (no HIP call here: a caller only spends the list's CPU
+// time).  False: keep the id list (or, forced, out of memory).
+static bool build_row(wv_index* idx, wv_batcher* b, const uint64_t* ids, int64_t n, wv_batch_row* row, int64_t* cap,
+                      bool force = false) {
     if (n <= 0) return false;
     const uint64_t id_base = batch_id_base(idx);
     constexpr uint64_t kSlots = 1ull << 36;  // beyond any index's capacity: such ids are never present
@@ -90,13 +89,14 @@ static bool build_row(wv_index* idx, wv_batcher* b, const uint64_t* ids, int64_t
         if (ids[i] >= id_base && ids[i] - id_base < kSlots) { top = std::max<uint64_t>(top, ids[i] - id_base); any = true; }
     const int64_t words = (int64_t)(top >> 5) + 1;
     if (!force && (!any || 2 * n <= words)) return false;
+    thread_local std::vector<uint32_t> bits;
     bits.assign((size_t)words, 0u);
     for (int64_t i = 0; i < n; i++)
         if (ids[i] >= id_base && ids[i] - id_base < kSlots) {
             const uint64_t sl = ids[i] - id_base;
             bits[sl >> 5] |= 1u << (sl & 31);
         }
-    wv_batcher::Row r{nullptr, 0};
+    wv_batcher::Row r{nullptr, nullptr, 0};
     {
         std::lock_guard<std::mutex> g(b->m);
         for (size_t i = 0; i < b->rows_free.size(); i++)
@@ -106,27 +106,23 @@ static bool build_row(wv_index* idx, wv_batcher* b, const uint64_t* ids, int64_t
                 break;
             }
     }
-    if (!r.d) {
+    if (!r.h) {
         r.cap = (words + 1023) / 1024 * 1024;
-        r.d = batch_row_alloc(idx, r.cap);
-        if (!r.d) return false;
+        r.h = batch_row_alloc(idx, r.cap, &r.d);
+        if (!r.h) return false;
     }
-    if (batch_row_upload(idx, r.d, bits.data(), words) != WV_OK) {
-        std::lock_guard<std::mutex> g(b->m);
-        b->rows_free.push_back(r);
-        return false;
-    }
-    *row = wv_batch_row{r.d, bits.data(), words, n};
+    memcpy(r.h, bits.data(), (size_t)words * sizeof(uint32_t));
+    *row = wv_batch_row{r.d, r.h, words, n};
     *cap = r.cap;
     return true;
 }
 
 static void release_row(wv_batcher* b, wv_batch_row* row, int64_t cap) {
-    if (!row->dev) return;
+    if (!row->host) return;
     std::lock_guard<std::mutex> g(b->m);
-    b->rows_free.push_back({const_cast<uint32_t*>(row->dev), cap});
-    row->dev = nullptr;
+    b->rows_free.push_back({const_cast<uint32_t*>(row->host), row->dev, cap});
     row->host = nullptr;
+    row->dev = nullptr;
 }
 
 static wv_batcher* get_batcher(wv_index* idx) {
@@ -156,23 +152,22 @@ static int launch_requests(wv_index* idx, wv_batcher* b, const std::vector<wv_ba
     if (!lists || n == 1) {
         rc = wv_index_search_by_vector_batch(idx, q.data(), n, d, k, grp[0]->allow_ids, grp[0]->n_allow,
                                              grp[0]->allow_mode, ids.data(), dists.data(), cnt.data());
-    } else if (std::any_of(grp.begin(), grp.end(), [](wv_batch_req* r) { return r->row.dev != nullptr; })) {
+    } else if (std::any_of(grp.begin(), grp.end(), [](wv_batch_req* r) { return r->row.host != nullptr; })) {
         // the lists as slot bitmaps read in place by the device: the callers
         // built theirs; the leader builds the (sparse) rest
         std::vector<wv_batch_row> rows((size_t)n);
         std::vector<std::pair<wv_batch_row, int64_t>> mine;
-        std::vector<std::vector<uint32_t>> mine_bits((size_t)n);  // their host bitmaps (data() stays put)
         rc = WV_OK;
         for (int64_t i = 0; i < n && !rc; i++) {
             wv_batch_req* r = grp[i];
-            if (r->row.dev) {
+            if (r->row.host) {
                 rows[(size_t)i] = r->row;
                 continue;
             }
             wv_batch_row row{nullptr, nullptr, 0, r->n_allow};
             int64_t cap = 0;
             if (r->n_allow > 0) {  // a sparse list: a row of its own all the same
-                if (!build_row(idx, b, r->allow_ids, r->n_allow, mine_bits[(size_t)i], &row, &cap, true)) {
+                if (!build_row(idx, b, r->allow_ids, r->n_allow, &row, &cap, true)) {
                     rc = set_err(WV_ERR_HIP, "could not stage the batch's allow bitmaps");
                     break;
                 }
@@ -271,7 +266,7 @@ extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int6
     // a dense list: its slot bitmap, built here (in parallel with the other
     // callers) instead of by the leader
     if (allow_mode == 1 && n_allow > 0 && batch_rows_on(idx))
-        build_row(idx, b, allow_ids, n_allow, req.bits, &req.row, &req.row_cap);
+        build_row(idx, b, allow_ids, n_allow, &req.row, &req.row_cap);
     std::unique_lock<std::mutex> lk(b->m);
     b->calls++;
     b->pending.push_back(&req);

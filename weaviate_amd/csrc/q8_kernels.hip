@@ -110,8 +110,8 @@ __global__ void k_pqa_from_bits(const uint32_t* __restrict__ raw, int64_t sw, in
 }
 
 // per-query bitmaps from the micro-batcher's slot-bitmap rows (batch_row.h:
-// device rows the callers filled); ANDed with present.  Thread per (query,
-// word).
+// page-locked rows the callers filled, read in place); ANDed with present.
+// Thread per (query, word).
 __global__ void k_pqa_from_rows(const wv_batch_row* __restrict__ rows, const int32_t* __restrict__ modes, int64_t nq,
                                 const uint32_t* __restrict__ present, int64_t vq, uint32_t* __restrict__ bits) {
     const int64_t n = nq * vq;

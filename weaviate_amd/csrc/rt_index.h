@@ -88,8 +88,6 @@ static void batcher_free(wv_index* idx, wv_batcher* b);
 
 struct wv_index {
     std::mutex mu;
-    std::mutex row_mu;                 // creates row_stream (the batcher's callers copy their allow bitmaps on it)
-    hipStream_t row_stream = nullptr;
     int metric = WV_METRIC_COSINE_DOT;
     int variant = WV_VARIANT_AVX256;
     int compression = WV_COMPRESSION_NONE;

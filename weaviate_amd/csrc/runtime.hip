@@ -155,7 +155,6 @@ extern "C" void wv_index_destroy(wv_index* idx) {
     if (idx->sub) wv_index_destroy(idx->sub);
     hipSetDevice(idx->device);
     batcher_free(idx, idx->batcher);
-    if (idx->row_stream) hipStreamDestroy(idx->row_stream);
     if (idx->stream) hipStreamSynchronize(idx->stream);
     if (idx->g_exec) hipGraphExecDestroy(idx->g_exec);
     if (idx->g_graph) hipGraphDestroy(idx->g_graph);
@@ -1843,8 +1842,8 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow_bitmap(wv_index* idx,
 }
 
 // The micro-batcher's filtered requests as slot bitmaps (batcher.hip): row q
-// = rows[q].words words of bits over slots (doc id - id_base) in device memory
-// (rows[q].dev; the same bits on the host at rows[q].host), list size rows[q].n.
+// = rows[q].words words of bits over slots (doc id - id_base) in page-locked
+// host memory the kernel reads in place (rows[q].dev); list size rows[q].n.
 static int batch_search_slot_bitmaps(wv_index* idx, const float* queries, int64_t nq, int64_t d, int32_t k,
                                      const wv_batch_row* rows, uint64_t* out_ids, float* out_dists,
                                      int32_t* out_counts) {
@@ -2112,28 +2111,23 @@ static void* batch_pinned_alloc(size_t bytes) {
     return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;
 }
 static void batch_pinned_free(void* p) { (void)hipHostFree(p); }
-// device rows for the batcher's allow bitmaps, each filled by its caller's
-// thread on a stream of its own (non-blocking: it does not wait for the
-// search running on idx->stream)
-static uint32_t* batch_row_alloc(wv_index* idx, int64_t words) {
+// page-locked rows for the batcher's allow bitmaps, mapped for kernels and
+// fine-grained: the callers rewrite a row for each list and the search reads
+// it in place (k_pqa_from_rows), so the device must not keep a cached copy
+static uint32_t* batch_row_alloc(wv_index* idx, int64_t words, const uint32_t** dev) {
     void* p = nullptr;
-    if (hipSetDevice(idx->device) != hipSuccess) return nullptr;
-    return hipMalloc(&p, (size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t)) == hipSuccess
-               ? static_cast<uint32_t*>(p) : nullptr;
+    (void)idx;
+    if (hipHostMalloc(&p, (size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return nullptr;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) { (void)hipHostFree(p); return nullptr; }
+    *dev = static_cast<const uint32_t*>(dp);
+    return static_cast<uint32_t*>(p);
 }
 static void batch_row_free(wv_index* idx, uint32_t* p) {
-    (void)hipSetDevice(idx->device);
-    (void)hipFree(p);
-}
-static int batch_row_upload(wv_index* idx, uint32_t* dev, const uint32_t* host, int64_t words) {
-    HIPCHK(hipSetDevice(idx->device));
-    {
-        std::lock_guard<std::mutex> g(idx->row_mu);
-        if (!idx->row_stream) HIPCHK(hipStreamCreateWithFlags(&idx->row_stream, hipStreamNonBlocking));
-    }
-    HIPCHK(hipMemcpyAsync(dev, host, (size_t)words * sizeof(uint32_t), hipMemcpyHostToDevice, idx->row_stream));
-    HIPCHK(hipStreamSynchronize(idx->row_stream));
-    return WV_OK;
+    (void)idx;
+    (void)hipHostFree(p);
 }
 // the create-time base: id_base itself is shifted by a ScanWindow while a
 // windowed search holds mu, and the callers read this without mu
