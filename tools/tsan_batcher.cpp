@@ -101,12 +101,12 @@ extern "C" int wv_index_search_by_vector_batch_multi_allow(wv_index* idx, const 
 
 static void* batch_pinned_alloc(size_t bytes) { return malloc(bytes); }
 static void batch_pinned_free(void* p) { free(p); }
-static uint32_t* batch_row_alloc(wv_index*, int64_t words, const uint32_t** dev) {
+static uint32_t* batch_row_alloc(int64_t words, const uint32_t** dev) {
     uint32_t* p = static_cast<uint32_t*>(malloc((size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t)));
     *dev = p;
     return p;
 }
-static void batch_row_free(wv_index*, uint32_t* p) { free(p); }
+static void batch_row_free(uint32_t* p) { free(p); }
 static uint64_t batch_id_base(const wv_index*) { return 0; }
 static bool batch_rows_on(const wv_index*) { return true; }
 

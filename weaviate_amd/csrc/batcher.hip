@@ -43,8 +43,8 @@ static void batch_pinned_free(void* p);
 // page-locked, device-mapped host rows for the allow bitmaps (allocated once,
 // pooled), filled by the caller's thread and read in place by the leader's
 // search (batch_search_slot_bitmaps, defined by the includer)
-static uint32_t* batch_row_alloc(wv_index* idx, int64_t words, const uint32_t** dev);
-static void batch_row_free(wv_index* idx, uint32_t* p);
+static uint32_t* batch_row_alloc(int64_t words, const uint32_t** dev);
+static void batch_row_free(uint32_t* p);
 static uint64_t batch_id_base(const wv_index* idx);
 static bool batch_rows_on(const wv_index* idx);  // option batch_rows
 
@@ -60,18 +60,40 @@ struct wv_batcher {
     std::vector<wv_batch_req*> pending;
     bool busy = false, in_window = false;
     int64_t calls = 0, launches = 0, max_batch_seen = 0;
-    // free page-locked bitmap rows (reused: an allocation per call would cost
-    // more than the list)
+    // free page-locked bitmap rows for the leader's sparse lists (reused: an
+    // allocation per call would cost more than the list); own mutex
     struct Row { uint32_t* h; const uint32_t* d; int64_t cap; };
+    std::mutex pool_m;
     std::vector<Row> rows_free;
 };
 
 static void batcher_free(wv_index* idx, wv_batcher* b) {
+    (void)idx;
     if (b && b->pin) batch_pinned_free(b->pin);
     if (b)
-        for (auto& r : b->rows_free) batch_row_free(idx, r.h);
+        for (auto& r : b->rows_free) batch_row_free(r.h);
     delete b;
 }
+
+// each calling thread's own row, kept across its calls (a thread has one call
+// in flight, so no lock and no pool traffic per call).  At thread exit the row
+// goes to a process-wide list the next new thread takes from -- never freed
+// there: a thread-exit destructor may run after the HIP runtime is gone
+struct wv_thread_row {
+    uint32_t* h = nullptr;
+    const uint32_t* d = nullptr;
+    int64_t cap = 0;
+    static std::mutex& spare_m() { static std::mutex* m = new std::mutex; return *m; }
+    static std::vector<wv_batcher::Row>& spare() {
+        static std::vector<wv_batcher::Row>* v = new std::vector<wv_batcher::Row>;
+        return *v;
+    }
+    ~wv_thread_row() {
+        if (!h) return;
+        std::lock_guard<std::mutex> g(spare_m());
+        spare().push_back({h, d, cap});
+    }
+};
 
 // A list as a slot bitmap when that is the smaller form (8-byte ids against
 // one bit per slot up to the largest listed slot: lists above ~1/64 of the
@@ -80,6 +102,8 @@ static void batcher_free(wv_index* idx, wv_batcher* b) {
 // time).  False: keep the id list (or, forced, out of memory).
 static bool build_row(wv_index* idx, wv_batcher* b, const uint64_t* ids, int64_t n, wv_batch_row* row, int64_t* cap,
                       bool force = false) {
+    // force (the leader's sparse lists): a pooled row, *cap its capacity;
+    // otherwise the calling thread's own row, *cap = -1 (nothing to release)
     if (n <= 0) return false;
     const uint64_t id_base = batch_id_base(idx);
     constexpr uint64_t kSlots = 1ull << 36;  // beyond any index's capacity: such ids are never present
@@ -96,20 +120,45 @@ static bool build_row(wv_index* idx, wv_batcher* b, const uint64_t* ids, int64_t
             const uint64_t sl = ids[i] - id_base;
             bits[sl >> 5] |= 1u << (sl & 31);
         }
+    (void)idx;
     wv_batcher::Row r{nullptr, nullptr, 0};
-    {
-        std::lock_guard<std::mutex> g(b->m);
-        for (size_t i = 0; i < b->rows_free.size(); i++)
-            if (b->rows_free[i].cap >= words) {
-                r = b->rows_free[i];
-                b->rows_free.erase(b->rows_free.begin() + (std::ptrdiff_t)i);
-                break;
+    if (!force) {
+        thread_local wv_thread_row mine;
+        if (mine.cap < words) {
+            if (mine.h) batch_row_free(mine.h);
+            mine.h = nullptr;
+            {
+                std::lock_guard<std::mutex> g(wv_thread_row::spare_m());
+                auto& sp = wv_thread_row::spare();
+                for (size_t i = 0; i < sp.size(); i++)
+                    if (sp[i].cap >= words) {
+                        mine.h = sp[i].h; mine.d = sp[i].d; mine.cap = sp[i].cap;
+                        sp.erase(sp.begin() + (std::ptrdiff_t)i);
+                        break;
+                    }
             }
-    }
-    if (!r.h) {
-        r.cap = (words + 1023) / 1024 * 1024;
-        r.h = batch_row_alloc(idx, r.cap, &r.d);
-        if (!r.h) return false;
+            if (!mine.h) {
+                mine.cap = (words + 1023) / 1024 * 1024;
+                mine.h = batch_row_alloc(mine.cap, &mine.d);
+                if (!mine.h) { mine.cap = 0; return false; }
+            }
+        }
+        r = wv_batcher::Row{mine.h, mine.d, -1};
+    } else {
+        {
+            std::lock_guard<std::mutex> g(b->pool_m);
+            for (size_t i = 0; i < b->rows_free.size(); i++)
+                if (b->rows_free[i].cap >= words) {
+                    r = b->rows_free[i];
+                    b->rows_free.erase(b->rows_free.begin() + (std::ptrdiff_t)i);
+                    break;
+                }
+        }
+        if (!r.h) {
+            r.cap = (words + 1023) / 1024 * 1024;
+            r.h = batch_row_alloc(r.cap, &r.d);
+            if (!r.h) return false;
+        }
     }
     memcpy(r.h, bits.data(), (size_t)words * sizeof(uint32_t));
     *row = wv_batch_row{r.d, r.h, words, n};
@@ -118,8 +167,8 @@ static bool build_row(wv_index* idx, wv_batcher* b, const uint64_t* ids, int64_t
 }
 
 static void release_row(wv_batcher* b, wv_batch_row* row, int64_t cap) {
-    if (!row->host) return;
-    std::lock_guard<std::mutex> g(b->m);
+    if (!row->host || cap < 0) return;  // (a thread's own row stays with the thread)
+    std::lock_guard<std::mutex> g(b->pool_m);
     b->rows_free.push_back({const_cast<uint32_t*>(row->host), row->dev, cap});
     row->host = nullptr;
     row->dev = nullptr;

@@ -2114,21 +2114,17 @@ static void batch_pinned_free(void* p) { (void)hipHostFree(p); }
 // page-locked rows for the batcher's allow bitmaps, mapped for kernels and
 // fine-grained: the callers rewrite a row for each list and the search reads
 // it in place (k_pqa_from_rows), so the device must not keep a cached copy
-static uint32_t* batch_row_alloc(wv_index* idx, int64_t words, const uint32_t** dev) {
+static uint32_t* batch_row_alloc(int64_t words, const uint32_t** dev) {
     void* p = nullptr;
-    (void)idx;
     if (hipHostMalloc(&p, (size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t),
-                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+                      hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
         return nullptr;
     void* dp = nullptr;
     if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) { (void)hipHostFree(p); return nullptr; }
     *dev = static_cast<const uint32_t*>(dp);
     return static_cast<uint32_t*>(p);
 }
-static void batch_row_free(wv_index* idx, uint32_t* p) {
-    (void)idx;
-    (void)hipHostFree(p);
-}
+static void batch_row_free(uint32_t* p) { (void)hipHostFree(p); }
 // the create-time base: id_base itself is shifted by a ScanWindow while a
 // windowed search holds mu, and the callers read this without mu
 static uint64_t batch_id_base(const wv_index* idx) { return idx->id_base0; }
