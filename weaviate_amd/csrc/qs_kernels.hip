@@ -2727,7 +2727,33 @@ __global__ __launch_bounds__(64) void k_rp_heap(const float* __restrict__ key, i
                         const uint32_t vmb = (uint32_t)__shfl((int)vm, 2 * u + lh);
                         if (((vmb >> li) & 1u) && (open || top > cur[u])) cb |= 1u << u;
                     }
-                    if (__any(cb != 0)) {
+                    if (open && __any(cb != 0)) {
+                        // the heap is still short: block by block with the top
+                        // re-read (as it fills, a window-wide test admits every row)
+#pragma unroll
+                        for (int u = 0; u < RPW / 2; u++) sE[lane + 64 * u] = cur[u];
+                        sBlk[lane] = blk;
+                        wave_sync_lds();
+                        for (int j = 0; j < nwin; j++) {
+                            const int lj = *s_len;
+                            const float tj = lj > 0 ? hd[0] : 0.f;
+                            const uint32_t vmj = (uint32_t)__shfl((int)vm, j);
+                            const float dist = lane < 32 ? sE[j * 32 + lane] : 0.f;
+                            uint64_t mask = __ballot(lane < 32 && ((vmj >> lane) & 1u) && (lj < k || tj > dist));
+                            if (mask == 0) continue;
+                            if (lane == 0) {
+                                ReplayHeap h{hid, hd, lj};
+                                while (mask) {
+                                    const int l = __builtin_ctzll(mask);
+                                    mask &= mask - 1;
+                                    ins(h, id_base + (uint64_t)sBlk[j] * 32 + (uint64_t)l, sE[j * 32 + l]);
+                                }
+                                *s_len = h.len;
+                            }
+                            wave_sync_lds();
+                        }
+                        wave_sync_lds();
+                    } else if (__any(cb != 0)) {
 #pragma unroll
                         for (int u = 0; u < RPW / 2; u++) sE[lane + 64 * u] = cur[u];
                         sBlk[lane] = blk;
