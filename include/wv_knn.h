@@ -153,8 +153,10 @@ int wv_index_search_by_vector_batch(wv_index *idx, const float *queries, int64_t
  * allow_offsets has nq+1 entries.  Results equal nq one-query calls of
  * wv_index_search_by_vector_batch (the concurrent filtered callers of
  * shard_read.go:415-424 in one launch); options "pqa" (default 1: one shared
- * block-key launch over the lists' union) and "pqa_budget_mb" (per-query
- * bitmap memory per launch, default 4096). */
+ * block-key launch over the lists' union), "pqa_keys" (default 1: int8 dot /
+ * cosine keys up to 768 dims masked per query, so each query's keys cover its
+ * own rows only) and "pqa_budget_mb" (per-query bitmap memory per launch,
+ * default 4096). */
 int wv_index_search_by_vector_batch_multi_allow(wv_index *idx, const float *queries, int64_t nq, int64_t d,
                                                 int32_t k, const uint64_t *allow_ids, const int64_t *allow_offsets,
                                                 const int32_t *allow_modes, uint64_t *out_ids, float *out_dists,
@@ -178,8 +180,11 @@ int wv_index_search_by_vector_batch_multi_allow_bitmap(wv_index *idx, const floa
  * "batch_window_us" option (default 0) for company, at most "batch_max"
  * (default 4096) queries per launch, grouped by (d, k); requests carrying
  * their own allow lists share a launch through
- * wv_index_search_by_vector_batch_multi_allow.  Results and errors equal those
- * of a one-query wv_index_search_by_vector_batch.  out_ids/out_dists capacity k. */
+ * wv_index_search_by_vector_batch_multi_allow (a dense list -- over 1/64 of
+ * its slot span -- travels as a slot bitmap the calling thread builds in a
+ * page-locked row of its own, option "batch_rows", default 1).  Results and
+ * errors equal those of a one-query wv_index_search_by_vector_batch.
+ * out_ids/out_dists capacity k. */
 int wv_index_search_by_vector(wv_index *idx, const float *query, int64_t d, int32_t k, const uint64_t *allow_ids,
                               int64_t n_allow, int32_t allow_mode, uint64_t *out_ids, float *out_dists,
                               int32_t *out_count);
