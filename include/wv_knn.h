@@ -177,8 +177,9 @@ int wv_index_search_by_vector_batch_multi_allow_bitmap(wv_index *idx, const floa
  * goroutine makes (shard_read.go:415-424).  Thread-safe; concurrent callers on
  * one index are coalesced into batched launches (micro-batcher, batcher.hip):
  * a caller that finds no batch running leads the next one, waiting up to the
- * "batch_window_us" option (default 0) for company, at most "batch_max"
- * (default 4096) queries per launch, grouped by (d, k); requests carrying
+ * "batch_window_us" option (default 1000) for company -- and no longer once as
+ * many callers are pending as were in the system during the previous batch --
+ * at most "batch_max" (default 4096) queries per launch, grouped by (d, k); requests carrying
  * their own allow lists share a launch through
  * wv_index_search_by_vector_batch_multi_allow (a dense list -- over 1/64 of
  * its slot span -- travels as a slot bitmap the calling thread builds in a

@@ -3,7 +3,7 @@
 // buffers -- how the cgo shim's goroutines would call it) on the C3 corpus for
 // S seconds; prints one JSON line with QPS, launches, mean batch and latency.
 // Build: hipcc -O2 -std=c++17 tools/serve_bench.cpp -Iinclude -Lweaviate_amd -lwvknn -Wl,-rpath,'$ORIGIN/../weaviate_amd' -o tools/serve_bench
-// Run:   tools/serve_bench [n=10000000] [threads=256] [seconds=10] [window_us=0] [allow_pct=0] [filtered_pct=100]
+// Run:   tools/serve_bench [n=10000000] [threads=256] [seconds=10] [window_us=1000, the library default] [allow_pct=0] [filtered_pct=100]
 // allow_pct > 0: filtered_pct % of the threads search under their own allow
 // list (a random allow_pct % of the ids, different per thread) -- filtered
 // callers, batched through wv_index_search_by_vector_batch_multi_allow; the
@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     const int64_t n = argc > 1 ? atoll(argv[1]) : 10000000;
     const int T = argc > 2 ? atoi(argv[2]) : 256;
     const double secs = argc > 3 ? atof(argv[3]) : 10.0;
-    const int64_t window = argc > 4 ? atoll(argv[4]) : 0;
+    const int64_t window = argc > 4 ? atoll(argv[4]) : 1000;
     const double allow_pct = argc > 5 ? atof(argv[5]) : 0.0;
     const double filtered_pct = argc > 6 ? atof(argv[6]) : 100.0;
     const int d = 768, k = 10, nq = 4096;

@@ -7,13 +7,19 @@
 // while a batch of B queries costs the same HBM pass plus MFMA work.  So
 // concurrent callers are coalesced: leader/follower, no background thread.
 // A caller enqueues its request; if no batch is running it becomes the
-// leader, optionally waits batch_window_us for company, takes every pending
+// leader, optionally waits batch_window_us for company (at most until as many
+// callers are pending as were in the system during the last batch), takes every pending
 // request, groups them by (d, k), runs each group's unfiltered requests
 // through wv_index_search_by_vector_batch and its filtered ones through
 // wv_index_search_by_vector_batch_multi_allow (each query its own list, one
 // block-key launch) and hands every follower its rows.  Requests
 // that arrive while a batch runs form the next batch.  Results are identical
 // to individual calls: each query of a batch is searched independently.
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 
@@ -31,7 +37,10 @@ struct wv_batch_req {
     int32_t* out_count;
     int rc = WV_OK;
     std::string err;
-    bool done = false;
+    // 0 = waiting, 1 = done (results written), 2 = lead the next batch; the
+    // caller sleeps on this word alone (futex), so a finished batch wakes its
+    // callers without a herd on the batcher's mutex
+    std::atomic<int> sig{0};
     wv_batch_row row{};   // the list as a slot bitmap in a page-locked row (row.host), built by the caller
     int64_t row_cap = 0;
 };
@@ -55,17 +64,32 @@ struct wv_batcher {
     // per launch); only the leader touches it
     uint64_t* pin = nullptr;
     size_t pin_cap = 0;
-    std::condition_variable cv;         // followers: their batch is done / leader slot free
     std::condition_variable cv_window;  // the leader waiting out batch_window_us
+    int64_t want = 0;                   // ... until this many requests are pending
     std::vector<wv_batch_req*> pending;
     bool busy = false, in_window = false;
     int64_t calls = 0, launches = 0, max_batch_seen = 0;
+    // callers in the system (pending + in the running batch): the most seen
+    // since the last launch, and the running batch's size.  A leader inside its
+    // window stops waiting once that many are pending (the callers it just
+    // served are coming back), so the pipeline settles on one full batch per
+    // cycle instead of two half batches alternating
+    int64_t in_system = 0, running = 0;
     // free page-locked bitmap rows for the leader's sparse lists (reused: an
     // allocation per call would cost more than the list); own mutex
     struct Row { uint32_t* h; const uint32_t* d; int64_t cap; };
     std::mutex pool_m;
     std::vector<Row> rows_free;
 };
+
+static void batch_futex_wait(std::atomic<int>* w, int v) {
+    syscall(SYS_futex, reinterpret_cast<int*>(w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+// the word may belong to a request whose caller has already returned (it saw
+// the store first): waking a stale address is harmless, nothing is dereferenced
+static void batch_futex_wake(std::atomic<int>* w) {
+    syscall(SYS_futex, reinterpret_cast<int*>(w), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
 
 static void batcher_free(wv_index* idx, wv_batcher* b) {
     (void)idx;
@@ -301,6 +325,13 @@ static void run_batch(wv_index* idx, wv_batcher* b, std::vector<wv_batch_req*>& 
     for (auto& g : groups) run_group(idx, b, g);
 }
 
+// a caller's request is done: its row back, its own error text
+static int finish_req(wv_batcher* b, wv_batch_req* req) {
+    release_row(b, &req->row, req->row_cap);
+    if (req->rc) return set_err(req->rc, "%s", req->err.c_str());
+    return WV_OK;
+}
+
 extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int64_t d, int32_t k,
                                          const uint64_t* allow_ids, int64_t n_allow, int32_t allow_mode,
                                          uint64_t* out_ids, float* out_dists, int32_t* out_count) {
@@ -319,40 +350,64 @@ extern "C" int wv_index_search_by_vector(wv_index* idx, const float* query, int6
     std::unique_lock<std::mutex> lk(b->m);
     b->calls++;
     b->pending.push_back(&req);
-    // only a leader inside its batch window wants to hear about arrivals (waking
-    // every waiting follower per arrival would cost O(callers^2) wakeups)
-    if (b->in_window) b->cv_window.notify_one();
-    while (!req.done) {
-        if (!b->busy) {
-            // become the leader for the next batch
-            b->busy = true;
-            const int64_t window = idx->batch_window_us;
-            if (window > 0 && (int64_t)b->pending.size() < idx->batch_max) {
-                b->in_window = true;
-                b->cv_window.wait_for(lk, std::chrono::microseconds(window),
-                                      [&] { return (int64_t)b->pending.size() >= idx->batch_max; });
-                b->in_window = false;
-            }
-            std::vector<wv_batch_req*> batch;
-            const size_t take = std::min(b->pending.size(), (size_t)std::max<int64_t>(idx->batch_max, 1));
-            batch.assign(b->pending.begin(), b->pending.begin() + take);
-            b->pending.erase(b->pending.begin(), b->pending.begin() + take);
-            b->launches++;
-            b->max_batch_seen = std::max<int64_t>(b->max_batch_seen, (int64_t)batch.size());
+    b->in_system = std::max<int64_t>(b->in_system, (int64_t)b->pending.size() + b->running);
+    // only a leader inside its batch window wants to hear about arrivals, and
+    // only about the one that completes its batch
+    if (b->in_window && (int64_t)b->pending.size() >= b->want) b->cv_window.notify_one();
+    bool lead = !b->busy;
+    if (lead) b->busy = true;
+    for (;;) {
+        if (!lead) {
+            // a follower: sleeps on its own word until its batch is done (1) or
+            // the leader's slot is handed to it (2, busy stays reserved for it)
             lk.unlock();
-            run_batch(idx, b, batch);
+            int st;
+            while ((st = req.sig.load(std::memory_order_acquire)) == 0) batch_futex_wait(&req.sig, 0);
+            if (st == 1) return finish_req(b, &req);
+            req.sig.store(0, std::memory_order_relaxed);
             lk.lock();
-            for (wv_batch_req* r : batch) r->done = true;
-            b->busy = false;
-            b->cv.notify_all();
-        } else {
-            b->cv.wait(lk);
         }
+        const int64_t window = idx->batch_window_us;
+        const int64_t want = std::min<int64_t>(idx->batch_max, std::max<int64_t>(b->in_system, 1));
+        if (window > 0 && (int64_t)b->pending.size() < want) {
+            b->in_window = true;
+            b->want = want;
+            b->cv_window.wait_for(lk, std::chrono::microseconds(window),
+                                  [&] { return (int64_t)b->pending.size() >= want; });
+            b->in_window = false;
+        }
+        std::vector<wv_batch_req*> batch;
+        const size_t take = std::min(b->pending.size(), (size_t)std::max<int64_t>(idx->batch_max, 1));
+        batch.assign(b->pending.begin(), b->pending.begin() + take);
+        b->pending.erase(b->pending.begin(), b->pending.begin() + take);
+        b->running = (int64_t)take;
+        b->in_system = (int64_t)(take + b->pending.size());
+        b->launches++;
+        b->max_batch_seen = std::max<int64_t>(b->max_batch_seen, (int64_t)batch.size());
+        lk.unlock();
+        run_batch(idx, b, batch);
+        lk.lock();
+        b->running = 0;
+        // the leader's slot goes to the oldest pending request (possibly our own,
+        // when the batch was capped at batch_max before it)
+        wv_batch_req* next = b->pending.empty() ? nullptr : b->pending.front();
+        if (!next) b->busy = false;
+        lk.unlock();
+        if (next && next != &req) {
+            next->sig.store(2, std::memory_order_release);
+            batch_futex_wake(&next->sig);
+        }
+        bool mine = false;
+        for (wv_batch_req* r : batch) {
+            if (r == &req) { mine = true; continue; }
+            std::atomic<int>* w = &r->sig;
+            w->store(1, std::memory_order_release);
+            batch_futex_wake(w);
+        }
+        if (mine) return finish_req(b, &req);
+        lk.lock();
+        lead = next == &req;
     }
-    lk.unlock();
-    release_row(b, &req.row, req.row_cap);
-    if (req.rc) return set_err(req.rc, "%s", req.err.c_str());
-    return WV_OK;
 }
 
 extern "C" int wv_index_batcher_stats(wv_index* idx, int64_t* out) {

@@ -290,7 +290,7 @@ struct wv_index {
     // micro-batcher of concurrent single-query searches (batcher.hip)
     wv_batcher* batcher = nullptr;
     // written by set_option under mu, read by the batcher leader without it
-    std::atomic<int64_t> batch_window_us{0}, batch_max{4096};
+    std::atomic<int64_t> batch_window_us{1000}, batch_max{4096};
     int gemv_max = 8, gemv_wg = 1024, exact_multi = 1;  // batches up to this many queries take the GEMV select kernel (kver 6)
 };
 
