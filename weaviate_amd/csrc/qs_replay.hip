@@ -34,7 +34,7 @@ int launch_blk_replay(wv_index* idx, hipStream_t s, const float* key, int64_t ld
     // form's three launches.  A host list (counters NULL: the cross-shard
     // replay's flagged queries, every one of which replays) takes the pooled
     // form: 9 flagged C3 queries on a 1.25M-row shard 2.8 -> 0.5 ms
-    const bool few = counters && max_list <= 16 && !rec_i && k < 64 && nch <= RP_MAXCH && idx->replay_par;
+    const bool few = counters && max_list <= idx->rp_few && !rec_i && k < 64 && nch <= RP_MAXCH && idx->replay_par;
     if (ub_ok && !few && blk_pooled(idx, k, nb)) {
         // pooled form: bounds + candidate pool (8 waves per query), exact
         // distances over the whole grid, one-wave heap per query

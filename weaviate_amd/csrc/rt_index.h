@@ -157,6 +157,7 @@ struct wv_index {
     int q8_gemv = 1;                // option q8_gemv: batches of <= 32 queries stream the int8 plane through registers (k_q8_gemv)
     int q8_live = 1;                // option q8_live: waves of a partial query group's padding skip their MFMAs (k_q8_blockkey LIVE)
     int q8_prio = 0;                // option q8_prio: s_setprio 1 for waves 4-7 of k_q8_blockkey (experiment)
+    int rp_few = 16;                // option rp_few: a device-counted replay list of at most this many queries takes k_blk_replay_par
     int q8_filter = 1;              // option q8_filter: the exact pass bounds rows from the int8 plane (1) or bf16 (0)
     unsigned char* X8 = nullptr;
     float* sb8 = nullptr;

@@ -780,6 +780,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "sel_lower") idx->sel_lower = value ? 1 : 0;  // per-query allow lists share one block-key launch
     else if (k == "pqa_alone") idx->pqa_alone = value ? 1 : 0;  // unresolved per-query lists searched alone
     else if (k == "pqa_keys") idx->pqa_keys = value ? 1 : 0;    // per-query masked int8 keys
+    else if (k == "rp_few") idx->rp_few = value;  // replay lists up to this long (device-counted) take the one-launch form
     else if (k == "batch_rows") idx->batch_rows = value ? 1 : 0;  // batcher: dense lists as slot bitmaps
     else if (k == "pqa_split_max") idx->pqa_split_max = std::max<int64_t>(value, 0);  // sparse lists searched alone
     else if (k == "pqa_budget_mb") idx->pqa_budget_mb = std::max<int64_t>(value, 1);
@@ -1335,7 +1336,7 @@ static int subindex_build(wv_index* idx, hipStream_t s, const std::vector<uint32
     set_dims(sb, idx->dims);
     sb->kernel_opt = idx->kernel_opt; sb->q8_opt = idx->q8_opt; sb->q8_R = idx->q8_R; sb->q8_filter = idx->q8_filter;
     sb->q8_stag = idx->q8_stag; sb->q8_shape = idx->q8_shape; sb->q8_pf = idx->q8_pf; sb->exact_filter = idx->exact_filter; sb->exact_bm = idx->exact_bm; sb->q8_bm = idx->q8_bm; sb->q8_gemv = idx->q8_gemv; sb->q8_live = idx->q8_live; sb->q8_prio = idx->q8_prio; sb->sel_split_max = idx->sel_split_max; sb->q8_bm_min = idx->q8_bm_min;
-    sb->exact_cap = idx->exact_cap; sb->replay_par = idx->replay_par; sb->margin = idx->margin;
+    sb->exact_cap = idx->exact_cap; sb->replay_par = idx->replay_par; sb->rp_few = idx->rp_few; sb->margin = idx->margin;
     sb->gemv_max = idx->gemv_max; sb->gemv_wg = idx->gemv_wg; sb->exact_multi = idx->exact_multi;
     sb->force_replay = idx->force_replay; sb->qs_force_flag = idx->qs_force_flag; sb->timing = idx->timing;
     sb->hiwater = 0;
