@@ -610,7 +610,9 @@ int wv_index_debug_bqmin(wv_index *idx, int64_t q, float *mins, int64_t *nblk, i
  * replay), "spans" (0 = auto), "kernel" (0 = auto: 7 = bf16 block-key path
  * (qs_kernels.hip, the default for the exact fp32 search up to 1536 dims),
  * 6 = HBM-streaming GEMV, 3 = f32 MFMA select; other values are rejected),
- * "replay_par" (flagged-query replay form, default 2), "exact_bm" / "exact_cap"
+ * "replay_par" (flagged-query replay form, default 2), "rp_few" (device-counted
+ * replay lists up to this long take the one-launch 8-wave form, default 16),
+ * "exact_bm" / "exact_cap"
  * / "exact_filter" (block-key exact pass forms; exact_filter 1 = bf16-plane row
  * bound in the capped pass, default), "replay_dbg" (1 = clock diagnostics of
  * the one-wave replay, printed), "pq_cand" (1 = minima-only PQ search, 0 = the
