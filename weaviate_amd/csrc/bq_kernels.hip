@@ -186,7 +186,8 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
                                                   const float* __restrict__ in_d, const int32_t* __restrict__ in_len,
                                                   int pop, uint64_t* __restrict__ out_ids, float* __restrict__ out_d,
                                                   int32_t* __restrict__ out_n, uint64_t* __restrict__ rec_ids,
-                                                  float* __restrict__ rec_d, int32_t* __restrict__ rec_n, int cap) {
+                                                  float* __restrict__ rec_d, int32_t* __restrict__ rec_n, int cap,
+                                                  const int32_t* __restrict__ skip) {
     // dynamic LDS: [R] heap records (PHeap) | [64] f32 | len
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     HeapRec* hr = reinterpret_cast<HeapRec*>(rsm);
@@ -195,6 +196,7 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
     const int lane = threadIdx.x;
     const int li = blockIdx.x;
     if (li >= nlist) return;
+    if (skip && skip[li]) return;  // answered by k_bq_fast
     const uint64_t* qc = qcodes + qlist[li];  // word w at qc[w * ldq]
     const float* Bq = bmin + (int64_t)li * nblk;
     // heap state handed over by the previous shard (layout order), or empty
@@ -425,6 +427,186 @@ __global__ __launch_bounds__(64) void k_rescore_ids(const float* __restrict__ X,
     const uint64_t id = ids[p];
     if (id < id_base || id - id_base >= (uint64_t)nslots) return;
     outE[p] = exact_dist<METRIC, VARIANT>(Q + (int64_t)qlist[li] * dpad, X + (int64_t)(id - id_base) * dpad, d);
+}
+
+// k_bq_fast<NW, METRIC, VARIANT>: a replay-free answer when hamming ties
+// cannot change it.  With h* the R-th smallest hamming distance,
+// S the rows below h* and T the rows at h*, the R-heap of flat/index.go:578-674
+// ends holding S plus some T' of T (which ones depends on the heap's tie
+// order).  If the m = min(k, heap size) smallest exact distances over S u T are
+// strictly increasing, strictly below the next one, and (when T was cut) all
+// from S, every possible T' rescores (flat/index.go:490-531) to the same
+// result, which is then written as the query's candidate list (m ids; the
+// rescoring and k_bq_final run on it as on a replayed heap) and skip[li] = 1.
+// Otherwise skip[li] = 0 and the replay runs.  Rows at or below h* are found
+// from the 32-row block minima: blocks with minimum <= H_R (the R-th smallest
+// block minimum) hold every such row.  One 256-thread workgroup per query.
+constexpr int BQF_CB = 2048;  // candidate blocks
+constexpr int BQF_RC = 2048;  // rows at or below H_R
+constexpr int BQF_UC = 1024;  // rows at or below h*
+constexpr int BQF_K = 64;     // k
+template <int NW, int METRIC, int VARIANT>
+__global__ __launch_bounds__(256) void k_bq_fast(const uint64_t* __restrict__ codes, int64_t ccap, int words,
+                                                 const uint32_t* __restrict__ valid, int64_t nslots,
+                                                 const uint64_t* __restrict__ qcodes, int64_t ldq,
+                                                 const int32_t* __restrict__ qlist, int nlist,
+                                                 const float* __restrict__ bmin, int64_t nblk, int R, int k,
+                                                 const float* __restrict__ X, int dpad, const float* __restrict__ Q,
+                                                 int d, uint64_t id_base, uint64_t* __restrict__ out_ids,
+                                                 int32_t* __restrict__ out_n, int32_t* __restrict__ skip) {
+    constexpr int HB = 64 * NW + 1;
+    __shared__ uint32_t hist[4][HB];
+    __shared__ uint32_t cblk[BQF_CB];
+    __shared__ uint32_t rslot[BQF_RC];
+    __shared__ uint16_t rh[BQF_RC];
+    __shared__ uint32_t uslot[BQF_UC];
+    __shared__ uint16_t uh[BQF_UC];
+    __shared__ float ud[BQF_UC];
+    __shared__ uint8_t upick[BQF_UC];
+    __shared__ float rd[4];
+    __shared__ int ri[4];
+    __shared__ uint32_t pslot[BQF_K];
+    __shared__ int s_ncb, s_nrow, s_nu, s_H, s_fail, s_tot;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = blockIdx.x;
+    if (li >= nlist) return;
+    const float* Bq = bmin + (int64_t)li * nblk;
+    for (int i = tid; i < 4 * HB; i += 256) (&hist[0][0])[i] = 0u;
+    if (tid == 0) { s_ncb = 0; s_nrow = 0; s_nu = 0; s_fail = k > BQF_K ? 1 : 0; }
+    __syncthreads();
+    // 1. histogram of the block minima (one copy per wave), H_R
+    for (int64_t b = tid; b < nblk; b += 256) {
+        const float v = Bq[b];
+        if (v < (float)HB) atomicAdd(&hist[w][(int)v], 1u);
+    }
+    __syncthreads();
+    for (int i = tid; i < HB; i += 256) hist[0][i] += hist[1][i] + hist[2][i] + hist[3][i];
+    __syncthreads();
+    // smallest H with count(<= H) >= R (HB - 1 when fewer): wave 0, a segment per lane
+    auto threshold = [&](int want) {
+        if (w == 0) {
+            constexpr int SEG = (HB + 63) / 64;
+            const int h0 = lane * SEG;
+            uint32_t sum = 0;
+            for (int h = h0; h < h0 + SEG && h < HB; h++) sum += hist[0][h];
+            uint32_t incl = sum;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            const uint64_t hit = __ballot(incl >= (uint32_t)want);
+            if (hit == 0) {
+                if (lane == 63) { s_H = HB - 1; s_tot = (int)incl; }
+            } else if (lane == __builtin_ctzll(hit)) {
+                uint32_t run = incl - sum;
+                int h = h0;
+                for (; h < h0 + SEG && h < HB; h++) {
+                    run += hist[0][h];
+                    if (run >= (uint32_t)want) break;
+                }
+                s_H = h;
+                s_tot = (int)run;
+            }
+        }
+        __syncthreads();
+    };
+    threshold(R);
+    const int HR = s_H;
+    // 2. the blocks holding every row at or below H_R
+    for (int64_t b = tid; b < nblk; b += 256) {
+        const float v = Bq[b];
+        if (v <= (float)HR) {
+            const int p = atomicAdd(&s_ncb, 1);
+            if (p < BQF_CB) cblk[p] = (uint32_t)b; else s_fail = 1;
+        }
+    }
+    for (int i = tid; i < HB; i += 256) hist[0][i] = 0u;
+    __syncthreads();
+    // 3. their rows' hamming distances (half a wave per block), rows <= H_R kept
+    if (!s_fail) {
+        const uint64_t* qc = qcodes + qlist[li];
+        uint64_t qw[NW];
+#pragma unroll
+        for (int c = 0; c < NW; c++) qw[c] = c < words ? qc[(int64_t)c * ldq] : 0ull;
+        const int ncb = s_ncb;
+        for (int i = tid >> 5; i < ncb; i += 8) {
+            const int64_t slot = (int64_t)cblk[i] * 32 + (tid & 31);
+            const bool ok = slot < nslots && ((valid[slot >> 5] >> (slot & 31)) & 1u);
+            uint32_t h = 0;
+#pragma unroll
+            for (int c = 0; c < NW; c++)
+                if (c < words) h += (uint32_t)__popcll((ok ? codes[(int64_t)c * ccap + slot] : 0ull) ^ qw[c]);
+            if (ok && h <= (uint32_t)HR) {
+                atomicAdd(&hist[0][h], 1u);
+                const int p = atomicAdd(&s_nrow, 1);
+                if (p < BQF_RC) { rslot[p] = (uint32_t)slot; rh[p] = (uint16_t)h; } else s_fail = 1;
+            }
+        }
+    }
+    __syncthreads();
+    if (s_fail) { if (tid == 0) skip[li] = 0; return; }
+    // 4. h*; U = rows <= h* (the heap holds min(R, |U|) of them: all of U
+    //    when |U| <= R, else S plus part of T)
+    threshold(R);
+    const int hs = s_H;
+    const int nrow = s_nrow;
+    for (int p = tid; p < nrow; p += 256)
+        if (rh[p] <= hs) {
+            const int u = atomicAdd(&s_nu, 1);
+            if (u < BQF_UC) { uslot[u] = rslot[p]; uh[u] = rh[p]; upick[u] = 0; } else s_fail = 1;
+        }
+    __syncthreads();
+    if (s_fail) { if (tid == 0) skip[li] = 0; return; }
+    const int nu = s_nu;
+    // 5. exact-order distances (the rescoring's createDistanceCalc, as k_rescore_ids)
+    const float* qv = Q + (int64_t)qlist[li] * dpad;
+    for (int u = tid; u < nu; u += 256) {
+        const float v = exact_dist<METRIC, VARIANT>(qv, X + (int64_t)uslot[u] * dpad, d);
+        ud[u] = v;
+        if (!(v < __builtin_inff()) || !(v > -__builtin_inff())) s_fail = 1;  // NaN / inf: the replay decides
+    }
+    __syncthreads();
+    if (s_fail) { if (tid == 0) skip[li] = 0; return; }
+    // 6. the m (+1) smallest, one block-wide argmin each
+    const int csz = nu < R ? nu : R;
+    const int m = k < csz ? k : csz;
+    const int picks = csz > m ? m + 1 : m;
+    const bool cut = nu > R;
+    float prev = -__builtin_inff();
+    bool good = true;
+    for (int j = 0; j < picks; j++) {
+        float bv = __builtin_inff();
+        int bi = -1;
+        for (int u = tid; u < nu; u += 256) {
+            const float v = ud[u];
+            if (!upick[u] && (bi < 0 || v < bv)) { bv = v; bi = u; }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o);
+            const int oi = __shfl_xor(bi, o);
+            if (oi >= 0 && (bi < 0 || ov < bv || (ov == bv && oi < bi))) { bv = ov; bi = oi; }
+        }
+        if (lane == 0) { rd[w] = bv; ri[w] = bi; }
+        __syncthreads();
+        bv = rd[0]; bi = ri[0];
+        for (int x = 1; x < 4; x++)
+            if (ri[x] >= 0 && (bi < 0 || rd[x] < bv || (rd[x] == bv && ri[x] < bi))) { bv = rd[x]; bi = ri[x]; }
+        __syncthreads();
+        // strictly increasing and finite; when T was cut, the m results from S
+        if (!(bv > prev) || !(bv < __builtin_inff()) || bi < 0) good = false;
+        if (j < m && cut && bi >= 0 && uh[bi] >= hs) good = false;
+        prev = bv;
+        if (!good) break;
+        if (tid == 0) {
+            upick[bi] = 1;
+            if (j < m) pslot[j] = uslot[bi];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) skip[li] = good ? 1 : 0;
+    if (!good) return;
+    for (int j = tid; j < m; j += 256) out_ids[(int64_t)li * R + j] = id_base + pslot[j];
+    if (tid == 0) out_n[li] = m;
 }
 
 // Rescoring heap (flat/index.go:525-531): the candidates, in pop order (asc = 1:

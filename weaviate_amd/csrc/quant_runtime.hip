@@ -191,7 +191,7 @@ static int bq_blockmin(wv_index* idx, hipStream_t s, const uint32_t* valid, int6
 static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t g0, int F, const uint64_t* in_ids,
                      const float* in_d, const int32_t* in_len, int pop, uint64_t* out_ids, float* out_d,
                      int32_t* out_n, uint64_t* rec_ids = nullptr, float* rec_d = nullptr, int32_t* rec_n = nullptr,
-                     int cap = 0) {
+                     int cap = 0, const int32_t* skip = nullptr) {
     const int64_t nq = idx->bq_nq;
     const int R = idx->bq_R;
     const int64_t nslots = idx->hiwater;
@@ -212,7 +212,7 @@ static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_
         k_bq_replay<NWV, RECV, BLKV><<<(unsigned)F, 64, lds_r, s>>>(idx->codes, idx->cap, words, valid, nslots, qc, nq, \
                                                               qlist + g0, F, bm, nblk, R, idx->id_base, in_ids, \
                                                               in_d, in_len, pop, out_ids, out_d, out_n, rec_ids, \
-                                                              rec_d, rec_n, cap);                               \
+                                                              rec_d, rec_n, cap, skip);                         \
     } while (0)
 #define WV_RPR(NWV, RECV)                                          \
     do {                                                           \
@@ -239,6 +239,46 @@ static int bq_replay(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_
 #undef WV_RP
     HIPCHK(hipGetLastError());
     return WV_OK;
+}
+
+// The replay-free answer of k_bq_fast (32-row minima, 8-24 code words, k <= 64,
+// not hamming): skip[li] = 1 for every query of the group it answered (its
+// candidate list then holds its m result ids)
+static bool bq_fast(wv_index* idx, hipStream_t s, const uint32_t* valid, int64_t g0, int F, int k, uint64_t* out_ids,
+                    int32_t* out_n, int32_t* skip, int* rc) {
+    *rc = WV_OK;
+    const int nw = bq_nw(idx);
+    if (!idx->bq_fast || bq_blk(idx) != 32 || k > BQF_K || idx->metric == WV_METRIC_HAMMING ||
+        (nw != 8 && nw != 12 && nw != 16 && nw != 24))
+        return false;
+    const bool v5 = idx->variant == WV_VARIANT_AVX512;
+    const int32_t* qlist = idx->ident.as<int32_t>() + g0;
+    const uint64_t* qc = idx->qcodes.as<uint64_t>();
+    const float* Qn = idx->qn.as<float>();
+#define WV_BF(NWV, M, V)                                                                                        \
+    k_bq_fast<NWV, M, V><<<(unsigned)F, 256, 0, s>>>(idx->codes, idx->cap, idx->words, valid, idx->hiwater, qc,  \
+                                                     idx->bq_nq, qlist, F, idx->bqmin.as<float>(), bq_nblk(idx), \
+                                                     idx->bq_R, k, idx->X, idx->dpad, Qn, idx->dims, idx->id_base, \
+                                                     out_ids, out_n, skip)
+#define WV_BFM(NWV)                                                                                             \
+    do {                                                                                                        \
+        switch (idx->metric) {                                                                                  \
+        case WV_METRIC_L2_SQUARED: if (v5) WV_BF(NWV, L2, AVX512); else WV_BF(NWV, L2, AVX256); break;          \
+        case WV_METRIC_DOT: if (v5) WV_BF(NWV, DOT, AVX512); else WV_BF(NWV, DOT, AVX256); break;               \
+        default: if (v5) WV_BF(NWV, COSINE, AVX512); else WV_BF(NWV, COSINE, AVX256); break;                    \
+        }                                                                                                       \
+    } while (0)
+    switch (nw) {
+    case 8: WV_BFM(8); break;
+    case 12: WV_BFM(12); break;
+    case 16: WV_BFM(16); break;
+    default: WV_BFM(24); break;
+    }
+#undef WV_BFM
+#undef WV_BF
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) *rc = set_err(WV_ERR_HIP, "k_bq_fast: %s", hipGetErrorString(e));
+    return *rc == WV_OK;
 }
 
 // Phase 3: exact distances of the candidate ids this shard holds
@@ -290,8 +330,14 @@ int search_bq(wv_index* idx, hipStream_t s, const float* d_qraw, int64_t nq, int
         const int F = (int)std::min<int64_t>(G, nq - g0);
         rc = bq_blockmin(idx, s, valid, g0, F);
         if (rc) return rc;
+        HIPCHK(idx->bqSkip.ensure((size_t)nq * sizeof(int32_t)));
+        int32_t* skip = idx->bqSkip.as<int32_t>() + g0;
+        const bool fast = bq_fast(idx, s, valid, g0, F, k, idx->ascI.as<uint64_t>() + g0 * R,
+                                  idx->cn.as<int32_t>() + g0, skip, &rc);
+        if (rc) return rc;
         rc = bq_replay(idx, s, valid, g0, F, nullptr, nullptr, nullptr, 1, idx->ascI.as<uint64_t>() + g0 * R,
-                       idx->ascD.as<float>() + g0 * R, idx->cn.as<int32_t>() + g0);
+                       idx->ascD.as<float>() + g0 * R, idx->cn.as<int32_t>() + g0, nullptr, nullptr, nullptr, 0,
+                       fast ? skip : nullptr);
         if (rc) return rc;
     }
     rc = bq_rescore(idx, s, idx->ascI.as<uint64_t>(), idx->cn.as<int32_t>(), idx->candE.as<float>());

@@ -119,8 +119,8 @@ struct wv_index {
     // block minima on the integer matrix cores (k_q8_blockkey<..., BQ>), 7..24 words
     unsigned char* bq8 = nullptr;
     int dpb8b = 0;
-    int bq8_opt = 1;
-    int64_t bq_last_nq = 0, bq_last_nblk = 0, bq_last_blk = 256;
+    int bq8_opt = 1;             // option bq8: block minima from the +-1 plane (1) or the VALU kernels (0)
+    int64_t bq_last_nq = 0, bq_last_nblk = 0, bq_last_blk = 256;  // debug hook (wv_index_debug_bqmin): the last BQ batch's first group
     int scan_window = 1;         // option scan_window: an allow list scans only [allow.Min, allow.Max]
     // gathered allow-list search: a sparse allow list's rows (ascending id) as
     // a temporary sub-index searched by the same pipeline (option gather_max:
@@ -128,7 +128,7 @@ struct wv_index {
     int64_t gather_max = 1 << 20;
     wv_index* sub = nullptr;
     DBuf subSlots;
-    DBuf allowIds, allowCnt;     // the allow list on the device, its candidate count  // debug hook (wv_index_debug_bqmin): the last BQ batch's first group             // option bq8: block minima from the +-1 plane (1) or the VALU kernels (0)
+    DBuf allowIds, allowCnt;     // the allow list on the device, its candidate count
     int64_t bq_nq = 0;           // BQ batch in flight (bq_begin): queries and R
     int bq_R = 0;
     int64_t qt_nq = 0, qt_ld = 0;  // sharded hnsw flat batch in flight (wv_index_quant_begin)
@@ -158,6 +158,7 @@ struct wv_index {
     int q8_live = 1;                // option q8_live: waves of a partial query group's padding skip their MFMAs (k_q8_blockkey LIVE)
     int q8_prio = 0;                // option q8_prio: s_setprio 1 for waves 4-7 of k_q8_blockkey (experiment)
     int rp_few = 16;                // option rp_few: a device-counted replay list of at most this many queries takes k_blk_replay_par
+    int bq_fast = 0;                // option bq_fast: BQ queries whose result no hamming tie can change skip the replay (k_bq_fast)
     int q8_filter = 1;              // option q8_filter: the exact pass bounds rows from the int8 plane (1) or bf16 (0)
     unsigned char* X8 = nullptr;
     float* sb8 = nullptr;
@@ -201,7 +202,7 @@ struct wv_index {
     uint64_t count = 0;    // flat.count: incremented per Add (flat/index.go:380-385)
     int64_t npresent = 0;
 
-    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, cslot, cn, ident, lut, ascI, ascD, ascN, rqq, rqm;
+    DBuf stage, slots, qraw, qn, qn2, spanA, spanI, candA, candI, candE, oIds, oD, oN, oF, valid, qlist, hI, hD, hN, rE, rB, qcodes, bqmin, bqSkip, cslot, cn, ident, lut, ascI, ascD, ascN, rqq, rqm;
 
     int margin = 8, force_replay = 0, spans_opt = 0, timing = 0, cbuf_opt = 0, kernel_opt = 3, bq_kernel = 0, sel_dbg = 0, qgroup_opt = 0, sel_opt = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -780,6 +780,7 @@ extern "C" int wv_index_set_option(wv_index* idx, const char* key, int64_t value
     else if (k == "sel_lower") idx->sel_lower = value ? 1 : 0;  // per-query allow lists share one block-key launch
     else if (k == "pqa_alone") idx->pqa_alone = value ? 1 : 0;  // unresolved per-query lists searched alone
     else if (k == "pqa_keys") idx->pqa_keys = value ? 1 : 0;    // per-query masked int8 keys
+    else if (k == "bq_fast") idx->bq_fast = value ? 1 : 0;  // replay-free BQ answers when ties cannot matter
     else if (k == "rp_few") idx->rp_few = value;  // replay lists up to this long (device-counted) take the one-launch form
     else if (k == "batch_rows") idx->batch_rows = value ? 1 : 0;  // batcher: dense lists as slot bitmaps
     else if (k == "pqa_split_max") idx->pqa_split_max = std::max<int64_t>(value, 0);  // sparse lists searched alone
