@@ -612,6 +612,8 @@ int wv_index_debug_bqmin(wv_index *idx, int64_t q, float *mins, int64_t *nblk, i
  * 6 = HBM-streaming GEMV, 3 = f32 MFMA select; other values are rejected),
  * "replay_par" (flagged-query replay form, default 2), "rp_few" (device-counted
  * replay lists up to this long take the one-launch 8-wave form, default 16),
+ * "bq_fast" (1 = BQ queries whose rescored result no hamming tie can change
+ * skip the R-heap replay, k_bq_fast; default 0: slower on C4),
  * "exact_bm" / "exact_cap"
  * / "exact_filter" (block-key exact pass forms; exact_filter 1 = bf16-plane row
  * bound in the capped pass, default), "replay_dbg" (1 = clock diagnostics of

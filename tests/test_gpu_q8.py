@@ -402,3 +402,39 @@ def test_q8_gemv_small_batches_match_blockkey(wv, oracle, metric, kind, variant,
         assert_same(orc.search(queries[qi], k, allow=allow), ids[qi, :counts[qi]], dists[qi, :counts[qi]],
                     ctx=f"a{qi}")
     idx.close()
+
+
+@pytest.mark.parametrize("metric,kind,n,d,k,rescore", [
+    ("cosine", 0, 30000, 1536, 10, 200),   # C4 width: most queries answered without the replay
+    ("dot", 0, 12000, 768, 64, 100),       # k at the fast path's cap
+    ("l2-squared", 2, 9000 + 5, 1000, 10, 40),  # ragged corpus
+    ("cosine", 1, 6000, 450, 10, 50),      # every code 0: one hamming value, the replay decides
+    ("l2-squared", 3, 8000, 512, 10, 30),  # small-integer data: exact-distance ties
+])
+def test_bq_fast_equals_replay_and_oracle(wv, oracle, metric, kind, n, d, k, rescore):
+    """k_bq_fast: queries whose rescored result no hamming tie
+    can change skip the R-heap replay.  Results with the fast path on equal
+    the replay-only results bit for bit and the oracle (flat/index.go:460-532),
+    also under an allow list."""
+    from test_gpu_flat import build_bq_pair
+    if kind == 3:  # signed small integers: codes vary, exact distances tie
+        data = gen(oracle, 1, 85, n, d) - np.float32(64)
+        queries = gen(oracle, 1, 86, 160, d) - np.float32(64)
+    else:
+        data = gen(oracle, kind, 85, n, d)
+        queries = gen(oracle, kind, 86, 160, d)
+    idx, orc = build_bq_pair(wv, oracle, metric, "avx256", data, rescore)
+    allow = wv.AllowList(range(0, n, 3))
+    for al in (None, allow):
+        idx.set_option("bq_fast", 1)
+        got = idx.search_by_vector_batch(queries, k, allow=al)
+        assert idx.stats()["last_route"] == ROUTE_BQ_INT8
+        idx.set_option("bq_fast", 0)
+        ref = idx.search_by_vector_batch(queries, k, allow=al)
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+        if al is None:
+            for q in range(0, len(queries), 10):
+                assert_same(orc.search(queries[q], k), got[0][q, :got[2][q]], got[1][q, :got[2][q]],
+                            f"bq fast {metric} q{q}")
+    idx.close()
