@@ -216,15 +216,34 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
         uint64_t qw[NW];
 #pragma unroll
         for (int w = 0; w < NW; w++) qw[w] = w < words ? qc[(int64_t)w * ldq] : 0ull;
-        int64_t cb0 = 0;
-        float bmc = lane < nblk ? Bq[lane] : __builtin_inff();
-        float bmn = 64 + lane < nblk ? Bq[64 + lane] : __builtin_inff();
-        uint64_t cmask;
-        {
+        // the block minima in windows of 16 chunks of 64 blocks: the next window
+        // loads while this one is scanned (16 loads in flight instead of one
+        // chunk ahead), and a chunk with no block under the top when its window
+        // came up is never looked at again (the top only falls once the heap is full)
+        float bw[16], bn[16];
+        auto load_win = [&](float* dst, int64_t base) {
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int64_t b = base + u * 64 + lane;
+                dst[u] = b < nblk ? Bq[b] : __builtin_inff();
+            }
+        };
+        auto win_mask = [&]() -> uint32_t {
             const int len = *s_len;
             const float top = len > 0 ? hr[0].d : 0.f;
-            cmask = __ballot(lane < nblk && bmc != __builtin_inff() && (len < R || top > bmc));
-        }
+            uint32_t m = 0;
+#pragma unroll
+            for (int u = 0; u < 16; u++)
+                if (__ballot(bw[u] != __builtin_inff() && (len < R || top > bw[u]))) m |= 1u << u;
+            return m;
+        };
+        int64_t wb0 = 0;
+        load_win(bw, 0);
+        load_win(bn, 1024);
+        uint32_t wm = win_mask();
+        int wi = -1;
+        float bmc = __builtin_inff();
+        uint64_t cmask = 0;
         auto next_blk = [&]() -> int64_t {
             const int len = *s_len;
             const float top = len > 0 ? hr[0].d : 0.f;
@@ -232,13 +251,25 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
                 while (cmask) {
                     const int j = __builtin_ctzll(cmask);
                     cmask &= cmask - 1;
-                    if (len < R || top > __shfl(bmc, j)) return cb0 + j;
+                    if (len < R || top > __shfl(bmc, j)) return wb0 + wi * 64 + j;
                 }
-                cb0 += 64;
-                if (cb0 >= nblk) return -1;
-                bmc = bmn;
-                bmn = cb0 + 64 + lane < nblk ? Bq[cb0 + 64 + lane] : __builtin_inff();
-                cmask = __ballot(cb0 + lane < nblk && bmc != __builtin_inff() && (len < R || top > bmc));
+                if (wi >= 0) wm &= ~((2u << wi) - 1u);
+                if (wm) {
+                    wi = __builtin_ctz(wm);
+                    float v = bw[0];
+#pragma unroll
+                    for (int u = 1; u < 16; u++) v = wi == u ? bw[u] : v;
+                    bmc = v;
+                    cmask = __ballot(bmc != __builtin_inff() && (len < R || top > bmc));
+                    continue;
+                }
+                wb0 += 1024;
+                if (wb0 >= nblk) return -1;
+#pragma unroll
+                for (int u = 0; u < 16; u++) bw[u] = bn[u];
+                load_win(bn, wb0 + 1024);
+                wm = win_mask();
+                wi = -1;
             }
         };
         uint64_t x[NW];
