@@ -272,9 +272,11 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
                 wi = -1;
             }
         };
-        uint64_t x[NW];
-        uint32_t vword = 0;
-        auto load = [&](int64_t pa, int64_t pb) {
+        // two pairs of blocks in flight: buffers A and B take alternate pairs, so
+        // a pair's codes load while the two pairs before it are inserted
+        uint64_t xa[NW], xb[NW];
+        uint32_t va = 0, vb = 0;
+        auto load = [&](uint64_t (&x)[NW], uint32_t& vword, int64_t pa, int64_t pb) {
             const int64_t blk = lane < 32 ? pa : pb;
             const int64_t srow = blk * 32 + (lane & 31);
             const bool in = blk >= 0 && srow < nslots;
@@ -282,10 +284,9 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
 #pragma unroll
             for (int w = 0; w < NW; w++) x[w] = (in && w < words) ? codes[(int64_t)w * ccap + srow] : 0ull;
         };
-        int64_t pa = next_blk();
-        int64_t pb = pa >= 0 ? next_blk() : -1;
-        if (pa >= 0) load(pa, pb);
-        while (pa >= 0) {
+        // the pair (pa, pb) in buffer x: its rows' distances, the pair after the
+        // one in the other buffer (fa >= 0) into x, then the insertions in id order
+        auto step = [&](uint64_t (&x)[NW], uint32_t& vword, int64_t& pa, int64_t& pb, int64_t fa) {
             const int64_t blk = lane < 32 ? pa : pb;
             const int64_t srow = blk * 32 + (lane & 31);
             const bool ok = blk >= 0 && srow < nslots && ((vword >> (lane & 31)) & 1u);
@@ -293,9 +294,9 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
 #pragma unroll
             for (int w = 0; w < NW; w++) h += (uint32_t)__popcll(x[w] ^ qw[w]);
             const float dist = (float)h;
-            const int64_t na = next_blk();
+            const int64_t na = fa >= 0 ? next_blk() : -1;
             const int64_t nb = na >= 0 ? next_blk() : -1;
-            if (na >= 0) load(na, nb);  // in flight during the insertions below
+            if (na >= 0) load(x, vword, na, nb);  // in flight during the insertions below
             const int len = *s_len;
             const float top = len > 0 ? hr[0].d : 0.f;
             uint64_t mask = __ballot(ok && (len < R || top > dist));
@@ -322,6 +323,18 @@ __global__ __launch_bounds__(64) void k_bq_replay(const uint64_t* __restrict__ c
             }
             pa = na;
             pb = nb;
+        };
+        int64_t pa = next_blk();
+        int64_t pb = pa >= 0 ? next_blk() : -1;
+        if (pa >= 0) load(xa, va, pa, pb);
+        int64_t qa = pa >= 0 ? next_blk() : -1;
+        int64_t qb = qa >= 0 ? next_blk() : -1;
+        if (qa >= 0) load(xb, vb, qa, qb);
+        while (true) {
+            if (pa < 0) break;
+            step(xa, va, pa, pb, qa);
+            if (qa < 0) break;
+            step(xb, vb, qa, qb, pa);
         }
     } else
     for (int64_t b0 = 0; b0 < nblk; b0 += 64) {
